@@ -1,0 +1,198 @@
+// K11: paged attention, prefill / chunked prefill (varlen, causal, prefix-cache aware), MFMA bf16.
+//
+// A chunk's own K/V are written into the paged cache first (rope_cache.hip), so this kernel reads
+// every key - cached prefix and new tokens alike - from the cache: one code path for prefill,
+// chunked prefill and prefix-cache hits.
+//
+// Work split: workgroup = (query tile, kv head, sequence), 4 waves x 32 rows; a row is a
+// (query token, query head of this kv head's GQA group) pair, so the G heads sharing a kv head
+// stream its K/V together.  Per 32-key tile, with v_mfma_f32_32x32x16_bf16:
+//   S^T = K . Q^T    A = K rows straight from the token-major cache (16 B per lane),
+//                    B = Q^T held in registers for the whole loop (pre-scaled by scale*log2 e).
+//                    The accumulator has the QUERY ROW on the lane, so the online-softmax max/sum
+//                    are per-lane plus one lane^32 exchange (cdna_hip_programming.md T12 idea).
+//   O^T += V^T . P^T A = V^T from the dim-major V cache (two 8-byte loads per lane),
+//                    B = P^T taken straight from the S^T accumulator registers (§3 "An accumulator
+//                    tile as the next MFMA's operand"): no LDS round trip, no shuffles.
+// Causal tiles past a workgroup's last query position are skipped; heavy tiles launch first.
+#include "common.h"
+
+namespace mxs {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+constexpr int kPBS = 16;
+constexpr float kPLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+template <int D, int G>
+__global__ void __launch_bounds__(256) paged_prefill_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kv, long block_stride,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ qsl,
+    const int* __restrict__ seq_lens, int Hkv, float scale) {
+  constexpr int KS = D / 16;   // k-steps of the QK^T product
+  constexpr int DT = D / 32;   // 32-row output tiles of O^T
+  constexpr int BQ = 128 / G;  // query tokens per workgroup
+  const int kvh = blockIdx.y, seq = blockIdx.z;
+  const int q0 = qsl[seq];
+  const int ql = qsl[seq + 1] - q0;
+  const int tile = gridDim.x - 1 - blockIdx.x;  // heaviest (latest) tiles first
+  const int t0 = tile * BQ;
+  if (t0 >= ql) return;
+  const int L = seq_lens[seq];
+  const int ctx0 = L - ql;
+  const int Hq = Hkv * G;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, c = lane & 31;
+
+  const int r = wid * 32 + c;
+  const int tok = t0 + r / G;
+  const int head = kvh * G + r % G;
+  const bool rvalid = tok < ql;
+  const int qpos = ctx0 + (rvalid ? tok : 0);
+  const int wg_last_pos = ctx0 + min(t0 + BQ, ql) - 1;
+  const int nkeys = wg_last_pos + 1;
+
+  // Q^T fragments (B operand): lane holds Q[row c][16 ks + 8 h + j], pre-scaled
+  bf16x8_t qf[KS];
+  {
+    const bf16_t* qp = q + (static_cast<size_t>(q0 + (rvalid ? tok : 0)) * Hq + head) * D + 8 * h;
+    const float qs = scale * kPLog2e;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const uint4 v = *reinterpret_cast<const uint4*>(qp + 16 * ks);
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        qf[ks][2 * k] = static_cast<__bf16>(bf2f_lo(w[k]) * qs);
+        qf[ks][2 * k + 1] = static_cast<__bf16>(bf2f_hi(w[k]) * qs);
+      }
+    }
+  }
+
+  const int* bt = block_tables + static_cast<size_t>(seq) * bt_stride;
+  const size_t k_head_off = static_cast<size_t>(kvh) * kPBS * D;
+  const size_t v_head_off = static_cast<size_t>(Hkv + kvh) * kPBS * D;
+
+  float16_ o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  for (int k0 = 0; k0 < nkeys; k0 += 32) {
+    // ---- K fragments (A operand): key k0 + c, dims 16 ks + 8 h
+    const int key = k0 + c;
+    const int kblk = bt[min(key, L - 1) / kPBS];
+    const bf16_t* kp = kv + kblk * block_stride + k_head_off + static_cast<size_t>(key % kPBS) * D + 8 * h;
+    uint4 kf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) kf[ks] = *reinterpret_cast<const uint4*>(kp + 16 * ks);
+    // ---- V^T fragments (A operand of the P*V product), keys in the accumulator's permuted order
+    uint2 vf[DT][2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int kb = min(k0 + 16 * s, L - 1) / kPBS;
+      const bf16_t* vp = kv + bt[kb] * block_stride + v_head_off + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const bf16_t* vr = vp + static_cast<size_t>(32 * dt + c) * kPBS;
+        vf[dt][s][0] = *reinterpret_cast<const uint2*>(vr);
+        vf[dt][s][1] = *reinterpret_cast<const uint2*>(vr + 8);
+      }
+    }
+    // ---- S^T = K Q^T
+    float16_ sacc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sacc[i] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[ks]), qf[ks], sacc, 0, 0, 0);
+    // ---- mask + online softmax (row = lane c, keys split across the two lane halves)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kk = k0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (kk > qpos) sacc[i] = -INFINITY;
+      mx = fmaxf(mx, sacc[i]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    float ps = 0.f;
+    bf16x8_t pf[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = exp2f(sacc[i] - mn);
+      ps += p;
+      pf[i >> 3][i & 7] = static_cast<__bf16>(p);
+    }
+    l = l * alpha + ps;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+    // keys >= L in the last tile: zero V so uninitialised cache bytes never reach the sum
+    if (k0 + 32 > L) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int kbase = k0 + 16 * s + 8 * half + 4 * h;
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            uint32_t* w = reinterpret_cast<uint32_t*>(&vf[dt][s][half]);
+            if (kbase + 0 >= L) w[0] &= 0xFFFF0000u;
+            if (kbase + 1 >= L) w[0] &= 0x0000FFFFu;
+            if (kbase + 2 >= L) w[1] &= 0xFFFF0000u;
+            if (kbase + 3 >= L) w[1] &= 0x0000FFFFu;
+          }
+        }
+    }
+    // ---- O^T += V^T P^T
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const uint4 a = make_uint4(vf[dt][s][0].x, vf[dt][s][0].y, vf[dt][s][1].x, vf[dt][s][1].y);
+        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), pf[s], o[dt], 0, 0, 0);
+      }
+  }
+
+  l += __shfl_xor(l, 32, 64);
+  if (!rvalid) return;
+  const float inv = 1.f / l;
+  bf16_t* op = out + (static_cast<size_t>(q0 + tok) * Hq + head) * D;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 32 * dt + 8 * g4 + 4 * h;
+      uint2 v;
+      v.x = pack2(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv);
+      v.y = pack2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+      *reinterpret_cast<uint2*>(op + d0) = v;
+    }
+}
+
+void launch_paged_prefill(bf16_t* out, const bf16_t* q, const bf16_t* kv, long block_stride,
+                          const int* block_tables, int bt_stride, const int* qsl, const int* seq_lens,
+                          int num_seqs, int max_q_len, int Hq, int Hkv, int D, float scale, hipStream_t s) {
+  if (num_seqs == 0 || max_q_len == 0) return;
+  const int G = Hq / Hkv;
+  const int BQ = 128 / G;
+  dim3 grid((max_q_len + BQ - 1) / BQ, Hkv, num_seqs), blk(256);
+#define MXS_PF(DD, GG)                                                                                     \
+  if (D == DD && G == GG) {                                                                                \
+    hipLaunchKernelGGL((paged_prefill_kernel<DD, GG>), grid, blk, 0, s, out, q, kv, block_stride,          \
+                       block_tables, bt_stride, qsl, seq_lens, Hkv, scale);                               \
+    MXS_CHECK_LAUNCH();                                                                                    \
+    return;                                                                                                \
+  }
+  MXS_PF(64, 1) MXS_PF(64, 2) MXS_PF(64, 4) MXS_PF(64, 8)
+  MXS_PF(128, 1) MXS_PF(128, 2) MXS_PF(128, 4) MXS_PF(128, 8)
+#undef MXS_PF
+}
+
+}  // namespace mxs

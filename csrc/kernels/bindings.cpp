@@ -1,0 +1,167 @@
+// Python bindings of the gfx950 kernels (module mxserve._C).  Every op launches on the current HIP
+// stream so the model runner can capture decode steps into hipGraphs.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <optional>
+
+namespace mxs {
+typedef unsigned short bf16_t;
+void launch_rms_norm(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, float, hipStream_t);
+void launch_fused_add_rms_norm(bf16_t*, const bf16_t*, bf16_t*, const bf16_t*, int, int, float, hipStream_t);
+void launch_silu_mul(bf16_t*, const bf16_t*, int, int, hipStream_t);
+void launch_rope_and_cache(bf16_t*, const bf16_t*, const int64_t*, const float*, bf16_t*, long, const int64_t*,
+                           const bf16_t*, const bf16_t*, int, int, int, int, int, float, hipStream_t);
+int decode_num_partitions(int);
+void launch_paged_decode(bf16_t*, float*, float*, const bf16_t*, const bf16_t*, long, const int*, int, const int*,
+                         int, int, int, int, int, float, hipStream_t);
+void launch_paged_prefill(bf16_t*, const bf16_t*, const bf16_t*, long, const int*, int, const int*, const int*,
+                          int, int, int, int, int, float, hipStream_t);
+void launch_sample(int64_t*, const float*, int, int, long, const float*, const float*, const int*, const int64_t*,
+                   const int64_t*, hipStream_t);
+void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStream_t);
+void launch_moe_align(int*, int*, const int*, int, int, int, hipStream_t);
+}  // namespace mxs
+
+namespace {
+
+using mxs::bf16_t;
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+
+inline bf16_t* bf(const at::Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
+
+void rms_norm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(out);
+  TORCH_CHECK(x.stride(-1) == 1, "x rows must be contiguous");
+  const int H = x.size(-1);
+  TORCH_CHECK(H % 8 == 0, "hidden size must be a multiple of 8");
+  const int rows = x.numel() / H;
+  const int x_stride = x.dim() >= 2 ? x.stride(-2) : H;
+  mxs::launch_rms_norm(bf(out), bf(x), bf(w), rows, H, x_stride, static_cast<float>(eps), stream());
+}
+
+void fused_add_rms_norm(at::Tensor out, at::Tensor x, at::Tensor residual, at::Tensor w, double eps) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(residual); CHECK_CONTIG(x); CHECK_CONTIG(residual); CHECK_CONTIG(out);
+  const int H = x.size(-1);
+  TORCH_CHECK(H % 8 == 0, "hidden size must be a multiple of 8");
+  mxs::launch_fused_add_rms_norm(bf(out), bf(x), bf(residual), bf(w), x.numel() / H, H, static_cast<float>(eps),
+                                 stream());
+}
+
+void silu_mul(at::Tensor out, at::Tensor gu) {
+  CHECK_CUDA(gu); CHECK_BF16(gu); CHECK_CONTIG(gu); CHECK_CONTIG(out);
+  const int I = gu.size(-1) / 2;
+  TORCH_CHECK(I % 8 == 0, "intermediate size must be a multiple of 8");
+  mxs::launch_silu_mul(bf(out), bf(gu), gu.numel() / (2 * I), I, stream());
+}
+
+// kv_layer: [NB, 2, Hkv, BS, D] view (block stride may exceed 2*Hkv*BS*D)
+void check_kv(const at::Tensor& kv, int Hkv, int D) {
+  CHECK_CUDA(kv); CHECK_BF16(kv);
+  TORCH_CHECK(kv.dim() == 5 && kv.size(1) == 2 && kv.size(2) == Hkv && kv.size(4) == D, "bad kv_layer shape");
+  TORCH_CHECK(kv.size(3) == 16, "block size must be 16");
+  TORCH_CHECK(kv.stride(4) == 1 && kv.stride(3) == D && kv.stride(2) == 16 * D && kv.stride(1) == Hkv * 16 * D,
+              "kv_layer inner dims must be dense");
+}
+
+void rope_and_cache(at::Tensor q_out, at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin, at::Tensor kv,
+                    at::Tensor slot_mapping, std::optional<at::Tensor> qn, std::optional<at::Tensor> kn, int64_t Hq,
+                    int64_t Hkv, int64_t D, double eps) {
+  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_CONTIG(qkv); CHECK_CONTIG(q_out);
+  TORCH_CHECK(positions.scalar_type() == at::kLong && slot_mapping.scalar_type() == at::kLong, "int64 indices");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == D, "cos_sin must be fp32 [P, D]");
+  TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv width mismatch");
+  check_kv(kv, Hkv, D);
+  const bf16_t* qnp = qn.has_value() ? bf(*qn) : nullptr;
+  const bf16_t* knp = kn.has_value() ? bf(*kn) : nullptr;
+  mxs::launch_rope_and_cache(bf(q_out), bf(qkv), positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), bf(kv),
+                             kv.stride(0), slot_mapping.data_ptr<int64_t>(), qnp, knp, qkv.size(0), Hq, Hkv, D, 16,
+                             static_cast<float>(eps), stream());
+}
+
+void paged_attention_decode(at::Tensor out, at::Tensor q, at::Tensor kv, at::Tensor block_tables,
+                            at::Tensor seq_lens, double scale, int64_t max_seq_len) {
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_CONTIG(out);
+  const int B = q.size(0), Hq = q.size(1), D = q.size(2);
+  const int Hkv = kv.size(2);
+  check_kv(kv, Hkv, D);
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && seq_lens.scalar_type() == at::kInt, "int32 tables");
+  TORCH_CHECK(block_tables.stride(1) == 1, "block_tables rows must be contiguous");
+  TORCH_CHECK(Hq % Hkv == 0, "GQA ratio");
+  const int P = mxs::decode_num_partitions(static_cast<int>(std::max<int64_t>(max_seq_len, 1)));
+  at::Tensor tmp_out, tmp_ml;
+  if (P > 1) {
+    tmp_out = at::empty({B, Hq, P, D}, q.options().dtype(at::kFloat));
+    tmp_ml = at::empty({B, Hq, P, 2}, q.options().dtype(at::kFloat));
+  }
+  mxs::launch_paged_decode(bf(out), P > 1 ? tmp_out.data_ptr<float>() : nullptr,
+                           P > 1 ? tmp_ml.data_ptr<float>() : nullptr, bf(q), bf(kv), kv.stride(0),
+                           block_tables.data_ptr<int>(), block_tables.stride(0), seq_lens.data_ptr<int>(), B, Hq,
+                           Hkv, D, P, static_cast<float>(scale), stream());
+}
+
+void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Tensor block_tables, at::Tensor qsl,
+                             at::Tensor seq_lens, double scale, int64_t max_q_len) {
+  CHECK_CUDA(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_CONTIG(out);
+  const int Hq = q.size(1), D = q.size(2);
+  const int Hkv = kv.size(2);
+  check_kv(kv, Hkv, D);
+  TORCH_CHECK(qsl.scalar_type() == at::kInt && seq_lens.scalar_type() == at::kInt, "int32 metadata");
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && block_tables.stride(1) == 1, "block_tables");
+  const int S = seq_lens.size(0);
+  mxs::launch_paged_prefill(bf(out), bf(q), bf(kv), kv.stride(0), block_tables.data_ptr<int>(),
+                            block_tables.stride(0), qsl.data_ptr<int>(), seq_lens.data_ptr<int>(), S,
+                            static_cast<int>(max_q_len), Hq, Hkv, D, static_cast<float>(scale), stream());
+}
+
+void sample(at::Tensor out, at::Tensor logits, at::Tensor temperature, at::Tensor top_p, at::Tensor top_k,
+            at::Tensor seeds, at::Tensor steps) {
+  CHECK_CUDA(logits);
+  TORCH_CHECK(logits.scalar_type() == at::kFloat && logits.stride(1) == 1, "logits must be fp32 rows");
+  TORCH_CHECK(temperature.scalar_type() == at::kFloat && top_p.scalar_type() == at::kFloat, "fp32 params");
+  TORCH_CHECK(top_k.scalar_type() == at::kInt && seeds.scalar_type() == at::kLong && steps.scalar_type() == at::kLong,
+              "int params");
+  mxs::launch_sample(out.data_ptr<int64_t>(), logits.data_ptr<float>(), logits.size(0), logits.size(1),
+                     logits.stride(0), temperature.data_ptr<float>(), top_p.data_ptr<float>(),
+                     top_k.data_ptr<int>(), seeds.data_ptr<int64_t>(), steps.data_ptr<int64_t>(), stream());
+}
+
+void moe_topk_softmax(at::Tensor w, at::Tensor ids, at::Tensor logits) {
+  CHECK_CUDA(logits); CHECK_BF16(logits); CHECK_CONTIG(logits);
+  TORCH_CHECK(logits.size(1) <= 64, "at most 64 experts");
+  mxs::launch_moe_topk_softmax(w.data_ptr<float>(), ids.data_ptr<int>(), bf(logits), logits.size(0),
+                               logits.size(1), w.size(1), stream());
+}
+
+void moe_align(at::Tensor expert_offsets, at::Tensor perm, at::Tensor topk_ids, int64_t e_lo, int64_t e_local) {
+  CHECK_CUDA(topk_ids); CHECK_CONTIG(topk_ids);
+  TORCH_CHECK(topk_ids.scalar_type() == at::kInt, "int32 ids");
+  TORCH_CHECK(e_local <= 256, "at most 256 local experts");
+  mxs::launch_moe_align(expert_offsets.data_ptr<int>(), perm.data_ptr<int>(), topk_ids.data_ptr<int>(),
+                        topk_ids.numel(), e_lo, e_local, stream());
+}
+
+}  // namespace
+
+void register_comm(pybind11::module_& m);  // comm.cpp: KV transfer agent + custom all-reduce
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "mxserve gfx950 HIP kernels";
+  m.def("rms_norm", &rms_norm);
+  m.def("fused_add_rms_norm", &fused_add_rms_norm);
+  m.def("silu_mul", &silu_mul);
+  m.def("rope_and_cache", &rope_and_cache);
+  m.def("paged_attention_decode", &paged_attention_decode);
+  m.def("paged_attention_prefill", &paged_attention_prefill);
+  m.def("sample", &sample);
+  m.def("moe_topk_softmax", &moe_topk_softmax);
+  m.def("moe_align", &moe_align);
+  m.def("decode_num_partitions", &mxs::decode_num_partitions);
+  register_comm(m);
+}

@@ -1,0 +1,124 @@
+// K02 RMSNorm (+ fused residual add) and K10 SiLU*mul for gfx950.
+// Memory-bound: every access is a 16-byte bf16x8 vector (cdna_hip_programming.md Guideline 13),
+// the row stays in registers between the reduction and the scaled write (one HBM pass).
+#include "common.h"
+
+namespace mxs {
+
+// One workgroup per row. NV = number of bf16x8 vectors each thread keeps in registers.
+template <int NV, bool ADD>
+__global__ void __launch_bounds__(1024) rmsnorm_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ x,
+                                                       bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
+                                                       int H, int x_stride, float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const bf16_t* xr = x + static_cast<size_t>(row) * x_stride;
+  bf16_t* rr = ADD ? residual + static_cast<size_t>(row) * H : nullptr;
+  const int nvec = H >> 3;
+  uint4 v[NV];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nvec) {
+      uint4 a = *reinterpret_cast<const uint4*>(xr + c * 8);
+      if (ADD) {
+        const uint4 b = *reinterpret_cast<const uint4*>(rr + c * 8);
+        uint32_t* pa = reinterpret_cast<uint32_t*>(&a);
+        const uint32_t* pb = reinterpret_cast<const uint32_t*>(&b);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          pa[k] = pack2(bf2f_lo(pa[k]) + bf2f_lo(pb[k]), bf2f_hi(pa[k]) + bf2f_hi(pb[k]));
+        *reinterpret_cast<uint4*>(rr + c * 8) = a;
+      }
+      v[i] = a;
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(&a);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float lo = bf2f_lo(p[k]), hi = bf2f_hi(p[k]);
+        ss += lo * lo + hi * hi;
+      }
+    }
+  }
+  const float inv = rsqrtf(block_sum(ss, scratch) / static_cast<float>(H) + eps);
+  bf16_t* orow = out + static_cast<size_t>(row) * H;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nvec) {
+      const uint4 wv = *reinterpret_cast<const uint4*>(w + c * 8);
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(&v[i]);
+      const uint32_t* pw = reinterpret_cast<const uint32_t*>(&wv);
+      uint4 o;
+      uint32_t* po = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        po[k] = pack2(bf2f_lo(p[k]) * inv * bf2f_lo(pw[k]), bf2f_hi(p[k]) * inv * bf2f_hi(pw[k]));
+      *reinterpret_cast<uint4*>(orow + c * 8) = o;
+    }
+  }
+}
+
+template <bool ADD>
+static void launch_rmsnorm_t(bf16_t* out, const bf16_t* x, bf16_t* res, const bf16_t* w, int rows, int H,
+                             int x_stride, float eps, hipStream_t s) {
+  const int nvec = H / 8;
+  // one bf16x8 per thread up to H = 8192 (1024 threads); wider rows keep NV vectors per thread
+  const int threads = nvec <= 1024 ? ((nvec + 63) / 64) * 64 : 1024;
+  const int nv = (nvec + threads - 1) / threads;
+  dim3 g(rows), b(threads);
+  switch (nv) {
+    case 1: hipLaunchKernelGGL((rmsnorm_kernel<1, ADD>), g, b, 0, s, out, x, res, w, H, x_stride, eps); break;
+    case 2: hipLaunchKernelGGL((rmsnorm_kernel<2, ADD>), g, b, 0, s, out, x, res, w, H, x_stride, eps); break;
+    case 3: hipLaunchKernelGGL((rmsnorm_kernel<3, ADD>), g, b, 0, s, out, x, res, w, H, x_stride, eps); break;
+    case 4: hipLaunchKernelGGL((rmsnorm_kernel<4, ADD>), g, b, 0, s, out, x, res, w, H, x_stride, eps); break;
+    default: hipLaunchKernelGGL((rmsnorm_kernel<8, ADD>), g, b, 0, s, out, x, res, w, H, x_stride, eps); break;
+  }
+  MXS_CHECK_LAUNCH();
+}
+
+void launch_rms_norm(bf16_t* out, const bf16_t* x, const bf16_t* w, int rows, int H, int x_stride, float eps,
+                     hipStream_t s) {
+  launch_rmsnorm_t<false>(out, x, nullptr, w, rows, H, x_stride, eps, s);
+}
+
+void launch_fused_add_rms_norm(bf16_t* out, const bf16_t* x, bf16_t* residual, const bf16_t* w, int rows, int H,
+                               float eps, hipStream_t s) {
+  launch_rmsnorm_t<true>(out, x, residual, w, rows, H, H, eps, s);
+}
+
+// out[t, i] = silu(gu[t, i]) * gu[t, I + i]; 8 elements per thread, grid-stride.
+__global__ void silu_mul_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ gu, int rows, int I) {
+  const int vec_per_row = I >> 3;
+  const long total = static_cast<long>(rows) * vec_per_row;
+  for (long idx = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; idx < total;
+       idx += static_cast<long>(gridDim.x) * blockDim.x) {
+    const long r = idx / vec_per_row;
+    const int c = static_cast<int>(idx - r * vec_per_row) * 8;
+    const bf16_t* g = gu + r * 2 * I + c;
+    const uint4 gv = *reinterpret_cast<const uint4*>(g);
+    const uint4 uv = *reinterpret_cast<const uint4*>(g + I);
+    const uint32_t* pg = reinterpret_cast<const uint32_t*>(&gv);
+    const uint32_t* pu = reinterpret_cast<const uint32_t*>(&uv);
+    uint4 o;
+    uint32_t* po = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float g0 = bf2f_lo(pg[k]), g1 = bf2f_hi(pg[k]);
+      const float s0 = g0 / (1.f + __expf(-g0)), s1 = g1 / (1.f + __expf(-g1));
+      po[k] = pack2(s0 * bf2f_lo(pu[k]), s1 * bf2f_hi(pu[k]));
+    }
+    *reinterpret_cast<uint4*>(out + r * I + c) = o;
+  }
+}
+
+void launch_silu_mul(bf16_t* out, const bf16_t* gu, int rows, int I, hipStream_t s) {
+  const long total = static_cast<long>(rows) * (I / 8);
+  long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(blocks), dim3(256), 0, s, out, gu, rows, I);
+  MXS_CHECK_LAUNCH();
+}
+
+}  // namespace mxs

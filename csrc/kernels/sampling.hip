@@ -1,0 +1,127 @@
+// K13: fused sampling. One workgroup per row of logits (vocab up to ~152k):
+//   temperature <= 0        -> argmax (lowest index on ties)
+//   otherwise               -> Gumbel-max over softmax(z / T) restricted to the top-k / top-p set:
+//                              argmax_v (z_v / T + g_v), g_v = -log(-log u_v),
+//                              u_v = hash(seed, step, v)  (counter-based: reproducible per request,
+//                              graph-capturable, no RNG state).  No sort: the top-k and top-p
+//                              thresholds are found by bisection over value with block reductions.
+// The hash matches mxserve/ops/reference.py::_hash_u32 bit for bit.
+#include "common.h"
+
+namespace mxs {
+
+__device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
+  x = (x ^ (x >> 16)) * 0x7FEB352Du;
+  x = (x ^ (x >> 15)) * 0x846CA68Bu;
+  return x ^ (x >> 16);
+}
+
+struct ArgMax {
+  float v;
+  int i;
+};
+
+__device__ __forceinline__ ArgMax better(ArgMax a, ArgMax b) {
+  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
+  return a;
+}
+
+__device__ ArgMax block_argmax(ArgMax a, float* sv, int* si) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ArgMax b{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};
+    a = better(a, b);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+    sv[wid] = a.v;
+    si[wid] = a.i;
+  }
+  __syncthreads();
+  ArgMax r{sv[0], si[0]};
+  for (int w = 1; w < nw; ++w) r = better(r, ArgMax{sv[w], si[w]});
+  return r;
+}
+
+__global__ void __launch_bounds__(1024) sample_kernel(int64_t* __restrict__ out, const float* __restrict__ logits,
+                                                      int V, long row_stride, const float* __restrict__ temperature,
+                                                      const float* __restrict__ top_p, const int* __restrict__ top_k,
+                                                      const int64_t* __restrict__ seeds,
+                                                      const int64_t* __restrict__ steps) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const int row = blockIdx.x;
+  const float* z = logits + row * row_stride;
+  const float t = temperature[row];
+  if (!(t > 0.f)) {
+    ArgMax a{-INFINITY, 0x7FFFFFFF};
+    for (int v = threadIdx.x; v < V; v += blockDim.x) a = better(a, ArgMax{z[v], v});
+    ArgMax r = block_argmax(a, sv, si);
+    if (threadIdx.x == 0) out[row] = r.i;
+    return;
+  }
+  const float invt = 1.f / t;
+  const int k = top_k[row];
+  const float p = top_p[row];
+  float thr = -INFINITY;
+  if ((k > 0 && k < V) || p < 1.f) {
+    float mx = -INFINITY, mn = INFINITY;
+    for (int v = threadIdx.x; v < V; v += blockDim.x) {
+      mx = fmaxf(mx, z[v]);
+      mn = fminf(mn, z[v]);
+    }
+    mx = block_max(mx, sv);
+    mn = -block_max(-mn, sv);
+    if (k > 0 && k < V) {  // largest tau with count(z >= tau) >= k
+      float lo = mn, hi = mx;
+      for (int it = 0; it < 32; ++it) {
+        const float mid = 0.5f * (lo + hi);
+        float cnt = 0.f;
+        for (int v = threadIdx.x; v < V; v += blockDim.x) cnt += z[v] >= mid ? 1.f : 0.f;
+        cnt = block_sum(cnt, sv);
+        if (cnt >= static_cast<float>(k)) lo = mid; else hi = mid;
+      }
+      thr = lo;
+    }
+    if (p < 1.f) {  // largest tau with mass(z >= tau) >= p * total, mass in softmax(z / T)
+      float tot = 0.f;
+      for (int v = threadIdx.x; v < V; v += blockDim.x) tot += __expf((z[v] - mx) * invt);
+      tot = block_sum(tot, sv);
+      float lo = fmaxf(mn, mx - 88.f * t), hi = mx;
+      for (int it = 0; it < 32; ++it) {
+        const float mid = 0.5f * (lo + hi);
+        float mass = 0.f;
+        for (int v = threadIdx.x; v < V; v += blockDim.x)
+          mass += z[v] >= mid ? __expf((z[v] - mx) * invt) : 0.f;
+        mass = block_sum(mass, sv);
+        if (mass >= p * tot) lo = mid; else hi = mid;
+      }
+      thr = fmaxf(thr, lo);
+    }
+  }
+  const uint32_t key = hash_u32(static_cast<uint32_t>(static_cast<uint64_t>(seeds[row]) * 0x9E3779B1ull +
+                                                      static_cast<uint64_t>(steps[row])));
+  ArgMax a{-INFINITY, 0x7FFFFFFF};
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    const float zv = z[v];
+    if (zv < thr) continue;
+    const uint32_t h = hash_u32(key ^ hash_u32(static_cast<uint32_t>(v) + 0x632BE5ABu));
+    const float u = (static_cast<float>(h >> 8) + 0.5f) * (1.f / 16777216.f);
+    const float g = -logf(-logf(u));
+    a = better(a, ArgMax{zv * invt + g, v});
+  }
+  ArgMax r = block_argmax(a, sv, si);
+  if (threadIdx.x == 0) out[row] = r.i;
+}
+
+void launch_sample(int64_t* out, const float* logits, int B, int V, long row_stride, const float* temperature,
+                   const float* top_p, const int* top_k, const int64_t* seeds, const int64_t* steps,
+                   hipStream_t s) {
+  if (B == 0) return;
+  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(1024), 0, s, out, logits, V, row_stride, temperature, top_p,
+                     top_k, seeds, steps);
+  MXS_CHECK_LAUNCH();
+}
+
+}  // namespace mxs

@@ -1,0 +1,71 @@
+"""Typed engine configuration (one dataclass tree, populated from the vLLM / SGLang /
+TRT-LLM flag dialects, `--extra-engine-args` YAML and MXS_* env; precedence CLI > YAML > env >
+defaults)."""
+from __future__ import annotations
+
+import dataclasses
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+
+@dataclass
+class EngineArgs:
+    model: str = "meta-llama/Llama-3.2-1B-Instruct"
+    served_model_name: Optional[str] = None
+    device: str = "auto"  # "auto" | "cuda" | "cpu"
+    dtype: str = "bfloat16"
+    tensor_parallel_size: int = 1
+    block_size: int = 16
+    max_model_len: int = 8192
+    max_num_seqs: int = 256
+    max_num_batched_tokens: int = 8192
+    enable_chunked_prefill: bool = True
+    enable_prefix_caching: bool = True
+    gpu_memory_utilization: float = 0.90
+    num_gpu_blocks: Optional[int] = None  # override the memory-derived count
+    enforce_eager: bool = False  # disable hipGraph capture of decode steps
+    cuda_graph_max_bs: int = 256
+    load_format: str = "auto"  # auto | safetensors | random
+    seed: int = 0
+    # disaggregation role: "agg" | "prefill" | "decode"
+    disagg_mode: str = "agg"
+    kv_transfer_backend: str = "xgmi"  # xgmi (hipIpc peer copy) | host (staged) | nixl (alias of xgmi)
+    bootstrap_port: int = 12345
+    trust_remote_code: bool = False
+    skip_tokenizer_init: bool = False
+    cpu_num_blocks: int = 2048
+
+    @property
+    def name(self) -> str:
+        return self.served_model_name or self.model
+
+    def replace(self, **kw) -> "EngineArgs":
+        return dataclasses.replace(self, **kw)
+
+    def resolved_device(self) -> str:
+        if self.device != "auto":
+            return self.device
+        import torch
+        return "cuda" if torch.cuda.is_available() else "cpu"
+
+
+def env_overrides() -> dict:
+    """MXS_* environment overrides (lowest precedence above defaults)."""
+    out = {}
+    for f in dataclasses.fields(EngineArgs):
+        v = os.environ.get("MXS_" + f.name.upper())
+        if v is None:
+            continue
+        t = f.type if isinstance(f.type, type) else str(f.type)
+        if "bool" in str(t):
+            out[f.name] = v.lower() in ("1", "true", "yes", "on")
+        elif "int" in str(t) and "Optional" not in str(t):
+            out[f.name] = int(v)
+        elif "float" in str(t):
+            out[f.name] = float(v)
+        elif "Optional[int]" in str(t):
+            out[f.name] = int(v)
+        else:
+            out[f.name] = v
+    return out

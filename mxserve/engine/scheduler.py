@@ -1,0 +1,188 @@
+"""Continuous-batching scheduler with chunked prefill and prefix caching (replaces the schedulers
+inside the vLLM / SGLang / TRT-LLM engines the reference wraps, SURVEY.md §3.3 "ENGINE STEP LOOP").
+
+Each step packs one token per running decode request plus prefill chunks under a token budget
+(`max_num_batched_tokens`); a long prompt is split over steps so decode latency stays bounded.
+When the block pool runs dry the lowest-priority (latest) running request is preempted and
+recomputed later.  Decodes are ordered before prefills in the batch, which lets the model runner
+use the decode attention kernel on the head of the batch and the prefill kernel on the tail.
+"""
+from __future__ import annotations
+
+import time
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Optional
+
+from .kv_manager import KVCacheManager
+from .request import Request, Status
+
+
+@dataclass
+class ScheduledReq:
+    req: Request
+    num_new_tokens: int
+    # sample a token at the end of this chunk (chunk reaches the end of the known tokens)
+    sample: bool
+
+
+@dataclass
+class SchedulerOutput:
+    decodes: list = field(default_factory=list)  # ScheduledReq, 1 token each
+    prefills: list = field(default_factory=list)  # ScheduledReq, chunk of >=1 token
+    preempted: list = field(default_factory=list)
+
+    @property
+    def num_tokens(self) -> int:
+        return len(self.decodes) + sum(s.num_new_tokens for s in self.prefills)
+
+    @property
+    def is_empty(self) -> bool:
+        return not self.decodes and not self.prefills
+
+    def all(self):
+        return self.decodes + self.prefills
+
+
+class Scheduler:
+    def __init__(self, kv: KVCacheManager, max_num_seqs: int = 256, max_num_batched_tokens: int = 8192,
+                 max_model_len: int = 8192, enable_chunked_prefill: bool = True):
+        self.kv = kv
+        self.max_num_seqs = max_num_seqs
+        self.max_num_batched_tokens = max_num_batched_tokens
+        self.max_model_len = max_model_len
+        self.chunked = enable_chunked_prefill
+        self.waiting: deque[Request] = deque()
+        self.running: list[Request] = []
+        self.finished_ids: list[str] = []
+        self.num_preemptions = 0
+
+    # ------------------------------------------------------------------ queue ops
+    def add(self, req: Request) -> None:
+        if req.num_prompt_tokens >= self.max_model_len:
+            raise ValueError(f"prompt of {req.num_prompt_tokens} tokens exceeds max_model_len "
+                             f"{self.max_model_len}")
+        req.status = Status.WAITING
+        self.waiting.append(req)
+
+    def abort(self, request_id: str) -> Optional[Request]:
+        for q in (self.running, self.waiting):
+            for r in list(q):
+                if r.request_id == request_id:
+                    q.remove(r)
+                    self._finish(r, Status.FINISHED_ABORTED)
+                    return r
+        return None
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def _finish(self, req: Request, status: Status) -> None:
+        req.status = status
+        req.finish_time = time.monotonic()
+        self.kv.free(req)
+
+    def _preempt(self, req: Request) -> None:
+        self.kv.free(req)
+        req.num_computed_tokens = 0
+        req.num_cached_tokens = 0
+        req.status = Status.PREEMPTED
+        req.num_preemptions += 1
+        self.num_preemptions += 1
+        self.waiting.appendleft(req)
+
+    # ------------------------------------------------------------------ schedule
+    def schedule(self) -> SchedulerOutput:
+        out = SchedulerOutput()
+        budget = self.max_num_batched_tokens
+        scheduled: list[ScheduledReq] = []
+        i = 0
+        while i < len(self.running) and budget > 0:
+            req = self.running[i]
+            n = req.num_tokens - req.num_computed_tokens
+            if n <= 0:
+                i += 1
+                continue
+            n = min(n, budget)
+            if n < req.num_tokens - req.num_computed_tokens and not self.chunked:
+                break
+            while not self.kv.allocate_slots(req, n):
+                victim = self.running.pop()
+                if victim is req:
+                    self._preempt(req)
+                    out.preempted.append(req)
+                    req = None
+                    break
+                self._preempt(victim)
+                out.preempted.append(victim)
+                scheduled = [s for s in scheduled if s.req is not victim]
+            if req is None:
+                break
+            scheduled.append(ScheduledReq(req, n, req.num_computed_tokens + n >= req.num_tokens))
+            budget -= n
+            i += 1
+
+        while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs and not out.preempted:
+            req = self.waiting[0]
+            if req.num_computed_tokens == 0 and not req.block_ids:
+                req.num_cached_tokens = self.kv.get_computed_blocks(req)
+                req.num_computed_tokens = req.num_cached_tokens
+            n = req.num_tokens - req.num_computed_tokens
+            if n > budget:
+                if not self.chunked:
+                    break
+                n = budget
+            if not self.kv.allocate_slots(req, n):
+                break
+            self.waiting.popleft()
+            req.status = Status.RUNNING
+            self.running.append(req)
+            scheduled.append(ScheduledReq(req, n, req.num_computed_tokens + n >= req.num_tokens))
+            budget -= n
+
+        for s in scheduled:
+            is_decode = s.num_new_tokens == 1 and s.req.num_computed_tokens >= s.req.num_prompt_tokens
+            (out.decodes if is_decode else out.prefills).append(s)
+        return out
+
+    # ------------------------------------------------------------------ update
+    def update(self, out: SchedulerOutput, sampled: dict[str, int]) -> list[Request]:
+        """Advance computed-token counters, append sampled tokens, retire finished requests.
+        Returns requests that produced a new token this step (finished ones included)."""
+        emitted = []
+        now = time.monotonic()
+        for s in out.all():
+            req = s.req
+            req.num_computed_tokens += s.num_new_tokens
+            self.kv.cache_computed_blocks(req)
+            if not s.sample:
+                continue
+            tok = sampled.get(req.request_id)
+            if tok is None:
+                continue
+            req.output_token_ids.append(int(tok))
+            if req.first_token_time is None:
+                req.first_token_time = now
+            st = req.check_stop(self.max_model_len)
+            if req.disagg_role == "prefill_only" and st is None:
+                st = Status.FINISHED_LENGTH
+            if st is not None:
+                if req.disagg_role == "prefill_only":
+                    # keep the blocks: the KV transfer reads them; released by release_blocks()
+                    req.status = st
+                    req.finish_time = now
+                else:
+                    self._finish(req, st)
+                self.running.remove(req)
+                self.finished_ids.append(req.request_id)
+            emitted.append(req)
+        return emitted
+
+    def release_blocks(self, req: Request) -> None:
+        self.kv.free(req)
+
+    def stats(self) -> dict:
+        return {"num_running": len(self.running), "num_waiting": len(self.waiting),
+                "kv_usage": self.kv.usage(), "kv_free_blocks": self.kv.num_free(),
+                "kv_total_blocks": self.kv.num_blocks, "prefix_hit_rate": self.kv.hit_rate(),
+                "num_preemptions": self.num_preemptions}

@@ -1,0 +1,234 @@
+"""Decoder-only transformer for the Llama / Qwen3 / Mixtral families over a paged KV cache.
+
+One forward = one engine step over a flattened token batch (decode tokens first, then prefill
+chunks; SURVEY.md §3.3 kernel sequence K01 -> L x [K02, K05, K04, K11|K12, K06, K02, K07, K10, K08]
+-> K02 -> K09).  Tensor parallelism: fused QKV / gate-up projections are
+column-parallel (whole heads per rank), o/down projections row-parallel followed by one all-reduce
+each, the LM head is vocab-parallel (all-gather of fp32 logits).  Mixtral MLPs are replaced by a
+top-2 MoE block whose experts are sharded over the same ranks (expert parallel, §2.4 P06).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import reference as ref
+from ..parallel.comm import get_tp, tp_all_gather, tp_all_reduce
+from .config import ModelConfig
+
+
+@dataclass
+class AttnMetadata:
+    """Per-step batch description (host ints + device tensors)."""
+    positions: torch.Tensor  # [T] int64
+    slot_mapping: torch.Tensor  # [T] int64
+    block_tables: torch.Tensor  # [S, max_blocks] int32
+    seq_lens: torch.Tensor  # [S] int32 total tokens in cache after this step
+    query_start_loc: torch.Tensor  # [S+1] int32
+    logits_indices: torch.Tensor  # [S_sample] int64 rows of hidden to project
+    num_decodes: int  # first num_decodes sequences have exactly one query token
+    num_prefills: int
+    num_prefill_tokens: int
+    max_query_len: int
+    max_seq_len: int
+    prefill_query_start_loc: Optional[torch.Tensor] = None  # [P+1] int32, rebased at 0
+
+    @property
+    def num_tokens(self) -> int:
+        return self.num_decodes + self.num_prefill_tokens
+
+
+def _shard_rows(w: torch.Tensor, rank: int, size: int) -> torch.Tensor:
+    n = w.shape[0] // size
+    return w[rank * n:(rank + 1) * n]
+
+
+def _shard_cols(w: torch.Tensor, rank: int, size: int) -> torch.Tensor:
+    n = w.shape[1] // size
+    return w[:, rank * n:(rank + 1) * n]
+
+
+class TransformerLM:
+    """Weights live in a flat dict of tensors (no nn.Module overhead on the hot path)."""
+
+    def __init__(self, cfg: ModelConfig, device: torch.device, dtype: torch.dtype = torch.bfloat16):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        tp = get_tp()
+        self.tp_rank, self.tp_size = tp.tp_rank, tp.tp_size
+        if cfg.num_heads % self.tp_size:
+            raise ValueError("num_heads must divide by tp_size")
+        self.nh = cfg.num_heads // self.tp_size
+        # KV heads: split when possible, otherwise replicate (e.g. 8 kv heads over tp=16)
+        self.kv_replicas = max(1, self.tp_size // cfg.num_kv_heads)
+        self.nkv = max(1, cfg.num_kv_heads // self.tp_size)
+        self.hd = cfg.head_dim
+        self.scale = 1.0 / math.sqrt(self.hd)
+        self.w: dict[str, torch.Tensor] = {}
+        self.cos_sin = ref.build_cos_sin_cache(cfg.head_dim, cfg.max_position_embeddings, cfg.rope_theta,
+                                               cfg.rope_scaling, device=self.device)
+        if cfg.is_moe:
+            if cfg.num_experts % self.tp_size:
+                raise ValueError("num_experts must divide by tp_size for expert parallelism")
+            self.e_local = cfg.num_experts // self.tp_size
+            self.e_offset = self.tp_rank * self.e_local
+        self.vocab_local = (cfg.vocab_size + self.tp_size - 1) // self.tp_size
+
+    # ------------------------------------------------------------------ weights
+    def local_shapes(self) -> dict[str, tuple]:
+        c = self.cfg
+        H, D = c.hidden_size, c.head_dim
+        shapes = {"embed": (c.vocab_size, H), "norm": (H,)}
+        if not c.tie_word_embeddings:
+            shapes["lm_head"] = (self.vocab_local, H)
+        I_loc = c.intermediate_size // self.tp_size if not c.is_moe else c.intermediate_size
+        for i in range(c.num_layers):
+            p = f"l{i}."
+            shapes[p + "in_norm"] = (H,)
+            shapes[p + "post_norm"] = (H,)
+            shapes[p + "qkv"] = ((self.nh + 2 * self.nkv) * D, H)
+            shapes[p + "o"] = (H, self.nh * D)
+            if c.qk_norm:
+                shapes[p + "q_norm"] = (D,)
+                shapes[p + "k_norm"] = (D,)
+            if c.is_moe:
+                shapes[p + "gate"] = (c.num_experts, H)
+                shapes[p + "w13"] = (self.e_local, 2 * I_loc, H)
+                shapes[p + "w2"] = (self.e_local, H, I_loc)
+            else:
+                shapes[p + "gate_up"] = (2 * I_loc, H)
+                shapes[p + "down"] = (H, I_loc)
+        return shapes
+
+    def init_random(self, seed: int = 0, std: float = 0.02) -> None:
+        """Random-init this rank's shard directly on the device (no host staging).  Synthetic
+        weights per the north star: no checkpoints are reachable on the GPU box."""
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed * 1000003 + self.tp_rank)
+        for name, shape in self.local_shapes().items():
+            if name.endswith("norm"):
+                t = torch.ones(shape, dtype=self.dtype, device=self.device)
+            else:
+                t = torch.empty(shape, dtype=self.dtype, device=self.device)
+                t.normal_(0.0, std, generator=g)
+            self.w[name] = t
+
+    def load_full_state(self, full: dict[str, torch.Tensor]) -> None:
+        """Take unsharded weights in this module's naming (see weights.py) and keep this rank's
+        shard.  Used by the safetensors loader and by TP/EP equivalence tests."""
+        c, r, s = self.cfg, self.tp_rank, self.tp_size
+        D = c.head_dim
+        out = {}
+        for name, t in full.items():
+            if name == "lm_head":
+                t = _pad_rows(t, self.vocab_local * s)
+                t = _shard_rows(t, r, s)
+            elif name.endswith(".qkv"):
+                qs, ks = c.num_heads * D, c.num_kv_heads * D
+                q, k, v = t[:qs], t[qs:qs + ks], t[qs + ks:]
+                kr = r // self.kv_replicas if self.kv_replicas > 1 else r
+                ksz = s // self.kv_replicas if self.kv_replicas > 1 else s
+                t = torch.cat([_shard_rows(q, r, s), _shard_rows(k, kr, ksz), _shard_rows(v, kr, ksz)])
+            elif name.endswith(".o"):
+                t = _shard_cols(t, r, s)
+            elif name.endswith(".gate_up"):
+                I = c.intermediate_size
+                t = torch.cat([_shard_rows(t[:I], r, s), _shard_rows(t[I:], r, s)])
+            elif name.endswith(".down"):
+                t = _shard_cols(t, r, s)
+            elif name.endswith(".w13") or name.endswith(".w2"):
+                t = t[self.e_offset:self.e_offset + self.e_local]
+            out[name] = t.to(device=self.device, dtype=self.dtype).contiguous()
+        if c.tie_word_embeddings:
+            out.pop("lm_head", None)
+        self.w = out
+
+    def lm_head_weight(self) -> torch.Tensor:
+        if self.cfg.tie_word_embeddings:
+            if self.tp_size == 1:
+                return self.w["embed"]
+            if "_lm_head_tied" not in self.w:
+                e = _pad_rows(self.w["embed"], self.vocab_local * self.tp_size)
+                self.w["_lm_head_tied"] = _shard_rows(e, self.tp_rank, self.tp_size).contiguous()
+            return self.w["_lm_head_tied"]
+        return self.w["lm_head"]
+
+    # ------------------------------------------------------------------ forward
+    def _attention(self, i: int, h: torch.Tensor, md: AttnMetadata, kv_layer: torch.Tensor):
+        c, w, p = self.cfg, self.w, f"l{i}."
+        qkv = F.linear(h, w[p + "qkv"])
+        q = ops.rope_and_cache(qkv, self.nh, self.nkv, self.hd, md.positions, self.cos_sin, kv_layer,
+                               md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"), c.rms_norm_eps)
+        nd = md.num_decodes
+        if not q.is_cuda:
+            o = ref.paged_attention(q, kv_layer, md.block_tables, md.query_start_loc, md.seq_lens, self.scale)
+        elif md.num_prefills == 0:
+            o = ops.paged_attention_decode(q, kv_layer, md.block_tables, md.seq_lens, self.scale,
+                                           md.max_seq_len)
+        elif nd == 0:
+            o = ops.paged_attention_prefill(q, kv_layer, md.block_tables, md.query_start_loc,
+                                            md.seq_lens, self.scale, md.max_query_len)
+        else:
+            o = torch.empty_like(q)
+            o[:nd] = ops.paged_attention_decode(q[:nd], kv_layer, md.block_tables[:nd], md.seq_lens[:nd],
+                                                self.scale, md.max_seq_len)
+            o[nd:] = ops.paged_attention_prefill(q[nd:], kv_layer, md.block_tables[nd:],
+                                                 md.prefill_query_start_loc, md.seq_lens[nd:], self.scale,
+                                                 md.max_query_len)
+        out = F.linear(o.reshape(o.shape[0], -1), w[p + "o"])
+        return tp_all_reduce(out)
+
+    def _mlp(self, i: int, h: torch.Tensor) -> torch.Tensor:
+        w, p = self.w, f"l{i}."
+        if self.cfg.is_moe:
+            router = F.linear(h, w[p + "gate"])
+            tw, tid = ops.moe_topk_softmax(router, self.cfg.num_experts_per_tok)
+            out = ops.moe_experts(h, w[p + "w13"], w[p + "w2"], tw, tid, self.e_offset)
+        else:
+            a = ops.silu_mul(F.linear(h, w[p + "gate_up"]))
+            out = F.linear(a, w[p + "down"])
+        return tp_all_reduce(out)
+
+    def embed(self, input_ids: torch.Tensor) -> torch.Tensor:
+        return F.embedding(input_ids, self.w["embed"])
+
+    def forward(self, input_ids: torch.Tensor, md: AttnMetadata, kv_cache: torch.Tensor) -> torch.Tensor:
+        """Returns final hidden states (normed) of the rows selected by md.logits_indices."""
+        c = self.cfg
+        x = self.embed(input_ids)
+        residual = None
+        for i in range(c.num_layers):
+            p = f"l{i}."
+            if residual is None:
+                residual = x
+                h = ops.rms_norm(x, self.w[p + "in_norm"], c.rms_norm_eps)
+            else:
+                h, residual = ops.fused_add_rms_norm(x, residual, self.w[p + "in_norm"], c.rms_norm_eps)
+            x = self._attention(i, h, md, kv_cache[:, i])
+            h, residual = ops.fused_add_rms_norm(x, residual, self.w[p + "post_norm"], c.rms_norm_eps)
+            x = self._mlp(i, h)
+        h, _ = ops.fused_add_rms_norm(x, residual, self.w["norm"], c.rms_norm_eps)
+        return h.index_select(0, md.logits_indices)
+
+    def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        logits = F.linear(hidden, self.lm_head_weight()).float()
+        if self.tp_size > 1:
+            logits = tp_all_gather(logits, dim=-1)
+        return logits[:, :self.cfg.vocab_size]
+
+
+def _pad_rows(t: torch.Tensor, n: int) -> torch.Tensor:
+    if t.shape[0] >= n:
+        return t
+    pad = torch.zeros((n - t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    return torch.cat([t, pad])
+
+
+def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16) -> TransformerLM:
+    return TransformerLM(cfg, device, dtype)

@@ -1,0 +1,141 @@
+"""Op registry: one entry point per engine op.
+
+GPU tensors go to the hand-written gfx950 HIP kernels in the in-tree extension `mxserve/_C*.so`
+(built by `python setup_ext.py` / `__graft_entry__.build()`); CPU tensors go to the PyTorch
+reference in `reference.py`.  A GPU tensor with no extension loaded is an error, never a silent
+fallback (the driver checks which `.so` files the GPU tests load).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+_EXT = None
+_EXT_ERR: Optional[BaseException] = None
+
+
+def ext():
+    """Load (once) and return the native HIP extension module."""
+    global _EXT, _EXT_ERR
+    if _EXT is None and _EXT_ERR is None:
+        try:
+            _EXT = importlib.import_module("mxserve._C")
+        except BaseException as e:  # noqa: BLE001 - re-raised on first GPU use
+            _EXT_ERR = e
+    if _EXT is None:
+        raise RuntimeError(
+            "mxserve HIP extension (mxserve/_C*.so) is not built or failed to load: "
+            f"{_EXT_ERR!r}. Run `python setup_ext.py` (hipcc --offload-arch=gfx950).")
+    return _EXT
+
+
+def has_ext() -> bool:
+    try:
+        ext()
+        return True
+    except RuntimeError:
+        return False
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda and os.environ.get("MXS_FORCE_REFERENCE_OPS", "0") != "1"
+
+
+# ----------------------------------------------------------------------------- norms / act
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    if _gpu(x):
+        out = torch.empty_like(x)
+        ext().rms_norm(out, x, w, eps)
+        return out
+    return ref.rms_norm(x, w, eps)
+
+
+def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float):
+    """Returns (normed, new_residual).  On GPU new_residual is `residual` updated in place."""
+    if _gpu(x):
+        out = torch.empty_like(x)
+        ext().fused_add_rms_norm(out, x, residual, w, eps)
+        return out, residual
+    return ref.fused_add_rms_norm(x, residual, w, eps)
+
+
+def silu_mul(gu: torch.Tensor) -> torch.Tensor:
+    if _gpu(gu):
+        out = torch.empty(gu.shape[:-1] + (gu.shape[-1] // 2,), dtype=gu.dtype, device=gu.device)
+        ext().silu_mul(out, gu)
+        return out
+    return ref.silu_mul(gu)
+
+
+# ----------------------------------------------------------------------------- attention
+def rope_and_cache(qkv: torch.Tensor, num_heads: int, num_kv_heads: int, head_dim: int,
+                   positions: torch.Tensor, cos_sin: torch.Tensor, kv_layer: torch.Tensor,
+                   slot_mapping: torch.Tensor, q_norm_w=None, k_norm_w=None, eps: float = 1e-6):
+    """qkv [T, (Hq+2Hkv)*D] (fused projection output).  Applies optional q/k head RMSNorm and RoPE,
+    writes K/V into the paged cache, returns q [T, Hq, D]."""
+    T = qkv.shape[0]
+    qs, ks = num_heads * head_dim, num_kv_heads * head_dim
+    if _gpu(qkv):
+        q = torch.empty(T, num_heads, head_dim, dtype=qkv.dtype, device=qkv.device)
+        ext().rope_and_cache(q, qkv, positions, cos_sin, kv_layer, slot_mapping,
+                             q_norm_w, k_norm_w, num_heads, num_kv_heads, head_dim, eps)
+        return q
+    q = qkv[:, :qs].reshape(T, num_heads, head_dim)
+    k = qkv[:, qs:qs + ks].reshape(T, num_kv_heads, head_dim)
+    v = qkv[:, qs + ks:].reshape(T, num_kv_heads, head_dim)
+    return ref.rope_and_cache(q, k, v, positions, cos_sin, kv_layer, slot_mapping, q_norm_w, k_norm_w, eps)
+
+
+def paged_attention_decode(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,
+                           seq_lens: torch.Tensor, scale: float, max_seq_len: int) -> torch.Tensor:
+    """One query token per sequence.  q [B, Hq, D] -> [B, Hq, D]."""
+    if _gpu(q):
+        out = torch.empty_like(q)
+        ext().paged_attention_decode(out, q, kv_layer, block_tables, seq_lens, scale, max_seq_len)
+        return out
+    return ref.paged_attention_decode(q, kv_layer, block_tables, seq_lens, scale)
+
+
+def paged_attention_prefill(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,
+                            query_start_loc: torch.Tensor, seq_lens: torch.Tensor, scale: float,
+                            max_query_len: int) -> torch.Tensor:
+    """Causal varlen attention of prefill chunks against the paged cache (prefix included)."""
+    if _gpu(q):
+        out = torch.empty_like(q)
+        ext().paged_attention_prefill(out, q, kv_layer, block_tables, query_start_loc, seq_lens,
+                                      scale, max_query_len)
+        return out
+    return ref.paged_attention(q, kv_layer, block_tables, query_start_loc, seq_lens, scale)
+
+
+# ----------------------------------------------------------------------------- sampling
+def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
+           top_k: torch.Tensor, seeds: torch.Tensor, steps: torch.Tensor) -> torch.Tensor:
+    if _gpu(logits):
+        out = torch.empty(logits.shape[0], dtype=torch.int64, device=logits.device)
+        ext().sample(out, logits, temperature, top_p, top_k, seeds, steps)
+        return out
+    return ref.sample(logits, temperature, top_p, top_k, seeds, steps)
+
+
+# ----------------------------------------------------------------------------- MoE
+def moe_topk_softmax(router_logits: torch.Tensor, k: int):
+    if _gpu(router_logits):
+        T, E = router_logits.shape
+        w = torch.empty(T, k, dtype=torch.float32, device=router_logits.device)
+        ids = torch.empty(T, k, dtype=torch.int32, device=router_logits.device)
+        ext().moe_topk_softmax(w, ids, router_logits)
+        return w, ids
+    return ref.moe_topk_softmax(router_logits, k)
+
+
+def moe_experts(x, w13, w2, topk_w, topk_ids, expert_offset: int = 0):
+    if _gpu(x):
+        from . import moe as _moe
+        return _moe.fused_experts(x, w13, w2, topk_w, topk_ids, expert_offset)
+    return ref.moe_experts(x, w13, w2, topk_w, topk_ids, expert_offset)

@@ -1,0 +1,237 @@
+"""Numerics of every gfx950 HIP kernel against the fp32 PyTorch reference (mxserve/ops/reference.py)."""
+import math
+
+import pytest
+import torch
+
+from mxserve import ops
+from mxserve.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, atol, rtol=0.0, name=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{name}: {bad} elements off, max err {err.max().item():.4g}"
+
+
+@pytest.mark.parametrize("H", [1024, 2048, 4096, 8192])
+@pytest.mark.parametrize("T", [1, 7, 128])
+def test_rms_norm(gpu, H, T):
+    x = torch.randn(T, H, device=gpu, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16()
+    _close(ops.rms_norm(x, w, 1e-5), ref.rms_norm(x.cpu(), w.cpu(), 1e-5), 0.02, 0.02, "rms_norm")
+
+
+@pytest.mark.parametrize("H", [2048, 4096])
+def test_fused_add_rms_norm(gpu, H):
+    T = 33
+    x = torch.randn(T, H, device=gpu, dtype=torch.bfloat16)
+    r = torch.randn(T, H, device=gpu, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16()
+    ey, er = ref.fused_add_rms_norm(x.cpu(), r.cpu(), w.cpu(), 1e-5)
+    y, r2 = ops.fused_add_rms_norm(x, r, w, 1e-5)
+    _close(r2, er, 0.02, 0.01, "residual")
+    _close(y, ey, 0.03, 0.02, "normed")
+
+
+@pytest.mark.parametrize("I", [8192, 3584, 1792])
+def test_silu_mul(gpu, I):
+    gu = torch.randn(19, 2 * I, device=gpu, dtype=torch.bfloat16)
+    _close(ops.silu_mul(gu), ref.silu_mul(gu.cpu()), 0.02, 0.02, "silu_mul")
+
+
+def _make_kv(nb, L, hkv, D, device, dtype=torch.bfloat16):
+    kv = torch.randn(nb, L, 2, hkv, 16, D, device=device, dtype=dtype) * 0.5
+    return kv
+
+
+@pytest.mark.parametrize("D,hq,hkv,qknorm", [(64, 32, 8, False), (128, 16, 8, True), (128, 8, 1, False)])
+def test_rope_and_cache(gpu, D, hq, hkv, qknorm):
+    T, L, nb = 37, 2, 20
+    cos_sin = ref.build_cos_sin_cache(D, 4096, 500000.0, None, device=gpu)
+    qkv = torch.randn(T, (hq + 2 * hkv) * D, device=gpu, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=gpu)
+    slots = torch.randperm(nb * 16, device=gpu)[:T]
+    slots[3] = -1
+    qn = (1 + 0.1 * torch.randn(D, device=gpu)).bfloat16() if qknorm else None
+    kn = (1 + 0.1 * torch.randn(D, device=gpu)).bfloat16() if qknorm else None
+    kv = torch.zeros(nb, L, 2, hkv, 16, D, device=gpu, dtype=torch.bfloat16)
+    kv_ref = kv.clone().cpu()
+    q = ops.rope_and_cache(qkv, hq, hkv, D, pos, cos_sin, kv[:, 1], slots, qn, kn, 1e-6)
+    qs, ks = hq * D, hkv * D
+    c = qkv.cpu()
+    q_ref = ref.rope_and_cache(c[:, :qs].reshape(T, hq, D), c[:, qs:qs + ks].reshape(T, hkv, D),
+                               c[:, qs + ks:].reshape(T, hkv, D), pos.cpu(), cos_sin.cpu(), kv_ref[:, 1],
+                               slots.cpu(), None if qn is None else qn.cpu(), None if kn is None else kn.cpu(), 1e-6)
+    _close(q, q_ref, 0.03, 0.02, "q")
+    _close(kv, kv_ref, 0.03, 0.02, "kv cache")
+    assert kv[:, 0].abs().sum().item() == 0  # other layer untouched
+
+
+def _paged_setup(seq_lens, hkv, D, L=2, device="cuda"):
+    nbs = [-(-s // 16) for s in seq_lens]
+    nb = sum(nbs) + 5
+    kv = _make_kv(nb, L, hkv, D, device)
+    perm = torch.randperm(nb)[: sum(nbs)]
+    mb = max(nbs)
+    bt = torch.zeros(len(seq_lens), mb, dtype=torch.int32)
+    o = 0
+    for i, n in enumerate(nbs):
+        bt[i, :n] = perm[o:o + n].to(torch.int32)
+        o += n
+    return kv, bt
+
+
+@pytest.mark.parametrize("D,G", [(64, 4), (128, 2), (128, 8), (64, 1), (128, 4)])
+@pytest.mark.parametrize("lens", [[1, 17, 100], [513, 2000, 31, 4096]])
+def test_paged_decode(gpu, D, G, lens):
+    hkv = 2
+    hq = hkv * G
+    kv, bt = _paged_setup(lens, hkv, D, device=gpu)
+    B = len(lens)
+    q = torch.randn(B, hq, D, device=gpu, dtype=torch.bfloat16)
+    sl = torch.tensor(lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    out = ops.paged_attention_decode(q, kv[:, 1], bt.to(gpu), sl.to(gpu), scale, max(lens))
+    exp = ref.paged_attention_decode(q.cpu(), kv[:, 1].cpu(), bt, sl, scale)
+    _close(out, exp, 0.02, 0.02, "decode")
+
+
+def test_paged_decode_graph_max_len(gpu):
+    """Graph capture launches with max_seq_len = max_model_len: idle partitions must be harmless."""
+    lens = [5, 700]
+    kv, bt = _paged_setup(lens, 8, 64, device=gpu)
+    q = torch.randn(2, 32, 64, device=gpu, dtype=torch.bfloat16)
+    sl = torch.tensor(lens, dtype=torch.int32)
+    out = ops.paged_attention_decode(q, kv[:, 0], bt.to(gpu), sl.to(gpu), 0.125, 8192)
+    exp = ref.paged_attention_decode(q.cpu(), kv[:, 0].cpu(), bt, sl, 0.125)
+    _close(out, exp, 0.02, 0.02, "decode-maxlen")
+
+
+@pytest.mark.parametrize("D,G", [(64, 4), (128, 2), (128, 8), (128, 1), (64, 8)])
+def test_paged_prefill(gpu, D, G):
+    hkv = 2
+    hq = hkv * G
+    # (context already cached, new query tokens): plain prefill, chunked continuation, 1-token tail
+    specs = [(0, 77), (300, 45), (16, 1), (0, 130), (33, 200)]
+    seq_lens = [c + n for c, n in specs]
+    kv, bt = _paged_setup(seq_lens, hkv, D, device=gpu)
+    qsl = [0]
+    for _, n in specs:
+        qsl.append(qsl[-1] + n)
+    T = qsl[-1]
+    q = torch.randn(T, hq, D, device=gpu, dtype=torch.bfloat16)
+    qsl_t = torch.tensor(qsl, dtype=torch.int32)
+    sl = torch.tensor(seq_lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    out = ops.paged_attention_prefill(q, kv[:, 1], bt.to(gpu), qsl_t.to(gpu), sl.to(gpu), scale,
+                                      max(n for _, n in specs))
+    exp = ref.paged_attention(q.cpu(), kv[:, 1].cpu(), bt, qsl_t, sl, scale)
+    _close(out, exp, 0.03, 0.03, "prefill")
+
+
+def test_prefill_softmax_rescale_spike(gpu):
+    """Force the online-softmax rescale: one key much larger late in the sequence (rule 26)."""
+    D, G, hkv = 64, 4, 1
+    lens = [256]
+    kv, bt = _paged_setup(lens, hkv, D, device=gpu)
+    q = torch.randn(256, G, D, device=gpu, dtype=torch.bfloat16)
+    nb_idx = int(bt[0, 200 // 16])
+    kv[nb_idx, 1, 0, 0, 200 % 16, :] = q[255, 0] * 4  # spike key 200 for query 255
+    out = ops.paged_attention_prefill(q, kv[:, 1], bt.to(gpu), torch.tensor([0, 256], dtype=torch.int32, device=gpu),
+                                      torch.tensor(lens, dtype=torch.int32, device=gpu), 0.125, 256)
+    exp = ref.paged_attention(q.cpu(), kv[:, 1].cpu(), bt, torch.tensor([0, 256], dtype=torch.int32),
+                              torch.tensor(lens, dtype=torch.int32), 0.125)
+    _close(out, exp, 0.03, 0.03, "prefill-spike")
+
+
+def test_sample_greedy(gpu):
+    B, V = 16, 128256
+    logits = torch.randn(B, V, device=gpu)
+    logits[3, 77] = 50.0
+    z = torch.zeros(B, device=gpu)
+    ids = ops.sample(logits, z, torch.ones(B, device=gpu), torch.zeros(B, dtype=torch.int32, device=gpu),
+                     torch.arange(B, device=gpu), torch.zeros(B, dtype=torch.int64, device=gpu))
+    assert torch.equal(ids.cpu(), logits.argmax(-1).cpu())
+    assert int(ids[3]) == 77
+
+
+@pytest.mark.parametrize("top_p,top_k", [(1.0, 0), (0.9, 0), (1.0, 50), (0.8, 20)])
+def test_sample_matches_reference(gpu, top_p, top_k):
+    B, V = 24, 32000
+    logits = torch.randn(B, V, device=gpu) * 3
+    t = torch.full((B,), 0.7, device=gpu)
+    tp = torch.full((B,), top_p, device=gpu)
+    tk = torch.full((B,), top_k, dtype=torch.int32, device=gpu)
+    seeds = torch.arange(100, 100 + B, device=gpu)
+    steps = torch.full((B,), 3, dtype=torch.int64, device=gpu)
+    ids = ops.sample(logits, t, tp, tk, seeds, steps).cpu()
+    exp = ref.sample(logits.cpu(), t.cpu(), tp.cpu(), tk.cpu(), seeds.cpu(), steps.cpu())
+    agree = (ids == exp).float().mean().item()
+    assert agree >= 0.9, f"only {agree:.2f} of rows agree with the reference sampler"
+
+
+def test_sample_distribution(gpu):
+    """Gumbel-max frequencies follow softmax(z/T)."""
+    V, N = 8, 4000
+    z = torch.tensor([2.0, 1.0, 0.5, 0.0, -1.0, -2.0, -3.0, -4.0], device=gpu)
+    logits = z.unsqueeze(0).repeat(N, 1).contiguous()
+    t = torch.ones(N, device=gpu)
+    ids = ops.sample(logits, t, torch.ones(N, device=gpu), torch.zeros(N, dtype=torch.int32, device=gpu),
+                     torch.arange(N, device=gpu), torch.zeros(N, dtype=torch.int64, device=gpu)).cpu()
+    freq = torch.bincount(ids, minlength=V).float() / N
+    p = torch.softmax(z.cpu(), -1)
+    assert (freq - p).abs().max().item() < 0.03
+
+
+def test_moe_topk_softmax(gpu):
+    T, E, K = 100, 8, 2
+    logits = torch.randn(T, E, device=gpu, dtype=torch.bfloat16)
+    w, ids = ops.moe_topk_softmax(logits, K)
+    ew, eids = ref.moe_topk_softmax(logits.cpu(), K)
+    assert torch.equal(ids.cpu(), eids)
+    _close(w, ew, 1e-3, 1e-3, "topk weights")
+
+
+def test_moe_align(gpu):
+    T, K, E = 300, 2, 8
+    ids = torch.randint(0, E, (T, K), dtype=torch.int32, device=gpu)
+    offs = torch.empty(E // 2 + 1, dtype=torch.int32, device=gpu)
+    perm = torch.full((T * K,), -1, dtype=torch.int32, device=gpu)
+    ops.ext().moe_align(offs, perm, ids, 4, E // 2)  # local experts 4..7
+    flat = ids.flatten().cpu()
+    o = offs.cpu().tolist()
+    p = perm.cpu()
+    for e in range(E // 2):
+        rows = p[o[e]:o[e + 1]]
+        exp = (flat == e + 4).nonzero().flatten()
+        assert torch.equal(rows.long(), exp), f"expert {e}"
+
+
+@pytest.mark.parametrize("T", [64, 300])
+def test_moe_experts_gpu_vs_ref(gpu, T):
+    H, I, E, K = 256, 192, 4, 2
+    x = torch.randn(T, H, device=gpu, dtype=torch.bfloat16)
+    w13 = torch.randn(E, 2 * I, H, device=gpu, dtype=torch.bfloat16) * 0.05
+    w2 = torch.randn(E, H, I, device=gpu, dtype=torch.bfloat16) * 0.05
+    logits = torch.randn(T, E, device=gpu, dtype=torch.bfloat16)
+    tw, tid = ops.moe_topk_softmax(logits, K)
+    out = ops.moe_experts(x, w13, w2, tw, tid, 0)
+    exp = ref.moe_experts(x.cpu(), w13.cpu(), w2.cpu(), tw.cpu(), tid.cpu(), 0)
+    _close(out, exp, 0.02, 0.03, "moe")
+
+
+def test_copy_blocks(gpu):
+    src = torch.randn(10, 4, 512, device=gpu, dtype=torch.bfloat16)
+    dst = torch.zeros(12, 4, 512, device=gpu, dtype=torch.bfloat16)
+    s_ids = torch.tensor([1, 5, 9], dtype=torch.int32, device=gpu)
+    d_ids = torch.tensor([0, 11, 3], dtype=torch.int32, device=gpu)
+    ops.ext().copy_blocks(dst.data_ptr(), src, s_ids, d_ids, src[0].numel() * 2)
+    torch.cuda.synchronize()
+    for s, d in zip(s_ids.tolist(), d_ids.tolist()):
+        assert torch.equal(dst[d], src[s])
+    assert dst[1].abs().sum().item() == 0
