@@ -4,6 +4,7 @@ worker HTTP server and by the in-process benchmark)."""
 from __future__ import annotations
 
 import asyncio
+import collections
 import logging
 import threading
 import time
@@ -68,6 +69,33 @@ class LLMEngine:
         self.requests.pop(request_id, None)
         self.runner.release(request_id)
 
+    # ------------------------------------------------------------------ disaggregation
+    def reserve_remote_prefill(self, prompt_token_ids: list, sampling: SamplingParams,
+                               request_id: str) -> Optional[Request]:
+        """Decode side: allocate the prompt's blocks; None if the pool is full."""
+        req = Request(request_id, list(prompt_token_ids), sampling, eos_token_ids=self.eos,
+                      disagg_role="remote_prefill")
+        if not self.scheduler.reserve_remote(req):
+            return None
+        self.requests[request_id] = req
+        return req
+
+    def complete_remote_prefill(self, request_id: str, first_token: int) -> StepOutput:
+        req = self.scheduler.complete_remote(request_id, first_token)
+        fin = req.is_finished
+        if fin:
+            self.requests.pop(request_id, None)
+            self.runner.release(request_id)
+        self.num_generated += 1
+        return StepOutput(req.request_id, int(first_token), fin, req.status.value if fin else None,
+                          req.num_prompt_tokens, req.num_cached_tokens, len(req.output_token_ids))
+
+    def release_prefill_blocks(self, request_id: str) -> None:
+        """Prefill side: drop the blocks kept alive for the KV transfer."""
+        req = self.requests.pop(request_id, None)
+        if req is not None:
+            self.scheduler.release_blocks(req)
+
     def has_unfinished(self) -> bool:
         return self.scheduler.has_work()
 
@@ -113,50 +141,96 @@ class LLMEngine:
 
 
 class AsyncEngine:
-    """Thread-driven engine loop with asyncio fan-out."""
+    """Engine loop on a dedicated thread.  The asyncio side never takes a lock that the step holds:
+    commands (add / abort / disagg hooks) go through a thread-safe inbox drained by the engine
+    thread between steps, and results come back through futures; tokens fan out to per-request
+    asyncio queues."""
 
     def __init__(self, engine: LLMEngine):
         self.engine = engine
-        self._lock = threading.Lock()
+        self._inbox: collections.deque = collections.deque()
         self._wake = threading.Event()
         self._queues: dict[str, tuple[asyncio.AbstractEventLoop, asyncio.Queue]] = {}
         self._stop = False
+        self.on_step = None  # optional callback(list[StepOutput]) run on the engine thread
+        self.last_stats: dict = engine.stats()
         self._thread = threading.Thread(target=self._loop, name="mxs-engine", daemon=True)
-        self.on_step = None  # optional callback(list[StepOutput])
         self._thread.start()
+
+    # ---------------------------------------------------------------- engine thread
+    def _drain(self) -> None:
+        while self._inbox:
+            fn, a, kw, loop, fut = self._inbox.popleft()
+            try:
+                r = fn(*a, **kw)
+                if fut is not None:
+                    loop.call_soon_threadsafe(_set_result, fut, r, None)
+            except BaseException as e:  # noqa: BLE001 - delivered to the awaiting coroutine
+                if fut is not None:
+                    loop.call_soon_threadsafe(_set_result, fut, None, e)
+                else:
+                    log.exception("engine command failed")
 
     def _loop(self) -> None:
         while not self._stop:
-            with self._lock:
-                busy = self.engine.has_unfinished()
-                outs = self.engine.step() if busy else []
-            if not busy:
+            self._drain()
+            if not self.engine.has_unfinished():
+                self.last_stats = self.engine.stats()
                 self._wake.wait(0.05)
                 self._wake.clear()
                 continue
+            try:
+                outs = self.engine.step()
+            except Exception:  # noqa: BLE001 - fail the in-flight requests, keep serving
+                log.exception("engine step failed")
+                outs = self._fail_all()
+            self.last_stats = self.engine.stats()
             if self.on_step is not None:
                 try:
                     self.on_step(outs)
                 except Exception:  # noqa: BLE001
                     log.exception("on_step callback failed")
-            for o in outs:
-                ent = self._queues.get(o.request_id)
-                if ent is None:
-                    continue
-                loop, q = ent
-                loop.call_soon_threadsafe(q.put_nowait, o)
-                if o.finished:
-                    self._queues.pop(o.request_id, None)
+            self._deliver(outs)
 
-    async def generate(self, prompt_token_ids: list, sampling: SamplingParams, request_id: Optional[str] = None,
-                       disagg_role: Optional[str] = None):
-        """Async iterator of StepOutput for one request."""
-        rid = request_id or uuid.uuid4().hex
-        q: asyncio.Queue = asyncio.Queue()
-        self._queues[rid] = (asyncio.get_running_loop(), q)
-        with self._lock:
-            self.engine.add_request(prompt_token_ids, sampling, rid, disagg_role)
+    def _deliver(self, outs) -> None:
+        for o in outs:
+            ent = self._queues.get(o.request_id)
+            if ent is None:
+                continue
+            loop, q = ent
+            loop.call_soon_threadsafe(q.put_nowait, o)
+            if o.finished:
+                self._queues.pop(o.request_id, None)
+
+    def _fail_all(self) -> list:
+        outs = []
+        for rid in list(self.engine.requests):
+            self.engine.abort(rid)
+            outs.append(StepOutput(rid, -1, True, "error", 0, 0, 0))
+        return outs
+
+    # ---------------------------------------------------------------- asyncio side
+    def submit(self, fn, *a, **kw) -> asyncio.Future:
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self._inbox.append((fn, a, kw, loop, fut))
         self._wake.set()
+        return fut
+
+    def submit_nowait(self, fn, *a, **kw) -> None:
+        self._inbox.append((fn, a, kw, None, None))
+        self._wake.set()
+
+    def open_stream(self, request_id: str) -> asyncio.Queue:
+        q: asyncio.Queue = asyncio.Queue()
+        self._queues[request_id] = (asyncio.get_running_loop(), q)
+        return q
+
+    def push(self, out: StepOutput) -> None:
+        """Deliver an output produced outside a step (e.g. a remotely prefilled first token)."""
+        self._deliver([out])
+
+    async def stream(self, request_id: str, q: asyncio.Queue):
         try:
             while True:
                 o = await q.get()
@@ -164,18 +238,35 @@ class AsyncEngine:
                 if o.finished:
                     return
         finally:
-            if self._queues.pop(rid, None) is not None:
-                with self._lock:
-                    self.engine.abort(rid)
+            if self._queues.pop(request_id, None) is not None:  # client went away mid-stream
+                self.submit_nowait(self.engine.abort, request_id)
 
-    def run_locked(self, fn, *a, **kw):
-        with self._lock:
-            return fn(*a, **kw)
+    async def generate(self, prompt_token_ids: list, sampling: SamplingParams, request_id: Optional[str] = None,
+                       disagg_role: Optional[str] = None):
+        """Async iterator of StepOutput for one request."""
+        rid = request_id or uuid.uuid4().hex
+        q = self.open_stream(rid)
+        try:
+            await self.submit(self.engine.add_request, prompt_token_ids, sampling, rid, disagg_role)
+        except BaseException:
+            self._queues.pop(rid, None)
+            raise
+        async for o in self.stream(rid, q):
+            yield o
 
     def shutdown(self) -> None:
         self._stop = True
         self._wake.set()
         self._thread.join(timeout=5)
+
+
+def _set_result(fut: asyncio.Future, r, e) -> None:
+    if fut.done():
+        return
+    if e is not None:
+        fut.set_exception(e)
+    else:
+        fut.set_result(r)
 
 
 def now() -> float:

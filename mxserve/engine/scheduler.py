@@ -56,6 +56,8 @@ class Scheduler:
         self.running: list[Request] = []
         self.finished_ids: list[str] = []
         self.num_preemptions = 0
+        # disaggregated decode: requests whose prompt KV is being written by a prefill worker
+        self.remote: dict[str, Request] = {}
 
     # ------------------------------------------------------------------ queue ops
     def add(self, req: Request) -> None:
@@ -66,6 +68,8 @@ class Scheduler:
         self.waiting.append(req)
 
     def abort(self, request_id: str) -> Optional[Request]:
+        if request_id in self.remote:
+            return self.cancel_remote(request_id)
         for q in (self.running, self.waiting):
             for r in list(q):
                 if r.request_id == request_id:
@@ -76,6 +80,41 @@ class Scheduler:
 
     def has_work(self) -> bool:
         return bool(self.waiting or self.running)
+
+    # ------------------------------------------------------------------ disaggregation (decode side)
+    def reserve_remote(self, req: Request) -> bool:
+        """Allocate KV blocks for the whole prompt of a request whose prefill runs remotely.
+        Locally cached prefix blocks are reused (only the rest must be transferred)."""
+        req.num_cached_tokens = self.kv.get_computed_blocks(req)
+        req.num_computed_tokens = req.num_cached_tokens
+        if not self.kv.allocate_slots(req, req.num_prompt_tokens - req.num_computed_tokens):
+            self.kv.free(req)
+            req.num_computed_tokens = req.num_cached_tokens = 0
+            return False
+        req.status = Status.WAITING
+        self.remote[req.request_id] = req
+        return True
+
+    def complete_remote(self, request_id: str, first_token: int) -> Request:
+        """KV for the prompt has landed: the request joins the running batch with its first token."""
+        req = self.remote.pop(request_id)
+        req.num_computed_tokens = req.num_prompt_tokens
+        self.kv.cache_computed_blocks(req)
+        req.output_token_ids.append(int(first_token))
+        req.first_token_time = time.monotonic()
+        st = req.check_stop(self.max_model_len)
+        if st is not None:
+            self._finish(req, st)
+        else:
+            req.status = Status.RUNNING
+            self.running.append(req)
+        return req
+
+    def cancel_remote(self, request_id: str) -> Optional[Request]:
+        req = self.remote.pop(request_id, None)
+        if req is not None:
+            self._finish(req, Status.FINISHED_ABORTED)
+        return req
 
     def _finish(self, req: Request, status: Status) -> None:
         req.status = status

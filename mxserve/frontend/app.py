@@ -1,0 +1,425 @@
+"""OpenAI-compatible HTTP frontend (replaces the Dynamo frontend: componentType frontend,
+examples/deploy/vllm/agg.yaml:12-17; port 8000, README.md:260).
+
+  GET  /v1/models                 {object: list, data: [{id, object: model, ...}]}
+  POST /v1/chat/completions       chat template -> tokens -> router -> worker stream (SSE or unary)
+  POST /v1/completions            same for raw prompts
+  GET  /health /live /metrics     readiness = at least one worker registered; dynamo_frontend_* metrics
+  POST /internal/register|heartbeat, GET /internal/workers   discovery (replaces etcd)
+
+Errors are `{"error": {"message": ...}}` (multi_convos_parallel.sh:44-45); `Authorization` is
+accepted and ignored (chat.sh:89).  The frontend tokenizes (workers run with
+--skip-tokenizer-init semantics), streams incremental detokenized text, applies stop strings,
+and retries a request on another worker if its worker fails before the first token.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import time
+import uuid
+from dataclasses import dataclass
+from typing import AsyncIterator, Optional
+
+from fastapi import FastAPI, Request as HTTPRequest
+from fastapi.responses import JSONResponse, Response, StreamingResponse
+
+from ..models.config import get_model_config
+from ..router.router import Registry, Router, WorkerInfo
+from .chat_template import render
+from .metrics import FrontendMetrics
+from .tokenizer import IncrementalDetokenizer, load_tokenizer
+
+log = logging.getLogger("mxserve.frontend")
+
+
+class APIError(Exception):
+    def __init__(self, status: int, message: str, etype: str = "invalid_request_error"):
+        super().__init__(message)
+        self.status, self.message, self.etype = status, message, etype
+
+
+def _err(status: int, message: str, etype: str = "invalid_request_error") -> JSONResponse:
+    return JSONResponse({"error": {"message": message, "type": etype, "code": status}}, status_code=status)
+
+
+@dataclass
+class TokenEvent:
+    token_id: int
+    finished: bool
+    finish_reason: Optional[str]
+    num_prompt_tokens: int
+    num_cached_tokens: int
+
+
+class LocalWorker:
+    """In-process worker (single-process serving: frontend + engine, no HTTP hop)."""
+
+    def __init__(self, aeng, model: str):
+        self.aeng = aeng
+        self.model = model
+
+    async def generate(self, token_ids, sampling: dict, request_id: str, prefill_url=None) -> AsyncIterator[TokenEvent]:
+        from ..worker.server import _sampling
+        async for o in self.aeng.generate(token_ids, _sampling(sampling), request_id):
+            yield TokenEvent(o.token_id, o.finished, o.finish_reason, o.num_prompt_tokens, o.num_cached_tokens)
+
+
+class Frontend:
+    def __init__(self, router_mode: str = "kv", ttl: float = 10.0, namespace: str = "default"):
+        self.registry = Registry(ttl=ttl)
+        self.router = Router(self.registry, router_mode)
+        self.metrics = FrontendMetrics()
+        self.namespace = namespace
+        self._tok = {}
+        self._cfg = {}
+        self.local: dict[str, LocalWorker] = {}
+        self._http = None
+        self.started = time.time()
+        self.app = self._build_app()
+
+    # ---------------------------------------------------------------- model info
+    def tokenizer(self, model: str):
+        if model not in self._tok:
+            cfg = get_model_config(model)
+            self._cfg[model] = cfg
+            self._tok[model] = load_tokenizer(cfg)
+        return self._tok[model]
+
+    def model_cfg(self, model: str):
+        self.tokenizer(model)
+        return self._cfg[model]
+
+    def add_local_worker(self, aeng, model: str, kv_total_blocks: int) -> None:
+        self.local[model] = LocalWorker(aeng, model)
+        self.registry.register(WorkerInfo(worker_id=f"local-{model}", url="local://", model=model,
+                                          kv_total_blocks=kv_total_blocks))
+        self.registry.workers[f"local-{model}"].last_seen = float("inf")
+
+    def resolve_model(self, name: Optional[str]) -> str:
+        models = self.registry.models()
+        if name in models:
+            return name
+        if name:
+            base = name.rstrip("/").split("/")[-1].lower()
+            for m in models:
+                if m.rstrip("/").split("/")[-1].lower() == base:
+                    return m
+        if not name and len(models) == 1:
+            return models[0]
+        raise APIError(404, f"The model `{name}` does not exist." if name else "model is required",
+                       "model_not_found")
+
+    async def http(self):
+        if self._http is None:
+            import aiohttp
+            self._http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None, sock_connect=5),
+                                               connector=aiohttp.TCPConnector(limit=0))
+        return self._http
+
+    # ---------------------------------------------------------------- request plane
+    async def _worker_stream(self, w: WorkerInfo, token_ids, sampling: dict, rid: str,
+                             prefill_url: Optional[str]) -> AsyncIterator[TokenEvent]:
+        if w.url.startswith("local://"):
+            async for ev in self.local[w.model].generate(token_ids, sampling, rid, prefill_url):
+                yield ev
+            return
+        sess = await self.http()
+        body = {"request_id": rid, "token_ids": token_ids, "sampling": sampling}
+        if prefill_url:
+            body["prefill_url"] = prefill_url
+        async with sess.post(w.url.rstrip("/") + "/generate", json=body) as r:
+            if r.status != 200:
+                raise ConnectionError(f"worker {w.worker_id} returned {r.status}")
+            async for line in r.content:
+                if not line.strip():
+                    continue
+                d = json.loads(line)
+                if d["t"] < 0:
+                    raise RuntimeError("worker failed the request")
+                yield TokenEvent(d["t"], d["f"], d["r"], d["p"], d["c"])
+
+    async def generate_tokens(self, model: str, token_ids: list, sampling: dict, rid: str) -> AsyncIterator[TokenEvent]:
+        """Route + stream, retrying on another worker if one fails before the first token."""
+        tried: set = set()
+        for attempt in range(3):
+            decode = [w for w in self.registry.list(model) if w.role in ("agg", "decode") and w.worker_id not in tried]
+            prefill = [w for w in self.registry.list(model, "prefill")]
+            if not decode:
+                raise APIError(503, f"no workers available for model {model}", "service_unavailable")
+            w, overlap = self.router.pick(decode, token_ids)
+            purl = None
+            if w.role == "decode" and prefill:
+                pw, _ = self.router.pick(prefill, token_ids)
+                purl = pw.url
+            if overlap:
+                self.metrics.kv_hit.labels(model).inc(overlap)
+            got_any = False
+            w.inflight += 1
+            try:
+                async for ev in self._worker_stream(w, token_ids, sampling, rid, purl):
+                    got_any = True
+                    yield ev
+                return
+            except (ConnectionError, OSError, asyncio.TimeoutError) as e:
+                if got_any:
+                    raise
+                log.warning("worker %s failed before first token (%r); retrying", w.worker_id, e)
+                tried.add(w.worker_id)
+                try:
+                    import aiohttp
+                    if isinstance(e, aiohttp.ClientConnectionError):
+                        self.registry.deregister(w.worker_id)
+                except ImportError:
+                    pass
+            finally:
+                w.inflight -= 1
+        raise APIError(503, "all workers failed", "service_unavailable")
+
+    # ---------------------------------------------------------------- OpenAI layer
+    def _sampling(self, body: dict, model: str, n_prompt: int) -> dict:
+        cfg = self.model_cfg(model)
+        limit = cfg.max_position_embeddings
+        mt = body.get("max_completion_tokens", body.get("max_tokens"))
+        mt = int(mt) if mt is not None else max(1, min(4096, limit - n_prompt))
+        if mt <= 0:
+            raise APIError(400, "max_tokens must be positive")
+        t = body.get("temperature")
+        tp = body.get("top_p")
+        if t is not None and not (0.0 <= float(t) <= 2.0):
+            raise APIError(400, "temperature must be in [0, 2]")
+        if body.get("n", 1) not in (1, None):
+            raise APIError(400, "only n=1 is supported")
+        return {"max_tokens": mt, "temperature": 1.0 if t is None else float(t),
+                "top_p": 1.0 if tp is None else float(tp), "top_k": int(body.get("top_k") or 0),
+                "seed": body.get("seed"), "ignore_eos": bool(body.get("ignore_eos", False)),
+                "min_tokens": int(body.get("min_tokens") or 0),
+                "stop_token_ids": list(body.get("stop_token_ids") or [])}
+
+    async def _run(self, endpoint: str, body: dict, prompt_ids: list, model: str, chat: bool):
+        stream = bool(body.get("stream", False))
+        rtype = "stream" if stream else "unary"
+        sampling = self._sampling(body, model, len(prompt_ids))
+        stops = body.get("stop") or []
+        if isinstance(stops, str):
+            stops = [stops]
+        rid = ("chatcmpl-" if chat else "cmpl-") + uuid.uuid4().hex
+        created = int(time.time())
+        tok = self.tokenizer(model)
+        m = self.metrics
+        m.inflight.labels(model).inc()
+        m.queued.labels(model).inc()
+        m.isl.labels(model).observe(len(prompt_ids))
+        t0 = time.perf_counter()
+        state = {"first": None, "last": None, "n": 0, "queued": True}
+
+        def on_token():
+            now = time.perf_counter()
+            if state["first"] is None:
+                state["first"] = now
+                m.ttft.labels(model).observe(now - t0)
+                m.queued.labels(model).dec()
+                state["queued"] = False
+            else:
+                m.itl.labels(model).observe(now - state["last"])
+            state["last"] = now
+            state["n"] += 1
+
+        def finish(status: str):
+            m.requests.labels(model, endpoint, rtype, status).inc()
+            m.inflight.labels(model).dec()
+            if state["queued"]:
+                m.queued.labels(model).dec()
+            m.duration.labels(model).observe(time.perf_counter() - t0)
+            m.osl.labels(model).observe(state["n"])
+
+        async def events():
+            """Yields (text_delta, finish_reason|None)."""
+            detok = IncrementalDetokenizer(tok)
+            text_so_far = ""
+            async for ev in self.generate_tokens(model, prompt_ids, sampling, rid):
+                on_token()
+                delta = detok.add(ev.token_id) if not (ev.finished and ev.finish_reason == "stop"
+                                                      and ev.token_id in tok.eos_token_ids) else ""
+                reason = ev.finish_reason if ev.finished else None
+                if ev.finished:
+                    delta += detok.flush()
+                if stops and delta:
+                    cand = text_so_far + delta
+                    hit = min((cand.find(s) for s in stops if s and s in cand), default=-1)
+                    if hit >= 0:
+                        yield cand[len(text_so_far):hit], "stop"
+                        return
+                    text_so_far = cand
+                if reason == "abort":
+                    reason = "stop"
+                yield delta, reason
+                if ev.finished:
+                    return
+
+        obj = "chat.completion" if chat else "text_completion"
+        if not stream:
+            try:
+                parts, reason = [], None
+                async for d, r in events():
+                    parts.append(d)
+                    reason = r or reason
+            except APIError:
+                finish("error")
+                raise
+            except Exception as e:  # noqa: BLE001
+                finish("error")
+                raise APIError(500, f"generation failed: {e}", "server_error")
+            finish("success")
+            text = "".join(parts)
+            choice = ({"index": 0, "message": {"role": "assistant", "content": text}, "finish_reason": reason or "stop"}
+                      if chat else {"index": 0, "text": text, "logprobs": None, "finish_reason": reason or "stop"})
+            return JSONResponse({"id": rid, "object": obj, "created": created, "model": model, "choices": [choice],
+                                 "usage": {"prompt_tokens": len(prompt_ids), "completion_tokens": state["n"],
+                                           "total_tokens": len(prompt_ids) + state["n"]}})
+
+        include_usage = bool((body.get("stream_options") or {}).get("include_usage"))
+        chunk_obj = "chat.completion.chunk" if chat else "text_completion"
+
+        def chunk(delta: Optional[str], reason: Optional[str], first: bool = False) -> bytes:
+            if chat:
+                d = {}
+                if first:
+                    d["role"] = "assistant"
+                if delta is not None:
+                    d["content"] = delta
+                ch = {"index": 0, "delta": d, "finish_reason": reason}
+            else:
+                ch = {"index": 0, "text": delta or "", "logprobs": None, "finish_reason": reason}
+            return ("data: " + json.dumps({"id": rid, "object": chunk_obj, "created": created, "model": model,
+                                           "choices": [ch]}) + "\n\n").encode()
+
+        async def sse():
+            status = "success"
+            try:
+                if chat:
+                    yield chunk("", None, first=True)
+                async for d, r in events():
+                    if d or r:
+                        yield chunk(d if d else ("" if r else None), r)
+                if include_usage:
+                    yield ("data: " + json.dumps({"id": rid, "object": chunk_obj, "created": created, "model": model,
+                                                  "choices": [], "usage": {"prompt_tokens": len(prompt_ids),
+                                                                           "completion_tokens": state["n"],
+                                                                           "total_tokens": len(prompt_ids) + state["n"]}})
+                           + "\n\n").encode()
+                yield b"data: [DONE]\n\n"
+            except APIError as e:
+                status = "error"
+                yield ("data: " + json.dumps({"error": {"message": e.message, "type": e.etype, "code": e.status}})
+                       + "\n\n").encode()
+            except Exception as e:  # noqa: BLE001
+                status = "error"
+                yield ("data: " + json.dumps({"error": {"message": str(e), "type": "server_error"}}) + "\n\n").encode()
+            finally:
+                finish(status)
+
+        return StreamingResponse(sse(), media_type="text/event-stream",
+                                 headers={"Cache-Control": "no-cache", "X-Request-Id": rid})
+
+    # ---------------------------------------------------------------- app
+    def _build_app(self) -> FastAPI:
+        app = FastAPI(title="mxserve frontend")
+        fe = self
+
+        @app.exception_handler(APIError)
+        async def _api_err(_req, e: APIError):
+            return _err(e.status, e.message, e.etype)
+
+        @app.get("/v1/models")
+        async def models():
+            data = [{"id": m, "object": "model", "created": int(fe.started), "owned_by": "mxserve"}
+                    for m in fe.registry.models()]
+            return {"object": "list", "data": data}
+
+        @app.post("/v1/chat/completions")
+        async def chat(request: HTTPRequest):
+            try:
+                body = await request.json()
+            except Exception:  # noqa: BLE001
+                return _err(400, "invalid JSON body")
+            if not isinstance(body, dict) or "messages" not in body:
+                return _err(400, "`messages` is required")
+            model = fe.resolve_model(body.get("model"))
+            try:
+                text = render(fe.model_cfg(model).chat_template, body["messages"])
+            except ValueError as e:
+                return _err(400, str(e))
+            ids = fe.tokenizer(model).encode(text)
+            return await fe._run("chat_completions", body, ids, model, chat=True)
+
+        @app.post("/v1/completions")
+        async def completions(request: HTTPRequest):
+            try:
+                body = await request.json()
+            except Exception:  # noqa: BLE001
+                return _err(400, "invalid JSON body")
+            model = fe.resolve_model(body.get("model"))
+            p = body.get("prompt")
+            if isinstance(p, list) and p and isinstance(p[0], int):
+                ids = list(p)
+            elif isinstance(p, str):
+                ids = fe.tokenizer(model).encode(p, add_special_tokens=True)
+            else:
+                return _err(400, "`prompt` must be a string or a list of token ids")
+            return await fe._run("completions", body, ids, model, chat=False)
+
+        @app.get("/health")
+        async def health():
+            ws = fe.registry.list()
+            if not ws:
+                return JSONResponse({"status": "no workers", "workers": []}, status_code=503)
+            return {"status": "healthy", "models": fe.registry.models(), "workers": len(ws)}
+
+        @app.get("/live")
+        async def live():
+            return {"status": "alive"}
+
+        @app.get("/metrics")
+        async def metrics():
+            for role in ("agg", "prefill", "decode"):
+                for model in fe.registry.models():
+                    fe.metrics.workers.labels(model, role).set(len(fe.registry.list(model, role)))
+            return Response(fe.metrics.render(), media_type="text/plain; version=0.0.4")
+
+        @app.post("/internal/register")
+        async def register(request: HTTPRequest):
+            d = await request.json()
+            info = WorkerInfo(worker_id=d["worker_id"], url=d["url"], model=d["model"], role=d.get("role", "agg"),
+                              block_size=int(d.get("block_size", 16)),
+                              kv_total_blocks=int(d.get("kv_total_blocks", 1) or 1), tp=int(d.get("tp", 1)))
+            fe.registry.register(info)
+            log.info("registered worker %s (%s) for %s at %s", info.worker_id, info.role, info.model, info.url)
+            return {"ok": True, "index": info.index}
+
+        @app.post("/internal/heartbeat")
+        async def heartbeat(request: HTTPRequest):
+            d = await request.json()
+            ok = fe.registry.heartbeat(d["worker_id"], d.get("load", {}), d.get("stored", ()), d.get("removed", ()))
+            return JSONResponse({"ok": ok}, status_code=200 if ok else 404)
+
+        @app.get("/internal/workers")
+        async def workers():
+            return {"workers": [w.public() for w in fe.registry.list()]}
+
+        @app.on_event("startup")
+        async def _startup():
+            async def reaper():
+                while True:
+                    await asyncio.sleep(1.0)
+                    for wid in fe.registry.expire():
+                        log.warning("worker %s lease expired", wid)
+            asyncio.get_running_loop().create_task(reaper())
+
+        @app.on_event("shutdown")
+        async def _shutdown():
+            if fe._http is not None:
+                await fe._http.close()
+
+        return app

@@ -1,0 +1,135 @@
+"""Tokenizers for the preprocessor.
+
+* HFTokenizer: a real `tokenizer.json` found on disk (HF_HOME / model dir) via the installed Rust
+  `tokenizers` library.
+* ByteTokenizer: self-contained fallback for the offline GPU box / random-init weights.  UTF-8
+  bytes map to ids [BYTE0, BYTE0 + 256), chat-template special tokens map to the model's real
+  special ids (Llama-3 / ChatML / Mistral), and any other id (random weights produce arbitrary
+  ids) decodes to a deterministic pseudo-word so streamed text stays readable.
+Both expose encode / decode / an incremental detokenizer used for streaming.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+from ..models.config import ModelConfig, find_local_model_dir
+
+BYTE0 = 3
+
+_SPECIALS = {
+    "llama3": {"<|begin_of_text|>": 128000, "<|end_of_text|>": 128001, "<|start_header_id|>": 128006,
+               "<|end_header_id|>": 128007, "<|eom_id|>": 128008, "<|eot_id|>": 128009},
+    "chatml": {"<|endoftext|>": 151643, "<|im_start|>": 151644, "<|im_end|>": 151645, "<think>": 151667,
+               "</think>": 151668},
+    "mistral": {"<s>": 1, "</s>": 2, "[INST]": 3, "[/INST]": 4},
+}
+
+_SYL = ["ka", "lo", "mi", "ne", "ru", "sa", "ti", "vo", "ze", "an", "el", "or", "um", "is", "ya", "po"]
+
+
+class ByteTokenizer:
+    def __init__(self, cfg: ModelConfig):
+        self.vocab_size = cfg.vocab_size
+        specials = dict(_SPECIALS.get(cfg.chat_template, {}))
+        # keep only specials that fit the vocab (tiny test models)
+        self.special_to_id = {k: v for k, v in specials.items() if v < cfg.vocab_size}
+        self.id_to_special = {v: k for k, v in self.special_to_id.items()}
+        self.byte0 = BYTE0 if cfg.chat_template != "mistral" else 8
+        self.eos_token_ids = list(cfg.eos_token_ids)
+        self.bos_token_id = cfg.bos_token_id
+        self._sorted_specials = sorted(self.special_to_id, key=len, reverse=True)
+
+    def encode(self, text: str, add_special_tokens: bool = False) -> list[int]:
+        ids: list[int] = []
+        if add_special_tokens and self.bos_token_id is not None:
+            ids.append(self.bos_token_id)
+        i = 0
+        n = len(text)
+        while i < n:
+            if text[i] in "<[":
+                hit = next((s for s in self._sorted_specials if text.startswith(s, i)), None)
+                if hit is not None:
+                    ids.append(self.special_to_id[hit])
+                    i += len(hit)
+                    continue
+            j = i
+            while j < n and text[j] not in "<[":
+                j += 1
+            if j == i:
+                j = i + 1
+            ids.extend(self.byte0 + b for b in text[i:j].encode("utf-8"))
+            i = j
+        return ids
+
+    def _piece(self, t: int, skip_special: bool) -> bytes:
+        if self.byte0 <= t < self.byte0 + 256:
+            return bytes([t - self.byte0])
+        if t in self.id_to_special:
+            return b"" if skip_special else self.id_to_special[t].encode()
+        if t < self.byte0:
+            return b""
+        # deterministic pseudo-word for ids outside the byte range
+        x = (t * 2654435761) & 0xFFFFFFFF
+        w = _SYL[x & 15] + _SYL[(x >> 4) & 15] + (_SYL[(x >> 8) & 15] if x & 0x1000 else "")
+        return (" " + w).encode()
+
+    def decode(self, ids: list[int], skip_special_tokens: bool = True) -> str:
+        return b"".join(self._piece(int(t), skip_special_tokens) for t in ids).decode("utf-8", errors="replace")
+
+    def convert_special(self, name: str) -> Optional[int]:
+        return self.special_to_id.get(name)
+
+
+class HFTokenizer:
+    def __init__(self, path: str, cfg: ModelConfig):
+        from tokenizers import Tokenizer
+        self.tok = Tokenizer.from_file(path)
+        self.vocab_size = self.tok.get_vocab_size()
+        self.eos_token_ids = list(cfg.eos_token_ids)
+        self.bos_token_id = cfg.bos_token_id
+
+    def encode(self, text: str, add_special_tokens: bool = False) -> list[int]:
+        return self.tok.encode(text, add_special_tokens=add_special_tokens).ids
+
+    def decode(self, ids: list[int], skip_special_tokens: bool = True) -> str:
+        return self.tok.decode(list(ids), skip_special_tokens=skip_special_tokens)
+
+    def convert_special(self, name: str) -> Optional[int]:
+        return self.tok.token_to_id(name)
+
+
+def load_tokenizer(cfg: ModelConfig, tokenizer_path: Optional[str] = None):
+    path = tokenizer_path
+    if path is None:
+        d = find_local_model_dir(cfg.name)
+        if d is not None and os.path.exists(os.path.join(d, "tokenizer.json")):
+            path = os.path.join(d, "tokenizer.json")
+    if path and os.path.exists(path):
+        return HFTokenizer(path, cfg)
+    return ByteTokenizer(cfg)
+
+
+class IncrementalDetokenizer:
+    """Streams text deltas; holds back incomplete UTF-8 sequences (U+FFFD at the tail)."""
+
+    def __init__(self, tokenizer, prompt_tail: Optional[list] = None, skip_special_tokens: bool = True):
+        self.tok = tokenizer
+        self.ids: list[int] = []
+        self.emitted = ""
+        self.skip = skip_special_tokens
+
+    def add(self, token_id: int) -> str:
+        self.ids.append(int(token_id))
+        text = self.tok.decode(self.ids, skip_special_tokens=self.skip)
+        if text.endswith("�"):
+            return ""
+        delta = text[len(self.emitted):] if text.startswith(self.emitted) else text
+        self.emitted = text
+        return delta
+
+    def flush(self) -> str:
+        text = self.tok.decode(self.ids, skip_special_tokens=self.skip)
+        delta = text[len(self.emitted):] if text.startswith(self.emitted) else ""
+        self.emitted = text
+        return delta

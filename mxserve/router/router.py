@@ -1,0 +1,153 @@
+"""Worker discovery + request routing (replaces etcd discovery and the Dynamo router, SURVEY.md
+§2.2 X03/X06, §5.8).
+
+Workers POST /register to the frontend and heartbeat with load + KV events; a worker that misses
+its lease (ttl) is dropped.  Routing modes:
+  round_robin | random | kv  -- kv = KV-aware: for each candidate worker the router knows, from the
+  workers' block-stored/removed events, how many leading 16-token blocks of the prompt that worker
+  already caches (native KvIndexer, csrc/runtime/block_pool.cpp).  Cost per worker:
+      cost = overlap_weight * (prompt blocks still to prefill) + (active KV blocks after admission)
+  normalised by the worker's pool size; lowest cost wins (ties -> fewest running requests).
+"""
+from __future__ import annotations
+
+import itertools
+import random
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+from .. import _native
+
+
+@dataclass
+class WorkerInfo:
+    worker_id: str
+    url: str
+    model: str
+    role: str = "agg"  # agg | prefill | decode
+    block_size: int = 16
+    kv_total_blocks: int = 1
+    tp: int = 1
+    index: int = -1
+    last_seen: float = field(default_factory=time.monotonic)
+    num_running: int = 0
+    num_waiting: int = 0
+    kv_active_blocks: int = 0
+    inflight: int = 0  # requests routed by this frontend and not finished
+
+    def public(self) -> dict:
+        return {"worker_id": self.worker_id, "url": self.url, "model": self.model, "role": self.role,
+                "kv_total_blocks": self.kv_total_blocks, "tp": self.tp, "num_running": self.num_running,
+                "num_waiting": self.num_waiting, "kv_active_blocks": self.kv_active_blocks,
+                "inflight": self.inflight}
+
+
+class Registry:
+    def __init__(self, ttl: float = 10.0):
+        self.ttl = ttl
+        self._lock = threading.Lock()
+        self.workers: dict[str, WorkerInfo] = {}
+        self._free_idx = list(range(63, -1, -1))
+        self.indexer = _native.rt().KvIndexer()
+
+    def register(self, info: WorkerInfo) -> WorkerInfo:
+        with self._lock:
+            old = self.workers.get(info.worker_id)
+            if old is not None:
+                info.index = old.index
+            else:
+                if not self._free_idx:
+                    raise RuntimeError("too many workers (max 64 per frontend)")
+                info.index = self._free_idx.pop()
+                self.indexer.remove_worker(info.index)
+            info.last_seen = time.monotonic()
+            self.workers[info.worker_id] = info
+            return info
+
+    def heartbeat(self, worker_id: str, load: dict, stored=(), removed=()) -> bool:
+        with self._lock:
+            w = self.workers.get(worker_id)
+            if w is None:
+                return False
+            w.last_seen = time.monotonic()
+            w.num_running = int(load.get("num_running", w.num_running))
+            w.num_waiting = int(load.get("num_waiting", w.num_waiting))
+            tot = int(load.get("kv_total_blocks", w.kv_total_blocks) or 1)
+            w.kv_total_blocks = tot
+            w.kv_active_blocks = tot - int(load.get("kv_free_blocks", tot))
+            if stored:
+                self.indexer.apply_stored(w.index, list(stored))
+            if removed:
+                self.indexer.apply_removed(w.index, list(removed))
+            return True
+
+    def deregister(self, worker_id: str) -> None:
+        with self._lock:
+            w = self.workers.pop(worker_id, None)
+            if w is not None:
+                self.indexer.remove_worker(w.index)
+                self._free_idx.append(w.index)
+
+    def expire(self) -> list[str]:
+        now = time.monotonic()
+        dead = [wid for wid, w in self.workers.items() if now - w.last_seen > self.ttl]
+        for wid in dead:
+            self.deregister(wid)
+        return dead
+
+    def list(self, model: Optional[str] = None, role: Optional[str] = None) -> list[WorkerInfo]:
+        with self._lock:
+            return [w for w in self.workers.values()
+                    if (model is None or w.model == model) and (role is None or w.role == role)]
+
+    def models(self) -> list[str]:
+        with self._lock:
+            return sorted({w.model for w in self.workers.values()})
+
+
+class Router:
+    def __init__(self, registry: Registry, mode: str = "kv", overlap_weight: float = 1.0, seed: int = 0):
+        if mode not in ("round_robin", "random", "kv"):
+            raise ValueError(f"unknown router mode {mode}")
+        self.reg = registry
+        self.mode = mode
+        self.overlap_weight = overlap_weight
+        self._rr = itertools.count()
+        self._rng = random.Random(seed)
+        self._hash = _native.rt().block_hashes
+
+    def block_hashes(self, token_ids: list, block_size: int = 16) -> list:
+        return self._hash(token_ids, block_size, 0, 0)
+
+    def pick(self, candidates: list[WorkerInfo], token_ids: Optional[list] = None) -> tuple[WorkerInfo, int]:
+        """Returns (worker, overlap_blocks)."""
+        if not candidates:
+            raise LookupError("no workers available")
+        if self.mode == "round_robin" or len(candidates) == 1:
+            w = candidates[next(self._rr) % len(candidates)]
+            return w, self._overlap(w, token_ids) if self.mode == "kv" else 0
+        if self.mode == "random":
+            return self._rng.choice(candidates), 0
+        bs = candidates[0].block_size
+        hashes = self.block_hashes(token_ids or [], bs)
+        n_workers = max(w.index for w in candidates) + 1
+        overlaps = self.reg.indexer.find_matches(hashes, n_workers) if hashes else [0] * n_workers
+        nblocks = -(-len(token_ids or []) // bs)
+        best, best_key = None, None
+        for w in candidates:
+            ov = overlaps[w.index]
+            prefill_blocks = max(0, nblocks - ov)
+            active = w.kv_active_blocks + nblocks
+            cost = (self.overlap_weight * prefill_blocks + active) / max(1, w.kv_total_blocks)
+            key = (cost, w.num_running + w.num_waiting + w.inflight, self._rng.random())
+            if best_key is None or key < best_key:
+                best, best_key = (w, ov), key
+        return best
+
+    def _overlap(self, w: WorkerInfo, token_ids) -> int:
+        if not token_ids:
+            return 0
+        hashes = self.block_hashes(token_ids, w.block_size)
+        return self.reg.indexer.find_matches(hashes, w.index + 1)[w.index] if hashes else 0

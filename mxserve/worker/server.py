@@ -1,0 +1,289 @@
+"""Worker process: one engine (one GPU, or a TP group) behind an HTTP control/request plane.
+
+Replaces `python3 -m dynamo.{vllm,sglang,trtllm}` (examples/deploy/*/agg.yaml:29-35).  Endpoints
+  POST /generate   token-level request plane used by the frontend: NDJSON stream of token ids
+                   (`prefill_url` set on a decode worker = disaggregated: reserve blocks, ask the
+                   prefill worker to fill them over xGMI, then decode; falls back to local prefill)
+  POST /prefill    prefill worker: compute the prompt, push its KV blocks into the decode worker's
+                   pool, return the first token
+  POST /kv_write   host-staged KV backend (decode side)
+  GET  /health /live /metrics /stats
+Discovery: registers with the frontend (MXS_FRONTEND_URL) and heartbeats load + KV events (the
+router's prefix index) every second; the lease expires if the worker dies.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import os
+import socket
+import threading
+import time
+import uuid
+from typing import Optional
+
+import msgpack
+from fastapi import FastAPI, Request as HTTPRequest
+from fastapi.responses import JSONResponse, PlainTextResponse, Response, StreamingResponse
+
+from ..disagg.kv_transfer import KVTransferAgent
+from ..engine.engine import AsyncEngine, LLMEngine, StepOutput
+from ..engine.request import SamplingParams
+from ..frontend.metrics import WorkerMetrics
+from .args import WorkerArgs
+
+log = logging.getLogger("mxserve.worker")
+
+
+def _sampling(d: dict) -> SamplingParams:
+    return SamplingParams(max_tokens=int(d.get("max_tokens", 16)), temperature=float(d.get("temperature", 1.0)),
+                          top_p=float(d.get("top_p", 1.0)), top_k=int(d.get("top_k", 0)), seed=d.get("seed"),
+                          stop_token_ids=list(d.get("stop_token_ids", [])), ignore_eos=bool(d.get("ignore_eos")),
+                          min_tokens=int(d.get("min_tokens", 0)))
+
+
+def _line(o: StepOutput) -> bytes:
+    return (json.dumps({"t": o.token_id, "f": o.finished, "r": o.finish_reason, "p": o.num_prompt_tokens,
+                        "c": o.num_cached_tokens}) + "\n").encode()
+
+
+class Worker:
+    def __init__(self, wargs: WorkerArgs, engine: Optional[LLMEngine] = None):
+        self.wargs = wargs
+        self.args = wargs.engine
+        self.engine = engine or LLMEngine(self.args)
+        self.aeng = AsyncEngine(self.engine)
+        self.role = self.args.disagg_mode
+        self.model = self.args.name
+        self.metrics = WorkerMetrics()
+        self.agent = KVTransferAgent(self.engine.runner, self.args.kv_transfer_backend)
+        self.worker_id = wargs.worker_id or f"{self.role}-{socket.gethostname()}-{uuid.uuid4().hex[:6]}"
+        self.url: Optional[str] = None
+        self._events_lock = threading.Lock()
+        self._stored: list = []
+        self._removed: list = []
+        self.aeng.on_step = self._on_step
+        self.ready = True
+        self._http = None
+        self.app = self._build_app()
+
+    # ---------------------------------------------------------------- engine-thread hook
+    def _on_step(self, outs) -> None:
+        stored, removed = self.engine.kv.take_events()
+        if stored or removed:
+            with self._events_lock:
+                self._stored.extend(stored)
+                self._removed.extend(removed)
+        self.metrics.gen_tokens.labels(self.model).inc(len(outs))
+
+    def take_events(self):
+        with self._events_lock:
+            s, r = self._stored, self._removed
+            self._stored, self._removed = [], []
+        return s, r
+
+    # ---------------------------------------------------------------- http client
+    async def http(self):
+        if self._http is None:
+            import aiohttp
+            self._http = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=None, sock_connect=10))
+        return self._http
+
+    # ---------------------------------------------------------------- handlers
+    async def _generate_stream(self, body: dict):
+        rid = body.get("request_id") or uuid.uuid4().hex
+        toks = list(body["token_ids"])
+        sp = _sampling(body.get("sampling", {}))
+        purl = body.get("prefill_url")
+        if purl and self.role == "decode":
+            q = await self._remote_prefill(rid, toks, sp, purl)
+            if q is not None:
+                async for o in self.aeng.stream(rid, q):
+                    yield _line(o)
+                return
+        async for o in self.aeng.generate(toks, sp, rid):
+            yield _line(o)
+
+    async def _remote_prefill(self, rid: str, toks: list, sp: SamplingParams, purl: str):
+        """Decode side of the disaggregated protocol.  Returns the token queue, or None to fall
+        back to local prefill."""
+        req = await self.aeng.submit(self.engine.reserve_remote_prefill, toks, sp, rid)
+        if req is None:
+            return None
+        q = self.aeng.open_stream(rid)
+        skip = req.num_cached_tokens // self.args.block_size
+        nblk = -(-len(toks) // self.args.block_size)
+        target = self.agent.descriptor(self.url)
+        target["block_ids"] = list(req.block_ids[skip:nblk])
+        target["skip_blocks"] = skip
+        payload = {"request_id": rid, "token_ids": toks, "sampling": _sp_dict(sp), "kv_target": target}
+        try:
+            sess = await self.http()
+            async with sess.post(purl.rstrip("/") + "/prefill", json=payload) as r:
+                if r.status != 200:
+                    raise RuntimeError(f"prefill worker returned {r.status}: {await r.text()}")
+                res = await r.json()
+            out = await self.aeng.submit(self.engine.complete_remote_prefill, rid, int(res["first_token"]))
+            self.aeng.push(out)
+            if "transfer_s" in res:
+                self.metrics.kv_xfer_lat.labels(self.model).observe(float(res["transfer_s"]))
+                self.metrics.kv_xfer_bytes.labels(self.model).inc(len(target["block_ids"]) * self.agent.block_bytes)
+            return q
+        except Exception as e:  # noqa: BLE001 - SURVEY §5.3: fall back to local prefill
+            log.warning("remote prefill failed for %s (%r); prefilling locally", rid, e)
+            await self.aeng.submit(self.engine.abort, rid)
+            self.aeng._queues.pop(rid, None)
+            return None
+
+    async def _prefill(self, body: dict) -> dict:
+        """Prefill side: compute, push KV into the decode worker's pool, return the first token."""
+        rid = body["request_id"]
+        toks = list(body["token_ids"])
+        sp = _sampling(body.get("sampling", {}))
+        sp.max_tokens = 1
+        first = None
+        async for o in self.aeng.generate(toks, sp, rid, disagg_role="prefill_only"):
+            first = o.token_id
+        req = self.engine.requests.get(rid)
+        target = body["kv_target"]
+        skip = int(target.get("skip_blocks", 0))
+        dst = list(target["block_ids"])
+        src = list(req.block_ids[skip:skip + len(dst)]) if req is not None else []
+        xfer_s = 0.0
+        try:
+            if len(src) != len(dst):
+                raise RuntimeError(f"block count mismatch: {len(src)} local vs {len(dst)} remote")
+            if target["backend"] == "xgmi" and self.agent.backend == "xgmi":
+                xfer_s = await asyncio.get_running_loop().run_in_executor(None, self.agent.push_xgmi, src, dst,
+                                                                          target)
+            else:
+                t0 = time.perf_counter()
+                data = await asyncio.get_running_loop().run_in_executor(None, self.agent.read_blocks, src)
+                sess = await self.http()
+                async with sess.post(target["url"].rstrip("/") + "/kv_write",
+                                     data=msgpack.packb({"block_ids": dst, "data": data}),
+                                     headers={"content-type": "application/msgpack"}) as r:
+                    if r.status != 200:
+                        raise RuntimeError(f"kv_write failed: {r.status}")
+                xfer_s = time.perf_counter() - t0
+        finally:
+            self.aeng.submit_nowait(self.engine.release_prefill_blocks, rid)
+        return {"first_token": first, "num_cached_tokens": req.num_cached_tokens if req else 0,
+                "transfer_s": xfer_s, "blocks": len(dst)}
+
+    # ---------------------------------------------------------------- app
+    def _build_app(self) -> FastAPI:
+        app = FastAPI(title="mxserve worker")
+        w = self
+
+        @app.post("/generate")
+        async def generate(request: HTTPRequest):
+            body = await request.json()
+            return StreamingResponse(w._generate_stream(body), media_type="application/x-ndjson")
+
+        @app.post("/prefill")
+        async def prefill(request: HTTPRequest):
+            try:
+                return JSONResponse(await w._prefill(await request.json()))
+            except Exception as e:  # noqa: BLE001
+                log.exception("prefill failed")
+                return JSONResponse({"error": {"message": str(e)}}, status_code=500)
+
+        @app.post("/kv_write")
+        async def kv_write(request: HTTPRequest):
+            d = msgpack.unpackb(await request.body())
+            await asyncio.get_running_loop().run_in_executor(None, w.agent.write_blocks, d["block_ids"], d["data"])
+            return {"ok": True}
+
+        @app.get("/kv_pool")
+        async def kv_pool():
+            return w.agent.descriptor(w.url)
+
+        @app.get("/health")
+        async def health():
+            if not w.ready:
+                return JSONResponse({"status": "starting"}, status_code=503)
+            return {"status": "ready", "model": w.model, "role": w.role, "worker_id": w.worker_id}
+
+        @app.get("/live")
+        async def live():
+            return {"status": "alive"}
+
+        @app.get("/stats")
+        async def stats():
+            return w.aeng.last_stats
+
+        @app.get("/metrics")
+        async def metrics():
+            w.metrics.update(w.model, w.aeng.last_stats)
+            return Response(w.metrics.render(), media_type="text/plain; version=0.0.4")
+
+        @app.on_event("startup")
+        async def _startup():
+            if w.wargs.frontend_url:
+                asyncio.get_running_loop().create_task(w._heartbeat_loop())
+
+        @app.on_event("shutdown")
+        async def _shutdown():
+            if w._http is not None:
+                await w._http.close()
+
+        return app
+
+    # ---------------------------------------------------------------- discovery
+    def registration(self) -> dict:
+        st = self.aeng.last_stats
+        return {"worker_id": self.worker_id, "url": self.url, "model": self.model, "role": self.role,
+                "block_size": self.args.block_size, "kv_total_blocks": st.get("kv_total_blocks", 0),
+                "tp": self.args.tensor_parallel_size}
+
+    async def _heartbeat_loop(self) -> None:
+        base = self.wargs.frontend_url.rstrip("/")
+        registered = False
+        while True:
+            try:
+                sess = await self.http()
+                if not registered:
+                    async with sess.post(base + "/internal/register", json=self.registration()) as r:
+                        registered = r.status == 200
+                        if registered:
+                            log.info("registered with frontend %s as %s", base, self.worker_id)
+                else:
+                    stored, removed = self.take_events()
+                    body = {"worker_id": self.worker_id, "load": self.aeng.last_stats, "stored": stored,
+                            "removed": removed}
+                    async with sess.post(base + "/internal/heartbeat", json=body) as r:
+                        if r.status == 404:
+                            registered = False
+            except Exception as e:  # noqa: BLE001 - frontend not up yet / restarting
+                log.debug("heartbeat failed: %r", e)
+                registered = False
+            await asyncio.sleep(1.0)
+
+
+def _sp_dict(sp: SamplingParams) -> dict:
+    return {"max_tokens": sp.max_tokens, "temperature": sp.temperature, "top_p": sp.top_p, "top_k": sp.top_k,
+            "seed": sp.seed, "stop_token_ids": list(sp.stop_token_ids), "ignore_eos": sp.ignore_eos,
+            "min_tokens": sp.min_tokens}
+
+
+def advertise_url(wargs: WorkerArgs, port: int) -> str:
+    host = wargs.advertise_host
+    if not host:
+        host = "127.0.0.1" if wargs.host in ("127.0.0.1", "localhost") else socket.gethostbyname(socket.gethostname())
+    return f"http://{host}:{port}"
+
+
+def serve(wargs: WorkerArgs) -> None:
+    import uvicorn
+    logging.basicConfig(level=os.environ.get("MXS_LOG_LEVEL", "INFO"),
+                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    if wargs.engine.tensor_parallel_size > 1:
+        from .tp import start_tp_group
+        start_tp_group(wargs.engine)
+    w = Worker(wargs)
+    w.url = advertise_url(wargs, wargs.port)
+    log.info("worker %s (%s, %s) serving %s on %s", w.worker_id, w.role, w.agent.backend, w.model, w.url)
+    uvicorn.run(w.app, host=wargs.host, port=wargs.port, log_level="warning", access_log=False)
+    w.engine.shutdown()
