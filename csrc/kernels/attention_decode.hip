@@ -1,190 +1,302 @@
 // K12: paged attention, decode (one query token per sequence), GQA-packed, split-KV.
 //
-// Regime: HBM-bound on the KV read (BASELINE config 2: 128 seqs x 2k context x 32 KiB/token =
-// 8.6 GB per step vs 2.5 GB of weights), so the design goal is full-bandwidth streaming with the
-// arithmetic hidden under it:
-//   * grid (Hkv, B, P): one workgroup per (kv head, sequence, PART-token partition); the G = Hq/Hkv
-//     query heads that share a kv head are processed together, so each K/V byte is read once.
-//   * 4 waves per workgroup, each streaming 64-token chunks.  QK^T with the TOKEN on the lane: a
-//     lane loads its token's K row as D/8 x 16-byte vectors (K cache is token-major), q comes from
-//     LDS as broadcast 16-byte reads; P*V with the DIM on the lane: the V cache is dim-major
-//     ([D][16] per block), so a lane's 16 tokens of one dim are 2 x 16-byte vectors and a wave reads
-//     one block's V as one contiguous 2*D*16-byte sweep.
-//   * V loads are issued before the QK^T math so both streams are in flight together; the block
-//     table slice of the partition is staged in LDS once (no dependent global load per chunk).
-//   * online softmax in base 2 (q pre-scaled by scale*log2 e), per-lane partial row sums, one
-//     cross-wave combine through LDS; multi-partition results are merged by a second tiny kernel
-//     with the usual max/sum (LSE) rescaling.
+// Regime: HBM-bound on the KV read (bench shape: 256 seqs x 4k context x 32 KiB/token = 35 GB per
+// step against 2.5 GB of weights).  v1 of this kernel put one TOKEN per lane for QK^T, so every
+// 16-byte load instruction touched 64 different 128-byte K rows; it streamed at 2.2 TB/s.  v2 (this
+// file) reads every K and V block as contiguous 1 KiB wave-instructions:
+//   * grid (Hkv, B, P): one workgroup per (kv head, sequence, partition); the G = Hq/Hkv query heads
+//     of a kv head are processed together so each K/V byte is read once.  P is chosen on the host so
+//     the grid has >= ~2048 workgroups (8 per CU) and partitions are as long as possible (P = 1 at
+//     large batch: no merge kernel at all).
+//   * K (token-major [16][D] per block): lane l loads 16-byte vectors v = l + 64 i, i.e. token
+//     v / (D/8), dims 8 (l % (D/8)) .. +7.  Each lane keeps its 8 dims of q (all G heads) in
+//     registers, so QK^T is FMAs + an in-register DPP reduction over the D/8 lanes of a token
+//     (quad_perm xor1/xor2, row_half_mirror, row_mirror): no LDS, no ds_bpermute.
+//   * softmax: per-token max over heads via DPP row_ror + permlane16/32 swaps (VALU only); lane
+//     (token, j) exponentiates head j, so exps are not duplicated; p goes to LDS once.
+//   * V (dim-major [D][16] per block): lane l loads dim v / 2, tokens 8 (l % 2) .. +7 -> P*V is FMAs
+//     with p read back from LDS as broadcast 16-byte reads; the two token halves of a dim are
+//     merged once at the end.
+//   * 2 blocks (32 tokens) per wave iteration with the next iteration's K/V loads issued before the
+//     current iteration's math (software pipeline); block ids come from scalar loads.
 #include "common.h"
 
 namespace mxs {
 
-constexpr int kBS = 16;       // tokens per KV block (SGLang --page-size 16, sglang/agg.yaml:38-39)
-constexpr int kPart = 512;    // tokens per split-KV partition
+constexpr int kBS = 16;  // tokens per KV block (SGLang --page-size 16, sglang/agg.yaml:38-39)
 constexpr int kWaves = 4;
+constexpr int kBPI = 2;  // blocks per wave iteration
 constexpr float kLog2e = 1.4426950408889634f;
+
+// DPP helpers (gfx9 encodings): quad_perm xor1 = 0xB1, xor2 = 0x4E, row_half_mirror = 0x141,
+// row_mirror = 0x140, row_ror:8 = 0x128.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float perm16_max(float v) {
+  // the swap returns {row 2k in both rows, row 2k+1 in both rows}: combine the pair
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return fmaxf(__int_as_float(r[0]), __int_as_float(r[1]));
+}
+__device__ __forceinline__ float perm32_max(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return fmaxf(__int_as_float(r[0]), __int_as_float(r[1]));
+}
+__device__ __forceinline__ float perm16_sum(float v) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(r[0]) + __int_as_float(r[1]);
+}
+__device__ __forceinline__ float perm32_sum(float v) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(r[0]) + __int_as_float(r[1]);
+}
+
+// sum over the LPT = D/8 lanes that hold one token (all of them receive the total)
+template <int LPT>
+__device__ __forceinline__ float token_sum(float v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x141>(v);
+  if constexpr (LPT == 16) v += dpp<0x140>(v);
+  return v;
+}
+
+// max over all 64 lanes, in which each run of LPT lanes holds the same value
+template <int LPT>
+__device__ __forceinline__ float wave_max_tok(float v) {
+  if constexpr (LPT == 8) v = fmaxf(v, dpp<0x128>(v));
+  v = perm16_max(v);
+  return perm32_max(v);
+}
 
 template <int D, int G>
 __global__ void __launch_bounds__(256) paged_decode_kernel(
     bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml,
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kv, long block_stride,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens, int Hkv,
-    float scale) {
-  constexpr int DPL = D / 64;       // dims per lane in the P*V phase
-  constexpr int KV16 = D / 8;       // 16-byte vectors per K row
+    float scale, int part_len) {
+  constexpr int LPT = D / 8;        // lanes per token in the K layout
+  constexpr int TPI = 64 / LPT;     // tokens per K wave-instruction
+  constexpr int KV = D / 32;        // 16-byte vectors per lane per block (K and V alike)
+  constexpr int TOK = kBPI * kBS;   // tokens per wave iteration
+  constexpr int KT = kBPI * KV;     // K tokens handled per lane per iteration
+  static_assert(G <= LPT, "one lane per (token, head) for the exponentials");
+
   const int kvh = blockIdx.x, seq = blockIdx.y, part = blockIdx.z;
   const int P = gridDim.z;
   const int L = seq_lens[seq];
-  const int start = part * kPart;
+  const int start = part * part_len;
   if (start >= L) return;
-  const int end = min(start + kPart, L);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int end = min(start + part_len, L);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int Hq = Hkv * G;
+  const int j = lane % LPT;  // dim chunk of this lane in K; head it exponentiates
 
-  __shared__ __attribute__((aligned(16))) float q_s[G][D];
-  __shared__ __attribute__((aligned(16))) float p_s[kWaves][G][64];
-  __shared__ int bt_s[kPart / kBS];
+  __shared__ __attribute__((aligned(16))) float p_s[kWaves][G][TOK];
   __shared__ float red_m[kWaves][G], red_l[kWaves][G];
   __shared__ __attribute__((aligned(16))) float red_o[kWaves][G][D];
 
-  const float qscale = scale * kLog2e;
-  for (int i = threadIdx.x; i < G * D; i += blockDim.x) {
-    const int g = i / D, d = i % D;
-    q_s[g][d] = bf2f(q[(static_cast<size_t>(seq) * Hq + kvh * G + g) * D + d]) * qscale;
+  // q for this lane's 8 dims, all G heads, pre-scaled for exp2
+  float qr[G][8];
+  {
+    const float qs = scale * kLog2e;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint4 v = *reinterpret_cast<const uint4*>(q + (static_cast<size_t>(seq) * Hq + kvh * G + g) * D + 8 * j);
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        qr[g][2 * k] = bf2f_lo(w[k]) * qs;
+        qr[g][2 * k + 1] = bf2f_hi(w[k]) * qs;
+      }
+    }
   }
-  const int nblk = (end - start + kBS - 1) / kBS;
-  for (int i = threadIdx.x; i < nblk; i += blockDim.x)
-    bt_s[i] = block_tables[static_cast<size_t>(seq) * bt_stride + start / kBS + i];
-  __syncthreads();
+  const int* btp = block_tables + static_cast<size_t>(seq) * bt_stride;
+  const char* kbase = reinterpret_cast<const char*>(kv) + static_cast<size_t>(kvh) * kBS * D * 2;
+  const char* vbase = reinterpret_cast<const char*>(kv) + static_cast<size_t>(Hkv + kvh) * kBS * D * 2;
+  const long bstride_bytes = block_stride * 2;
 
-  const size_t k_head_off = static_cast<size_t>(kvh) * kBS * D;
-  const size_t v_head_off = static_cast<size_t>(Hkv + kvh) * kBS * D;
+  const int blk0 = start / kBS;
+  const int nblk = (end - 1) / kBS - blk0 + 1;          // blocks touched by this partition
+  const int niter = (nblk + kWaves * kBPI - 1) / (kWaves * kBPI);
 
-  float m[G], lsum[G], acc[G][DPL];
+  float m[G], acc[G][KV];
+  float lsum = 0.f;  // partial row sum of head j (lanes with j < G)
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     m[g] = -INFINITY;
-    lsum[g] = 0.f;
 #pragma unroll
-    for (int j = 0; j < DPL; ++j) acc[g][j] = 0.f;
+    for (int i = 0; i < KV; ++i) acc[g][i] = 0.f;
   }
 
-  for (int c0 = start + wid * 64; c0 < end; c0 += kWaves * 64) {
-    // ---- issue K loads (token on lane)
-    const int tok = c0 + lane;
-    const bool tvalid = tok < end;
-    uint4 kr[KV16];
-    if (tvalid) {
-      const int blk = bt_s[(tok - start) / kBS];
-      const uint4* kp = reinterpret_cast<const uint4*>(kv + blk * block_stride + k_head_off +
-                                                       static_cast<size_t>(tok % kBS) * D);
+  uint4 kr[kBPI][KV], vr[kBPI][KV];
+  auto load = [&](int it, uint4 (&kd)[kBPI][KV], uint4 (&vd)[kBPI][KV]) {
 #pragma unroll
-      for (int i = 0; i < KV16; ++i) kr[i] = kp[i];
-    }
-    // ---- issue V loads (dim on lane) for the chunk's up-to-4 blocks
-    const int nb = min(4, (end - c0 + kBS - 1) / kBS);
-    uint4 vr[4][DPL][2];
+    for (int b = 0; b < kBPI; ++b) {
+      const int bi = (it * kWaves + wid) * kBPI + b;
+      if (bi < nblk) {
+        const long off = static_cast<long>(btp[blk0 + bi]) * bstride_bytes;
+        const uint4* kp = reinterpret_cast<const uint4*>(kbase + off);
+        const uint4* vp = reinterpret_cast<const uint4*>(vbase + off);
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      if (b < nb) {
-        const int blk = bt_s[(c0 - start) / kBS + b];
-#pragma unroll
-        for (int j = 0; j < DPL; ++j) {
-          const uint4* vp = reinterpret_cast<const uint4*>(kv + blk * block_stride + v_head_off +
-                                                           static_cast<size_t>(lane + 64 * j) * kBS);
-          vr[b][j][0] = vp[0];
-          vr[b][j][1] = vp[1];
+        for (int i = 0; i < KV; ++i) {
+          kd[b][i] = kp[lane + 64 * i];
+          vd[b][i] = vp[lane + 64 * i];
         }
       }
     }
-    // ---- scores
-    float s[G];
+  };
+  if (niter > 0) load(0, kr, vr);
+
+  for (int it = 0; it < niter; ++it) {
+    uint4 kn[kBPI][KV], vn[kBPI][KV];
+    if (it + 1 < niter) load(it + 1, kn, vn);  // next iteration's loads in flight under this math
+    const int tok0 = (blk0 + (it * kWaves + wid) * kBPI) * kBS;  // first token of this iteration
+    if (tok0 < end) {
+      // ---- scores: lane holds KT tokens (b, i) -> token tok0 + 16 b + (lane + 64 i) / LPT
+      float s[KT][G];
 #pragma unroll
-    for (int g = 0; g < G; ++g) s[g] = 0.f;
-    if (tvalid) {
+      for (int b = 0; b < kBPI; ++b)
 #pragma unroll
-      for (int i = 0; i < KV16; ++i) {
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(&kr[i]);
-        float kf[8];
+        for (int i = 0; i < KV; ++i) {
+          const uint32_t* w = reinterpret_cast<const uint32_t*>(&kr[b][i]);
+          float kf[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          kf[2 * k] = bf2f_lo(w[k]);
-          kf[2 * k + 1] = bf2f_hi(w[k]);
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const float4_ qa = *reinterpret_cast<const float4_*>(&q_s[g][i * 8]);
-          const float4_ qb = *reinterpret_cast<const float4_*>(&q_s[g][i * 8 + 4]);
-          s[g] += qa[0] * kf[0] + qa[1] * kf[1] + qa[2] * kf[2] + qa[3] * kf[3] + qb[0] * kf[4] +
-                  qb[1] * kf[5] + qb[2] * kf[6] + qb[3] * kf[7];
-        }
-      }
-    }
-    // ---- online softmax (base 2)
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float sv = tvalid ? s[g] : -INFINITY;
-      const float mx = wave_max(sv);
-      const float mn = fmaxf(m[g], mx);
-      const float alpha = exp2f(m[g] - mn);
-      const float p = tvalid ? exp2f(sv - mn) : 0.f;
-      m[g] = mn;
-      lsum[g] = lsum[g] * alpha + p;
-#pragma unroll
-      for (int j = 0; j < DPL; ++j) acc[g][j] *= alpha;
-      p_s[wid][g][lane] = p;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- P * V
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      if (b < nb) {
-        const int tb = c0 + b * kBS;  // first token of this block
-        const bool full = tb + kBS <= end;
-#pragma unroll
-        for (int t4 = 0; t4 < 4; ++t4) {
-          float pv[G][4];
+          for (int k = 0; k < 4; ++k) {
+            kf[2 * k] = bf2f_lo(w[k]);
+            kf[2 * k + 1] = bf2f_hi(w[k]);
+          }
 #pragma unroll
           for (int g = 0; g < G; ++g) {
-            const float4_ pp = *reinterpret_cast<const float4_*>(&p_s[wid][g][b * kBS + t4 * 4]);
-            pv[g][0] = pp[0]; pv[g][1] = pp[1]; pv[g][2] = pp[2]; pv[g][3] = pp[3];
-          }
+            float a = 0.f;
 #pragma unroll
-          for (int j = 0; j < DPL; ++j) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(&vr[b][j][t4 >> 1]);
-            float vf[4] = {bf2f_lo(w[(t4 & 1) * 2]), bf2f_hi(w[(t4 & 1) * 2]), bf2f_lo(w[(t4 & 1) * 2 + 1]),
-                           bf2f_hi(w[(t4 & 1) * 2 + 1])};
+            for (int d = 0; d < 8; ++d) a += qr[g][d] * kf[d];
+            s[b * KV + i][g] = token_sum<LPT>(a);
+          }
+        }
+      // mask tokens past the end of the partition
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const int tok = tok0 + (t / KV) * kBS + (lane + 64 * (t % KV)) / LPT;
+        if (tok >= end) {
+#pragma unroll
+          for (int g = 0; g < G; ++g) s[t][g] = -INFINITY;
+        }
+      }
+      // ---- online softmax
+      float alpha[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float mx = s[0][g];
+#pragma unroll
+        for (int t = 1; t < KT; ++t) mx = fmaxf(mx, s[t][g]);
+        mx = wave_max_tok<LPT>(mx);
+        const float mn = fmaxf(m[g], mx);
+        alpha[g] = exp2f(m[g] - mn);
+        m[g] = mn;
+#pragma unroll
+        for (int i = 0; i < KV; ++i) acc[g][i] *= alpha[g];
+      }
+      if (j < G) {
+        float mj = m[0], aj = alpha[0];
+#pragma unroll
+        for (int g = 1; g < G; ++g)
+          if (j == g) {
+            mj = m[g];
+            aj = alpha[g];
+          }
+        float ps = 0.f;
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+          float sv = s[t][0];
+#pragma unroll
+          for (int g = 1; g < G; ++g)
+            if (j == g) sv = s[t][g];
+          const float p = exp2f(sv - mj);
+          ps += p;
+          p_s[wid][j][(t / KV) * kBS + (lane + 64 * (t % KV)) / LPT] = p;
+        }
+        // each token is held by one lane per head, so ps counts every token once
+        lsum = lsum * aj + ps;
+      }
+      // ---- P * V  (lane: dims lane/2 + 32 i, tokens 8 (lane % 2) .. +7 of each block)
+#pragma unroll
+      for (int b = 0; b < kBPI; ++b) {
+        const int tb = tok0 + b * kBS;
+        if (tb < end) {
+          float pv[G][8];
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const float4_ a = *reinterpret_cast<const float4_*>(&p_s[wid][g][b * kBS + 8 * (lane & 1)]);
+            const float4_ c = *reinterpret_cast<const float4_*>(&p_s[wid][g][b * kBS + 8 * (lane & 1) + 4]);
+            pv[g][0] = a[0]; pv[g][1] = a[1]; pv[g][2] = a[2]; pv[g][3] = a[3];
+            pv[g][4] = c[0]; pv[g][5] = c[1]; pv[g][6] = c[2]; pv[g][7] = c[3];
+          }
+          const bool full = tb + kBS <= end;
+#pragma unroll
+          for (int i = 0; i < KV; ++i) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(&vr[b][i]);
+            float vf[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              vf[2 * k] = bf2f_lo(w[k]);
+              vf[2 * k + 1] = bf2f_hi(w[k]);
+            }
             if (!full) {
 #pragma unroll
-              for (int u = 0; u < 4; ++u)
-                if (tb + t4 * 4 + u >= end) vf[u] = 0.f;  // never multiply uninitialised cache bytes
+              for (int u = 0; u < 8; ++u)
+                if (tb + 8 * (lane & 1) + u >= end) vf[u] = 0.f;  // never touch unwritten cache bytes
             }
 #pragma unroll
-            for (int g = 0; g < G; ++g)
-              acc[g][j] += pv[g][0] * vf[0] + pv[g][1] * vf[1] + pv[g][2] * vf[2] + pv[g][3] * vf[3];
+            for (int g = 0; g < G; ++g) {
+              float a = acc[g][i];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) a += pv[g][u] * vf[u];
+              acc[g][i] = a;
+            }
           }
         }
       }
     }
-    __builtin_amdgcn_wave_barrier();
+    if (it + 1 < niter) {
+#pragma unroll
+      for (int b = 0; b < kBPI; ++b)
+#pragma unroll
+        for (int i = 0; i < KV; ++i) {
+          kr[b][i] = kn[b][i];
+          vr[b][i] = vn[b][i];
+        }
+    }
   }
 
-  // ---- combine the 4 waves
+  // ---- per-wave totals: merge the two token halves of each dim, row sums per head
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int i = 0; i < KV; ++i) acc[g][i] += dpp<0xB1>(acc[g][i]);
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    const float l = wave_sum(lsum[g]);
+    float lg = (j == g) ? lsum : 0.f;
+    lg += dpp<0xB1>(lg);
+    lg += dpp<0x4E>(lg);
+    lg += dpp<0x141>(lg);
+    lg += dpp<0x140>(lg);
+    lg = perm16_sum(lg);
+    lg = perm32_sum(lg);
     if (lane == 0) {
       red_m[wid][g] = m[g];
-      red_l[wid][g] = l;
+      red_l[wid][g] = lg;
     }
+    if ((lane & 1) == 0) {
 #pragma unroll
-    for (int j = 0; j < DPL; ++j) red_o[wid][g][lane + 64 * j] = acc[g][j];
+      for (int i = 0; i < KV; ++i) red_o[wid][g][lane / 2 + 32 * i] = acc[g][i];
+    }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < G * D; i += blockDim.x) {
-    const int g = i / D, d = i % D;
+  for (int x = threadIdx.x; x < G * D; x += blockDim.x) {
+    const int g = x / D, d = x % D;
     float M = -INFINITY;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) M = fmaxf(M, red_m[w][g]);
@@ -214,9 +326,10 @@ template <int D>
 __global__ void __launch_bounds__(D) paged_decode_reduce_kernel(bf16_t* __restrict__ out,
                                                                 const float* __restrict__ tmp_out,
                                                                 const float* __restrict__ tmp_ml,
-                                                                const int* __restrict__ seq_lens, int Hq, int P) {
+                                                                const int* __restrict__ seq_lens, int Hq, int P,
+                                                                int part_len) {
   const int head = blockIdx.x, seq = blockIdx.y, d = threadIdx.x;
-  const int np = min(P, (seq_lens[seq] + kPart - 1) / kPart);
+  const int np = min(P, (seq_lens[seq] + part_len - 1) / part_len);
   const size_t base = (static_cast<size_t>(seq) * Hq + head) * P;
   float M = -INFINITY;
   for (int p = 0; p < np; ++p) M = fmaxf(M, tmp_ml[(base + p) * 2]);
@@ -229,21 +342,40 @@ __global__ void __launch_bounds__(D) paged_decode_reduce_kernel(bf16_t* __restri
   out[(static_cast<size_t>(seq) * Hq + head) * D + d] = f2bf(np > 0 ? O / Ls : 0.f);
 }
 
-int decode_num_partitions(int max_seq_len) { return (max_seq_len + kPart - 1) / kPart; }
+// Partition plan: enough workgroups to fill 256 CUs ~8 deep, partitions as long as possible, a
+// multiple of one full wave sweep (kWaves * kBPI blocks = 128 tokens).
+void decode_plan(int B, int Hkv, int max_seq_len, int* P, int* part_len) {
+  const int target = 2048;
+  const int sweep = kWaves * kBPI * kBS;
+  int p = (target + B * Hkv - 1) / (B * Hkv);
+  const int max_p = (max_seq_len + 255) / 256;  // never below 256 tokens per partition
+  if (p > max_p) p = max_p;
+  if (p < 1) p = 1;
+  int len = (max_seq_len + p - 1) / p;
+  len = ((len + sweep - 1) / sweep) * sweep;
+  *P = (max_seq_len + len - 1) / len;
+  *part_len = len;
+}
+
+int decode_num_partitions(int max_seq_len) {
+  int P, len;
+  decode_plan(1, 1, max_seq_len, &P, &len);
+  return P;
+}
 
 void launch_paged_decode(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, const bf16_t* kv,
                          long block_stride, const int* block_tables, int bt_stride, const int* seq_lens, int B,
-                         int Hq, int Hkv, int D, int P, float scale, hipStream_t s) {
+                         int Hq, int Hkv, int D, int P, int part_len, float scale, hipStream_t s) {
   if (B == 0) return;
   const int G = Hq / Hkv;
   dim3 grid(Hkv, B, P), blk(256);
 #define MXS_DEC(DD, GG)                                                                                    \
   if (D == DD && G == GG) {                                                                                \
     hipLaunchKernelGGL((paged_decode_kernel<DD, GG>), grid, blk, 0, s, out, tmp_out, tmp_ml, q, kv,        \
-                       block_stride, block_tables, bt_stride, seq_lens, Hkv, scale);                      \
+                       block_stride, block_tables, bt_stride, seq_lens, Hkv, scale, part_len);            \
     if (P > 1)                                                                                             \
       hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(Hq, B), dim3(DD), 0, s, out, tmp_out,     \
-                         tmp_ml, seq_lens, Hq, P);                                                         \
+                         tmp_ml, seq_lens, Hq, P, part_len);                                               \
     MXS_CHECK_LAUNCH();                                                                                    \
     return;                                                                                                \
   }

@@ -14,8 +14,9 @@ void launch_silu_mul(bf16_t*, const bf16_t*, int, int, hipStream_t);
 void launch_rope_and_cache(bf16_t*, const bf16_t*, const int64_t*, const float*, bf16_t*, long, const int64_t*,
                            const bf16_t*, const bf16_t*, int, int, int, int, int, float, hipStream_t);
 int decode_num_partitions(int);
+void decode_plan(int, int, int, int*, int*);
 void launch_paged_decode(bf16_t*, float*, float*, const bf16_t*, const bf16_t*, long, const int*, int, const int*,
-                         int, int, int, int, int, float, hipStream_t);
+                         int, int, int, int, int, int, float, hipStream_t);
 void launch_paged_prefill(bf16_t*, const bf16_t*, const bf16_t*, long, const int*, int, const int*, const int*,
                           int, int, int, int, int, float, hipStream_t);
 void launch_sample(int64_t*, const float*, int, int, long, const float*, const float*, const int*, const int64_t*,
@@ -94,7 +95,8 @@ void paged_attention_decode(at::Tensor out, at::Tensor q, at::Tensor kv, at::Ten
   TORCH_CHECK(block_tables.scalar_type() == at::kInt && seq_lens.scalar_type() == at::kInt, "int32 tables");
   TORCH_CHECK(block_tables.stride(1) == 1, "block_tables rows must be contiguous");
   TORCH_CHECK(Hq % Hkv == 0, "GQA ratio");
-  const int P = mxs::decode_num_partitions(static_cast<int>(std::max<int64_t>(max_seq_len, 1)));
+  int P = 1, part_len = 0;
+  mxs::decode_plan(B, Hkv, static_cast<int>(std::max<int64_t>(max_seq_len, 1)), &P, &part_len);
   at::Tensor tmp_out, tmp_ml;
   if (P > 1) {
     tmp_out = at::empty({B, Hq, P, D}, q.options().dtype(at::kFloat));
@@ -103,7 +105,7 @@ void paged_attention_decode(at::Tensor out, at::Tensor q, at::Tensor kv, at::Ten
   mxs::launch_paged_decode(bf(out), P > 1 ? tmp_out.data_ptr<float>() : nullptr,
                            P > 1 ? tmp_ml.data_ptr<float>() : nullptr, bf(q), bf(kv), kv.stride(0),
                            block_tables.data_ptr<int>(), block_tables.stride(0), seq_lens.data_ptr<int>(), B, Hq,
-                           Hkv, D, P, static_cast<float>(scale), stream());
+                           Hkv, D, P, part_len, static_cast<float>(scale), stream());
 }
 
 void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Tensor block_tables, at::Tensor qsl,
@@ -163,5 +165,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_topk_softmax", &moe_topk_softmax);
   m.def("moe_align", &moe_align);
   m.def("decode_num_partitions", &mxs::decode_num_partitions);
+  m.def("decode_plan", [](int B, int Hkv, int max_seq_len) {
+    int P = 1, len = 0;
+    mxs::decode_plan(B, Hkv, max_seq_len, &P, &len);
+    return std::make_pair(P, len);
+  });
   register_comm(m);
 }
