@@ -56,6 +56,8 @@ class KVCacheManager:
     def allocate_slots(self, req: Request, num_new_tokens: int) -> bool:
         """Ensure blocks for num_computed + num_new tokens.  False if the pool is exhausted."""
         need_tokens = req.num_computed_tokens + num_new_tokens
+        if need_tokens <= len(req.block_ids) * self.block_size:  # common decode case
+            return True
         need_blocks = -(-need_tokens // self.block_size) - len(req.block_ids)
         if need_blocks <= 0:
             return True

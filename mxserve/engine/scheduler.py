@@ -190,10 +190,12 @@ class Scheduler:
         Returns requests that produced a new token this step (finished ones included)."""
         emitted = []
         now = time.monotonic()
+        bs = self.kv.block_size
         for s in out.all():
             req = s.req
             req.num_computed_tokens += s.num_new_tokens
-            self.kv.cache_computed_blocks(req)
+            if req.num_computed_tokens // bs > req.num_registered_blocks:
+                self.kv.cache_computed_blocks(req)
             if not s.sample:
                 continue
             tok = sampled.get(req.request_id)

@@ -176,11 +176,10 @@ class TransformerLM:
                                             md.seq_lens, self.scale, md.max_query_len)
         else:
             o = torch.empty_like(q)
-            o[:nd] = ops.paged_attention_decode(q[:nd], kv_layer, md.block_tables[:nd], md.seq_lens[:nd],
-                                                self.scale, md.max_seq_len)
-            o[nd:] = ops.paged_attention_prefill(q[nd:], kv_layer, md.block_tables[nd:],
-                                                 md.prefill_query_start_loc, md.seq_lens[nd:], self.scale,
-                                                 md.max_query_len)
+            ops.paged_attention_decode(q[:nd], kv_layer, md.block_tables[:nd], md.seq_lens[:nd], self.scale,
+                                       md.max_seq_len, out=o[:nd])
+            ops.paged_attention_prefill(q[nd:], kv_layer, md.block_tables[nd:], md.prefill_query_start_loc,
+                                        md.seq_lens[nd:], self.scale, md.max_query_len, out=o[nd:])
         out = F.linear(o.reshape(o.shape[0], -1), w[p + "o"])
         return tp_all_reduce(out)
 

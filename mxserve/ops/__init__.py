@@ -92,10 +92,11 @@ def rope_and_cache(qkv: torch.Tensor, num_heads: int, num_kv_heads: int, head_di
 
 
 def paged_attention_decode(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,
-                           seq_lens: torch.Tensor, scale: float, max_seq_len: int) -> torch.Tensor:
-    """One query token per sequence.  q [B, Hq, D] -> [B, Hq, D]."""
+                           seq_lens: torch.Tensor, scale: float, max_seq_len: int,
+                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One query token per sequence.  q [B, Hq, D] -> [B, Hq, D] (written into `out` if given)."""
     if _gpu(q):
-        out = torch.empty_like(q)
+        out = torch.empty_like(q) if out is None else out
         ext().paged_attention_decode(out, q, kv_layer, block_tables, seq_lens, scale, max_seq_len)
         return out
     return ref.paged_attention_decode(q, kv_layer, block_tables, seq_lens, scale)
@@ -103,10 +104,10 @@ def paged_attention_decode(q: torch.Tensor, kv_layer: torch.Tensor, block_tables
 
 def paged_attention_prefill(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,
                             query_start_loc: torch.Tensor, seq_lens: torch.Tensor, scale: float,
-                            max_query_len: int) -> torch.Tensor:
+                            max_query_len: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Causal varlen attention of prefill chunks against the paged cache (prefix included)."""
     if _gpu(q):
-        out = torch.empty_like(q)
+        out = torch.empty_like(q) if out is None else out
         ext().paged_attention_prefill(out, q, kv_layer, block_tables, query_start_loc, seq_lens,
                                       scale, max_query_len)
         return out
