@@ -1,0 +1,4 @@
+from mxserve.worker.__main__ import main
+
+if __name__ == "__main__":
+    main(dialect="vllm")

@@ -123,6 +123,16 @@ class ModelRunner:
 
     # ------------------------------------------------------------------ memory
     def _determine_num_blocks(self) -> int:
+        n = self._local_num_blocks()
+        tp = get_tp()
+        if tp.tp_size > 1:  # every rank must manage the same block ids
+            import torch.distributed as dist
+            t = torch.tensor([n], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=tp.cpu_group or tp.group)
+            n = int(t.item())
+        return n
+
+    def _local_num_blocks(self) -> int:
         a, c, m = self.args, self.cfg, self.model
         per_block = c.num_layers * 2 * m.nkv * self.bs * c.head_dim * (2 if self.dtype != torch.float32 else 4)
         if a.num_gpu_blocks:

@@ -1,0 +1,44 @@
+"""`python -m mxserve.frontend` (also `python -m dynamo.frontend`): the OpenAI HTTP frontend.
+
+Workers register themselves (MXS_FRONTEND_URL); `--local-model` additionally runs an engine inside
+the frontend process (single-process serving, no request-plane hop)."""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="python -m dynamo.frontend")
+    ap.add_argument("--http-host", default=os.environ.get("DYN_HTTP_HOST", "0.0.0.0"))
+    ap.add_argument("--http-port", type=int, default=int(os.environ.get("DYN_HTTP_PORT", "8000")))
+    ap.add_argument("--router-mode", choices=["round_robin", "random", "kv"],
+                    default=os.environ.get("DYN_ROUTER_MODE", "kv"))
+    ap.add_argument("--lease-ttl", type=float, default=float(os.environ.get("MXS_LEASE_TTL", "10")))
+    ap.add_argument("--namespace", default=os.environ.get("DYN_NAMESPACE", "default"))
+    ap.add_argument("--local-model", default=os.environ.get("MXS_LOCAL_MODEL"),
+                    help="also serve this model from an in-process engine")
+    ap.add_argument("--local-device", default=os.environ.get("MXS_LOCAL_DEVICE", "auto"))
+    return ap
+
+
+def main(argv=None) -> None:
+    import uvicorn
+    from .app import Frontend
+    a = build_parser().parse_args(argv)
+    logging.basicConfig(level=os.environ.get("MXS_LOG_LEVEL", "INFO"),
+                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    fe = Frontend(router_mode=a.router_mode, ttl=a.lease_ttl, namespace=a.namespace)
+    if a.local_model:
+        from ..config import EngineArgs, env_overrides
+        from ..engine.engine import AsyncEngine, LLMEngine
+        kw = env_overrides()
+        kw.update(model=a.local_model, device=a.local_device)
+        eng = LLMEngine(EngineArgs(**kw))
+        fe.add_local_worker(AsyncEngine(eng), eng.args.name, eng.runner.num_blocks)
+    uvicorn.run(fe.app, host=a.http_host, port=a.http_port, log_level="warning", access_log=False)
+
+
+if __name__ == "__main__":
+    main()

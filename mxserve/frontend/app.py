@@ -15,6 +15,7 @@ and retries a request on another worker if its worker fails before the first tok
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import json
 import logging
 import time
@@ -235,25 +236,29 @@ class Frontend:
             m.osl.labels(model).observe(state["n"])
 
         async def events():
-            """Yields (text_delta, finish_reason|None)."""
+            """Yields (text_delta, finish_reason|None).  With stop strings, text that could still be
+            the start of a stop string is held back until it is disambiguated."""
             detok = IncrementalDetokenizer(tok)
-            text_so_far = ""
+            full, emitted = "", 0
+            hold = max((len(x) for x in stops if x), default=1) - 1
             async for ev in self.generate_tokens(model, prompt_ids, sampling, rid):
                 on_token()
-                delta = detok.add(ev.token_id) if not (ev.finished and ev.finish_reason == "stop"
-                                                      and ev.token_id in tok.eos_token_ids) else ""
-                reason = ev.finish_reason if ev.finished else None
+                eos_hit = ev.finished and ev.finish_reason == "stop" and ev.token_id in tok.eos_token_ids
+                full += "" if eos_hit else detok.add(ev.token_id)
                 if ev.finished:
-                    delta += detok.flush()
-                if stops and delta:
-                    cand = text_so_far + delta
-                    hit = min((cand.find(s) for s in stops if s and s in cand), default=-1)
-                    if hit >= 0:
-                        yield cand[len(text_so_far):hit], "stop"
+                    full += detok.flush()
+                reason = ("stop" if ev.finish_reason == "abort" else ev.finish_reason) if ev.finished else None
+                if stops:
+                    lo = max(0, emitted - hold)
+                    hits = [i for i in (full.find(x, lo) for x in stops if x) if i >= 0]
+                    if hits:
+                        yield full[emitted:min(hits)], "stop"
                         return
-                    text_so_far = cand
-                if reason == "abort":
-                    reason = "stop"
+                    end = len(full) if ev.finished else max(emitted, len(full) - hold)
+                else:
+                    end = len(full)
+                delta = full[emitted:end]
+                emitted = end
                 yield delta, reason
                 if ev.finished:
                     return
@@ -325,7 +330,7 @@ class Frontend:
 
     # ---------------------------------------------------------------- app
     def _build_app(self) -> FastAPI:
-        app = FastAPI(title="mxserve frontend")
+        app = FastAPI(title="mxserve frontend", lifespan=self._lifespan)
         fe = self
 
         @app.exception_handler(APIError)
@@ -408,18 +413,18 @@ class Frontend:
         async def workers():
             return {"workers": [w.public() for w in fe.registry.list()]}
 
-        @app.on_event("startup")
-        async def _startup():
-            async def reaper():
-                while True:
-                    await asyncio.sleep(1.0)
-                    for wid in fe.registry.expire():
-                        log.warning("worker %s lease expired", wid)
-            asyncio.get_running_loop().create_task(reaper())
-
-        @app.on_event("shutdown")
-        async def _shutdown():
-            if fe._http is not None:
-                await fe._http.close()
-
         return app
+
+    @contextlib.asynccontextmanager
+    async def _lifespan(self, app):
+        async def reaper():
+            while True:
+                await asyncio.sleep(1.0)
+                for wid in self.registry.expire():
+                    log.warning("worker %s lease expired", wid)
+        task = asyncio.get_running_loop().create_task(reaper())
+        yield
+        task.cancel()
+        if self._http is not None:
+            await self._http.close()
+            self._http = None

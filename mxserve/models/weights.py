@@ -92,6 +92,9 @@ def load_safetensors_state(cfg: ModelConfig, model_dir: Optional[str] = None) ->
 
 def load_weights(model, load_format: str = "auto", seed: int = 0) -> str:
     """Populate `model` (TransformerLM).  Returns the source used: 'safetensors' | 'random'."""
+    if load_format == "random_full":  # unsharded host init, then shard: identical model for any TP size
+        model.load_full_state(random_full_state(model.cfg, seed=seed, std=0.05, dtype=torch.float32))
+        return "random_full"
     if load_format in ("auto", "safetensors"):
         sd = load_safetensors_state(model.cfg)
         if sd is not None:

@@ -14,6 +14,7 @@ router's prefix index) every second; the lease expires if the worker dies (SURVE
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import json
 import logging
 import os
@@ -174,7 +175,7 @@ class Worker:
 
     # ---------------------------------------------------------------- app
     def _build_app(self) -> FastAPI:
-        app = FastAPI(title="mxserve worker")
+        app = FastAPI(title="mxserve worker", lifespan=self._lifespan)
         w = self
 
         @app.post("/generate")
@@ -219,17 +220,19 @@ class Worker:
             w.metrics.update(w.model, w.aeng.last_stats)
             return Response(w.metrics.render(), media_type="text/plain; version=0.0.4")
 
-        @app.on_event("startup")
-        async def _startup():
-            if w.wargs.frontend_url:
-                asyncio.get_running_loop().create_task(w._heartbeat_loop())
-
-        @app.on_event("shutdown")
-        async def _shutdown():
-            if w._http is not None:
-                await w._http.close()
-
         return app
+
+    @contextlib.asynccontextmanager
+    async def _lifespan(self, app):
+        task = None
+        if self.wargs.frontend_url:
+            task = asyncio.get_running_loop().create_task(self._heartbeat_loop())
+        yield
+        if task is not None:
+            task.cancel()
+        if self._http is not None:
+            await self._http.close()
+            self._http = None
 
     # ---------------------------------------------------------------- discovery
     def registration(self) -> dict:

@@ -1,0 +1,173 @@
+"""OpenAI frontend + workers over real HTTP on localhost, CPU engines (BASELINE config 1 plumbing,
+SURVEY.md §4.2 T4/T5): /v1/models, chat + completions (unary and SSE), error shapes, metrics
+names from the reference dashboard, aggregated and disaggregated (host-staged KV) serving."""
+import json
+
+import httpx
+import pytest
+
+from mxserve.config import EngineArgs
+from mxserve.frontend.app import Frontend
+from mxserve.worker.args import WorkerArgs
+from mxserve.worker.server import Worker
+from tests.serving_utils import Server, wait_for
+
+MODEL = "tiny-llama"
+
+
+def _worker(frontend_url, role="agg", seed=7):
+    ea = EngineArgs(model=MODEL, device="cpu", cpu_num_blocks=256, max_model_len=1024, max_num_batched_tokens=64,
+                    disagg_mode=role, load_format="random", seed=seed)
+    wa = WorkerArgs(engine=ea, host="127.0.0.1", frontend_url=frontend_url, worker_id=f"{role}-w")
+    w = Worker(wa)
+    srv = Server(w.app)
+    w.url = srv.url
+    return w, srv
+
+
+@pytest.fixture(scope="module")
+def agg_stack():
+    fe = Frontend(router_mode="kv", ttl=30)
+    fs = Server(fe.app).start()
+    w, ws = _worker(fs.url)
+    ws.start()
+    wait_for(lambda: len(fe.registry.list()) == 1)
+    yield fe, fs, w
+    ws.stop()
+    fs.stop()
+    w.aeng.shutdown()
+
+
+def test_models(agg_stack):
+    fe, fs, _ = agg_stack
+    d = httpx.get(fs.url + "/v1/models").json()
+    assert d["object"] == "list" and d["data"][0]["id"] == MODEL and d["data"][0]["object"] == "model"
+    assert httpx.get(fs.url + "/health").status_code == 200
+
+
+def test_chat_unary(agg_stack):
+    _, fs, _ = agg_stack
+    r = httpx.post(fs.url + "/v1/chat/completions", headers={"Authorization": "Bearer dummy"},
+                   json={"model": MODEL, "messages": [{"role": "user", "content": "hi there"}], "max_tokens": 7,
+                         "temperature": 0}, timeout=60)
+    assert r.status_code == 200
+    d = r.json()
+    assert d["object"] == "chat.completion"
+    assert isinstance(d["choices"][0]["message"]["content"], str)
+    assert d["usage"]["completion_tokens"] <= 7 and d["usage"]["prompt_tokens"] > 0
+    assert d["choices"][0]["finish_reason"] in ("stop", "length")
+
+
+def test_chat_stream_matches_unary(agg_stack):
+    _, fs, _ = agg_stack
+    body = {"model": MODEL, "messages": [{"role": "system", "content": "be brief"},
+                                         {"role": "user", "content": "count"}], "max_tokens": 9, "temperature": 0,
+            "ignore_eos": True}
+    unary = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=60).json()
+    text, reasons, saw_done = "", [], False
+    with httpx.stream("POST", fs.url + "/v1/chat/completions", json=dict(body, stream=True,
+                                                                        stream_options={"include_usage": True}),
+                      timeout=60) as r:
+        assert r.headers["content-type"].startswith("text/event-stream")
+        for line in r.iter_lines():
+            if not line.startswith("data: "):
+                continue
+            payload = line[6:]
+            if payload == "[DONE]":
+                saw_done = True
+                break
+            ch = json.loads(payload)
+            if ch["choices"]:
+                text += ch["choices"][0]["delta"].get("content") or ""
+                if ch["choices"][0]["finish_reason"]:
+                    reasons.append(ch["choices"][0]["finish_reason"])
+            else:
+                assert ch["usage"]["completion_tokens"] == 9
+    assert saw_done and reasons == ["length"]
+    assert text == unary["choices"][0]["message"]["content"]
+
+
+def test_completions_and_prefix_routing(agg_stack):
+    fe, fs, w = agg_stack
+    prompt = "the same long prefix " * 8
+    for _ in range(2):
+        r = httpx.post(fs.url + "/v1/completions", json={"model": MODEL, "prompt": prompt, "max_tokens": 3,
+                                                         "temperature": 0}, timeout=60)
+        assert r.status_code == 200 and r.json()["object"] == "text_completion"
+    # the worker published its cached blocks; the router's index now holds them
+    wait_for(lambda: fe.registry.indexer.size() > 0, timeout=10)
+
+
+def test_errors(agg_stack):
+    _, fs, _ = agg_stack
+    r = httpx.post(fs.url + "/v1/chat/completions", json={"model": "nope", "messages": [{"role": "user",
+                                                                                       "content": "x"}]})
+    assert r.status_code == 404 and "message" in r.json()["error"]
+    r = httpx.post(fs.url + "/v1/chat/completions", json={"model": MODEL})
+    assert r.status_code == 400 and "message" in r.json()["error"]
+    r = httpx.post(fs.url + "/v1/chat/completions", content=b"{not json")
+    assert r.status_code == 400
+
+
+def test_metrics_names(agg_stack):
+    _, fs, _ = agg_stack
+    httpx.post(fs.url + "/v1/chat/completions", json={"model": MODEL, "messages": [{"role": "user", "content": "m"}],
+                                                      "max_tokens": 2}, timeout=60)
+    text = httpx.get(fs.url + "/metrics").text
+    for name in ("dynamo_frontend_requests_total", "dynamo_frontend_time_to_first_token_seconds_sum",
+                 "dynamo_frontend_time_to_first_token_seconds_count", "dynamo_frontend_inter_token_latency_seconds_sum",
+                 "dynamo_frontend_request_duration_seconds_sum", "dynamo_frontend_input_sequence_tokens_sum",
+                 "dynamo_frontend_output_sequence_tokens_sum", "dynamo_frontend_inflight_requests"):
+        assert name in text, name
+    assert 'request_type="unary"' in text and 'status="success"' in text
+
+
+def test_stop_strings(agg_stack):
+    _, fs, _ = agg_stack
+    body = {"model": MODEL, "messages": [{"role": "user", "content": "x"}], "max_tokens": 30, "temperature": 0,
+            "ignore_eos": True}
+    full = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=60).json()["choices"][0]["message"]["content"]
+    if len(full) < 4:
+        pytest.skip("generated text too short to cut")
+    stop = full[2:4]
+    cut = httpx.post(fs.url + "/v1/chat/completions", json=dict(body, stop=[stop]), timeout=60).json()
+    assert cut["choices"][0]["message"]["content"] == full[:full.find(stop)]
+    assert cut["choices"][0]["finish_reason"] == "stop"
+
+
+def test_disaggregated_matches_aggregated():
+    """Prefill worker + decode worker (host-staged KV transfer) give the agg result token for token."""
+    fe = Frontend(router_mode="round_robin", ttl=30)
+    fs = Server(fe.app).start()
+    pw, ps = _worker(fs.url, role="prefill")
+    dw, ds = _worker(fs.url, role="decode")
+    ps.start()
+    ds.start()
+    try:
+        wait_for(lambda: len(fe.registry.list()) == 2)
+        body = {"model": MODEL, "messages": [{"role": "user", "content": "disaggregate me " * 5}], "max_tokens": 8,
+                "temperature": 0, "ignore_eos": True}
+        r = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=120)
+        assert r.status_code == 200, r.text
+        disagg = r.json()["choices"][0]["message"]["content"]
+        assert pw.agent.backend == "host"
+        # the decode worker really received the prompt's KV from the prefill worker
+        assert dw.metrics.kv_xfer_bytes.labels(MODEL)._value.get() > 0
+        # aggregated reference with the same weights (same seed)
+        agg, ags = _worker(None, role="agg")
+        ags.start()
+        fe2 = Frontend(router_mode="round_robin")
+        fe2.registry.register(__import__("mxserve.router.router", fromlist=["WorkerInfo"]).WorkerInfo(
+            worker_id="a", url=ags.url, model=MODEL))
+        fs2 = Server(fe2.app).start()
+        ref = httpx.post(fs2.url + "/v1/chat/completions", json=body, timeout=120).json()
+        assert disagg == ref["choices"][0]["message"]["content"]
+        fs2.stop()
+        ags.stop()
+        agg.aeng.shutdown()
+    finally:
+        ps.stop()
+        ds.stop()
+        fs.stop()
+        pw.aeng.shutdown()
+        dw.aeng.shutdown()
