@@ -1,0 +1,172 @@
+"""Load generator for an OpenAI-compatible endpoint.
+
+    python3 -m benchmarks.utils.benchmark --benchmark-name NAME --endpoint-url URL --model M \
+        --output-dir DIR [--isl 4000 --osl 500] [--concurrency 1,2,4,...] [--request-rate 8,16,...]
+
+For each concurrency level (closed loop) and each request rate (open loop, Poisson arrivals) it
+streams /v1/completions requests with synthetic prompts of ~ISL tokens and exactly OSL output
+tokens (ignore_eos), and records TTFT (first streamed token), ITL (gaps between streamed chunks),
+end-to-end latency and throughput.  One JSON file per point under DIR/NAME/, plus summary.json.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import random
+import time
+
+import aiohttp
+import numpy as np
+
+WORDS = ("alpha bravo charlie delta echo foxtrot golf hotel india juliet kilo lima mike november oscar papa "
+         "quebec romeo sierra tango uniform victor whiskey xray yankee zulu").split()
+
+
+def synth_prompt(rng: random.Random, isl: int, token_ids: bool, vocab: int):
+    if token_ids:
+        return [rng.randrange(100, vocab - 100) for _ in range(isl)]
+    # ~1 token per word for BPE tokenizers; byte tokenizers see more
+    return " ".join(rng.choice(WORDS) for _ in range(isl))
+
+
+async def one_request(sess, url: str, model: str, prompt, osl: int, t_sched: float) -> dict:
+    body = {"model": model, "prompt": prompt, "max_tokens": osl, "ignore_eos": True, "stream": True,
+            "temperature": 1.0, "stream_options": {"include_usage": True}}
+    t0 = max(time.perf_counter(), t_sched)
+    first, last, gaps, n_chunks, usage, err = None, None, [], 0, None, None
+    try:
+        async with sess.post(url, json=body) as r:
+            if r.status != 200:
+                return {"ok": False, "error": f"HTTP {r.status}: {(await r.text())[:200]}"}
+            async for raw in r.content:
+                line = raw.decode().strip()
+                if not line.startswith("data: "):
+                    continue
+                data = line[6:]
+                if data == "[DONE]":
+                    break
+                ch = json.loads(data)
+                if "error" in ch:
+                    err = ch["error"].get("message")
+                    break
+                if ch.get("usage"):
+                    usage = ch["usage"]
+                if ch.get("choices"):
+                    now = time.perf_counter()
+                    if first is None:
+                        first = now
+                    else:
+                        gaps.append(now - last)
+                    last = now
+                    n_chunks += 1
+    except (aiohttp.ClientError, asyncio.TimeoutError) as e:
+        return {"ok": False, "error": repr(e)}
+    if err or first is None:
+        return {"ok": False, "error": err or "no tokens"}
+    out_tokens = usage["completion_tokens"] if usage else n_chunks
+    return {"ok": True, "ttft": first - t_sched, "e2e": last - t_sched, "itl": gaps, "out": out_tokens,
+            "in": usage["prompt_tokens"] if usage else None, "start": t0}
+
+
+def summarize(results: list, wall: float, label: dict) -> dict:
+    ok = [r for r in results if r["ok"]]
+    def pct(xs, q):
+        return float(np.percentile(xs, q)) * 1e3 if xs else None
+    ttft = [r["ttft"] for r in ok]
+    itl = [g for r in ok for g in r["itl"]]
+    e2e = [r["e2e"] for r in ok]
+    out = sum(r["out"] for r in ok)
+    return dict(label, requests=len(results), failed=len(results) - len(ok), duration_s=wall,
+                output_tok_per_s=out / wall if wall > 0 else 0.0, requests_per_s=len(ok) / wall if wall > 0 else 0.0,
+                ttft_ms_p50=pct(ttft, 50), ttft_ms_p90=pct(ttft, 90), ttft_ms_p99=pct(ttft, 99),
+                itl_ms_p50=pct(itl, 50), itl_ms_p90=pct(itl, 90), itl_ms_p99=pct(itl, 99),
+                e2e_ms_p50=pct(e2e, 50), errors=[r["error"] for r in results if not r["ok"]][:5])
+
+
+async def run_concurrency(url, model, conc, n, isl, osl, token_ids, vocab, seed):
+    rng = random.Random(seed)
+    prompts = [synth_prompt(rng, isl, token_ids, vocab) for _ in range(n)]
+    results = []
+    it = iter(prompts)
+    conn = aiohttp.TCPConnector(limit=0)
+    async with aiohttp.ClientSession(connector=conn, timeout=aiohttp.ClientTimeout(total=None)) as sess:
+        t0 = time.perf_counter()
+
+        async def worker():
+            for p in it:
+                results.append(await one_request(sess, url, model, p, osl, time.perf_counter()))
+        await asyncio.gather(*(worker() for _ in range(conc)))
+        wall = time.perf_counter() - t0
+    return summarize(results, wall, {"mode": "concurrency", "concurrency": conc, "isl": isl, "osl": osl})
+
+
+async def run_rate(url, model, rate, n, isl, osl, token_ids, vocab, seed):
+    rng = random.Random(seed)
+    prompts = [synth_prompt(rng, isl, token_ids, vocab) for _ in range(n)]
+    gaps = np.random.default_rng(seed).exponential(1.0 / rate, size=n)
+    conn = aiohttp.TCPConnector(limit=0)
+    async with aiohttp.ClientSession(connector=conn, timeout=aiohttp.ClientTimeout(total=None)) as sess:
+        t0 = time.perf_counter()
+        tasks = []
+        t = t0
+        for p, g in zip(prompts, gaps):
+            t += g
+            await asyncio.sleep(max(0.0, t - time.perf_counter()))
+            tasks.append(asyncio.create_task(one_request(sess, url, model, p, osl, t)))
+        results = await asyncio.gather(*tasks)
+        wall = time.perf_counter() - t0
+    return summarize(list(results), wall, {"mode": "request_rate", "request_rate": rate, "isl": isl, "osl": osl})
+
+
+def _endpoint(url: str) -> str:
+    u = url.rstrip("/")
+    if u.endswith("/v1/completions"):
+        return u
+    if u.endswith("/v1/chat/completions"):
+        return u[: -len("/chat/completions")] + "/completions"
+    if u.endswith("/v1"):
+        return u + "/completions"
+    return u + "/v1/completions"
+
+
+def main(argv=None) -> None:
+    ap = argparse.ArgumentParser(prog="python3 -m benchmarks.utils.benchmark")
+    ap.add_argument("--benchmark-name", required=True)
+    ap.add_argument("--endpoint-url", required=True)
+    ap.add_argument("--model", required=True)
+    ap.add_argument("--output-dir", required=True)
+    ap.add_argument("--isl", type=int, default=int(os.environ.get("BENCH_ISL", "4000")))
+    ap.add_argument("--osl", type=int, default=int(os.environ.get("BENCH_OSL", "500")))
+    ap.add_argument("--concurrency", default=os.environ.get("BENCH_CONCURRENCY", "1,2,4,8,16,32,64"))
+    ap.add_argument("--request-rate", default=os.environ.get("BENCH_REQUEST_RATE", ""))
+    ap.add_argument("--num-requests", type=int, default=0, help="per point (default max(4*conc, 16))")
+    ap.add_argument("--token-ids", action="store_true", help="send prompts as token-id lists (exact ISL)")
+    ap.add_argument("--vocab", type=int, default=32000)
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args(argv)
+    url = _endpoint(a.endpoint_url)
+    out_dir = os.path.join(a.output_dir, a.benchmark_name)
+    os.makedirs(out_dir, exist_ok=True)
+    points = []
+    for c in [int(x) for x in a.concurrency.split(",") if x.strip()]:
+        n = a.num_requests or max(4 * c, 16)
+        s = asyncio.run(run_concurrency(url, a.model, c, n, a.isl, a.osl, a.token_ids, a.vocab, a.seed + c))
+        points.append(s)
+        with open(os.path.join(out_dir, f"concurrency_{c}.json"), "w") as f:
+            json.dump(s, f, indent=2)
+        print(json.dumps({k: v for k, v in s.items() if k != "errors"}), flush=True)
+    for r in [float(x) for x in a.request_rate.split(",") if x.strip()]:
+        n = a.num_requests or max(int(r * 30), 16)
+        s = asyncio.run(run_rate(url, a.model, r, n, a.isl, a.osl, a.token_ids, a.vocab, a.seed + int(r * 100)))
+        points.append(s)
+        with open(os.path.join(out_dir, f"rate_{r:g}.json"), "w") as f:
+            json.dump(s, f, indent=2)
+        print(json.dumps({k: v for k, v in s.items() if k != "errors"}), flush=True)
+    with open(os.path.join(out_dir, "summary.json"), "w") as f:
+        json.dump({"benchmark": a.benchmark_name, "endpoint": url, "model": a.model, "points": points}, f, indent=2)
+
+
+if __name__ == "__main__":
+    main()

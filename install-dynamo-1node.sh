@@ -1,0 +1,76 @@
+#!/usr/bin/env bash
+# Install the mxserve serving platform on a single-node cluster with MI355X GPUs:
+#   1) default StorageClass (local-path) for model-cache PVCs
+#   2) DGD / DGDR / DCD CRDs (group nvidia.com/v1alpha1, so the example manifests apply unchanged)
+#   3) the mxserve operator (replaces the Dynamo operator + etcd + NATS: workers register with the
+#      frontend directly, no external state store)
+#   4) AMD GPU Operator (or the ROCm k8s-device-plugin DaemonSet) and wait for amd.com/gpu allocatable
+set -euo pipefail
+HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
+
+NAMESPACE="${NAMESPACE:-dynamo-system}"
+RELEASE_VERSION="${RELEASE_VERSION:-0.1.0}"                       # mxserve image tag
+MXS_IMAGE="${MXS_IMAGE:-mxserve/mxserve-rocm:${RELEASE_VERSION}}"
+NAMESPACE_RESTRICTED_OPERATOR="${NAMESPACE_RESTRICTED_OPERATOR:-false}"
+PROMETHEUS_ENDPOINT="${PROMETHEUS_ENDPOINT:-http://prometheus-kube-prometheus-prometheus.monitoring.svc.cluster.local:9090}"
+LOCAL_PATH_MANIFEST_URL="${LOCAL_PATH_MANIFEST_URL:-https://raw.githubusercontent.com/rancher/local-path-provisioner/master/deploy/local-path-storage.yaml}"
+GPU_RESOURCE="${GPU_RESOURCE:-amd.com/gpu}"
+GPU_OPERATOR_NS="${GPU_OPERATOR_NS:-kube-amd-gpu}"
+GPU_OPERATOR_RELEASE="${GPU_OPERATOR_RELEASE:-amd-gpu-operator}"
+AMD_HELM_REPO_NAME="${AMD_HELM_REPO_NAME:-rocm}"
+AMD_HELM_REPO_URL="${AMD_HELM_REPO_URL:-https://rocm.github.io/gpu-operator}"
+GPU_OPERATOR_MODE="${GPU_OPERATOR_MODE:-operator}"                 # operator | device-plugin | skip
+ROCM_DEVICE_PLUGIN_URL="${ROCM_DEVICE_PLUGIN_URL:-https://raw.githubusercontent.com/ROCm/k8s-device-plugin/master/k8s-ds-amdgpu-dp.yaml}"
+GPU_OPERATOR_HELM_TIMEOUT="${GPU_OPERATOR_HELM_TIMEOUT:-15m}"
+GPU_ALLOCATABLE_WAIT_ATTEMPTS="${GPU_ALLOCATABLE_WAIT_ATTEMPTS:-120}"
+GPU_ALLOCATABLE_WAIT_INTERVAL="${GPU_ALLOCATABLE_WAIT_INTERVAL:-5}"
+
+say() { printf '\n[install] %s\n' "$*"; }
+die() { printf 'ERROR: %s\n' "$*" >&2; exit 1; }
+for c in kubectl; do command -v "$c" >/dev/null || die "missing $c"; done
+kubectl version >/dev/null 2>&1 || die "cannot reach the cluster (KUBECONFIG?)"
+
+say "storage: default StorageClass"
+if ! kubectl get storageclass -o jsonpath='{range .items[*]}{.metadata.annotations.storageclass\.kubernetes\.io/is-default-class}{"\n"}{end}' | grep -q true; then
+  kubectl apply -f "$LOCAL_PATH_MANIFEST_URL"
+  kubectl patch storageclass local-path -p '{"metadata":{"annotations":{"storageclass.kubernetes.io/is-default-class":"true"}}}'
+fi
+
+say "CRDs"
+kubectl apply -f "$HERE/deploy/crds/"
+
+say "operator ${MXS_IMAGE} in ${NAMESPACE}"
+kubectl create namespace "$NAMESPACE" --dry-run=client -o yaml | kubectl apply -f -
+watch_args='[]'
+[[ "$NAMESPACE_RESTRICTED_OPERATOR" == "true" ]] && watch_args="[\"--namespace\", \"${NAMESPACE}\"]"
+sed -e "s#IMAGE_PLACEHOLDER#${MXS_IMAGE}#g" -e "s#NAMESPACE_PLACEHOLDER#${NAMESPACE}#g" \
+    -e "s#WATCH_ARGS_PLACEHOLDER#${watch_args}#" -e "s#GPU_RESOURCE_PLACEHOLDER#${GPU_RESOURCE}#" \
+    "$HERE/deploy/operator/operator.yaml" | kubectl apply -n "$NAMESPACE" -f -
+kubectl -n "$NAMESPACE" rollout status deploy/mxserve-operator --timeout=600s
+say "metrics: workers expose /metrics via PodMonitors; Prometheus at ${PROMETHEUS_ENDPOINT}"
+
+case "$GPU_OPERATOR_MODE" in
+  operator)
+    command -v helm >/dev/null || die "helm is required for GPU_OPERATOR_MODE=operator"
+    say "AMD GPU Operator (${GPU_OPERATOR_RELEASE} in ${GPU_OPERATOR_NS})"
+    helm repo add "$AMD_HELM_REPO_NAME" "$AMD_HELM_REPO_URL" >/dev/null 2>&1 || true
+    helm repo update >/dev/null
+    helm upgrade --install "$GPU_OPERATOR_RELEASE" "$AMD_HELM_REPO_NAME/gpu-operator-charts" \
+      -n "$GPU_OPERATOR_NS" --create-namespace --wait --timeout "$GPU_OPERATOR_HELM_TIMEOUT"
+    ;;
+  device-plugin)
+    say "ROCm k8s-device-plugin DaemonSet"
+    kubectl apply -f "$ROCM_DEVICE_PLUGIN_URL"
+    ;;
+  skip) say "GPU operator installation skipped" ;;
+  *) die "GPU_OPERATOR_MODE must be operator|device-plugin|skip" ;;
+esac
+
+say "waiting for ${GPU_RESOURCE} to become allocatable"
+for ((i = 1; i <= GPU_ALLOCATABLE_WAIT_ATTEMPTS; i++)); do
+  n="$(kubectl get nodes -o jsonpath="{range .items[*]}{.status.allocatable.${GPU_RESOURCE//./\\.}}{\"\\n\"}{end}" \
+       | awk '{s += $1} END {print s + 0}')"
+  if [[ "$n" -gt 0 ]]; then say "${n} x ${GPU_RESOURCE} allocatable"; exit 0; fi
+  sleep "$GPU_ALLOCATABLE_WAIT_INTERVAL"
+done
+die "no ${GPU_RESOURCE} allocatable after $((GPU_ALLOCATABLE_WAIT_ATTEMPTS * GPU_ALLOCATABLE_WAIT_INTERVAL))s"

@@ -95,7 +95,8 @@ class Frontend:
     def add_local_worker(self, aeng, model: str, kv_total_blocks: int) -> None:
         self.local[model] = LocalWorker(aeng, model)
         self.registry.register(WorkerInfo(worker_id=f"local-{model}", url="local://", model=model,
-                                          kv_total_blocks=kv_total_blocks))
+                                          kv_total_blocks=kv_total_blocks,
+                                          max_model_len=aeng.engine.args.max_model_len))
         self.registry.workers[f"local-{model}"].last_seen = float("inf")
 
     def resolve_model(self, name: Optional[str]) -> str:
@@ -179,13 +180,20 @@ class Frontend:
         raise APIError(503, "all workers failed", "service_unavailable")
 
     # ---------------------------------------------------------------- OpenAI layer
+    def context_limit(self, model: str) -> int:
+        lens = [w.max_model_len for w in self.registry.list(model) if w.max_model_len > 0]
+        return min(lens) if lens else self.model_cfg(model).max_position_embeddings
+
     def _sampling(self, body: dict, model: str, n_prompt: int) -> dict:
-        cfg = self.model_cfg(model)
-        limit = cfg.max_position_embeddings
+        limit = self.context_limit(model)
+        if n_prompt >= limit:
+            raise APIError(400, f"This model's maximum context length is {limit} tokens; the prompt has "
+                                f"{n_prompt} tokens.")
         mt = body.get("max_completion_tokens", body.get("max_tokens"))
         mt = int(mt) if mt is not None else max(1, min(4096, limit - n_prompt))
         if mt <= 0:
             raise APIError(400, "max_tokens must be positive")
+        mt = min(mt, limit - n_prompt)
         t = body.get("temperature")
         tp = body.get("top_p")
         if t is not None and not (0.0 <= float(t) <= 2.0):
@@ -398,7 +406,8 @@ class Frontend:
             d = await request.json()
             info = WorkerInfo(worker_id=d["worker_id"], url=d["url"], model=d["model"], role=d.get("role", "agg"),
                               block_size=int(d.get("block_size", 16)),
-                              kv_total_blocks=int(d.get("kv_total_blocks", 1) or 1), tp=int(d.get("tp", 1)))
+                              kv_total_blocks=int(d.get("kv_total_blocks", 1) or 1), tp=int(d.get("tp", 1)),
+                              max_model_len=int(d.get("max_model_len", 0) or 0))
             fe.registry.register(info)
             log.info("registered worker %s (%s) for %s at %s", info.worker_id, info.role, info.model, info.url)
             return {"ok": True, "index": info.index}

@@ -1,0 +1,170 @@
+"""Implementation of `deploy-incluster.sh` (reference deploy-incluster.sh:14-659, same flags, env
+and printed quick test) over the REST client instead of kubectl text parsing:
+
+  --manifest FILE  --namespace NS (dynamo-system)  --model M  --hf-token T  --nodeport P  --no-wait
+  env: MANIFEST_FILE NAMESPACE MODEL HF_TOKEN NODEPORT NO_WAIT PODS_TIMEOUT ENDPOINTS_TIMEOUT
+       SERVICES_TIMEOUT DEPLOYMENTS_TIMEOUT
+
+Steps: validate -> warn if no allocatable amd.com/gpu -> ensure namespace -> hf-token-secret (keys
+HF_TOKEN, HUGGING_FACE_HUB_TOKEN, token; "dummy" when no token) -> apply the manifest as-is ->
+find Deployments by `nvidia.com/dynamo-namespace=<ns>-<dgd>` and Services by `<dgd>-` prefix ->
+NodePort for every non-headless Service (fixed port for the frontend if given) -> wait for every
+Deployment ready (all replicas, not just the first pod) -> print the quick test.
+Fixes the reference quirks listed in SURVEY.md Appendix B items 2, 3 and 5.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from typing import Optional
+
+import yaml
+
+from .client import ApiError, KubeClient
+from .resources import GPU_RESOURCE, NS_LABEL
+
+
+def log(msg: str) -> None:
+    print(f"\n==> {msg}\n", flush=True)
+
+
+def warn(msg: str) -> None:
+    print(f"WARN: {msg}\n", file=sys.stderr, flush=True)
+
+
+class DeployError(RuntimeError):
+    pass
+
+
+def parse_args(argv=None) -> argparse.Namespace:
+    e = os.environ
+    ap = argparse.ArgumentParser(prog="deploy-incluster.sh", description="Deploy a DynamoGraphDeployment manifest")
+    ap.add_argument("--manifest", default=e.get("MANIFEST_FILE", ""))
+    ap.add_argument("--namespace", default=e.get("NAMESPACE", "dynamo-system"))
+    ap.add_argument("--model", default=e.get("MODEL", ""))
+    ap.add_argument("--hf-token", default=e.get("HF_TOKEN", ""))
+    ap.add_argument("--nodeport", default=e.get("NODEPORT", ""))
+    ap.add_argument("--no-wait", action="store_true", default=e.get("NO_WAIT", "false") == "true")
+    ap.add_argument("--server", default=e.get("MXS_KUBE_SERVER"), help=argparse.SUPPRESS)
+    a = ap.parse_args(argv)
+    a.pods_timeout = int(e.get("PODS_TIMEOUT", "1200"))
+    a.endpoints_timeout = int(e.get("ENDPOINTS_TIMEOUT", "300"))
+    a.services_timeout = int(e.get("SERVICES_TIMEOUT", "180"))
+    a.deployments_timeout = int(e.get("DEPLOYMENTS_TIMEOUT", "180"))
+    a.poll = float(e.get("MXS_POLL_SECONDS", "3"))
+    return a
+
+
+def _poll(fn, timeout: float, interval: float, what: str):
+    t0 = time.time()
+    while True:
+        v = fn()
+        if v:
+            return v
+        if time.time() - t0 > timeout:
+            raise DeployError(f"timed out after {timeout:.0f}s waiting for {what}")
+        time.sleep(interval)
+
+
+def run(a: argparse.Namespace, k: Optional[KubeClient] = None) -> dict:
+    if not a.manifest:
+        raise DeployError("--manifest is required")
+    if not os.path.isfile(a.manifest):
+        raise DeployError(f"manifest not found: {a.manifest}")
+    if a.nodeport and not (a.nodeport.isdigit() and 30000 <= int(a.nodeport) <= 32767):
+        raise DeployError(f"--nodeport must be in 30000-32767, got {a.nodeport}")
+    with open(a.manifest) as f:
+        docs = [d for d in yaml.safe_load_all(f) if isinstance(d, dict)]
+    if not docs:
+        raise DeployError("manifest contains no objects")
+    k = k or (KubeClient(a.server) if a.server else KubeClient())
+    ns = a.namespace
+
+    nodes = k.list("Node")
+    gpus = sum(int((n.get("status") or {}).get("allocatable", {}).get(GPU_RESOURCE, 0) or 0) for n in nodes)
+    if gpus == 0:
+        warn(f"no allocatable {GPU_RESOURCE} on any node (is the AMD GPU Operator / device plugin running?)")
+    else:
+        log(f"cluster has {gpus} allocatable {GPU_RESOURCE}")
+
+    if k.get("Namespace", ns) is None:
+        k.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+    tok = a.hf_token or "dummy"
+    k.apply({"apiVersion": "v1", "kind": "Secret", "metadata": {"name": "hf-token-secret", "namespace": ns},
+             "type": "Opaque", "stringData": {"HF_TOKEN": tok, "HUGGING_FACE_HUB_TOKEN": tok, "token": tok}})
+    log(f"applying {a.manifest} to namespace {ns}")
+    dgds = []
+    for d in docs:
+        d.setdefault("metadata", {})["namespace"] = ns
+        k.apply(d)
+        if d.get("kind") == "DynamoGraphDeployment":
+            dgds.append(d["metadata"]["name"])
+    result = {"namespace": ns, "graphs": {}}
+    for g in dgds:
+        sel = f"{NS_LABEL}={ns}-{g}"
+        deps = _poll(lambda: k.list("Deployment", ns, sel), a.deployments_timeout, a.poll, f"deployments of {g}")
+        svcs = _poll(lambda: [s for s in k.list("Service", ns) if s["metadata"]["name"].startswith(g + "-")],
+                     a.services_timeout, a.poll, f"services of {g}")
+        fe = [s for s in svcs if "frontend" in s["metadata"]["name"]]
+        if not fe:
+            raise DeployError(f"no frontend service for {g}")
+        ports = {}
+        for s in svcs:
+            if (s.get("spec") or {}).get("clusterIP") == "None":
+                continue  # headless worker services are not exposed
+            name = s["metadata"]["name"]
+            pl = [dict(p) for p in s["spec"]["ports"]]
+            if a.nodeport and s is fe[0]:
+                pl[0]["nodePort"] = int(a.nodeport)
+            cur = k.merge_patch("Service", name, ns, {"spec": {"type": "NodePort", "ports": pl}})
+            ports[name] = (cur.get("spec") or {}).get("ports", [{}])[0].get("nodePort")
+        if not a.no_wait:
+            def ready():
+                ds = k.list("Deployment", ns, sel)
+                return all(int((d.get("status") or {}).get("readyReplicas", 0) or 0) >= int(d["spec"].get("replicas", 1))
+                           for d in ds) and ds
+            _poll(ready, a.pods_timeout, a.poll, f"all pods of {g} ready")
+        result["graphs"][g] = {"deployments": sorted(d["metadata"]["name"] for d in deps),
+                               "services": sorted(s["metadata"]["name"] for s in svcs),
+                               "frontend": fe[0]["metadata"]["name"], "nodeports": ports}
+    node_ip = "<node-ip>"
+    for n in nodes:
+        for ad in (n.get("status") or {}).get("addresses", []):
+            if ad.get("type") == "InternalIP":
+                node_ip = ad["address"]
+    result["node_ip"] = node_ip
+    print_quick_test(result, a.model)
+    return result
+
+
+def print_quick_test(result: dict, model: str) -> None:
+    for g, info in result["graphs"].items():
+        port = info["nodeports"].get(info["frontend"])
+        base = f"http://{result['node_ip']}:{port}"
+        m = model or "<model>"
+        print(f"""
+==> Quick test for {g} (namespace {result['namespace']})
+
+export DYNAMO_BASE_URL={base}
+curl -s $DYNAMO_BASE_URL/v1/models | python3 -m json.tool
+curl -s $DYNAMO_BASE_URL/v1/chat/completions -H 'Content-Type: application/json' \\
+  -d '{json.dumps({"model": m, "messages": [{"role": "user", "content": "Hello!"}], "max_tokens": 64})}'
+./chat.sh $DYNAMO_BASE_URL/v1/chat/completions {m}
+""", flush=True)
+
+
+def main(argv=None) -> int:
+    a = parse_args(argv)
+    try:
+        run(a)
+        return 0
+    except (DeployError, ApiError) as e:
+        print(f"ERROR: {e}", file=sys.stderr)
+        return 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

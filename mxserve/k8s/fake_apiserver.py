@@ -1,0 +1,160 @@
+"""In-process fake Kubernetes apiserver: the REST subset the operator and deploy scripts use
+(CRUD, merge-patch, /status, labelSelector lists, ownerReference-free storage).  Used by the
+operator tests and the script tests; `python -m mxserve.k8s.fake_apiserver
+--port P` runs it standalone.  Optionally marks Deployments ready (simulated kubelet)."""
+from __future__ import annotations
+
+import argparse
+import copy
+import itertools
+import time
+import uuid
+
+from fastapi import FastAPI, Request
+from fastapi.responses import JSONResponse
+
+
+def _merge(dst: dict, patch: dict) -> dict:
+    for k, v in patch.items():
+        if v is None:
+            dst.pop(k, None)
+        elif isinstance(v, dict) and isinstance(dst.get(k), dict):
+            _merge(dst[k], v)
+        else:
+            dst[k] = copy.deepcopy(v)
+    return dst
+
+
+def _match(labels: dict, selector: str | None) -> bool:
+    if not selector:
+        return True
+    for term in selector.split(","):
+        term = term.strip()
+        if not term:
+            continue
+        if "!=" in term:
+            k, v = term.split("!=", 1)
+            if labels.get(k) == v:
+                return False
+        elif "=" in term:
+            k, v = term.split("=", 1)
+            if labels.get(k) != v.lstrip("="):
+                return False
+        elif labels.get(term) is None:
+            return False
+    return True
+
+
+class FakeApiServer:
+    def __init__(self, auto_ready: bool = True, nodes: int = 1, gpus_per_node: int = 8,
+                 gpu_resource: str = "amd.com/gpu"):
+        self.store: dict[tuple, dict] = {}  # (group/version, plural, ns, name) -> obj
+        self.auto_ready = auto_ready
+        self.log: list = []
+        self._rv = itertools.count(1)
+        for i in range(nodes):
+            self._put("v1", "nodes", None, {
+                "apiVersion": "v1", "kind": "Node", "metadata": {"name": f"node-{i}", "labels": {}},
+                "status": {"allocatable": {gpu_resource: str(gpus_per_node), "cpu": "128"},
+                           "addresses": [{"type": "InternalIP", "address": f"10.0.0.{i + 10}"}]}})
+        self.app = self._build()
+
+    def _put(self, gv, plural, ns, obj):
+        meta = obj.setdefault("metadata", {})
+        meta.setdefault("uid", str(uuid.uuid4()))
+        meta.setdefault("creationTimestamp", time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()))
+        meta["resourceVersion"] = str(next(self._rv))
+        if ns:
+            meta["namespace"] = ns
+        if plural == "deployments" and self.auto_ready:
+            r = int(obj.get("spec", {}).get("replicas", 1))
+            obj["status"] = {"replicas": r, "readyReplicas": r, "availableReplicas": r}
+        if plural == "services" and obj.get("spec", {}).get("type") == "NodePort":
+            used = {p.get("nodePort") for o in self.objects("services") for p in o["spec"].get("ports", [])}
+            for p in obj["spec"].get("ports", []):
+                if not p.get("nodePort"):
+                    p["nodePort"] = next(n for n in range(30000, 32768) if n not in used)
+                    used.add(p["nodePort"])
+        self.store[(gv, plural, ns, meta["name"])] = obj
+        return obj
+
+    def objects(self, plural: str, ns: str | None = None) -> list:
+        return [o for (gv, p, n, _), o in self.store.items() if p == plural and (ns is None or n == ns)]
+
+    def _build(self) -> FastAPI:
+        app = FastAPI()
+        srv = self
+
+        def handle(method: str, gv: str, plural: str, ns, name, sub, body, params):
+            srv.log.append((method, gv, plural, ns, name, sub))
+            key = (gv, plural, ns, name)
+            if name is None:
+                if method == "GET":
+                    items = [copy.deepcopy(o) for (g, p, n, _), o in srv.store.items()
+                             if g == gv and p == plural and (ns is None or n == ns)
+                             and _match(o["metadata"].get("labels") or {}, params.get("labelSelector"))]
+                    return 200, {"kind": "List", "apiVersion": gv, "items": items}
+                if method == "POST":
+                    nm = body["metadata"]["name"]
+                    if (gv, plural, ns, nm) in srv.store:
+                        return 409, {"kind": "Status", "reason": "AlreadyExists", "message": f"{nm} exists"}
+                    return 201, copy.deepcopy(srv._put(gv, plural, ns, copy.deepcopy(body)))
+                return 405, {}
+            cur = srv.store.get(key)
+            if cur is None:
+                if method == "PUT":
+                    return 201, copy.deepcopy(srv._put(gv, plural, ns, copy.deepcopy(body)))
+                return 404, {"kind": "Status", "reason": "NotFound", "message": f"{plural} {name} not found"}
+            if method == "GET":
+                return 200, copy.deepcopy(cur)
+            if method == "DELETE":
+                del srv.store[key]
+                return 200, {"kind": "Status", "status": "Success"}
+            if method == "PATCH":
+                if sub == "status":
+                    cur.setdefault("status", {})
+                    _merge(cur["status"], body.get("status", {}))
+                else:
+                    body = {k: v for k, v in body.items() if k != "status"}
+                    _merge(cur, body)
+                    if plural in ("deployments", "services"):
+                        srv._put(gv, plural, ns, cur)
+                return 200, copy.deepcopy(cur)
+            if method == "PUT":
+                return 200, copy.deepcopy(srv._put(gv, plural, ns, copy.deepcopy(body)))
+            return 405, {}
+
+        async def core(request: Request, path: str):
+            parts = [p for p in path.split("/") if p]
+            # api/v1[/namespaces/ns]/plural[/name][/sub]  |  apis/group/version[/namespaces/ns]/plural[...]
+            if parts[0] == "api":
+                gv, rest = parts[1], parts[2:]
+            else:
+                gv, rest = f"{parts[1]}/{parts[2]}", parts[3:]
+            ns = None
+            if len(rest) >= 2 and rest[0] == "namespaces" and len(rest) > 2:
+                ns, rest = rest[1], rest[2:]
+            plural = rest[0]
+            name = rest[1] if len(rest) > 1 else None
+            sub = rest[2] if len(rest) > 2 else None
+            body = None
+            if request.method in ("POST", "PUT", "PATCH"):
+                body = await request.json()
+            code, out = handle(request.method, gv, plural, ns, name, sub, body, dict(request.query_params))
+            return JSONResponse(out, status_code=code)
+
+        app.add_api_route("/{path:path}", core, methods=["GET", "POST", "PUT", "PATCH", "DELETE"])
+        return app
+
+
+def main(argv=None) -> None:
+    import uvicorn
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--port", type=int, default=16443)
+    ap.add_argument("--no-auto-ready", action="store_true")
+    a = ap.parse_args(argv)
+    uvicorn.run(FakeApiServer(auto_ready=not a.no_auto_ready).app, host="127.0.0.1", port=a.port, log_level="warning")
+
+
+if __name__ == "__main__":
+    main()

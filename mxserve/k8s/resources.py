@@ -1,0 +1,305 @@
+"""DynamoGraphDeployment (DGD) / DynamoGraphDeploymentRequest (DGDR) schema + rendering.
+
+Same group/version/kinds as the reference manifests (`nvidia.com/v1alpha1`, examples/deploy/vllm/
+agg.yaml:6-7, examples/dgdr/trtllm/dgdr.yaml:6-7) so they apply unchanged; SURVEY.md Appendix A.3
+lists the fields honoured here.  Rendering (pure functions, unit-tested without a cluster):
+
+  DGD  -> one DynamoComponentDeployment (DCD) per service (owned by the DGD)
+  DCD  -> Deployment + Service (+ PodMonitor), names `<dgd>-<service key lowercased>`, label
+          `nvidia.com/dynamo-namespace=<ns>-<dgd>` (what deploy-incluster.sh:252-256 selects on),
+          single-container pods, `resources.limits.gpu` -> `amd.com/gpu` (AMD GPU Operator / ROCm
+          device plugin), readiness = /health (true only once the model is servable).
+"""
+from __future__ import annotations
+
+import copy
+import os
+import re
+from dataclasses import dataclass, field
+from typing import Optional
+
+GROUP = "nvidia.com"
+VERSION = "v1alpha1"
+API_VERSION = f"{GROUP}/{VERSION}"
+DGD_KIND = "DynamoGraphDeployment"
+DGDR_KIND = "DynamoGraphDeploymentRequest"
+DCD_KIND = "DynamoComponentDeployment"
+NS_LABEL = "nvidia.com/dynamo-namespace"
+COMPONENT_LABEL = "nvidia.com/dynamo-component"
+TYPE_LABEL = "nvidia.com/dynamo-component-type"
+SUBTYPE_LABEL = "nvidia.com/dynamo-sub-component-type"
+GPU_RESOURCE = os.environ.get("MXS_GPU_RESOURCE", "amd.com/gpu")
+DEFAULT_IMAGE = os.environ.get("MXS_DEFAULT_IMAGE", "ghcr.io/mxserve/mxserve-rocm:0.1.0")
+FRONTEND_PORT = 8000
+WORKER_PORT = 8081
+
+_DNS = re.compile(r"^[a-z0-9]([-a-z0-9]*[a-z0-9])?$")
+
+
+class ValidationError(ValueError):
+    pass
+
+
+@dataclass
+class ServiceSpec:
+    key: str
+    component_type: str  # frontend | worker | planner | ...
+    sub_component_type: Optional[str] = None  # prefill | decode
+    replicas: int = 1
+    gpus: int = 0
+    env_from_secret: Optional[str] = None
+    envs: list = field(default_factory=list)
+    volume_mounts: list = field(default_factory=list)
+    image: Optional[str] = None
+    working_dir: Optional[str] = None
+    command: Optional[list] = None
+    args: Optional[list] = None
+
+    @property
+    def dns_name(self) -> str:
+        return self.key.lower()
+
+
+@dataclass
+class GraphSpec:
+    name: str
+    namespace: str
+    services: list
+    pvcs: list = field(default_factory=list)
+    uid: Optional[str] = None
+
+
+def _int(v, what: str) -> int:
+    try:
+        return int(str(v))
+    except (TypeError, ValueError):
+        raise ValidationError(f"{what} must be an integer, got {v!r}") from None
+
+
+def parse_dgd(obj: dict, namespace: Optional[str] = None) -> GraphSpec:
+    if obj.get("apiVersion") != API_VERSION or obj.get("kind") != DGD_KIND:
+        raise ValidationError(f"expected {API_VERSION} {DGD_KIND}, got {obj.get('apiVersion')} {obj.get('kind')}")
+    meta = obj.get("metadata") or {}
+    name = meta.get("name")
+    if not name or not _DNS.match(name):
+        raise ValidationError(f"metadata.name {name!r} is not a DNS-1123 label")
+    spec = obj.get("spec") or {}
+    svcs = spec.get("services") or {}
+    if not isinstance(svcs, dict) or not svcs:
+        raise ValidationError("spec.services must be a non-empty map")
+    out = []
+    for key, s in svcs.items():
+        s = s or {}
+        ctype = s.get("componentType")
+        if ctype not in ("frontend", "worker", "planner", "main"):
+            raise ValidationError(f"services.{key}.componentType must be frontend|worker|planner, got {ctype!r}")
+        sub = s.get("subComponentType")
+        if sub is not None and sub not in ("prefill", "decode"):
+            raise ValidationError(f"services.{key}.subComponentType must be prefill|decode")
+        lim = ((s.get("resources") or {}).get("limits") or {})
+        mc = ((s.get("extraPodSpec") or {}).get("mainContainer") or {})
+        for vm in s.get("volumeMounts") or []:
+            if "name" not in vm or "mountPoint" not in vm:
+                raise ValidationError(f"services.{key}.volumeMounts entries need name and mountPoint")
+        for e in s.get("envs") or []:
+            if "name" not in e:
+                raise ValidationError(f"services.{key}.envs entries need a name")
+        if not _DNS.match(f"{name}-{key.lower()}"):
+            raise ValidationError(f"service key {key!r} does not form a valid DNS name")
+        out.append(ServiceSpec(
+            key=key, component_type=ctype, sub_component_type=sub, replicas=_int(s.get("replicas", 1), "replicas"),
+            gpus=_int(lim.get("gpu", 0), f"services.{key}.resources.limits.gpu"),
+            env_from_secret=s.get("envFromSecret"), envs=list(s.get("envs") or []),
+            volume_mounts=list(s.get("volumeMounts") or []), image=mc.get("image"),
+            working_dir=mc.get("workingDir"), command=mc.get("command"), args=mc.get("args")))
+    if not any(s.component_type == "frontend" for s in out):
+        raise ValidationError("a graph needs one frontend service")
+    pvcs = list(spec.get("pvcs") or [])
+    for p in pvcs:
+        if "name" not in p:
+            raise ValidationError("spec.pvcs entries need a name")
+    known = {p["name"] for p in pvcs}
+    for s in out:
+        for vm in s.volume_mounts:
+            if vm["name"] not in known:
+                raise ValidationError(f"volumeMount {vm['name']!r} of {s.key} is not declared in spec.pvcs")
+    return GraphSpec(name=name, namespace=namespace or meta.get("namespace") or "default", services=out,
+                     pvcs=pvcs, uid=meta.get("uid"))
+
+
+def _owner(kind: str, name: str, uid: Optional[str]) -> list:
+    if not uid:
+        return []
+    return [{"apiVersion": API_VERSION, "kind": kind, "name": name, "uid": uid, "controller": True,
+             "blockOwnerDeletion": True}]
+
+
+def frontend_url(g: GraphSpec) -> str:
+    fe = next(s for s in g.services if s.component_type == "frontend")
+    return f"http://{g.name}-{fe.dns_name}.{g.namespace}.svc.cluster.local:{FRONTEND_PORT}"
+
+
+def render_dcds(g: GraphSpec) -> list[dict]:
+    """DGD -> DynamoComponentDeployment objects (one per service)."""
+    out = []
+    for s in g.services:
+        out.append({
+            "apiVersion": API_VERSION, "kind": DCD_KIND,
+            "metadata": {"name": f"{g.name}-{s.dns_name}", "namespace": g.namespace,
+                         "labels": {NS_LABEL: f"{g.namespace}-{g.name}", COMPONENT_LABEL: s.key},
+                         "ownerReferences": _owner(DGD_KIND, g.name, g.uid)},
+            "spec": {"dynamoNamespace": f"{g.namespace}-{g.name}", "serviceName": s.key,
+                     "componentType": s.component_type, "subComponentType": s.sub_component_type,
+                     "replicas": s.replicas, "gpus": s.gpus, "image": s.image or DEFAULT_IMAGE}})
+    return out
+
+
+def _container(g: GraphSpec, s: ServiceSpec) -> dict:
+    is_fe = s.component_type == "frontend"
+    port = FRONTEND_PORT if is_fe else WORKER_PORT
+    cmd = s.command or (["python3", "-m", "dynamo.frontend"] if is_fe else ["python3", "-m", "mxserve.worker"])
+    env = [{"name": "DYN_NAMESPACE", "value": f"{g.namespace}-{g.name}"},
+           {"name": "POD_IP", "valueFrom": {"fieldRef": {"fieldPath": "status.podIP"}}},
+           {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}]
+    if is_fe:
+        env.append({"name": "DYN_HTTP_PORT", "value": str(FRONTEND_PORT)})
+    else:
+        env += [{"name": "MXS_FRONTEND_URL", "value": frontend_url(g)},
+                {"name": "DYN_SYSTEM_PORT", "value": str(WORKER_PORT)}]
+    env += [dict(e) for e in s.envs]
+    c = {"name": "main", "image": s.image or DEFAULT_IMAGE, "command": list(cmd), "env": env,
+         "ports": [{"name": "http" if is_fe else "system", "containerPort": port}],
+         "readinessProbe": {"httpGet": {"path": "/health", "port": port}, "periodSeconds": 5,
+                            "failureThreshold": 720},
+         "livenessProbe": {"httpGet": {"path": "/live", "port": port}, "periodSeconds": 10,
+                           "initialDelaySeconds": 30, "failureThreshold": 6}}
+    if s.args:
+        c["args"] = [str(a) for a in s.args]
+    if s.working_dir:
+        c["workingDir"] = s.working_dir
+    if s.env_from_secret:
+        c["envFrom"] = [{"secretRef": {"name": s.env_from_secret, "optional": True}}]
+    if s.gpus:
+        c["resources"] = {"limits": {GPU_RESOURCE: str(s.gpus)}, "requests": {GPU_RESOURCE: str(s.gpus)}}
+    if s.volume_mounts:
+        c["volumeMounts"] = [{"name": vm["name"], "mountPath": vm["mountPoint"]} for vm in s.volume_mounts]
+    if s.gpus:  # shared memory for the TP ranks' host-side metadata and RCCL
+        c.setdefault("volumeMounts", []).append({"name": "dshm", "mountPath": "/dev/shm"})
+    return c
+
+
+def render_children(g: GraphSpec, dcd_uids: Optional[dict] = None) -> list[dict]:
+    """Deployment + Service (+ PodMonitor) per service, owned by its DCD."""
+    objs = []
+    dcd_uids = dcd_uids or {}
+    for s in g.services:
+        name = f"{g.name}-{s.dns_name}"
+        labels = {NS_LABEL: f"{g.namespace}-{g.name}", COMPONENT_LABEL: s.key, TYPE_LABEL: s.component_type,
+                  "app.kubernetes.io/name": name, "app.kubernetes.io/managed-by": "mxserve-operator"}
+        if s.sub_component_type:
+            labels[SUBTYPE_LABEL] = s.sub_component_type
+        owner = _owner(DCD_KIND, name, dcd_uids.get(name))
+        pod_spec = {"containers": [_container(g, s)], "terminationGracePeriodSeconds": 30}
+        vols = [{"name": vm["name"], "persistentVolumeClaim": {"claimName": vm["name"]}} for vm in s.volume_mounts]
+        if s.gpus:
+            vols.append({"name": "dshm", "emptyDir": {"medium": "Memory"}})
+            if s.sub_component_type in ("prefill", "decode"):
+                # xGMI KV transfer between prefill and decode pods opens the peer's KV pool with
+                # hipIpcOpenMemHandle: the pods need a shared IPC namespace
+                pod_spec["hostIPC"] = True
+        if vols:
+            pod_spec["volumes"] = vols
+        objs.append({
+            "apiVersion": "apps/v1", "kind": "Deployment",
+            "metadata": {"name": name, "namespace": g.namespace, "labels": dict(labels), "ownerReferences": owner},
+            "spec": {"replicas": s.replicas, "selector": {"matchLabels": {"app.kubernetes.io/name": name}},
+                     "template": {"metadata": {"labels": dict(labels)}, "spec": pod_spec}}})
+        is_fe = s.component_type == "frontend"
+        svc_spec = {"selector": {"app.kubernetes.io/name": name},
+                    "ports": [{"name": "http" if is_fe else "system", "port": FRONTEND_PORT if is_fe else WORKER_PORT,
+                               "targetPort": FRONTEND_PORT if is_fe else WORKER_PORT}]}
+        if not is_fe:
+            svc_spec["clusterIP"] = "None"  # workers register themselves; deploy-incluster skips headless
+        objs.append({"apiVersion": "v1", "kind": "Service",
+                     "metadata": {"name": name, "namespace": g.namespace, "labels": dict(labels),
+                                  "ownerReferences": owner},
+                     "spec": svc_spec})
+        objs.append({"apiVersion": "monitoring.coreos.com/v1", "kind": "PodMonitor",
+                     "metadata": {"name": name, "namespace": g.namespace, "labels": dict(labels),
+                                  "ownerReferences": owner},
+                     "spec": {"selector": {"matchLabels": {"app.kubernetes.io/name": name}},
+                              "podMetricsEndpoints": [{"port": "http" if is_fe else "system", "path": "/metrics",
+                                                       "interval": "15s"}]}})
+    return objs
+
+
+# --------------------------------------------------------------------------- DGDR
+@dataclass
+class RequestSpec:
+    name: str
+    namespace: str
+    model: str
+    backend: str
+    config_map: Optional[str]
+    config_key: Optional[str]
+    isl: int
+    osl: int
+    ttft_ms: float
+    itl_ms: float
+    system: str
+    workers_image: Optional[str]
+    auto_apply: bool
+    uid: Optional[str] = None
+
+
+def parse_dgdr(obj: dict, namespace: Optional[str] = None) -> RequestSpec:
+    if obj.get("apiVersion") != API_VERSION or obj.get("kind") != DGDR_KIND:
+        raise ValidationError(f"expected {API_VERSION} {DGDR_KIND}")
+    meta = obj.get("metadata") or {}
+    spec = obj.get("spec") or {}
+    pc = spec.get("profilingConfig") or {}
+    cfg = pc.get("config") or {}
+    sla = cfg.get("sla") or {}
+    sweep = cfg.get("sweep") or {}
+    cm = pc.get("configMapRef") or {}
+    if not spec.get("model"):
+        raise ValidationError("spec.model is required")
+    for k in ("isl", "osl", "ttft", "itl"):
+        if k in sla and float(sla[k]) <= 0:
+            raise ValidationError(f"sla.{k} must be positive")
+    return RequestSpec(
+        name=meta.get("name", "dgdr"), namespace=namespace or meta.get("namespace") or "default",
+        model=spec["model"], backend=spec.get("backend", "vllm"), config_map=cm.get("name"), config_key=cm.get("key"),
+        isl=int(sla.get("isl", 4000)), osl=int(sla.get("osl", 500)), ttft_ms=float(sla.get("ttft", 600)),
+        itl_ms=float(sla.get("itl", 25)), system=str(sweep.get("aicSystem", "mi355x")),
+        workers_image=(spec.get("deploymentOverrides") or {}).get("workersImage"),
+        auto_apply=bool(spec.get("autoApply", False)), uid=meta.get("uid"))
+
+
+def apply_plan_to_template(template: dict, plan: dict, req: RequestSpec) -> dict:
+    """Fill a DGD template (the DGDR's ConfigMap) with the profiler's plan: replica counts, TP
+    degree (`gpu` limit + `--tp`), worker image override, model name."""
+    dgd = copy.deepcopy(template)
+    dgd.setdefault("metadata", {})["name"] = dgd["metadata"].get("name") or req.name
+    dgd["metadata"]["namespace"] = req.namespace
+    for key, s in (dgd.get("spec", {}).get("services") or {}).items():
+        if s.get("componentType") != "worker":
+            continue
+        role = s.get("subComponentType") or "agg"
+        p = plan.get(role) or plan.get("agg") or {}
+        if "replicas" in p:
+            s["replicas"] = int(p["replicas"])
+        if "tp" in p:
+            s.setdefault("resources", {}).setdefault("limits", {})["gpu"] = str(p["tp"])
+            mc = s.setdefault("extraPodSpec", {}).setdefault("mainContainer", {})
+            args = [str(a) for a in mc.get("args") or []]
+            for flag in ("--tp", "--tensor-parallel-size", "--tp-size"):
+                if flag in args:
+                    args[args.index(flag) + 1] = str(p["tp"])
+                    break
+            else:
+                args += ["--tensor-parallel-size", str(p["tp"])]
+            mc["args"] = args
+        if req.workers_image:
+            s.setdefault("extraPodSpec", {}).setdefault("mainContainer", {})["image"] = req.workers_image
+    return dgd

@@ -30,6 +30,7 @@ class WorkerInfo:
     block_size: int = 16
     kv_total_blocks: int = 1
     tp: int = 1
+    max_model_len: int = 0  # 0 = unknown
     index: int = -1
     last_seen: float = field(default_factory=time.monotonic)
     num_running: int = 0

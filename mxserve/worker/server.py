@@ -239,7 +239,7 @@ class Worker:
         st = self.aeng.last_stats
         return {"worker_id": self.worker_id, "url": self.url, "model": self.model, "role": self.role,
                 "block_size": self.args.block_size, "kv_total_blocks": st.get("kv_total_blocks", 0),
-                "tp": self.args.tensor_parallel_size}
+                "tp": self.args.tensor_parallel_size, "max_model_len": self.args.max_model_len}
 
     async def _heartbeat_loop(self) -> None:
         base = self.wargs.frontend_url.rstrip("/")

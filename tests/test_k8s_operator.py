@@ -1,0 +1,152 @@
+"""Operator against the in-process fake apiserver + schema validation of every
+example manifest (ours, and the reference's when mounted)."""
+import glob
+import os
+
+import pytest
+import yaml
+
+from mxserve.k8s.client import KubeClient
+from mxserve.k8s.fake_apiserver import FakeApiServer
+from mxserve.k8s.operator import Operator
+from mxserve.k8s.resources import (NS_LABEL, ValidationError, parse_dgd, parse_dgdr, render_children,
+                                   render_dcds)
+from mxserve.worker.args import parse_worker_args
+from tests.serving_utils import Server
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+
+
+def _manifests(base):
+    out = []
+    for p in sorted(glob.glob(os.path.join(base, "examples", "**", "*.yaml"), recursive=True)):
+        with open(p) as f:
+            for d in yaml.safe_load_all(f):
+                if isinstance(d, dict) and d.get("kind") in ("DynamoGraphDeployment", "DynamoGraphDeploymentRequest"):
+                    out.append((p, d))
+    return out
+
+
+@pytest.mark.parametrize("base", [ROOT, REF])
+def test_every_example_manifest_parses(base):
+    if not os.path.isdir(base):
+        pytest.skip("reference not mounted")
+    ms = _manifests(base)
+    assert ms
+    for path, d in ms:
+        if d["kind"] == "DynamoGraphDeployment":
+            g = parse_dgd(d, "ns")
+            for s in g.services:
+                if s.component_type == "worker":
+                    # the worker CLI accepts every dialect/flag the manifests use
+                    dialect = (s.command or ["", "", "dynamo.vllm"])[-1].split(".")[-1]
+                    wa = parse_worker_args([str(a) for a in (s.args or [])], dialect)
+                    if s.sub_component_type:
+                        assert wa.engine.disagg_mode == s.sub_component_type, path
+        else:
+            r = parse_dgdr(d, "ns")
+            assert r.isl == 4000 and r.ttft_ms == 600
+
+
+def test_render_contract():
+    with open(os.path.join(ROOT, "examples/deploy/vllm/disagg.yaml")) as f:
+        g = parse_dgd(yaml.safe_load(f), "dynamo-system")
+    dcds = render_dcds(g)
+    assert {d["metadata"]["name"] for d in dcds} == {"vllm-disagg-frontend", "vllm-disagg-vllmdecodeworker",
+                                                     "vllm-disagg-vllmprefillworker"}
+    kids = render_children(g)
+    deps = [o for o in kids if o["kind"] == "Deployment"]
+    for d in deps:
+        assert d["metadata"]["labels"][NS_LABEL] == "dynamo-system-vllm-disagg"
+        assert len(d["spec"]["template"]["spec"]["containers"]) == 1  # deploy-incluster waits for 1/1
+    w = next(d for d in deps if d["metadata"]["name"].endswith("decodeworker"))
+    c = w["spec"]["template"]["spec"]["containers"][0]
+    assert c["resources"]["limits"] == {"amd.com/gpu": "1"}
+    assert c["envFrom"][0]["secretRef"]["name"] == "hf-token-secret"
+    assert c["command"] == ["python3", "-m", "dynamo.vllm"] and "--is-decode-worker" in c["args"]
+    assert any(e["name"] == "MXS_FRONTEND_URL" and "vllm-disagg-frontend" in e["value"] for e in c["env"])
+    assert w["spec"]["template"]["spec"].get("hostIPC") is True
+    fe_svc = next(o for o in kids if o["kind"] == "Service" and "frontend" in o["metadata"]["name"])
+    assert fe_svc["spec"]["ports"][0]["port"] == 8000 and "clusterIP" not in fe_svc["spec"]
+    wk_svc = next(o for o in kids if o["kind"] == "Service" and o["metadata"]["name"].endswith("prefillworker"))
+    assert wk_svc["spec"]["clusterIP"] == "None"
+
+
+def test_invalid_specs_rejected():
+    base = {"apiVersion": "nvidia.com/v1alpha1", "kind": "DynamoGraphDeployment", "metadata": {"name": "x"},
+            "spec": {"services": {"Frontend": {"componentType": "frontend"}}}}
+    parse_dgd(base)
+    bad = yaml.safe_load(yaml.safe_dump(base))
+    bad["spec"]["services"]["W"] = {"componentType": "gpu-thing"}
+    with pytest.raises(ValidationError):
+        parse_dgd(bad)
+    bad2 = yaml.safe_load(yaml.safe_dump(base))
+    bad2["spec"]["services"]["W"] = {"componentType": "worker", "volumeMounts": [{"name": "m", "mountPoint": "/m"}]}
+    with pytest.raises(ValidationError):
+        parse_dgd(bad2)  # undeclared pvc
+    bad3 = yaml.safe_load(yaml.safe_dump(base))
+    bad3["metadata"]["name"] = "Bad_Name"
+    with pytest.raises(ValidationError):
+        parse_dgd(bad3)
+
+
+@pytest.fixture()
+def cluster():
+    fake = FakeApiServer()
+    srv = Server(fake.app).start()
+    yield fake, KubeClient(server=srv.url)
+    srv.stop()
+
+
+def test_reconcile_dgd_lifecycle(cluster):
+    fake, k = cluster
+    with open(os.path.join(ROOT, "examples/deploy/vllm/agg.yaml")) as f:
+        dgd = yaml.safe_load(f)
+    dgd["metadata"]["namespace"] = "dynamo-system"
+    k.create(dgd)
+    op = Operator(k)
+    op.reconcile_all()
+    deps = {d["metadata"]["name"] for d in fake.objects("deployments", "dynamo-system")}
+    assert deps == {"vllm-agg-frontend", "vllm-agg-vllmdecodeworker"}
+    assert {d["metadata"]["name"] for d in fake.objects("dynamocomponentdeployments")} == deps
+    assert len(fake.objects("podmonitors")) == 2
+    st = k.get("DynamoGraphDeployment", "vllm-agg", "dynamo-system")["status"]
+    assert st["state"] == "successful"
+    sel = k.list("Deployment", "dynamo-system", f"{NS_LABEL}=dynamo-system-vllm-agg")
+    assert len(sel) == 2
+    # scale a service and drop another: reconcile converges
+    dgd["spec"]["services"]["VllmDecodeWorker"]["replicas"] = 3
+    k.merge_patch("DynamoGraphDeployment", "vllm-agg", "dynamo-system", {"spec": dgd["spec"]})
+    op.reconcile_all()
+    assert k.get("Deployment", "vllm-agg-vllmdecodeworker", "dynamo-system")["spec"]["replicas"] == 3
+    # deleting the DGD garbage-collects its components
+    k.delete("DynamoGraphDeployment", "vllm-agg", "dynamo-system")
+    op.reconcile_all()
+    assert fake.objects("deployments", "dynamo-system") == []
+    assert fake.objects("dynamocomponentdeployments") == []
+
+
+def test_reconcile_dgdr_autoapply(cluster):
+    fake, k = cluster
+    ns = "dynamo-system"
+    with open(os.path.join(ROOT, "examples/dgdr/trtllm/disagg.yaml")) as f:
+        tmpl = f.read()
+    k.create({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "qwen-config", "namespace": ns},
+              "data": {"disagg.yaml": tmpl}})
+    with open(os.path.join(ROOT, "examples/dgdr/trtllm/dgdr.yaml")) as f:
+        req = yaml.safe_load(f)
+    req["metadata"]["namespace"] = ns
+    k.create(req)
+    op = Operator(k)
+    op.reconcile_all()
+    st = k.get("DynamoGraphDeploymentRequest", "qwen-trtllm", ns)["status"]
+    assert st["state"] == "Successful", st
+    assert st["profilingResults"]["feasible"]
+    dgd = k.get("DynamoGraphDeployment", "trtllm-disagg", ns)
+    assert dgd is not None and dgd["metadata"]["ownerReferences"][0]["kind"] == "DynamoGraphDeploymentRequest"
+    pre = dgd["spec"]["services"]["TRTLLMPrefillWorker"]
+    assert pre["extraPodSpec"]["mainContainer"]["image"] == req["spec"]["deploymentOverrides"]["workersImage"]
+    op.reconcile_all()  # second pass reconciles the generated DGD into deployments
+    names = {d["metadata"]["name"] for d in fake.objects("deployments", ns)}
+    assert "trtllm-disagg-trtllmprefillworker" in names and "trtllm-disagg-frontend" in names

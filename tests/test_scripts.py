@@ -1,0 +1,149 @@
+"""Drop-in scripts: deploy-incluster.sh and run-dgdr.sh against the fake
+apiserver + a live operator thread; chat.sh and multi_convos_parallel.sh against a local CPU
+frontend; `bash -n` on every shell script."""
+import glob
+import os
+import subprocess
+import threading
+import time
+
+import pytest
+import yaml
+
+from mxserve.config import EngineArgs
+from mxserve.engine.engine import AsyncEngine, LLMEngine
+from mxserve.frontend.app import Frontend
+from mxserve.k8s.client import KubeClient
+from mxserve.k8s.fake_apiserver import FakeApiServer
+from mxserve.k8s.operator import Operator
+from tests.serving_utils import Server
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_shell_syntax():
+    scripts = glob.glob(os.path.join(ROOT, "*.sh")) + glob.glob(os.path.join(ROOT, "examples", "**", "*.sh"),
+                                                                  recursive=True)
+    assert len(scripts) >= 8
+    for s in scripts:
+        r = subprocess.run(["bash", "-n", s], capture_output=True, text=True)
+        assert r.returncode == 0, (s, r.stderr)
+
+
+@pytest.fixture()
+def cluster():
+    fake = FakeApiServer()
+    srv = Server(fake.app).start()
+    k = KubeClient(server=srv.url)
+    op = Operator(k)
+    stop = threading.Event()
+
+    def loop():
+        while not stop.is_set():
+            try:
+                op.reconcile_all()
+            except Exception:  # noqa: BLE001
+                pass
+            time.sleep(0.2)
+    t = threading.Thread(target=loop, daemon=True)
+    t.start()
+    yield fake, k, srv.url
+    stop.set()
+    t.join(timeout=5)
+    srv.stop()
+
+
+def _env(url, **kw):
+    e = dict(os.environ, MXS_KUBE_SERVER=url, MXS_POLL_SECONDS="0.2", PYTHONPATH=ROOT)
+    e.update(kw)
+    return e
+
+
+def test_deploy_incluster(cluster):
+    fake, k, url = cluster
+    r = subprocess.run([os.path.join(ROOT, "deploy-incluster.sh"), "--manifest", "examples/deploy/vllm/disagg.yaml",
+                        "--model", "meta-llama/Llama-3.2-1B-Instruct", "--nodeport", "30123"], cwd=ROOT,
+                       env=_env(url), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "export DYNAMO_BASE_URL=http://10.0.0.10:30123" in r.stdout
+    sec = k.get("Secret", "hf-token-secret", "dynamo-system")
+    assert set(sec["stringData"]) == {"HF_TOKEN", "HUGGING_FACE_HUB_TOKEN", "token"}
+    svc = k.get("Service", "vllm-disagg-frontend", "dynamo-system")
+    assert svc["spec"]["type"] == "NodePort" and svc["spec"]["ports"][0]["nodePort"] == 30123
+    # headless worker services are left alone
+    assert k.get("Service", "vllm-disagg-vllmdecodeworker", "dynamo-system")["spec"].get("type") != "NodePort"
+
+
+def test_deploy_incluster_rejects_bad_nodeport(cluster):
+    _, _, url = cluster
+    r = subprocess.run([os.path.join(ROOT, "deploy-incluster.sh"), "--manifest", "examples/deploy/vllm/agg.yaml",
+                        "--nodeport", "8080"], cwd=ROOT, env=_env(url), capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "30000-32767" in r.stderr
+
+
+def test_run_dgdr(cluster):
+    fake, k, url = cluster
+    r = subprocess.run([os.path.join(ROOT, "examples/dgdr/trtllm/run-dgdr.sh")], cwd=ROOT,
+                       env=_env(url, FRONTEND_TIMEOUT="60"), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    cm = k.get("ConfigMap", "qwen-config", "dynamo-system")
+    assert "disagg.yaml" in cm["data"]
+    fe = k.get("Service", "trtllm-disagg-frontend", "dynamo-system")
+    assert fe["spec"]["ports"][0]["nodePort"] == 30081
+
+
+@pytest.fixture(scope="module")
+def local_frontend():
+    fe = Frontend(router_mode="round_robin")
+    eng = LLMEngine(EngineArgs(model="tiny-qwen3", device="cpu", cpu_num_blocks=1024, max_model_len=2048))
+    aeng = AsyncEngine(eng)
+    fe.add_local_worker(aeng, "tiny-qwen3", 256)
+    srv = Server(fe.app).start()
+    yield srv.url
+    srv.stop()
+    aeng.shutdown()
+
+
+def test_chat_sh(local_frontend):
+    r = subprocess.run([os.path.join(ROOT, "chat.sh"), local_frontend + "/v1/chat/completions", "tiny-qwen3"],
+                       input="hello\nsecond turn\n", capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    # random weights ramble: the second turn's history may outgrow the tiny context -> clean 400
+    assert r.stdout.count("Assistant:") == 2
+    assert "generation failed" not in r.stdout
+
+
+def test_multi_convos(local_frontend):
+    env = dict(os.environ, API_URL=local_frontend + "/v1/chat/completions", MODEL="tiny-qwen3", NUM_CONVOS="4",
+               CONCURRENCY="2", MAX_TOKENS="8")
+    r = subprocess.run([os.path.join(ROOT, "examples/dgdr/trtllm/multi_convos_parallel.sh")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("Transcript: Conversation") == 4 and "Done." in r.stdout
+    # failures surface as a non-zero exit
+    env["MODEL"] = "no-such-model"
+    r = subprocess.run([os.path.join(ROOT, "examples/dgdr/trtllm/multi_convos_parallel.sh")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1 and "API error" in r.stdout
+
+
+def test_chat_extraction():
+    from mxserve.clients.chat import extract_final, strip_think
+    assert extract_final("<think>x</think>\nanswer") == "answer"
+    assert extract_final("blah\nFINAL: 42\nmore") == "42\nmore"
+    assert extract_final("<think>only thinking") == ""
+    assert strip_think("<think>a\nb</think>\nfinal text") == "final text"
+
+
+def test_run_benchmarks_sh(local_frontend, tmp_path):
+    env = dict(os.environ, BENCH_ISL="20", BENCH_OSL="4", BENCH_CONCURRENCY="1,2", BENCH_REQUEST_RATE="4",
+               BENCH_EXTRA_ARGS="--num-requests 4")
+    r = subprocess.run([os.path.join(ROOT, "run-benchmarks.sh"), "-u", local_frontend, "-m", "tiny-qwen3",
+                        "-o", str(tmp_path), "-b", "smoke", "-p"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json as _json
+    summ = _json.load(open(tmp_path / "smoke" / "summary.json"))
+    assert len(summ["points"]) == 3 and all(p["failed"] == 0 for p in summ["points"])
+    assert all(p["output_tok_per_s"] > 0 and p["ttft_ms_p50"] is not None for p in summ["points"])
+    assert (tmp_path / "plots" / "summary.md").exists()
