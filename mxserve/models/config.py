@@ -134,6 +134,15 @@ _reg(ModelConfig(
     name="tiny-mixtral", arch="mixtral", hidden_size=128, intermediate_size=192, num_layers=2, num_heads=4,
     num_kv_heads=2, head_dim=32, vocab_size=512, rope_theta=1000000.0, max_position_embeddings=2048,
     num_experts=4, num_experts_per_tok=2, bos_token_id=1, eos_token_ids=[2], chat_template="mistral"))
+_reg(ModelConfig(
+    name="tiny-qwen3-gpu", arch="qwen3", hidden_size=256, intermediate_size=512, num_layers=2, num_heads=4,
+    num_kv_heads=2, head_dim=128, vocab_size=1024, rope_theta=1000000.0, rms_norm_eps=1e-6,
+    tie_word_embeddings=True, max_position_embeddings=4096, qk_norm=True, eos_token_ids=[2],
+    chat_template="chatml"))
+_reg(ModelConfig(
+    name="tiny-mixtral-gpu", arch="mixtral", hidden_size=256, intermediate_size=512, num_layers=2, num_heads=8,
+    num_kv_heads=2, head_dim=64, vocab_size=1024, rope_theta=1000000.0, max_position_embeddings=4096,
+    num_experts=4, num_experts_per_tok=2, bos_token_id=1, eos_token_ids=[2], chat_template="mistral"))
 # A GPU-test config: real head dims (64/128) and GQA ratios, few layers.
 _reg(ModelConfig(
     name="small-llama", arch="llama", hidden_size=1024, intermediate_size=2816, num_layers=4, num_heads=16,

@@ -1,0 +1,245 @@
+"""Unit tests: native block pool / hashing / KV indexer, scheduler (chunked prefill, prefix caching,
+preemption, invariants), router cost, tokenizer + chat templates, worker flag dialects, SLA planner."""
+import random
+
+import pytest
+
+from mxserve import _native
+from mxserve.engine.kv_manager import KVCacheManager
+from mxserve.engine.request import Request, SamplingParams, Status
+from mxserve.engine.scheduler import Scheduler
+
+rt = _native.rt()
+
+
+# ----------------------------------------------------------------------------- block pool
+def test_block_pool_alloc_free_evict():
+    p = rt.BlockPool(8, True)
+    a = p.allocate(5)
+    assert len(set(a)) == 5 and p.num_free() == 3
+    with pytest.raises(RuntimeError):
+        p.allocate(4)
+    p.cache_blocks(a[:2], [11, 22])
+    p.free(list(reversed(a)))
+    assert p.num_free() == 8 and p.check_invariants()
+    hit = p.get_cached_prefix([11, 22, 33])
+    assert hit == a[:2] and p.ref_count(a[0]) == 1
+    with pytest.raises(RuntimeError):
+        p.free([a[4]])  # already free -> double free detected
+    p.free(hit)
+    # eviction: allocating everything drops the cached hashes
+    p.allocate(8)
+    assert p.num_cached() == 0
+    stored, removed = p.take_events()
+    assert stored == [11, 22] and sorted(removed) == [11, 22]
+    assert p.check_invariants()
+
+
+def test_block_pool_random_ops_invariants():
+    rng = random.Random(0)
+    p = rt.BlockPool(64, True)
+    held = []
+    for step in range(3000):
+        op = rng.random()
+        if op < 0.4 and p.num_free() > 0:
+            n = rng.randint(1, min(4, p.num_free()))
+            blocks = p.allocate(n)
+            hs = [rng.randint(1, 200) for _ in blocks]
+            p.cache_blocks(blocks, hs)
+            held.append(blocks)
+        elif op < 0.7 and held:
+            p.free(held.pop(rng.randrange(len(held))))
+        else:
+            hit = p.get_cached_prefix([rng.randint(1, 200) for _ in range(3)])
+            if hit:
+                held.append(hit)
+        if step % 97 == 0:
+            assert p.check_invariants()
+    assert p.check_invariants()
+
+
+def test_block_hashes_chained_and_stable():
+    toks = list(range(100))
+    h = rt.block_hashes(toks, 16)
+    assert len(h) == 6
+    assert rt.block_hashes(toks[:48], 16) == h[:3]  # prefix property
+    other = toks[:]
+    other[20] = 999
+    h2 = rt.block_hashes(other, 16)
+    assert h2[0] == h[0] and all(a != b for a, b in zip(h2[1:], h[1:]))  # chained
+    assert rt.block_hashes(toks, 16, 0, 0) == h
+
+
+def test_kv_indexer():
+    ix = rt.KvIndexer()
+    h = rt.block_hashes(list(range(64)), 16)
+    ix.apply_stored(0, h[:4])
+    ix.apply_stored(3, h[:2])
+    assert ix.find_matches(h, 4) == [4, 0, 0, 2]
+    ix.apply_removed(0, h[1:2])
+    assert ix.find_matches(h, 4) == [1, 0, 0, 2]
+    ix.remove_worker(3)
+    assert ix.find_matches(h, 4) == [1, 0, 0, 0] and ix.num_blocks(0) == 3
+
+
+# ----------------------------------------------------------------------------- scheduler
+def _req(rid, n, max_tokens=4, base=0):
+    return Request(rid, [base + i % 50 for i in range(n)], SamplingParams(max_tokens=max_tokens, ignore_eos=True))
+
+
+def _run(s: Scheduler, steps=200):
+    done = []
+    for _ in range(steps):
+        so = s.schedule()
+        if so.is_empty:
+            break
+        assert s.kv.check_invariants()
+        toks = {x.req.request_id: 7 for x in so.all() if x.sample}
+        done += [r for r in s.update(so, toks) if r.is_finished]
+    return done
+
+
+def test_chunked_prefill_budget_and_decode_first():
+    kv = KVCacheManager(256, 16)
+    s = Scheduler(kv, max_num_seqs=8, max_num_batched_tokens=64, max_model_len=2048)
+    s.add(_req("a", 150))
+    s.add(_req("b", 10))
+    so = s.schedule()
+    assert so.num_tokens <= 64 and so.prefills[0].num_new_tokens == 64 and not so.prefills[0].sample
+    finished = [r for r in s.update(so, {}) if r.is_finished]
+    # a keeps chunking; once b decodes, decodes come first in the batch
+    saw_mixed = False
+    for _ in range(200):
+        so = s.schedule()
+        if so.is_empty:
+            break
+        assert so.num_tokens <= 64
+        saw_mixed |= bool(so.decodes and so.prefills)
+        finished += [r for r in s.update(so, {x.req.request_id: 7 for x in so.all() if x.sample}) if r.is_finished]
+    assert saw_mixed and {r.request_id for r in finished} == {"a", "b"}
+
+
+def test_prefix_cache_hits_and_first_token_recompute():
+    kv = KVCacheManager(64, 16)
+    s = Scheduler(kv, max_num_batched_tokens=512, max_model_len=1024)
+    s.add(_req("a", 64))
+    _run(s)
+    b = _req("b", 64)  # identical prompt: 3 full blocks reused, last block recomputed
+    s.add(b)
+    so = s.schedule()
+    assert b.num_cached_tokens == 48 and so.prefills[0].num_new_tokens == 16
+    _run(s)
+    assert kv.hit_rate() > 0 and kv.check_invariants()
+
+
+def test_preemption_recompute():
+    kv = KVCacheManager(12, 16)  # tiny pool forces preemption
+    s = Scheduler(kv, max_num_seqs=4, max_num_batched_tokens=256, max_model_len=1024)
+    for i in range(3):
+        s.add(_req(f"r{i}", 40, max_tokens=40, base=i * 7))
+    done = _run(s, steps=2000)
+    assert len(done) == 3 and all(len(r.output_token_ids) == 40 for r in done)
+    assert s.num_preemptions > 0 and kv.num_free() == 12 and kv.check_invariants()
+
+
+def test_stop_conditions():
+    r = Request("x", [1, 2], SamplingParams(max_tokens=10, stop_token_ids=[9]), eos_token_ids=(5,))
+    r.output_token_ids = [3]
+    assert r.check_stop(100) is None
+    r.output_token_ids.append(5)
+    assert r.check_stop(100) == Status.FINISHED_STOPPED
+    r2 = Request("y", [1], SamplingParams(max_tokens=3, ignore_eos=True), eos_token_ids=(5,))
+    r2.output_token_ids = [5, 5]
+    assert r2.check_stop(100) is None
+    r2.output_token_ids.append(5)
+    assert r2.check_stop(100) == Status.FINISHED_LENGTH
+    r3 = Request("z", [1], SamplingParams(max_tokens=10, min_tokens=3), eos_token_ids=(5,))
+    r3.output_token_ids = [5]
+    assert r3.check_stop(100) is None
+
+
+def test_remote_prefill_reserve_and_complete():
+    kv = KVCacheManager(32, 16)
+    s = Scheduler(kv, max_model_len=1024)
+    r = _req("d", 40, max_tokens=3)
+    assert s.reserve_remote(r) and len(r.block_ids) == 3 and "d" in s.remote
+    assert s.schedule().is_empty  # waits for its KV
+    s.complete_remote("d", 11)
+    assert r.output_token_ids == [11] and r in s.running
+    done = _run(s)
+    assert done and done[0].output_token_ids[0] == 11 and kv.num_free() == 32
+
+
+# ----------------------------------------------------------------------------- router
+def test_kv_router_prefers_cached_worker():
+    from mxserve.router.router import Registry, Router, WorkerInfo
+    reg = Registry()
+    a = reg.register(WorkerInfo("a", "http://a", "m", kv_total_blocks=1000))
+    b = reg.register(WorkerInfo("b", "http://b", "m", kv_total_blocks=1000))
+    router = Router(reg, "kv")
+    toks = list(range(320))
+    reg.heartbeat("b", {"num_running": 5}, stored=router.block_hashes(toks))
+    w, ov = router.pick([a, b], toks)
+    assert w.worker_id == "b" and ov == 20
+    # load balances when nothing is cached
+    reg.heartbeat("b", {"kv_total_blocks": 1000, "kv_free_blocks": 100})
+    w, ov = router.pick([a, b], list(range(1000, 1100)))
+    assert w.worker_id == "a" and ov == 0
+    reg.expire()
+    assert len(reg.list()) == 2
+
+
+# ----------------------------------------------------------------------------- tokenizer / templates
+def test_byte_tokenizer_and_templates():
+    from mxserve.frontend.chat_template import render
+    from mxserve.frontend.tokenizer import ByteTokenizer, IncrementalDetokenizer
+    from mxserve.models.config import get_model_config
+    cfg = get_model_config("meta-llama/Llama-3.2-1B-Instruct")
+    tok = ByteTokenizer(cfg)
+    text = render("llama3", [{"role": "system", "content": "S"}, {"role": "user", "content": "héllo"}])
+    assert text.startswith("<|begin_of_text|><|start_header_id|>system<|end_header_id|>\n\nS<|eot_id|>")
+    assert text.endswith("<|start_header_id|>assistant<|end_header_id|>\n\n")
+    ids = tok.encode(text)
+    assert ids[0] == 128000 and 128009 in ids
+    assert tok.decode(ids, skip_special_tokens=False) == text
+    assert "héllo" in tok.decode(ids)
+    d = IncrementalDetokenizer(tok)
+    out = "".join(d.add(t) for t in tok.encode("日本語 ok")) + d.flush()
+    assert out == "日本語 ok"
+    q = render("chatml", [{"role": "user", "content": "hi"}])
+    assert q == "<|im_start|>user\nhi<|im_end|>\n<|im_start|>assistant\n"
+    assert render("mistral", [{"role": "user", "content": "x"}]) == "<s>[INST] x [/INST]"
+
+
+# ----------------------------------------------------------------------------- worker dialects
+def test_worker_dialects(tmp_path):
+    from mxserve.worker.args import parse_worker_args
+    v = parse_worker_args(["--model", "meta-llama/Llama-3.2-1B-Instruct", "--is-prefill-worker"], "vllm")
+    assert v.engine.model == "meta-llama/Llama-3.2-1B-Instruct" and v.engine.disagg_mode == "prefill"
+    s = parse_worker_args(["--model-path", "m", "--served-model-name", "served", "--page-size", "16", "--tp", "2",
+                           "--trust-remote-code", "--skip-tokenizer-init", "--disaggregation-mode", "decode",
+                           "--disaggregation-transfer-backend", "nixl", "--disaggregation-bootstrap-port", "12345",
+                           "--host", "0.0.0.0"], "sglang")
+    assert s.engine.tensor_parallel_size == 2 and s.engine.name == "served" and s.engine.disagg_mode == "decode"
+    assert s.engine.kv_transfer_backend == "xgmi" and s.engine.bootstrap_port == 12345
+    y = tmp_path / "e.yaml"
+    y.write_text("max_batch_size: 64\nmax_num_tokens: 2048\nkv_cache_config:\n  free_gpu_memory_fraction: 0.5\n")
+    t = parse_worker_args(["--model-path", "Qwen/Qwen3-0.6B", "--extra-engine-args", str(y),
+                           "--max-num-seqs", "32"], "trtllm")
+    assert t.engine.max_num_seqs == 32 and t.engine.max_num_batched_tokens == 2048  # CLI beats YAML
+    assert t.engine.gpu_memory_utilization == 0.5
+    with pytest.raises(ValueError):
+        parse_worker_args(["--model", "m", "--page-size", "32"], "sglang")
+
+
+# ----------------------------------------------------------------------------- SLA planner
+def test_sla_plan_meets_targets():
+    from mxserve.profiler.sla import plan
+    p = plan("Qwen/Qwen3-0.6B", 4000, 500, 600, 25)
+    assert p["feasible"]
+    d = p["disagg"]
+    assert d["prefill"]["ttft_ms"] <= 600 and d["decode"]["itl_ms"] <= 25
+    assert d["gpus_used"] <= 8
+    big = plan("meta-llama/Meta-Llama-3-70B-Instruct", 2000, 256, 1000, 40)
+    assert big["agg"]["tp"] >= 1 and big["feasible"]
+    assert not plan("meta-llama/Meta-Llama-3-70B-Instruct", 4000, 500, 1, 1)["feasible"]
