@@ -102,10 +102,10 @@ def _run(s: Scheduler, steps=200):
 def test_chunked_prefill_budget_and_decode_first():
     kv = KVCacheManager(256, 16)
     s = Scheduler(kv, max_num_seqs=8, max_num_batched_tokens=64, max_model_len=2048)
-    s.add(_req("a", 150))
     s.add(_req("b", 10))
+    s.add(_req("a", 150))
     so = s.schedule()
-    assert so.num_tokens <= 64 and so.prefills[0].num_new_tokens == 64 and not so.prefills[0].sample
+    assert so.num_tokens == 64 and so.prefills[1].num_new_tokens == 54 and not so.prefills[1].sample
     finished = [r for r in s.update(so, {}) if r.is_finished]
     # a keeps chunking; once b decodes, decodes come first in the batch
     saw_mixed = False
