@@ -106,7 +106,7 @@ def test_chunked_prefill_budget_and_decode_first():
     s.add(_req("a", 150))
     so = s.schedule()
     assert so.num_tokens == 64 and so.prefills[1].num_new_tokens == 54 and not so.prefills[1].sample
-    finished = [r for r in s.update(so, {}) if r.is_finished]
+    finished = [r for r in s.update(so, {x.req.request_id: 7 for x in so.all() if x.sample}) if r.is_finished]
     # a keeps chunking; once b decodes, decodes come first in the batch
     saw_mixed = False
     for _ in range(200):
