@@ -63,6 +63,7 @@ class InputBuffers:
         self.host = torch.zeros(off, dtype=torch.uint8, pin_memory=pin)
         self.dev = self.host.to(device) if device.type != "cpu" else self.host
         self.caps = {name: n for name, (_, n, _) in self.layout.items()}
+        self._done = None
         tdt = {np.int64: torch.int64, np.int32: torch.int32, np.float32: torch.float32}
         self.hn, self.d = {}, {}
         for name, (o, n, dt) in self.layout.items():
@@ -73,6 +74,15 @@ class InputBuffers:
     def upload(self) -> None:
         if self.dev is not self.host:
             self.dev.copy_(self.host, non_blocking=True)
+            if self._done is None:
+                self._done = torch.cuda.Event()
+            self._done.record()
+
+    def wait_free(self) -> None:
+        """Block until the last upload has consumed the pinned buffer (a step that samples nothing
+        never syncs the host, and the next step must not overwrite bytes still in flight)."""
+        if self._done is not None:
+            self._done.synchronize()
 
     def host_bytes(self) -> bytes:
         return self.host.numpy().tobytes()
@@ -185,6 +195,7 @@ class ModelRunner:
     def _prepare(self, so: SchedulerOutput, graph_bs: int = 0) -> dict:
         """Fill the pinned staging buffer for this step; returns the host-side meta."""
         bs = self.bs
+        self.buf.wait_free()
         h = self.buf.hn
         dec, pre = so.decodes, so.prefills
         nd, S = len(dec), len(dec) + len(pre)
