@@ -79,17 +79,19 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
   float m = -INFINITY, l = 0.f;
+  // lowest query position held by this wave: key tiles entirely at or below it need no causal mask
+  const int wave_tok0 = t0 + (wid * 32) / G;
+  const int wave_min_pos = ctx0 + min(wave_tok0, ql - 1);
 
-  for (int k0 = 0; k0 < nkeys; k0 += 32) {
-    // ---- K fragments (A operand): key k0 + c, dims 16 ks + 8 h
+  // software pipeline: tile k0 + 32 is loaded while tile k0 is computed
+  uint4 kf[KS];
+  uint2 vf[DT][2][2];
+  auto load_tile = [&](int k0, uint4 (&kd)[KS], uint2 (&vd)[DT][2][2]) {
     const int key = k0 + c;
     const int kblk = bt[min(key, L - 1) / kPBS];
     const bf16_t* kp = kv + kblk * block_stride + k_head_off + static_cast<size_t>(key % kPBS) * D + 8 * h;
-    uint4 kf[KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) kf[ks] = *reinterpret_cast<const uint4*>(kp + 16 * ks);
-    // ---- V^T fragments (A operand of the P*V product), keys in the accumulator's permuted order
-    uint2 vf[DT][2][2];
+    for (int ks = 0; ks < KS; ++ks) kd[ks] = *reinterpret_cast<const uint4*>(kp + 16 * ks);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int kb = min(k0 + 16 * s, L - 1) / kPBS;
@@ -97,10 +99,21 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const bf16_t* vr = vp + static_cast<size_t>(32 * dt + c) * kPBS;
-        vf[dt][s][0] = *reinterpret_cast<const uint2*>(vr);
-        vf[dt][s][1] = *reinterpret_cast<const uint2*>(vr + 8);
+        vd[dt][s][0] = *reinterpret_cast<const uint2*>(vr);
+        vd[dt][s][1] = *reinterpret_cast<const uint2*>(vr + 8);
       }
     }
+  };
+  load_tile(0, kf, vf);
+
+  for (int k0 = 0; k0 < nkeys; k0 += 32) {
+    uint4 kn[KS];
+    uint2 vn[DT][2][2];
+    // D = 128 would exceed the 256-VGPR budget with a second tile in flight: load in place instead
+    constexpr bool kPipe = D <= 64;
+    const bool more = kPipe && k0 + 32 < nkeys;
+    if (more) load_tile(k0 + 32, kn, vn);
+    if (!kPipe && k0 > 0) load_tile(k0, kf, vf);
     // ---- S^T = K Q^T
     float16_ sacc;
 #pragma unroll
@@ -108,23 +121,27 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
       sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[ks]), qf[ks], sacc, 0, 0, 0);
-    // ---- mask + online softmax (row = lane c, keys split across the two lane halves)
-    float mx = -INFINITY;
+    // ---- causal mask only on tiles that cross the diagonal of some row of this wave
+    if (k0 + 31 > wave_min_pos) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int kk = k0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-      if (kk > qpos) sacc[i] = -INFINITY;
-      mx = fmaxf(mx, sacc[i]);
+      for (int i = 0; i < 16; ++i) {
+        const int kk = k0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (kk > qpos) sacc[i] = -INFINITY;
+      }
     }
+    // ---- online softmax (row = lane c, keys split across the two lane halves)
+    float mx = sacc[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mx = fmaxf(mx, sacc[i]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);
     m = mn;
     float ps = 0.f;
     bf16x8_t pf[2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float p = exp2f(sacc[i] - mn);
+      const float p = __builtin_amdgcn_exp2f(sacc[i] - mn);
       ps += p;
       pf[i >> 3][i & 7] = static_cast<__bf16>(p);
     }
@@ -158,6 +175,17 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
         const uint4 a = make_uint4(vf[dt][s][0].x, vf[dt][s][0].y, vf[dt][s][1].x, vf[dt][s][1].y);
         o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), pf[s], o[dt], 0, 0, 0);
       }
+    if (more) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) kf[ks] = kn[ks];
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          vf[dt][s][0] = vn[dt][s][0];
+          vf[dt][s][1] = vn[dt][s][1];
+        }
+    }
   }
 
   l += __shfl_xor(l, 32, 64);

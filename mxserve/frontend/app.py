@@ -28,6 +28,7 @@ from fastapi.responses import JSONResponse, Response, StreamingResponse
 
 from ..models.config import get_model_config
 from ..router.router import Registry, Router, WorkerInfo
+from ..utils.tracing import TRACER
 from .chat_template import render
 from .metrics import FrontendMetrics
 from .tokenizer import IncrementalDetokenizer, load_tokenizer
@@ -206,7 +207,8 @@ class Frontend:
                 "min_tokens": int(body.get("min_tokens") or 0),
                 "stop_token_ids": list(body.get("stop_token_ids") or [])}
 
-    async def _run(self, endpoint: str, body: dict, prompt_ids: list, model: str, chat: bool):
+    async def _run(self, endpoint: str, body: dict, prompt_ids: list, model: str, chat: bool,
+                   xrid: Optional[str] = None):
         stream = bool(body.get("stream", False))
         rtype = "stream" if stream else "unary"
         sampling = self._sampling(body, model, len(prompt_ids))
@@ -214,6 +216,9 @@ class Frontend:
         if isinstance(stops, str):
             stops = [stops]
         rid = ("chatcmpl-" if chat else "cmpl-") + uuid.uuid4().hex
+        trace = TRACER.start(xrid or rid)
+        trace.attrs.update(model=model, endpoint=endpoint, prompt_tokens=len(prompt_ids), stream=stream)
+        trace.mark("received")
         created = int(time.time())
         tok = self.tokenizer(model)
         m = self.metrics
@@ -227,6 +232,7 @@ class Frontend:
             now = time.perf_counter()
             if state["first"] is None:
                 state["first"] = now
+                trace.mark("first_token")
                 m.ttft.labels(model).observe(now - t0)
                 m.queued.labels(model).dec()
                 state["queued"] = False
@@ -242,6 +248,8 @@ class Frontend:
                 m.queued.labels(model).dec()
             m.duration.labels(model).observe(time.perf_counter() - t0)
             m.osl.labels(model).observe(state["n"])
+            trace.attrs.update(status=status, completion_tokens=state["n"])
+            TRACER.finish(trace)
 
         async def events():
             """Yields (text_delta, finish_reason|None).  With stop strings, text that could still be
@@ -334,7 +342,7 @@ class Frontend:
                 finish(status)
 
         return StreamingResponse(sse(), media_type="text/event-stream",
-                                 headers={"Cache-Control": "no-cache", "X-Request-Id": rid})
+                                 headers={"Cache-Control": "no-cache", "X-Request-Id": xrid or rid})
 
     # ---------------------------------------------------------------- app
     def _build_app(self) -> FastAPI:
@@ -365,7 +373,8 @@ class Frontend:
             except ValueError as e:
                 return _err(400, str(e))
             ids = fe.tokenizer(model).encode(text)
-            return await fe._run("chat_completions", body, ids, model, chat=True)
+            return await fe._run("chat_completions", body, ids, model, chat=True,
+                                 xrid=request.headers.get("x-request-id"))
 
         @app.post("/v1/completions")
         async def completions(request: HTTPRequest):
@@ -381,7 +390,12 @@ class Frontend:
                 ids = fe.tokenizer(model).encode(p, add_special_tokens=True)
             else:
                 return _err(400, "`prompt` must be a string or a list of token ids")
-            return await fe._run("completions", body, ids, model, chat=False)
+            return await fe._run("completions", body, ids, model, chat=False,
+                                 xrid=request.headers.get("x-request-id"))
+
+        @app.get("/debug/traces")
+        async def traces(n: int = 100):
+            return {"traces": TRACER.recent(n)}
 
         @app.get("/health")
         async def health():

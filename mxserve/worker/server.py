@@ -32,6 +32,7 @@ from ..disagg.kv_transfer import KVTransferAgent
 from ..engine.engine import AsyncEngine, LLMEngine, StepOutput
 from ..engine.request import SamplingParams
 from ..frontend.metrics import WorkerMetrics
+from ..utils.tracing import FAULTS
 from .args import WorkerArgs
 
 log = logging.getLogger("mxserve.worker")
@@ -77,6 +78,9 @@ class Worker:
                 self._stored.extend(stored)
                 self._removed.extend(removed)
         self.metrics.gen_tokens.labels(self.model).inc(len(outs))
+        if FAULTS.active():
+            FAULTS.step_delay()
+            FAULTS.count_tokens(len(outs))
 
     def take_events(self):
         with self._events_lock:
@@ -103,7 +107,13 @@ class Worker:
                 async for o in self.aeng.stream(rid, q):
                     yield _line(o)
                 return
+        drop = FAULTS.hit("drop_stream")
+        n = 0
         async for o in self.aeng.generate(toks, sp, rid):
+            n += 1
+            if drop and n > 1:  # fault injection: abort mid-stream
+                await self.aeng.submit(self.engine.abort, rid)
+                raise ConnectionError("fault injection: stream dropped")
             yield _line(o)
 
     async def _remote_prefill(self, rid: str, toks: list, sp: SamplingParams, purl: str):
@@ -140,6 +150,8 @@ class Worker:
     async def _prefill(self, body: dict) -> dict:
         """Prefill side: compute, push KV into the decode worker's pool, return the first token."""
         rid = body["request_id"]
+        if FAULTS.hit("fail_prefill"):
+            raise RuntimeError("fault injection: prefill rejected")
         toks = list(body["token_ids"])
         sp = _sampling(body.get("sampling", {}))
         sp.max_tokens = 1

@@ -171,3 +171,63 @@ def test_disaggregated_matches_aggregated():
         fs.stop()
         pw.aeng.shutdown()
         dw.aeng.shutdown()
+
+
+def test_request_trace_by_x_request_id(agg_stack):
+    _, fs, _ = agg_stack
+    r = httpx.post(fs.url + "/v1/chat/completions", headers={"x-request-id": "trace-me-1"},
+                   json={"model": MODEL, "messages": [{"role": "user", "content": "t"}], "max_tokens": 3}, timeout=60)
+    assert r.status_code == 200
+    tr = [t for t in httpx.get(fs.url + "/debug/traces").json()["traces"] if t["request_id"] == "trace-me-1"]
+    assert tr and tr[0]["status"] == "success"
+    spans = tr[0]["spans_ms"]
+    assert spans["received"] <= spans["first_token"] <= spans["done"]
+
+
+def test_retry_on_dead_worker_before_first_token(agg_stack):
+    """A registered worker that refuses connections is skipped (and dropped) before the first token."""
+    from mxserve.router.router import WorkerInfo
+    from tests.serving_utils import free_port
+    _, _, w = agg_stack
+    fe = Frontend(router_mode="round_robin", ttl=30)
+    fe.registry.register(WorkerInfo(worker_id="dead", url=f"http://127.0.0.1:{free_port()}", model=MODEL))
+    fe.registry.register(WorkerInfo(worker_id="live", url=w.url, model=MODEL))
+    fs = Server(fe.app).start()
+    try:
+        for _ in range(2):
+            r = httpx.post(fs.url + "/v1/chat/completions",
+                           json={"model": MODEL, "messages": [{"role": "user", "content": "r"}], "max_tokens": 2},
+                           timeout=60)
+            assert r.status_code == 200, r.text
+        assert [x.worker_id for x in fe.registry.list()] == ["live"]
+    finally:
+        fs.stop()
+
+
+def test_disagg_prefill_failure_falls_back_to_local():
+    """Fault injection: the prefill worker rejects every /prefill; the decode worker
+    prefills locally and the answer is unchanged."""
+    from mxserve.utils.tracing import FAULTS
+    fe = Frontend(router_mode="round_robin", ttl=30)
+    fs = Server(fe.app).start()
+    pw, ps = _worker(fs.url, role="prefill")
+    dw, ds = _worker(fs.url, role="decode")
+    ps.start()
+    ds.start()
+    body = {"model": MODEL, "messages": [{"role": "user", "content": "fallback " * 4}], "max_tokens": 6,
+            "temperature": 0, "ignore_eos": True}
+    try:
+        wait_for(lambda: len(fe.registry.list()) == 2)
+        ok = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=120).json()
+        FAULTS.p = {"fail_prefill": 1.0}
+        r = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=120)
+        assert r.status_code == 200, r.text
+        assert r.json()["choices"][0]["message"]["content"] == ok["choices"][0]["message"]["content"]
+        assert dw.engine.kv.check_invariants() and pw.engine.kv.check_invariants()
+    finally:
+        FAULTS.p = {}
+        ps.stop()
+        ds.stop()
+        fs.stop()
+        pw.aeng.shutdown()
+        dw.aeng.shutdown()
