@@ -26,6 +26,9 @@ class EngineArgs:
     num_gpu_blocks: Optional[int] = None  # override the memory-derived count
     enforce_eager: bool = False  # disable hipGraph capture of decode steps
     cuda_graph_max_bs: int = 256
+    # schedule + launch step N+1 before waiting for step N's sampled tokens (host work overlaps
+    # the GPU; decode inputs are read on the device from the last sampled token of each row)
+    async_scheduling: bool = True
     load_format: str = "auto"  # auto | safetensors | random
     seed: int = 0
     # disaggregation role: "agg" | "prefill" | "decode"

@@ -47,6 +47,9 @@ class LLMEngine:
         self.num_generated = 0
         self.num_prompt_computed = 0
         self.check_invariants = False
+        # async scheduling: the launched-but-not-collected step (scheduler output, runner handle)
+        self.async_scheduling = bool(args.async_scheduling)
+        self._inflight: Optional[tuple] = None
 
     # ------------------------------------------------------------------ requests
     def add_request(self, prompt_token_ids: list, sampling: Optional[SamplingParams] = None,
@@ -97,18 +100,31 @@ class LLMEngine:
             self.scheduler.release_blocks(req)
 
     def has_unfinished(self) -> bool:
-        return self.scheduler.has_work()
+        return self.scheduler.has_work() or self._inflight is not None
 
     # ------------------------------------------------------------------ step
     def step(self) -> list[StepOutput]:
+        """One engine iteration.  Synchronous: schedule, run, land.  Async: schedule and launch
+        step N+1 first, then land step N (whose GPU work finished while the host was busy), so the
+        GPU queue never drains between steps."""
         so = self.scheduler.schedule()
-        if so.is_empty:
+        handle = None
+        if not so.is_empty:
+            handle = self.runner.launch(so)
+            for s in so.prefills:
+                self.num_prompt_computed += s.num_new_tokens
+            self.num_steps += 1
+        if self.async_scheduling:
+            done, self._inflight = self._inflight, ((so, handle) if handle is not None else None)
+        else:
+            done = (so, handle) if handle is not None else None
+        if done is None:
             return []
-        sampled = self.runner.execute(so)
-        for s in so.prefills:
-            self.num_prompt_computed += s.num_new_tokens
+        dso, dh = done
+        return self._land(dso, self.runner.collect(dh))
+
+    def _land(self, so, sampled: dict) -> list[StepOutput]:
         emitted = self.scheduler.update(so, sampled)
-        self.num_steps += 1
         outs = []
         for req in emitted:
             fin = req.is_finished

@@ -31,7 +31,7 @@ class KVCacheManager:
         """Extend req.block_hashes to cover every full block of known tokens."""
         bs = self.block_size
         have = len(req.block_hashes)
-        want = req.num_tokens // bs
+        want = req.num_known_tokens // bs
         if want <= have:
             return
         parent = req.block_hashes[-1] if have else 0

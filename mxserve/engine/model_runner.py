@@ -47,6 +47,7 @@ class InputBuffers:
 
     _SEGS = (("input_ids", np.int64, "T"), ("positions", np.int64, "T"), ("slot_mapping", np.int64, "T"),
              ("logits_indices", np.int64, "S"), ("seeds", np.int64, "S"), ("steps", np.int64, "S"),
+             ("srows", np.int64, "S"),
              ("bt_idx", np.int64, "U"), ("seq_lens", np.int32, "S"), ("qsl", np.int32, "S1"),
              ("rows", np.int32, "S"), ("top_k", np.int32, "S"), ("bt_val", np.int32, "U"),
              ("temperature", np.float32, "S"), ("top_p", np.float32, "S"))
@@ -116,9 +117,13 @@ class ModelRunner:
         # incrementally (a decode step touches at most one new entry per request)
         n_rows = args.max_num_seqs + 8
         self.bt_dev = torch.zeros(n_rows, self.max_blocks_per_seq, dtype=torch.int32, device=self.device)
+        # last sampled token per row: a decode whose input was sampled by a step still in flight
+        # (async scheduling) reads it here on the device
+        self.last_tok = torch.zeros(n_rows, dtype=torch.int64, device=self.device)
+        self.pad_row = n_rows - 1  # graph padding rows point here; never given to a request
         self._row_of: dict[str, int] = {}
         self._row_state: dict[str, tuple] = {}
-        self._free_rows = list(range(n_rows - 1, -1, -1))
+        self._free_rows = list(range(n_rows - 2, -1, -1))
         self._row_temp = np.zeros(n_rows, dtype=np.float32)
         self._row_topp = np.ones(n_rows, dtype=np.float32)
         self._row_topk = np.zeros(n_rows, dtype=np.int32)
@@ -127,6 +132,12 @@ class ModelRunner:
         self.buf = InputBuffers(self.max_tokens_per_step, n_rows,
                                 self.max_tokens_per_step // self.bs + 4 * self.max_blocks_per_seq + n_rows,
                                 self.device, pin=self.is_gpu)
+        # sampled ids come back through two alternating pinned buffers (step N's result is read
+        # while step N+1, launched just before, may already be writing the other one)
+        self._out_slot = 0
+        if self.is_gpu:
+            self._out_pinned = [torch.zeros(n_rows, dtype=torch.int64, pin_memory=True) for _ in range(2)]
+            self._out_events = [torch.cuda.Event(), torch.cuda.Event()]
         self.graphs: dict[int, tuple] = {}
         if self.is_gpu and not args.enforce_eager:
             self._capture_graphs()
@@ -204,14 +215,19 @@ class ModelRunner:
         toks, pos, slots, lens, rows, steps = [], [], [], [], [], []
         for s in dec:
             r = s.req
-            p = r.num_computed_tokens
+            p = s.start
             npr = len(r.prompt_token_ids)
-            toks.append(r.output_token_ids[p - npr] if p >= npr else r.prompt_token_ids[p])
+            if p < npr:
+                toks.append(r.prompt_token_ids[p])
+            elif p - npr < len(r.output_token_ids):
+                toks.append(r.output_token_ids[p - npr])
+            else:  # sampled by the step in flight: read from last_tok on the device
+                toks.append(-1)
             pos.append(p)
             slots.append(r.block_ids[p // bs] * bs + p % bs)
             lens.append(p + 1)
             rows.append(self._row_for(r, upd_idx, upd_val))
-            steps.append(len(r.output_token_ids))
+            steps.append(s.out_idx)
         T = nd
         h["input_ids"][:nd] = toks
         h["positions"][:nd] = pos
@@ -221,7 +237,7 @@ class ModelRunner:
         max_q = 0
         for i, s in enumerate(pre):
             r = s.req
-            start, n = r.num_computed_tokens, s.num_new_tokens
+            start, n = s.start, s.num_new_tokens
             at = r.all_token_ids()
             h["input_ids"][T:T + n] = at[start:start + n]
             p = np.arange(start, start + n, dtype=np.int64)
@@ -235,7 +251,7 @@ class ModelRunner:
             max_q = max(max_q, n)
             if s.sample:
                 sample_rows.append(nd + i)
-                steps.append(len(r.output_token_ids))
+                steps.append(s.out_idx)
         rows_np = np.asarray(rows, dtype=np.int32)
         h["seq_lens"][:S] = lens
         h["qsl"][:S + 1] = qsl
@@ -248,12 +264,14 @@ class ModelRunner:
         h["top_k"][:ns] = self._row_topk[srows]
         h["seeds"][:ns] = self._row_seed[srows]
         h["steps"][:ns] = steps
+        h["srows"][:ns] = srows
         if graph_bs > S:  # padding rows of a graph bucket: no cache write, 1-token context, greedy
             h["input_ids"][S:graph_bs] = 0
             h["positions"][S:graph_bs] = 0
             h["slot_mapping"][S:graph_bs] = -1
             h["seq_lens"][S:graph_bs] = 1
-            h["rows"][S:graph_bs] = 0
+            h["rows"][S:graph_bs] = self.pad_row
+            h["srows"][S:graph_bs] = self.pad_row
             h["temperature"][S:graph_bs] = 0.0
         U = len(upd_idx)
         big_update = None
@@ -280,10 +298,11 @@ class ModelRunner:
                 bt.index_copy_(0, torch.from_numpy(idx), torch.from_numpy(val))
 
     # ------------------------------------------------------------------ execute
-    def execute(self, so: SchedulerOutput) -> dict[str, int]:
-        """Driver-rank entry: prepare inputs, fan them out to TP followers, run."""
+    def launch(self, so: SchedulerOutput) -> Optional[dict]:
+        """Driver-rank entry: prepare inputs, fan them out to TP followers, enqueue the step and
+        the copy of its sampled ids to the host.  Does not wait for the GPU."""
         if so.is_empty:
-            return {}
+            return None
         S = len(so.decodes) + len(so.prefills)
         gbs = 0
         if self.graphs and not so.prefills and S <= max(self.graphs):
@@ -292,19 +311,45 @@ class ModelRunner:
         if get_tp().tp_size > 1:
             tp_broadcast_object(("step", self.buf.host_bytes(), meta))
         ids = self.execute_host(meta)
+        handle = {"so": so, "rows": meta["sample_rows"]}
         if ids is None:
+            return handle
+        if self.is_gpu:
+            self._out_slot ^= 1
+            pinned = self._out_pinned[self._out_slot][:ids.shape[0]]
+            pinned.copy_(ids, non_blocking=True)
+            ev = self._out_events[self._out_slot]
+            ev.record()
+            handle.update(pinned=pinned, ev=ev)
+        else:
+            handle["ids"] = ids
+        return handle
+
+    def collect(self, handle: Optional[dict]) -> dict[str, int]:
+        """Wait for a launched step's sampled ids; {request_id: token}."""
+        if handle is None:
             return {}
-        reqs = so.all()
-        ids = ids.tolist()
-        return {reqs[r].req.request_id: ids[k] for k, r in enumerate(meta["sample_rows"])}
+        if "ev" in handle:
+            handle["ev"].synchronize()
+            ids = handle["pinned"].tolist()
+        elif "ids" in handle:
+            ids = handle["ids"].tolist()
+        else:
+            return {}
+        reqs = handle["so"].all()
+        return {reqs[r].req.request_id: ids[k] for k, r in enumerate(handle["rows"])}
+
+    def execute(self, so: SchedulerOutput) -> dict[str, int]:
+        return self.collect(self.launch(so))
 
     @torch.inference_mode()
     def execute_host(self, meta: dict):
+        """Run one step on this rank; returns the device tensor of sampled ids (or None)."""
         self._upload(meta)
         if meta["graph_bs"]:
             g, out = self.graphs[meta["graph_bs"]]
             g.replay()
-            return out[:meta["S"]].cpu()
+            return out[:meta["S"]]
         return self._forward_eager(meta, sample=bool(meta["sample_rows"]))
 
     def follower_loop(self) -> None:
@@ -326,7 +371,8 @@ class ModelRunner:
         return dict(input_ids=d["input_ids"][:T], positions=d["positions"][:T], slot_mapping=d["slot_mapping"][:T],
                     seq_lens=d["seq_lens"][:S], qsl=d["qsl"][:S + 1], rows=d["rows"][:S],
                     logits_indices=d["logits_indices"][:ns], temperature=d["temperature"][:ns],
-                    top_p=d["top_p"][:ns], top_k=d["top_k"][:ns], seeds=d["seeds"][:ns], steps=d["steps"][:ns])
+                    top_p=d["top_p"][:ns], top_k=d["top_k"][:ns], seeds=d["seeds"][:ns], steps=d["steps"][:ns],
+                    srows=d["srows"][:ns])
 
     def _forward_eager(self, meta: dict, sample: bool):
         S, T, nd = meta["S"], meta["T"], meta["nd"]
@@ -339,25 +385,35 @@ class ModelRunner:
                           seq_lens=v["seq_lens"], query_start_loc=v["qsl"], logits_indices=v["logits_indices"],
                           num_decodes=nd, num_prefills=S - nd, num_prefill_tokens=T - nd,
                           max_query_len=meta["max_q"], max_seq_len=meta["max_seq"], prefill_query_start_loc=pq)
-        hidden = self.model.forward(v["input_ids"], md, self.kv_cache)
+        inp = v["input_ids"]
+        if nd:
+            d_in = inp[:nd]
+            d_in.copy_(torch.where(d_in < 0, self.last_tok.index_select(0, v["rows"][:nd].long()), d_in))
+        hidden = self.model.forward(inp, md, self.kv_cache)
         if not sample:
             return None
         logits = self.model.compute_logits(hidden)
         ids = ops.sample(logits, v["temperature"], v["top_p"], v["top_k"], v["seeds"], v["steps"])
-        return ids.cpu()
+        self.last_tok.index_copy_(0, v["srows"], ids)
+        return ids
 
     # ------------------------------------------------------------------ hipGraph decode
     def _graph_body(self, b: int) -> torch.Tensor:
         v = self._views(b, b, b)
-        bt = self.bt_dev.index_select(0, v["rows"].long())
+        rows = v["rows"].long()
+        bt = self.bt_dev.index_select(0, rows)
+        inp = v["input_ids"]
+        inp = torch.where(inp < 0, self.last_tok.index_select(0, rows), inp)
         md = AttnMetadata(
             positions=v["positions"], slot_mapping=v["slot_mapping"], block_tables=bt,
             seq_lens=v["seq_lens"], query_start_loc=v["qsl"], logits_indices=self._arange[:b],
             num_decodes=b, num_prefills=0, num_prefill_tokens=0, max_query_len=1,
             max_seq_len=self.args.max_model_len)
-        hidden = self.model.forward(v["input_ids"], md, self.kv_cache)
+        hidden = self.model.forward(inp, md, self.kv_cache)
         logits = self.model.compute_logits(hidden)
-        return ops.sample(logits, v["temperature"], v["top_p"], v["top_k"], v["seeds"], v["steps"])
+        ids = ops.sample(logits, v["temperature"], v["top_p"], v["top_k"], v["seeds"], v["steps"])
+        self.last_tok.index_copy_(0, v["srows"], ids)
+        return ids
 
     def _capture_graphs(self) -> None:
         maxb = min(self.args.cuda_graph_max_bs, self.args.max_num_seqs)
@@ -367,7 +423,8 @@ class ModelRunner:
         h = self.buf.hn
         h["slot_mapping"][:] = -1
         h["seq_lens"][:] = 1
-        h["rows"][:] = 0
+        h["rows"][:] = self.pad_row
+        h["srows"][:] = self.pad_row
         h["qsl"][:] = np.arange(len(h["qsl"]))
         h["temperature"][:] = 0
         h["top_p"][:] = 1

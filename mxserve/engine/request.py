@@ -79,6 +79,10 @@ class Request:
     finish_time: Optional[float] = None
     num_preemptions: int = 0
     kv_gen: int = 0  # bumped whenever block_ids is rebuilt from scratch (free / preempt)
+    # tokens scheduled for sampling whose value is still on the GPU (async scheduling: step N+1 is
+    # scheduled before step N's sampled ids reach the host; a decode's input is then read on the
+    # device from the row's last sampled token)
+    num_pending: int = 0
 
     def __post_init__(self):
         self.seed = self.sampling.seed if self.sampling.seed is not None else _next_seed()
@@ -89,7 +93,17 @@ class Request:
 
     @property
     def num_tokens(self) -> int:
+        """Tokens the sequence will hold once in-flight samples land (scheduling view)."""
+        return len(self.prompt_token_ids) + len(self.output_token_ids) + self.num_pending
+
+    @property
+    def num_known_tokens(self) -> int:
         return len(self.prompt_token_ids) + len(self.output_token_ids)
+
+    def can_grow(self, max_model_len: int) -> bool:
+        """False once the in-flight samples already reach max_tokens / the context limit."""
+        n_out = len(self.output_token_ids) + self.num_pending
+        return n_out < self.sampling.max_tokens and self.num_tokens < max_model_len
 
     def token_at(self, i: int) -> int:
         n = len(self.prompt_token_ids)
@@ -112,6 +126,6 @@ class Request:
                 return Status.FINISHED_STOPPED
             if last in self.sampling.stop_token_ids:
                 return Status.FINISHED_STOPPED
-        if n_out >= self.sampling.max_tokens or self.num_tokens >= max_model_len:
+        if n_out >= self.sampling.max_tokens or self.num_known_tokens >= max_model_len:
             return Status.FINISHED_LENGTH
         return None

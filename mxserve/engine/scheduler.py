@@ -24,6 +24,8 @@ class ScheduledReq:
     num_new_tokens: int
     # sample a token at the end of this chunk (chunk reaches the end of the known tokens)
     sample: bool
+    start: int = 0  # first position computed by this chunk
+    out_idx: int = 0  # index of the output token this chunk samples (RNG counter)
 
 
 @dataclass
@@ -139,7 +141,7 @@ class Scheduler:
         while i < len(self.running) and budget > 0:
             req = self.running[i]
             n = req.num_tokens - req.num_computed_tokens
-            if n <= 0:
+            if n <= 0 or (req.num_pending and not req.can_grow(self.max_model_len)):
                 i += 1
                 continue
             n = min(n, budget)
@@ -163,6 +165,8 @@ class Scheduler:
 
         while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs and not out.preempted:
             req = self.waiting[0]
+            if req.num_pending:  # preempted with a sample still in flight: wait for it
+                break
             if req.num_computed_tokens == 0 and not req.block_ids:
                 req.num_cached_tokens = self.kv.get_computed_blocks(req)
                 req.num_computed_tokens = req.num_cached_tokens
@@ -180,41 +184,58 @@ class Scheduler:
             budget -= n
 
         for s in scheduled:
-            is_decode = s.num_new_tokens == 1 and s.req.num_computed_tokens >= s.req.num_prompt_tokens
+            r = s.req
+            is_decode = s.num_new_tokens == 1 and r.num_computed_tokens >= r.num_prompt_tokens
             (out.decodes if is_decode else out.prefills).append(s)
+            # advance now (not at update) so the next step can be scheduled while this one runs
+            s.start = r.num_computed_tokens
+            r.num_computed_tokens += s.num_new_tokens
+            if s.sample:
+                s.out_idx = len(r.output_token_ids) + r.num_pending
+                r.num_pending += 1
         return out
 
     # ------------------------------------------------------------------ update
     def update(self, out: SchedulerOutput, sampled: dict[str, int]) -> list[Request]:
-        """Advance computed-token counters, append sampled tokens, retire finished requests.
-        Returns requests that produced a new token this step (finished ones included)."""
+        """Land a step's results: register newly full blocks, append sampled tokens, retire
+        finished requests.  Returns requests that produced a new token this step (finished ones
+        included).  With async scheduling the next step may already be in flight; a request that
+        finishes here simply has its in-flight result discarded at the next update."""
         emitted = []
         now = time.monotonic()
         bs = self.kv.block_size
         for s in out.all():
             req = s.req
-            req.num_computed_tokens += s.num_new_tokens
-            if req.num_computed_tokens // bs > req.num_registered_blocks:
-                self.kv.cache_computed_blocks(req)
-            if not s.sample:
+            if req.is_finished:  # aborted / finished while this step was in flight
                 continue
+            if not s.sample:
+                if min(req.num_computed_tokens, req.num_known_tokens) // bs > req.num_registered_blocks:
+                    self.kv.cache_computed_blocks(req)
+                continue
+            req.num_pending -= 1
             tok = sampled.get(req.request_id)
             if tok is None:
                 continue
             req.output_token_ids.append(int(tok))
             if req.first_token_time is None:
                 req.first_token_time = now
+            if min(req.num_computed_tokens, req.num_known_tokens) // bs > req.num_registered_blocks:
+                self.kv.cache_computed_blocks(req)
             st = req.check_stop(self.max_model_len)
             if req.disagg_role == "prefill_only" and st is None:
                 st = Status.FINISHED_LENGTH
             if st is not None:
+                preempted = req.status == Status.PREEMPTED
                 if req.disagg_role == "prefill_only":
                     # keep the blocks: the KV transfer reads them; released by release_blocks()
                     req.status = st
                     req.finish_time = now
                 else:
                     self._finish(req, st)
-                self.running.remove(req)
+                if preempted:
+                    self.waiting.remove(req)
+                else:
+                    self.running.remove(req)
                 self.finished_ids.append(req.request_id)
             emitted.append(req)
         return emitted

@@ -59,6 +59,8 @@ def _parser(dialect: str) -> argparse.ArgumentParser:
     ap.add_argument("--enforce-eager", "--disable-cuda-graph", dest="enforce_eager", action="store_true",
                     default=None)
     ap.add_argument("--enable-prefix-caching", dest="enable_prefix_caching", action="store_true", default=None)
+    ap.add_argument("--async-scheduling", dest="async_scheduling", action="store_true", default=None)
+    ap.add_argument("--no-async-scheduling", dest="async_scheduling", action="store_false")
     ap.add_argument("--no-enable-prefix-caching", "--disable-radix-cache", dest="enable_prefix_caching",
                     action="store_false")
     ap.add_argument("--no-enable-chunked-prefill", dest="enable_chunked_prefill", action="store_false",
@@ -125,6 +127,7 @@ def parse_worker_args(argv: list[str], dialect: str = "vllm") -> WorkerArgs:
         "gpu_memory_utilization": a.gpu_memory_utilization, "num_gpu_blocks": a.num_gpu_blocks,
         "enforce_eager": a.enforce_eager, "enable_prefix_caching": a.enable_prefix_caching,
         "enable_chunked_prefill": a.enable_chunked_prefill, "device": a.device,
+        "async_scheduling": a.async_scheduling,
         "trust_remote_code": a.trust_remote_code or None, "skip_tokenizer_init": a.skip_tokenizer_init or None,
         "bootstrap_port": a.disaggregation_bootstrap_port,
     }

@@ -1,0 +1,77 @@
+"""CPU engine tests: async scheduling (step N+1 launched before step N lands) must produce exactly
+the tokens of the synchronous engine -- under greedy and seeded sampling, EOS stops, max_tokens,
+prefix-cache hits, chunked prefill and preemption (tiny pool)."""
+import random
+
+import pytest
+
+from mxserve.config import EngineArgs
+from mxserve.engine.engine import LLMEngine
+from mxserve.engine.request import SamplingParams
+
+
+def _engine(async_sched: bool, blocks: int = 256, budget: int = 64):
+    ea = EngineArgs(model="tiny-llama", device="cpu", cpu_num_blocks=blocks, max_model_len=512,
+                    max_num_batched_tokens=budget, max_num_seqs=8, load_format="random", seed=3,
+                    async_scheduling=async_sched)
+    e = LLMEngine(ea)
+    e.check_invariants = True
+    return e
+
+
+def _workload(seed=0):
+    rng = random.Random(seed)
+    shared = [rng.randrange(3, 500) for _ in range(40)]
+    reqs = []
+    for i in range(10):
+        toks = (shared if i % 3 == 0 else []) + [rng.randrange(3, 500) for _ in range(rng.randint(5, 70))]
+        sp = SamplingParams(max_tokens=rng.randint(1, 24), temperature=0.0 if i % 2 else 0.8, top_p=0.9,
+                            seed=100 + i, ignore_eos=(i % 4 == 0), stop_token_ids=[7, 11] if i % 5 == 1 else [])
+        reqs.append((f"r{i}", toks, sp))
+    return reqs
+
+
+def _run(engine, reqs, staggered=True):
+    out = {}
+    pending = list(reqs)
+    stream = {}
+    while pending or engine.has_unfinished():
+        if pending:
+            rid, toks, sp = pending.pop(0)
+            engine.add_request(toks, SamplingParams(**vars(sp)), request_id=rid)
+            if not staggered:
+                continue
+        for o in engine.step():
+            stream.setdefault(o.request_id, []).append(o.token_id)
+            if o.finished:
+                out[o.request_id] = (o.finish_reason, o.num_output_tokens)
+    return out, stream
+
+
+@pytest.mark.parametrize("blocks,budget", [(256, 64), (14, 48)])
+def test_async_matches_sync(blocks, budget):
+    reqs = _workload()
+    sync_out, sync_tok = _run(_engine(False, blocks, budget), reqs)
+    eng = _engine(True, blocks, budget)
+    async_out, async_tok = _run(eng, reqs)
+    assert sync_out == async_out
+    assert sync_tok == async_tok
+    assert eng.kv.num_free() == blocks and eng.kv.check_invariants()
+    assert not eng.requests and eng._inflight is None
+    if blocks == 14:
+        assert eng.scheduler.num_preemptions > 0
+
+
+def test_async_abort_in_flight():
+    eng = _engine(True)
+    a = eng.add_request(list(range(3, 40)), SamplingParams(max_tokens=50, ignore_eos=True), request_id="a")
+    eng.add_request(list(range(5, 30)), SamplingParams(max_tokens=5, ignore_eos=True), request_id="b")
+    for _ in range(4):
+        eng.step()
+    assert a.num_pending == 1  # a step is in flight
+    eng.abort("a")
+    outs = []
+    while eng.has_unfinished():
+        outs += eng.step()
+    assert all(o.request_id == "b" for o in outs)
+    assert eng.kv.num_free() == 256 and eng.kv.check_invariants()
