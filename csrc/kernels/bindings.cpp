@@ -23,6 +23,7 @@ void launch_sample(int64_t*, const float*, int, int, long, const float*, const f
                    const int64_t*, hipStream_t);
 void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStream_t);
 void launch_moe_align(int*, int*, const int*, int, int, int, hipStream_t);
+bool launch_skinny_gemm(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, hipStream_t);
 }  // namespace mxs
 
 namespace {
@@ -134,6 +135,16 @@ void sample(at::Tensor out, at::Tensor logits, at::Tensor temperature, at::Tenso
                      top_k.data_ptr<int>(), seeds.data_ptr<int64_t>(), steps.data_ptr<int64_t>(), stream());
 }
 
+// out[M,N] = x[M,K] . w[N,K]^T for M <= 256; false if the shape is unsupported (caller falls back)
+bool skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
+  TORCH_CHECK(x.size(1) == w.size(1) && out.size(0) == x.size(0) && out.size(1) == w.size(0), "shape mismatch");
+  if (x.stride(1) != 1 || out.stride(1) != 1) return false;
+  return mxs::launch_skinny_gemm(bf(out), bf(x), bf(w), x.size(0), w.size(0), w.size(1), x.stride(0),
+                                 out.stride(0), stream());
+}
+
 void moe_topk_softmax(at::Tensor w, at::Tensor ids, at::Tensor logits) {
   CHECK_CUDA(logits); CHECK_BF16(logits); CHECK_CONTIG(logits);
   TORCH_CHECK(logits.size(1) <= 64, "at most 64 experts");
@@ -164,6 +175,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sample", &sample);
   m.def("moe_topk_softmax", &moe_topk_softmax);
   m.def("moe_align", &moe_align);
+  m.def("skinny_gemm", &skinny_gemm);
   m.def("decode_num_partitions", &mxs::decode_num_partitions);
   m.def("decode_plan", [](int B, int Hkv, int max_seq_len) {
     int P = 1, len = 0;

@@ -162,7 +162,7 @@ class TransformerLM:
     # ------------------------------------------------------------------ forward
     def _attention(self, i: int, h: torch.Tensor, md: AttnMetadata, kv_layer: torch.Tensor):
         c, w, p = self.cfg, self.w, f"l{i}."
-        qkv = F.linear(h, w[p + "qkv"])
+        qkv = ops.linear(h, w[p + "qkv"])
         q = ops.rope_and_cache(qkv, self.nh, self.nkv, self.hd, md.positions, self.cos_sin, kv_layer,
                                md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"), c.rms_norm_eps)
         nd = md.num_decodes
@@ -180,7 +180,7 @@ class TransformerLM:
                                        md.max_seq_len, out=o[:nd])
             ops.paged_attention_prefill(q[nd:], kv_layer, md.block_tables[nd:], md.prefill_query_start_loc,
                                         md.seq_lens[nd:], self.scale, md.max_query_len, out=o[nd:])
-        out = F.linear(o.reshape(o.shape[0], -1), w[p + "o"])
+        out = ops.linear(o.reshape(o.shape[0], -1), w[p + "o"])
         return tp_all_reduce(out)
 
     def _mlp(self, i: int, h: torch.Tensor) -> torch.Tensor:
@@ -190,8 +190,8 @@ class TransformerLM:
             tw, tid = ops.moe_topk_softmax(router, self.cfg.num_experts_per_tok)
             out = ops.moe_experts(h, w[p + "w13"], w[p + "w2"], tw, tid, self.e_offset)
         else:
-            a = ops.silu_mul(F.linear(h, w[p + "gate_up"]))
-            out = F.linear(a, w[p + "down"])
+            a = ops.silu_mul(ops.linear(h, w[p + "gate_up"]))
+            out = ops.linear(a, w[p + "down"])
         return tp_all_reduce(out)
 
     def embed(self, input_ids: torch.Tensor) -> torch.Tensor:
@@ -216,7 +216,7 @@ class TransformerLM:
         return h.index_select(0, md.logits_indices)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        logits = F.linear(hidden, self.lm_head_weight()).float()
+        logits = ops.linear(hidden, self.lm_head_weight()).float()
         if self.tp_size > 1:
             logits = tp_all_gather(logits, dim=-1)
         return logits[:, :self.cfg.vocab_size]

@@ -46,6 +46,25 @@ def _gpu(t: torch.Tensor) -> bool:
     return t.is_cuda and os.environ.get("MXS_FORCE_REFERENCE_OPS", "0") != "1"
 
 
+# ----------------------------------------------------------------------------- GEMM
+SKINNY_MAX_M = 256
+
+
+_SKINNY = os.environ.get("MXS_SKINNY_GEMM", "0") == "1"
+
+
+def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """y = x @ w.T.  hipBLASLt by default.  MXS_SKINNY_GEMM=1 routes decode-sized GEMMs (M <= 256)
+    to the weight-streaming MFMA kernel (csrc/kernels/gemm_skinny.hip).  Measured inside hipGraphs
+    (profiles/r1_v4_microbench_gemm.jsonl) it only ties hipBLASLt at M <= 16 and loses at larger M
+    (no LDS reuse of the activation tile yet), so it is opt-in."""
+    if _SKINNY and _gpu(x) and x.dim() == 2 and x.shape[0] <= SKINNY_MAX_M:
+        out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+        if ext().skinny_gemm(out, x, w):
+            return out
+    return torch.nn.functional.linear(x, w)
+
+
 # ----------------------------------------------------------------------------- norms / act
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
     if _gpu(x):

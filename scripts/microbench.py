@@ -29,6 +29,29 @@ def timeit(fn, iters=20, warmup=3):
     return s.elapsed_time(e) / iters
 
 
+def timeit_graph(fn, iters=20):
+    """Kernel time without host launch gaps: `iters` calls captured in one hipGraph."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.inference_mode(), torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    g.replay()
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) / iters
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="meta-llama/Llama-3.2-1B-Instruct")
@@ -117,15 +140,19 @@ def main():
     H, I = cfg.hidden_size, cfg.intermediate_size
     shapes = {"qkv": ((m.nh + 2 * m.nkv) * cfg.head_dim, H), "o": (H, m.nh * cfg.head_dim), "gate_up": (2 * I, H),
               "down": (H, I), "lm_head": (cfg.vocab_size, H)}
-    for Mrows in (T, B):
+    for Mrows in (T, B, 64, 16, 1) if B not in (64, 16, 1) else (T, B):
         for name, (N, K) in shapes.items():
             if name == "lm_head" and Mrows == T:
                 continue
             x = torch.randn(Mrows, K, dtype=torch.bfloat16, device=dev)
             w = torch.randn(N, K, dtype=torch.bfloat16, device=dev)
-            tt = timeit(lambda: F.linear(x, w))
-            out.append({"op": f"gemm_{name}", "M": Mrows, "N": N, "K": K, "ms": tt,
-                        "TFLOPs": 2 * Mrows * N * K / tt / 1e9, "GBps_w": N * K * 2 / tt / 1e6})
+            impls = {"hipblaslt": lambda: F.linear(x, w)}
+            if Mrows <= ops.SKINNY_MAX_M:
+                impls["skinny"] = lambda: ops.linear(x, w)
+            for impl, fn in impls.items():
+                tt = timeit_graph(fn)
+                out.append({"op": f"gemm_{name}", "impl": impl, "M": Mrows, "N": N, "K": K, "ms": tt,
+                            "TFLOPs": 2 * Mrows * N * K / tt / 1e9, "GBps_w": N * K * 2 / tt / 1e6})
     # elementwise
     x = torch.randn(T, H, dtype=torch.bfloat16, device=dev)
     w = torch.ones(H, dtype=torch.bfloat16, device=dev)

@@ -235,3 +235,25 @@ def test_copy_blocks(gpu):
     for s, d in zip(s_ids.tolist(), d_ids.tolist()):
         assert torch.equal(dst[d], src[s])
     assert dst[1].abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("N,K", [(3072, 2048), (2048, 8192), (16384, 2048), (6144, 4096), (1056, 1024)])
+@pytest.mark.parametrize("M", [1, 3, 16, 24, 33, 64, 100, 256])
+def test_skinny_gemm(gpu, M, N, K):
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = (torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.02).to(torch.bfloat16)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    assert ops.ext().skinny_gemm(out, x, w), "shape unexpectedly unsupported"
+    want = x.float() @ w.float().t()
+    _close(out, want, atol=2e-2, rtol=2e-2, name=f"skinny {M}x{N}x{K}")
+
+
+def test_skinny_gemm_strided_input_and_fallback(gpu):
+    x = torch.randn(8, 4096, device="cuda", dtype=torch.bfloat16)[:, :2048]  # row stride 4096
+    w = torch.randn(512, 2048, device="cuda", dtype=torch.bfloat16) * 0.02
+    _close(ops.linear(x, w), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2, name="strided")
+    w_odd = torch.randn(100, 2048, device="cuda", dtype=torch.bfloat16)  # N % 16 != 0 -> hipBLASLt
+    out = torch.empty(8, 100, device="cuda", dtype=torch.bfloat16)
+    assert not ops.ext().skinny_gemm(out, x.contiguous(), w_odd)
+    _close(ops.linear(x, w_odd), x.float() @ w_odd.float().t(), atol=0.3, rtol=2e-2, name="fallback")
