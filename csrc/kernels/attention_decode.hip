@@ -25,8 +25,20 @@ namespace mxs {
 
 constexpr int kBS = 16;  // tokens per KV block (SGLang --page-size 16, sglang/agg.yaml:38-39)
 constexpr int kWaves = 4;
-constexpr int kBPI = 2;  // blocks per wave iteration
+constexpr int kSweepBlocks = 8;  // host partition lengths are multiples of 8 blocks (128 tokens)
 constexpr float kLog2e = 1.4426950408889634f;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// v_dot2c_f32_bf16: c + a.lo * b.lo + a.hi * b.hi (bf16 products are exact in fp32)
+__device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), c, false);
+}
+// round-to-nearest-even for finite values (softmax weights are in [0, 1])
+__device__ __forceinline__ uint32_t f2bf_rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
 
 // DPP helpers (gfx9 encodings): quad_perm xor1 = 0xB1, xor2 = 0x4E, row_half_mirror = 0x141,
 // row_mirror = 0x140, row_ror:8 = 0x128.
@@ -76,6 +88,9 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ kv, long block_stride,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens, int Hkv,
     float scale, int part_len) {
+  // blocks per wave iteration: 2 at D = 64; 1 at D = 128, where a block is already 4 KiB per lane-set
+  // and a second prefetched block would cost 64 more VGPRs
+  constexpr int kBPI = D <= 64 ? 2 : 1;
   constexpr int LPT = D / 8;        // lanes per token in the K layout
   constexpr int TPI = 64 / LPT;     // tokens per K wave-instruction
   constexpr int KV = D / 32;        // 16-byte vectors per lane per block (K and V alike)
@@ -94,12 +109,12 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   const int Hq = Hkv * G;
   const int j = lane % LPT;  // dim chunk of this lane in K; head it exponentiates
 
-  __shared__ __attribute__((aligned(16))) float p_s[kWaves][G][TOK];
+  __shared__ __attribute__((aligned(16))) bf16_t p_s[kWaves][G][TOK];
   __shared__ float red_m[kWaves][G], red_l[kWaves][G];
   __shared__ __attribute__((aligned(16))) float red_o[kWaves][G][D];
 
-  // q for this lane's 8 dims, all G heads, pre-scaled for exp2
-  float qr[G][8];
+  // q for this lane's 8 dims, all G heads, pre-scaled for exp2, as bf16 pairs for v_dot2
+  uint32_t qr[G][4];
   {
     const float qs = scale * kLog2e;
 #pragma unroll
@@ -107,10 +122,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
       const uint4 v = *reinterpret_cast<const uint4*>(q + (static_cast<size_t>(seq) * Hq + kvh * G + g) * D + 8 * j);
       const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        qr[g][2 * k] = bf2f_lo(w[k]) * qs;
-        qr[g][2 * k + 1] = bf2f_hi(w[k]) * qs;
-      }
+      for (int k = 0; k < 4; ++k) qr[g][k] = f2bf_rne(bf2f_lo(w[k]) * qs) | (f2bf_rne(bf2f_hi(w[k]) * qs) << 16);
     }
   }
   const int* btp = block_tables + static_cast<size_t>(seq) * bt_stride;
@@ -138,12 +150,14 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
       const int bi = (it * kWaves + wid) * kBPI + b;
       if (bi < nblk) {
         const long off = static_cast<long>(btp[blk0 + bi]) * bstride_bytes;
-        const uint4* kp = reinterpret_cast<const uint4*>(kbase + off);
-        const uint4* vp = reinterpret_cast<const uint4*>(vbase + off);
+        const u32x4* kp = reinterpret_cast<const u32x4*>(kbase + off);
+        const u32x4* vp = reinterpret_cast<const u32x4*>(vbase + off);
+        // KV bytes are read once per step: non-temporal loads keep them from evicting the
+        // weights / block tables from L2 (MI355X_MICROARCH nt-weights: 5-10 % per decode layer)
 #pragma unroll
         for (int i = 0; i < KV; ++i) {
-          kd[b][i] = kp[lane + 64 * i];
-          vd[b][i] = vp[lane + 64 * i];
+          kd[b][i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(kp + lane + 64 * i));
+          vd[b][i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(vp + lane + 64 * i));
         }
       }
     }
@@ -162,17 +176,11 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
 #pragma unroll
         for (int i = 0; i < KV; ++i) {
           const uint32_t* w = reinterpret_cast<const uint32_t*>(&kr[b][i]);
-          float kf[8];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            kf[2 * k] = bf2f_lo(w[k]);
-            kf[2 * k + 1] = bf2f_hi(w[k]);
-          }
 #pragma unroll
           for (int g = 0; g < G; ++g) {
             float a = 0.f;
 #pragma unroll
-            for (int d = 0; d < 8; ++d) a += qr[g][d] * kf[d];
+            for (int k = 0; k < 4; ++k) a = dot2(w[k], qr[g][k], a);
             s[b * KV + i][g] = token_sum<LPT>(a);
           }
         }
@@ -214,9 +222,9 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
 #pragma unroll
           for (int g = 1; g < G; ++g)
             if (j == g) sv = s[t][g];
-          const float p = exp2f(sv - mj);
-          ps += p;
-          p_s[wid][j][(t / KV) * kBS + (lane + 64 * (t % KV)) / LPT] = p;
+          const uint32_t pb = f2bf_rne(exp2f(sv - mj));
+          ps += __uint_as_float(pb << 16);  // the row sum sees exactly the weights P*V uses
+          p_s[wid][j][(t / KV) * kBS + (lane + 64 * (t % KV)) / LPT] = static_cast<bf16_t>(pb);
         }
         // each token is held by one lane per head, so ps counts every token once
         lsum = lsum * aj + ps;
@@ -226,34 +234,25 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
       for (int b = 0; b < kBPI; ++b) {
         const int tb = tok0 + b * kBS;
         if (tb < end) {
-          float pv[G][8];
+          uint4 pv[G];  // 8 bf16 weights: tokens 8 (lane % 2) .. +7 of block b, per head
 #pragma unroll
-          for (int g = 0; g < G; ++g) {
-            const float4_ a = *reinterpret_cast<const float4_*>(&p_s[wid][g][b * kBS + 8 * (lane & 1)]);
-            const float4_ c = *reinterpret_cast<const float4_*>(&p_s[wid][g][b * kBS + 8 * (lane & 1) + 4]);
-            pv[g][0] = a[0]; pv[g][1] = a[1]; pv[g][2] = a[2]; pv[g][3] = a[3];
-            pv[g][4] = c[0]; pv[g][5] = c[1]; pv[g][6] = c[2]; pv[g][7] = c[3];
-          }
+          for (int g = 0; g < G; ++g) pv[g] = *reinterpret_cast<const uint4*>(&p_s[wid][g][b * kBS + 8 * (lane & 1)]);
           const bool full = tb + kBS <= end;
 #pragma unroll
           for (int i = 0; i < KV; ++i) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(&vr[b][i]);
-            float vf[8];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              vf[2 * k] = bf2f_lo(w[k]);
-              vf[2 * k + 1] = bf2f_hi(w[k]);
-            }
-            if (!full) {
+            uint32_t vw[4] = {vr[b][i].x, vr[b][i].y, vr[b][i].z, vr[b][i].w};
+            if (!full) {  // never let unwritten cache bytes (possibly NaN) reach the sum
 #pragma unroll
               for (int u = 0; u < 8; ++u)
-                if (tb + 8 * (lane & 1) + u >= end) vf[u] = 0.f;  // never touch unwritten cache bytes
+                if (tb + 8 * (lane & 1) + u >= end) vw[u / 2] &= (u & 1) ? 0x0000FFFFu : 0xFFFF0000u;
             }
 #pragma unroll
             for (int g = 0; g < G; ++g) {
               float a = acc[g][i];
-#pragma unroll
-              for (int u = 0; u < 8; ++u) a += pv[g][u] * vf[u];
+              a = dot2(vw[0], pv[g].x, a);
+              a = dot2(vw[1], pv[g].y, a);
+              a = dot2(vw[2], pv[g].z, a);
+              a = dot2(vw[3], pv[g].w, a);
               acc[g][i] = a;
             }
           }
@@ -343,10 +342,10 @@ __global__ void __launch_bounds__(D) paged_decode_reduce_kernel(bf16_t* __restri
 }
 
 // Partition plan: enough workgroups to fill 256 CUs ~8 deep, partitions as long as possible, a
-// multiple of one full wave sweep (kWaves * kBPI blocks = 128 tokens).
+// multiple of one full wave sweep (kWaves * kBPI blocks <= 8 blocks = 128 tokens).
 void decode_plan(int B, int Hkv, int max_seq_len, int* P, int* part_len) {
   const int target = 2048;
-  const int sweep = kWaves * kBPI * kBS;
+  const int sweep = kSweepBlocks * kBS;
   int p = (target + B * Hkv - 1) / (B * Hkv);
   const int max_p = (max_seq_len + 255) / 256;  // never below 256 tokens per partition
   if (p > max_p) p = max_p;
