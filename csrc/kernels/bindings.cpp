@@ -19,8 +19,8 @@ void launch_paged_decode(bf16_t*, float*, float*, const bf16_t*, const bf16_t*, 
                          int, int, int, int, int, int, float, hipStream_t);
 void launch_paged_prefill(bf16_t*, const bf16_t*, const bf16_t*, long, const int*, int, const int*, const int*,
                           int, int, int, int, int, float, hipStream_t);
-void launch_sample(int64_t*, const float*, int, int, long, const float*, const float*, const int*, const int64_t*,
-                   const int64_t*, hipStream_t);
+void launch_sample(int64_t*, const void*, bool, int, int, long, const float*, const float*, const int*,
+                   const int64_t*, const int64_t*, hipStream_t);
 void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStream_t);
 void launch_moe_align(int*, int*, const int*, int, int, int, hipStream_t);
 bool launch_skinny_gemm(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, hipStream_t);
@@ -126,11 +126,13 @@ void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Te
 void sample(at::Tensor out, at::Tensor logits, at::Tensor temperature, at::Tensor top_p, at::Tensor top_k,
             at::Tensor seeds, at::Tensor steps) {
   CHECK_CUDA(logits);
-  TORCH_CHECK(logits.scalar_type() == at::kFloat && logits.stride(1) == 1, "logits must be fp32 rows");
+  TORCH_CHECK((logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16) && logits.stride(1) == 1,
+              "logits must be fp32 or bf16 rows");
   TORCH_CHECK(temperature.scalar_type() == at::kFloat && top_p.scalar_type() == at::kFloat, "fp32 params");
   TORCH_CHECK(top_k.scalar_type() == at::kInt && seeds.scalar_type() == at::kLong && steps.scalar_type() == at::kLong,
               "int params");
-  mxs::launch_sample(out.data_ptr<int64_t>(), logits.data_ptr<float>(), logits.size(0), logits.size(1),
+  mxs::launch_sample(out.data_ptr<int64_t>(), logits.data_ptr(), logits.scalar_type() == at::kBFloat16,
+                     logits.size(0), logits.size(1),
                      logits.stride(0), temperature.data_ptr<float>(), top_p.data_ptr<float>(),
                      top_k.data_ptr<int>(), seeds.data_ptr<int64_t>(), steps.data_ptr<int64_t>(), stream());
 }

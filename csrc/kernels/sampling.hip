@@ -44,7 +44,32 @@ __device__ ArgMax block_argmax(ArgMax a, float* sv, int* si) {
   return r;
 }
 
-__global__ void __launch_bounds__(1024) sample_kernel(int64_t* __restrict__ out, const float* __restrict__ logits,
+__device__ __forceinline__ float ld(const float* p, int v) { return p[v]; }
+__device__ __forceinline__ float ld(const bf16_t* p, int v) { return bf2f(p[v]); }
+
+// 8 consecutive logits starting at v (v % 8 == 0, row 16-byte aligned)
+__device__ __forceinline__ void ld8(const bf16_t* p, int v, float (&o)[8]) {
+  const uint4 w = *reinterpret_cast<const uint4*>(p + v);
+  const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    o[2 * k] = bf2f_lo(u[k]);
+    o[2 * k + 1] = bf2f_hi(u[k]);
+  }
+}
+__device__ __forceinline__ void ld8(const float* p, int v, float (&o)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p + v), b = *reinterpret_cast<const float4*>(p + v + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
+__device__ __forceinline__ float gumbel(uint32_t key, int v) {
+  const uint32_t h = hash_u32(key ^ hash_u32(static_cast<uint32_t>(v) + 0x632BE5ABu));
+  const float u = (static_cast<float>(h >> 8) + 0.5f) * (1.f / 16777216.f);
+  return -logf(-logf(u));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(1024) sample_kernel(int64_t* __restrict__ out, const T* __restrict__ logits,
                                                       int V, long row_stride, const float* __restrict__ temperature,
                                                       const float* __restrict__ top_p, const int* __restrict__ top_k,
                                                       const int64_t* __restrict__ seeds,
@@ -52,11 +77,22 @@ __global__ void __launch_bounds__(1024) sample_kernel(int64_t* __restrict__ out,
   __shared__ float sv[16];
   __shared__ int si[16];
   const int row = blockIdx.x;
-  const float* z = logits + row * row_stride;
+  const T* z = logits + row * row_stride;
   const float t = temperature[row];
+  // vectorised single pass when rows are 16-byte aligned (every vocab in the registry)
+  const bool vec = (V % 8 == 0) && (row_stride % 8 == 0) && ((reinterpret_cast<uintptr_t>(logits) & 15) == 0);
   if (!(t > 0.f)) {
     ArgMax a{-INFINITY, 0x7FFFFFFF};
-    for (int v = threadIdx.x; v < V; v += blockDim.x) a = better(a, ArgMax{z[v], v});
+    if (vec) {
+      for (int v = 8 * threadIdx.x; v < V; v += 8 * blockDim.x) {
+        float x[8];
+        ld8(z, v, x);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a = better(a, ArgMax{x[u], v + u});
+      }
+    } else {
+      for (int v = threadIdx.x; v < V; v += blockDim.x) a = better(a, ArgMax{ld(z, v), v});
+    }
     ArgMax r = block_argmax(a, sv, si);
     if (threadIdx.x == 0) out[row] = r.i;
     return;
@@ -68,8 +104,8 @@ __global__ void __launch_bounds__(1024) sample_kernel(int64_t* __restrict__ out,
   if ((k > 0 && k < V) || p < 1.f) {
     float mx = -INFINITY, mn = INFINITY;
     for (int v = threadIdx.x; v < V; v += blockDim.x) {
-      mx = fmaxf(mx, z[v]);
-      mn = fminf(mn, z[v]);
+      mx = fmaxf(mx, ld(z, v));
+      mn = fminf(mn, ld(z, v));
     }
     mx = block_max(mx, sv);
     mn = -block_max(-mn, sv);
@@ -78,7 +114,7 @@ __global__ void __launch_bounds__(1024) sample_kernel(int64_t* __restrict__ out,
       for (int it = 0; it < 32; ++it) {
         const float mid = 0.5f * (lo + hi);
         float cnt = 0.f;
-        for (int v = threadIdx.x; v < V; v += blockDim.x) cnt += z[v] >= mid ? 1.f : 0.f;
+        for (int v = threadIdx.x; v < V; v += blockDim.x) cnt += ld(z, v) >= mid ? 1.f : 0.f;
         cnt = block_sum(cnt, sv);
         if (cnt >= static_cast<float>(k)) lo = mid; else hi = mid;
       }
@@ -86,14 +122,16 @@ __global__ void __launch_bounds__(1024) sample_kernel(int64_t* __restrict__ out,
     }
     if (p < 1.f) {  // largest tau with mass(z >= tau) >= p * total, mass in softmax(z / T)
       float tot = 0.f;
-      for (int v = threadIdx.x; v < V; v += blockDim.x) tot += __expf((z[v] - mx) * invt);
+      for (int v = threadIdx.x; v < V; v += blockDim.x) tot += __expf((ld(z, v) - mx) * invt);
       tot = block_sum(tot, sv);
       float lo = fmaxf(mn, mx - 88.f * t), hi = mx;
       for (int it = 0; it < 32; ++it) {
         const float mid = 0.5f * (lo + hi);
         float mass = 0.f;
-        for (int v = threadIdx.x; v < V; v += blockDim.x)
-          mass += z[v] >= mid ? __expf((z[v] - mx) * invt) : 0.f;
+        for (int v = threadIdx.x; v < V; v += blockDim.x) {
+          const float zv = ld(z, v);
+          mass += zv >= mid ? __expf((zv - mx) * invt) : 0.f;
+        }
         mass = block_sum(mass, sv);
         if (mass >= p * tot) lo = mid; else hi = mid;
       }
@@ -103,24 +141,34 @@ __global__ void __launch_bounds__(1024) sample_kernel(int64_t* __restrict__ out,
   const uint32_t key = hash_u32(static_cast<uint32_t>(static_cast<uint64_t>(seeds[row]) * 0x9E3779B1ull +
                                                       static_cast<uint64_t>(steps[row])));
   ArgMax a{-INFINITY, 0x7FFFFFFF};
-  for (int v = threadIdx.x; v < V; v += blockDim.x) {
-    const float zv = z[v];
-    if (zv < thr) continue;
-    const uint32_t h = hash_u32(key ^ hash_u32(static_cast<uint32_t>(v) + 0x632BE5ABu));
-    const float u = (static_cast<float>(h >> 8) + 0.5f) * (1.f / 16777216.f);
-    const float g = -logf(-logf(u));
-    a = better(a, ArgMax{zv * invt + g, v});
+  if (vec) {
+    for (int v = 8 * threadIdx.x; v < V; v += 8 * blockDim.x) {
+      float x[8];
+      ld8(z, v, x);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (x[u] >= thr) a = better(a, ArgMax{x[u] * invt + gumbel(key, v + u), v + u});
+    }
+  } else {
+    for (int v = threadIdx.x; v < V; v += blockDim.x) {
+      const float zv = ld(z, v);
+      if (zv >= thr) a = better(a, ArgMax{zv * invt + gumbel(key, v), v});
+    }
   }
   ArgMax r = block_argmax(a, sv, si);
   if (threadIdx.x == 0) out[row] = r.i;
 }
 
-void launch_sample(int64_t* out, const float* logits, int B, int V, long row_stride, const float* temperature,
-                   const float* top_p, const int* top_k, const int64_t* seeds, const int64_t* steps,
-                   hipStream_t s) {
+void launch_sample(int64_t* out, const void* logits, bool bf16, int B, int V, long row_stride,
+                   const float* temperature, const float* top_p, const int* top_k, const int64_t* seeds,
+                   const int64_t* steps, hipStream_t s) {
   if (B == 0) return;
-  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(1024), 0, s, out, logits, V, row_stride, temperature, top_p,
-                     top_k, seeds, steps);
+  if (bf16)
+    hipLaunchKernelGGL(sample_kernel<bf16_t>, dim3(B), dim3(1024), 0, s, out, static_cast<const bf16_t*>(logits), V,
+                       row_stride, temperature, top_p, top_k, seeds, steps);
+  else
+    hipLaunchKernelGGL(sample_kernel<float>, dim3(B), dim3(1024), 0, s, out, static_cast<const float*>(logits), V,
+                       row_stride, temperature, top_p, top_k, seeds, steps);
   MXS_CHECK_LAUNCH();
 }
 

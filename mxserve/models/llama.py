@@ -216,7 +216,8 @@ class TransformerLM:
         return h.index_select(0, md.logits_indices)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        logits = ops.linear(hidden, self.lm_head_weight()).float()
+        # bf16 on the GPU: the sampling kernel reads bf16 rows directly (no fp32 copy of [B, V])
+        logits = ops.linear(hidden, self.lm_head_weight())
         if self.tp_size > 1:
             logits = tp_all_gather(logits, dim=-1)
         return logits[:, :self.cfg.vocab_size]

@@ -149,9 +149,10 @@ def test_prefill_softmax_rescale_spike(gpu):
     _close(out, exp, 0.03, 0.03, "prefill-spike")
 
 
-def test_sample_greedy(gpu):
-    B, V = 16, 128256
-    logits = torch.randn(B, V, device=gpu)
+@pytest.mark.parametrize("dtype,V", [(torch.float32, 128256), (torch.bfloat16, 128256), (torch.bfloat16, 1001)])
+def test_sample_greedy(gpu, dtype, V):
+    B = 16
+    logits = torch.randn(B, V, device=gpu).to(dtype)
     logits[3, 77] = 50.0
     z = torch.zeros(B, device=gpu)
     ids = ops.sample(logits, z, torch.ones(B, device=gpu), torch.zeros(B, dtype=torch.int32, device=gpu),
@@ -160,10 +161,11 @@ def test_sample_greedy(gpu):
     assert int(ids[3]) == 77
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("top_p,top_k", [(1.0, 0), (0.9, 0), (1.0, 50), (0.8, 20)])
-def test_sample_matches_reference(gpu, top_p, top_k):
+def test_sample_matches_reference(gpu, top_p, top_k, dtype):
     B, V = 24, 32000
-    logits = torch.randn(B, V, device=gpu) * 3
+    logits = (torch.randn(B, V, device=gpu) * 3).to(dtype)
     t = torch.full((B,), 0.7, device=gpu)
     tp = torch.full((B,), top_p, device=gpu)
     tk = torch.full((B,), top_k, dtype=torch.int32, device=gpu)
@@ -190,7 +192,10 @@ def test_sample_distribution(gpu):
 
 def test_moe_topk_softmax(gpu):
     T, E, K = 100, 8, 2
-    logits = torch.randn(T, E, device=gpu, dtype=torch.bfloat16)
+    g = torch.Generator().manual_seed(0)
+    # distinct values per row (random bf16 logits tie often, and tie order is not part of the contract)
+    logits = (torch.stack([torch.randperm(E, generator=g) for _ in range(T)]).float() * 0.37 - 1.2)
+    logits = logits.to(device=gpu, dtype=torch.bfloat16)
     w, ids = ops.moe_topk_softmax(logits, K)
     ew, eids = ref.moe_topk_softmax(logits.cpu(), K)
     assert torch.equal(ids.cpu(), eids)
