@@ -33,10 +33,18 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
   constexpr int KS = D / 16;   // k-steps of the QK^T product
   constexpr int DT = D / 32;   // 32-row output tiles of O^T
   constexpr int BQ = 128 / G;  // query tokens per workgroup
-  const int kvh = blockIdx.y, seq = blockIdx.z;
+  // XCD-aware order: the hardware deals workgroups round-robin over the 8 XCDs, which would spread
+  // every (sequence, kv head)'s query tiles over all eight L2s and make each L2 stream the K/V of
+  // every head.  Remap so consecutive virtual ids run on one XCD: all query tiles of a (seq, kv head)
+  // share one L2, which then holds just that head's K/V.
+  const int NT = gridDim.x, total = NT * gridDim.y * gridDim.z;
+  const int lin = blockIdx.x + NT * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int v = (total % 8 == 0) ? (lin % 8) * (total / 8) + lin / 8 : lin;
+  const int pair = v / NT;
+  const int kvh = pair % gridDim.y, seq = pair / gridDim.y;
   const int q0 = qsl[seq];
   const int ql = qsl[seq + 1] - q0;
-  const int tile = gridDim.x - 1 - blockIdx.x;  // heaviest (latest) tiles first
+  const int tile = NT - 1 - (v - pair * NT);  // heaviest (latest) tiles first
   const int t0 = tile * BQ;
   if (t0 >= ql) return;
   const int L = seq_lens[seq];
@@ -83,19 +91,25 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
   const int wave_tok0 = t0 + (wid * 32) / G;
   const int wave_min_pos = ctx0 + min(wave_tok0, ql - 1);
 
-  // software pipeline: tile k0 + 32 is loaded while tile k0 is computed
+  // software pipeline: tile k0 + 32 is loaded while tile k0 is computed.  A 32-key tile spans two
+  // cache blocks whose ids are wave-uniform scalar loads (SMEM, lgkmcnt), fetched one tile further
+  // ahead still: a per-lane block-table gather would be a VMEM load the K/V addresses depend on, and
+  // vmcnt's in-order accounting would then make every iteration wait for the loads just issued.
   uint4 kf[KS];
   uint2 vf[DT][2][2];
-  auto load_tile = [&](int k0, uint4 (&kd)[KS], uint2 (&vd)[DT][2][2]) {
-    const int key = k0 + c;
-    const int kblk = bt[min(key, L - 1) / kPBS];
-    const bf16_t* kp = kv + kblk * block_stride + k_head_off + static_cast<size_t>(key % kPBS) * D + 8 * h;
+  auto tile_blocks = [&](int k0, int& b0, int& b1) {
+    b0 = bt[min(k0, L - 1) / kPBS];
+    b1 = bt[min(k0 + 16, L - 1) / kPBS];
+  };
+  auto load_tile = [&](int b0, int b1, uint4 (&kd)[KS], uint2 (&vd)[DT][2][2]) {
+    // keys past L read (and later mask) valid bytes of the last block
+    const int kblk = c < 16 ? b0 : b1;
+    const bf16_t* kp = kv + kblk * block_stride + k_head_off + static_cast<size_t>(c & 15) * D + 8 * h;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) kd[ks] = *reinterpret_cast<const uint4*>(kp + 16 * ks);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int kb = min(k0 + 16 * s, L - 1) / kPBS;
-      const bf16_t* vp = kv + bt[kb] * block_stride + v_head_off + 4 * h;
+      const bf16_t* vp = kv + (s ? b1 : b0) * block_stride + v_head_off + 4 * h;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const bf16_t* vr = vp + static_cast<size_t>(32 * dt + c) * kPBS;
@@ -104,24 +118,20 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
       }
     }
   };
-  load_tile(0, kf, vf);
+  int cb0, cb1, nb0, nb1;
+  tile_blocks(0, cb0, cb1);
+  tile_blocks(32, nb0, nb1);
+  load_tile(cb0, cb1, kf, vf);
 
-  for (int k0 = 0; k0 < nkeys; k0 += 32) {
-    uint4 kn[KS];
-    uint2 vn[DT][2][2];
-    // D = 128 would exceed the 256-VGPR budget with a second tile in flight: load in place instead
-    constexpr bool kPipe = D <= 64;
-    const bool more = kPipe && k0 + 32 < nkeys;
-    if (more) load_tile(k0 + 32, kn, vn);
-    if (!kPipe && k0 > 0) load_tile(k0, kf, vf);
-    // ---- S^T = K Q^T
+  // One 32-key tile: S^T = K Q^T, causal mask, online softmax, O^T += V^T P^T.
+  auto compute = [&](int k0, uint4 (&kt)[KS], uint2 (&vt)[DT][2][2]) {
     float16_ sacc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) sacc[i] = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
-      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[ks]), qf[ks], sacc, 0, 0, 0);
-    // ---- causal mask only on tiles that cross the diagonal of some row of this wave
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kt[ks]), qf[ks], sacc, 0, 0, 0);
+    // causal mask only on tiles that cross the diagonal of some row of this wave
     if (k0 + 31 > wave_min_pos) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -129,27 +139,34 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
         if (kk > qpos) sacc[i] = -INFINITY;
       }
     }
-    // ---- online softmax (row = lane c, keys split across the two lane halves)
+    // online softmax (row = lane c, keys split across the two lane halves).  Lazy rescale: the
+    // running max only moves (and O, l are rescaled) when a tile raises it by more than 2^8, so
+    // most tiles skip the D/2 multiplies; both halves of a row see the same max, hence the same
+    // decision, and p <= 2^8 stays well inside bf16 / fp32 range.
     float mx = sacc[0];
 #pragma unroll
     for (int i = 1; i < 16; ++i) mx = fmaxf(mx, sacc[i]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = __builtin_amdgcn_exp2f(m - mn);
-    m = mn;
+    const bool bump = mx > m + 8.f;
+    if (__ballot(bump)) {
+      const float mn = bump ? mx : m;
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);  // 0 on the first tile (m = -inf)
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+    }
     float ps = 0.f;
     bf16x8_t pf[2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float p = __builtin_amdgcn_exp2f(sacc[i] - mn);
+      const float p = __builtin_amdgcn_exp2f(sacc[i] - m);
       ps += p;
       pf[i >> 3][i & 7] = static_cast<__bf16>(p);
     }
-    l = l * alpha + ps;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+    l += ps;
     // keys >= L in the last tile: zero V so uninitialised cache bytes never reach the sum
     if (k0 + 32 > L) {
 #pragma unroll
@@ -159,7 +176,7 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
           const int kbase = k0 + 16 * s + 8 * half + 4 * h;
 #pragma unroll
           for (int dt = 0; dt < DT; ++dt) {
-            uint32_t* w = reinterpret_cast<uint32_t*>(&vf[dt][s][half]);
+            uint32_t* w = reinterpret_cast<uint32_t*>(&vt[dt][s][half]);
             if (kbase + 0 >= L) w[0] &= 0xFFFF0000u;
             if (kbase + 1 >= L) w[0] &= 0x0000FFFFu;
             if (kbase + 2 >= L) w[1] &= 0xFFFF0000u;
@@ -167,24 +184,44 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
           }
         }
     }
-    // ---- O^T += V^T P^T
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        const uint4 a = make_uint4(vf[dt][s][0].x, vf[dt][s][0].y, vf[dt][s][1].x, vf[dt][s][1].y);
+        const uint4 a = make_uint4(vt[dt][s][0].x, vt[dt][s][0].y, vt[dt][s][1].x, vt[dt][s][1].y);
         o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), pf[s], o[dt], 0, 0, 0);
       }
-    if (more) {
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) kf[ks] = kn[ks];
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          vf[dt][s][0] = vn[dt][s][0];
-          vf[dt][s][1] = vn[dt][s][1];
-        }
+  };
+
+  if constexpr (D <= 64) {
+    // two register sets in ping-pong: tile k0 computes from one while k0 + 32 lands in the other
+    // (no register copies between iterations)
+    uint4 kb[KS];
+    uint2 vb[DT][2][2];
+    for (int k0 = 0;;) {
+      bool more = k0 + 32 < nkeys;
+      if (more) {
+        load_tile(nb0, nb1, kb, vb);
+        tile_blocks(k0 + 64, nb0, nb1);
+      }
+      compute(k0, kf, vf);
+      if (!more) break;
+      k0 += 32;
+      more = k0 + 32 < nkeys;
+      if (more) {
+        load_tile(nb0, nb1, kf, vf);
+        tile_blocks(k0 + 64, nb0, nb1);
+      }
+      compute(k0, kb, vb);
+      if (!more) break;
+      k0 += 32;
+    }
+  } else {
+    // D = 128: a second tile in flight would exceed the 256-VGPR budget; load in place
+    for (int k0 = 0; k0 < nkeys; k0 += 32) {
+      if (k0 > 0) load_tile(cb0, cb1, kf, vf);
+      tile_blocks(k0 + 32, cb0, cb1);
+      compute(k0, kf, vf);
     }
   }
 
