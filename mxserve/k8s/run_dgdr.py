@@ -1,5 +1,6 @@
 """Implementation of examples/dgdr/trtllm/run-dgdr.sh (reference run-dgdr.sh:4-54): create the
-namespace, (re)create ConfigMap CONFIGMAP_NAME from DISAGG_FILE (key = its file name), apply
+namespace, (re)create ConfigMap CONFIGMAP_NAME from DISAGG_FILE (under the key the DGDR's
+configMapRef names, so DISAGG_FILE=disagg_cache.yaml still lands where the request looks), apply
 DGDR_FILE, wait for the generated graph's frontend Service and expose it on FRONTEND_NODEPORT."""
 from __future__ import annotations
 
@@ -24,12 +25,14 @@ def main(k: KubeClient | None = None) -> int:
     k = k or (KubeClient(e["MXS_KUBE_SERVER"]) if e.get("MXS_KUBE_SERVER") else KubeClient())
     if k.get("Namespace", ns) is None:
         k.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
-    with open(disagg) as f:
-        k.apply({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": cm_name, "namespace": ns},
-                 "data": {os.path.basename(disagg): f.read()}})
-    print(f"==> ConfigMap {cm_name} updated from {disagg}")
     with open(dgdr_file) as f:
         req = yaml.safe_load(f)
+    ref = (((req.get("spec") or {}).get("profilingConfig") or {}).get("configMapRef") or {})
+    key = ref.get("key") or os.path.basename(disagg)
+    with open(disagg) as f:
+        k.apply({"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": cm_name, "namespace": ns},
+                 "data": {key: f.read()}})
+    print(f"==> ConfigMap {cm_name} updated from {disagg} (key {key})")
     req["metadata"]["namespace"] = ns
     k.apply(req)
     print(f"==> applied {dgdr_file}; waiting for the generated frontend Service")

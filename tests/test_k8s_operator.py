@@ -150,3 +150,37 @@ def test_reconcile_dgdr_autoapply(cluster):
     op.reconcile_all()  # second pass reconciles the generated DGD into deployments
     names = {d["metadata"]["name"] for d in fake.objects("deployments", ns)}
     assert "trtllm-disagg-trtllmprefillworker" in names and "trtllm-disagg-frontend" in names
+
+
+def test_grafana_dashboard_is_generated_and_uses_exported_metrics():
+    """R17: the committed ConfigMap is exactly the generator's output, and every dynamo_* series a
+    panel queries is one the frontend / worker actually export."""
+    import io
+    import json
+    import re
+    import sys as _sys
+    from pathlib import Path
+
+    import yaml
+
+    from mxserve.frontend import metrics as mx_metrics
+    from mxserve.k8s import dashboard
+
+    buf = io.StringIO()
+    old = _sys.stdout
+    _sys.stdout = buf
+    try:
+        dashboard.main()
+    finally:
+        _sys.stdout = old
+    path = Path(__file__).resolve().parents[1] / "examples/dgdr/trtllm/grafana-dynamo-dashboard-configmap.yaml"
+    assert path.read_text() == buf.getvalue(), "regenerate with python -m mxserve.k8s.dashboard"
+    cm = yaml.safe_load(path.read_text())
+    assert cm["metadata"]["labels"] == {"grafana_dashboard": "1"} and cm["metadata"]["namespace"] == "monitoring"
+    d = json.loads(cm["data"]["mxserve-dashboard.json"])
+    exprs = " ".join(t["expr"] for p in d["panels"] for t in p["targets"])
+    used = set(re.findall(r"dynamo_[a-z_]+", exprs))
+    src = Path(mx_metrics.__file__).read_text()
+    exported = set(re.findall(r'"(dynamo_[a-z_]+)"', src))
+    base = {re.sub(r"_(sum|count|bucket|total)$", "", u) for u in used}
+    assert base <= exported, sorted(base - exported)
