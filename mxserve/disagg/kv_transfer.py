@@ -1,19 +1,30 @@
 """KV transfer agent for disaggregated prefill -> decode (replaces NIXL).
 
 Backends
-  xgmi  the decode worker exports its block-major KV pool once (hipIpcGetMemHandle of the pool's
-        allocation + offset); the prefill worker opens it (hipIpcOpenMemHandle, lazy peer access)
-        and pushes a request's blocks with ONE copy kernel on a side stream: stores travel over
-        xGMI straight into the decode GPU's HBM (or stay on-chip when both workers share a GPU).
+  xgmi  the decode worker owns a STAGING ARENA of KV blocks (4 GiB by default: 8,192 Llama-3.2-1B
+        blocks, i.e. 32 concurrent 4k-token prompts) allocated once and exported with
+        hipIpcGetMemHandle; the prefill worker maps it once (hipIpcOpenMemHandle, lazy peer
+        access).  Per request:
+          decode   reserve a contiguous extent of the arena, send its offset with the request;
+          prefill  ONE copy kernel writes the request's blocks into that extent -- the stores travel
+                   over xGMI into the decode GPU's HBM (or stay on-chip when both share a GPU);
+          decode   ONE copy kernel on its compute stream scatters extent -> the reserved pool blocks
+                   (ordered before the next step); the extent is recycled once that copy is done.
+        Why an arena and not the pool itself: on this ROCm 7.2 / dmabuf-IPC stack hipIpcOpenMemHandle
+        never returns for an allocation whose size mod 4 GiB lies in [2 GiB, 4 GiB) (measured with
+        scripts/ipc_probe.py: 0.5, 1, 1.5, 4, 4.5, 8, 12, 16 GiB map in ~2 ms; 2, 2.5, 3, 6 and a
+        19.5 GiB serving pool hang), so the exported allocation is a fixed, IPC-safe size rather
+        than whatever the pool happens to be; the extra on-GPU scatter costs ~30-60 us per
+        4000-token prompt.
   host  staged through host memory over the control plane (CPU backend, or GPUs without a shared
         IPC namespace): the prefill side ships the block bytes, the decode side writes them.
-Block layout is identical on both sides ([L, 2, Hkv, 16, D] per block), so a transfer is a list of
-(src_block, dst_block) pairs.
+Block layout is identical on both sides ([L, 2, Hkv, 16, D] per block).
 """
 from __future__ import annotations
 
 import base64
 import logging
+import math
 import os
 import threading
 import time
@@ -24,9 +35,23 @@ import torch
 
 log = logging.getLogger(__name__)
 
+STAGING_BYTES = int(os.environ.get("MXS_KV_STAGING_BYTES", str(4 << 30)))
+_GIB = 1 << 30
+
+
+def ipc_safe_blocks(k: int, block_bytes: int) -> int:
+    """Largest count <= k of block_bytes-sized blocks whose allocation -- rounded up to the caching
+    allocator's 2 MiB granule -- keeps (size mod 4 GiB) below 2 GiB (see the module docstring)."""
+    lim = 2 * _GIB - (2 << 20)
+    r = (k * block_bytes) % (4 * _GIB)
+    if r <= lim:
+        return k
+    base = k * block_bytes - r  # start of this 4 GiB window
+    return max(1, (base + lim) // block_bytes)
+
 
 class KVTransferAgent:
-    def __init__(self, runner, backend: str = "xgmi"):
+    def __init__(self, runner, backend: str = "xgmi", max_prompt_tokens: Optional[int] = None):
         self.runner = runner
         self.kv = runner.kv_cache
         self.block_bytes = runner.block_bytes
@@ -37,18 +62,98 @@ class KVTransferAgent:
         self._opened: dict[str, int] = {}
         self.bytes_moved = 0
         self.transfers = 0
+        # staging arena (decode side, allocated lazily by the first descriptor() call): at least one
+        # max-length prompt, at most STAGING_BYTES
+        bs = getattr(getattr(runner, "args", None), "block_size", 16)
+        mtok = max_prompt_tokens or getattr(getattr(runner, "args", None), "max_model_len", 8192)
+        bb = max(1, self.block_bytes)
+        self.arena_blocks = max(math.ceil(mtok / bs), STAGING_BYTES // bb)
+        self.arena_blocks = ipc_safe_blocks(self.arena_blocks, bb)
+        self.staging: Optional[torch.Tensor] = None
+        self._free: list[list[int]] = []  # sorted free extents [start, length]
+        self._draining: list[tuple[int, int, object]] = []  # (start, n, event) until landed
+        self._desc: Optional[dict] = None
 
     # -------------------------------------------------------------- decode side
+    def _ensure_staging(self) -> None:
+        if self.staging is not None or self.backend != "xgmi":
+            return
+        self.staging = torch.empty((self.arena_blocks,) + tuple(self.kv.shape[1:]), dtype=self.kv.dtype,
+                                   device=self.kv.device)
+        self._free = [[0, self.arena_blocks]]
+        log.info("KV staging arena: %d blocks (%.2f GB)", self.arena_blocks,
+                 self.arena_blocks * self.block_bytes / 1e9)
+
     def descriptor(self, host_url: Optional[str] = None) -> dict:
+        if self._desc is not None:
+            return dict(self._desc, url=host_url)
         d = {"backend": self.backend, "block_bytes": self.block_bytes, "pid": os.getpid(),
              "num_blocks": int(self.kv.shape[0]), "url": host_url,
              "shape": list(self.kv.shape[1:]), "dtype": str(self.kv.dtype).replace("torch.", "")}
         if self.backend == "xgmi":
             from .. import ops
-            handle, off = ops.ext().ipc_export_pool(self.kv)
-            d.update(handle=base64.b64encode(handle).decode(), offset=int(off),
-                     device=self.kv.device.index, data_ptr=int(self.kv.data_ptr()))
-        return d
+            self._ensure_staging()
+            handle, off = ops.ext().ipc_export_pool(self.staging)
+            d.update(handle=base64.b64encode(handle).decode(), offset=int(off), device=self.kv.device.index,
+                     data_ptr=int(self.staging.data_ptr()), arena_blocks=self.arena_blocks)
+        self._desc = d
+        return dict(d)
+
+    def _reclaim(self) -> None:
+        still = []
+        for start, n, ev in self._draining:
+            if ev is None or ev.query():
+                self._free_extent(start, n)
+            else:
+                still.append((start, n, ev))
+        self._draining = still
+
+    def _free_extent(self, start: int, n: int) -> None:
+        f = self._free
+        f.append([start, n])
+        f.sort()
+        merged = [f[0]]
+        for s0, n0 in f[1:]:
+            if merged[-1][0] + merged[-1][1] == s0:
+                merged[-1][1] += n0
+            else:
+                merged.append([s0, n0])
+        self._free = merged
+
+    def acquire(self, n: int) -> Optional[int]:
+        """Offset of a free extent of n arena blocks, or None (caller transfers via the host)."""
+        if self.backend != "xgmi" or n <= 0:
+            return None
+        self._ensure_staging()
+        with self._lock:
+            self._reclaim()
+            for ext in self._free:
+                if ext[1] >= n:
+                    start = ext[0]
+                    ext[0] += n
+                    ext[1] -= n
+                    if ext[1] == 0:
+                        self._free.remove(ext)
+                    return start
+            return None
+
+    def release(self, start: int, n: int, after=None) -> None:
+        """Recycle an extent; `after` (a recorded event) delays it until the landing copy is done."""
+        with self._lock:
+            self._draining.append((start, n, after))
+
+    def land(self, start: int, dst_ids: list[int]) -> None:
+        """Scatter a filled extent into the pool blocks on the CURRENT stream (call it on the engine's
+        stream so the copy is ordered before the step that reads the blocks), then recycle it."""
+        from .. import ops
+        n = len(dst_ids)
+        if n:
+            s = torch.arange(start, start + n, dtype=torch.int32).pin_memory().to(self.kv.device, non_blocking=True)
+            d = torch.tensor(dst_ids, dtype=torch.int32).pin_memory().to(self.kv.device, non_blocking=True)
+            ops.ext().copy_blocks(int(self.kv.data_ptr()), self.staging, s, d, self.block_bytes)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.release(start, n, ev)
 
     def write_blocks(self, dst_ids: list[int], payload: bytes) -> None:
         """Host backend, decode side: place shipped blocks into the pool."""
@@ -73,23 +178,35 @@ class KVTransferAgent:
                 self._opened[key] = ptr
             return ptr
 
+    def connect(self, target: dict) -> None:
+        """Map the target's staging slots ahead of the first transfer."""
+        if target.get("backend") == "xgmi" and self.backend == "xgmi":
+            self._remote_ptr(target)
+
     def read_blocks(self, src_ids: list[int]) -> bytes:
         idx = torch.tensor(src_ids, dtype=torch.long, device=self.kv.device)
         blk = self.kv.index_select(0, idx)
         return blk.cpu().contiguous().view(torch.uint8).numpy().tobytes()
 
-    def push_xgmi(self, src_ids: list[int], dst_ids: list[int], target: dict) -> float:
-        """Copy blocks into the (IPC-mapped) target pool; returns seconds spent (blocking)."""
+    def push_xgmi(self, src_ids: list[int], target: dict, start: int) -> float:
+        """Copy blocks into the target's staging arena at block offset `start` (IPC-mapped);
+        blocking, returns seconds."""
         from .. import ops
         if not src_ids:
             return 0.0
         if int(target["block_bytes"]) != self.block_bytes:
             raise ValueError("KV block layout mismatch between prefill and decode workers")
+        if start < 0 or start + len(src_ids) > int(target["arena_blocks"]):
+            raise ValueError(f"extent [{start}, +{len(src_ids)}) outside the staging arena")
         t0 = time.perf_counter()
         ptr = self._remote_ptr(target)
+        base = start
+        # the blocks were written on the compute stream: order the copy after everything queued there
+        self._stream.wait_stream(torch.cuda.current_stream(self.kv.device))
         with torch.cuda.stream(self._stream):
             s = torch.tensor(src_ids, dtype=torch.int32).pin_memory().to(self.kv.device, non_blocking=True)
-            d = torch.tensor(dst_ids, dtype=torch.int32).pin_memory().to(self.kv.device, non_blocking=True)
+            d = torch.arange(base, base + len(src_ids), dtype=torch.int32).pin_memory().to(self.kv.device,
+                                                                                         non_blocking=True)
             ops.ext().copy_blocks(ptr, self.kv, s, d, self.block_bytes)
         self._stream.synchronize()
         self.bytes_moved += len(src_ids) * self.block_bytes

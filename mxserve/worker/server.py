@@ -60,6 +60,8 @@ class Worker:
         self.model = self.args.name
         self.metrics = WorkerMetrics()
         self.agent = KVTransferAgent(self.engine.runner, self.args.kv_transfer_backend)
+        if self.role == "decode":  # allocate + export the staging arena before traffic arrives
+            self.agent.descriptor()
         self.worker_id = wargs.worker_id or f"{self.role}-{socket.gethostname()}-{uuid.uuid4().hex[:6]}"
         self.url: Optional[str] = None
         self._events_lock = threading.Lock()
@@ -125,9 +127,15 @@ class Worker:
         q = self.aeng.open_stream(rid)
         skip = req.num_cached_tokens // self.args.block_size
         nblk = -(-len(toks) // self.args.block_size)
+        dst = list(req.block_ids[skip:nblk])
         target = self.agent.descriptor(self.url)
-        target["block_ids"] = list(req.block_ids[skip:nblk])
+        # xgmi: reserve an extent of the IPC-mapped staging arena; none free -> host-staged this time
+        start = self.agent.acquire(len(dst)) if target["backend"] == "xgmi" else None
+        if start is None:
+            target["backend"] = "host"
+        target["block_ids"] = dst
         target["skip_blocks"] = skip
+        target["arena_start"] = start
         payload = {"request_id": rid, "token_ids": toks, "sampling": _sp_dict(sp), "kv_target": target}
         try:
             sess = await self.http()
@@ -135,7 +143,14 @@ class Worker:
                 if r.status != 200:
                     raise RuntimeError(f"prefill worker returned {r.status}: {await r.text()}")
                 res = await r.json()
-            out = await self.aeng.submit(self.engine.complete_remote_prefill, rid, int(res["first_token"]))
+
+            def land_and_complete(tok: int):
+                if start is not None:  # staging extent -> pool blocks, on the engine's stream
+                    self.agent.land(start, dst)
+                return self.engine.complete_remote_prefill(rid, tok)
+
+            out = await self.aeng.submit(land_and_complete, int(res["first_token"]))
+            start = None
             self.aeng.push(out)
             if "transfer_s" in res:
                 self.metrics.kv_xfer_lat.labels(self.model).observe(float(res["transfer_s"]))
@@ -143,6 +158,8 @@ class Worker:
             return q
         except Exception as e:  # noqa: BLE001 - SURVEY §5.3: fall back to local prefill
             log.warning("remote prefill failed for %s (%r); prefilling locally", rid, e)
+            if start is not None:
+                self.agent.release(start, len(dst))
             await self.aeng.submit(self.engine.abort, rid)
             self.aeng._queues.pop(rid, None)
             return None
@@ -168,8 +185,8 @@ class Worker:
             if len(src) != len(dst):
                 raise RuntimeError(f"block count mismatch: {len(src)} local vs {len(dst)} remote")
             if target["backend"] == "xgmi" and self.agent.backend == "xgmi":
-                xfer_s = await asyncio.get_running_loop().run_in_executor(None, self.agent.push_xgmi, src, dst,
-                                                                          target)
+                xfer_s = await asyncio.get_running_loop().run_in_executor(None, self.agent.push_xgmi, src, target,
+                                                                          int(target["arena_start"]))
             else:
                 t0 = time.perf_counter()
                 data = await asyncio.get_running_loop().run_in_executor(None, self.agent.read_blocks, src)

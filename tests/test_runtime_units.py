@@ -243,3 +243,38 @@ def test_sla_plan_meets_targets():
     big = plan("meta-llama/Meta-Llama-3-70B-Instruct", 2000, 256, 1000, 40)
     assert big["agg"]["tp"] >= 1 and big["feasible"]
     assert not plan("meta-llama/Meta-Llama-3-70B-Instruct", 4000, 500, 1, 1)["feasible"]
+
+
+# ----------------------------------------------------------------------------- KV transfer staging
+def test_ipc_safe_staging_sizes():
+    from mxserve.disagg.kv_transfer import ipc_safe_blocks
+    gib = 1 << 30
+    for bb in (524288, 2 << 20, 32768, 81920, 1835008):
+        for g in (0.5, 1, 2, 3, 4, 4.5, 6, 8, 19.53):
+            k = int(g * gib) // bb
+            kk = ipc_safe_blocks(k, bb)
+            alloc = -(-kk * bb // (2 << 20)) * (2 << 20)  # caching-allocator 2 MiB granule
+            assert kk <= k and alloc % (4 * gib) < 2 * gib, (bb, g)
+    assert ipc_safe_blocks(8192, 524288) == 8192  # 4 GiB exactly is safe
+
+
+def test_staging_arena_extents():
+    import torch
+    from mxserve.disagg.kv_transfer import KVTransferAgent
+
+    class R:
+        kv_cache = torch.zeros(4, 2, 2, 1, 16, 8)
+        block_bytes = kv_cache[0].numel() * 4
+
+    a = KVTransferAgent(R(), "host", max_prompt_tokens=64)
+    a.backend = "xgmi"  # exercise the arena bookkeeping without a GPU
+    a.arena_blocks = 10
+    x = a.acquire(4)
+    y = a.acquire(4)
+    assert (x, y) == (0, 4) and a.acquire(4) is None
+    a.release(x, 4)  # no event: reclaimed at the next acquire
+    assert a.acquire(3) == 0 and a.acquire(2) == 8
+    a.release(y, 4)
+    a.release(0, 3)
+    a.release(8, 2)
+    assert a.acquire(10) == 0  # all extents merged back

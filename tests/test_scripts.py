@@ -4,6 +4,7 @@ frontend; `bash -n` on every shell script."""
 import glob
 import os
 import subprocess
+import sys
 import threading
 import time
 
@@ -147,3 +148,30 @@ def test_run_benchmarks_sh(local_frontend, tmp_path):
     assert len(summ["points"]) == 3 and all(p["failed"] == 0 for p in summ["points"])
     assert all(p["output_tok_per_s"] > 0 and p["ttft_ms_p50"] is not None for p in summ["points"])
     assert (tmp_path / "plots" / "summary.md").exists()
+
+
+@pytest.mark.parametrize("mode,nproc", [("agg", 1), ("agg", 2), ("disagg", 2)])
+def test_bench_contract_cpu(mode, nproc, tmp_path):
+    """bench.py prints exactly one JSON line with the driver's contract fields (CPU plumbing run;
+    world 2 goes through torch.distributed.run like the driver's multi-GPU launch)."""
+    import json
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "12", "--warmup", "8", "--qps", "20",
+           "--mode", mode, "--device", "cpu"]
+    if nproc > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port)] + cmd[1:] + ["--gpus", str(nproc)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == nproc and d["steps"] == 12 and d["warmup"] == 8 and d["value"] > 0
+    assert d["config"]["mode"] == mode
