@@ -13,9 +13,18 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <vector>
+#include <pybind11/stl.h>
 
 namespace mxs {
 void launch_copy_blocks(char*, const char*, const int*, const int*, int, long, hipStream_t);
+constexpr int kArMaxRanks = 8;
+struct ArPeers {
+  char* recv[kArMaxRanks];
+  unsigned* flags[kArMaxRanks];
+};
+void launch_custom_allreduce(unsigned short*, const unsigned short*, long, const ArPeers&, int, int, long, unsigned*,
+                             unsigned*, hipStream_t);
 }
 
 namespace {
@@ -71,9 +80,52 @@ void copy_blocks(int64_t dst_ptr, at::Tensor src, at::Tensor src_ids, at::Tensor
                           c10::hip::getCurrentHIPStream().stream());
 }
 
+// Custom all-reduce buffers: uncached device memory (peers write into it over xGMI and this rank
+// polls / reads it without stale L2 lines), zeroed, exported for the peers.
+pybind11::tuple car_alloc(int64_t bytes) {
+  void* p = nullptr;
+  hip_check(hipExtMallocWithFlags(&p, static_cast<size_t>(bytes), hipDeviceMallocUncached), "hipExtMallocWithFlags");
+  hip_check(hipMemset(p, 0, static_cast<size_t>(bytes)), "hipMemset");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  hipIpcMemHandle_t h;
+  hip_check(hipIpcGetMemHandle(&h, p), "hipIpcGetMemHandle");
+  return pybind11::make_tuple(reinterpret_cast<int64_t>(p),
+                              pybind11::bytes(reinterpret_cast<const char*>(&h), sizeof(h)));
+}
+
+void car_free(int64_t ptr) { (void)hipFree(reinterpret_cast<void*>(ptr)); }
+
+int64_t car_read_u32(int64_t ptr) {  // synchronous 4-byte device -> host read (error word)
+  unsigned v = 0;
+  hip_check(hipMemcpy(&v, reinterpret_cast<void*>(ptr), sizeof(v), hipMemcpyDeviceToHost), "hipMemcpy");
+  return v;
+}
+
+void custom_allreduce(at::Tensor out, at::Tensor x, std::vector<int64_t> recv_ptrs, std::vector<int64_t> flag_ptrs,
+                      int64_t rank, int64_t slot_elems, int64_t epochs_ptr, int64_t err_ptr) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "x: contiguous bf16 GPU tensor");
+  TORCH_CHECK(out.is_contiguous() && out.numel() == x.numel(), "out shape");
+  const int n = static_cast<int>(recv_ptrs.size());
+  TORCH_CHECK(n >= 1 && n <= mxs::kArMaxRanks && static_cast<int>(flag_ptrs.size()) == n, "1..8 ranks");
+  TORCH_CHECK(x.numel() % 8 == 0 && x.numel() <= slot_elems, "numel must be a multiple of 8 and fit a slot");
+  mxs::ArPeers peers{};
+  for (int r = 0; r < n; ++r) {
+    peers.recv[r] = reinterpret_cast<char*>(recv_ptrs[r]);
+    peers.flags[r] = reinterpret_cast<unsigned*>(flag_ptrs[r]);
+  }
+  mxs::launch_custom_allreduce(reinterpret_cast<unsigned short*>(out.data_ptr()),
+                               reinterpret_cast<const unsigned short*>(x.data_ptr()), x.numel(), peers,
+                               static_cast<int>(rank), n, slot_elems, reinterpret_cast<unsigned*>(epochs_ptr),
+                               reinterpret_cast<unsigned*>(err_ptr), c10::hip::getCurrentHIPStream().stream());
+}
+
 }  // namespace
 
 void register_comm(pybind11::module_& m) {
+  m.def("car_alloc", &car_alloc);
+  m.def("car_free", &car_free);
+  m.def("car_read_u32", &car_read_u32);
+  m.def("custom_allreduce", &custom_allreduce);
   m.def("ipc_export_pool", &export_pool);
   m.def("ipc_open_pool", &open_pool);
   m.def("ipc_close_all", &close_all);

@@ -1,0 +1,113 @@
+// K18: one-shot IPC all-reduce for TP decode.
+//
+// xGMI on an MI355X node is a full mesh: every GPU has a direct link to each of its 7 peers, so a
+// ring (RCCL's algorithm for small messages) walks one link per hop and pays 2(N-1) latencies.
+// Here every rank PUSHES its input straight into a receive slot of every peer (N-1 links carry
+// stores at once, posted writes: no round trip), raises one flag per (block, peer), waits for the
+// N-1 flags addressed to it, and sums the N slots from its OWN memory.
+//
+// Buffers (allocated once per rank with hipDeviceMallocUncached, exported with hipIpc, mapped by
+// every peer; each well under 2 GiB, see mxserve/disagg/kv_transfer.py for the size rule):
+//   recv[2][N][max_elems]  two parities: call k writes parity k & 1, so a peer can run one call
+//                          ahead without overwriting slots this rank is still summing (it cannot
+//                          run two ahead: call k+1 waits for this rank's flags of call k+1, which
+//                          are only raised after this rank has finished call k) - no exit barrier
+//   flags[max_blocks][N]   flag[b][r] = last epoch rank r published for block b
+//   epoch[max_blocks]      per-block call counter kept on the device (hipGraph-safe: no host
+//                          epoch argument that a captured graph would freeze)
+// Memory model: payload stores + __threadfence_system() (release at system scope) before a flag is
+// stored with a system-scope atomic; the waiter polls with system-scope atomic loads and then
+// fences acquire at system scope.  The uncached allocation keeps stale lines out of every L2.
+// Spins are bounded: a peer that never arrives sets err[0] and the call returns (the host then
+// falls back to RCCL for good), so a broken link cannot hang the GPU.
+#include "common.h"
+
+namespace mxs {
+
+constexpr int kArMaxRanks = 8;
+constexpr int kArMaxBlocks = 64;
+
+struct ArPeers {
+  char* recv[kArMaxRanks];    // each rank's recv base, mapped into this process
+  unsigned* flags[kArMaxRanks];
+};
+
+__device__ __forceinline__ void st_flag(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned ld_flag(unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// x: this rank's input (bf16, n elements, n % 8 == 0); out: result (may alias x)
+__global__ void __launch_bounds__(512) custom_allreduce_kernel(bf16_t* out, const bf16_t* __restrict__ x, long n,
+                                                               ArPeers peers, int rank, int nranks,
+                                                               long slot_elems, unsigned* epochs, unsigned* err) {
+  const int b = blockIdx.x;
+  const long nv = n / 8;  // 16-byte vectors
+  const long per = (nv + gridDim.x - 1) / gridDim.x;
+  const long v0 = b * per, v1 = min(nv, v0 + per);
+  __shared__ unsigned s_epoch;
+  if (threadIdx.x == 0) s_epoch = epochs[b] + 1;
+  __syncthreads();
+  const unsigned e = s_epoch;
+  const int par = e & 1;
+  // 1. push this block's chunk into slot [par][rank] of every rank (self included)
+  const uint4* xs = reinterpret_cast<const uint4*>(x);
+  for (int r = 0; r < nranks; ++r) {
+    uint4* dst = reinterpret_cast<uint4*>(peers.recv[r] + ((static_cast<long>(par) * nranks + rank) * slot_elems) * 2);
+    for (long v = v0 + threadIdx.x; v < v1; v += blockDim.x) dst[v] = xs[v];
+  }
+  // 2. release + one flag per peer
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < nranks) st_flag(peers.flags[threadIdx.x] + b * kArMaxRanks + rank, e);
+  // 3. wait for every rank's flag of this epoch (bounded spin)
+  if (threadIdx.x < nranks) {
+    unsigned* f = peers.flags[rank] + b * kArMaxRanks + threadIdx.x;
+    long spins = 0;
+    while (static_cast<int>(ld_flag(f) - e) < 0) {
+      if (++spins > (1L << 26) || ld_flag(err) != 0) {
+        atomicExch(err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  // 4. sum the N slots (local memory) in fp32, rank order (every rank gets identical bits)
+  const char* mine = peers.recv[rank] + (static_cast<long>(par) * nranks * slot_elems) * 2;
+  uint4* o = reinterpret_cast<uint4*>(out);
+  for (long v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < nranks; ++r) {
+      const uint4 w = reinterpret_cast<const uint4*>(mine + r * slot_elems * 2)[v];
+      const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[2 * k] += bf2f_lo(u[k]);
+        acc[2 * k + 1] += bf2f_hi(u[k]);
+      }
+    }
+    uint4 rr;
+    rr.x = pack2(acc[0], acc[1]);
+    rr.y = pack2(acc[2], acc[3]);
+    rr.z = pack2(acc[4], acc[5]);
+    rr.w = pack2(acc[6], acc[7]);
+    o[v] = rr;
+  }
+  if (threadIdx.x == 0) epochs[b] = e;
+}
+
+void launch_custom_allreduce(bf16_t* out, const bf16_t* x, long n, const ArPeers& peers, int rank, int nranks,
+                             long slot_elems, unsigned* epochs, unsigned* err, hipStream_t s) {
+  // ALWAYS kArMaxBlocks blocks: every block then counts the same calls, so the parity of a call is
+  // the same in every block and chunk ranges may differ between calls of different sizes without a
+  // peer that runs one call ahead ever writing into the parity this rank is still summing
+  hipLaunchKernelGGL(custom_allreduce_kernel, dim3(kArMaxBlocks), dim3(512), 0, s, out, x, n, peers, rank, nranks,
+                     slot_elems, epochs, err);
+  MXS_CHECK_LAUNCH();
+}
+
+}  // namespace mxs

@@ -135,6 +135,7 @@ class ModelRunner:
         # sampled ids come back through two alternating pinned buffers (step N's result is read
         # while step N+1, launched just before, may already be writing the other one)
         self._out_slot = 0
+        self._steps = 0
         if self.is_gpu:
             self._out_pinned = [torch.zeros(n_rows, dtype=torch.int64, pin_memory=True) for _ in range(2)]
             self._out_events = [torch.cuda.Event(), torch.cuda.Event()]
@@ -308,7 +309,13 @@ class ModelRunner:
         if self.graphs and not so.prefills and S <= max(self.graphs):
             gbs = min(x for x in self.graphs if x >= S)
         meta = self._prepare(so, gbs)
-        if get_tp().tp_size > 1:
+        tp = get_tp()
+        if tp.tp_size > 1:
+            self._steps += 1
+            if tp.custom_ar is not None and not tp.custom_ar.disabled and self._steps % 512 == 0 \
+                    and not tp.custom_ar.check():
+                meta["car_disable"] = True
+                self._disable_custom_ar()
             tp_broadcast_object(("step", self.buf.host_bytes(), meta))
         ids = self.execute_host(meta)
         handle = {"so": so, "rows": meta["sample_rows"]}
@@ -359,8 +366,18 @@ class ModelRunner:
             if msg is None or msg[0] == "shutdown":
                 return
             _, host_bytes, meta = msg
+            if meta.get("car_disable"):
+                self._disable_custom_ar()
             self.buf.load_host_bytes(host_bytes)
             self.execute_host(meta)
+
+    def _disable_custom_ar(self) -> None:
+        """Every rank at the same step: RCCL from now on; the captured graphs still hold the custom
+        all-reduce kernels, so decode runs eagerly."""
+        tp = get_tp()
+        if tp.custom_ar is not None:
+            tp.custom_ar.disabled = True
+        self.graphs.clear()
 
     def shutdown_followers(self) -> None:
         if get_tp().tp_size > 1 and get_tp().tp_rank == 0:

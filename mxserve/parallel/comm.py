@@ -61,10 +61,12 @@ def init_distributed(tp_size: int, backend: Optional[str] = None, device: Option
     st = ParallelState(tp_rank=dist.get_rank(), tp_size=world, group=dist.group.WORLD)
     # scheduler metadata goes rank0 -> TP ranks over a CPU (gloo) group, never a GPU collective
     st.cpu_group = dist.new_group(backend="gloo") if backend != "gloo" else st.group
-    if enable_custom_ar and backend == "nccl" and os.environ.get("MXS_CUSTOM_AR", "1") == "1":
+    # custom IPC all-reduce: validated between processes sharing one GPU (tests/test_custom_ar_gpu.py);
+    # opt-in until it has run across a real xGMI mesh
+    if enable_custom_ar and backend == "nccl" and os.environ.get("MXS_CUSTOM_AR", "0") == "1":
         try:
             from .custom_allreduce import CustomAllReduce
-            st.custom_ar = CustomAllReduce.create(st.group, device)
+            st.custom_ar = CustomAllReduce.create(st.group, device, cpu_group=st.cpu_group)
         except Exception as e:  # noqa: BLE001 - RCCL remains correct
             import logging
             logging.getLogger(__name__).warning("custom all-reduce disabled: %r", e)

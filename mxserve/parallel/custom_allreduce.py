@@ -1,0 +1,88 @@
+"""Custom one-shot IPC all-reduce for tensor-parallel decode.
+
+Kernel: csrc/kernels/custom_allreduce.hip (push into every peer's receive slot over the xGMI mesh,
+flag, sum locally).  This module owns the buffers: each rank allocates uncached receive slots
+(2 parities x N ranks x max_bytes) and a 64 KiB signal page, exports both with hipIpc, exchanges
+the handles over the CPU group and maps every peer's.  All sizes stay far below 2 GiB (the
+dmabuf IPC size rule in mxserve/disagg/kv_transfer.py).
+
+Used for bf16 tensors up to `max_bytes` (decode-sized: 70B TP8 at batch 256 is 4 MiB); larger
+all-reduces go to RCCL.  Graph-safe: the per-call epoch lives on the device.  A rank whose peer
+never arrives gives up after ~2 s and raises the error word; `check()` (called by the engine between
+steps) then turns the path off for good and every later all-reduce uses RCCL.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+log = logging.getLogger(__name__)
+
+SIGNAL_BYTES = 64 << 10
+_FLAGS_OFF, _EPOCHS_OFF, _ERR_OFF = 0, 4096, 8192
+
+
+class CustomAllReduce:
+    def __init__(self, rank: int, world: int, max_bytes: int, recv_ptrs: list, flag_ptrs: list, own: tuple,
+                 device: torch.device):
+        self.rank, self.world = rank, world
+        self.max_bytes = max_bytes
+        self.slot_elems = max_bytes // 2
+        self.recv_ptrs, self.flag_ptrs = recv_ptrs, flag_ptrs
+        self._own = own  # (recv_ptr, signal_ptr) allocated by this rank
+        sig = flag_ptrs[rank]
+        self.epochs_ptr = sig + _EPOCHS_OFF
+        self.err_ptr = sig + _ERR_OFF
+        self.device = device
+        self.disabled = False
+
+    @classmethod
+    def create(cls, group, device: Optional[torch.device] = None, max_bytes: int = 8 << 20,
+               cpu_group=None) -> "CustomAllReduce":
+        from .. import ops
+        ext = ops.ext()
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        if world > 8:
+            raise ValueError("custom all-reduce supports up to 8 ranks (one xGMI mesh)")
+        recv_ptr, recv_h = ext.car_alloc(2 * world * max_bytes)
+        sig_ptr, sig_h = ext.car_alloc(SIGNAL_BYTES)
+        handles = [None] * world
+        dist.all_gather_object(handles, (recv_h, sig_h), group=cpu_group or group)
+        recv_ptrs, flag_ptrs = [], []
+        for r, (rh, sh) in enumerate(handles):
+            if r == rank:
+                recv_ptrs.append(recv_ptr)
+                flag_ptrs.append(sig_ptr)
+            else:
+                recv_ptrs.append(int(ext.ipc_open_pool(rh, 0)))
+                flag_ptrs.append(int(ext.ipc_open_pool(sh, 0)))
+        dist.barrier(group=cpu_group or group)
+        log.info("custom all-reduce ready: rank %d/%d, %d MiB slots", rank, world, max_bytes >> 20)
+        return cls(rank, world, max_bytes, recv_ptrs, flag_ptrs, (recv_ptr, sig_ptr), device)
+
+    def should_use(self, x: torch.Tensor) -> bool:
+        return (not self.disabled and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
+                and x.numel() % 8 == 0 and x.numel() * 2 <= self.max_bytes)
+
+    def all_reduce(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Sum of x over the group (in place unless `out` is given)."""
+        from .. import ops
+        out = x if out is None else out
+        ops.ext().custom_allreduce(out, x, self.recv_ptrs, self.flag_ptrs, self.rank, self.slot_elems,
+                                   self.epochs_ptr, self.err_ptr)
+        return out
+
+    def check(self) -> bool:
+        """True while healthy.  Reads every rank's error word (all signal pages are mapped here); a
+        timed-out peer disables the path (RCCL from then on)."""
+        if self.disabled:
+            return False
+        from .. import ops
+        if any(ops.ext().car_read_u32(p + _ERR_OFF) != 0 for p in self.flag_ptrs):
+            log.error("custom all-reduce: a peer timed out; falling back to RCCL")
+            self.disabled = True
+        return not self.disabled

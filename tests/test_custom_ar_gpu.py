@@ -1,0 +1,95 @@
+"""Custom IPC all-reduce (K18) between ranks that share GPU 0 (the 1-GPU test box): each rank is a
+process with its own buffers, exported and mapped over hipIpc exactly as across xGMI peers.  Checks
+exact sums for several sizes back to back (parity reuse across calls of different sizes), in place
+and out of place, and inside a captured hipGraph (device-side epochs).  The parent never
+initialises HIP."""
+import multiprocessing as mp
+import os
+import traceback
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [8, 2048, 4096 * 8, 1 << 20, 4096 * 8, 8]
+
+
+def _rank(rank, world, port, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        from mxserve.parallel.custom_allreduce import CustomAllReduce
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        car = CustomAllReduce.create(dist.group.WORLD, torch.device("cuda:0"), max_bytes=4 << 20)
+        errs = []
+
+        def inp(n, call):  # exact in bf16: small integers
+            return ((torch.arange(n, device="cuda:0") % 13) + rank * 3 + call).to(torch.bfloat16)
+
+        def want(n, call):
+            return sum(((torch.arange(n, device="cuda:0") % 13) + r * 3 + call) for r in range(world)).float()
+
+        for call, n in enumerate(SIZES):
+            x = inp(n, call)
+            if call % 2:
+                out = torch.empty_like(x)
+                car.all_reduce(x, out)
+            else:
+                out = car.all_reduce(x)
+            torch.cuda.synchronize()
+            if not torch.equal(out.float(), want(n, call)):
+                errs.append(f"call {call} n={n}: max err {(out.float() - want(n, call)).abs().max().item()}")
+        # hipGraph: 3 captured all-reduces, replayed twice
+        xs = [inp(4096, 100 + i) for i in range(3)]
+        bufs = [x.clone() for x in xs]
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=s):
+                for b in bufs:
+                    car.all_reduce(b)
+        for rep in range(2):
+            for b, x in zip(bufs, xs):
+                b.copy_(x)
+            torch.cuda.synchronize()
+            dist.barrier()
+            g.replay()
+            torch.cuda.synchronize()
+            for i, b in enumerate(bufs):
+                if not torch.equal(b.float(), want(4096, 100 + i)):
+                    errs.append(f"graph rep {rep} buf {i}")
+        assert car.check(), "error word raised"
+        dist.barrier()
+        q.put((rank, errs))
+    except BaseException:  # noqa: BLE001
+        q.put((rank, [traceback.format_exc()]))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_custom_allreduce_ranks_on_one_gpu(world):
+    import socket
+    import torch
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    if torch.cuda.is_initialized():
+        pytest.skip("HIP already initialised in the test process; run this file on its own")
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        res = dict(q.get(timeout=180) for _ in range(world))
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert res[r] == [], res[r]
