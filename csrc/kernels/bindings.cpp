@@ -24,6 +24,8 @@ void launch_sample(int64_t*, const void*, bool, int, int, long, const float*, co
 void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStream_t);
 void launch_moe_align(int*, int*, const int*, int, int, int, hipStream_t);
 bool launch_skinny_gemm(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, hipStream_t);
+bool launch_moe_grouped_gemm(bf16_t*, const bf16_t*, const bf16_t*, const int*, int, int, int, int, int, bool,
+                             hipStream_t);
 }  // namespace mxs
 
 namespace {
@@ -147,6 +149,18 @@ bool skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w) {
                                  out.stride(0), stream());
 }
 
+// y[r] = x[r] . w[e(r)]^T over expert-sorted rows (offs = moe_align offsets); silu: w rows are
+// [gate; up] and y = silu(gate) * up (width N/2).  False if the shape is unsupported.
+bool moe_grouped_gemm(at::Tensor y, at::Tensor x, at::Tensor w, at::Tensor offs, bool silu) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
+  TORCH_CHECK(w.dim() == 3 && x.dim() == 2 && y.dim() == 2, "w [E, N, K], x [rows, K], y [rows, N']");
+  TORCH_CHECK(offs.scalar_type() == at::kInt && offs.numel() == w.size(0) + 1, "offs: int32 [E + 1]");
+  const int N = w.size(1), K = w.size(2);
+  TORCH_CHECK(x.size(1) == K && y.size(0) == x.size(0) && y.size(1) == (silu ? N / 2 : N), "shape mismatch");
+  return mxs::launch_moe_grouped_gemm(bf(y), bf(x), bf(w), offs.data_ptr<int>(), w.size(0), x.size(0), N, K,
+                                      y.size(1), silu, stream());
+}
+
 void moe_topk_softmax(at::Tensor w, at::Tensor ids, at::Tensor logits) {
   CHECK_CUDA(logits); CHECK_BF16(logits); CHECK_CONTIG(logits);
   TORCH_CHECK(logits.size(1) <= 64, "at most 64 experts");
@@ -178,6 +192,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_topk_softmax", &moe_topk_softmax);
   m.def("moe_align", &moe_align);
   m.def("skinny_gemm", &skinny_gemm);
+  m.def("moe_grouped_gemm", &moe_grouped_gemm);
   m.def("decode_num_partitions", &mxs::decode_num_partitions);
   m.def("decode_plan", [](int B, int Hkv, int max_seq_len) {
     int P = 1, len = 0;

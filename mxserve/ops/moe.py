@@ -1,13 +1,12 @@
-"""MoE expert computation on the GPU (K15-K17).
+"""MoE expert computation on the GPU (K15-K17), Mixtral 8x7B top-2, experts sharded over EP ranks.
 
-Two regimes (Mixtral 8x7B, top-2, experts sharded over EP ranks):
-  * decode / small T (<= DENSE_MAX_TOKENS): the step is bound by streaming the local experts'
-    weights, and with >= ~32 tokens every expert is hit anyway, so each local expert runs over all
-    tokens and the results are combined with a [T, E_local] routing-weight matrix (zero for
-    unrouted pairs).  No host sync, so the step stays hipGraph-capturable.
-  * prefill / large T: tokens are bucketed by expert with the moe_align counting-sort kernel and
-    each expert runs a GEMM over only its rows (no wasted FLOPs); the weighted results are
-    scatter-added back to token order.
+fused_experts: the moe_align counting sort buckets the (token, slot) assignments by local expert,
+the rows are gathered once, and two MFMA grouped-GEMM launches (csrc/kernels/moe_gemm.hip) run
+every local expert over exactly its rows -- gate_up with SiLU*mul fused into the epilogue, then
+down -- before a weighted scatter-add restores token order.  No host sync anywhere, so decode steps
+stay hipGraph-capturable and prefill costs two launches instead of 2 x E_local GEMMs.
+_fused_experts_loop keeps the per-expert formulation (dense over all tokens at small T, sorted rows
+otherwise) for shapes the grouped kernel does not tile.
 """
 from __future__ import annotations
 
@@ -15,6 +14,10 @@ import torch
 import torch.nn.functional as F
 
 DENSE_MAX_TOKENS = 256
+# grouped kernel up to this many tokens (decode / mixed steps, graph-capturable); above it the
+# per-expert hipBLASLt GEMMs over sorted rows are faster (profiles/r1_moe_layer_mixtral.jsonl:
+# grouped 0.82 / 0.86 ms vs 0.89 / 1.22 ms at T = 64 / 256; 2.77 vs 2.01 ms at T = 2048)
+GROUPED_MAX_TOKENS = 512
 
 
 def _silu_mul(h: torch.Tensor) -> torch.Tensor:
@@ -32,8 +35,9 @@ def combine_weights(topk_w: torch.Tensor, topk_ids: torch.Tensor, e_local: int, 
     return cw
 
 
-def fused_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
-                  topk_ids: torch.Tensor, expert_offset: int = 0) -> torch.Tensor:
+def _fused_experts_loop(x, w13, w2, topk_w, topk_ids, expert_offset):
+    """Reference-structured fallback (shapes the grouped kernel does not tile): dense per-expert
+    GEMMs for small T, per-expert GEMMs over moe_align-sorted rows otherwise."""
     T, H = x.shape
     e_local = w13.shape[0]
     if T <= DENSE_MAX_TOKENS:
@@ -61,4 +65,36 @@ def fused_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: 
     wts = topk_w.reshape(-1).index_select(0, rows).unsqueeze(1)
     out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
     out.index_add_(0, tok, ys.float() * wts)
+    return out.to(x.dtype)
+
+
+def fused_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
+                  topk_ids: torch.Tensor, expert_offset: int = 0) -> torch.Tensor:
+    """K15 align -> gather -> K16 grouped GEMM (gate_up with SiLU*mul fused in its epilogue) ->
+    K16 grouped GEMM (down) -> K17 weighted scatter-add.  Entirely on the device (no host sync):
+    graph-capturable for decode.  Large prefill chunks take the per-expert hipBLASLt loop."""
+    from . import ext
+    T, H = x.shape
+    if T > GROUPED_MAX_TOKENS:
+        return _fused_experts_loop(x, w13, w2, topk_w, topk_ids, expert_offset)
+    K = topk_ids.shape[1]
+    e_local, two_i, _ = w13.shape
+    dev = x.device
+    ids = topk_ids.to(torch.int32).contiguous()
+    offs = torch.empty(e_local + 1, dtype=torch.int32, device=dev)
+    perm = torch.full((T * K,), -1, dtype=torch.int32, device=dev)
+    ext().moe_align(offs, perm, ids, expert_offset, e_local)
+    valid = (perm >= 0).unsqueeze(1)
+    rows = perm.clamp(min=0).long()
+    tok = rows // K
+    xs = x.index_select(0, tok)  # rows past the routed count are ignored by the GEMMs
+    h = torch.empty(T * K, two_i // 2, dtype=x.dtype, device=dev)
+    ys = torch.empty(T * K, H, dtype=x.dtype, device=dev)
+    if not (ext().moe_grouped_gemm(h, xs, w13.contiguous(), offs, True)
+            and ext().moe_grouped_gemm(ys, h, w2.contiguous(), offs, False)):
+        return _fused_experts_loop(x, w13, w2, topk_w, topk_ids, expert_offset)
+    wts = topk_w.reshape(-1).index_select(0, rows).unsqueeze(1)
+    contrib = torch.where(valid, ys.float() * wts, torch.zeros((), dtype=torch.float32, device=dev))
+    out = torch.zeros(T, H, dtype=torch.float32, device=dev)
+    out.index_add_(0, tok, contrib)
     return out.to(x.dtype)

@@ -262,3 +262,42 @@ def test_skinny_gemm_strided_input_and_fallback(gpu):
     out = torch.empty(8, 100, device="cuda", dtype=torch.bfloat16)
     assert not ops.ext().skinny_gemm(out, x.contiguous(), w_odd)
     _close(ops.linear(x, w_odd), x.float() @ w_odd.float().t(), atol=0.3, rtol=2e-2, name="fallback")
+
+
+@pytest.mark.parametrize("counts", [[0, 5, 300, 1], [128, 129, 0, 3], [1, 1, 1, 1]])
+@pytest.mark.parametrize("silu", [False, True])
+def test_moe_grouped_gemm(gpu, counts, silu):
+    E, N, K = len(counts), 256, 320
+    rows = sum(counts) + 37  # extra rows past the routed count must be left alone
+    g = torch.Generator(device="cuda").manual_seed(sum(counts) + silu)
+    x = torch.randn(rows, K, device=gpu, dtype=torch.bfloat16, generator=g)
+    w = (torch.randn(E, N, K, device=gpu, dtype=torch.bfloat16, generator=g) * 0.05).to(torch.bfloat16)
+    offs = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=gpu)
+    y = torch.full((rows, N // 2 if silu else N), 7.0, device=gpu, dtype=torch.bfloat16)
+    assert ops.ext().moe_grouped_gemm(y, x, w, offs, silu)
+    o = offs.tolist()
+    for e in range(E):
+        a, b = o[e], o[e + 1]
+        if b == a:
+            continue
+        ref_y = x[a:b].float() @ w[e].float().t()
+        if silu:
+            gt, up = ref_y[:, :N // 2], ref_y[:, N // 2:]
+            ref_y = gt * torch.sigmoid(gt) * up
+        _close(y[a:b], ref_y, atol=3e-2, rtol=3e-2, name=f"expert {e}")
+    assert torch.all(y[o[-1]:] == 7.0), "rows past the routed count were written"
+
+
+def test_moe_experts_uses_grouped_kernel(gpu, monkeypatch):
+    from mxserve.ops import moe as moe_mod
+    called = []
+    monkeypatch.setattr(moe_mod, "_fused_experts_loop", lambda *a, **k: called.append(1))
+    H, I, E, K, T = 256, 192, 4, 2, 50
+    x = torch.randn(T, H, device=gpu, dtype=torch.bfloat16)
+    w13 = torch.randn(E, 2 * I, H, device=gpu, dtype=torch.bfloat16) * 0.05
+    w2 = torch.randn(E, H, I, device=gpu, dtype=torch.bfloat16) * 0.05
+    tw, tid = ops.moe_topk_softmax(torch.randn(T, E, device=gpu, dtype=torch.bfloat16), K)
+    out = moe_mod.fused_experts(x, w13, w2, tw, tid, 2)  # EP: this rank holds experts 2, 3
+    assert not called and out is not None
+    exp = ref.moe_experts(x.cpu(), w13.cpu(), w2.cpu(), tw.cpu(), tid.cpu(), 2)
+    _close(out, exp, 0.02, 0.03, "moe ep")
