@@ -1,0 +1,90 @@
+"""SLA planner (X13) against the fake apiserver with a scripted metrics source and clock."""
+import pytest
+
+from mxserve.k8s.client import KubeClient
+from mxserve.k8s.fake_apiserver import FakeApiServer
+from mxserve.planner.planner import Planner, PlannerConfig, parse_prometheus
+from tests.serving_utils import Server
+
+
+def _dgd(kind="disagg"):
+    svc = {"Frontend": {"componentType": "frontend", "replicas": 1}}
+    if kind == "disagg":
+        for sub in ("prefill", "decode"):
+            svc[f"W{sub}"] = {"componentType": "worker", "subComponentType": sub, "replicas": 1,
+                              "resources": {"limits": {"gpu": "1"}}}
+    else:
+        svc["W"] = {"componentType": "worker", "replicas": 1, "resources": {"limits": {"gpu": "1"}}}
+    return {"apiVersion": "nvidia.com/v1alpha1", "kind": "DynamoGraphDeployment",
+            "metadata": {"name": "g", "namespace": "ns"}, "spec": {"services": svc}}
+
+
+class Feed:
+    """Cumulative frontend counters advanced by (rps, isl, osl, ttft_s, itl_s) per window."""
+
+    def __init__(self):
+        self.c = {}
+        self.t = 0.0
+
+    def advance(self, secs, rps, isl=4000, osl=500, ttft=0.1, itl=0.01):
+        n = rps * secs
+        for k, v in (("dynamo_frontend_requests_total", n), ("dynamo_frontend_input_sequence_tokens_count", n),
+                     ("dynamo_frontend_input_sequence_tokens_sum", n * isl),
+                     ("dynamo_frontend_output_sequence_tokens_count", n),
+                     ("dynamo_frontend_output_sequence_tokens_sum", n * osl),
+                     ("dynamo_frontend_time_to_first_token_seconds_count", n),
+                     ("dynamo_frontend_time_to_first_token_seconds_sum", n * ttft),
+                     ("dynamo_frontend_inter_token_latency_seconds_count", n * osl),
+                     ("dynamo_frontend_inter_token_latency_seconds_sum", n * osl * itl)):
+            self.c[k] = self.c.get(k, 0.0) + v
+        self.t += secs
+
+
+@pytest.fixture()
+def api():
+    fake = FakeApiServer()
+    srv = Server(fake.app).start()
+    yield KubeClient(srv.url)
+    srv.stop()
+
+
+def test_parse_prometheus_sums_label_sets():
+    text = ('# HELP x\n# TYPE x counter\ndynamo_frontend_requests_total{model="a",status="success"} 3.0\n'
+            'dynamo_frontend_requests_total{model="a",status="error"} 1\nfoo 2.5e1\n')
+    m = parse_prometheus(text)
+    assert m["dynamo_frontend_requests_total"] == 4.0 and m["foo"] == 25.0
+
+
+def test_planner_scales_up_on_load_and_sla_breach_then_down_after_cooldown(api):
+    api.create(_dgd())
+    feed = Feed()
+    cfg = PlannerConfig(namespace="ns", dgd="g", model="meta-llama/Llama-3.2-1B-Instruct", cooldown_s=100,
+                        max_gpus=8)
+    p = Planner(cfg, api, lambda: dict(feed.c), clock=lambda: feed.t)
+    assert p.step() is None  # first scrape only sets the baseline
+    feed.advance(30, rps=60, ttft=0.9, itl=0.03)  # heavy load, both SLAs broken
+    rec = p.step()
+    svc = api.get("DynamoGraphDeployment", "g", "ns")["spec"]["services"]
+    pre, dec = svc["Wprefill"]["replicas"], svc["Wdecode"]["replicas"]
+    assert pre >= 2 and dec >= 2 and pre + dec <= 8, rec
+    feed.advance(30, rps=0.2)  # idle, inside the cooldown: hold
+    p.step()
+    svc = api.get("DynamoGraphDeployment", "g", "ns")["spec"]["services"]
+    assert (svc["Wprefill"]["replicas"], svc["Wdecode"]["replicas"]) == (pre, dec)
+    for _ in range(5):  # past the cooldown: back to one replica each
+        feed.advance(30, rps=0.2)
+        p.step()
+    svc = api.get("DynamoGraphDeployment", "g", "ns")["spec"]["services"]
+    assert (svc["Wprefill"]["replicas"], svc["Wdecode"]["replicas"]) == (1, 1)
+
+
+def test_planner_agg_graph_and_dry_run(api):
+    api.create(_dgd("agg"))
+    feed = Feed()
+    cfg = PlannerConfig(namespace="ns", dgd="g", model="meta-llama/Llama-3.2-1B-Instruct", dry_run=True)
+    p = Planner(cfg, api, lambda: dict(feed.c), clock=lambda: feed.t)
+    p.step()
+    feed.advance(30, rps=200)
+    rec = p.step()
+    assert rec["changes"]["W"] == 8  # capped by the node's GPUs
+    assert api.get("DynamoGraphDeployment", "g", "ns")["spec"]["services"]["W"]["replicas"] == 1  # dry run
