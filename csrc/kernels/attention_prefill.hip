@@ -241,11 +241,240 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// v3: K/V tiles shared through LDS.  v2 gives every wave its own copy of each K/V tile straight
+// from L2 (4x the load traffic of one workgroup); v3 is the structure of the guide's "Fused
+// attention prefill": 8 waves x 32 rows = 256 query rows per workgroup, 64-key tiles double-
+// buffered in LDS (global loads for tile i+1 issued before tile i is multiplied, written to the
+// other buffer after it), XOR-swizzled 16-byte chunks so the fragment reads of 32 consecutive rows
+// spread over the banks.  V is stored per dim with its keys permuted (bits 2 and 3 of the key index
+// swapped inside each 16-key group) so the 8 keys a lane needs for the P^T operand taken straight
+// from the S^T accumulator are one contiguous ds_read_b128.
+template <int D, int G>
+__global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kv, long block_stride,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ qsl,
+    const int* __restrict__ seq_lens, int Hkv, float scale) {
+  constexpr int KS = D / 16, DT = D / 32;
+  constexpr int BQ = 256 / G;        // query tokens per workgroup
+  constexpr int KT = 64;             // keys per tile
+  constexpr int KROW = D * 2;        // bytes of one K row in LDS
+  constexpr int KCH = D / 8;         // 16-byte chunks per K row
+  constexpr int KBYTES = KT * KROW;
+  constexpr int VBYTES = D * KT * 2; // [D][64 keys]
+  constexpr int NK = KT * KCH / 512; // K chunks staged per thread per tile
+  constexpr int NV = D * 8 / 512;    // V chunks (8 keys of one dim) staged per thread per tile
+  __shared__ __attribute__((aligned(16))) char lds[2][KBYTES + VBYTES];
+
+  const int NTL = gridDim.x, total = NTL * gridDim.y * gridDim.z;
+  const int lin = blockIdx.x + NTL * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int vix = (total % 8 == 0) ? (lin % 8) * (total / 8) + lin / 8 : lin;
+  const int pair = vix / NTL;
+  const int kvh = pair % gridDim.y, seq = pair / gridDim.y;
+  const int q0 = qsl[seq];
+  const int ql = qsl[seq + 1] - q0;
+  const int t0 = (NTL - 1 - (vix - pair * NTL)) * BQ;  // heaviest tiles first
+  if (t0 >= ql) return;
+  const int L = seq_lens[seq];
+  const int ctx0 = L - ql;
+  const int Hq = Hkv * G;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane >> 5, c = lane & 31;
+
+  const int r = wid * 32 + c;
+  const int tok = t0 + r / G;
+  const int head = kvh * G + r % G;
+  const bool rvalid = tok < ql;
+  const int qpos = ctx0 + (rvalid ? tok : 0);
+  const int nkeys = ctx0 + min(t0 + BQ, ql);
+  const int wave_min_pos = ctx0 + min(t0 + (wid * 32) / G, ql - 1);
+  const int wave_max_pos = ctx0 + min(t0 + (wid * 32 + 31) / G, ql - 1);
+
+  bf16x8_t qf[KS];
+  {
+    const bf16_t* qp = q + (static_cast<size_t>(q0 + (rvalid ? tok : 0)) * Hq + head) * D + 8 * h;
+    const float qs = scale * kPLog2e;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const uint4 v = *reinterpret_cast<const uint4*>(qp + 16 * ks);
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        qf[ks][2 * k] = static_cast<__bf16>(bf2f_lo(w[k]) * qs);
+        qf[ks][2 * k + 1] = static_cast<__bf16>(bf2f_hi(w[k]) * qs);
+      }
+    }
+  }
+
+  const int* bt = block_tables + static_cast<size_t>(seq) * bt_stride;
+  const char* kvb = reinterpret_cast<const char*>(kv);
+  const size_t k_head_off = static_cast<size_t>(kvh) * kPBS * D * 2;
+  const size_t v_head_off = static_cast<size_t>(Hkv + kvh) * kPBS * D * 2;
+  const long bstride = block_stride * 2;
+  const int last_blk = (L - 1) / kPBS;
+
+  // ---- staging: global -> registers (tile k0), registers -> LDS buffer
+  uint4 sk[NK], sv[NV];
+  auto gload = [&](int k0) {
+    int bid[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bid[j] = bt[min(k0 / kPBS + j, last_blk)];  // wave-uniform: scalar loads
+#pragma unroll
+    for (int n = 0; n < NK; ++n) {
+      const int ci = tid + 512 * n, key = ci / KCH, ch = ci % KCH;
+      sk[n] = *reinterpret_cast<const uint4*>(kvb + bid[key >> 4] * bstride + k_head_off + (key & 15) * KROW + ch * 16);
+    }
+#pragma unroll
+    for (int n = 0; n < NV; ++n) {
+      const int ci = tid + 512 * n, blk = ci / (2 * D), rem = ci % (2 * D), dim = rem >> 1, half = rem & 1;
+      uint4 v = *reinterpret_cast<const uint4*>(kvb + bid[blk] * bstride + v_head_off + dim * 32 + half * 16);
+      const int kb = k0 + blk * 16 + half * 8;  // keys >= L: zero (unwritten cache bytes may be NaN)
+      if (kb + 8 > L) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (kb + u >= L) w[u >> 1] &= (u & 1) ? 0x0000FFFFu : 0xFFFF0000u;
+      }
+      sv[n] = v;
+    }
+  };
+  auto sstore = [&](int buf) {
+    char* kl = lds[buf];
+    char* vl = lds[buf] + KBYTES;
+#pragma unroll
+    for (int n = 0; n < NK; ++n) {
+      const int ci = tid + 512 * n, key = ci / KCH, ch = ci % KCH;
+      *reinterpret_cast<uint4*>(kl + key * KROW + ((ch ^ (key & 7)) << 4)) = sk[n];
+    }
+#pragma unroll
+    for (int n = 0; n < NV; ++n) {
+      const int ci = tid + 512 * n, blk = ci / (2 * D), rem = ci % (2 * D), dim = rem >> 1, half = rem & 1;
+      // keys blk*16 + 8 half + j: j < 4 -> group position 4 half + j, j >= 4 -> 8 + 4 half + j - 4
+      char* row = vl + dim * (KT * 2);
+      const int c0 = blk * 2 + 0, c1 = blk * 2 + 1;  // 16-byte chunks of this block's 16 keys
+      uint2 lo = make_uint2(sv[n].x, sv[n].y), hi = make_uint2(sv[n].z, sv[n].w);
+      *reinterpret_cast<uint2*>(row + ((c0 ^ (dim & 7)) << 4) + half * 8) = lo;
+      *reinterpret_cast<uint2*>(row + ((c1 ^ (dim & 7)) << 4) + half * 8) = hi;
+    }
+  };
+
+  float16_ o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  auto compute = [&](int buf, int k0) {
+    const char* kl = lds[buf];
+    const char* vl = lds[buf] + KBYTES;
+    float16_ sacc[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[kt][i] = 0.f;
+      const int key = kt * 32 + c;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const uint4 a = *reinterpret_cast<const uint4*>(kl + key * KROW + (((2 * ks + h) ^ (key & 7)) << 4));
+        sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), qf[ks], sacc[kt], 0, 0, 0);
+      }
+    }
+    if (k0 + KT - 1 > wave_min_pos) {  // tile crosses the diagonal (or the end) of some row of this wave
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kk = k0 + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (kk > qpos) sacc[kt][i] = -INFINITY;
+        }
+    }
+    float mx = sacc[0][0];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[kt][i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const bool bump = mx > m + 8.f;  // lazy rescale, as in v2
+    if (__ballot(bump)) {
+      const float mn = bump ? mx : m;
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+    }
+    float ps = 0.f;
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(sacc[kt][i] - m);
+        ps += p;
+        pf[kt][i >> 3][i & 7] = static_cast<__bf16>(p);
+      }
+    l += ps;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int dim = 32 * dt + c;
+          const uint4 a = *reinterpret_cast<const uint4*>(vl + dim * (KT * 2) + (((4 * kt + 2 * s2 + h) ^ (dim & 7)) << 4));
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), pf[kt][s2], o[dt], 0, 0, 0);
+        }
+  };
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int it = 0, k0 = 0; k0 < nkeys; ++it, k0 += KT) {
+    const int buf = it & 1;
+    const bool more = k0 + KT < nkeys;
+    if (more) gload(k0 + KT);           // in flight under this tile's MFMAs
+    if (k0 <= wave_max_pos) compute(buf, k0);  // waves whose rows all precede the tile skip it
+    if (more) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  l += __shfl_xor(l, 32, 64);
+  if (!rvalid) return;
+  const float inv = 1.f / l;
+  bf16_t* op = out + (static_cast<size_t>(q0 + tok) * Hq + head) * D;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 32 * dt + 8 * g4 + 4 * h;
+      uint2 v;
+      v.x = pack2(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv);
+      v.y = pack2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+      *reinterpret_cast<uint2*>(op + d0) = v;
+    }
+}
+
 void launch_paged_prefill(bf16_t* out, const bf16_t* q, const bf16_t* kv, long block_stride,
                           const int* block_tables, int bt_stride, const int* qsl, const int* seq_lens,
-                          int num_seqs, int max_q_len, int Hq, int Hkv, int D, float scale, hipStream_t s) {
+                          int num_seqs, int max_q_len, int Hq, int Hkv, int D, float scale, int version,
+                          hipStream_t s) {
   if (num_seqs == 0 || max_q_len == 0) return;
   const int G = Hq / Hkv;
+  if (version != 2) {
+    dim3 grid3((max_q_len + 256 / G - 1) / (256 / G), Hkv, num_seqs), blk3(512);
+#define MXS_PF3(DD, GG)                                                                                    \
+    if (D == DD && G == GG) {                                                                              \
+      hipLaunchKernelGGL((paged_prefill_v3_kernel<DD, GG>), grid3, blk3, 0, s, out, q, kv, block_stride,   \
+                         block_tables, bt_stride, qsl, seq_lens, Hkv, scale);                             \
+      MXS_CHECK_LAUNCH();                                                                                  \
+      return;                                                                                              \
+    }
+    MXS_PF3(64, 1) MXS_PF3(64, 2) MXS_PF3(64, 4) MXS_PF3(64, 8)
+    MXS_PF3(128, 1) MXS_PF3(128, 2) MXS_PF3(128, 4) MXS_PF3(128, 8)
+#undef MXS_PF3
+  }
   const int BQ = 128 / G;
   dim3 grid((max_q_len + BQ - 1) / BQ, Hkv, num_seqs), blk(256);
 #define MXS_PF(DD, GG)                                                                                     \

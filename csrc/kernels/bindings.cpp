@@ -18,7 +18,7 @@ void decode_plan(int, int, int, int*, int*);
 void launch_paged_decode(bf16_t*, float*, float*, const bf16_t*, const bf16_t*, long, const int*, int, const int*,
                          int, int, int, int, int, int, float, hipStream_t);
 void launch_paged_prefill(bf16_t*, const bf16_t*, const bf16_t*, long, const int*, int, const int*, const int*,
-                          int, int, int, int, int, float, hipStream_t);
+                          int, int, int, int, int, float, int, hipStream_t);
 void launch_sample(int64_t*, const void*, bool, int, int, long, const float*, const float*, const int*,
                    const int64_t*, const int64_t*, hipStream_t);
 void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStream_t);
@@ -112,7 +112,7 @@ void paged_attention_decode(at::Tensor out, at::Tensor q, at::Tensor kv, at::Ten
 }
 
 void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Tensor block_tables, at::Tensor qsl,
-                             at::Tensor seq_lens, double scale, int64_t max_q_len) {
+                             at::Tensor seq_lens, double scale, int64_t max_q_len, int64_t version) {
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_CONTIG(out);
   const int Hq = q.size(1), D = q.size(2);
   const int Hkv = kv.size(2);
@@ -122,7 +122,8 @@ void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Te
   const int S = seq_lens.size(0);
   mxs::launch_paged_prefill(bf(out), bf(q), bf(kv), kv.stride(0), block_tables.data_ptr<int>(),
                             block_tables.stride(0), qsl.data_ptr<int>(), seq_lens.data_ptr<int>(), S,
-                            static_cast<int>(max_q_len), Hq, Hkv, D, static_cast<float>(scale), stream());
+                            static_cast<int>(max_q_len), Hq, Hkv, D, static_cast<float>(scale),
+                            static_cast<int>(version), stream());
 }
 
 void sample(at::Tensor out, at::Tensor logits, at::Tensor temperature, at::Tensor top_p, at::Tensor top_k,
@@ -187,7 +188,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("silu_mul", &silu_mul);
   m.def("rope_and_cache", &rope_and_cache);
   m.def("paged_attention_decode", &paged_attention_decode);
-  m.def("paged_attention_prefill", &paged_attention_prefill);
+  m.def("paged_attention_prefill", &paged_attention_prefill, pybind11::arg("out"), pybind11::arg("q"),
+        pybind11::arg("kv"), pybind11::arg("block_tables"), pybind11::arg("qsl"), pybind11::arg("seq_lens"),
+        pybind11::arg("scale"), pybind11::arg("max_q_len"), pybind11::arg("version") = 3);
   m.def("sample", &sample);
   m.def("moe_topk_softmax", &moe_topk_softmax);
   m.def("moe_align", &moe_align);

@@ -42,6 +42,9 @@ def has_ext() -> bool:
         return False
 
 
+_PREFILL_VERSION = int(os.environ.get("MXS_PREFILL_KERNEL", "3"))
+
+
 def _gpu(t: torch.Tensor) -> bool:
     return t.is_cuda and os.environ.get("MXS_FORCE_REFERENCE_OPS", "0") != "1"
 
@@ -123,12 +126,14 @@ def paged_attention_decode(q: torch.Tensor, kv_layer: torch.Tensor, block_tables
 
 def paged_attention_prefill(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,
                             query_start_loc: torch.Tensor, seq_lens: torch.Tensor, scale: float,
-                            max_query_len: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Causal varlen attention of prefill chunks against the paged cache (prefix included)."""
+                            max_query_len: int, out: Optional[torch.Tensor] = None,
+                            version: int = 0) -> torch.Tensor:
+    """Causal varlen attention of prefill chunks against the paged cache (prefix included).
+    version: 0 = default (v3, LDS-shared K/V tiles; MXS_PREFILL_KERNEL=2 selects v2), 2 or 3."""
     if _gpu(q):
         out = torch.empty_like(q) if out is None else out
         ext().paged_attention_prefill(out, q, kv_layer, block_tables, query_start_loc, seq_lens,
-                                      scale, max_query_len)
+                                      scale, max_query_len, version or _PREFILL_VERSION)
         return out
     return ref.paged_attention(q, kv_layer, block_tables, query_start_loc, seq_lens, scale)
 

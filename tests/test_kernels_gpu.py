@@ -112,8 +112,9 @@ def test_paged_decode_graph_max_len(gpu):
     _close(out, exp, 0.02, 0.02, "decode-maxlen")
 
 
-@pytest.mark.parametrize("D,G", [(64, 4), (128, 2), (128, 8), (128, 1), (64, 8)])
-def test_paged_prefill(gpu, D, G):
+@pytest.mark.parametrize("version", [2, 3])
+@pytest.mark.parametrize("D,G", [(64, 4), (128, 2), (128, 8), (128, 1), (64, 8), (64, 1)])
+def test_paged_prefill(gpu, D, G, version):
     hkv = 2
     hq = hkv * G
     # (context already cached, new query tokens): plain prefill, chunked continuation, 1-token tail
@@ -129,12 +130,13 @@ def test_paged_prefill(gpu, D, G):
     sl = torch.tensor(seq_lens, dtype=torch.int32)
     scale = 1 / math.sqrt(D)
     out = ops.paged_attention_prefill(q, kv[:, 1], bt.to(gpu), qsl_t.to(gpu), sl.to(gpu), scale,
-                                      max(n for _, n in specs))
+                                      max(n for _, n in specs), version=version)
     exp = ref.paged_attention(q.cpu(), kv[:, 1].cpu(), bt, qsl_t, sl, scale)
-    _close(out, exp, 0.03, 0.03, "prefill")
+    _close(out, exp, 0.03, 0.03, f"prefill v{version}")
 
 
-def test_prefill_softmax_rescale_spike(gpu):
+@pytest.mark.parametrize("version", [2, 3])
+def test_prefill_softmax_rescale_spike(gpu, version):
     """Force the online-softmax rescale: one key much larger late in the sequence (rule 26)."""
     D, G, hkv = 64, 4, 1
     lens = [256]
@@ -143,7 +145,7 @@ def test_prefill_softmax_rescale_spike(gpu):
     nb_idx = int(bt[0, 200 // 16])
     kv[nb_idx, 1, 0, 0, 200 % 16, :] = q[255, 0] * 4  # spike key 200 for query 255
     out = ops.paged_attention_prefill(q, kv[:, 1], bt.to(gpu), torch.tensor([0, 256], dtype=torch.int32, device=gpu),
-                                      torch.tensor(lens, dtype=torch.int32, device=gpu), 0.125, 256)
+                                      torch.tensor(lens, dtype=torch.int32, device=gpu), 0.125, 256, version=version)
     exp = ref.paged_attention(q.cpu(), kv[:, 1].cpu(), bt, torch.tensor([0, 256], dtype=torch.int32),
                               torch.tensor(lens, dtype=torch.int32), 0.125)
     _close(out, exp, 0.03, 0.03, "prefill-spike")
