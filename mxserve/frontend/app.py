@@ -46,6 +46,13 @@ def _err(status: int, message: str, etype: str = "invalid_request_error") -> JSO
     return JSONResponse({"error": {"message": message, "type": etype, "code": status}}, status_code=status)
 
 
+try:  # a stream cut mid-body surfaces as aiohttp.ClientPayloadError, not a ConnectionError
+    import aiohttp as _aiohttp
+    _STREAM_ERRORS = (ConnectionError, OSError, asyncio.TimeoutError, _aiohttp.ClientError)
+except ImportError:  # pragma: no cover
+    _STREAM_ERRORS = (ConnectionError, OSError, asyncio.TimeoutError)
+
+
 @dataclass
 class TokenEvent:
     token_id: int
@@ -69,8 +76,10 @@ class LocalWorker:
 
 
 class Frontend:
-    def __init__(self, router_mode: str = "kv", ttl: float = 10.0, namespace: str = "default"):
+    def __init__(self, router_mode: str = "kv", ttl: float = 10.0, namespace: str = "default",
+                 migrate: bool = True):
         self.registry = Registry(ttl=ttl)
+        self.migrate = migrate  # move a broken stream to another worker (prompt + generated re-prefilled)
         self.router = Router(self.registry, router_mode)
         self.metrics = FrontendMetrics()
         self.namespace = namespace
@@ -144,41 +153,58 @@ class Frontend:
                 yield TokenEvent(d["t"], d["f"], d["r"], d["p"], d["c"])
 
     async def generate_tokens(self, model: str, token_ids: list, sampling: dict, rid: str) -> AsyncIterator[TokenEvent]:
-        """Route + stream, retrying on another worker if one fails before the first token."""
+        """Route + stream.  A worker that fails before the first token is retried elsewhere; one that
+        fails MID-stream (connection lost, stream cut without a final event) is migrated: another
+        worker re-prefills prompt + the tokens generated so far and continues with the remaining
+        budget, so the client sees one uninterrupted stream."""
         tried: set = set()
-        for attempt in range(3):
+        generated: list = []
+        max_tokens = int(sampling.get("max_tokens", 16))
+        for attempt in range(4):
             decode = [w for w in self.registry.list(model) if w.role in ("agg", "decode") and w.worker_id not in tried]
             prefill = [w for w in self.registry.list(model, "prefill")]
             if not decode:
-                raise APIError(503, f"no workers available for model {model}", "service_unavailable")
-            w, overlap = self.router.pick(decode, token_ids)
+                break
+            ids = token_ids + generated
+            sp = sampling
+            if generated:
+                sp = dict(sampling, max_tokens=max_tokens - len(generated),
+                          min_tokens=max(0, int(sampling.get("min_tokens") or 0) - len(generated)))
+            w, overlap = self.router.pick(decode, ids)
             purl = None
             if w.role == "decode" and prefill:
-                pw, _ = self.router.pick(prefill, token_ids)
+                pw, _ = self.router.pick(prefill, ids)
                 purl = pw.url
             if overlap:
                 self.metrics.kv_hit.labels(model).inc(overlap)
-            got_any = False
             w.inflight += 1
             try:
-                async for ev in self._worker_stream(w, token_ids, sampling, rid, purl):
-                    got_any = True
+                async for ev in self._worker_stream(w, ids, sp, rid, purl):
+                    generated.append(ev.token_id)
                     yield ev
-                return
-            except (ConnectionError, OSError, asyncio.TimeoutError) as e:
-                if got_any:
+                    if ev.finished:
+                        return
+                raise ConnectionError(f"worker {w.worker_id} ended the stream early")
+            except _STREAM_ERRORS as e:
+                if generated and not self.migrate:
                     raise
-                log.warning("worker %s failed before first token (%r); retrying", w.worker_id, e)
+                log.warning("worker %s failed after %d tokens (%r); %s", w.worker_id, len(generated), e,
+                            "migrating" if generated else "retrying")
+                if generated:
+                    self.metrics.migrations.labels(model).inc()
                 tried.add(w.worker_id)
                 try:
                     import aiohttp
-                    if isinstance(e, aiohttp.ClientConnectionError):
+                    if isinstance(e, aiohttp.ClientConnectionError) and not generated:
                         self.registry.deregister(w.worker_id)
                 except ImportError:
                     pass
             finally:
                 w.inflight -= 1
-        raise APIError(503, "all workers failed", "service_unavailable")
+        if generated:
+            raise ConnectionError("request could not be migrated: no other worker")
+        raise APIError(503, f"no workers available for model {model}" if not tried else "all workers failed",
+                       "service_unavailable")
 
     # ---------------------------------------------------------------- OpenAI layer
     def context_limit(self, model: str) -> int:

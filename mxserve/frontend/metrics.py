@@ -34,6 +34,8 @@ class FrontendMetrics:
         self.workers = Gauge("dynamo_frontend_workers", "Registered workers", ["model", "role"], registry=r)
         self.kv_hit = Counter("dynamo_frontend_kv_router_overlap_blocks", "Prefix blocks matched by the KV router",
                               ["model"], registry=r)
+        self.migrations = Counter("dynamo_frontend_request_migrations", "Streams moved to another worker mid-request",
+                                  ["model"], registry=r)
 
     def render(self) -> bytes:
         return generate_latest(self.registry)

@@ -59,6 +59,7 @@ class Worker:
         self.role = self.args.disagg_mode
         self.model = self.args.name
         self.metrics = WorkerMetrics()
+        self.faults = FAULTS  # tests may give one worker its own Faults
         self.agent = KVTransferAgent(self.engine.runner, self.args.kv_transfer_backend)
         if self.role == "decode":  # allocate + export the staging arena before traffic arrives
             self.agent.descriptor()
@@ -80,9 +81,9 @@ class Worker:
                 self._stored.extend(stored)
                 self._removed.extend(removed)
         self.metrics.gen_tokens.labels(self.model).inc(len(outs))
-        if FAULTS.active():
-            FAULTS.step_delay()
-            FAULTS.count_tokens(len(outs))
+        if self.faults.active():
+            self.faults.step_delay()
+            self.faults.count_tokens(len(outs))
 
     def take_events(self):
         with self._events_lock:
@@ -109,7 +110,7 @@ class Worker:
                 async for o in self.aeng.stream(rid, q):
                     yield _line(o)
                 return
-        drop = FAULTS.hit("drop_stream")
+        drop = self.faults.hit("drop_stream")
         n = 0
         async for o in self.aeng.generate(toks, sp, rid):
             n += 1
@@ -167,7 +168,7 @@ class Worker:
     async def _prefill(self, body: dict) -> dict:
         """Prefill side: compute, push KV into the decode worker's pool, return the first token."""
         rid = body["request_id"]
-        if FAULTS.hit("fail_prefill"):
+        if self.faults.hit("fail_prefill"):
             raise RuntimeError("fault injection: prefill rejected")
         toks = list(body["token_ids"])
         sp = _sampling(body.get("sampling", {}))

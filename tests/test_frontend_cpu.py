@@ -231,3 +231,35 @@ def test_disagg_prefill_failure_falls_back_to_local():
         fs.stop()
         pw.aeng.shutdown()
         dw.aeng.shutdown()
+
+
+def test_mid_stream_migration_keeps_greedy_output():
+    """a worker that drops the stream after its first token; the frontend re-prefills
+    prompt + generated tokens on the other worker and the client sees the same greedy text."""
+    from mxserve.utils.tracing import Faults
+    fe = Frontend(router_mode="round_robin", ttl=30)
+    fs = Server(fe.app).start()
+    a, as_ = _worker(fs.url, role="agg")
+    b, bs_ = _worker(fs.url, role="agg")
+    a.worker_id, b.worker_id = "flaky", "healthy"
+    a.faults = Faults("drop_stream:1.0")
+    as_.start()
+    bs_.start()
+    body = {"model": MODEL, "messages": [{"role": "user", "content": "migrate me"}], "max_tokens": 12,
+            "temperature": 0, "ignore_eos": True}
+    try:
+        wait_for(lambda: len(fe.registry.list()) == 2)
+        outs = [httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=120).json() for _ in range(2)]
+        texts = {o["choices"][0]["message"]["content"] for o in outs}
+        assert len(texts) == 1, outs  # one request hit the flaky worker first, the other did not
+        assert all(o["usage"]["completion_tokens"] == 12 for o in outs)
+        text = httpx.get(fs.url + "/metrics").text
+        assert "dynamo_frontend_request_migrations_total" in text
+        assert any(ln.startswith("dynamo_frontend_request_migrations_total") and not ln.endswith(" 0.0")
+                   for ln in text.splitlines())
+    finally:
+        as_.stop()
+        bs_.stop()
+        fs.stop()
+        a.aeng.shutdown()
+        b.aeng.shutdown()
