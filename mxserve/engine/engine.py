@@ -18,6 +18,7 @@ from .kv_manager import KVCacheManager
 from .model_runner import ModelRunner
 from .request import Request, SamplingParams, Status
 from .scheduler import Scheduler
+from ..utils.tracing import ROCTX
 
 log = logging.getLogger(__name__)
 
@@ -110,7 +111,11 @@ class LLMEngine:
         so = self.scheduler.schedule()
         handle = None
         if not so.is_empty:
-            handle = self.runner.launch(so)
+            if ROCTX.lib is not None:  # MXS_ROCTX=1: named ranges on the rocprofv3 timeline
+                with ROCTX.range(f"step {self.num_steps} d{len(so.decodes)} p{len(so.prefills)}"):
+                    handle = self.runner.launch(so)
+            else:
+                handle = self.runner.launch(so)
             for s in so.prefills:
                 self.num_prompt_computed += s.num_new_tokens
             self.num_steps += 1

@@ -27,8 +27,8 @@ def main(argv=None) -> None:
     import uvicorn
     from .app import Frontend
     a = build_parser().parse_args(argv)
-    logging.basicConfig(level=os.environ.get("MXS_LOG_LEVEL", "INFO"),
-                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    from ..utils.logs import setup_logging
+    setup_logging()
     fe = Frontend(router_mode=a.router_mode, ttl=a.lease_ttl, namespace=a.namespace)
     if a.local_model:
         from ..config import EngineArgs, env_overrides

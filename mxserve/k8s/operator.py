@@ -185,7 +185,8 @@ def main(argv=None) -> None:
     ap.add_argument("--server", default=None, help="apiserver URL (default: in-cluster / kubeconfig)")
     ap.add_argument("--no-podmonitors", action="store_true")
     a = ap.parse_args(argv)
-    logging.basicConfig(level="INFO", format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    from ..utils.logs import setup_logging
+    setup_logging()
     op = Operator(KubeClient(a.server) if a.server else KubeClient(), a.namespace, not a.no_podmonitors)
     op.run(a.interval)
 

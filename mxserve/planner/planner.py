@@ -221,7 +221,8 @@ def main(argv=None) -> None:
     ap.add_argument("--server", default=None)
     ap.add_argument("--dry-run", action="store_true")
     a = ap.parse_args(argv)
-    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    from ..utils.logs import setup_logging
+    setup_logging()
     from ..k8s.client import KubeClient
     cfg = PlannerConfig(namespace=a.namespace, dgd=a.dgd, model=a.model, ttft_ms=a.ttft, itl_ms=a.itl,
                         interval_s=a.interval, cooldown_s=a.cooldown, max_gpus=a.max_gpus, dry_run=a.dry_run)

@@ -310,8 +310,8 @@ def advertise_url(wargs: WorkerArgs, port: int) -> str:
 
 def serve(wargs: WorkerArgs) -> None:
     import uvicorn
-    logging.basicConfig(level=os.environ.get("MXS_LOG_LEVEL", "INFO"),
-                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    from ..utils.logs import setup_logging
+    setup_logging()
     if wargs.engine.tensor_parallel_size > 1:
         from .tp import start_tp_group
         start_tp_group(wargs.engine)

@@ -66,7 +66,8 @@ def follower_main() -> None:
     from ..engine.model_runner import ModelRunner
     from ..models.config import get_model_config
     from ..parallel.comm import init_distributed
-    logging.basicConfig(level=os.environ.get("MXS_LOG_LEVEL", "INFO"))
+    from ..utils.logs import setup_logging
+    setup_logging()
     args = EngineArgs(**json.loads(os.environ["MXS_TP_ARGS"]))
     rank = int(os.environ["RANK"])
     use_gpu = args.resolved_device() == "cuda"
