@@ -64,8 +64,9 @@ def _run(cmd: list[str]) -> None:
 
 def build_rt(force: bool = False) -> str:
     out = os.path.join(ROOT, "mxserve", "_rt" + _ext_suffix())
-    srcs = sorted(glob.glob(os.path.join(ROOT, "csrc", "runtime", "*.cpp")))
-    if force or _stale(out, srcs):
+    rdir = os.path.join(ROOT, "csrc", "runtime")
+    srcs = sorted(p for p in glob.glob(os.path.join(rdir, "*.cpp")) if not os.path.basename(p).startswith("test_"))
+    if force or _stale(out, srcs + glob.glob(os.path.join(rdir, "*.h"))):
         _run(["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", *_pybind_includes(),
               *srcs, "-o", out])
     return out
