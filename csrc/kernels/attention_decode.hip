@@ -82,6 +82,11 @@ __device__ __forceinline__ float wave_max_tok(float v) {
   return perm32_max(v);
 }
 
+__device__ __forceinline__ int decode_part_len(int L, int P) {
+  const int per = (L + P - 1) / P;
+  return ((per + 127) / 128) * 128;
+}
+
 template <int D, int G>
 __global__ void __launch_bounds__(256) paged_decode_kernel(
     bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml,
@@ -101,6 +106,10 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   const int kvh = blockIdx.x, seq = blockIdx.y, part = blockIdx.z;
   const int P = gridDim.z;
   const int L = seq_lens[seq];
+  // part_len 0: split THIS sequence evenly over the P partitions (multiples of 128 tokens).  The
+  // grid of a captured decode graph is sized for max_model_len, so a fixed length would leave the
+  // high partitions empty and the low ones doing all the work.
+  if (part_len <= 0) part_len = decode_part_len(L, P);
   const int start = part * part_len;
   if (start >= L) return;
   const int end = min(start + part_len, L);
@@ -328,6 +337,7 @@ __global__ void __launch_bounds__(D) paged_decode_reduce_kernel(bf16_t* __restri
                                                                 const int* __restrict__ seq_lens, int Hq, int P,
                                                                 int part_len) {
   const int head = blockIdx.x, seq = blockIdx.y, d = threadIdx.x;
+  if (part_len <= 0) part_len = decode_part_len(seq_lens[seq], P);
   const int np = min(P, (seq_lens[seq] + part_len - 1) / part_len);
   const size_t base = (static_cast<size_t>(seq) * Hq + head) * P;
   float M = -INFINITY;

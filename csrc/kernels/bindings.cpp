@@ -108,7 +108,8 @@ void paged_attention_decode(at::Tensor out, at::Tensor q, at::Tensor kv, at::Ten
   mxs::launch_paged_decode(bf(out), P > 1 ? tmp_out.data_ptr<float>() : nullptr,
                            P > 1 ? tmp_ml.data_ptr<float>() : nullptr, bf(q), bf(kv), kv.stride(0),
                            block_tables.data_ptr<int>(), block_tables.stride(0), seq_lens.data_ptr<int>(), B, Hq,
-                           Hkv, D, P, part_len, static_cast<float>(scale), stream());
+                           Hkv, D, P, /*part_len: split each sequence evenly*/ 0, static_cast<float>(scale),
+                           stream());
 }
 
 void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Tensor block_tables, at::Tensor qsl,
