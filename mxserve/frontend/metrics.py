@@ -53,7 +53,7 @@ class WorkerMetrics:
         self.running = Gauge("dynamo_component_num_requests_running", "Running requests", ["model"], registry=r)
         self.waiting = Gauge("dynamo_component_num_requests_waiting", "Waiting requests", ["model"], registry=r)
         self.gen_tokens = Counter("dynamo_component_generation_tokens", "Generated tokens", ["model"], registry=r)
-        self.kv_xfer_bytes = Counter("dynamo_component_kv_transfer_bytes", "KV bytes moved P->D", ["model"],
+        self.kv_xfer_bytes = Counter("dynamo_component_kv_transfer_bytes", "KV bytes moved P->D", ["model", "backend"],
                                      registry=r)
         self.kv_xfer_lat = Histogram("dynamo_component_kv_transfer_seconds", "KV transfer latency", ["model"],
                                      buckets=_LAT, registry=r)

@@ -155,7 +155,8 @@ class Worker:
             self.aeng.push(out)
             if "transfer_s" in res:
                 self.metrics.kv_xfer_lat.labels(self.model).observe(float(res["transfer_s"]))
-                self.metrics.kv_xfer_bytes.labels(self.model).inc(len(target["block_ids"]) * self.agent.block_bytes)
+                self.metrics.kv_xfer_bytes.labels(self.model, target["backend"]).inc(
+                    len(target["block_ids"]) * self.agent.block_bytes)
             return q
         except Exception as e:  # noqa: BLE001 - SURVEY §5.3: fall back to local prefill
             log.warning("remote prefill failed for %s (%r); prefilling locally", rid, e)

@@ -1,0 +1,81 @@
+"""End-to-end disaggregated serving on the GPU: the OpenAI frontend (this process,
+CPU only) + a prefill worker and a decode worker started exactly as the manifests start them
+(`python -m dynamo.vllm --is-prefill-worker / --is-decode-worker`), both on GPU 0.  The decode
+worker reserves blocks and an extent of its IPC staging arena, the prefill worker computes the
+prompt and pushes the KV blocks with the copy kernel, the decode worker lands them and streams the
+rest.  Runs first in the GPU suite (file name) because the parent must not have initialised HIP
+before it starts GPU child processes."""
+import os
+import subprocess
+import sys
+import time
+
+import httpx
+import pytest
+
+from mxserve.frontend.app import Frontend
+from tests.serving_utils import Server, free_port, wait_for
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MODEL = "small-llama"
+
+
+def _worker(role: str, fe_url: str, port: int, log):
+    cmd = [sys.executable, "-m", "dynamo.vllm", "--model", MODEL, f"--is-{role}-worker", "--frontend-url", fe_url,
+           "--host", "127.0.0.1", "--port", str(port), "--num-gpu-blocks-override", "4096", "--max-model-len",
+           "4096", "--max-num-seqs", "16", "--enforce-eager", "--worker-id", f"{role}-0"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MXS_KV_STAGING_BYTES=str(1 << 30),
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    return subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT)
+
+
+def test_disaggregated_chat_over_ipc(tmp_path):
+    import torch
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    if torch.cuda.is_initialized():
+        pytest.skip("HIP already initialised in the test process; run this file on its own")
+    fe = Frontend(router_mode="kv", ttl=60)
+    fs = Server(fe.app).start()
+    logs = {r: open(tmp_path / f"{r}.log", "w") for r in ("prefill", "decode")}
+    ports = {r: free_port() for r in logs}
+    procs = {r: _worker(r, fs.url, ports[r], logs[r]) for r in logs}
+    try:
+        def ready():
+            for r, p in procs.items():
+                if p.poll() is not None:
+                    raise RuntimeError(f"{r} worker exited:\n" + (tmp_path / f"{r}.log").read_text()[-4000:])
+            return len(fe.registry.list()) == 2
+        wait_for(ready, timeout=240, interval=1.0)
+        body = {"model": MODEL, "messages": [{"role": "user", "content": "disaggregated " * 40}], "max_tokens": 24,
+                "temperature": 0, "ignore_eos": True}
+        r = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=120)
+        assert r.status_code == 200, r.text
+        d = r.json()
+        assert d["usage"]["completion_tokens"] == 24
+        # the prompt's KV came from the prefill worker over the IPC staging arena (not host-staged)
+        m = httpx.get(f"http://127.0.0.1:{ports['decode']}/metrics", timeout=10).text
+        moved = [ln for ln in m.splitlines()
+                 if ln.startswith("dynamo_component_kv_transfer_bytes_total") and 'backend="xgmi"' in ln]
+        assert moved and float(moved[0].split()[-1]) > 0, m[-2000:]
+        # streaming through the same path, several requests at once
+        t0 = time.time()
+        outs = []
+        for i in range(4):
+            b = dict(body, messages=[{"role": "user", "content": f"request {i} " * 30}], max_tokens=8)
+            outs.append(httpx.post(fs.url + "/v1/chat/completions", json=b, timeout=120))
+        assert all(o.status_code == 200 and o.json()["usage"]["completion_tokens"] == 8 for o in outs)
+        assert time.time() - t0 < 120
+    finally:
+        for p in procs.values():
+            p.terminate()
+        for p in procs.values():
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        fs.stop()
+        for f in logs.values():
+            f.close()

@@ -152,7 +152,7 @@ def test_disaggregated_matches_aggregated():
         disagg = r.json()["choices"][0]["message"]["content"]
         assert pw.agent.backend == "host"
         # the decode worker really received the prompt's KV from the prefill worker
-        assert dw.metrics.kv_xfer_bytes.labels(MODEL)._value.get() > 0
+        assert dw.metrics.kv_xfer_bytes.labels(MODEL, "host")._value.get() > 0
         # aggregated reference with the same weights (same seed)
         agg, ags = _worker(None, role="agg")
         ags.start()
