@@ -224,6 +224,7 @@ class AsyncEngine:
                 self._queues.pop(o.request_id, None)
 
     def _fail_all(self) -> list:
+        self.engine._inflight = None  # the failed step's results are never collected
         outs = []
         for rid in list(self.engine.requests):
             self.engine.abort(rid)

@@ -75,3 +75,40 @@ def test_async_abort_in_flight():
         outs += eng.step()
     assert all(o.request_id == "b" for o in outs)
     assert eng.kv.num_free() == 256 and eng.kv.check_invariants()
+
+
+def test_async_engine_survives_a_failed_step():
+    """A step that raises fails the requests in flight (error outputs) and the engine keeps serving."""
+    import asyncio
+    from mxserve.engine.engine import AsyncEngine
+    eng = _engine(True)
+    aeng = AsyncEngine(eng)
+    real = eng.runner.launch
+    calls = {"n": 0}
+
+    def flaky(so):
+        calls["n"] += 1
+        if calls["n"] == 3:
+            raise RuntimeError("injected step failure")
+        return real(so)
+
+    eng.runner.launch = flaky
+
+    async def run(rid):
+        out = []
+        async for o in aeng.generate(list(range(3, 30)), SamplingParams(max_tokens=6, ignore_eos=True), rid):
+            out.append(o)
+        return out
+
+    async def main():
+        first = await run("a")
+        second = await run("b")
+        return first, second
+
+    try:
+        first, second = asyncio.run(main())
+    finally:
+        aeng.shutdown()
+    assert first[-1].finished and first[-1].finish_reason == "error"
+    assert [o.finish_reason for o in second if o.finished] == ["length"] and len(second) == 6
+    assert eng.kv.check_invariants() and eng._inflight is None
