@@ -16,6 +16,10 @@ class EngineArgs:
     device: str = "auto"  # "auto" | "cuda" | "cpu"
     dtype: str = "bfloat16"
     tensor_parallel_size: int = 1
+    # MoE expert parallelism over the TP ranks: "allreduce" (each rank runs its experts over the
+    # replicated batch, partial outputs summed by the TP all-reduce) or "a2a" (token slices
+    # dispatched to expert owners with all-to-all, mxserve/parallel/expert.py)
+    moe_dispatch: str = "allreduce"
     block_size: int = 16
     max_model_len: int = 8192
     max_num_seqs: int = 256

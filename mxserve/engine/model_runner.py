@@ -104,7 +104,7 @@ class ModelRunner:
         self.dtype = _DTYPES[args.dtype] if self.is_gpu else torch.float32
         self.bs = args.block_size
         t0 = time.time()
-        self.model = build_model(cfg, self.device, self.dtype)
+        self.model = build_model(cfg, self.device, self.dtype, args.moe_dispatch)
         self.weight_source = load_weights(self.model, args.load_format, args.seed)
         log.info("weights (%s) ready in %.1fs", self.weight_source, time.time() - t0)
         self.max_blocks_per_seq = math.ceil(args.max_model_len / self.bs)

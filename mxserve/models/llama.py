@@ -56,8 +56,12 @@ def _shard_cols(w: torch.Tensor, rank: int, size: int) -> torch.Tensor:
 class TransformerLM:
     """Weights live in a flat dict of tensors (no nn.Module overhead on the hot path)."""
 
-    def __init__(self, cfg: ModelConfig, device: torch.device, dtype: torch.dtype = torch.bfloat16):
+    def __init__(self, cfg: ModelConfig, device: torch.device, dtype: torch.dtype = torch.bfloat16,
+                 moe_dispatch: str = "allreduce"):
+        if moe_dispatch not in ("allreduce", "a2a"):
+            raise ValueError(f"moe_dispatch must be allreduce|a2a, got {moe_dispatch!r}")
         self.cfg = cfg
+        self.moe_dispatch = moe_dispatch
         self.device = torch.device(device)
         self.dtype = dtype
         tp = get_tp()
@@ -185,6 +189,10 @@ class TransformerLM:
 
     def _mlp(self, i: int, h: torch.Tensor) -> torch.Tensor:
         w, p = self.w, f"l{i}."
+        if self.cfg.is_moe and self.moe_dispatch == "a2a" and self.tp_size > 1:
+            from ..parallel.expert import moe_a2a
+            return moe_a2a(h, w[p + "gate"], w[p + "w13"], w[p + "w2"], self.cfg.num_experts_per_tok,
+                           self.tp_rank, self.tp_size, get_tp().group)
         if self.cfg.is_moe:
             router = F.linear(h, w[p + "gate"])
             tw, tid = ops.moe_topk_softmax(router, self.cfg.num_experts_per_tok)
@@ -230,5 +238,5 @@ def _pad_rows(t: torch.Tensor, n: int) -> torch.Tensor:
     return torch.cat([t, pad])
 
 
-def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16) -> TransformerLM:
-    return TransformerLM(cfg, device, dtype)
+def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, moe_dispatch: str = "allreduce") -> TransformerLM:
+    return TransformerLM(cfg, device, dtype, moe_dispatch)

@@ -45,6 +45,8 @@ def _parser(dialect: str) -> argparse.ArgumentParser:
     ap.add_argument("--seed", type=int, default=None)
     # parallelism
     ap.add_argument("--tensor-parallel-size", "--tp", "--tp-size", dest="tp", type=int, default=None)
+    ap.add_argument("--moe-dispatch", choices=["allreduce", "a2a"], default=None,
+                    help="MoE expert parallelism: partial sums + all-reduce, or all-to-all token dispatch")
     # memory / batching (vLLM names, then SGLang / TRT-LLM aliases)
     ap.add_argument("--block-size", "--page-size", "--tokens-per-block", dest="block_size", type=int, default=None)
     ap.add_argument("--max-model-len", "--context-length", "--max-seq-len", dest="max_model_len", type=int,
@@ -91,6 +93,7 @@ _YAML_MAP = {
     "enable_chunked_prefill": "enable_chunked_prefill", "tokens_per_block": "block_size",
     "max_model_len": "max_model_len", "max_num_seqs": "max_num_seqs", "block_size": "block_size",
     "gpu_memory_utilization": "gpu_memory_utilization", "enforce_eager": "enforce_eager",
+    "moe_dispatch": "moe_dispatch",
 }
 
 
@@ -127,7 +130,7 @@ def parse_worker_args(argv: list[str], dialect: str = "vllm") -> WorkerArgs:
         "gpu_memory_utilization": a.gpu_memory_utilization, "num_gpu_blocks": a.num_gpu_blocks,
         "enforce_eager": a.enforce_eager, "enable_prefix_caching": a.enable_prefix_caching,
         "enable_chunked_prefill": a.enable_chunked_prefill, "device": a.device,
-        "async_scheduling": a.async_scheduling,
+        "async_scheduling": a.async_scheduling, "moe_dispatch": a.moe_dispatch,
         "trust_remote_code": a.trust_remote_code or None, "skip_tokenizer_init": a.skip_tokenizer_init or None,
         "bootstrap_port": a.disaggregation_bootstrap_port,
     }

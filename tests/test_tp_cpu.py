@@ -19,13 +19,13 @@ def _port():
 PROMPTS = [[5, 9, 13, 200, 31, 7, 77, 8, 100, 3] * 3, [44, 45, 46], list(range(60, 140))]
 
 
-def _args(model, tp):
+def _args(model, tp, moe_dispatch="allreduce"):
     from mxserve.config import EngineArgs
     return EngineArgs(model=model, device="cpu", tensor_parallel_size=tp, cpu_num_blocks=128, max_model_len=512,
-                      max_num_batched_tokens=48, load_format="random_full", seed=3)
+                      max_num_batched_tokens=48, load_format="random_full", seed=3, moe_dispatch=moe_dispatch)
 
 
-def _rank(rank, world, port, model, q):
+def _rank(rank, world, port, model, q, moe_dispatch="allreduce"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     torch.set_num_threads(1)
     from mxserve.engine.request import SamplingParams
@@ -33,19 +33,20 @@ def _rank(rank, world, port, model, q):
     init_distributed(world, backend="gloo")
     if rank == 0:
         from mxserve.engine.engine import LLMEngine
-        eng = LLMEngine(_args(model, world))
+        eng = LLMEngine(_args(model, world, moe_dispatch))
         out = eng.generate(PROMPTS, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True))
         eng.shutdown()
         q.put(out)
     else:
         from mxserve.engine.model_runner import ModelRunner
         from mxserve.models.config import get_model_config
-        runner = ModelRunner(_args(model, world), get_model_config(model))
+        runner = ModelRunner(_args(model, world, moe_dispatch), get_model_config(model))
         runner.follower_loop()
 
 
-@pytest.mark.parametrize("model", ["tiny-llama", "tiny-mixtral"])
-def test_tp2_matches_tp1(model):
+@pytest.mark.parametrize("model,moe_dispatch", [("tiny-llama", "allreduce"), ("tiny-mixtral", "allreduce"),
+                                                ("tiny-mixtral", "a2a")])
+def test_tp2_matches_tp1(model, moe_dispatch):
     from mxserve.engine.engine import LLMEngine
     from mxserve.engine.request import SamplingParams
     ref = LLMEngine(_args(model, 1)).generate(PROMPTS, SamplingParams(max_tokens=6, temperature=0.0,
@@ -53,7 +54,7 @@ def test_tp2_matches_tp1(model):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, model, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, model, q, moe_dispatch)) for r in range(2)]
     for p in procs:
         p.start()
     out = q.get(timeout=240)
