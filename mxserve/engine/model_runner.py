@@ -49,7 +49,7 @@ class InputBuffers:
              ("logits_indices", np.int64, "S"), ("seeds", np.int64, "S"), ("steps", np.int64, "S"),
              ("srows", np.int64, "S"),
              ("bt_idx", np.int64, "U"), ("seq_lens", np.int32, "S"), ("qsl", np.int32, "S1"),
-             ("rows", np.int32, "S"), ("top_k", np.int32, "S"), ("bt_val", np.int32, "U"),
+             ("rows", np.int32, "S"), ("sseq", np.int32, "S"), ("top_k", np.int32, "S"), ("bt_val", np.int32, "U"),
              ("temperature", np.float32, "S"), ("top_p", np.float32, "S"))
 
     def __init__(self, T: int, S: int, U: int, device: torch.device, pin: bool):
@@ -266,6 +266,7 @@ class ModelRunner:
         h["seeds"][:ns] = self._row_seed[srows]
         h["steps"][:ns] = steps
         h["srows"][:ns] = srows
+        h["sseq"][:ns] = sample_rows
         if graph_bs > S:  # padding rows of a graph bucket: no cache write, 1-token context, greedy
             h["input_ids"][S:graph_bs] = 0
             h["positions"][S:graph_bs] = 0
@@ -389,7 +390,7 @@ class ModelRunner:
                     seq_lens=d["seq_lens"][:S], qsl=d["qsl"][:S + 1], rows=d["rows"][:S],
                     logits_indices=d["logits_indices"][:ns], temperature=d["temperature"][:ns],
                     top_p=d["top_p"][:ns], top_k=d["top_k"][:ns], seeds=d["seeds"][:ns], steps=d["steps"][:ns],
-                    srows=d["srows"][:ns])
+                    srows=d["srows"][:ns], sseq=d["sseq"][:ns])
 
     def _forward_eager(self, meta: dict, sample: bool):
         S, T, nd = meta["S"], meta["T"], meta["nd"]
@@ -401,7 +402,8 @@ class ModelRunner:
         md = AttnMetadata(positions=v["positions"], slot_mapping=v["slot_mapping"], block_tables=bt,
                           seq_lens=v["seq_lens"], query_start_loc=v["qsl"], logits_indices=v["logits_indices"],
                           num_decodes=nd, num_prefills=S - nd, num_prefill_tokens=T - nd,
-                          max_query_len=meta["max_q"], max_seq_len=meta["max_seq"], prefill_query_start_loc=pq)
+                          max_query_len=meta["max_q"], max_seq_len=meta["max_seq"], prefill_query_start_loc=pq,
+                          sample_seq=v["sseq"])
         inp = v["input_ids"]
         if nd:
             d_in = inp[:nd]

@@ -10,6 +10,7 @@ top-2 MoE block whose experts are sharded over the same ranks (expert parallel, 
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -37,6 +38,7 @@ class AttnMetadata:
     max_query_len: int
     max_seq_len: int
     prefill_query_start_loc: Optional[torch.Tensor] = None  # [P+1] int32, rebased at 0
+    sample_seq: Optional[torch.Tensor] = None  # [S_sample] int32: sequence of each logits row
 
     @property
     def num_tokens(self) -> int:
@@ -62,6 +64,8 @@ class TransformerLM:
             raise ValueError(f"moe_dispatch must be allreduce|a2a, got {moe_dispatch!r}")
         self.cfg = cfg
         self.moe_dispatch = moe_dispatch
+        # last layer of a prefill step: attention/o_proj/MLP only for the rows that produce logits
+        self.prune_last_layer = os.environ.get("MXS_PRUNE_LAST_LAYER", "1") == "1"
         self.device = torch.device(device)
         self.dtype = dtype
         tp = get_tp()
@@ -187,6 +191,30 @@ class TransformerLM:
         out = ops.linear(o.reshape(o.shape[0], -1), w[p + "o"])
         return tp_all_reduce(out)
 
+    def _attention_sampled(self, i: int, h: torch.Tensor, md: AttnMetadata, kv_layer: torch.Tensor):
+        """Last layer of a step with prefill chunks: K/V of every token still go to the cache, but
+        only the rows that produce logits (the last token of each sampled sequence) need attention,
+        o_proj and the MLP.  Each such row is a single query at position seq_len - 1 over its whole
+        context, i.e. exactly a decode query, so it runs on the decode kernel."""
+        c, w, p = self.cfg, self.w, f"l{i}."
+        qkv = ops.linear(h, w[p + "qkv"])
+        q = ops.rope_and_cache(qkv, self.nh, self.nkv, self.hd, md.positions, self.cos_sin, kv_layer,
+                               md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"), c.rms_norm_eps)
+        ns = md.logits_indices.shape[0]
+        if ns == 0:  # no sequence samples this step: the layer only wrote K/V
+            return h.new_empty((0, h.shape[1]))
+        qs = q.index_select(0, md.logits_indices)
+        seq = md.sample_seq.long()
+        bt = md.block_tables.index_select(0, seq)
+        sl = md.seq_lens.index_select(0, seq)
+        if not q.is_cuda:
+            qsl = torch.arange(ns + 1, dtype=torch.int32, device=q.device)
+            o = ref.paged_attention(qs, kv_layer, bt, qsl, sl, self.scale)
+        else:
+            o = ops.paged_attention_decode(qs, kv_layer, bt, sl, self.scale, md.max_seq_len)
+        out = ops.linear(o.reshape(ns, -1), w[p + "o"])
+        return tp_all_reduce(out)
+
     def _mlp(self, i: int, h: torch.Tensor) -> torch.Tensor:
         w, p = self.w, f"l{i}."
         if self.cfg.is_moe and self.moe_dispatch == "a2a" and self.tp_size > 1:
@@ -210,6 +238,8 @@ class TransformerLM:
         c = self.cfg
         x = self.embed(input_ids)
         residual = None
+        # steps with prefill chunks: the last layer only computes the rows that produce logits
+        prune = self.prune_last_layer and md.num_prefills > 0 and md.sample_seq is not None
         for i in range(c.num_layers):
             p = f"l{i}."
             if residual is None:
@@ -217,11 +247,17 @@ class TransformerLM:
                 h = ops.rms_norm(x, self.w[p + "in_norm"], c.rms_norm_eps)
             else:
                 h, residual = ops.fused_add_rms_norm(x, residual, self.w[p + "in_norm"], c.rms_norm_eps)
-            x = self._attention(i, h, md, kv_cache[:, i])
+            if prune and i == c.num_layers - 1:
+                x = self._attention_sampled(i, h, md, kv_cache[:, i])
+                residual = residual.index_select(0, md.logits_indices)
+                if x.shape[0] == 0:  # no sequence samples this step: the layer only wrote K/V
+                    return x
+            else:
+                x = self._attention(i, h, md, kv_cache[:, i])
             h, residual = ops.fused_add_rms_norm(x, residual, self.w[p + "post_norm"], c.rms_norm_eps)
             x = self._mlp(i, h)
         h, _ = ops.fused_add_rms_norm(x, residual, self.w["norm"], c.rms_norm_eps)
-        return h.index_select(0, md.logits_indices)
+        return h if prune else h.index_select(0, md.logits_indices)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         # bf16 on the GPU: the sampling kernel reads bf16 rows directly (no fp32 copy of [B, V])

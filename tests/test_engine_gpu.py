@@ -52,6 +52,47 @@ def test_forward_matches_cpu_reference(gpu, name):
     assert hit > 0.95
 
 
+@pytest.mark.parametrize("name", ["small-llama", "tiny-qwen3-gpu"])
+def test_pruned_last_layer_matches_full(gpu, name):
+    """Prefill steps compute the last layer only for the rows that sample (on the decode kernel);
+    the logits must match the full last layer, and the K/V written must be identical."""
+    cfg = get_model_config(name)
+    sd = random_full_state(cfg, seed=2, std=0.05)
+    lens = [40, 30, 77]
+    n = sum(lens)
+    ids = torch.randint(3, cfg.vocab_size, (n,), generator=torch.Generator().manual_seed(1)).to(gpu)
+    pos, slots, bts, blk = [], [], [], 0
+    for L in lens:
+        nb = (L + 15) // 16
+        pos += list(range(L))
+        slots += [(blk + p // 16) * 16 + p % 16 for p in range(L)]
+        bts.append(list(range(blk, blk + nb)) + [0] * (8 - nb))
+        blk += nb
+    qsl = torch.tensor([0, 40, 70, 147], dtype=torch.int32, device=gpu)
+    # sequence 1 is a mid-prompt chunk: it writes K/V but does not sample
+    sample_seq = torch.tensor([0, 2], dtype=torch.int32, device=gpu)
+    md = AttnMetadata(positions=torch.tensor(pos, device=gpu), slot_mapping=torch.tensor(slots, device=gpu),
+                      block_tables=torch.tensor(bts, dtype=torch.int32, device=gpu),
+                      seq_lens=torch.tensor(lens, dtype=torch.int32, device=gpu), query_start_loc=qsl,
+                      logits_indices=torch.tensor([39, 146], device=gpu), num_decodes=0, num_prefills=3,
+                      num_prefill_tokens=n, max_query_len=77, max_seq_len=77, prefill_query_start_loc=qsl,
+                      sample_seq=sample_seq)
+    m = TransformerLM(cfg, gpu, torch.bfloat16)
+    m.load_full_state(sd)
+    out = {}
+    for prune in (False, True):
+        m.prune_last_layer = prune
+        kv = torch.zeros(blk + 1, cfg.num_layers, 2, cfg.num_kv_heads, 16, cfg.head_dim,
+                         dtype=torch.bfloat16, device=gpu)
+        out[prune] = (m.compute_logits(m.forward(ids, md, kv)).float().cpu(), kv.float().cpu())
+    (full, kv_full), (pruned, kv_pruned) = out[False], out[True]
+    assert pruned.shape == full.shape == (2, cfg.vocab_size)
+    assert torch.equal(kv_full, kv_pruned)
+    scale = full.abs().max().item()
+    assert (pruned - full).abs().max().item() < 0.03 * scale
+    assert (pruned.topk(5, -1).indices == full.argmax(-1, keepdim=True)).any(-1).all()
+
+
 def _engine(gpu, eager, **kw):
     args = EngineArgs(model="small-llama", device="cuda", num_gpu_blocks=2048, max_model_len=2048,
                       max_num_seqs=32, cuda_graph_max_bs=32, enforce_eager=eager, load_format="random", seed=5, **kw)
