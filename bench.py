@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--max-warmup-s", type=float, default=120.0,
+                    help="cap on the extra warmup that waits for the first finished request")
     return ap.parse_args()
 
 
@@ -88,6 +90,8 @@ class Driver:
         self.last_tok: dict = {}
         self.itls: list = []
         self.record = False
+        self.finished = 0
+        self.warmup_steps = 0
         self.c = {"ttft": [], "tokens": 0}
 
     def due(self) -> list:
@@ -105,7 +109,8 @@ class Driver:
         if self.nxt < self.horizon:
             time.sleep(max(0.0, self.t_start + self.arrivals[self.nxt] - time.perf_counter()))
 
-    def token(self, rid: str, now: float) -> None:
+    def token(self, rid: str, now: float, finished: bool = False) -> None:
+        self.finished += finished
         if rid not in self.first_tok:
             self.first_tok[rid] = now
             if self.record:
@@ -120,7 +125,7 @@ class Driver:
         ttft = np.array(self.c["ttft"]) if self.c["ttft"] else np.array([np.nan])
         itl = np.array(self.itls) if self.itls else np.array([np.nan])
         return [dt, float(self.c["tokens"]), float(np.nanmedian(ttft)), float(np.nanmedian(itl)),
-                float(len(self.c["ttft"]))]
+                float(len(self.c["ttft"])), float(self.warmup_steps)]
 
 
 def timed_phases(a, step, barrier, drv, on_phase=lambda phase: None) -> float:
@@ -129,10 +134,13 @@ def timed_phases(a, step, barrier, drv, on_phase=lambda phase: None) -> float:
     barrier()
     vlog("warmup")
     drv.t_start = time.perf_counter()
-    for i in range(a.warmup):
+    i = 0
+    while i < a.warmup or (drv.finished == 0 and time.perf_counter() - drv.t_start < a.max_warmup_s):
         step()
         if i % 200 == 0:
             vlog(f"warmup step {i}: {drv.nxt} arrivals, {len(drv.first_tok)} first tokens")
+        i += 1
+    drv.warmup_steps = i
     on_phase("timed")
     barrier()
     vlog("timed")
@@ -159,7 +167,7 @@ def run_agg(a, eng, sp, drv, barrier) -> float:
         outs = eng.step()
         now = time.perf_counter()
         for o in outs:
-            drv.token(o.request_id, now)
+            drv.token(o.request_id, now, o.finished)
 
     return timed_phases(a, step, barrier, drv)
 
@@ -225,7 +233,7 @@ def run_disagg_decode(a, eng, sp, drv, barrier, conn) -> float:
             outs = eng.step()
             now = time.perf_counter()
             for o in outs:
-                drv.token(o.request_id, now)
+                drv.token(o.request_id, now, o.finished)
         elif inflight:  # nothing to decode yet: block until a prefill lands (or an arrival is due)
             conn.poll(0.05)
 
@@ -334,7 +342,7 @@ def main():
         vlog("paired")
         if is_prefill:
             run_disagg_prefill(eng, a.temperature, barrier, conn)
-            local_stats = [0.0, 0.0, float("nan"), float("nan"), 0.0]
+            local_stats = [0.0, 0.0, float("nan"), float("nan"), 0.0, float("nan")]
         else:
             drv = Driver(a, rank, eng.model_config.vocab_size, 2 * a.qps)
             local_stats = drv.stats(run_disagg_decode(a, eng, sp, drv, barrier, conn))
@@ -365,6 +373,7 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "warmup_steps_executed": int(np.nanmax(col[:, 5])),
             "ms_per_step": round(t_max / a.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
