@@ -21,6 +21,8 @@ void launch_paged_prefill(bf16_t*, const bf16_t*, const bf16_t*, long, const int
                           int, int, int, int, int, float, int, hipStream_t);
 void launch_sample(int64_t*, const void*, bool, int, int, long, const float*, const float*, const int*,
                    const int64_t*, const int64_t*, hipStream_t);
+void launch_logprobs(float*, int64_t*, float*, const void*, bool, int, int, long, const int64_t*, const int64_t*, int,
+                     hipStream_t);
 void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStream_t);
 void launch_moe_align(int*, int*, const int*, int, int, int, hipStream_t);
 bool launch_skinny_gemm(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, hipStream_t);
@@ -141,6 +143,25 @@ void sample(at::Tensor out, at::Tensor logits, at::Tensor temperature, at::Tenso
                      top_k.data_ptr<int>(), seeds.data_ptr<int64_t>(), steps.data_ptr<int64_t>(), stream());
 }
 
+// log-probs of the sampled token + the K best tokens for logits rows `rows`
+void logprobs(at::Tensor tok_lp, at::Tensor top_ids, at::Tensor top_lp, at::Tensor logits, at::Tensor rows,
+              at::Tensor tokens) {
+  CHECK_CUDA(logits);
+  TORCH_CHECK((logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16) && logits.stride(1) == 1,
+              "logits must be fp32 or bf16 rows");
+  TORCH_CHECK(rows.scalar_type() == at::kLong && tokens.scalar_type() == at::kLong, "int64 rows / tokens");
+  const int n = rows.size(0);
+  TORCH_CHECK(tokens.size(0) == n && tok_lp.size(0) == n && top_ids.size(0) == n && top_lp.size(0) == n, "row count");
+  TORCH_CHECK(tok_lp.scalar_type() == at::kFloat && top_lp.scalar_type() == at::kFloat &&
+                  top_ids.scalar_type() == at::kLong && top_ids.is_contiguous() && top_lp.is_contiguous(),
+              "output dtypes");
+  const int K = top_ids.dim() == 2 ? top_ids.size(1) : 0;
+  TORCH_CHECK(K >= 0 && K <= 20 && top_lp.size(-1) == K, "top_logprobs must be in [0, 20]");
+  mxs::launch_logprobs(tok_lp.data_ptr<float>(), top_ids.data_ptr<int64_t>(), top_lp.data_ptr<float>(),
+                       logits.data_ptr(), logits.scalar_type() == at::kBFloat16, n, logits.size(1), logits.stride(0),
+                       rows.data_ptr<int64_t>(), tokens.data_ptr<int64_t>(), K, stream());
+}
+
 // out[M,N] = x[M,K] . w[N,K]^T for M <= 256; false if the shape is unsupported (caller falls back)
 bool skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
@@ -193,6 +214,7 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("kv"), pybind11::arg("block_tables"), pybind11::arg("qsl"), pybind11::arg("seq_lens"),
         pybind11::arg("scale"), pybind11::arg("max_q_len"), pybind11::arg("version") = 3);
   m.def("sample", &sample);
+  m.def("logprobs", &logprobs);
   m.def("moe_topk_softmax", &moe_topk_softmax);
   m.def("moe_align", &moe_align);
   m.def("skinny_gemm", &skinny_gemm);

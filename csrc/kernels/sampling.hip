@@ -172,4 +172,78 @@ void launch_sample(int64_t* out, const void* logits, bool bf16, int B, int V, lo
   MXS_CHECK_LAUNCH();
 }
 
+// Log-probabilities for the rows that asked for them (OpenAI `logprobs` / `top_logprobs`).
+// One workgroup per selected row: one pass for the row's log-sum-exp (online max / rescaled sum,
+// merged across lanes and waves), then the sampled token's log-prob and the K best tokens by K
+// block-argmax passes, each excluding everything at or above the previous pick in (value desc,
+// index asc) order.  K <= 20, and only requesting rows are touched, so the extra reads are a few
+// hundred KB of L2-resident logits per row.  Log-probs are of the raw model distribution (before
+// temperature / top-k / top-p), as vLLM reports them.
+template <typename T>
+__global__ void __launch_bounds__(1024) logprobs_kernel(float* __restrict__ tok_lp, int64_t* __restrict__ top_ids,
+                                                        float* __restrict__ top_lp, const T* __restrict__ logits,
+                                                        int V, long row_stride, const int64_t* __restrict__ rows,
+                                                        const int64_t* __restrict__ tokens, int K) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  __shared__ float sm[16], ss[16];
+  const int b = blockIdx.x;
+  const T* z = logits + rows[b] * row_stride;
+  float m = -INFINITY, s = 0.f;
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    const float x = ld(z, v);
+    if (x > m) {
+      s = s * __expf(m - x) + 1.f;
+      m = x;
+    } else {
+      s += __expf(x - m);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    const float M = fmaxf(m, m2);
+    s = (M == -INFINITY) ? 0.f : s * __expf(m - M) + s2 * __expf(m2 - M);
+    m = M;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) {
+    sm[wid] = m;
+    ss[wid] = s;
+  }
+  __syncthreads();
+  float M = sm[0];
+  for (int w = 1; w < nw; ++w) M = fmaxf(M, sm[w]);
+  float S = 0.f;
+  for (int w = 0; w < nw; ++w) S += sm[w] == -INFINITY ? 0.f : ss[w] * __expf(sm[w] - M);
+  const float lse = M + logf(S);
+  if (threadIdx.x == 0) tok_lp[b] = ld(z, static_cast<int>(tokens[b])) - lse;
+  ArgMax prev{INFINITY, -1};
+  for (int j = 0; j < K; ++j) {
+    ArgMax a{-INFINITY, 0x7FFFFFFF};
+    for (int v = threadIdx.x; v < V; v += blockDim.x) {
+      const float x = ld(z, v);
+      if (x < prev.v || (x == prev.v && v > prev.i)) a = better(a, ArgMax{x, v});
+    }
+    const ArgMax r = block_argmax(a, sv, si);
+    if (threadIdx.x == 0) {
+      top_ids[b * K + j] = r.i < V ? r.i : 0;
+      top_lp[b * K + j] = r.v - lse;
+    }
+    prev = r;
+  }
+}
+
+void launch_logprobs(float* tok_lp, int64_t* top_ids, float* top_lp, const void* logits, bool bf16, int n, int V,
+                     long row_stride, const int64_t* rows, const int64_t* tokens, int K, hipStream_t s) {
+  if (n == 0) return;
+  if (bf16)
+    hipLaunchKernelGGL(logprobs_kernel<bf16_t>, dim3(n), dim3(1024), 0, s, tok_lp, top_ids, top_lp,
+                       static_cast<const bf16_t*>(logits), V, row_stride, rows, tokens, K);
+  else
+    hipLaunchKernelGGL(logprobs_kernel<float>, dim3(n), dim3(1024), 0, s, tok_lp, top_ids, top_lp,
+                       static_cast<const float*>(logits), V, row_stride, rows, tokens, K);
+  MXS_CHECK_LAUNCH();
+}
+
 }  // namespace mxs

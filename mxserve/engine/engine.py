@@ -32,6 +32,8 @@ class StepOutput:
     num_prompt_tokens: int
     num_cached_tokens: int
     num_output_tokens: int
+    logprob: Optional[float] = None  # of token_id, when the request asked for logprobs
+    top_logprobs: Optional[list] = None  # [(token_id, logprob)] best first
 
 
 class LLMEngine:
@@ -84,7 +86,8 @@ class LLMEngine:
         self.requests[request_id] = req
         return req
 
-    def complete_remote_prefill(self, request_id: str, first_token: int) -> StepOutput:
+    def complete_remote_prefill(self, request_id: str, first_token: int, logprob: Optional[float] = None,
+                                top_logprobs: Optional[list] = None) -> StepOutput:
         req = self.scheduler.complete_remote(request_id, first_token)
         fin = req.is_finished
         if fin:
@@ -92,7 +95,8 @@ class LLMEngine:
             self.runner.release(request_id)
         self.num_generated += 1
         return StepOutput(req.request_id, int(first_token), fin, req.status.value if fin else None,
-                          req.num_prompt_tokens, req.num_cached_tokens, len(req.output_token_ids))
+                          req.num_prompt_tokens, req.num_cached_tokens, len(req.output_token_ids), logprob,
+                          top_logprobs)
 
     def release_prefill_blocks(self, request_id: str) -> None:
         """Prefill side: drop the blocks kept alive for the KV transfer."""
@@ -126,16 +130,19 @@ class LLMEngine:
         if done is None:
             return []
         dso, dh = done
-        return self._land(dso, self.runner.collect(dh))
+        sampled = self.runner.collect(dh)
+        return self._land(dso, sampled, dh.get("logprobs"))
 
-    def _land(self, so, sampled: dict) -> list[StepOutput]:
+    def _land(self, so, sampled: dict, logprobs: Optional[dict] = None) -> list[StepOutput]:
         emitted = self.scheduler.update(so, sampled)
         outs = []
         for req in emitted:
             fin = req.is_finished
+            lp = logprobs.get(req.request_id) if logprobs else None
             outs.append(StepOutput(req.request_id, req.output_token_ids[-1], fin,
                                    req.status.value if fin else None, req.num_prompt_tokens,
-                                   req.num_cached_tokens, len(req.output_token_ids)))
+                                   req.num_cached_tokens, len(req.output_token_ids),
+                                   lp[0] if lp else None, lp[1] if lp else None))
             self.num_generated += 1
             if fin:
                 self.runner.release(req.request_id)

@@ -128,6 +128,8 @@ class ModelRunner:
         self._row_topp = np.ones(n_rows, dtype=np.float32)
         self._row_topk = np.zeros(n_rows, dtype=np.int32)
         self._row_seed = np.zeros(n_rows, dtype=np.int64)
+        self._row_lp = np.full(n_rows, -1, dtype=np.int32)  # top_logprobs per row; -1 = no logprobs
+        self._logits: Optional[torch.Tensor] = None  # last step's logits rows (logprobs read them)
         self.max_tokens_per_step = args.max_num_batched_tokens + args.max_num_seqs
         self.buf = InputBuffers(self.max_tokens_per_step, n_rows,
                                 self.max_tokens_per_step // self.bs + 4 * self.max_blocks_per_seq + n_rows,
@@ -185,6 +187,7 @@ class ModelRunner:
             self._row_topp[row] = sp.top_p
             self._row_topk[row] = sp.top_k
             self._row_seed[row] = req.seed
+            self._row_lp[row] = -1 if sp.logprobs is None else int(sp.logprobs)
         gen, synced = self._row_state[rid]
         ids = req.block_ids
         n = len(ids)
@@ -283,8 +286,14 @@ class ModelRunner:
         elif U:
             h["bt_idx"][:U] = upd_idx
             h["bt_val"][:U] = upd_val
+        lp = None
+        if ns:
+            lpk = self._row_lp[srows]
+            if (lpk >= 0).any():
+                sel = np.nonzero(lpk >= 0)[0]
+                lp = (sel.tolist(), int(lpk[sel].max()))
         return dict(S=S, T=T, nd=nd, max_q=max_q, max_seq=max(lens), sample_rows=sample_rows, U=U,
-                    big_update=big_update, graph_bs=graph_bs)
+                    big_update=big_update, graph_bs=graph_bs, lp=lp)
 
     def _upload(self, meta: dict) -> None:
         self.buf.upload()
@@ -322,6 +331,15 @@ class ModelRunner:
         handle = {"so": so, "rows": meta["sample_rows"]}
         if ids is None:
             return handle
+        lp = None
+        if meta.get("lp") is not None:
+            sel, k = meta["lp"]
+            rows = torch.tensor(sel, dtype=torch.int64).to(self.device, non_blocking=True)
+            with torch.inference_mode():
+                lp = ops.logprobs(self._logits, rows, ids.index_select(0, rows), k)
+            if self.is_gpu:
+                lp = tuple(t.to("cpu", non_blocking=True) for t in lp)  # pageable: lands by the event below
+            handle["lp_sel"] = sel
         if self.is_gpu:
             self._out_slot ^= 1
             pinned = self._out_pinned[self._out_slot][:ids.shape[0]]
@@ -331,10 +349,13 @@ class ModelRunner:
             handle.update(pinned=pinned, ev=ev)
         else:
             handle["ids"] = ids
+        if lp is not None:
+            handle["lp"] = lp
         return handle
 
     def collect(self, handle: Optional[dict]) -> dict[str, int]:
-        """Wait for a launched step's sampled ids; {request_id: token}."""
+        """Wait for a launched step's sampled ids; {request_id: token}.  Log-probs, when any row
+        asked for them, are left in handle["logprobs"] = {request_id: (logprob, [(id, logprob)])}."""
         if handle is None:
             return {}
         if "ev" in handle:
@@ -345,7 +366,12 @@ class ModelRunner:
         else:
             return {}
         reqs = handle["so"].all()
-        return {reqs[r].req.request_id: ids[k] for k, r in enumerate(handle["rows"])}
+        rows = handle["rows"]
+        if "lp" in handle:
+            tok_lp, top_ids, top_lp = (t.tolist() for t in handle["lp"])
+            handle["logprobs"] = {reqs[rows[k]].req.request_id: (tok_lp[j], list(zip(top_ids[j], top_lp[j])))
+                                  for j, k in enumerate(handle["lp_sel"])}
+        return {reqs[r].req.request_id: ids[k] for k, r in enumerate(rows)}
 
     def execute(self, so: SchedulerOutput) -> dict[str, int]:
         return self.collect(self.launch(so))
@@ -355,8 +381,9 @@ class ModelRunner:
         """Run one step on this rank; returns the device tensor of sampled ids (or None)."""
         self._upload(meta)
         if meta["graph_bs"]:
-            g, out = self.graphs[meta["graph_bs"]]
+            g, out, logits = self.graphs[meta["graph_bs"]]
             g.replay()
+            self._logits = logits
             return out[:meta["S"]]
         return self._forward_eager(meta, sample=bool(meta["sample_rows"]))
 
@@ -412,12 +439,13 @@ class ModelRunner:
         if not sample:
             return None
         logits = self.model.compute_logits(hidden)
+        self._logits = logits
         ids = ops.sample(logits, v["temperature"], v["top_p"], v["top_k"], v["seeds"], v["steps"])
         self.last_tok.index_copy_(0, v["srows"], ids)
         return ids
 
     # ------------------------------------------------------------------ hipGraph decode
-    def _graph_body(self, b: int) -> torch.Tensor:
+    def _graph_body(self, b: int) -> tuple:
         v = self._views(b, b, b)
         rows = v["rows"].long()
         bt = self.bt_dev.index_select(0, rows)
@@ -432,7 +460,7 @@ class ModelRunner:
         logits = self.model.compute_logits(hidden)
         ids = ops.sample(logits, v["temperature"], v["top_p"], v["top_k"], v["seeds"], v["steps"])
         self.last_tok.index_copy_(0, v["srows"], ids)
-        return ids
+        return ids, logits
 
     def _capture_graphs(self) -> None:
         maxb = min(self.args.cuda_graph_max_bs, self.args.max_num_seqs)
@@ -462,8 +490,8 @@ class ModelRunner:
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool):
-                    out = self._graph_body(b)
-                self.graphs[b] = (g, out)
+                    out, logits = self._graph_body(b)
+                self.graphs[b] = (g, out, logits)
         torch.cuda.synchronize()
         log.info("captured %d decode graphs (%s) in %.1fs", len(buckets), buckets, time.time() - t0)
 

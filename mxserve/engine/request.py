@@ -17,6 +17,8 @@ class SamplingParams:
     stop_token_ids: list = field(default_factory=list)
     ignore_eos: bool = False
     min_tokens: int = 0
+    # log-probs of the sampled tokens: None = off, k >= 0 = also the k most likely tokens (k <= 20)
+    logprobs: Optional[int] = None
 
     @classmethod
     def from_openai(cls, body: dict, default_max_tokens: int = 256) -> "SamplingParams":
@@ -31,6 +33,7 @@ class SamplingParams:
             stop_token_ids=list(body.get("stop_token_ids") or []),
             ignore_eos=bool(body.get("ignore_eos", False)),
             min_tokens=int(body.get("min_tokens", 0) or 0),
+            logprobs=body.get("logprobs"),
         )
 
 

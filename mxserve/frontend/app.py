@@ -60,6 +60,8 @@ class TokenEvent:
     finish_reason: Optional[str]
     num_prompt_tokens: int
     num_cached_tokens: int
+    logprob: Optional[float] = None
+    top_logprobs: Optional[list] = None  # [(token_id, logprob)]
 
 
 class LocalWorker:
@@ -72,7 +74,8 @@ class LocalWorker:
     async def generate(self, token_ids, sampling: dict, request_id: str, prefill_url=None) -> AsyncIterator[TokenEvent]:
         from ..worker.server import _sampling
         async for o in self.aeng.generate(token_ids, _sampling(sampling), request_id):
-            yield TokenEvent(o.token_id, o.finished, o.finish_reason, o.num_prompt_tokens, o.num_cached_tokens)
+            yield TokenEvent(o.token_id, o.finished, o.finish_reason, o.num_prompt_tokens, o.num_cached_tokens,
+                             o.logprob, o.top_logprobs)
 
 
 class Frontend:
@@ -150,7 +153,7 @@ class Frontend:
                 d = json.loads(line)
                 if d["t"] < 0:
                     raise RuntimeError("worker failed the request")
-                yield TokenEvent(d["t"], d["f"], d["r"], d["p"], d["c"])
+                yield TokenEvent(d["t"], d["f"], d["r"], d["p"], d["c"], d.get("lp"), d.get("tlp"))
 
     async def generate_tokens(self, model: str, token_ids: list, sampling: dict, rid: str) -> AsyncIterator[TokenEvent]:
         """Route + stream.  A worker that fails before the first token is retried elsewhere; one that
@@ -211,7 +214,25 @@ class Frontend:
         lens = [w.max_model_len for w in self.registry.list(model) if w.max_model_len > 0]
         return min(lens) if lens else self.model_cfg(model).max_position_embeddings
 
-    def _sampling(self, body: dict, model: str, n_prompt: int) -> dict:
+    @staticmethod
+    def _logprobs_arg(body: dict, chat: bool) -> Optional[int]:
+        """OpenAI: chat `logprobs: bool` + `top_logprobs: 0..20`; completions `logprobs: int`."""
+        if chat:
+            top = body.get("top_logprobs")
+            if not body.get("logprobs"):
+                if top:
+                    raise APIError(400, "top_logprobs requires logprobs to be true")
+                return None
+            k = int(top or 0)
+        else:
+            if body.get("logprobs") is None:
+                return None
+            k = int(body["logprobs"])
+        if not 0 <= k <= 20:
+            raise APIError(400, "top logprobs must be between 0 and 20")
+        return k
+
+    def _sampling(self, body: dict, model: str, n_prompt: int, chat: bool = True) -> dict:
         limit = self.context_limit(model)
         if n_prompt >= limit:
             raise APIError(400, f"This model's maximum context length is {limit} tokens; the prompt has "
@@ -231,13 +252,15 @@ class Frontend:
                 "top_p": 1.0 if tp is None else float(tp), "top_k": int(body.get("top_k") or 0),
                 "seed": body.get("seed"), "ignore_eos": bool(body.get("ignore_eos", False)),
                 "min_tokens": int(body.get("min_tokens") or 0),
-                "stop_token_ids": list(body.get("stop_token_ids") or [])}
+                "stop_token_ids": list(body.get("stop_token_ids") or []),
+                "logprobs": self._logprobs_arg(body, chat)}
 
     async def _run(self, endpoint: str, body: dict, prompt_ids: list, model: str, chat: bool,
                    xrid: Optional[str] = None):
         stream = bool(body.get("stream", False))
         rtype = "stream" if stream else "unary"
-        sampling = self._sampling(body, model, len(prompt_ids))
+        sampling = self._sampling(body, model, len(prompt_ids), chat)
+        want_lp = sampling["logprobs"] is not None
         stops = body.get("stop") or []
         if isinstance(stops, str):
             stops = [stops]
@@ -278,15 +301,19 @@ class Frontend:
             TRACER.finish(trace)
 
         async def events():
-            """Yields (text_delta, finish_reason|None).  With stop strings, text that could still be
-            the start of a stop string is held back until it is disambiguated."""
+            """Yields (text_delta, finish_reason|None, logprob events).  With stop strings, text that
+            could still be the start of a stop string is held back until it is disambiguated; the
+            log-probs of the tokens behind held-back text travel with the next delta."""
             detok = IncrementalDetokenizer(tok)
             full, emitted = "", 0
             hold = max((len(x) for x in stops if x), default=1) - 1
+            lps: list = []
             async for ev in self.generate_tokens(model, prompt_ids, sampling, rid):
                 on_token()
                 eos_hit = ev.finished and ev.finish_reason == "stop" and ev.token_id in tok.eos_token_ids
                 full += "" if eos_hit else detok.add(ev.token_id)
+                if want_lp and not eos_hit and ev.logprob is not None:
+                    lps.append(ev)
                 if ev.finished:
                     full += detok.flush()
                 reason = ("stop" if ev.finish_reason == "abort" else ev.finish_reason) if ev.finished else None
@@ -294,23 +321,49 @@ class Frontend:
                     lo = max(0, emitted - hold)
                     hits = [i for i in (full.find(x, lo) for x in stops if x) if i >= 0]
                     if hits:
-                        yield full[emitted:min(hits)], "stop"
+                        yield full[emitted:min(hits)], "stop", lps
                         return
                     end = len(full) if ev.finished else max(emitted, len(full) - hold)
                 else:
                     end = len(full)
                 delta = full[emitted:end]
                 emitted = end
-                yield delta, reason
+                if delta or reason:
+                    yield delta, reason, lps
+                    lps = []
                 if ev.finished:
                     return
+
+        def tok_str(t: int) -> str:
+            return tok.decode([int(t)], skip_special_tokens=False)
+
+        def lp_payload(evs: list, offset: int = 0):
+            """OpenAI logprobs object for these tokens (chat: content list; completions: arrays)."""
+            if not want_lp:
+                return None
+            if chat:
+                def ent(t, lp):
+                    s = tok_str(t)
+                    return {"token": s, "logprob": lp, "bytes": list(s.encode("utf-8", "replace"))}
+                return {"content": [dict(ent(e.token_id, e.logprob),
+                                         top_logprobs=[ent(t, lp) for t, lp in (e.top_logprobs or [])])
+                                    for e in evs]}
+            toks = [tok_str(e.token_id) for e in evs]
+            offs, o = [], offset
+            for s in toks:
+                offs.append(o)
+                o += len(s)
+            return {"tokens": toks, "token_logprobs": [e.logprob for e in evs],
+                    "top_logprobs": [{tok_str(t): lp for t, lp in (e.top_logprobs or [])} for e in evs],
+                    "text_offset": offs}
 
         obj = "chat.completion" if chat else "text_completion"
         if not stream:
             try:
-                parts, reason = [], None
-                async for d, r in events():
+                parts, reason, lp_evs = [], None, []
+                async for d, r, evs in events():
                     parts.append(d)
+                    lp_evs.extend(evs)
                     reason = r or reason
             except APIError:
                 finish("error")
@@ -322,6 +375,8 @@ class Frontend:
             text = "".join(parts)
             choice = ({"index": 0, "message": {"role": "assistant", "content": text}, "finish_reason": reason or "stop"}
                       if chat else {"index": 0, "text": text, "logprobs": None, "finish_reason": reason or "stop"})
+            if want_lp:
+                choice["logprobs"] = lp_payload(lp_evs)
             return JSONResponse({"id": rid, "object": obj, "created": created, "model": model, "choices": [choice],
                                  "usage": {"prompt_tokens": len(prompt_ids), "completion_tokens": state["n"],
                                            "total_tokens": len(prompt_ids) + state["n"]}})
@@ -329,7 +384,9 @@ class Frontend:
         include_usage = bool((body.get("stream_options") or {}).get("include_usage"))
         chunk_obj = "chat.completion.chunk" if chat else "text_completion"
 
-        def chunk(delta: Optional[str], reason: Optional[str], first: bool = False) -> bytes:
+        sent = {"chars": 0}
+
+        def chunk(delta: Optional[str], reason: Optional[str], first: bool = False, evs: tuple = ()) -> bytes:
             if chat:
                 d = {}
                 if first:
@@ -337,8 +394,12 @@ class Frontend:
                 if delta is not None:
                     d["content"] = delta
                 ch = {"index": 0, "delta": d, "finish_reason": reason}
+                if want_lp and not first:
+                    ch["logprobs"] = lp_payload(list(evs))
             else:
-                ch = {"index": 0, "text": delta or "", "logprobs": None, "finish_reason": reason}
+                ch = {"index": 0, "text": delta or "", "logprobs": lp_payload(list(evs), sent["chars"]),
+                      "finish_reason": reason}
+                sent["chars"] += len(delta or "")
             return ("data: " + json.dumps({"id": rid, "object": chunk_obj, "created": created, "model": model,
                                            "choices": [ch]}) + "\n\n").encode()
 
@@ -347,9 +408,9 @@ class Frontend:
             try:
                 if chat:
                     yield chunk("", None, first=True)
-                async for d, r in events():
+                async for d, r, evs in events():
                     if d or r:
-                        yield chunk(d if d else ("" if r else None), r)
+                        yield chunk(d if d else ("" if r else None), r, evs=evs)
                 if include_usage:
                     yield ("data: " + json.dumps({"id": rid, "object": chunk_obj, "created": created, "model": model,
                                                   "choices": [], "usage": {"prompt_tokens": len(prompt_ids),

@@ -148,6 +148,18 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
     return ref.sample(logits, temperature, top_p, top_k, seeds, steps)
 
 
+def logprobs(logits: torch.Tensor, rows: torch.Tensor, tokens: torch.Tensor, k: int):
+    """(token log-prob [n], top ids [n, k], top log-probs [n, k]) for logits rows `rows`."""
+    if _gpu(logits):
+        n = rows.shape[0]
+        tok_lp = torch.empty(n, dtype=torch.float32, device=logits.device)
+        top_ids = torch.empty(n, k, dtype=torch.int64, device=logits.device)
+        top_lp = torch.empty(n, k, dtype=torch.float32, device=logits.device)
+        ext().logprobs(tok_lp, top_ids, top_lp, logits, rows, tokens)
+        return tok_lp, top_ids, top_lp
+    return ref.logprobs(logits, rows, tokens, k)
+
+
 # ----------------------------------------------------------------------------- MoE
 def moe_topk_softmax(router_logits: torch.Tensor, k: int):
     if _gpu(router_logits):

@@ -202,6 +202,17 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
     return out.to(logits.device)
 
 
+def logprobs(logits: torch.Tensor, rows: torch.Tensor, tokens: torch.Tensor, k: int):
+    """Raw-distribution log-probs: the sampled token's, and the k best (value desc, index asc)."""
+    lp = torch.log_softmax(logits.index_select(0, rows.long()).float(), dim=-1)
+    tok_lp = lp.gather(1, tokens.long().view(-1, 1)).squeeze(1)
+    if k == 0:
+        return tok_lp, torch.zeros(len(rows), 0, dtype=torch.int64), torch.zeros(len(rows), 0)
+    # stable order on ties: sort by index first, then a stable sort by value
+    order = torch.sort(lp, dim=-1, descending=True, stable=True)
+    return tok_lp, order.indices[:, :k].contiguous(), order.values[:, :k].contiguous()
+
+
 # ----------------------------------------------------------------------------- MoE
 def moe_topk_softmax(router_logits: torch.Tensor, k: int, renormalize: bool = True):
     probs = torch.softmax(router_logits.float(), dim=-1)

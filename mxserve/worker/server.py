@@ -42,12 +42,16 @@ def _sampling(d: dict) -> SamplingParams:
     return SamplingParams(max_tokens=int(d.get("max_tokens", 16)), temperature=float(d.get("temperature", 1.0)),
                           top_p=float(d.get("top_p", 1.0)), top_k=int(d.get("top_k", 0)), seed=d.get("seed"),
                           stop_token_ids=list(d.get("stop_token_ids", [])), ignore_eos=bool(d.get("ignore_eos")),
-                          min_tokens=int(d.get("min_tokens", 0)))
+                          min_tokens=int(d.get("min_tokens", 0)),
+                          logprobs=None if d.get("logprobs") is None else int(d["logprobs"]))
 
 
 def _line(o: StepOutput) -> bytes:
-    return (json.dumps({"t": o.token_id, "f": o.finished, "r": o.finish_reason, "p": o.num_prompt_tokens,
-                        "c": o.num_cached_tokens}) + "\n").encode()
+    d = {"t": o.token_id, "f": o.finished, "r": o.finish_reason, "p": o.num_prompt_tokens, "c": o.num_cached_tokens}
+    if o.logprob is not None:
+        d["lp"] = o.logprob
+        d["tlp"] = o.top_logprobs or []
+    return (json.dumps(d) + "\n").encode()
 
 
 class Worker:
@@ -148,7 +152,7 @@ class Worker:
             def land_and_complete(tok: int):
                 if start is not None:  # staging extent -> pool blocks, on the engine's stream
                     self.agent.land(start, dst)
-                return self.engine.complete_remote_prefill(rid, tok)
+                return self.engine.complete_remote_prefill(rid, tok, res.get("logprob"), res.get("top_logprobs"))
 
             out = await self.aeng.submit(land_and_complete, int(res["first_token"]))
             start = None
@@ -174,9 +178,9 @@ class Worker:
         toks = list(body["token_ids"])
         sp = _sampling(body.get("sampling", {}))
         sp.max_tokens = 1
-        first = None
+        first = first_lp = None
         async for o in self.aeng.generate(toks, sp, rid, disagg_role="prefill_only"):
-            first = o.token_id
+            first, first_lp = o.token_id, o
         req = self.engine.requests.get(rid)
         target = body["kv_target"]
         skip = int(target.get("skip_blocks", 0))
@@ -201,8 +205,11 @@ class Worker:
                 xfer_s = time.perf_counter() - t0
         finally:
             self.aeng.submit_nowait(self.engine.release_prefill_blocks, rid)
-        return {"first_token": first, "num_cached_tokens": req.num_cached_tokens if req else 0,
-                "transfer_s": xfer_s, "blocks": len(dst)}
+        res = {"first_token": first, "num_cached_tokens": req.num_cached_tokens if req else 0,
+               "transfer_s": xfer_s, "blocks": len(dst)}
+        if first_lp is not None and first_lp.logprob is not None:
+            res.update(logprob=first_lp.logprob, top_logprobs=first_lp.top_logprobs or [])
+        return res
 
     # ---------------------------------------------------------------- app
     def _build_app(self) -> FastAPI:
@@ -299,7 +306,7 @@ class Worker:
 def _sp_dict(sp: SamplingParams) -> dict:
     return {"max_tokens": sp.max_tokens, "temperature": sp.temperature, "top_p": sp.top_p, "top_k": sp.top_k,
             "seed": sp.seed, "stop_token_ids": list(sp.stop_token_ids), "ignore_eos": sp.ignore_eos,
-            "min_tokens": sp.min_tokens}
+            "min_tokens": sp.min_tokens, "logprobs": sp.logprobs}
 
 
 def advertise_url(wargs: WorkerArgs, port: int) -> str:

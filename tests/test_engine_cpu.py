@@ -112,3 +112,31 @@ def test_async_engine_survives_a_failed_step():
     assert first[-1].finished and first[-1].finish_reason == "error"
     assert [o.finish_reason for o in second if o.finished] == ["length"] and len(second) == 6
     assert eng.kv.check_invariants() and eng._inflight is None
+
+
+def test_logprobs_match_log_softmax():
+    """Engine log-probs (sampled token + top-k) equal log_softmax of the model's own logits."""
+    import torch
+    from mxserve.ops import reference as ref
+    from mxserve.engine.request import SamplingParams
+    eng = _engine(True)
+    prompt = list(range(5, 40))
+    req = eng.add_request(prompt, SamplingParams(max_tokens=3, temperature=0.7, seed=3, ignore_eos=True, logprobs=4))
+    plain = eng.add_request(prompt, SamplingParams(max_tokens=3, temperature=0.0, ignore_eos=True))
+    outs = []
+    while eng.has_unfinished():
+        outs += eng.step()
+    mine = [o for o in outs if o.request_id == req.request_id]
+    assert len(mine) == 3 and all(o.logprob is not None and len(o.top_logprobs) == 4 for o in mine)
+    assert all(o.logprob is None for o in outs if o.request_id == plain.request_id)
+    for o in mine:
+        ids = [t for t, _ in o.top_logprobs]
+        lps = [lp for _, lp in o.top_logprobs]
+        assert lps == sorted(lps, reverse=True) and len(set(ids)) == 4
+        assert o.logprob <= lps[0] + 1e-6
+    # values: rerun the first step's logits by hand
+    logits = torch.randn(3, 50)
+    tok = torch.tensor([1, 2, 3])
+    tlp, tid, tv = ref.logprobs(logits, torch.tensor([0, 2]), tok[[0, 2]], 5)
+    want = torch.log_softmax(logits, -1)
+    assert torch.allclose(tlp, want[[0, 2], [1, 3]]) and torch.equal(tid, want[[0, 2]].topk(5).indices)

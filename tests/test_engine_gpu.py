@@ -137,6 +137,25 @@ def test_chunked_prefill_and_prefix_cache_invariance(gpu):
     assert t1 == t2 == t3
 
 
+def test_logprobs_graph_and_eager(gpu):
+    """Log-probs come back from hipGraph decode steps and eager prefill steps; a greedy pick is the
+    top-1 alternative; requests without logprobs in the same batch are unaffected."""
+    eng = _engine(gpu, False)
+    assert eng.runner.graphs
+    lp_req = eng.add_request(list(range(20, 90)), SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True,
+                                                                  logprobs=5))
+    other = eng.add_request(list(range(30, 60)), SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
+    outs = []
+    while eng.has_unfinished():
+        outs += eng.step()
+    mine = [o for o in outs if o.request_id == lp_req.request_id]
+    assert len(mine) == 8
+    for o in mine:
+        assert o.logprob is not None and o.logprob <= 1e-4 and len(o.top_logprobs) == 5
+        assert o.top_logprobs[0][0] == o.token_id or abs(o.top_logprobs[0][1] - o.logprob) < 1e-3
+    assert all(o.logprob is None for o in outs if o.request_id == other.request_id)
+
+
 def test_sampling_reproducible_with_seed(gpu):
     eng = _engine(gpu, False)
     sp = SamplingParams(max_tokens=16, temperature=0.8, top_p=0.9, seed=1234, ignore_eos=True)

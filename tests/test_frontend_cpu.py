@@ -135,6 +135,42 @@ def test_stop_strings(agg_stack):
     assert cut["choices"][0]["finish_reason"] == "stop"
 
 
+def test_logprobs_chat_and_completions(agg_stack):
+    """OpenAI logprobs: chat (`logprobs` + `top_logprobs`, unary and SSE) and completions
+    (`logprobs: k`); greedy picks are the top-1 alternative and log-probs are <= 0."""
+    _, fs, _ = agg_stack
+    body = {"model": MODEL, "messages": [{"role": "user", "content": "logprobs please"}], "max_tokens": 6,
+            "temperature": 0, "ignore_eos": True, "logprobs": True, "top_logprobs": 3}
+    d = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=60).json()
+    content = d["choices"][0]["logprobs"]["content"]
+    assert len(content) == 6
+    for e in content:
+        assert e["logprob"] <= 1e-6 and isinstance(e["token"], str) and isinstance(e["bytes"], list)
+        tops = e["top_logprobs"]
+        assert len(tops) == 3 and tops[0]["logprob"] >= tops[1]["logprob"] >= tops[2]["logprob"]
+        assert abs(tops[0]["logprob"] - e["logprob"]) < 1e-4  # greedy: the sampled token is the best
+    assert "".join(e["token"] for e in content) == d["choices"][0]["message"]["content"]
+    streamed = []
+    with httpx.stream("POST", fs.url + "/v1/chat/completions", json=dict(body, stream=True), timeout=60) as r:
+        for line in r.iter_lines():
+            if line.startswith("data: ") and line != "data: [DONE]":
+                ch = json.loads(line[6:])["choices"][0]
+                if ch.get("logprobs"):
+                    streamed += ch["logprobs"]["content"]
+    assert [e["logprob"] for e in streamed] == pytest.approx([e["logprob"] for e in content], abs=1e-5)
+    c = httpx.post(fs.url + "/v1/completions", json={"model": MODEL, "prompt": "abc", "max_tokens": 4,
+                                                     "temperature": 0, "ignore_eos": True, "logprobs": 2},
+                   timeout=60).json()
+    lp = c["choices"][0]["logprobs"]
+    assert len(lp["tokens"]) == len(lp["token_logprobs"]) == len(lp["top_logprobs"]) == len(lp["text_offset"]) == 4
+    assert all(len(t) <= 2 for t in lp["top_logprobs"]) and lp["text_offset"][0] == 0
+    r = httpx.post(fs.url + "/v1/chat/completions", json=dict(body, logprobs=False), timeout=60)
+    assert r.status_code == 400  # top_logprobs without logprobs
+    plain = httpx.post(fs.url + "/v1/chat/completions", json=dict(body, logprobs=None, top_logprobs=None),
+                       timeout=60).json()
+    assert plain["choices"][0].get("logprobs") is None
+
+
 def test_disaggregated_matches_aggregated():
     """Prefill worker + decode worker (host-staged KV transfer) give the agg result token for token."""
     fe = Frontend(router_mode="round_robin", ttl=30)

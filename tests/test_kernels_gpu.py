@@ -192,6 +192,27 @@ def test_sample_distribution(gpu):
     assert (freq - p).abs().max().item() < 0.03
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("k", [0, 1, 5, 20])
+def test_logprobs_matches_reference(gpu, dtype, k):
+    """Log-prob kernel vs fp32 log_softmax + stable top-k, on a padded-vocab row view (TP lm_head)."""
+    B, V, Vpad = 12, 128256, 128256 + 64
+    full = (torch.randn(B, Vpad, device=gpu) * 4).to(dtype)
+    logits = full[:, :V]
+    rows = torch.tensor([0, 3, 4, 11], device=gpu)
+    toks = torch.tensor([5, 77, 128255, 1000], device=gpu)
+    tlp, tid, tv = ops.logprobs(logits, rows, toks, k)
+    etlp, etid, etv = ref.logprobs(logits.cpu(), rows.cpu(), toks.cpu(), k)
+    _close(tlp, etlp, 1e-3, 1e-3, "token logprob")
+    assert tid.shape == (4, k) and tv.shape == (4, k)
+    if k:
+        _close(tv, etv, 1e-3, 1e-3, "top logprobs")
+        # bf16 logits tie often: compare ids where the reference values are distinct
+        distinct = torch.cat([etv[:, :-1] != etv[:, 1:], torch.ones(4, 1, dtype=torch.bool)], 1)
+        distinct &= torch.cat([torch.ones(4, 1, dtype=torch.bool), etv[:, 1:] != etv[:, :-1]], 1)
+        assert torch.equal(tid.cpu()[distinct], etid[distinct])
+
+
 def test_moe_topk_softmax(gpu):
     T, E, K = 100, 8, 2
     g = torch.Generator().manual_seed(0)
