@@ -25,6 +25,8 @@ struct ArPeers {
 };
 void launch_custom_allreduce(unsigned short*, const unsigned short*, long, const ArPeers&, int, int, long, unsigned*,
                              unsigned*, hipStream_t);
+void launch_custom_allreduce_2shot(unsigned short*, const unsigned short*, long, const ArPeers&, int, int, long,
+                                   unsigned*, unsigned*, hipStream_t);
 }
 
 namespace {
@@ -102,7 +104,7 @@ int64_t car_read_u32(int64_t ptr) {  // synchronous 4-byte device -> host read (
 }
 
 void custom_allreduce(at::Tensor out, at::Tensor x, std::vector<int64_t> recv_ptrs, std::vector<int64_t> flag_ptrs,
-                      int64_t rank, int64_t slot_elems, int64_t epochs_ptr, int64_t err_ptr) {
+                      int64_t rank, int64_t slot_elems, int64_t epochs_ptr, int64_t err_ptr, bool two_shot) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "x: contiguous bf16 GPU tensor");
   TORCH_CHECK(out.is_contiguous() && out.numel() == x.numel(), "out shape");
   const int n = static_cast<int>(recv_ptrs.size());
@@ -113,10 +115,10 @@ void custom_allreduce(at::Tensor out, at::Tensor x, std::vector<int64_t> recv_pt
     peers.recv[r] = reinterpret_cast<char*>(recv_ptrs[r]);
     peers.flags[r] = reinterpret_cast<unsigned*>(flag_ptrs[r]);
   }
-  mxs::launch_custom_allreduce(reinterpret_cast<unsigned short*>(out.data_ptr()),
-                               reinterpret_cast<const unsigned short*>(x.data_ptr()), x.numel(), peers,
-                               static_cast<int>(rank), n, slot_elems, reinterpret_cast<unsigned*>(epochs_ptr),
-                               reinterpret_cast<unsigned*>(err_ptr), c10::hip::getCurrentHIPStream().stream());
+  auto launch = two_shot ? mxs::launch_custom_allreduce_2shot : mxs::launch_custom_allreduce;
+  launch(reinterpret_cast<unsigned short*>(out.data_ptr()), reinterpret_cast<const unsigned short*>(x.data_ptr()),
+         x.numel(), peers, static_cast<int>(rank), n, slot_elems, reinterpret_cast<unsigned*>(epochs_ptr),
+         reinterpret_cast<unsigned*>(err_ptr), c10::hip::getCurrentHIPStream().stream());
 }
 
 }  // namespace
@@ -125,7 +127,9 @@ void register_comm(pybind11::module_& m) {
   m.def("car_alloc", &car_alloc);
   m.def("car_free", &car_free);
   m.def("car_read_u32", &car_read_u32);
-  m.def("custom_allreduce", &custom_allreduce);
+  m.def("custom_allreduce", &custom_allreduce, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("recv_ptrs"),
+        pybind11::arg("flag_ptrs"), pybind11::arg("rank"), pybind11::arg("slot_elems"), pybind11::arg("epochs_ptr"),
+        pybind11::arg("err_ptr"), pybind11::arg("two_shot") = false);
   m.def("ipc_export_pool", &export_pool);
   m.def("ipc_open_pool", &open_pool);
   m.def("ipc_close_all", &close_all);

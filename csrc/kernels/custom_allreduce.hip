@@ -110,4 +110,108 @@ void launch_custom_allreduce(bf16_t* out, const bf16_t* x, long n, const ArPeers
   MXS_CHECK_LAUNCH();
 }
 
+// Two-shot variant for larger messages (N > 2): reduce-scatter by push, then all-gather by push.
+// Rank q owns slice q (1/N of the vectors).  Phase 1 pushes slice r of the input into rank r's slot
+// [par][rank]; phase 2 sums the N contributions to the owned slice and pushes the result into every
+// rank's slot [par][rank] at the same positions (the phase-1 data there sits at the receiver's own
+// slice: disjoint); phase 3 reads every slice from its owner's slot.  Each xGMI link carries 2/N of
+// the message instead of the one-shot's whole message, for one more flag round trip.  Same
+// buffers, epochs and parity argument as the one-shot kernel (a peer can only get one call ahead:
+// call k+1's phase 2 needs this rank's phase-1 flag of k+1); phase-2 flags live in the second half
+// of the flag page.
+constexpr int kArFlags2 = kArMaxBlocks * kArMaxRanks;
+
+__device__ __forceinline__ void ar_wait(unsigned* f, unsigned e, unsigned* err) {
+  long spins = 0;
+  while (static_cast<int>(ld_flag(f) - e) < 0) {
+    if (++spins > (1L << 26) || ld_flag(err) != 0) {
+      atomicExch(err, 1u);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__global__ void __launch_bounds__(512) custom_allreduce_2shot_kernel(bf16_t* out, const bf16_t* __restrict__ x,
+                                                                     long n, ArPeers peers, int rank, int nranks,
+                                                                     long slot_elems, unsigned* epochs,
+                                                                     unsigned* err) {
+  const int b = blockIdx.x;
+  const long nv = n / 8;
+  const long sl = (nv + nranks - 1) / nranks;
+  const long per = (sl + gridDim.x - 1) / gridDim.x;
+  const long o0 = b * per, o1 = min(sl, o0 + per);
+  __shared__ unsigned s_epoch;
+  if (threadIdx.x == 0) s_epoch = epochs[b] + 1;
+  __syncthreads();
+  const unsigned e = s_epoch;
+  const int par = e & 1;
+  const long my_slot = (static_cast<long>(par) * nranks + rank) * slot_elems * 2;  // bytes
+  // 1. reduce-scatter push: slice r -> rank r
+  const uint4* xs = reinterpret_cast<const uint4*>(x);
+  for (int r = 0; r < nranks; ++r) {
+    uint4* dst = reinterpret_cast<uint4*>(peers.recv[r] + my_slot);
+    const long base = r * sl;
+    for (long o = o0 + threadIdx.x; o < o1; o += blockDim.x) {
+      const long v = base + o;
+      if (v < nv) dst[v] = xs[v];
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < nranks) st_flag(peers.flags[threadIdx.x] + b * kArMaxRanks + rank, e);
+  if (threadIdx.x < nranks) ar_wait(peers.flags[rank] + b * kArMaxRanks + threadIdx.x, e, err);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  // 2. sum the owned slice (fp32, rank order) and push it to every rank
+  const char* mine = peers.recv[rank] + (static_cast<long>(par) * nranks * slot_elems) * 2;
+  {
+    const long base = rank * sl;
+    for (long o = o0 + threadIdx.x; o < o1; o += blockDim.x) {
+      const long v = base + o;
+      if (v >= nv) break;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < nranks; ++r) {
+        const uint4 w = reinterpret_cast<const uint4*>(mine + r * slot_elems * 2)[v];
+        const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          acc[2 * k] += bf2f_lo(u[k]);
+          acc[2 * k + 1] += bf2f_hi(u[k]);
+        }
+      }
+      uint4 rr;
+      rr.x = pack2(acc[0], acc[1]);
+      rr.y = pack2(acc[2], acc[3]);
+      rr.z = pack2(acc[4], acc[5]);
+      rr.w = pack2(acc[6], acc[7]);
+      for (int r = 0; r < nranks; ++r) reinterpret_cast<uint4*>(peers.recv[r] + my_slot)[v] = rr;
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < nranks) st_flag(peers.flags[threadIdx.x] + kArFlags2 + b * kArMaxRanks + rank, e);
+  if (threadIdx.x < nranks) ar_wait(peers.flags[rank] + kArFlags2 + b * kArMaxRanks + threadIdx.x, e, err);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  // 3. gather: slice q from slot [par][q] (local memory)
+  uint4* o = reinterpret_cast<uint4*>(out);
+  for (int q = 0; q < nranks; ++q) {
+    const uint4* src = reinterpret_cast<const uint4*>(mine + q * slot_elems * 2);
+    const long base = q * sl;
+    for (long oo = o0 + threadIdx.x; oo < o1; oo += blockDim.x) {
+      const long v = base + oo;
+      if (v < nv) o[v] = src[v];
+    }
+  }
+  if (threadIdx.x == 0) epochs[b] = e;
+}
+
+void launch_custom_allreduce_2shot(bf16_t* out, const bf16_t* x, long n, const ArPeers& peers, int rank,
+                                   int nranks, long slot_elems, unsigned* epochs, unsigned* err, hipStream_t s) {
+  hipLaunchKernelGGL(custom_allreduce_2shot_kernel, dim3(kArMaxBlocks), dim3(512), 0, s, out, x, n, peers, rank,
+                     nranks, slot_elems, epochs, err);
+  MXS_CHECK_LAUNCH();
+}
+
 }  // namespace mxs

@@ -1,7 +1,10 @@
-"""Custom one-shot IPC all-reduce for tensor-parallel decode.
+"""Custom IPC all-reduce for tensor-parallel decode.
 
-Kernel: csrc/kernels/custom_allreduce.hip (push into every peer's receive slot over the xGMI mesh,
-flag, sum locally).  This module owns the buffers: each rank allocates uncached receive slots
+Kernels: csrc/kernels/custom_allreduce.hip.  One-shot (push the whole input into every peer's
+receive slot over the xGMI mesh, flag, sum locally) for small messages; two-shot (reduce-scatter
+by push, all-gather by push: each link carries 2/N of the message, one more flag round trip) from
+`two_shot_min_bytes` up when there are more than 2 ranks (MXS_CAR_TWO_SHOT_MIN_BYTES, default
+512 KiB: 70B TP8 decode at batch >= 32).  This module owns the buffers: each rank allocates uncached receive slots
 (2 parities x N ranks x max_bytes) and a 64 KiB signal page, exports both with hipIpc, exchanges
 the handles over the CPU group and maps every peer's.  All sizes stay far below 2 GiB (the
 dmabuf IPC size rule in mxserve/disagg/kv_transfer.py).
@@ -14,6 +17,7 @@ steps) then turns the path off for good and every later all-reduce uses RCCL.
 from __future__ import annotations
 
 import logging
+import os
 from typing import Optional
 
 import torch
@@ -38,6 +42,7 @@ class CustomAllReduce:
         self.err_ptr = sig + _ERR_OFF
         self.device = device
         self.disabled = False
+        self.two_shot_min_bytes = int(os.environ.get("MXS_CAR_TWO_SHOT_MIN_BYTES", str(512 << 10)))
 
     @classmethod
     def create(cls, group, device: Optional[torch.device] = None, max_bytes: int = 8 << 20,
@@ -72,8 +77,9 @@ class CustomAllReduce:
         """Sum of x over the group (in place unless `out` is given)."""
         from .. import ops
         out = x if out is None else out
+        two_shot = self.world > 2 and x.numel() * 2 >= self.two_shot_min_bytes
         ops.ext().custom_allreduce(out, x, self.recv_ptrs, self.flag_ptrs, self.rank, self.slot_elems,
-                                   self.epochs_ptr, self.err_ptr)
+                                   self.epochs_ptr, self.err_ptr, two_shot)
         return out
 
     def check(self) -> bool:

@@ -11,7 +11,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [8, 2048, 4096 * 8, 1 << 20, 4096 * 8, 8]
+SIZES = [8, 2048, 4096 * 8, 1 << 20, 4096 * 8 + 8, 8, 24, 1 << 21]
 
 
 def _rank(rank, world, port, q):
@@ -22,6 +22,7 @@ def _rank(rank, world, port, q):
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         car = CustomAllReduce.create(dist.group.WORLD, torch.device("cuda:0"), max_bytes=4 << 20)
+        assert car.world == world
         errs = []
 
         def inp(n, call):  # exact in bf16: small integers
@@ -30,7 +31,11 @@ def _rank(rank, world, port, q):
         def want(n, call):
             return sum(((torch.arange(n, device="cuda:0") % 13) + r * 3 + call) for r in range(world)).float()
 
-        for call, n in enumerate(SIZES):
+        # pass 0: default choice (one-shot below 512 KiB, two-shot above for world > 2);
+        # pass 1: two-shot for every size (world > 2), interleaved epochs with pass 0's calls
+        calls = [(n, 0) for n in SIZES] + [(n, 1) for n in SIZES]
+        for call, (n, forced) in enumerate(calls):
+            car.two_shot_min_bytes = 0 if forced else 512 << 10
             x = inp(n, call)
             if call % 2:
                 out = torch.empty_like(x)
@@ -40,8 +45,9 @@ def _rank(rank, world, port, q):
             torch.cuda.synchronize()
             if not torch.equal(out.float(), want(n, call)):
                 errs.append(f"call {call} n={n}: max err {(out.float() - want(n, call)).abs().max().item()}")
-        # hipGraph: 3 captured all-reduces, replayed twice
-        xs = [inp(4096, 100 + i) for i in range(3)]
+        # hipGraph: 3 captured all-reduces (one two-shot when world > 2), replayed twice
+        car.two_shot_min_bytes = 512 << 10
+        xs = [inp(4096 if i != 1 else 1 << 19, 20 + i) for i in range(3)]
         bufs = [x.clone() for x in xs]
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream()
@@ -58,7 +64,7 @@ def _rank(rank, world, port, q):
             g.replay()
             torch.cuda.synchronize()
             for i, b in enumerate(bufs):
-                if not torch.equal(b.float(), want(4096, 100 + i)):
+                if not torch.equal(b.float(), want(b.numel(), 20 + i)):
                     errs.append(f"graph rep {rep} buf {i}")
         assert car.check(), "error word raised"
         dist.barrier()
@@ -67,7 +73,7 @@ def _rank(rank, world, port, q):
         q.put((rank, [traceback.format_exc()]))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_custom_allreduce_ranks_on_one_gpu(world):
     import socket
     import torch
