@@ -27,6 +27,8 @@ void launch_custom_allreduce(unsigned short*, const unsigned short*, long, const
                              unsigned*, hipStream_t);
 void launch_custom_allreduce_2shot(unsigned short*, const unsigned short*, long, const ArPeers&, int, int, long,
                                    unsigned*, unsigned*, hipStream_t);
+void launch_ipc_all_to_all(void*, const void*, long, const ArPeers&, int, int, long, unsigned*, unsigned*,
+                           hipStream_t);
 }
 
 namespace {
@@ -121,6 +123,27 @@ void custom_allreduce(at::Tensor out, at::Tensor x, std::vector<int64_t> recv_pt
          reinterpret_cast<unsigned*>(err_ptr), c10::hip::getCurrentHIPStream().stream());
 }
 
+// equal splits: out/in hold N segments of seg_bytes each; segment d of `in` goes to rank d
+void ipc_all_to_all(at::Tensor out, at::Tensor in, std::vector<int64_t> recv_ptrs, std::vector<int64_t> flag_ptrs,
+                    int64_t rank, int64_t slot_bytes, int64_t epochs_ptr, int64_t err_ptr) {
+  TORCH_CHECK(in.is_cuda() && in.is_contiguous() && out.is_contiguous(), "contiguous GPU tensors");
+  TORCH_CHECK(in.scalar_type() == out.scalar_type() && in.numel() == out.numel(), "in/out shape");
+  const int n = static_cast<int>(recv_ptrs.size());
+  TORCH_CHECK(n >= 1 && n <= mxs::kArMaxRanks && static_cast<int>(flag_ptrs.size()) == n, "1..8 ranks");
+  const long bytes = in.numel() * in.element_size();
+  TORCH_CHECK(bytes % n == 0, "equal splits");
+  const long seg = bytes / n;
+  TORCH_CHECK(seg % 4 == 0 && seg <= slot_bytes, "segment must be a multiple of 4 bytes and fit a slot");
+  mxs::ArPeers peers{};
+  for (int r = 0; r < n; ++r) {
+    peers.recv[r] = reinterpret_cast<char*>(recv_ptrs[r]);
+    peers.flags[r] = reinterpret_cast<unsigned*>(flag_ptrs[r]);
+  }
+  mxs::launch_ipc_all_to_all(out.data_ptr(), in.data_ptr(), seg, peers, static_cast<int>(rank), n, slot_bytes,
+                             reinterpret_cast<unsigned*>(epochs_ptr), reinterpret_cast<unsigned*>(err_ptr),
+                             c10::hip::getCurrentHIPStream().stream());
+}
+
 }  // namespace
 
 void register_comm(pybind11::module_& m) {
@@ -130,6 +153,7 @@ void register_comm(pybind11::module_& m) {
   m.def("custom_allreduce", &custom_allreduce, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("recv_ptrs"),
         pybind11::arg("flag_ptrs"), pybind11::arg("rank"), pybind11::arg("slot_elems"), pybind11::arg("epochs_ptr"),
         pybind11::arg("err_ptr"), pybind11::arg("two_shot") = false);
+  m.def("ipc_all_to_all", &ipc_all_to_all);
   m.def("ipc_export_pool", &export_pool);
   m.def("ipc_open_pool", &open_pool);
   m.def("ipc_close_all", &close_all);

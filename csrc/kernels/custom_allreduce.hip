@@ -214,4 +214,53 @@ void launch_custom_allreduce_2shot(bf16_t* out, const bf16_t* x, long n, const A
   MXS_CHECK_LAUNCH();
 }
 
+// Equal-split all-to-all over the same IPC slots (EP dispatch / combine of fixed-capacity MoE
+// layouts, SURVEY.md §5.8 "direct peer writes into pre-registered IPC receive buffers"): segment d
+// of the input is pushed into rank d's slot [par][rank], one flag per (block, peer), then segment r
+// of the output is read from this rank's slot [par][r].  Every rank pushes on all N-1 links at
+// once.  Same epochs / flags / parity rule as the all-reduce kernels (calls of both kinds may
+// interleave: every rank issues the same sequence).  V = uint4 when segments are 16-byte multiples.
+template <typename V>
+__global__ void __launch_bounds__(512) ipc_all_to_all_kernel(V* __restrict__ out, const V* __restrict__ in,
+                                                             long seg_v, ArPeers peers, int rank, int nranks,
+                                                             long slot_bytes, unsigned* epochs, unsigned* err) {
+  const int b = blockIdx.x;
+  const long per = (seg_v + gridDim.x - 1) / gridDim.x;
+  const long v0 = b * per, v1 = min(seg_v, v0 + per);
+  __shared__ unsigned s_epoch;
+  if (threadIdx.x == 0) s_epoch = epochs[b] + 1;
+  __syncthreads();
+  const unsigned e = s_epoch;
+  const int par = e & 1;
+  for (int d = 0; d < nranks; ++d) {
+    V* dst = reinterpret_cast<V*>(peers.recv[d] + (static_cast<long>(par) * nranks + rank) * slot_bytes);
+    const V* src = in + d * seg_v;
+    for (long v = v0 + threadIdx.x; v < v1; v += blockDim.x) dst[v] = src[v];
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < nranks) st_flag(peers.flags[threadIdx.x] + b * kArMaxRanks + rank, e);
+  if (threadIdx.x < nranks) ar_wait(peers.flags[rank] + b * kArMaxRanks + threadIdx.x, e, err);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  for (int r = 0; r < nranks; ++r) {
+    const V* src = reinterpret_cast<const V*>(peers.recv[rank] + (static_cast<long>(par) * nranks + r) * slot_bytes);
+    V* dst = out + r * seg_v;
+    for (long v = v0 + threadIdx.x; v < v1; v += blockDim.x) dst[v] = src[v];
+  }
+  if (threadIdx.x == 0) epochs[b] = e;
+}
+
+void launch_ipc_all_to_all(void* out, const void* in, long seg_bytes, const ArPeers& peers, int rank, int nranks,
+                           long slot_bytes, unsigned* epochs, unsigned* err, hipStream_t s) {
+  if (seg_bytes % 16 == 0)
+    hipLaunchKernelGGL(ipc_all_to_all_kernel<uint4>, dim3(kArMaxBlocks), dim3(512), 0, s, static_cast<uint4*>(out),
+                       static_cast<const uint4*>(in), seg_bytes / 16, peers, rank, nranks, slot_bytes, epochs, err);
+  else
+    hipLaunchKernelGGL(ipc_all_to_all_kernel<uint32_t>, dim3(kArMaxBlocks), dim3(512), 0, s,
+                       static_cast<uint32_t*>(out), static_cast<const uint32_t*>(in), seg_bytes / 4, peers, rank,
+                       nranks, slot_bytes, epochs, err);
+  MXS_CHECK_LAUNCH();
+}
+
 }  // namespace mxs

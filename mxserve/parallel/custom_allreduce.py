@@ -82,6 +82,19 @@ class CustomAllReduce:
                                    self.epochs_ptr, self.err_ptr, two_shot)
         return out
 
+    def can_all_to_all(self, x: torch.Tensor) -> bool:
+        nbytes = x.numel() * x.element_size()
+        return (not self.disabled and x.is_cuda and x.is_contiguous() and nbytes % self.world == 0
+                and (nbytes // self.world) % 4 == 0 and nbytes // self.world <= self.max_bytes)
+
+    def all_to_all(self, out: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+        """Equal-split all-to-all (segment d of x -> rank d; segment r of out <- rank r) by direct
+        peer pushes into the IPC slots (EP dispatch / combine, graph-capturable)."""
+        from .. import ops
+        ops.ext().ipc_all_to_all(out, x, self.recv_ptrs, self.flag_ptrs, self.rank, self.max_bytes,
+                                 self.epochs_ptr, self.err_ptr)
+        return out
+
     def check(self) -> bool:
         """True while healthy.  Reads every rank's error word (all signal pages are mapped here); a
         timed-out peer disables the path (RCCL from then on)."""

@@ -19,7 +19,10 @@ Two dispatch layouts:
             sorted by destination -- large prefill chunks, where padding to the worst case would
             ship N x the needed bytes.
 RCCL's all_to_all_single over xGMI is one send per peer link, so all 7 links carry a slice at
-once -- the collective shape point-to-point xGMI likes, unlike a ring.
+once -- the collective shape point-to-point xGMI likes, unlike a ring.  With the IPC slots of the
+custom all-reduce mapped (MXS_CUSTOM_AR=1), the equal-split exchanges of the fixed layout skip
+RCCL: each rank pushes its segments straight into the peers' receive slots (one kernel, all links,
+no host involvement; csrc/kernels/custom_allreduce.hip ipc_all_to_all_kernel).
 """
 from __future__ import annotations
 
@@ -34,6 +37,12 @@ FIXED_MAX_PAIRS = 512
 
 
 def _a2a(out: torch.Tensor, inp: torch.Tensor, group, out_splits=None, in_splits=None) -> torch.Tensor:
+    if out_splits is None and inp.is_cuda:
+        from .comm import get_tp
+        tp = get_tp()
+        car = tp.custom_ar
+        if car is not None and (group is None or group is tp.group) and car.can_all_to_all(inp):
+            return car.all_to_all(out, inp)
     dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
     return out
 

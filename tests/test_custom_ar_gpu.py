@@ -45,6 +45,18 @@ def _rank(rank, world, port, q):
             torch.cuda.synchronize()
             if not torch.equal(out.float(), want(n, call)):
                 errs.append(f"call {call} n={n}: max err {(out.float() - want(n, call)).abs().max().item()}")
+        # equal-split IPC all-to-all (EP dispatch), interleaved with all-reduces: bf16 segments of
+        # 16-byte multiples and int32 segments of 4-byte multiples
+        for call, (seg, dt) in enumerate([(24, torch.bfloat16), (3, torch.int32), (4096, torch.bfloat16), (5, torch.int32)]):
+            x = torch.cat([torch.arange(seg, device="cuda:0") + 1000 * rank + d for d in range(world)]).to(dt)
+            out = torch.empty_like(x)
+            assert car.can_all_to_all(x)
+            car.all_to_all(out, x)
+            car.all_reduce(inp(64, call))
+            torch.cuda.synchronize()
+            exp = torch.cat([torch.arange(seg, device="cuda:0") + 1000 * r + rank for r in range(world)]).to(dt)
+            if not torch.equal(out, exp):
+                errs.append(f"a2a call {call} seg={seg} {dt}")
         # hipGraph: 3 captured all-reduces (one two-shot when world > 2), replayed twice
         car.two_shot_min_bytes = 512 << 10
         xs = [inp(4096 if i != 1 else 1 << 19, 20 + i) for i in range(3)]
