@@ -36,6 +36,43 @@ from .tokenizer import IncrementalDetokenizer, load_tokenizer
 log = logging.getLogger("mxserve.frontend")
 
 
+MAX_N = 16  # choices per request (`n`)
+
+
+async def _merge(gens: list):
+    """Interleave async generators as items arrive: yields (generator index, item).  The first
+    exception ends the merge and is raised; the other generators are closed."""
+    if len(gens) == 1:
+        async for item in gens[0]:
+            yield 0, item
+        return
+    q: asyncio.Queue = asyncio.Queue()
+    done = object()
+
+    async def pump(i, g):
+        try:
+            async for item in g:
+                await q.put((i, item))
+            await q.put((i, done))
+        except BaseException as e:  # noqa: BLE001 - re-raised by the consumer
+            await q.put((i, e))
+
+    tasks = [asyncio.ensure_future(pump(i, g)) for i, g in enumerate(gens)]
+    try:
+        left = len(gens)
+        while left:
+            i, item = await q.get()
+            if item is done:
+                left -= 1
+            elif isinstance(item, BaseException):
+                raise item
+            else:
+                yield i, item
+    finally:
+        for t in tasks:
+            t.cancel()
+
+
 class APIError(Exception):
     def __init__(self, status: int, message: str, etype: str = "invalid_request_error"):
         super().__init__(message)
@@ -246,8 +283,9 @@ class Frontend:
         tp = body.get("top_p")
         if t is not None and not (0.0 <= float(t) <= 2.0):
             raise APIError(400, "temperature must be in [0, 2]")
-        if body.get("n", 1) not in (1, None):
-            raise APIError(400, "only n=1 is supported")
+        n = body.get("n")
+        if n is not None and not (isinstance(n, int) and 1 <= n <= MAX_N):
+            raise APIError(400, f"n must be an integer in [1, {MAX_N}]")
         return {"max_tokens": mt, "temperature": 1.0 if t is None else float(t),
                 "top_p": 1.0 if tp is None else float(tp), "top_k": int(body.get("top_k") or 0),
                 "seed": body.get("seed"), "ignore_eos": bool(body.get("ignore_eos", False)),
@@ -261,6 +299,7 @@ class Frontend:
         rtype = "stream" if stream else "unary"
         sampling = self._sampling(body, model, len(prompt_ids), chat)
         want_lp = sampling["logprobs"] is not None
+        n_choices = int(body.get("n") or 1)
         stops = body.get("stop") or []
         if isinstance(stops, str):
             stops = [stops]
@@ -275,9 +314,9 @@ class Frontend:
         m.queued.labels(model).inc()
         m.isl.labels(model).observe(len(prompt_ids))
         t0 = time.perf_counter()
-        state = {"first": None, "last": None, "n": 0, "queued": True}
+        state = {"first": None, "last": {}, "n": 0, "queued": True}
 
-        def on_token():
+        def on_token(idx: int):
             now = time.perf_counter()
             if state["first"] is None:
                 state["first"] = now
@@ -285,9 +324,9 @@ class Frontend:
                 m.ttft.labels(model).observe(now - t0)
                 m.queued.labels(model).dec()
                 state["queued"] = False
-            else:
-                m.itl.labels(model).observe(now - state["last"])
-            state["last"] = now
+            elif idx in state["last"]:
+                m.itl.labels(model).observe(now - state["last"][idx])
+            state["last"][idx] = now
             state["n"] += 1
 
         def finish(status: str):
@@ -300,7 +339,17 @@ class Frontend:
             trace.attrs.update(status=status, completion_tokens=state["n"])
             TRACER.finish(trace)
 
-        async def events():
+        def sub_request(idx: int) -> tuple:
+            """Choice idx of an n > 1 request: its own request id and seed (same prompt, so the
+            choices after the first hit the prefix cache)."""
+            if n_choices == 1:
+                return rid, sampling
+            sp = dict(sampling)
+            if sp.get("seed") is not None:
+                sp["seed"] = int(sp["seed"]) + idx
+            return f"{rid}-{idx}", sp
+
+        async def events(idx: int = 0):
             """Yields (text_delta, finish_reason|None, logprob events).  With stop strings, text that
             could still be the start of a stop string is held back until it is disambiguated; the
             log-probs of the tokens behind held-back text travel with the next delta."""
@@ -308,8 +357,9 @@ class Frontend:
             full, emitted = "", 0
             hold = max((len(x) for x in stops if x), default=1) - 1
             lps: list = []
-            async for ev in self.generate_tokens(model, prompt_ids, sampling, rid):
-                on_token()
+            sub_rid, sub_sp = sub_request(idx)
+            async for ev in self.generate_tokens(model, prompt_ids, sub_sp, sub_rid):
+                on_token(idx)
                 eos_hit = ev.finished and ev.finish_reason == "stop" and ev.token_id in tok.eos_token_ids
                 full += "" if eos_hit else detok.add(ev.token_id)
                 if want_lp and not eos_hit and ev.logprob is not None:
@@ -359,12 +409,22 @@ class Frontend:
 
         obj = "chat.completion" if chat else "text_completion"
         if not stream:
-            try:
+            async def one_choice(idx: int) -> dict:
                 parts, reason, lp_evs = [], None, []
-                async for d, r, evs in events():
+                async for d, r, evs in events(idx):
                     parts.append(d)
                     lp_evs.extend(evs)
                     reason = r or reason
+                text = "".join(parts)
+                choice = ({"index": idx, "message": {"role": "assistant", "content": text},
+                           "finish_reason": reason or "stop"}
+                          if chat else {"index": idx, "text": text, "logprobs": None, "finish_reason": reason or "stop"})
+                if want_lp:
+                    choice["logprobs"] = lp_payload(lp_evs)
+                return choice
+
+            try:
+                choices = list(await asyncio.gather(*(one_choice(i) for i in range(n_choices))))
             except APIError:
                 finish("error")
                 raise
@@ -372,34 +432,30 @@ class Frontend:
                 finish("error")
                 raise APIError(500, f"generation failed: {e}", "server_error")
             finish("success")
-            text = "".join(parts)
-            choice = ({"index": 0, "message": {"role": "assistant", "content": text}, "finish_reason": reason or "stop"}
-                      if chat else {"index": 0, "text": text, "logprobs": None, "finish_reason": reason or "stop"})
-            if want_lp:
-                choice["logprobs"] = lp_payload(lp_evs)
-            return JSONResponse({"id": rid, "object": obj, "created": created, "model": model, "choices": [choice],
+            return JSONResponse({"id": rid, "object": obj, "created": created, "model": model, "choices": choices,
                                  "usage": {"prompt_tokens": len(prompt_ids), "completion_tokens": state["n"],
                                            "total_tokens": len(prompt_ids) + state["n"]}})
 
         include_usage = bool((body.get("stream_options") or {}).get("include_usage"))
         chunk_obj = "chat.completion.chunk" if chat else "text_completion"
 
-        sent = {"chars": 0}
+        sent = [0] * n_choices  # characters streamed per choice (completions text_offset)
 
-        def chunk(delta: Optional[str], reason: Optional[str], first: bool = False, evs: tuple = ()) -> bytes:
+        def chunk(delta: Optional[str], reason: Optional[str], first: bool = False, evs: tuple = (),
+                  idx: int = 0) -> bytes:
             if chat:
                 d = {}
                 if first:
                     d["role"] = "assistant"
                 if delta is not None:
                     d["content"] = delta
-                ch = {"index": 0, "delta": d, "finish_reason": reason}
+                ch = {"index": idx, "delta": d, "finish_reason": reason}
                 if want_lp and not first:
                     ch["logprobs"] = lp_payload(list(evs))
             else:
-                ch = {"index": 0, "text": delta or "", "logprobs": lp_payload(list(evs), sent["chars"]),
+                ch = {"index": idx, "text": delta or "", "logprobs": lp_payload(list(evs), sent[idx]),
                       "finish_reason": reason}
-                sent["chars"] += len(delta or "")
+                sent[idx] += len(delta or "")
             return ("data: " + json.dumps({"id": rid, "object": chunk_obj, "created": created, "model": model,
                                            "choices": [ch]}) + "\n\n").encode()
 
@@ -407,10 +463,11 @@ class Frontend:
             status = "success"
             try:
                 if chat:
-                    yield chunk("", None, first=True)
-                async for d, r, evs in events():
+                    for i in range(n_choices):
+                        yield chunk("", None, first=True, idx=i)
+                async for i, (d, r, evs) in _merge([events(i) for i in range(n_choices)]):
                     if d or r:
-                        yield chunk(d if d else ("" if r else None), r, evs=evs)
+                        yield chunk(d if d else ("" if r else None), r, evs=evs, idx=i)
                 if include_usage:
                     yield ("data: " + json.dumps({"id": rid, "object": chunk_obj, "created": created, "model": model,
                                                   "choices": [], "usage": {"prompt_tokens": len(prompt_ids),

@@ -171,6 +171,32 @@ def test_logprobs_chat_and_completions(agg_stack):
     assert plain["choices"][0].get("logprobs") is None
 
 
+def test_n_choices_unary_and_stream(agg_stack):
+    """`n` > 1: one choice per index, seeds offset per choice, usage sums every choice; SSE chunks
+    carry the choice index and every choice ends with its own finish_reason."""
+    _, fs, _ = agg_stack
+    body = {"model": MODEL, "messages": [{"role": "user", "content": "several"}], "max_tokens": 5,
+            "temperature": 0.9, "seed": 11, "ignore_eos": True, "n": 3}
+    d = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=60).json()
+    assert [c["index"] for c in d["choices"]] == [0, 1, 2]
+    assert d["usage"]["completion_tokens"] == 15
+    greedy = httpx.post(fs.url + "/v1/chat/completions", json=dict(body, temperature=0, n=2), timeout=60).json()
+    a, b = (c["message"]["content"] for c in greedy["choices"])
+    assert a == b
+    texts, reasons = {}, {}
+    with httpx.stream("POST", fs.url + "/v1/completions",
+                      json={"model": MODEL, "prompt": "abc", "max_tokens": 4, "temperature": 0, "ignore_eos": True,
+                            "n": 2, "stream": True}, timeout=60) as r:
+        for line in r.iter_lines():
+            if line.startswith("data: ") and line != "data: [DONE]":
+                for ch in json.loads(line[6:])["choices"]:
+                    texts[ch["index"]] = texts.get(ch["index"], "") + ch["text"]
+                    if ch["finish_reason"]:
+                        reasons[ch["index"]] = ch["finish_reason"]
+    assert reasons == {0: "length", 1: "length"} and texts[0] == texts[1]
+    assert httpx.post(fs.url + "/v1/chat/completions", json=dict(body, n=0)).status_code == 400
+
+
 def test_disaggregated_matches_aggregated():
     """Prefill worker + decode worker (host-staged KV transfer) give the agg result token for token."""
     fe = Frontend(router_mode="round_robin", ttl=30)
