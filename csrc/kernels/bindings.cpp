@@ -23,6 +23,8 @@ void launch_sample(int64_t*, const void*, bool, int, int, long, const float*, co
                    const int64_t*, const int64_t*, hipStream_t);
 void launch_logprobs(float*, int64_t*, float*, const void*, bool, int, int, long, const int64_t*, const int64_t*, int,
                      hipStream_t);
+void launch_penalties(void*, bool, int, int, long, const int*, long, const int64_t*, const int*, const int*,
+                      const float*, const float*, const float*, int*, hipStream_t);
 void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStream_t);
 void launch_moe_align(int*, int*, const int*, int, int, int, hipStream_t);
 bool launch_skinny_gemm(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, hipStream_t);
@@ -162,6 +164,28 @@ void logprobs(at::Tensor tok_lp, at::Tensor top_ids, at::Tensor top_lp, at::Tens
                        rows.data_ptr<int64_t>(), tokens.data_ptr<int64_t>(), K, stream());
 }
 
+// frequency / presence / repetition penalties, in place on logits rows [B, V]
+void apply_penalties(at::Tensor logits, at::Tensor hist, at::Tensor srows, at::Tensor hlen, at::Tensor plen,
+                     at::Tensor rep, at::Tensor freq, at::Tensor pres, at::Tensor counts) {
+  CHECK_CUDA(logits);
+  TORCH_CHECK((logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16) && logits.stride(1) == 1,
+              "logits must be fp32 or bf16 rows");
+  const int B = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(V <= 163840, "vocab too large for the penalty bitmap");
+  TORCH_CHECK(hist.scalar_type() == at::kInt && hist.dim() == 2 && hist.stride(1) == 1, "hist: int32 [rows, L]");
+  TORCH_CHECK(srows.scalar_type() == at::kLong && srows.size(0) == B, "srows");
+  TORCH_CHECK(hlen.scalar_type() == at::kInt && plen.scalar_type() == at::kInt && hlen.size(0) == B &&
+                  plen.size(0) == B, "hlen / plen");
+  TORCH_CHECK(rep.scalar_type() == at::kFloat && freq.scalar_type() == at::kFloat && pres.scalar_type() == at::kFloat &&
+                  rep.size(0) == B && freq.size(0) == B && pres.size(0) == B, "penalty params");
+  TORCH_CHECK(counts.scalar_type() == at::kInt && counts.is_contiguous() && counts.numel() >= static_cast<long>(B) * V,
+              "counts scratch");
+  mxs::launch_penalties(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, B, V, logits.stride(0),
+                        hist.data_ptr<int>(), hist.stride(0), srows.data_ptr<int64_t>(), hlen.data_ptr<int>(),
+                        plen.data_ptr<int>(), rep.data_ptr<float>(), freq.data_ptr<float>(), pres.data_ptr<float>(),
+                        counts.data_ptr<int>(), stream());
+}
+
 // out[M,N] = x[M,K] . w[N,K]^T for M <= 256; false if the shape is unsupported (caller falls back)
 bool skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
@@ -215,6 +239,7 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("scale"), pybind11::arg("max_q_len"), pybind11::arg("version") = 3);
   m.def("sample", &sample);
   m.def("logprobs", &logprobs);
+  m.def("apply_penalties", &apply_penalties);
   m.def("moe_topk_softmax", &moe_topk_softmax);
   m.def("moe_align", &moe_align);
   m.def("skinny_gemm", &skinny_gemm);

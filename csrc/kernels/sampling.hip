@@ -246,4 +246,75 @@ void launch_logprobs(float* tok_lp, int64_t* top_ids, float* top_lp, const void*
   MXS_CHECK_LAUNCH();
 }
 
+// Sampling penalties (OpenAI frequency_penalty / presence_penalty, vLLM repetition_penalty),
+// applied in place to the logits rows before sampling.  One workgroup per sampled row; rows with
+// neutral penalties exit at once (the kernel sits in every decode graph).  The row's token history
+// (prompt then generated tokens, written on the device every step) is hist[row, 0:hlen):
+//   prompt tokens    -> LDS presence bitmap (V <= 163840 bits = 20 KiB)
+//   generated tokens -> per-token counts in a global int32 scratch row (V x 4 B; LDS cannot hold
+//                       counts for a 128k-152k vocab), zeroed first, atomics at L2, read back with
+//                       atomic loads so no stale L1 line is used
+// then for every v:  seen = in prompt or count > 0
+//   repetition: z = seen ? (z > 0 ? z / rep : z * rep) : z;   z -= count * freq + (count > 0) * pres
+constexpr int kPenMaxVocab = 163840;
+
+template <typename T>
+__device__ __forceinline__ void st(T* p, float v);
+template <>
+__device__ __forceinline__ void st<float>(float* p, float v) { *p = v; }
+template <>
+__device__ __forceinline__ void st<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+
+template <typename T>
+__global__ void __launch_bounds__(1024) penalties_kernel(T* __restrict__ logits, int V, long row_stride,
+                                                         const int* __restrict__ hist, long hist_stride,
+                                                         const int64_t* __restrict__ srows,
+                                                         const int* __restrict__ hlen, const int* __restrict__ plen,
+                                                         const float* __restrict__ rep,
+                                                         const float* __restrict__ freq,
+                                                         const float* __restrict__ pres, int* __restrict__ counts) {
+  __shared__ unsigned bits[kPenMaxVocab / 32];
+  const int b = blockIdx.x;
+  const float rp = rep[b], fp = freq[b], pp = pres[b];
+  if (rp == 1.f && fp == 0.f && pp == 0.f) return;
+  T* z = logits + b * row_stride;
+  int* cnt = counts + static_cast<long>(b) * V;
+  const int* h = hist + srows[b] * hist_stride;
+  const int n = hlen[b], np = min(plen[b], n);
+  for (int w = threadIdx.x; w < (V + 31) / 32; w += blockDim.x) bits[w] = 0u;
+  for (int v = threadIdx.x; v < V; v += blockDim.x) cnt[v] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int t = h[i];
+    if (t < 0 || t >= V) continue;
+    if (i < np)
+      atomicOr(&bits[t >> 5], 1u << (t & 31));
+    else
+      atomicAdd(&cnt[t], 1);
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    const int c = __hip_atomic_load(&cnt[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool seen = c > 0 || ((bits[v >> 5] >> (v & 31)) & 1u);
+    if (!seen) continue;
+    float x = ld(z, v);
+    if (rp != 1.f) x = x > 0.f ? x / rp : x * rp;
+    if (c > 0) x -= static_cast<float>(c) * fp + pp;
+    st(z + v, x);
+  }
+}
+
+void launch_penalties(void* logits, bool bf16, int B, int V, long row_stride, const int* hist, long hist_stride,
+                      const int64_t* srows, const int* hlen, const int* plen, const float* rep, const float* freq,
+                      const float* pres, int* counts, hipStream_t s) {
+  if (B == 0) return;
+  if (bf16)
+    hipLaunchKernelGGL(penalties_kernel<bf16_t>, dim3(B), dim3(1024), 0, s, static_cast<bf16_t*>(logits), V,
+                       row_stride, hist, hist_stride, srows, hlen, plen, rep, freq, pres, counts);
+  else
+    hipLaunchKernelGGL(penalties_kernel<float>, dim3(B), dim3(1024), 0, s, static_cast<float*>(logits), V, row_stride,
+                       hist, hist_stride, srows, hlen, plen, rep, freq, pres, counts);
+  MXS_CHECK_LAUNCH();
+}
+
 }  // namespace mxs

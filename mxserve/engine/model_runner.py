@@ -47,10 +47,12 @@ class InputBuffers:
 
     _SEGS = (("input_ids", np.int64, "T"), ("positions", np.int64, "T"), ("slot_mapping", np.int64, "T"),
              ("logits_indices", np.int64, "S"), ("seeds", np.int64, "S"), ("steps", np.int64, "S"),
-             ("srows", np.int64, "S"),
+             ("srows", np.int64, "S"), ("trow", np.int64, "T"),
              ("bt_idx", np.int64, "U"), ("seq_lens", np.int32, "S"), ("qsl", np.int32, "S1"),
              ("rows", np.int32, "S"), ("sseq", np.int32, "S"), ("top_k", np.int32, "S"), ("bt_val", np.int32, "U"),
-             ("temperature", np.float32, "S"), ("top_p", np.float32, "S"))
+             ("hlen", np.int32, "S"), ("plen", np.int32, "S"),
+             ("temperature", np.float32, "S"), ("top_p", np.float32, "S"),
+             ("rep", np.float32, "S"), ("freq", np.float32, "S"), ("pres", np.float32, "S"))
 
     def __init__(self, T: int, S: int, U: int, device: torch.device, pin: bool):
         cap = {"T": T, "S": S, "S1": S + 1, "U": U}
@@ -129,6 +131,15 @@ class ModelRunner:
         self._row_topk = np.zeros(n_rows, dtype=np.int32)
         self._row_seed = np.zeros(n_rows, dtype=np.int64)
         self._row_lp = np.full(n_rows, -1, dtype=np.int32)  # top_logprobs per row; -1 = no logprobs
+        # sampling penalties: per-row (repetition, frequency, presence) and prompt length, and the
+        # token history every step writes on the device (input token of each position)
+        self._row_pen = np.tile(np.array([1.0, 0.0, 0.0], dtype=np.float32), (n_rows, 1))
+        self._row_plen = np.zeros(n_rows, dtype=np.int32)
+        self._hist_init: list = []
+        self.hist_len = args.max_model_len
+        self.hist = torch.zeros(n_rows, self.hist_len, dtype=torch.int32, device=self.device)
+        self._pen_counts = (torch.empty(n_rows, cfg.vocab_size, dtype=torch.int32, device=self.device)
+                            if self.is_gpu else None)
         self._logits: Optional[torch.Tensor] = None  # last step's logits rows (logprobs read them)
         self.max_tokens_per_step = args.max_num_batched_tokens + args.max_num_seqs
         self.buf = InputBuffers(self.max_tokens_per_step, n_rows,
@@ -188,6 +199,10 @@ class ModelRunner:
             self._row_topk[row] = sp.top_k
             self._row_seed[row] = req.seed
             self._row_lp[row] = -1 if sp.logprobs is None else int(sp.logprobs)
+            self._row_pen[row] = (sp.repetition_penalty, sp.frequency_penalty, sp.presence_penalty)
+            self._row_plen[row] = len(req.prompt_token_ids)
+            if sp.has_penalties:  # history of tokens this row never computes (prefix-cache hits)
+                self._hist_init.append((row, req.all_token_ids()[:self.hist_len]))
         gen, synced = self._row_state[rid]
         ids = req.block_ids
         n = len(ids)
@@ -233,6 +248,7 @@ class ModelRunner:
             rows.append(self._row_for(r, upd_idx, upd_val))
             steps.append(s.out_idx)
         T = nd
+        h["trow"][:nd] = rows
         h["input_ids"][:nd] = toks
         h["positions"][:nd] = pos
         h["slot_mapping"][:nd] = slots
@@ -248,10 +264,12 @@ class ModelRunner:
             h["positions"][T:T + n] = p
             bids = np.asarray(r.block_ids, dtype=np.int64)
             h["slot_mapping"][T:T + n] = bids[p // bs] * bs + p % bs
+            row = self._row_for(r, upd_idx, upd_val)
+            h["trow"][T:T + n] = row
             T += n
             qsl.append(T)
             lens.append(start + n)
-            rows.append(self._row_for(r, upd_idx, upd_val))
+            rows.append(row)
             max_q = max(max_q, n)
             if s.sample:
                 sample_rows.append(nd + i)
@@ -270,6 +288,11 @@ class ModelRunner:
         h["steps"][:ns] = steps
         h["srows"][:ns] = srows
         h["sseq"][:ns] = sample_rows
+        pen = self._row_pen[srows]
+        h["rep"][:ns], h["freq"][:ns], h["pres"][:ns] = pen[:, 0], pen[:, 1], pen[:, 2]
+        h["plen"][:ns] = self._row_plen[srows]
+        h["hlen"][:ns] = np.asarray(lens, dtype=np.int32)[sample_rows] if ns else []
+        use_pen = bool(ns) and bool((pen[:, 0] != 1.0).any() or (pen[:, 1:] != 0.0).any())
         if graph_bs > S:  # padding rows of a graph bucket: no cache write, 1-token context, greedy
             h["input_ids"][S:graph_bs] = 0
             h["positions"][S:graph_bs] = 0
@@ -277,7 +300,11 @@ class ModelRunner:
             h["seq_lens"][S:graph_bs] = 1
             h["rows"][S:graph_bs] = self.pad_row
             h["srows"][S:graph_bs] = self.pad_row
+            h["trow"][S:graph_bs] = self.pad_row
             h["temperature"][S:graph_bs] = 0.0
+            h["rep"][S:graph_bs], h["freq"][S:graph_bs], h["pres"][S:graph_bs] = 1.0, 0.0, 0.0
+            h["hlen"][S:graph_bs] = 1
+            h["plen"][S:graph_bs] = 1
         U = len(upd_idx)
         big_update = None
         if U > self.buf.caps["bt_idx"]:
@@ -292,11 +319,15 @@ class ModelRunner:
             if (lpk >= 0).any():
                 sel = np.nonzero(lpk >= 0)[0]
                 lp = (sel.tolist(), int(lpk[sel].max()))
+        hist_init, self._hist_init = self._hist_init, []
         return dict(S=S, T=T, nd=nd, max_q=max_q, max_seq=max(lens), sample_rows=sample_rows, U=U,
-                    big_update=big_update, graph_bs=graph_bs, lp=lp)
+                    big_update=big_update, graph_bs=graph_bs, lp=lp, pen=use_pen, hist_init=hist_init)
 
     def _upload(self, meta: dict) -> None:
         self.buf.upload()
+        for row, toks in meta.get("hist_init") or ():
+            t = torch.tensor(toks, dtype=torch.int32)
+            self.hist[row, :len(toks)].copy_(t.to(self.device) if self.is_gpu else t)
         bt = self.bt_dev.view(-1)
         if meta["U"]:
             U = meta["U"]
@@ -417,7 +448,17 @@ class ModelRunner:
                     seq_lens=d["seq_lens"][:S], qsl=d["qsl"][:S + 1], rows=d["rows"][:S],
                     logits_indices=d["logits_indices"][:ns], temperature=d["temperature"][:ns],
                     top_p=d["top_p"][:ns], top_k=d["top_k"][:ns], seeds=d["seeds"][:ns], steps=d["steps"][:ns],
-                    srows=d["srows"][:ns], sseq=d["sseq"][:ns])
+                    srows=d["srows"][:ns], sseq=d["sseq"][:ns], trow=d["trow"][:T], hlen=d["hlen"][:ns],
+                    plen=d["plen"][:ns], rep=d["rep"][:ns], freq=d["freq"][:ns], pres=d["pres"][:ns])
+
+    def _write_hist(self, v: dict, inp: torch.Tensor) -> None:
+        """Token history for the penalties: every input token at (its row, its position)."""
+        idx = v["trow"] * self.hist_len + v["positions"]
+        self.hist.view(-1).index_copy_(0, idx, inp.to(torch.int32))
+
+    def _penalize(self, v: dict, logits: torch.Tensor) -> None:
+        ops.apply_penalties(logits, self.hist, v["srows"], v["hlen"], v["plen"], v["rep"], v["freq"], v["pres"],
+                            self._pen_counts)
 
     def _forward_eager(self, meta: dict, sample: bool):
         S, T, nd = meta["S"], meta["T"], meta["nd"]
@@ -435,10 +476,13 @@ class ModelRunner:
         if nd:
             d_in = inp[:nd]
             d_in.copy_(torch.where(d_in < 0, self.last_tok.index_select(0, v["rows"][:nd].long()), d_in))
+        self._write_hist(v, inp)
         hidden = self.model.forward(inp, md, self.kv_cache)
         if not sample:
             return None
         logits = self.model.compute_logits(hidden)
+        if meta.get("pen"):
+            self._penalize(v, logits)
         self._logits = logits
         ids = ops.sample(logits, v["temperature"], v["top_p"], v["top_k"], v["seeds"], v["steps"])
         self.last_tok.index_copy_(0, v["srows"], ids)
@@ -451,6 +495,7 @@ class ModelRunner:
         bt = self.bt_dev.index_select(0, rows)
         inp = v["input_ids"]
         inp = torch.where(inp < 0, self.last_tok.index_select(0, rows), inp)
+        self._write_hist(v, inp)
         md = AttnMetadata(
             positions=v["positions"], slot_mapping=v["slot_mapping"], block_tables=bt,
             seq_lens=v["seq_lens"], query_start_loc=v["qsl"], logits_indices=self._arange[:b],
@@ -458,6 +503,7 @@ class ModelRunner:
             max_seq_len=self.args.max_model_len)
         hidden = self.model.forward(inp, md, self.kv_cache)
         logits = self.model.compute_logits(hidden)
+        self._penalize(v, logits)  # rows with neutral penalties exit at once
         ids = ops.sample(logits, v["temperature"], v["top_p"], v["top_k"], v["seeds"], v["steps"])
         self.last_tok.index_copy_(0, v["srows"], ids)
         return ids, logits
@@ -475,6 +521,11 @@ class ModelRunner:
         h["qsl"][:] = np.arange(len(h["qsl"]))
         h["temperature"][:] = 0
         h["top_p"][:] = 1
+        h["trow"][:] = self.pad_row
+        h["rep"][:] = 1
+        h["freq"][:] = 0
+        h["pres"][:] = 0
+        h["hlen"][:] = 1
         self.buf.upload()
         t0 = time.time()
         torch.cuda.synchronize()

@@ -19,6 +19,13 @@ class SamplingParams:
     min_tokens: int = 0
     # log-probs of the sampled tokens: None = off, k >= 0 = also the k most likely tokens (k <= 20)
     logprobs: Optional[int] = None
+    repetition_penalty: float = 1.0  # > 1 discourages tokens of the prompt and the output (vLLM)
+    frequency_penalty: float = 0.0  # OpenAI: minus count * value for generated tokens
+    presence_penalty: float = 0.0  # OpenAI: minus value once a token was generated
+
+    @property
+    def has_penalties(self) -> bool:
+        return self.repetition_penalty != 1.0 or self.frequency_penalty != 0.0 or self.presence_penalty != 0.0
 
     @classmethod
     def from_openai(cls, body: dict, default_max_tokens: int = 256) -> "SamplingParams":
@@ -34,6 +41,9 @@ class SamplingParams:
             ignore_eos=bool(body.get("ignore_eos", False)),
             min_tokens=int(body.get("min_tokens", 0) or 0),
             logprobs=body.get("logprobs"),
+            repetition_penalty=float(body.get("repetition_penalty") or 1.0),
+            frequency_penalty=float(body.get("frequency_penalty") or 0.0),
+            presence_penalty=float(body.get("presence_penalty") or 0.0),
         )
 
 

@@ -286,12 +286,20 @@ class Frontend:
         n = body.get("n")
         if n is not None and not (isinstance(n, int) and 1 <= n <= MAX_N):
             raise APIError(400, f"n must be an integer in [1, {MAX_N}]")
+        pens = {}
+        for key, lo, hi, dflt in (("frequency_penalty", -2.0, 2.0, 0.0), ("presence_penalty", -2.0, 2.0, 0.0),
+                                  ("repetition_penalty", 1e-6, 10.0, 1.0)):
+            v = body.get(key)
+            v = dflt if v is None else float(v)
+            if not lo <= v <= hi:
+                raise APIError(400, f"{key} must be in [{lo:g}, {hi:g}]")
+            pens[key] = v
         return {"max_tokens": mt, "temperature": 1.0 if t is None else float(t),
                 "top_p": 1.0 if tp is None else float(tp), "top_k": int(body.get("top_k") or 0),
                 "seed": body.get("seed"), "ignore_eos": bool(body.get("ignore_eos", False)),
                 "min_tokens": int(body.get("min_tokens") or 0),
                 "stop_token_ids": list(body.get("stop_token_ids") or []),
-                "logprobs": self._logprobs_arg(body, chat)}
+                "logprobs": self._logprobs_arg(body, chat), **pens}
 
     async def _run(self, endpoint: str, body: dict, prompt_ids: list, model: str, chat: bool,
                    xrid: Optional[str] = None):

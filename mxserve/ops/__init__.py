@@ -148,6 +148,17 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
     return ref.sample(logits, temperature, top_p, top_k, seeds, steps)
 
 
+def apply_penalties(logits, hist, srows, hlen, plen, rep, freq, pres, counts=None) -> torch.Tensor:
+    """In place on logits [B, V]: repetition (prompt + output), frequency / presence (output)
+    penalties from the device token history; `counts` is a [>= B, V] int32 scratch."""
+    if _gpu(logits):
+        if counts is None:
+            counts = torch.empty(logits.shape[0], logits.shape[1], dtype=torch.int32, device=logits.device)
+        ext().apply_penalties(logits, hist, srows, hlen, plen, rep, freq, pres, counts)
+        return logits
+    return ref.apply_penalties(logits, hist, srows, hlen, plen, rep, freq, pres)
+
+
 def logprobs(logits: torch.Tensor, rows: torch.Tensor, tokens: torch.Tensor, k: int):
     """(token log-prob [n], top ids [n, k], top log-probs [n, k]) for logits rows `rows`."""
     if _gpu(logits):

@@ -202,6 +202,28 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_p: torch.Tensor,
     return out.to(logits.device)
 
 
+def apply_penalties(logits, hist, srows, hlen, plen, rep, freq, pres) -> torch.Tensor:
+    """In place: repetition penalty over prompt + generated tokens, frequency / presence penalties
+    over generated tokens (history hist[row, :hlen], the first plen entries being the prompt)."""
+    for b in range(logits.shape[0]):
+        rp, fp, pp = float(rep[b]), float(freq[b]), float(pres[b])
+        if rp == 1.0 and fp == 0.0 and pp == 0.0:
+            continue
+        V = logits.shape[1]
+        h = hist[int(srows[b]), :int(hlen[b])].long().cpu()
+        np_ = min(int(plen[b]), len(h))
+        counts = torch.bincount(h[np_:].clamp(0, V - 1), minlength=V).to(logits.device)
+        seen = counts > 0
+        if np_:
+            seen[h[:np_].clamp(0, V - 1).to(logits.device)] = True
+        z = logits[b].float()
+        if rp != 1.0:
+            z = torch.where(seen, torch.where(z > 0, z / rp, z * rp), z)
+        z = z - counts.float() * fp - (counts > 0).float() * pp
+        logits[b] = z.to(logits.dtype)
+    return logits
+
+
 def logprobs(logits: torch.Tensor, rows: torch.Tensor, tokens: torch.Tensor, k: int):
     """Raw-distribution log-probs: the sampled token's, and the k best (value desc, index asc)."""
     lp = torch.log_softmax(logits.index_select(0, rows.long()).float(), dim=-1)

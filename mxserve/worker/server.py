@@ -43,7 +43,10 @@ def _sampling(d: dict) -> SamplingParams:
                           top_p=float(d.get("top_p", 1.0)), top_k=int(d.get("top_k", 0)), seed=d.get("seed"),
                           stop_token_ids=list(d.get("stop_token_ids", [])), ignore_eos=bool(d.get("ignore_eos")),
                           min_tokens=int(d.get("min_tokens", 0)),
-                          logprobs=None if d.get("logprobs") is None else int(d["logprobs"]))
+                          logprobs=None if d.get("logprobs") is None else int(d["logprobs"]),
+                          repetition_penalty=float(d.get("repetition_penalty", 1.0)),
+                          frequency_penalty=float(d.get("frequency_penalty", 0.0)),
+                          presence_penalty=float(d.get("presence_penalty", 0.0)))
 
 
 def _line(o: StepOutput) -> bytes:
@@ -306,7 +309,8 @@ class Worker:
 def _sp_dict(sp: SamplingParams) -> dict:
     return {"max_tokens": sp.max_tokens, "temperature": sp.temperature, "top_p": sp.top_p, "top_k": sp.top_k,
             "seed": sp.seed, "stop_token_ids": list(sp.stop_token_ids), "ignore_eos": sp.ignore_eos,
-            "min_tokens": sp.min_tokens, "logprobs": sp.logprobs}
+            "min_tokens": sp.min_tokens, "logprobs": sp.logprobs, "repetition_penalty": sp.repetition_penalty,
+            "frequency_penalty": sp.frequency_penalty, "presence_penalty": sp.presence_penalty}
 
 
 def advertise_url(wargs: WorkerArgs, port: int) -> str:

@@ -140,3 +140,31 @@ def test_logprobs_match_log_softmax():
     tlp, tid, tv = ref.logprobs(logits, torch.tensor([0, 2]), tok[[0, 2]], 5)
     want = torch.log_softmax(logits, -1)
     assert torch.allclose(tlp, want[[0, 2], [1, 3]]) and torch.equal(tid, want[[0, 2]].topk(5).indices)
+
+
+def test_penalties_change_only_penalized_requests():
+    """Presence penalty 2 forbids repeats in a greedy stream (random logits are O(1) apart);
+    a neighbour without penalties in the same batch produces exactly its solo tokens; the
+    reference penalty op matches a hand computation."""
+    import torch
+    from mxserve.ops import reference as ref
+    prompt = list(range(5, 25))
+    solo = _engine(True).generate([prompt], SamplingParams(max_tokens=40, temperature=0.0, ignore_eos=True))[0]
+    eng = _engine(True)
+    pen = eng.add_request(prompt, SamplingParams(max_tokens=40, temperature=0.0, ignore_eos=True,
+                                                 presence_penalty=2.0, repetition_penalty=1.3))
+    plain = eng.add_request(prompt, SamplingParams(max_tokens=40, temperature=0.0, ignore_eos=True))
+    while eng.has_unfinished():
+        eng.step()
+    assert plain.output_token_ids == solo
+    out = pen.output_token_ids
+    assert len(set(out)) == len(out), out
+    assert len(set(solo)) < len(solo), "the unpenalized greedy stream should repeat (premise of the test)"
+    # op semantics on a hand example: vocab 6, prompt [1], generated [2, 2, 3]
+    logits = torch.tensor([[1.0, 2.0, -1.0, 0.5, 3.0, 0.0]])
+    hist = torch.tensor([[1, 2, 2, 3]], dtype=torch.int32)
+    one = lambda v, dt=torch.float32: torch.tensor([v], dtype=dt)  # noqa: E731
+    ref.apply_penalties(logits, hist, one(0, torch.int64), one(4, torch.int32), one(1, torch.int32),
+                        one(2.0), one(0.5), one(0.25))
+    want = torch.tensor([[1.0, 1.0, -2.0 - 1.0 - 0.25, 0.25 - 0.5 - 0.25, 3.0, 0.0]])
+    assert torch.allclose(logits, want)

@@ -156,6 +156,25 @@ def test_logprobs_graph_and_eager(gpu):
     assert all(o.logprob is None for o in outs if o.request_id == other.request_id)
 
 
+def test_penalties_in_graph_decode(gpu):
+    """Presence penalty through hipGraph decode: no repeated token in a penalized greedy stream,
+    and an unpenalized neighbour in the same batch is unchanged."""
+    prompt = list(range(10, 40))
+    sp = SamplingParams(max_tokens=48, temperature=0.0, ignore_eos=True)
+    # same batch shape without penalties: identical numerics for the unpenalized request
+    solo = _engine(gpu, False).generate([prompt, prompt], sp)[1]
+    eng = _engine(gpu, False)
+    assert eng.runner.graphs
+    pen = eng.add_request(prompt, SamplingParams(max_tokens=48, temperature=0.0, ignore_eos=True,
+                                                 presence_penalty=2.0, repetition_penalty=1.2))
+    plain = eng.add_request(prompt, sp)
+    while eng.has_unfinished():
+        eng.step()
+    out = pen.output_token_ids
+    assert len(set(out)) == len(out), out
+    assert plain.output_token_ids == solo
+
+
 def test_sampling_reproducible_with_seed(gpu):
     eng = _engine(gpu, False)
     sp = SamplingParams(max_tokens=16, temperature=0.8, top_p=0.9, seed=1234, ignore_eos=True)

@@ -197,6 +197,16 @@ def test_n_choices_unary_and_stream(agg_stack):
     assert httpx.post(fs.url + "/v1/chat/completions", json=dict(body, n=0)).status_code == 400
 
 
+def test_penalty_params(agg_stack):
+    _, fs, _ = agg_stack
+    body = {"model": MODEL, "messages": [{"role": "user", "content": "repeat"}], "max_tokens": 12, "temperature": 0,
+            "ignore_eos": True, "presence_penalty": 2.0, "frequency_penalty": 0.5, "repetition_penalty": 1.2}
+    r = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=60)
+    assert r.status_code == 200 and r.json()["usage"]["completion_tokens"] == 12
+    assert httpx.post(fs.url + "/v1/chat/completions", json=dict(body, presence_penalty=3.0)).status_code == 400
+    assert httpx.post(fs.url + "/v1/chat/completions", json=dict(body, repetition_penalty=0)).status_code == 400
+
+
 def test_disaggregated_matches_aggregated():
     """Prefill worker + decode worker (host-staged KV transfer) give the agg result token for token."""
     fe = Frontend(router_mode="round_robin", ttl=30)

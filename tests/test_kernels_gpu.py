@@ -213,6 +213,32 @@ def test_logprobs_matches_reference(gpu, dtype, k):
         assert torch.equal(tid.cpu()[distinct], etid[distinct])
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_penalties_match_reference(gpu, dtype):
+    """Penalty kernel vs the reference on random histories (repeats, prompt/output split, rows
+    with neutral penalties untouched), on a padded-vocab view."""
+    B, V, L, rows_total = 6, 128256, 300, 10
+    g = torch.Generator().manual_seed(3)
+    full = (torch.randn(B, V + 64, generator=g) * 3).to(dtype)
+    hist = torch.randint(0, 2000, (rows_total, L), generator=g, dtype=torch.int32)  # small range: many repeats
+    srows = torch.tensor([3, 0, 9, 5, 1, 7])
+    hlen = torch.tensor([300, 1, 150, 64, 0, 299], dtype=torch.int32)
+    plen = torch.tensor([100, 1, 150, 0, 0, 10], dtype=torch.int32)
+    rep = torch.tensor([1.3, 1.0, 1.0, 0.8, 1.5, 1.0])
+    freq = torch.tensor([0.5, 0.0, 0.2, -0.3, 0.0, 0.0])
+    pres = torch.tensor([0.25, 0.0, 1.0, 0.0, 0.5, 0.0])
+    exp = full[:, :V].clone()
+    ref.apply_penalties(exp, hist, srows, hlen, plen, rep, freq, pres)
+    got_full = full.to(gpu)
+    got = got_full[:, :V]
+    ops.apply_penalties(got, hist.to(gpu), srows.to(gpu), hlen.to(gpu), plen.to(gpu), rep.to(gpu), freq.to(gpu),
+                        pres.to(gpu))
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    _close(got, exp, tol, tol, "penalized logits")
+    assert torch.equal(got_full[:, V:].cpu(), full[:, V:])  # padding columns untouched
+    assert torch.equal(got[5].cpu(), full[5, :V]) and torch.equal(got[1].cpu(), full[1, :V])  # neutral rows
+
+
 def test_moe_topk_softmax(gpu):
     T, E, K = 100, 8, 2
     g = torch.Generator().manual_seed(0)
