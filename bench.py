@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--enforce-eager", action="store_true")
+    ap.add_argument("--kv-cache-dtype", default=os.environ.get("MXS_BENCH_KV_DTYPE", "auto"),
+                    help="auto (bf16, the headline) | fp8 (e4m3fn KV cache: a separate, labelled data point)")
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--device", default="auto")
@@ -313,7 +315,7 @@ def main():
 
     args = EngineArgs(model=a.model, device="cuda" if on_gpu else "cpu", max_num_seqs=a.max_num_seqs,
                       max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=a.max_model_len,
-                      enforce_eager=a.enforce_eager, seed=a.seed)
+                      enforce_eager=a.enforce_eager, seed=a.seed, kv_cache_dtype=a.kv_cache_dtype)
     if not on_gpu:  # plumbing run only (CPU container): keep it tiny
         args = args.replace(model="tiny-llama", max_model_len=1024, cpu_num_blocks=4096)
         a.isl, a.osl = min(a.isl, 200), min(a.osl, 20)
@@ -384,7 +386,8 @@ def main():
                        "global_batch": int(world * a.max_num_seqs), "seq_len": a.isl + a.osl,
                        "parallelism": f"disagg {world // 2}P+{world // 2}D" if disagg else f"dp{world}",
                        "mode": a.mode, "isl": a.isl, "osl": a.osl,
-                       "qps_per_gpu": a.qps, "qps_node": a.qps * world},
+                       "qps_per_gpu": a.qps, "qps_node": a.qps * world,
+                       "kv_cache_dtype": "fp8_e4m3fn" if eng.runner.kv_fp8 else ("bf16" if on_gpu else "fp32")},
             "ttft_p50_ms": None if ttft_p50 is None else round(ttft_p50, 2),
             "itl_p50_ms": None if itl_p50 is None else round(itl_p50, 3),
             "requests_with_first_token": int(col[:, 4].sum()),

@@ -19,6 +19,9 @@
 //     merged once at the end.
 //   * 2 blocks (32 tokens) per wave iteration with the next iteration's K/V loads issued before the
 //     current iteration's math (software pipeline); block ids come from scalar loads.
+//   * EB = 1: fp8 (e4m3fn) cache.  Same lane -> (token, dims) map with 8-byte loads (still whole
+//     512-byte wave-instructions), converted to bf16 words in registers right before the math, so
+//     the step reads half the bytes; k_scale folds into q, v_scale into the output.
 #include "common.h"
 
 namespace mxs {
@@ -87,12 +90,31 @@ __device__ __forceinline__ int decode_part_len(int L, int P) {
   return ((per + 127) / 128) * 128;
 }
 
-template <int D, int G>
+template <int EB>
+struct KVVec;
+template <>
+struct KVVec<2> {  // 8 bf16
+  using raw = u32x4;
+  using reg = uint4;
+  __device__ static uint4 bf16(const uint4& v) { return v; }
+};
+template <>
+struct KVVec<1> {  // 8 fp8
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  using raw = u32x2;
+  using reg = uint2;
+  __device__ static uint4 bf16(const uint2& v) { return fp8x8_to_bf16x8(v); }
+};
+
+template <int D, int G, int EB>
 __global__ void __launch_bounds__(256) paged_decode_kernel(
     bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml,
-    const bf16_t* __restrict__ q, const bf16_t* __restrict__ kv, long block_stride,
+    const bf16_t* __restrict__ q, const void* __restrict__ kv, long block_stride,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens, int Hkv,
-    float scale, int part_len) {
+    float scale, int part_len, float v_scale) {
+  using Vec = KVVec<EB>;
+  using KR = typename Vec::reg;
+  using KRaw = typename Vec::raw;
   // blocks per wave iteration: 2 at D = 64; 1 at D = 128, where a block is already 4 KiB per lane-set
   // and a second prefetched block would cost 64 more VGPRs
   constexpr int kBPI = D <= 64 ? 2 : 1;
@@ -135,9 +157,9 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     }
   }
   const int* btp = block_tables + static_cast<size_t>(seq) * bt_stride;
-  const char* kbase = reinterpret_cast<const char*>(kv) + static_cast<size_t>(kvh) * kBS * D * 2;
-  const char* vbase = reinterpret_cast<const char*>(kv) + static_cast<size_t>(Hkv + kvh) * kBS * D * 2;
-  const long bstride_bytes = block_stride * 2;
+  const char* kbase = reinterpret_cast<const char*>(kv) + static_cast<size_t>(kvh) * kBS * D * EB;
+  const char* vbase = reinterpret_cast<const char*>(kv) + static_cast<size_t>(Hkv + kvh) * kBS * D * EB;
+  const long bstride_bytes = block_stride * EB;
 
   const int blk0 = start / kBS;
   const int nblk = (end - 1) / kBS - blk0 + 1;          // blocks touched by this partition
@@ -152,21 +174,21 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     for (int i = 0; i < KV; ++i) acc[g][i] = 0.f;
   }
 
-  uint4 kr[kBPI][KV], vr[kBPI][KV];
-  auto load = [&](int it, uint4 (&kd)[kBPI][KV], uint4 (&vd)[kBPI][KV]) {
+  KR kr[kBPI][KV], vr[kBPI][KV];
+  auto load = [&](int it, KR (&kd)[kBPI][KV], KR (&vd)[kBPI][KV]) {
 #pragma unroll
     for (int b = 0; b < kBPI; ++b) {
       const int bi = (it * kWaves + wid) * kBPI + b;
       if (bi < nblk) {
         const long off = static_cast<long>(btp[blk0 + bi]) * bstride_bytes;
-        const u32x4* kp = reinterpret_cast<const u32x4*>(kbase + off);
-        const u32x4* vp = reinterpret_cast<const u32x4*>(vbase + off);
+        const KRaw* kp = reinterpret_cast<const KRaw*>(kbase + off);
+        const KRaw* vp = reinterpret_cast<const KRaw*>(vbase + off);
         // KV bytes are read once per step: non-temporal loads keep them from evicting the
         // weights / block tables from L2 (MI355X_MICROARCH nt-weights: 5-10 % per decode layer)
 #pragma unroll
         for (int i = 0; i < KV; ++i) {
-          kd[b][i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(kp + lane + 64 * i));
-          vd[b][i] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(vp + lane + 64 * i));
+          kd[b][i] = __builtin_bit_cast(KR, __builtin_nontemporal_load(kp + lane + 64 * i));
+          vd[b][i] = __builtin_bit_cast(KR, __builtin_nontemporal_load(vp + lane + 64 * i));
         }
       }
     }
@@ -174,7 +196,7 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   if (niter > 0) load(0, kr, vr);
 
   for (int it = 0; it < niter; ++it) {
-    uint4 kn[kBPI][KV], vn[kBPI][KV];
+    KR kn[kBPI][KV], vn[kBPI][KV];
     if (it + 1 < niter) load(it + 1, kn, vn);  // next iteration's loads in flight under this math
     const int tok0 = (blk0 + (it * kWaves + wid) * kBPI) * kBS;  // first token of this iteration
     if (tok0 < end) {
@@ -184,7 +206,8 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
       for (int b = 0; b < kBPI; ++b)
 #pragma unroll
         for (int i = 0; i < KV; ++i) {
-          const uint32_t* w = reinterpret_cast<const uint32_t*>(&kr[b][i]);
+          const uint4 kw = Vec::bf16(kr[b][i]);
+          const uint32_t* w = reinterpret_cast<const uint32_t*>(&kw);
 #pragma unroll
           for (int g = 0; g < G; ++g) {
             float a = 0.f;
@@ -249,7 +272,8 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
           const bool full = tb + kBS <= end;
 #pragma unroll
           for (int i = 0; i < KV; ++i) {
-            uint32_t vw[4] = {vr[b][i].x, vr[b][i].y, vr[b][i].z, vr[b][i].w};
+            const uint4 vb = Vec::bf16(vr[b][i]);
+            uint32_t vw[4] = {vb.x, vb.y, vb.z, vb.w};
             if (!full) {  // never let unwritten cache bytes (possibly NaN) reach the sum
 #pragma unroll
               for (int u = 0; u < 8; ++u)
@@ -317,10 +341,10 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     }
     const int head = kvh * G + g;
     if (P == 1) {
-      out[(static_cast<size_t>(seq) * Hq + head) * D + d] = f2bf(O / Ls);
+      out[(static_cast<size_t>(seq) * Hq + head) * D + d] = f2bf(O / Ls * v_scale);
     } else {
       const size_t base = (static_cast<size_t>(seq) * Hq + head) * P + part;
-      tmp_out[base * D + d] = O / Ls;
+      tmp_out[base * D + d] = O / Ls * v_scale;
       if (d == 0) {
         tmp_ml[base * 2] = M;
         tmp_ml[base * 2 + 1] = Ls;
@@ -372,16 +396,23 @@ int decode_num_partitions(int max_seq_len) {
   return P;
 }
 
-void launch_paged_decode(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, const bf16_t* kv,
+void launch_paged_decode(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, const void* kv, bool kv_fp8,
                          long block_stride, const int* block_tables, int bt_stride, const int* seq_lens, int B,
-                         int Hq, int Hkv, int D, int P, int part_len, float scale, hipStream_t s) {
+                         int Hq, int Hkv, int D, int P, int part_len, float scale, float k_scale, float v_scale,
+                         hipStream_t s) {
   if (B == 0) return;
   const int G = Hq / Hkv;
   dim3 grid(Hkv, B, P), blk(256);
+  if (kv_fp8) scale *= k_scale;
+  else v_scale = 1.f;
 #define MXS_DEC(DD, GG)                                                                                    \
   if (D == DD && G == GG) {                                                                                \
-    hipLaunchKernelGGL((paged_decode_kernel<DD, GG>), grid, blk, 0, s, out, tmp_out, tmp_ml, q, kv,        \
-                       block_stride, block_tables, bt_stride, seq_lens, Hkv, scale, part_len);            \
+    if (kv_fp8)                                                                                            \
+      hipLaunchKernelGGL((paged_decode_kernel<DD, GG, 1>), grid, blk, 0, s, out, tmp_out, tmp_ml, q, kv,   \
+                         block_stride, block_tables, bt_stride, seq_lens, Hkv, scale, part_len, v_scale); \
+    else                                                                                                   \
+      hipLaunchKernelGGL((paged_decode_kernel<DD, GG, 2>), grid, blk, 0, s, out, tmp_out, tmp_ml, q, kv,   \
+                         block_stride, block_tables, bt_stride, seq_lens, Hkv, scale, part_len, v_scale); \
     if (P > 1)                                                                                             \
       hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(Hq, B), dim3(DD), 0, s, out, tmp_out,     \
                          tmp_ml, seq_lens, Hq, P, part_len);                                               \

@@ -250,11 +250,22 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
 // spread over the banks.  V is stored per dim with its keys permuted (bits 2 and 3 of the key index
 // swapped inside each 16-key group) so the 8 keys a lane needs for the P^T operand taken straight
 // from the S^T accumulator are one contiguous ds_read_b128.
-template <int D, int G>
+// EB = 1: fp8 (e4m3fn) cache.  The staging loads fetch 8 bytes per 8 keys/dims and convert them to
+// bf16 words before the LDS store, so LDS layout and MFMA loop are the bf16 ones; k_scale folds
+// into q, v_scale into the final normalisation.
+template <int EB>
+__device__ __forceinline__ uint4 ld8_kv(const char* p) {
+  if constexpr (EB == 2)
+    return *reinterpret_cast<const uint4*>(p);
+  else
+    return fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(p));
+}
+
+template <int D, int G, int EB>
 __global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
-    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const bf16_t* __restrict__ kv, long block_stride,
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const void* __restrict__ kv, long block_stride,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ qsl,
-    const int* __restrict__ seq_lens, int Hkv, float scale) {
+    const int* __restrict__ seq_lens, int Hkv, float scale, float v_scale) {
   constexpr int KS = D / 16, DT = D / 32;
   constexpr int BQ = 256 / G;        // query tokens per workgroup
   constexpr int KT = 64;             // keys per tile
@@ -307,9 +318,9 @@ __global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
 
   const int* bt = block_tables + static_cast<size_t>(seq) * bt_stride;
   const char* kvb = reinterpret_cast<const char*>(kv);
-  const size_t k_head_off = static_cast<size_t>(kvh) * kPBS * D * 2;
-  const size_t v_head_off = static_cast<size_t>(Hkv + kvh) * kPBS * D * 2;
-  const long bstride = block_stride * 2;
+  const size_t k_head_off = static_cast<size_t>(kvh) * kPBS * D * EB;
+  const size_t v_head_off = static_cast<size_t>(Hkv + kvh) * kPBS * D * EB;
+  const long bstride = block_stride * EB;
   const int last_blk = (L - 1) / kPBS;
 
   // ---- staging: global -> registers (tile k0), registers -> LDS buffer
@@ -321,12 +332,12 @@ __global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
 #pragma unroll
     for (int n = 0; n < NK; ++n) {
       const int ci = tid + 512 * n, key = ci / KCH, ch = ci % KCH;
-      sk[n] = *reinterpret_cast<const uint4*>(kvb + bid[key >> 4] * bstride + k_head_off + (key & 15) * KROW + ch * 16);
+      sk[n] = ld8_kv<EB>(kvb + bid[key >> 4] * bstride + k_head_off + (key & 15) * (D * EB) + ch * 8 * EB);
     }
 #pragma unroll
     for (int n = 0; n < NV; ++n) {
       const int ci = tid + 512 * n, blk = ci / (2 * D), rem = ci % (2 * D), dim = rem >> 1, half = rem & 1;
-      uint4 v = *reinterpret_cast<const uint4*>(kvb + bid[blk] * bstride + v_head_off + dim * 32 + half * 16);
+      uint4 v = ld8_kv<EB>(kvb + bid[blk] * bstride + v_head_off + dim * 16 * EB + half * 8 * EB);
       const int kb = k0 + blk * 16 + half * 8;  // keys >= L: zero (unwritten cache bytes may be NaN)
       if (kb + 8 > L) {
         uint32_t* w = reinterpret_cast<uint32_t*>(&v);
@@ -442,7 +453,7 @@ __global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
 
   l += __shfl_xor(l, 32, 64);
   if (!rvalid) return;
-  const float inv = 1.f / l;
+  const float inv = v_scale / l;
   bf16_t* op = out + (static_cast<size_t>(q0 + tok) * Hq + head) * D;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
@@ -456,18 +467,24 @@ __global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
     }
 }
 
-void launch_paged_prefill(bf16_t* out, const bf16_t* q, const bf16_t* kv, long block_stride,
+void launch_paged_prefill(bf16_t* out, const bf16_t* q, const void* kv_ptr, bool kv_fp8, long block_stride,
                           const int* block_tables, int bt_stride, const int* qsl, const int* seq_lens,
                           int num_seqs, int max_q_len, int Hq, int Hkv, int D, float scale, int version,
-                          hipStream_t s) {
+                          float k_scale, float v_scale, hipStream_t s) {
   if (num_seqs == 0 || max_q_len == 0) return;
   const int G = Hq / Hkv;
-  if (version != 2) {
+  const bf16_t* kv = static_cast<const bf16_t*>(kv_ptr);
+  if (version != 2 || kv_fp8) {  // the fp8 cache has the v3 path only
     dim3 grid3((max_q_len + 256 / G - 1) / (256 / G), Hkv, num_seqs), blk3(512);
+    const float sc = kv_fp8 ? scale * k_scale : scale, vs = kv_fp8 ? v_scale : 1.f;
 #define MXS_PF3(DD, GG)                                                                                    \
     if (D == DD && G == GG) {                                                                              \
-      hipLaunchKernelGGL((paged_prefill_v3_kernel<DD, GG>), grid3, blk3, 0, s, out, q, kv, block_stride,   \
-                         block_tables, bt_stride, qsl, seq_lens, Hkv, scale);                             \
+      if (kv_fp8)                                                                                          \
+        hipLaunchKernelGGL((paged_prefill_v3_kernel<DD, GG, 1>), grid3, blk3, 0, s, out, q, kv_ptr,        \
+                           block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs);             \
+      else                                                                                                 \
+        hipLaunchKernelGGL((paged_prefill_v3_kernel<DD, GG, 2>), grid3, blk3, 0, s, out, q, kv_ptr,        \
+                           block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs);             \
       MXS_CHECK_LAUNCH();                                                                                  \
       return;                                                                                              \
     }

@@ -11,14 +11,14 @@ typedef unsigned short bf16_t;
 void launch_rms_norm(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, float, hipStream_t);
 void launch_fused_add_rms_norm(bf16_t*, const bf16_t*, bf16_t*, const bf16_t*, int, int, float, hipStream_t);
 void launch_silu_mul(bf16_t*, const bf16_t*, int, int, hipStream_t);
-void launch_rope_and_cache(bf16_t*, const bf16_t*, const int64_t*, const float*, bf16_t*, long, const int64_t*,
-                           const bf16_t*, const bf16_t*, int, int, int, int, int, float, hipStream_t);
+void launch_rope_and_cache(bf16_t*, const bf16_t*, const int64_t*, const float*, void*, bool, long, const int64_t*,
+                           const bf16_t*, const bf16_t*, int, int, int, int, int, float, float, float, hipStream_t);
 int decode_num_partitions(int);
 void decode_plan(int, int, int, int*, int*);
-void launch_paged_decode(bf16_t*, float*, float*, const bf16_t*, const bf16_t*, long, const int*, int, const int*,
-                         int, int, int, int, int, int, float, hipStream_t);
-void launch_paged_prefill(bf16_t*, const bf16_t*, const bf16_t*, long, const int*, int, const int*, const int*,
-                          int, int, int, int, int, float, int, hipStream_t);
+void launch_paged_decode(bf16_t*, float*, float*, const bf16_t*, const void*, bool, long, const int*, int, const int*,
+                         int, int, int, int, int, int, float, float, float, hipStream_t);
+void launch_paged_prefill(bf16_t*, const bf16_t*, const void*, bool, long, const int*, int, const int*, const int*,
+                          int, int, int, int, int, float, int, float, float, hipStream_t);
 void launch_sample(int64_t*, const void*, bool, int, int, long, const float*, const float*, const int*,
                    const int64_t*, const int64_t*, hipStream_t);
 void launch_logprobs(float*, int64_t*, float*, const void*, bool, int, int, long, const int64_t*, const int64_t*, int,
@@ -69,36 +69,41 @@ void silu_mul(at::Tensor out, at::Tensor gu) {
   mxs::launch_silu_mul(bf(out), bf(gu), gu.numel() / (2 * I), I, stream());
 }
 
-// kv_layer: [NB, 2, Hkv, BS, D] view (block stride may exceed 2*Hkv*BS*D)
-void check_kv(const at::Tensor& kv, int Hkv, int D) {
-  CHECK_CUDA(kv); CHECK_BF16(kv);
+// kv_layer: [NB, 2, Hkv, BS, D] view (block stride may exceed 2*Hkv*BS*D); bf16, or fp8 e4m3fn
+// (float8_e4m3fn or raw uint8) for the fp8 KV cache.  Returns true for fp8.
+bool check_kv(const at::Tensor& kv, int Hkv, int D) {
+  CHECK_CUDA(kv);
+  const bool fp8 = kv.scalar_type() == at::kFloat8_e4m3fn || kv.scalar_type() == at::kByte;
+  TORCH_CHECK(fp8 || kv.scalar_type() == at::kBFloat16, "kv cache must be bf16 or fp8 (e4m3fn)");
   TORCH_CHECK(kv.dim() == 5 && kv.size(1) == 2 && kv.size(2) == Hkv && kv.size(4) == D, "bad kv_layer shape");
   TORCH_CHECK(kv.size(3) == 16, "block size must be 16");
   TORCH_CHECK(kv.stride(4) == 1 && kv.stride(3) == D && kv.stride(2) == 16 * D && kv.stride(1) == Hkv * 16 * D,
               "kv_layer inner dims must be dense");
+  return fp8;
 }
 
 void rope_and_cache(at::Tensor q_out, at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin, at::Tensor kv,
                     at::Tensor slot_mapping, std::optional<at::Tensor> qn, std::optional<at::Tensor> kn, int64_t Hq,
-                    int64_t Hkv, int64_t D, double eps) {
+                    int64_t Hkv, int64_t D, double eps, double k_scale, double v_scale) {
   CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_CONTIG(qkv); CHECK_CONTIG(q_out);
   TORCH_CHECK(positions.scalar_type() == at::kLong && slot_mapping.scalar_type() == at::kLong, "int64 indices");
   TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == D, "cos_sin must be fp32 [P, D]");
   TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv width mismatch");
-  check_kv(kv, Hkv, D);
+  const bool fp8 = check_kv(kv, Hkv, D);
   const bf16_t* qnp = qn.has_value() ? bf(*qn) : nullptr;
   const bf16_t* knp = kn.has_value() ? bf(*kn) : nullptr;
-  mxs::launch_rope_and_cache(bf(q_out), bf(qkv), positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), bf(kv),
-                             kv.stride(0), slot_mapping.data_ptr<int64_t>(), qnp, knp, qkv.size(0), Hq, Hkv, D, 16,
-                             static_cast<float>(eps), stream());
+  mxs::launch_rope_and_cache(bf(q_out), bf(qkv), positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
+                             kv.data_ptr(), fp8, kv.stride(0), slot_mapping.data_ptr<int64_t>(), qnp, knp, qkv.size(0),
+                             Hq, Hkv, D, 16, static_cast<float>(eps), static_cast<float>(k_scale),
+                             static_cast<float>(v_scale), stream());
 }
 
 void paged_attention_decode(at::Tensor out, at::Tensor q, at::Tensor kv, at::Tensor block_tables,
-                            at::Tensor seq_lens, double scale, int64_t max_seq_len) {
+                            at::Tensor seq_lens, double scale, int64_t max_seq_len, double k_scale, double v_scale) {
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_CONTIG(out);
   const int B = q.size(0), Hq = q.size(1), D = q.size(2);
   const int Hkv = kv.size(2);
-  check_kv(kv, Hkv, D);
+  const bool fp8 = check_kv(kv, Hkv, D);
   TORCH_CHECK(block_tables.scalar_type() == at::kInt && seq_lens.scalar_type() == at::kInt, "int32 tables");
   TORCH_CHECK(block_tables.stride(1) == 1, "block_tables rows must be contiguous");
   TORCH_CHECK(Hq % Hkv == 0, "GQA ratio");
@@ -110,25 +115,27 @@ void paged_attention_decode(at::Tensor out, at::Tensor q, at::Tensor kv, at::Ten
     tmp_ml = at::empty({B, Hq, P, 2}, q.options().dtype(at::kFloat));
   }
   mxs::launch_paged_decode(bf(out), P > 1 ? tmp_out.data_ptr<float>() : nullptr,
-                           P > 1 ? tmp_ml.data_ptr<float>() : nullptr, bf(q), bf(kv), kv.stride(0),
+                           P > 1 ? tmp_ml.data_ptr<float>() : nullptr, bf(q), kv.data_ptr(), fp8, kv.stride(0),
                            block_tables.data_ptr<int>(), block_tables.stride(0), seq_lens.data_ptr<int>(), B, Hq,
                            Hkv, D, P, /*part_len: split each sequence evenly*/ 0, static_cast<float>(scale),
-                           stream());
+                           static_cast<float>(k_scale), static_cast<float>(v_scale), stream());
 }
 
 void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Tensor block_tables, at::Tensor qsl,
-                             at::Tensor seq_lens, double scale, int64_t max_q_len, int64_t version) {
+                             at::Tensor seq_lens, double scale, int64_t max_q_len, int64_t version, double k_scale,
+                             double v_scale) {
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_CONTIG(out);
   const int Hq = q.size(1), D = q.size(2);
   const int Hkv = kv.size(2);
-  check_kv(kv, Hkv, D);
+  const bool fp8 = check_kv(kv, Hkv, D);
   TORCH_CHECK(qsl.scalar_type() == at::kInt && seq_lens.scalar_type() == at::kInt, "int32 metadata");
   TORCH_CHECK(block_tables.scalar_type() == at::kInt && block_tables.stride(1) == 1, "block_tables");
   const int S = seq_lens.size(0);
-  mxs::launch_paged_prefill(bf(out), bf(q), bf(kv), kv.stride(0), block_tables.data_ptr<int>(),
+  mxs::launch_paged_prefill(bf(out), bf(q), kv.data_ptr(), fp8, kv.stride(0), block_tables.data_ptr<int>(),
                             block_tables.stride(0), qsl.data_ptr<int>(), seq_lens.data_ptr<int>(), S,
                             static_cast<int>(max_q_len), Hq, Hkv, D, static_cast<float>(scale),
-                            static_cast<int>(version), stream());
+                            static_cast<int>(version), static_cast<float>(k_scale), static_cast<float>(v_scale),
+                            stream());
 }
 
 void sample(at::Tensor out, at::Tensor logits, at::Tensor temperature, at::Tensor top_p, at::Tensor top_k,
@@ -232,11 +239,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);
   m.def("silu_mul", &silu_mul);
-  m.def("rope_and_cache", &rope_and_cache);
-  m.def("paged_attention_decode", &paged_attention_decode);
+  m.def("rope_and_cache", &rope_and_cache, pybind11::arg("q_out"), pybind11::arg("qkv"), pybind11::arg("positions"),
+        pybind11::arg("cos_sin"), pybind11::arg("kv"), pybind11::arg("slot_mapping"), pybind11::arg("qn"),
+        pybind11::arg("kn"), pybind11::arg("Hq"), pybind11::arg("Hkv"), pybind11::arg("D"), pybind11::arg("eps"),
+        pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0);
+  m.def("paged_attention_decode", &paged_attention_decode, pybind11::arg("out"), pybind11::arg("q"),
+        pybind11::arg("kv"), pybind11::arg("block_tables"), pybind11::arg("seq_lens"), pybind11::arg("scale"),
+        pybind11::arg("max_seq_len"), pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0);
   m.def("paged_attention_prefill", &paged_attention_prefill, pybind11::arg("out"), pybind11::arg("q"),
         pybind11::arg("kv"), pybind11::arg("block_tables"), pybind11::arg("qsl"), pybind11::arg("seq_lens"),
-        pybind11::arg("scale"), pybind11::arg("max_q_len"), pybind11::arg("version") = 3);
+        pybind11::arg("scale"), pybind11::arg("max_q_len"), pybind11::arg("version") = 3,
+        pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0);
   m.def("sample", &sample);
   m.def("logprobs", &logprobs);
   m.def("apply_penalties", &apply_penalties);

@@ -21,6 +21,10 @@ class EngineArgs:
     # dispatched to expert owners with all-to-all, mxserve/parallel/expert.py)
     moe_dispatch: str = "allreduce"
     block_size: int = 16
+    # KV cache storage: "auto" (= the model dtype, bf16) or "fp8" / "fp8_e4m3" (OCP e4m3fn, the
+    # gfx950 fp8 format: half the bytes per token, so twice the tokens per GB and half the decode
+    # attention traffic; attention math stays bf16/fp32)
+    kv_cache_dtype: str = "auto"
     max_model_len: int = 8192
     max_num_seqs: int = 256
     max_num_batched_tokens: int = 8192

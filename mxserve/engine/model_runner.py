@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 import time
 from typing import Optional
 
@@ -110,10 +111,19 @@ class ModelRunner:
         self.weight_source = load_weights(self.model, args.load_format, args.seed)
         log.info("weights (%s) ready in %.1fs", self.weight_source, time.time() - t0)
         self.max_blocks_per_seq = math.ceil(args.max_model_len / self.bs)
+        # fp8 KV cache: e4m3fn bytes held in a uint8 tensor (every torch indexing op supports it;
+        # the kernels and the reference ops read it as e4m3fn)
+        kvd = args.kv_cache_dtype.lower()
+        if kvd not in ("auto", "bf16", "bfloat16", "fp8", "fp8_e4m3", "fp8_e4m3fn"):
+            raise ValueError(f"kv_cache_dtype must be auto|fp8 (got {args.kv_cache_dtype!r})")
+        self.kv_fp8 = kvd.startswith("fp8")
+        self.kv_dtype = torch.uint8 if self.kv_fp8 else self.dtype
+        if self.kv_fp8 and "MXS_KV_SCALE" not in os.environ:
+            self.model.calibrate_kv_scales(self.bs)
         self.num_blocks = self._determine_num_blocks()
         m = self.model
         self.kv_cache = torch.zeros(self.num_blocks, cfg.num_layers, 2, m.nkv, self.bs, cfg.head_dim,
-                                    dtype=self.dtype, device=self.device)
+                                    dtype=self.kv_dtype, device=self.device)
         self.block_bytes = self.kv_cache[0].numel() * self.kv_cache.element_size()
         # block tables live on the device, one persistent row per live request, updated
         # incrementally (a decode step touches at most one new entry per request)
@@ -169,7 +179,7 @@ class ModelRunner:
 
     def _local_num_blocks(self) -> int:
         a, c, m = self.args, self.cfg, self.model
-        per_block = c.num_layers * 2 * m.nkv * self.bs * c.head_dim * (2 if self.dtype != torch.float32 else 4)
+        per_block = c.num_layers * 2 * m.nkv * self.bs * c.head_dim * torch.empty(0, dtype=self.kv_dtype).element_size()
         if a.num_gpu_blocks:
             return int(a.num_gpu_blocks)
         if not self.is_gpu:

@@ -66,6 +66,10 @@ class TransformerLM:
         self.moe_dispatch = moe_dispatch
         # last layer of a prefill step: attention/o_proj/MLP only for the rows that produce logits
         self.prune_last_layer = os.environ.get("MXS_PRUNE_LAST_LAYER", "1") == "1"
+        # fp8 KV cache: stored = x / scale, per layer (1.0 until the runner calibrates them from a
+        # probe prefill, mxserve/engine/model_runner.py::_calibrate_kv_scales; MXS_KV_SCALE fixes all)
+        ks = float(os.environ.get("MXS_KV_SCALE", "1.0"))
+        self.kv_scales = [{"k_scale": ks, "v_scale": ks} for _ in range(cfg.num_layers)]
         self.device = torch.device(device)
         self.dtype = dtype
         tp = get_tp()
@@ -172,22 +176,25 @@ class TransformerLM:
         c, w, p = self.cfg, self.w, f"l{i}."
         qkv = ops.linear(h, w[p + "qkv"])
         q = ops.rope_and_cache(qkv, self.nh, self.nkv, self.hd, md.positions, self.cos_sin, kv_layer,
-                               md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"), c.rms_norm_eps)
+                               md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"), c.rms_norm_eps,
+                               **self.kv_scales[i])
         nd = md.num_decodes
         if not q.is_cuda:
-            o = ref.paged_attention(q, kv_layer, md.block_tables, md.query_start_loc, md.seq_lens, self.scale)
+            o = ref.paged_attention(q, kv_layer, md.block_tables, md.query_start_loc, md.seq_lens, self.scale,
+                                    **self.kv_scales[i])
         elif md.num_prefills == 0:
             o = ops.paged_attention_decode(q, kv_layer, md.block_tables, md.seq_lens, self.scale,
-                                           md.max_seq_len)
+                                           md.max_seq_len, **self.kv_scales[i])
         elif nd == 0:
             o = ops.paged_attention_prefill(q, kv_layer, md.block_tables, md.query_start_loc,
-                                            md.seq_lens, self.scale, md.max_query_len)
+                                            md.seq_lens, self.scale, md.max_query_len, **self.kv_scales[i])
         else:
             o = torch.empty_like(q)
             ops.paged_attention_decode(q[:nd], kv_layer, md.block_tables[:nd], md.seq_lens[:nd], self.scale,
-                                       md.max_seq_len, out=o[:nd])
+                                       md.max_seq_len, out=o[:nd], **self.kv_scales[i])
             ops.paged_attention_prefill(q[nd:], kv_layer, md.block_tables[nd:], md.prefill_query_start_loc,
-                                        md.seq_lens[nd:], self.scale, md.max_query_len, out=o[nd:])
+                                        md.seq_lens[nd:], self.scale, md.max_query_len, out=o[nd:],
+                                        **self.kv_scales[i])
         out = ops.linear(o.reshape(o.shape[0], -1), w[p + "o"])
         return tp_all_reduce(out)
 
@@ -199,7 +206,8 @@ class TransformerLM:
         c, w, p = self.cfg, self.w, f"l{i}."
         qkv = ops.linear(h, w[p + "qkv"])
         q = ops.rope_and_cache(qkv, self.nh, self.nkv, self.hd, md.positions, self.cos_sin, kv_layer,
-                               md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"), c.rms_norm_eps)
+                               md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"), c.rms_norm_eps,
+                               **self.kv_scales[i])
         ns = md.logits_indices.shape[0]
         if ns == 0:  # no sequence samples this step: the layer only wrote K/V
             return h.new_empty((0, h.shape[1]))
@@ -209,9 +217,9 @@ class TransformerLM:
         sl = md.seq_lens.index_select(0, seq)
         if not q.is_cuda:
             qsl = torch.arange(ns + 1, dtype=torch.int32, device=q.device)
-            o = ref.paged_attention(qs, kv_layer, bt, qsl, sl, self.scale)
+            o = ref.paged_attention(qs, kv_layer, bt, qsl, sl, self.scale, **self.kv_scales[i])
         else:
-            o = ops.paged_attention_decode(qs, kv_layer, bt, sl, self.scale, md.max_seq_len)
+            o = ops.paged_attention_decode(qs, kv_layer, bt, sl, self.scale, md.max_seq_len, **self.kv_scales[i])
         out = ops.linear(o.reshape(ns, -1), w[p + "o"])
         return tp_all_reduce(out)
 
@@ -229,6 +237,31 @@ class TransformerLM:
             a = ops.silu_mul(ops.linear(h, w[p + "gate_up"]))
             out = ops.linear(a, w[p + "down"])
         return tp_all_reduce(out)
+
+    @torch.inference_mode()
+    def calibrate_kv_scales(self, block_size: int = 16, n: int = 256, headroom: float = 2.0) -> None:
+        """Per-layer K / V scales for an fp8 KV cache from one probe prefill (seeded random tokens,
+        bf16 scratch cache): scale = amax / (448 / headroom), so the probe's largest value sits a
+        factor `headroom` below the e4m3 limit and small values stay out of the subnormal range
+        (vLLM's --calculate-kv-scales idea).  Every worker of a model derives the same scales from
+        the same weights, so prefill and decode workers agree on the bytes they exchange."""
+        c, dev = self.cfg, self.device
+        g = torch.Generator().manual_seed(1234)
+        ids = torch.randint(3, c.vocab_size, (n,), generator=g).to(dev)
+        nb = -(-n // block_size)
+        kv = torch.zeros(nb, c.num_layers, 2, self.nkv, block_size, c.head_dim, dtype=self.dtype, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        pos = torch.arange(n, device=dev)
+        qsl = torch.tensor([0, n], **i32)
+        md = AttnMetadata(positions=pos, slot_mapping=pos.clone(), block_tables=torch.arange(nb, **i32).unsqueeze(0),
+                          seq_lens=torch.tensor([n], **i32), query_start_loc=qsl,
+                          logits_indices=torch.tensor([n - 1], device=dev), num_decodes=0, num_prefills=1,
+                          num_prefill_tokens=n, max_query_len=n, max_seq_len=n, prefill_query_start_loc=qsl)
+        self.forward(ids, md, kv)
+        amax = kv.float().abs().amax(dim=(0, 3, 4, 5)).cpu()  # [L, 2]
+        lim = 448.0 / headroom
+        self.kv_scales = [{"k_scale": max(float(amax[i, 0]) / lim, 1e-8),
+                           "v_scale": max(float(amax[i, 1]) / lim, 1e-8)} for i in range(c.num_layers)]
 
     def embed(self, input_ids: torch.Tensor) -> torch.Tensor:
         return F.embedding(input_ids, self.w["embed"])

@@ -97,45 +97,48 @@ def silu_mul(gu: torch.Tensor) -> torch.Tensor:
 # ----------------------------------------------------------------------------- attention
 def rope_and_cache(qkv: torch.Tensor, num_heads: int, num_kv_heads: int, head_dim: int,
                    positions: torch.Tensor, cos_sin: torch.Tensor, kv_layer: torch.Tensor,
-                   slot_mapping: torch.Tensor, q_norm_w=None, k_norm_w=None, eps: float = 1e-6):
+                   slot_mapping: torch.Tensor, q_norm_w=None, k_norm_w=None, eps: float = 1e-6,
+                   k_scale: float = 1.0, v_scale: float = 1.0):
     """qkv [T, (Hq+2Hkv)*D] (fused projection output).  Applies optional q/k head RMSNorm and RoPE,
-    writes K/V into the paged cache, returns q [T, Hq, D]."""
+    writes K/V into the paged cache (bf16, or fp8 e4m3fn storing x / scale), returns q [T, Hq, D]."""
     T = qkv.shape[0]
     qs, ks = num_heads * head_dim, num_kv_heads * head_dim
     if _gpu(qkv):
         q = torch.empty(T, num_heads, head_dim, dtype=qkv.dtype, device=qkv.device)
         ext().rope_and_cache(q, qkv, positions, cos_sin, kv_layer, slot_mapping,
-                             q_norm_w, k_norm_w, num_heads, num_kv_heads, head_dim, eps)
+                             q_norm_w, k_norm_w, num_heads, num_kv_heads, head_dim, eps, k_scale, v_scale)
         return q
     q = qkv[:, :qs].reshape(T, num_heads, head_dim)
     k = qkv[:, qs:qs + ks].reshape(T, num_kv_heads, head_dim)
     v = qkv[:, qs + ks:].reshape(T, num_kv_heads, head_dim)
-    return ref.rope_and_cache(q, k, v, positions, cos_sin, kv_layer, slot_mapping, q_norm_w, k_norm_w, eps)
+    return ref.rope_and_cache(q, k, v, positions, cos_sin, kv_layer, slot_mapping, q_norm_w, k_norm_w, eps,
+                              k_scale, v_scale)
 
 
 def paged_attention_decode(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,
                            seq_lens: torch.Tensor, scale: float, max_seq_len: int,
-                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                           out: Optional[torch.Tensor] = None, k_scale: float = 1.0,
+                           v_scale: float = 1.0) -> torch.Tensor:
     """One query token per sequence.  q [B, Hq, D] -> [B, Hq, D] (written into `out` if given)."""
     if _gpu(q):
         out = torch.empty_like(q) if out is None else out
-        ext().paged_attention_decode(out, q, kv_layer, block_tables, seq_lens, scale, max_seq_len)
+        ext().paged_attention_decode(out, q, kv_layer, block_tables, seq_lens, scale, max_seq_len, k_scale, v_scale)
         return out
-    return ref.paged_attention_decode(q, kv_layer, block_tables, seq_lens, scale)
+    return ref.paged_attention_decode(q, kv_layer, block_tables, seq_lens, scale, k_scale, v_scale)
 
 
 def paged_attention_prefill(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,
                             query_start_loc: torch.Tensor, seq_lens: torch.Tensor, scale: float,
                             max_query_len: int, out: Optional[torch.Tensor] = None,
-                            version: int = 0) -> torch.Tensor:
+                            version: int = 0, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
     """Causal varlen attention of prefill chunks against the paged cache (prefix included).
     version: 0 = default (v3, LDS-shared K/V tiles; MXS_PREFILL_KERNEL=2 selects v2), 2 or 3."""
     if _gpu(q):
         out = torch.empty_like(q) if out is None else out
         ext().paged_attention_prefill(out, q, kv_layer, block_tables, query_start_loc, seq_lens,
-                                      scale, max_query_len, version or _PREFILL_VERSION)
+                                      scale, max_query_len, version or _PREFILL_VERSION, k_scale, v_scale)
         return out
-    return ref.paged_attention(q, kv_layer, block_tables, query_start_loc, seq_lens, scale)
+    return ref.paged_attention(q, kv_layer, block_tables, query_start_loc, seq_lens, scale, k_scale, v_scale)
 
 
 # ----------------------------------------------------------------------------- sampling

@@ -67,8 +67,23 @@ def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) 
     return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(x.dtype)
 
 
-def write_kv(kv_layer: torch.Tensor, k: torch.Tensor, v: torch.Tensor, slot_mapping: torch.Tensor):
-    """kv_layer [NB, 2, Hkv, BS, D]; k, v [T, Hkv, D]."""
+FP8_KV = (torch.float8_e4m3fn, torch.uint8)
+FP8_MAX = 448.0
+
+
+def is_fp8_kv(kv: torch.Tensor) -> bool:
+    return kv.dtype in FP8_KV
+
+
+def write_kv(kv_layer: torch.Tensor, k: torch.Tensor, v: torch.Tensor, slot_mapping: torch.Tensor,
+             k_scale: float = 1.0, v_scale: float = 1.0):
+    """kv_layer [NB, 2, Hkv, BS, D]; k, v [T, Hkv, D].  An fp8 (e4m3fn) cache stores x / scale,
+    saturated to +-448."""
+    if is_fp8_kv(kv_layer):
+        k = (k.float() / k_scale).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+        v = (v.float() / v_scale).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+        if kv_layer.dtype == torch.uint8:
+            k, v = k.view(torch.uint8), v.view(torch.uint8)
     bs = kv_layer.shape[3]
     d = kv_layer.shape[4]
     valid = slot_mapping >= 0
@@ -87,7 +102,7 @@ def write_kv(kv_layer: torch.Tensor, k: torch.Tensor, v: torch.Tensor, slot_mapp
 def rope_and_cache(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, positions: torch.Tensor,
                    cos_sin: torch.Tensor, kv_layer: torch.Tensor, slot_mapping: torch.Tensor,
                    q_norm_w: Optional[torch.Tensor] = None, k_norm_w: Optional[torch.Tensor] = None,
-                   eps: float = 1e-6):
+                   eps: float = 1e-6, k_scale: float = 1.0, v_scale: float = 1.0):
     """Optional per-head RMSNorm (Qwen3), RoPE on q/k, write k/v into the paged cache.
     q [T, Hq, D], k/v [T, Hkv, D].  Returns rotated q (new tensor)."""
     if q_norm_w is not None:
@@ -95,12 +110,22 @@ def rope_and_cache(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, positions:
         k = rms_norm(k, k_norm_w, eps)
     q = apply_rope(q, positions, cos_sin)
     k = apply_rope(k, positions, cos_sin)
-    write_kv(kv_layer, k, v, slot_mapping)
+    write_kv(kv_layer, k, v, slot_mapping, k_scale, v_scale)
     return q
 
 
-def gather_kv(kv_layer: torch.Tensor, block_table: torch.Tensor, n: int):
-    """Return K, V [n, Hkv, D] for the first n tokens of a sequence."""
+def gather_kv(kv_layer: torch.Tensor, block_table: torch.Tensor, n: int, k_scale: float = 1.0,
+              v_scale: float = 1.0):
+    """Return K, V [n, Hkv, D] for the first n tokens of a sequence (fp32, dequantised, for an fp8
+    cache)."""
+    if is_fp8_kv(kv_layer):
+        K, V = _gather_raw(kv_layer.view(torch.uint8), block_table, n)
+        f8 = torch.float8_e4m3fn
+        return K.view(f8).float() * k_scale, V.view(f8).float() * v_scale
+    return _gather_raw(kv_layer, block_table, n)
+
+
+def _gather_raw(kv_layer: torch.Tensor, block_table: torch.Tensor, n: int):
     bs, d, hkv = kv_layer.shape[3], kv_layer.shape[4], kv_layer.shape[2]
     nb = (n + bs - 1) // bs
     blocks = block_table[:nb].long()
@@ -127,7 +152,8 @@ def _attend(q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, q_pos0: int, scal
 
 
 def paged_attention(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,
-                    query_start_loc: torch.Tensor, seq_lens: torch.Tensor, scale: float) -> torch.Tensor:
+                    query_start_loc: torch.Tensor, seq_lens: torch.Tensor, scale: float, k_scale: float = 1.0,
+                    v_scale: float = 1.0) -> torch.Tensor:
     """Varlen causal attention over the paged cache (prefill chunks and decode alike).
     q [T, Hq, D]; sequence i owns q rows query_start_loc[i]:query_start_loc[i+1], whose positions
     are the LAST q_len positions of its seq_lens[i] tokens (cache already holds them)."""
@@ -138,14 +164,14 @@ def paged_attention(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch
         a, b = qsl[i], qsl[i + 1]
         if b <= a:
             continue
-        K, V = gather_kv(kv_layer, block_tables[i], sl[i])
+        K, V = gather_kv(kv_layer, block_tables[i], sl[i], k_scale, v_scale)
         out[a:b] = _attend(q[a:b], K, V, sl[i] - (b - a), scale)
     return out.to(q.dtype)
 
 
-def paged_attention_decode(q, kv_layer, block_tables, seq_lens, scale):
+def paged_attention_decode(q, kv_layer, block_tables, seq_lens, scale, k_scale: float = 1.0, v_scale: float = 1.0):
     qsl = torch.arange(q.shape[0] + 1, dtype=torch.int32)
-    return paged_attention(q, kv_layer, block_tables, qsl, seq_lens, scale)
+    return paged_attention(q, kv_layer, block_tables, qsl, seq_lens, scale, k_scale, v_scale)
 
 
 # ----------------------------------------------------------------------------- sampling

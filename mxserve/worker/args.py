@@ -58,6 +58,8 @@ def _parser(dialect: str) -> argparse.ArgumentParser:
     ap.add_argument("--gpu-memory-utilization", "--mem-fraction-static", "--free-gpu-memory-fraction",
                     dest="gpu_memory_utilization", type=float, default=None)
     ap.add_argument("--num-gpu-blocks-override", dest="num_gpu_blocks", type=int, default=None)
+    ap.add_argument("--kv-cache-dtype", dest="kv_cache_dtype", default=None,
+                    help="auto (bf16) | fp8 | fp8_e4m3 (vLLM / SGLang flag; TRT-LLM: kv_cache_config.dtype)")
     ap.add_argument("--enforce-eager", "--disable-cuda-graph", dest="enforce_eager", action="store_true",
                     default=None)
     ap.add_argument("--enable-prefix-caching", dest="enable_prefix_caching", action="store_true", default=None)
@@ -113,6 +115,8 @@ def load_extra_engine_args(path: str) -> dict:
         out["gpu_memory_utilization"] = float(kvc["free_gpu_memory_fraction"])
     if "enable_block_reuse" in kvc:
         out["enable_prefix_caching"] = bool(kvc["enable_block_reuse"])
+    if kvc.get("dtype"):
+        out["kv_cache_dtype"] = str(kvc["dtype"])
     if d.get("cuda_graph_config") is None and "cuda_graph_config" in d:
         out["enforce_eager"] = True
     return out
@@ -132,7 +136,7 @@ def parse_worker_args(argv: list[str], dialect: str = "vllm") -> WorkerArgs:
         "enable_chunked_prefill": a.enable_chunked_prefill, "device": a.device,
         "async_scheduling": a.async_scheduling, "moe_dispatch": a.moe_dispatch,
         "trust_remote_code": a.trust_remote_code or None, "skip_tokenizer_init": a.skip_tokenizer_init or None,
-        "bootstrap_port": a.disaggregation_bootstrap_port,
+        "bootstrap_port": a.disaggregation_bootstrap_port, "kv_cache_dtype": a.kv_cache_dtype,
     }
     kw.update({k: v for k, v in cli.items() if v is not None})
     mode = "agg"

@@ -81,6 +81,11 @@ def main():
     out.append({"op": "paged_decode_attn_layer", "B": B, "ctx": ctx, "ms": t, "GBps": byts / t / 1e6})
     t8k = timeit(lambda: ops.paged_attention_decode(q, kv[:, 0], bt, sl, 0.125, 8192))
     out.append({"op": "paged_decode_attn_layer_graphgrid8192", "ms": t8k, "GBps": byts / t8k / 1e6})
+    # fp8 (e4m3fn) cache of the same shape: half the bytes per token
+    kv8 = torch.empty(nb, 2, m.nkv, 16, cfg.head_dim, dtype=torch.uint8, device=dev)
+    kv8.copy_((kv[:, 0].float() * 16).to(torch.float8_e4m3fn).view(torch.uint8))
+    t = timeit(lambda: ops.paged_attention_decode(q, kv8, bt, sl, 0.125, ctx + 1, k_scale=1 / 16, v_scale=1 / 16))
+    out.append({"op": "paged_decode_attn_layer_fp8kv", "B": B, "ctx": ctx, "ms": t, "GBps": byts / 2 / t / 1e6})
 
     # ---- full decode step (eager and graph)
     pos = torch.full((B,), ctx, dtype=torch.int64, device=dev)
@@ -111,6 +116,32 @@ def main():
         tg = timeit(g.replay, iters=20)
     out.append({"op": "decode_step", "B": B, "ctx": ctx, "eager_ms": te, "graph_ms": tg,
                 "tok_per_s": B / tg * 1e3})
+    # same decode step over an fp8 (e4m3fn) copy of the cache (--kv-cache-dtype fp8)
+    kv8 = torch.empty(kv.shape, dtype=torch.uint8, device=dev)
+    for li in range(cfg.num_layers):
+        kv8[:, li].copy_((kv[:, li].float() * 16).to(torch.float8_e4m3fn).view(torch.uint8))
+    scales_bf16 = m.kv_scales
+    m.kv_scales = [{"k_scale": 1 / 16, "v_scale": 1 / 16} for _ in range(cfg.num_layers)]
+
+    def step8():
+        h = m.forward(ids, md, kv8)
+        lg = m.compute_logits(h)
+        return ops.sample(lg, temp, torch.ones(B, device=dev), torch.zeros(B, dtype=torch.int32, device=dev),
+                          torch.arange(B, device=dev), torch.zeros(B, dtype=torch.int64, device=dev))
+
+    with torch.inference_mode():
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            step8()
+        torch.cuda.current_stream().wait_stream(s)
+        g8 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g8):
+            step8()
+        tg8 = timeit(g8.replay, iters=20)
+    out.append({"op": "decode_step_fp8kv", "B": B, "ctx": ctx, "graph_ms": tg8, "tok_per_s": B / tg8 * 1e3})
+    m.kv_scales = scales_bf16
+    del kv8, g8
 
     # ---- prefill chunk (ctx 0, T tokens as 2 sequences)
     T = a.prefill

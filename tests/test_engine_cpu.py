@@ -168,3 +168,20 @@ def test_penalties_change_only_penalized_requests():
                         one(2.0), one(0.5), one(0.25))
     want = torch.tensor([[1.0, 1.0, -2.0 - 1.0 - 0.25, 0.25 - 0.5 - 0.25, 3.0, 0.0]])
     assert torch.allclose(logits, want)
+
+
+def test_fp8_kv_cache_engine():
+    """--kv-cache-dtype fp8: the pool holds e4m3fn bytes (1 byte per element), generation runs through
+    chunked prefill + prefix cache + decode, and the logits stay close to the full-precision cache."""
+    import torch
+    e32 = _engine(True)
+    ea = e32.args.replace(kv_cache_dtype="fp8")
+    e8 = LLMEngine(ea)
+    assert e8.runner.kv_cache.dtype == torch.uint8
+    assert e8.runner.block_bytes * 4 == e32.runner.block_bytes  # fp32 CPU reference cache vs 1-byte fp8
+    prompts = [list(range(7, 7 + n)) for n in (5, 40, 130)]
+    sp = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True)
+    a, b = e32.generate(prompts, sp), e8.generate(prompts, sp)
+    assert all(len(x) == 12 for x in b)
+    same = sum(x == y for pa, pb in zip(a, b) for x, y in zip(pa, pb))
+    assert same >= 0.6 * 36, (a, b)  # tiny random model: fp8 rounding flips some near-ties

@@ -93,6 +93,45 @@ def test_pruned_last_layer_matches_full(gpu, name):
     assert (pruned.topk(5, -1).indices == full.argmax(-1, keepdim=True)).any(-1).all()
 
 
+@pytest.mark.parametrize("name", ["small-llama", "tiny-qwen3-gpu"])
+def test_fp8_kv_forward_close_to_bf16(gpu, name):
+    """fp8 (e4m3fn) KV cache vs bf16 cache, same weights: prefill logits stay close."""
+    cfg = get_model_config(name)
+    sd = random_full_state(cfg, seed=1, std=0.05)
+    n = 77
+    ids = torch.randint(3, cfg.vocab_size, (n,), generator=torch.Generator().manual_seed(0)).to(gpu)
+    m = TransformerLM(cfg, gpu, torch.bfloat16)
+    m.load_full_state(sd)
+    shape = (8, cfg.num_layers, 2, cfg.num_kv_heads, 16, cfg.head_dim)
+    a = m.compute_logits(m.forward(ids, _prefill_md(n, gpu), torch.zeros(shape, dtype=torch.bfloat16,
+                                                                          device=gpu))).float().cpu()
+    m.calibrate_kv_scales()
+    b = m.compute_logits(m.forward(ids, _prefill_md(n, gpu), torch.zeros(shape, dtype=torch.uint8,
+                                                                          device=gpu))).float().cpu()
+    # e4m3 keeps 3 mantissa bits (up to 6 % per element); a random-weight model passes that noise
+    # through every layer untrained, so bound the typical error and the ranking, not the worst logit
+    scale = a.abs().max().item()
+    err = (b - a).abs()
+    assert err.mean().item() < 0.03 * scale and err.max().item() < 0.3 * scale
+    assert (b.topk(5, -1).indices == a.argmax(-1, keepdim=True)).any(-1).float().mean().item() > 0.9
+
+
+def test_fp8_kv_engine_graph_decode(gpu):
+    """Engine with --kv-cache-dtype fp8: half the block bytes, twice the blocks for the same memory,
+    hipGraph decode + chunked prefill produce full-length greedy outputs."""
+    e16 = _engine(gpu, False)
+    e8 = _engine(gpu, False, kv_cache_dtype="fp8")
+    assert e8.runner.kv_cache.dtype == torch.uint8 and e8.runner.graphs
+    assert e8.runner.block_bytes * 2 == e16.runner.block_bytes
+    prompts = [list(range(10, 10 + n)) for n in (5, 40, 130, 300)]
+    sp = SamplingParams(max_tokens=24, temperature=0.0, ignore_eos=True)
+    graph = e8.generate(prompts, sp)
+    eager = _engine(gpu, True, kv_cache_dtype="fp8").generate(prompts, sp)
+    assert all(len(x) == 24 for x in graph)
+    # same cache bytes through the graph and the eager path (bf16 reduction order aside)
+    assert sum(x == y for x, y in zip(graph, eager)) >= 3, (graph, eager)
+
+
 def _engine(gpu, eager, **kw):
     args = EngineArgs(model="small-llama", device="cuda", num_gpu_blocks=2048, max_model_len=2048,
                       max_num_seqs=32, cuda_graph_max_bs=32, enforce_eager=eager, load_format="random", seed=5, **kw)

@@ -151,6 +151,85 @@ def test_prefill_softmax_rescale_spike(gpu, version):
     _close(out, exp, 0.03, 0.03, "prefill-spike")
 
 
+# ---- fp8 (e4m3fn) KV cache: the cache bytes are shared by kernel and reference, so attention must
+# match the reference over the same dequantised values; the write path is checked byte-for-byte
+# against torch's e4m3fn rounding (off by one ulp allowed where f32 rounding of RoPE differs).
+def _fp8_cache(kv_bf16, scale=1.0):
+    return (kv_bf16.float() / scale).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+
+
+@pytest.mark.parametrize("D,hq,hkv,qknorm", [(64, 32, 8, False), (128, 16, 8, True)])
+@pytest.mark.parametrize("kscale", [1.0, 0.05])
+def test_rope_and_cache_fp8(gpu, D, hq, hkv, qknorm, kscale):
+    T, L, nb = 37, 2, 20
+    cos_sin = ref.build_cos_sin_cache(D, 4096, 500000.0, None, device=gpu)
+    qkv = (torch.randn(T, (hq + 2 * hkv) * D, device=gpu) * 3).to(torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=gpu)
+    slots = torch.randperm(nb * 16, device=gpu)[:T]
+    slots[5] = -1
+    qn = (1 + 0.1 * torch.randn(D, device=gpu)).bfloat16() if qknorm else None
+    kn = (1 + 0.1 * torch.randn(D, device=gpu)).bfloat16() if qknorm else None
+    kv = torch.zeros(nb, L, 2, hkv, 16, D, device=gpu, dtype=torch.uint8)
+    kv_ref = kv.clone().cpu()
+    q = ops.rope_and_cache(qkv, hq, hkv, D, pos, cos_sin, kv[:, 1], slots, qn, kn, 1e-6, k_scale=kscale,
+                           v_scale=kscale)
+    qs, ks = hq * D, hkv * D
+    c = qkv.cpu()
+    q_ref = ref.rope_and_cache(c[:, :qs].reshape(T, hq, D), c[:, qs:qs + ks].reshape(T, hkv, D),
+                               c[:, qs + ks:].reshape(T, hkv, D), pos.cpu(), cos_sin.cpu(), kv_ref[:, 1],
+                               slots.cpu(), None if qn is None else qn.cpu(), None if kn is None else kn.cpu(), 1e-6,
+                               k_scale=kscale, v_scale=kscale)
+    _close(q, q_ref, 0.03, 0.02, "q")
+    got = kv.cpu().view(torch.float8_e4m3fn).float()
+    exp = kv_ref.view(torch.float8_e4m3fn).float()
+    # e4m3 has 3 mantissa bits: one ulp is 12.5 % relative.  V (bf16 in, no RoPE) at scale 1 is
+    # exact; otherwise x * (1/scale) vs x / scale may straddle a rounding tie: one ulp at most
+    if kscale == 1.0:
+        _close(got[:, 1, 1], exp[:, 1, 1], 0.0, 0.0, "v bytes")
+    for kvi, name in ((0, "k"), (1, "v")):
+        _close(got[:, 1, kvi], exp[:, 1, kvi], 2 ** -9, 0.13, f"{name} bytes")
+        ulp = (kv.cpu()[:, 1, kvi].view(torch.int8).int() - kv_ref[:, 1, kvi].view(torch.int8).int()).abs()
+        assert ulp.max().item() <= 1, f"{name}: {ulp.max().item()} ulp"
+    assert kv[:, 0].sum().item() == 0  # other layer untouched
+
+
+@pytest.mark.parametrize("D,G", [(64, 4), (128, 2), (128, 8), (64, 1)])
+@pytest.mark.parametrize("scales", [(1.0, 1.0), (0.02, 0.05)])
+def test_paged_decode_fp8(gpu, D, G, scales):
+    ks, vs = scales
+    hkv, lens = 2, [1, 17, 513, 2000, 4096]
+    kv, bt = _paged_setup(lens, hkv, D, device=gpu)
+    kv8 = _fp8_cache(kv * (ks * 4), ks)  # stored values ~ N(0, 2): the fp8 grid is coarse there
+    B = len(lens)
+    q = torch.randn(B, hkv * G, D, device=gpu, dtype=torch.bfloat16)
+    sl = torch.tensor(lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    out = ops.paged_attention_decode(q, kv8[:, 1], bt.to(gpu), sl.to(gpu), scale, max(lens), k_scale=ks, v_scale=vs)
+    exp = ref.paged_attention_decode(q.cpu(), kv8[:, 1].cpu(), bt, sl, scale, ks, vs)
+    _close(out, exp, 0.02 * max(1.0, exp.abs().max().item()), 0.02, "decode fp8")
+
+
+@pytest.mark.parametrize("D,G", [(64, 4), (128, 2), (128, 8)])
+def test_paged_prefill_fp8(gpu, D, G):
+    hkv, ks, vs = 2, 0.5, 0.25
+    specs = [(0, 77), (300, 45), (16, 1), (33, 200)]
+    seq_lens = [c + n for c, n in specs]
+    kv, bt = _paged_setup(seq_lens, hkv, D, device=gpu)
+    kv8 = _fp8_cache(kv, 1.0)
+    qsl = [0]
+    for _, n in specs:
+        qsl.append(qsl[-1] + n)
+    q = torch.randn(qsl[-1], hkv * G, D, device=gpu, dtype=torch.bfloat16)
+    qsl_t = torch.tensor(qsl, dtype=torch.int32)
+    sl = torch.tensor(seq_lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    # version 2 requested: the fp8 cache always runs v3
+    out = ops.paged_attention_prefill(q, kv8[:, 1], bt.to(gpu), qsl_t.to(gpu), sl.to(gpu), scale,
+                                      max(n for _, n in specs), version=2, k_scale=ks, v_scale=vs)
+    exp = ref.paged_attention(q.cpu(), kv8[:, 1].cpu(), bt, qsl_t, sl, scale, ks, vs)
+    _close(out, exp, 0.03, 0.03, "prefill fp8")
+
+
 @pytest.mark.parametrize("dtype,V", [(torch.float32, 128256), (torch.bfloat16, 128256), (torch.bfloat16, 1001)])
 def test_sample_greedy(gpu, dtype, V):
     B = 16
