@@ -11,6 +11,8 @@ typedef unsigned short bf16_t;
 void launch_rms_norm(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, float, hipStream_t);
 void launch_fused_add_rms_norm(bf16_t*, const bf16_t*, bf16_t*, const bf16_t*, int, int, float, hipStream_t);
 void launch_silu_mul(bf16_t*, const bf16_t*, int, int, hipStream_t);
+void launch_embed_rms_norm(bf16_t*, bf16_t*, const int64_t*, const bf16_t*, const bf16_t*, int, int, float,
+                           hipStream_t);
 void launch_rope_and_cache(bf16_t*, const bf16_t*, const int64_t*, const float*, void*, bool, long, const int64_t*,
                            const bf16_t*, const bf16_t*, int, int, int, int, int, float, float, float, hipStream_t);
 int decode_num_partitions(int);
@@ -60,6 +62,17 @@ void fused_add_rms_norm(at::Tensor out, at::Tensor x, at::Tensor residual, at::T
   TORCH_CHECK(H % 8 == 0, "hidden size must be a multiple of 8");
   mxs::launch_fused_add_rms_norm(bf(out), bf(x), bf(residual), bf(w), x.numel() / H, H, static_cast<float>(eps),
                                  stream());
+}
+
+// K01 + first K02: out = rmsnorm(table[ids]) * w, residual = table[ids]
+void embed_rms_norm(at::Tensor out, at::Tensor residual, at::Tensor ids, at::Tensor table, at::Tensor w, double eps) {
+  CHECK_CUDA(table); CHECK_BF16(table); CHECK_BF16(w); CHECK_CONTIG(table); CHECK_CONTIG(out); CHECK_CONTIG(residual);
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous(), "ids must be contiguous int64");
+  const int H = table.size(1);
+  TORCH_CHECK(H % 8 == 0 && out.size(-1) == H && residual.size(-1) == H, "hidden size");
+  TORCH_CHECK(out.numel() == ids.numel() * H && residual.numel() == ids.numel() * H, "row count");
+  mxs::launch_embed_rms_norm(bf(out), bf(residual), ids.data_ptr<int64_t>(), bf(table), bf(w), ids.numel(), H,
+                             static_cast<float>(eps), stream());
 }
 
 void silu_mul(at::Tensor out, at::Tensor gu) {
@@ -239,6 +252,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);
   m.def("silu_mul", &silu_mul);
+  m.def("embed_rms_norm", &embed_rms_norm);
   m.def("rope_and_cache", &rope_and_cache, pybind11::arg("q_out"), pybind11::arg("qkv"), pybind11::arg("positions"),
         pybind11::arg("cos_sin"), pybind11::arg("kv"), pybind11::arg("slot_mapping"), pybind11::arg("qn"),
         pybind11::arg("kn"), pybind11::arg("Hq"), pybind11::arg("Hkv"), pybind11::arg("D"), pybind11::arg("eps"),

@@ -1,4 +1,5 @@
-// K02 RMSNorm (+ fused residual add) and K10 SiLU*mul for gfx950.
+// K02 RMSNorm (+ fused residual add), K01 embedding gather fused into the first RMSNorm, and K10
+// SiLU*mul for gfx950.
 // Memory-bound: every access is a 16-byte bf16x8 vector (cdna_hip_programming.md Guideline 13),
 // the row stays in registers between the reduction and the scaled write (one HBM pass).
 #include "common.h"
@@ -6,14 +7,18 @@
 namespace mxs {
 
 // One workgroup per row. NV = number of bf16x8 vectors each thread keeps in registers.
-template <int NV, bool ADD>
+// EMBED: row r of x is the embedding row ids[r] (x = the table); the gathered row is also written to
+// `residual` (the residual stream starts as the embedding), so the first layer's input norm reads
+// the table once instead of an embedding kernel writing x and the norm reading it back.
+template <int NV, bool ADD, bool EMBED = false>
 __global__ void __launch_bounds__(1024) rmsnorm_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ x,
                                                        bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
-                                                       int H, int x_stride, float eps) {
+                                                       int H, int x_stride, float eps,
+                                                       const int64_t* __restrict__ ids = nullptr) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
-  const bf16_t* xr = x + static_cast<size_t>(row) * x_stride;
-  bf16_t* rr = ADD ? residual + static_cast<size_t>(row) * H : nullptr;
+  const bf16_t* xr = x + (EMBED ? ids[row] : static_cast<int64_t>(row)) * x_stride;
+  bf16_t* rr = (ADD || EMBED) ? residual + static_cast<size_t>(row) * H : nullptr;
   const int nvec = H >> 3;
   uint4 v[NV];
   float ss = 0.f;
@@ -31,6 +36,7 @@ __global__ void __launch_bounds__(1024) rmsnorm_kernel(bf16_t* __restrict__ out,
           pa[k] = pack2(bf2f_lo(pa[k]) + bf2f_lo(pb[k]), bf2f_hi(pa[k]) + bf2f_hi(pb[k]));
         *reinterpret_cast<uint4*>(rr + c * 8) = a;
       }
+      if (EMBED) *reinterpret_cast<uint4*>(rr + c * 8) = a;
       v[i] = a;
       const uint32_t* p = reinterpret_cast<const uint32_t*>(&a);
 #pragma unroll
@@ -59,22 +65,32 @@ __global__ void __launch_bounds__(1024) rmsnorm_kernel(bf16_t* __restrict__ out,
   }
 }
 
-template <bool ADD>
+template <bool ADD, bool EMBED = false>
 static void launch_rmsnorm_t(bf16_t* out, const bf16_t* x, bf16_t* res, const bf16_t* w, int rows, int H,
-                             int x_stride, float eps, hipStream_t s) {
+                             int x_stride, float eps, hipStream_t s, const int64_t* ids = nullptr) {
+  if (rows == 0) return;
   const int nvec = H / 8;
   // one bf16x8 per thread up to H = 8192 (1024 threads); wider rows keep NV vectors per thread
   const int threads = nvec <= 1024 ? ((nvec + 63) / 64) * 64 : 1024;
   const int nv = (nvec + threads - 1) / threads;
   dim3 g(rows), b(threads);
+#define MXS_RMS(NVV) \
+  hipLaunchKernelGGL((rmsnorm_kernel<NVV, ADD, EMBED>), g, b, 0, s, out, x, res, w, H, x_stride, eps, ids)
   switch (nv) {
-    case 1: hipLaunchKernelGGL((rmsnorm_kernel<1, ADD>), g, b, 0, s, out, x, res, w, H, x_stride, eps); break;
-    case 2: hipLaunchKernelGGL((rmsnorm_kernel<2, ADD>), g, b, 0, s, out, x, res, w, H, x_stride, eps); break;
-    case 3: hipLaunchKernelGGL((rmsnorm_kernel<3, ADD>), g, b, 0, s, out, x, res, w, H, x_stride, eps); break;
-    case 4: hipLaunchKernelGGL((rmsnorm_kernel<4, ADD>), g, b, 0, s, out, x, res, w, H, x_stride, eps); break;
-    default: hipLaunchKernelGGL((rmsnorm_kernel<8, ADD>), g, b, 0, s, out, x, res, w, H, x_stride, eps); break;
+    case 1: MXS_RMS(1); break;
+    case 2: MXS_RMS(2); break;
+    case 3: MXS_RMS(3); break;
+    case 4: MXS_RMS(4); break;
+    default: MXS_RMS(8); break;
   }
+#undef MXS_RMS
   MXS_CHECK_LAUNCH();
+}
+
+// h = rmsnorm(table[ids]) * w, residual = table[ids]
+void launch_embed_rms_norm(bf16_t* out, bf16_t* residual, const int64_t* ids, const bf16_t* table, const bf16_t* w,
+                           int rows, int H, float eps, hipStream_t s) {
+  launch_rmsnorm_t<false, true>(out, table, residual, w, rows, H, H, eps, s, ids);
 }
 
 void launch_rms_norm(bf16_t* out, const bf16_t* x, const bf16_t* w, int rows, int H, int x_stride, float eps,

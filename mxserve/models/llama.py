@@ -269,16 +269,14 @@ class TransformerLM:
     def forward(self, input_ids: torch.Tensor, md: AttnMetadata, kv_cache: torch.Tensor) -> torch.Tensor:
         """Returns final hidden states (normed) of the rows selected by md.logits_indices."""
         c = self.cfg
-        x = self.embed(input_ids)
-        residual = None
+        # K01: the embedding gather runs inside the first layer's input RMSNorm kernel
+        h, residual = ops.embed_rms_norm(input_ids, self.w["embed"], self.w["l0.in_norm"], c.rms_norm_eps)
+        x = None
         # steps with prefill chunks: the last layer only computes the rows that produce logits
         prune = self.prune_last_layer and md.num_prefills > 0 and md.sample_seq is not None
         for i in range(c.num_layers):
             p = f"l{i}."
-            if residual is None:
-                residual = x
-                h = ops.rms_norm(x, self.w[p + "in_norm"], c.rms_norm_eps)
-            else:
+            if i > 0:
                 h, residual = ops.fused_add_rms_norm(x, residual, self.w[p + "in_norm"], c.rms_norm_eps)
             if prune and i == c.num_layers - 1:
                 x = self._attention_sampled(i, h, md, kv_cache[:, i])

@@ -86,6 +86,19 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
     return ref.fused_add_rms_norm(x, residual, w, eps)
 
 
+def embed_rms_norm(ids: torch.Tensor, table: torch.Tensor, w: torch.Tensor, eps: float):
+    """Embedding gather fused with the first layer's input RMSNorm: returns (normed, residual)
+    where residual = table[ids]."""
+    if _gpu(table):
+        T, H = ids.shape[0], table.shape[1]
+        out = torch.empty(T, H, dtype=table.dtype, device=table.device)
+        res = torch.empty(T, H, dtype=table.dtype, device=table.device)
+        ext().embed_rms_norm(out, res, ids, table, w, eps)
+        return out, res
+    x = torch.nn.functional.embedding(ids, table)
+    return ref.rms_norm(x, w, eps), x
+
+
 def silu_mul(gu: torch.Tensor) -> torch.Tensor:
     if _gpu(gu):
         out = torch.empty(gu.shape[:-1] + (gu.shape[-1] // 2,), dtype=gu.dtype, device=gu.device)

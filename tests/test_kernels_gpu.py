@@ -38,6 +38,19 @@ def test_fused_add_rms_norm(gpu, H):
     _close(y, ey, 0.03, 0.02, "normed")
 
 
+@pytest.mark.parametrize("H", [1024, 2048, 4096, 8192])
+def test_embed_rms_norm(gpu, H):
+    """Embedding gather fused into the first RMSNorm: residual = table[ids] bit-exact, normed vs fp32."""
+    V, T = 5000, 67
+    table = torch.randn(V, H, device=gpu, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16()
+    ids = torch.randint(0, V, (T,), device=gpu)
+    ids[3] = V - 1
+    h, res = ops.embed_rms_norm(ids, table, w, 1e-5)
+    assert torch.equal(res, table[ids])
+    _close(h, ref.rms_norm(table[ids].cpu(), w.cpu(), 1e-5), 0.02, 0.02, "embed_rms_norm")
+
+
 @pytest.mark.parametrize("I", [8192, 3584, 1792])
 def test_silu_mul(gpu, I):
     gu = torch.randn(19, 2 * I, device=gpu, dtype=torch.bfloat16)
