@@ -28,7 +28,8 @@ void launch_logprobs(float*, int64_t*, float*, const void*, bool, int, int, long
 void launch_penalties(void*, bool, int, int, long, const int*, long, const int64_t*, const int*, const int*,
                       const float*, const float*, const float*, int*, hipStream_t);
 void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStream_t);
-void launch_moe_align(int*, int*, const int*, int, int, int, hipStream_t);
+void launch_moe_align(int*, int*, const int*, int, int, int, int*, hipStream_t);
+void launch_moe_combine(bf16_t*, const bf16_t*, const float*, const int*, int, int, int, hipStream_t);
 bool launch_skinny_gemm(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, hipStream_t);
 bool launch_moe_grouped_gemm(bf16_t*, const bf16_t*, const bf16_t*, const int*, int, int, int, int, int, bool,
                              hipStream_t);
@@ -235,12 +236,25 @@ void moe_topk_softmax(at::Tensor w, at::Tensor ids, at::Tensor logits) {
                                logits.size(1), w.size(1), stream());
 }
 
-void moe_align(at::Tensor expert_offsets, at::Tensor perm, at::Tensor topk_ids, int64_t e_lo, int64_t e_local) {
+void moe_align(at::Tensor expert_offsets, at::Tensor perm, at::Tensor topk_ids, int64_t e_lo, int64_t e_local,
+               std::optional<at::Tensor> inv) {
   CHECK_CUDA(topk_ids); CHECK_CONTIG(topk_ids);
   TORCH_CHECK(topk_ids.scalar_type() == at::kInt, "int32 ids");
   TORCH_CHECK(e_local <= 256, "at most 256 local experts");
+  if (inv.has_value())
+    TORCH_CHECK(inv->scalar_type() == at::kInt && inv->numel() == topk_ids.numel(), "inv: int32 [T K]");
   mxs::launch_moe_align(expert_offsets.data_ptr<int>(), perm.data_ptr<int>(), topk_ids.data_ptr<int>(),
-                        topk_ids.numel(), e_lo, e_local, stream());
+                        topk_ids.numel(), e_lo, e_local, inv.has_value() ? inv->data_ptr<int>() : nullptr, stream());
+}
+
+// K17: out[t] = sum_k topk_w[t, k] * ys[inv[t, k]] (inv from moe_align; < 0 = not a local expert)
+void moe_combine(at::Tensor out, at::Tensor ys, at::Tensor topk_w, at::Tensor inv) {
+  CHECK_CUDA(ys); CHECK_BF16(ys); CHECK_BF16(out); CHECK_CONTIG(ys); CHECK_CONTIG(out);
+  TORCH_CHECK(topk_w.scalar_type() == at::kFloat && topk_w.is_contiguous() && topk_w.dim() == 2, "topk_w fp32 [T, K]");
+  TORCH_CHECK(inv.scalar_type() == at::kInt && inv.is_contiguous() && inv.numel() == topk_w.numel(), "inv");
+  const int T = topk_w.size(0), K = topk_w.size(1), H = ys.size(1);
+  TORCH_CHECK(K <= 8 && H % 8 == 0 && out.size(0) == T && out.size(1) == H, "shapes");
+  mxs::launch_moe_combine(bf(out), bf(ys), topk_w.data_ptr<float>(), inv.data_ptr<int>(), T, K, H, stream());
 }
 
 }  // namespace
@@ -268,7 +282,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("logprobs", &logprobs);
   m.def("apply_penalties", &apply_penalties);
   m.def("moe_topk_softmax", &moe_topk_softmax);
-  m.def("moe_align", &moe_align);
+  m.def("moe_align", &moe_align, pybind11::arg("expert_offsets"), pybind11::arg("perm"), pybind11::arg("topk_ids"),
+        pybind11::arg("e_lo"), pybind11::arg("e_local"), pybind11::arg("inv") = pybind11::none());
+  m.def("moe_combine", &moe_combine);
   m.def("skinny_gemm", &skinny_gemm);
   m.def("moe_grouped_gemm", &moe_grouped_gemm);
   m.def("decode_num_partitions", &mxs::decode_num_partitions);

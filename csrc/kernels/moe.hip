@@ -1,6 +1,7 @@
 // K14 (MoE router): softmax over experts -> top-k -> renormalise, one wave per token (lane = expert).
 // K15 (MoE align): tokens bucketed by expert with a counting sort so each expert's rows are
-// contiguous for the grouped GEMM; K17 combine is a weighted scatter-add back to token order.
+// contiguous for the grouped GEMM; K17 (MoE combine): each token gathers its top-k expert rows
+// through the inverse permutation and sums them with the routing weights (no scatter atomics).
 #include "common.h"
 
 namespace mxs {
@@ -55,9 +56,10 @@ void launch_moe_topk_softmax(float* w, int* ids, const bf16_t* logits, int T, in
 // index of each permuted row.  Only experts in [e_lo, e_lo + E_local) are kept (expert parallel).
 // One workgroup: per 64-assignment chunk every wave-lane learns its rank among equal experts from
 // one ballot per local expert (E_local <= 64 on every config here).
+// inv (optional): inv[i] = permuted row of assignment i, -1 when its expert is not local.
 __global__ void __launch_bounds__(64) moe_align_kernel(int* __restrict__ expert_offsets, int* __restrict__ perm,
                                                        const int* __restrict__ topk_ids, int TK, int e_lo,
-                                                       int E_local) {
+                                                       int E_local, int* __restrict__ inv) {
   __shared__ int cnt[257];
   const int lane = threadIdx.x;
   const unsigned long long lt = (1ull << lane) - 1ull;
@@ -86,13 +88,54 @@ __global__ void __launch_bounds__(64) moe_align_kernel(int* __restrict__ expert_
       __syncthreads();
     }
     if (dst >= 0) perm[dst] = i;
+    if (inv != nullptr && i < TK) inv[i] = dst;
   }
 }
 
 void launch_moe_align(int* expert_offsets, int* perm, const int* topk_ids, int TK, int e_lo, int E_local,
-                      hipStream_t s) {
+                      int* inv, hipStream_t s) {
   hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(64), 0, s, expert_offsets, perm, topk_ids, TK, e_lo,
-                     E_local);
+                     E_local, inv);
+  MXS_CHECK_LAUNCH();
+}
+
+// out[t] = sum_k w[t, k] * ys[inv[t K + k]] (rows with inv < 0 belong to other ranks' experts).
+// One workgroup per token; 16-byte vectors, fp32 accumulation, one bf16 write per element.
+__global__ void __launch_bounds__(256) moe_combine_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ ys,
+                                                          const float* __restrict__ topk_w,
+                                                          const int* __restrict__ inv, int K, int H) {
+  const int t = blockIdx.x;
+  int rows[8];
+  float ws[8];
+  for (int k = 0; k < K; ++k) {
+    rows[k] = inv[t * K + k];
+    ws[k] = topk_w[t * K + k];
+  }
+  for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < K; ++k) {
+      if (rows[k] < 0) continue;
+      const uint4 v = *reinterpret_cast<const uint4*>(ys + static_cast<size_t>(rows[k]) * H + c * 8);
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] += ws[k] * bf2f_lo(p[j]);
+        acc[2 * j + 1] += ws[k] * bf2f_hi(p[j]);
+      }
+    }
+    uint4 o;
+    o.x = pack2(acc[0], acc[1]);
+    o.y = pack2(acc[2], acc[3]);
+    o.z = pack2(acc[4], acc[5]);
+    o.w = pack2(acc[6], acc[7]);
+    *reinterpret_cast<uint4*>(out + static_cast<size_t>(t) * H + c * 8) = o;
+  }
+}
+
+void launch_moe_combine(bf16_t* out, const bf16_t* ys, const float* topk_w, const int* inv, int T, int K, int H,
+                        hipStream_t s) {
+  if (T == 0) return;
+  hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, s, out, ys, topk_w, inv, K, H);
   MXS_CHECK_LAUNCH();
 }
 

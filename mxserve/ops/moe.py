@@ -3,7 +3,8 @@
 fused_experts: the moe_align counting sort buckets the (token, slot) assignments by local expert,
 the rows are gathered once, and two MFMA grouped-GEMM launches (csrc/kernels/moe_gemm.hip) run
 every local expert over exactly its rows -- gate_up with SiLU*mul fused into the epilogue, then
-down -- before a weighted scatter-add restores token order.  No host sync anywhere, so decode steps
+down -- before the combine kernel gathers each token's top-k rows back (weighted, fp32 accumulate,
+one bf16 write per element; csrc/kernels/moe.hip).  No host sync anywhere, so decode steps
 stay hipGraph-capturable and prefill costs two launches instead of 2 x E_local GEMMs.
 _fused_experts_loop keeps the per-expert formulation (dense over all tokens at small T, sorted rows
 otherwise) for shapes the grouped kernel does not tile.
@@ -83,8 +84,8 @@ def fused_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: 
     ids = topk_ids.to(torch.int32).contiguous()
     offs = torch.empty(e_local + 1, dtype=torch.int32, device=dev)
     perm = torch.full((T * K,), -1, dtype=torch.int32, device=dev)
-    ext().moe_align(offs, perm, ids, expert_offset, e_local)
-    valid = (perm >= 0).unsqueeze(1)
+    inv = torch.empty(T * K, dtype=torch.int32, device=dev)
+    ext().moe_align(offs, perm, ids, expert_offset, e_local, inv)
     rows = perm.clamp(min=0).long()
     tok = rows // K
     xs = x.index_select(0, tok)  # rows past the routed count are ignored by the GEMMs
@@ -93,8 +94,6 @@ def fused_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: 
     if not (ext().moe_grouped_gemm(h, xs, w13.contiguous(), offs, True)
             and ext().moe_grouped_gemm(ys, h, w2.contiguous(), offs, False)):
         return _fused_experts_loop(x, w13, w2, topk_w, topk_ids, expert_offset)
-    wts = topk_w.reshape(-1).index_select(0, rows).unsqueeze(1)
-    contrib = torch.where(valid, ys.float() * wts, torch.zeros((), dtype=torch.float32, device=dev))
-    out = torch.zeros(T, H, dtype=torch.float32, device=dev)
-    out.index_add_(0, tok, contrib)
-    return out.to(x.dtype)
+    out = torch.empty(T, H, dtype=x.dtype, device=dev)
+    ext().moe_combine(out, ys, topk_w.float().contiguous(), inv)  # K17
+    return out

@@ -348,7 +348,8 @@ def test_moe_align(gpu):
     ids = torch.randint(0, E, (T, K), dtype=torch.int32, device=gpu)
     offs = torch.empty(E // 2 + 1, dtype=torch.int32, device=gpu)
     perm = torch.full((T * K,), -1, dtype=torch.int32, device=gpu)
-    ops.ext().moe_align(offs, perm, ids, 4, E // 2)  # local experts 4..7
+    inv = torch.empty(T * K, dtype=torch.int32, device=gpu)
+    ops.ext().moe_align(offs, perm, ids, 4, E // 2, inv)  # local experts 4..7
     flat = ids.flatten().cpu()
     o = offs.cpu().tolist()
     p = perm.cpu()
@@ -356,6 +357,25 @@ def test_moe_align(gpu):
         rows = p[o[e]:o[e + 1]]
         exp = (flat == e + 4).nonzero().flatten()
         assert torch.equal(rows.long(), exp), f"expert {e}"
+    iv = inv.cpu().long()
+    local = flat >= 4
+    assert torch.equal(p[iv[local]].long(), torch.arange(T * K)[local])  # inverse permutation
+    assert (iv[~local] == -1).all()
+
+
+def test_moe_combine(gpu):
+    """K17: each token sums its top-k expert rows (gathered through the inverse permutation) with
+    the routing weights; rows owned by other ranks (inv < 0) contribute nothing."""
+    T, K, H, R = 77, 2, 512, 120
+    ys = torch.randn(R, H, device=gpu, dtype=torch.bfloat16)
+    w = torch.rand(T, K, device=gpu)
+    inv = torch.randint(-1, R, (T * K,), device=gpu, dtype=torch.int32)
+    out = torch.empty(T, H, device=gpu, dtype=torch.bfloat16)
+    ops.ext().moe_combine(out, ys, w, inv)
+    yv = torch.cat([ys.float().cpu(), torch.zeros(1, H)])
+    idx = inv.cpu().long().view(T, K)
+    exp = (yv[torch.where(idx < 0, R, idx)] * w.cpu().unsqueeze(-1)).sum(1)
+    _close(out, exp, 0.02, 0.01, "moe_combine")
 
 
 @pytest.mark.parametrize("T", [64, 300])
