@@ -17,6 +17,9 @@ def build_parser() -> argparse.ArgumentParser:
                     default=os.environ.get("DYN_ROUTER_MODE", "kv"))
     ap.add_argument("--lease-ttl", type=float, default=float(os.environ.get("MXS_LEASE_TTL", "10")))
     ap.add_argument("--namespace", default=os.environ.get("DYN_NAMESPACE", "default"))
+    ap.add_argument("--reasoning-parser", "--dyn-reasoning-parser", dest="reasoning_parser",
+                    choices=["qwen3", "basic", "deepseek_r1"], default=os.environ.get("MXS_REASONING_PARSER"),
+                    help="split <think> blocks of chat completions into message.reasoning_content")
     ap.add_argument("--local-model", default=os.environ.get("MXS_LOCAL_MODEL"),
                     help="also serve this model from an in-process engine")
     ap.add_argument("--local-device", default=os.environ.get("MXS_LOCAL_DEVICE", "auto"))
@@ -29,7 +32,8 @@ def main(argv=None) -> None:
     a = build_parser().parse_args(argv)
     from ..utils.logs import setup_logging
     setup_logging()
-    fe = Frontend(router_mode=a.router_mode, ttl=a.lease_ttl, namespace=a.namespace)
+    fe = Frontend(router_mode=a.router_mode, ttl=a.lease_ttl, namespace=a.namespace,
+                  reasoning_parser=a.reasoning_parser)
     if a.local_model:
         from ..config import EngineArgs, env_overrides
         from ..engine.engine import AsyncEngine, LLMEngine

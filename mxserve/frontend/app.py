@@ -18,6 +18,7 @@ import asyncio
 import contextlib
 import json
 import logging
+import os
 import time
 import uuid
 from dataclasses import dataclass
@@ -31,6 +32,7 @@ from ..router.router import Registry, Router, WorkerInfo
 from ..utils.tracing import TRACER
 from .chat_template import render
 from .metrics import FrontendMetrics
+from .reasoning import ReasoningSplitter, split_text
 from .tokenizer import IncrementalDetokenizer, load_tokenizer
 
 log = logging.getLogger("mxserve.frontend")
@@ -117,8 +119,12 @@ class LocalWorker:
 
 class Frontend:
     def __init__(self, router_mode: str = "kv", ttl: float = 10.0, namespace: str = "default",
-                 migrate: bool = True):
+                 migrate: bool = True, reasoning_parser: Optional[str] = None):
         self.registry = Registry(ttl=ttl)
+        # chat completions: split <think> blocks into `reasoning_content` (qwen3 | basic | deepseek_r1)
+        self.reasoning_parser = reasoning_parser or os.environ.get("MXS_REASONING_PARSER") or None
+        if self.reasoning_parser:
+            ReasoningSplitter(self.reasoning_parser)  # validate the name at startup
         self.migrate = migrate  # move a broken stream to another worker (prompt + generated re-prefilled)
         self.router = Router(self.registry, router_mode)
         self.metrics = FrontendMetrics()
@@ -424,9 +430,14 @@ class Frontend:
                     lp_evs.extend(evs)
                     reason = r or reason
                 text = "".join(parts)
-                choice = ({"index": idx, "message": {"role": "assistant", "content": text},
-                           "finish_reason": reason or "stop"}
-                          if chat else {"index": idx, "text": text, "logprobs": None, "finish_reason": reason or "stop"})
+                if chat:
+                    reasoning, text = split_text(text, self.reasoning_parser)
+                    msg = {"role": "assistant", "content": text}
+                    if reasoning is not None:
+                        msg["reasoning_content"] = reasoning
+                    choice = {"index": idx, "message": msg, "finish_reason": reason or "stop"}
+                else:
+                    choice = {"index": idx, "text": text, "logprobs": None, "finish_reason": reason or "stop"}
                 if want_lp:
                     choice["logprobs"] = lp_payload(lp_evs)
                 return choice
@@ -449,12 +460,17 @@ class Frontend:
 
         sent = [0] * n_choices  # characters streamed per choice (completions text_offset)
 
+        splitters = ([ReasoningSplitter(self.reasoning_parser) for _ in range(n_choices)]
+                     if chat and self.reasoning_parser else None)
+
         def chunk(delta: Optional[str], reason: Optional[str], first: bool = False, evs: tuple = (),
-                  idx: int = 0) -> bytes:
+                  idx: int = 0, reasoning: Optional[str] = None) -> bytes:
             if chat:
                 d = {}
                 if first:
                     d["role"] = "assistant"
+                if reasoning:
+                    d["reasoning_content"] = reasoning
                 if delta is not None:
                     d["content"] = delta
                 ch = {"index": idx, "delta": d, "finish_reason": reason}
@@ -474,8 +490,11 @@ class Frontend:
                     for i in range(n_choices):
                         yield chunk("", None, first=True, idx=i)
                 async for i, (d, r, evs) in _merge([events(i) for i in range(n_choices)]):
-                    if d or r:
-                        yield chunk(d if d else ("" if r else None), r, evs=evs, idx=i)
+                    rd = None
+                    if splitters is not None:
+                        rd, d = splitters[i].feed(d, final=bool(r))
+                    if d or r or rd:
+                        yield chunk(d if d else ("" if r else None), r, evs=evs, idx=i, reasoning=rd)
                 if include_usage:
                     yield ("data: " + json.dumps({"id": rid, "object": chunk_obj, "created": created, "model": model,
                                                   "choices": [], "usage": {"prompt_tokens": len(prompt_ids),

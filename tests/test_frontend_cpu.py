@@ -207,6 +207,30 @@ def test_penalty_params(agg_stack):
     assert httpx.post(fs.url + "/v1/chat/completions", json=dict(body, repetition_penalty=0)).status_code == 400
 
 
+def test_reasoning_parser_fields(agg_stack):
+    """With a reasoning parser the <think> part goes to message.reasoning_content (unary) and
+    delta.reasoning_content (SSE).  deepseek_r1 starts in reasoning mode, so a completion without
+    </think> is all reasoning: the plumbing is visible with any model."""
+    fe, fs, _ = agg_stack
+    body = {"model": MODEL, "messages": [{"role": "user", "content": "think"}], "max_tokens": 6, "temperature": 0,
+            "ignore_eos": True}
+    plain = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=60).json()["choices"][0]["message"]
+    fe.reasoning_parser = "deepseek_r1"
+    try:
+        msg = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=60).json()["choices"][0]["message"]
+        assert msg["content"] == "" and msg["reasoning_content"] == plain["content"].strip("\n")
+        rs, cs = "", ""
+        with httpx.stream("POST", fs.url + "/v1/chat/completions", json=dict(body, stream=True), timeout=60) as r:
+            for line in r.iter_lines():
+                if line.startswith("data: ") and line != "data: [DONE]":
+                    d = json.loads(line[6:])["choices"][0]["delta"]
+                    rs += d.get("reasoning_content") or ""
+                    cs += d.get("content") or ""
+        assert rs == plain["content"] and cs == ""
+    finally:
+        fe.reasoning_parser = None
+
+
 def test_disaggregated_matches_aggregated():
     """Prefill worker + decode worker (host-staged KV transfer) give the agg result token for token."""
     fe = Frontend(router_mode="round_robin", ttl=30)

@@ -278,3 +278,20 @@ def test_staging_arena_extents():
     a.release(0, 3)
     a.release(8, 2)
     assert a.acquire(10) == 0  # all extents merged back
+
+
+def test_reasoning_splitter_streaming_and_unary():
+    """<think> blocks go to reasoning_content; tags split across chunks are held back; deepseek_r1
+    starts inside the reasoning block."""
+    from mxserve.frontend.reasoning import ReasoningSplitter, split_text
+    text = "<think>\nplan: add 2 and 2\n</think>\n\nFINAL: 4"
+    assert split_text(text, "qwen3") == ("plan: add 2 and 2", "FINAL: 4")
+    assert split_text(text, None) == (None, text)
+    assert split_text("no reasoning here", "qwen3") == (None, "no reasoning here")
+    assert split_text("thinking...</think>answer", "deepseek_r1") == ("thinking...", "answer")
+    for cut in range(1, len(text)):
+        sp = ReasoningSplitter("qwen3")
+        parts = [sp.feed(text[i:i + cut], final=i + cut >= len(text)) for i in range(0, len(text), cut)]
+        r = "".join(p[0] for p in parts)
+        c = "".join(p[1] for p in parts)
+        assert r == "\nplan: add 2 and 2\n" and c == "\n\nFINAL: 4", cut
