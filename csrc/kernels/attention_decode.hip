@@ -353,6 +353,231 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// MFMA variant: the dot products run on the matrix cores (v_mfma_f32_16x16x32_bf16), which matters
+// once VALU, not HBM, is the limit -- wide GQA groups (G = 8: Llama-3-70B at TP 8 keeps one kv
+// head per rank, so every K/V byte feeds 8 query heads) and the fp8 cache (half the bytes, same
+// math).  Per wave iteration: two KV blocks (32 tokens).
+//   S = K . Q^T   A = K rows (token = lane & 15, dims 8 (lane >> 4) + 32 ks ...), B = Q^T with the
+//                 G query heads on the columns (zero-padded to 16), kept in registers all along.
+//                 C: lane holds tokens 4 (lane >> 4) + i of one block for head lane & 15.
+//   online softmax per head (column): max over the lane's 8 scores, then over the 4 lanes of a
+//                 column (lane ^ 16, lane ^ 32).
+//   O^T += V^T . P^T   B = P^T straight from the S accumulators of the two blocks (k = 8 q + j:
+//                 j < 4 -> block 0 token 4 q + j, j >= 4 -> block 1 token 4 q + j - 4), A = V^T
+//                 from the dim-major cache: two 4-token pieces per lane, one per block.
+// The G x D output of each wave merges through LDS exactly as in the VALU kernel above.
+typedef __bf16 bf16x8d_t __attribute__((ext_vector_type(8)));
+typedef float f32x4d_t __attribute__((ext_vector_type(4)));
+
+// KV bytes are read once per step: non-temporal loads keep them from evicting the weights and block
+// tables from L2 / MALL (as in the VALU kernel)
+typedef unsigned int u32x2d_t __attribute__((ext_vector_type(2)));
+template <int EB>
+__device__ __forceinline__ uint4 ld_k8(const char* p) {
+  if constexpr (EB == 2)
+    return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p)));
+  else
+    return fp8x8_to_bf16x8(__builtin_bit_cast(uint2, __builtin_nontemporal_load(reinterpret_cast<const u32x2d_t*>(p))));
+}
+template <int EB>
+__device__ __forceinline__ uint2 ld_v4(const char* p) {
+  if constexpr (EB == 2)
+    return __builtin_bit_cast(uint2, __builtin_nontemporal_load(reinterpret_cast<const u32x2d_t*>(p)));
+  else
+    return fp8x4_to_bf16x4(__builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p)));
+}
+
+template <int D, int G, int EB>
+__global__ void __launch_bounds__(256) paged_decode_mfma_kernel(
+    bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml,
+    const bf16_t* __restrict__ q, const void* __restrict__ kv, long block_stride,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens, int Hkv,
+    float scale, int part_len, float v_scale) {
+  constexpr int KS = D / 32;  // k-steps of S = K Q^T
+  constexpr int DT = D / 16;  // 16-dim tiles of O^T
+  static_assert(G <= 16, "query heads of a kv head must fit the 16 MFMA columns");
+  const int kvh = blockIdx.x, seq = blockIdx.y, part = blockIdx.z;
+  const int P = gridDim.z;
+  const int L = seq_lens[seq];
+  if (part_len <= 0) part_len = decode_part_len(L, P);
+  const int start = part * part_len;
+  if (start >= L) return;
+  const int end = min(start + part_len, L);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 15, qd = lane >> 4;
+  const int Hq = Hkv * G;
+
+  __shared__ float red_m[kWaves][G], red_l[kWaves][G];
+  __shared__ __attribute__((aligned(16))) float red_o[kWaves][G][D];
+
+  // Q^T (B operand): lane holds dims 32 ks + 8 qd .. +7 of head c, pre-scaled for exp2
+  bf16x8d_t qf[KS];
+  {
+    const float qs = scale * kLog2e;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (c < G) {
+        const uint4 v = *reinterpret_cast<const uint4*>(q + (static_cast<size_t>(seq) * Hq + kvh * G + c) * D +
+                                                        32 * ks + 8 * qd);
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          qf[ks][2 * k] = static_cast<__bf16>(bf2f_lo(w[k]) * qs);
+          qf[ks][2 * k + 1] = static_cast<__bf16>(bf2f_hi(w[k]) * qs);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) qf[ks][k] = static_cast<__bf16>(0.f);
+      }
+    }
+  }
+  const int* btp = block_tables + static_cast<size_t>(seq) * bt_stride;
+  const char* kbase = reinterpret_cast<const char*>(kv) + static_cast<size_t>(kvh) * kBS * D * EB;
+  const char* vbase = reinterpret_cast<const char*>(kv) + static_cast<size_t>(Hkv + kvh) * kBS * D * EB;
+  const long bsb = block_stride * EB;
+  const int blk0 = start / kBS;
+  const int nblk = (end - 1) / kBS - blk0 + 1;
+  const int niter = (nblk + kWaves * 2 - 1) / (kWaves * 2);
+
+  f32x4d_t o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4d_t{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+
+  uint4 ka[2][KS];
+  uint2 va[DT][2];
+  auto load = [&](int it, uint4 (&kd)[2][KS], uint2 (&vd)[DT][2]) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int bi = (it * kWaves + wid) * 2 + b;
+      // blocks past this partition (a wave's whole pair, or the second block of the last pair) read
+      // the partition's last block instead: valid memory, and their tokens are masked or skipped
+      const long off = static_cast<long>(btp[blk0 + min(bi, nblk - 1)]) * bsb;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) kd[b][ks] = ld_k8<EB>(kbase + off + (c * D + 32 * ks + 8 * qd) * EB);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) vd[dt][b] = ld_v4<EB>(vbase + off + ((16 * dt + c) * kBS + 4 * qd) * EB);
+    }
+  };
+  if (niter > 0) load(0, ka, va);
+
+  for (int it = 0; it < niter; ++it) {
+    uint4 kn[2][KS];
+    uint2 vn[DT][2];
+    if (it + 1 < niter) load(it + 1, kn, vn);
+    const int tok0 = (blk0 + (it * kWaves + wid) * 2) * kBS;
+    if (tok0 < end) {
+      f32x4d_t s[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        s[b] = f32x4d_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          s[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8d_t, ka[b][ks]), qf[ks], s[b], 0,
+                                                          0, 0);
+      }
+      const bool tail = tok0 + 32 > end;
+      if (tail) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (tok0 + 16 * b + 4 * qd + i >= end) s[b][i] = -INFINITY;
+      }
+      float mx = s[0][0];
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[b][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float alpha = exp2f(m - mn);  // 0 on the first tile
+      m = mn;
+      lsum *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      bf16x8d_t pf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const __bf16 pb = static_cast<__bf16>(exp2f(s[j >> 2][j & 3] - m));
+        pf[j] = pb;
+        lsum += static_cast<float>(pb);  // the row sum sees exactly the weights P V uses
+      }
+      if (tail) {  // unwritten cache bytes past the end (possibly NaN) never reach the sum
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (tok0 + 16 * b + 4 * qd + i >= end) {
+#pragma unroll
+              for (int dt = 0; dt < DT; ++dt) {
+                uint32_t& w = (i < 2) ? va[dt][b].x : va[dt][b].y;
+                w &= (i & 1) ? 0x0000FFFFu : 0xFFFF0000u;
+              }
+            }
+      }
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const uint4 a = make_uint4(va[dt][0].x, va[dt][0].y, va[dt][1].x, va[dt][1].y);
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8d_t, a), pf, o[dt], 0, 0, 0);
+      }
+    }
+    if (it + 1 < niter) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) ka[b][ks] = kn[b][ks];
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        va[dt][0] = vn[dt][0];
+        va[dt][1] = vn[dt][1];
+      }
+    }
+  }
+
+  // ---- per-wave totals: the row sum of head c is spread over the 4 lanes of its column
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (c < G) {
+    if (qd == 0) {
+      red_m[wid][c] = m;
+      red_l[wid][c] = lsum;
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red_o[wid][c][16 * dt + 4 * qd + i] = o[dt][i];
+  }
+  __syncthreads();
+  for (int x = threadIdx.x; x < G * D; x += blockDim.x) {
+    const int g = x / D, d = x % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) M = fmaxf(M, red_m[w][g]);
+    float Ls = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      const float f = red_m[w][g] == -INFINITY ? 0.f : exp2f(red_m[w][g] - M);
+      Ls += red_l[w][g] * f;
+      O += red_o[w][g][d] * f;
+    }
+    const int head = kvh * G + g;
+    if (P == 1) {
+      out[(static_cast<size_t>(seq) * Hq + head) * D + d] = f2bf(O / Ls * v_scale);
+    } else {
+      const size_t base = (static_cast<size_t>(seq) * Hq + head) * P + part;
+      tmp_out[base * D + d] = O / Ls * v_scale;
+      if (d == 0) {
+        tmp_ml[base * 2] = M;
+        tmp_ml[base * 2 + 1] = Ls;
+      }
+    }
+  }
+}
+
 // Merge partitions: one workgroup per (head, seq), one thread per dim.
 template <int D>
 __global__ void __launch_bounds__(D) paged_decode_reduce_kernel(bf16_t* __restrict__ out,
@@ -396,15 +621,42 @@ int decode_num_partitions(int max_seq_len) {
   return P;
 }
 
+// impl: 0 = auto, 1 = VALU dot2 kernel, 2 = MFMA kernel.  Auto takes the MFMA kernel from G = 4 query
+// heads per kv head up (profiles/r1_v12_decode_attn_probe.jsonl, 4k context: 1B bf16 B 256 0.363 ->
+// 0.323 ms = 6.5 TB/s, 8B bf16 0.371 -> 0.324 ms, 1B fp8 0.275 -> 0.202 ms, 70B-TP8 shard (G 8)
+// 0.136 -> 0.098 ms); at G <= 2 the MFMA columns are mostly padding and the VALU kernel is as fast
+// or faster (Qwen3-0.6B bf16 0.631 vs 0.636 ms, fp8 0.358 vs 0.545 ms).
 void launch_paged_decode(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, const void* kv, bool kv_fp8,
                          long block_stride, const int* block_tables, int bt_stride, const int* seq_lens, int B,
                          int Hq, int Hkv, int D, int P, int part_len, float scale, float k_scale, float v_scale,
-                         hipStream_t s) {
+                         int impl, hipStream_t s) {
   if (B == 0) return;
   const int G = Hq / Hkv;
   dim3 grid(Hkv, B, P), blk(256);
   if (kv_fp8) scale *= k_scale;
   else v_scale = 1.f;
+  const bool mfma = impl == 2 || (impl == 0 && G >= 4);
+  if (mfma) {
+#define MXS_DECM(DD, GG)                                                                                   \
+    if (D == DD && G == GG) {                                                                              \
+      if (kv_fp8)                                                                                          \
+        hipLaunchKernelGGL((paged_decode_mfma_kernel<DD, GG, 1>), grid, blk, 0, s, out, tmp_out, tmp_ml, q,  \
+                           kv, block_stride, block_tables, bt_stride, seq_lens, Hkv, scale, part_len,      \
+                           v_scale);                                                                       \
+      else                                                                                                 \
+        hipLaunchKernelGGL((paged_decode_mfma_kernel<DD, GG, 2>), grid, blk, 0, s, out, tmp_out, tmp_ml, q,  \
+                           kv, block_stride, block_tables, bt_stride, seq_lens, Hkv, scale, part_len,      \
+                           v_scale);                                                                       \
+      if (P > 1)                                                                                           \
+        hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(Hq, B), dim3(DD), 0, s, out, tmp_out,   \
+                           tmp_ml, seq_lens, Hq, P, part_len);                                             \
+      MXS_CHECK_LAUNCH();                                                                                  \
+      return;                                                                                              \
+    }
+    MXS_DECM(64, 1) MXS_DECM(64, 2) MXS_DECM(64, 4) MXS_DECM(64, 8)
+    MXS_DECM(128, 1) MXS_DECM(128, 2) MXS_DECM(128, 4) MXS_DECM(128, 8)
+#undef MXS_DECM
+  }
 #define MXS_DEC(DD, GG)                                                                                    \
   if (D == DD && G == GG) {                                                                                \
     if (kv_fp8)                                                                                            \

@@ -18,7 +18,7 @@ void launch_rope_and_cache(bf16_t*, const bf16_t*, const int64_t*, const float*,
 int decode_num_partitions(int);
 void decode_plan(int, int, int, int*, int*);
 void launch_paged_decode(bf16_t*, float*, float*, const bf16_t*, const void*, bool, long, const int*, int, const int*,
-                         int, int, int, int, int, int, float, float, float, hipStream_t);
+                         int, int, int, int, int, int, float, float, float, int, hipStream_t);
 void launch_paged_prefill(bf16_t*, const bf16_t*, const void*, bool, long, const int*, int, const int*, const int*,
                           int, int, int, int, int, float, int, float, float, hipStream_t);
 void launch_sample(int64_t*, const void*, bool, int, int, long, const float*, const float*, const int*,
@@ -113,7 +113,8 @@ void rope_and_cache(at::Tensor q_out, at::Tensor qkv, at::Tensor positions, at::
 }
 
 void paged_attention_decode(at::Tensor out, at::Tensor q, at::Tensor kv, at::Tensor block_tables,
-                            at::Tensor seq_lens, double scale, int64_t max_seq_len, double k_scale, double v_scale) {
+                            at::Tensor seq_lens, double scale, int64_t max_seq_len, double k_scale, double v_scale,
+                            int64_t impl) {
   CHECK_CUDA(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_CONTIG(out);
   const int B = q.size(0), Hq = q.size(1), D = q.size(2);
   const int Hkv = kv.size(2);
@@ -132,7 +133,8 @@ void paged_attention_decode(at::Tensor out, at::Tensor q, at::Tensor kv, at::Ten
                            P > 1 ? tmp_ml.data_ptr<float>() : nullptr, bf(q), kv.data_ptr(), fp8, kv.stride(0),
                            block_tables.data_ptr<int>(), block_tables.stride(0), seq_lens.data_ptr<int>(), B, Hq,
                            Hkv, D, P, /*part_len: split each sequence evenly*/ 0, static_cast<float>(scale),
-                           static_cast<float>(k_scale), static_cast<float>(v_scale), stream());
+                           static_cast<float>(k_scale), static_cast<float>(v_scale), static_cast<int>(impl),
+                           stream());
 }
 
 void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Tensor block_tables, at::Tensor qsl,
@@ -273,7 +275,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0);
   m.def("paged_attention_decode", &paged_attention_decode, pybind11::arg("out"), pybind11::arg("q"),
         pybind11::arg("kv"), pybind11::arg("block_tables"), pybind11::arg("seq_lens"), pybind11::arg("scale"),
-        pybind11::arg("max_seq_len"), pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0);
+        pybind11::arg("max_seq_len"), pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0,
+        pybind11::arg("impl") = 0);
   m.def("paged_attention_prefill", &paged_attention_prefill, pybind11::arg("out"), pybind11::arg("q"),
         pybind11::arg("kv"), pybind11::arg("block_tables"), pybind11::arg("qsl"), pybind11::arg("seq_lens"),
         pybind11::arg("scale"), pybind11::arg("max_q_len"), pybind11::arg("version") = 3,

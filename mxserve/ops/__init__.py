@@ -45,6 +45,9 @@ def has_ext() -> bool:
 _PREFILL_VERSION = int(os.environ.get("MXS_PREFILL_KERNEL", "3"))
 
 
+_DECODE_IMPL = int(os.environ.get("MXS_DECODE_ATTN", "0"))
+
+
 def _gpu(t: torch.Tensor) -> bool:
     return t.is_cuda and os.environ.get("MXS_FORCE_REFERENCE_OPS", "0") != "1"
 
@@ -131,11 +134,14 @@ def rope_and_cache(qkv: torch.Tensor, num_heads: int, num_kv_heads: int, head_di
 def paged_attention_decode(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,
                            seq_lens: torch.Tensor, scale: float, max_seq_len: int,
                            out: Optional[torch.Tensor] = None, k_scale: float = 1.0,
-                           v_scale: float = 1.0) -> torch.Tensor:
-    """One query token per sequence.  q [B, Hq, D] -> [B, Hq, D] (written into `out` if given)."""
+                           v_scale: float = 1.0, impl: Optional[int] = None) -> torch.Tensor:
+    """One query token per sequence.  q [B, Hq, D] -> [B, Hq, D] (written into `out` if given).
+    impl: 0 auto (MFMA kernel from G = 4 query heads per kv head), 1 VALU dot2, 2 MFMA;
+    MXS_DECODE_ATTN overrides the default."""
     if _gpu(q):
         out = torch.empty_like(q) if out is None else out
-        ext().paged_attention_decode(out, q, kv_layer, block_tables, seq_lens, scale, max_seq_len, k_scale, v_scale)
+        ext().paged_attention_decode(out, q, kv_layer, block_tables, seq_lens, scale, max_seq_len, k_scale, v_scale,
+                                     _DECODE_IMPL if impl is None else impl)
         return out
     return ref.paged_attention_decode(q, kv_layer, block_tables, seq_lens, scale, k_scale, v_scale)
 

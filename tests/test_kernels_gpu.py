@@ -99,9 +99,10 @@ def _paged_setup(seq_lens, hkv, D, L=2, device="cuda"):
     return kv, bt
 
 
-@pytest.mark.parametrize("D,G", [(64, 4), (128, 2), (128, 8), (64, 1), (128, 4)])
-@pytest.mark.parametrize("lens", [[1, 17, 100], [513, 2000, 31, 4096]])
-def test_paged_decode(gpu, D, G, lens):
+@pytest.mark.parametrize("impl", [1, 2])  # VALU dot2 kernel, MFMA kernel
+@pytest.mark.parametrize("D,G", [(64, 4), (128, 2), (128, 8), (64, 1), (128, 4), (64, 8)])
+@pytest.mark.parametrize("lens", [[1, 17, 100], [513, 2000, 31, 4096], [16, 32, 33, 47]])
+def test_paged_decode(gpu, D, G, lens, impl):
     hkv = 2
     hq = hkv * G
     kv, bt = _paged_setup(lens, hkv, D, device=gpu)
@@ -109,18 +110,19 @@ def test_paged_decode(gpu, D, G, lens):
     q = torch.randn(B, hq, D, device=gpu, dtype=torch.bfloat16)
     sl = torch.tensor(lens, dtype=torch.int32)
     scale = 1 / math.sqrt(D)
-    out = ops.paged_attention_decode(q, kv[:, 1], bt.to(gpu), sl.to(gpu), scale, max(lens))
+    out = ops.paged_attention_decode(q, kv[:, 1], bt.to(gpu), sl.to(gpu), scale, max(lens), impl=impl)
     exp = ref.paged_attention_decode(q.cpu(), kv[:, 1].cpu(), bt, sl, scale)
-    _close(out, exp, 0.02, 0.02, "decode")
+    _close(out, exp, 0.02, 0.02, f"decode impl {impl}")
 
 
-def test_paged_decode_graph_max_len(gpu):
+@pytest.mark.parametrize("impl", [1, 2])
+def test_paged_decode_graph_max_len(gpu, impl):
     """Graph capture launches with max_seq_len = max_model_len: idle partitions must be harmless."""
     lens = [5, 700]
     kv, bt = _paged_setup(lens, 8, 64, device=gpu)
     q = torch.randn(2, 32, 64, device=gpu, dtype=torch.bfloat16)
     sl = torch.tensor(lens, dtype=torch.int32)
-    out = ops.paged_attention_decode(q, kv[:, 0], bt.to(gpu), sl.to(gpu), 0.125, 8192)
+    out = ops.paged_attention_decode(q, kv[:, 0], bt.to(gpu), sl.to(gpu), 0.125, 8192, impl=impl)
     exp = ref.paged_attention_decode(q.cpu(), kv[:, 0].cpu(), bt, sl, 0.125)
     _close(out, exp, 0.02, 0.02, "decode-maxlen")
 
@@ -206,9 +208,10 @@ def test_rope_and_cache_fp8(gpu, D, hq, hkv, qknorm, kscale):
     assert kv[:, 0].sum().item() == 0  # other layer untouched
 
 
+@pytest.mark.parametrize("impl", [1, 2])
 @pytest.mark.parametrize("D,G", [(64, 4), (128, 2), (128, 8), (64, 1)])
 @pytest.mark.parametrize("scales", [(1.0, 1.0), (0.02, 0.05)])
-def test_paged_decode_fp8(gpu, D, G, scales):
+def test_paged_decode_fp8(gpu, D, G, scales, impl):
     ks, vs = scales
     hkv, lens = 2, [1, 17, 513, 2000, 4096]
     kv, bt = _paged_setup(lens, hkv, D, device=gpu)
@@ -217,7 +220,8 @@ def test_paged_decode_fp8(gpu, D, G, scales):
     q = torch.randn(B, hkv * G, D, device=gpu, dtype=torch.bfloat16)
     sl = torch.tensor(lens, dtype=torch.int32)
     scale = 1 / math.sqrt(D)
-    out = ops.paged_attention_decode(q, kv8[:, 1], bt.to(gpu), sl.to(gpu), scale, max(lens), k_scale=ks, v_scale=vs)
+    out = ops.paged_attention_decode(q, kv8[:, 1], bt.to(gpu), sl.to(gpu), scale, max(lens), k_scale=ks, v_scale=vs,
+                                     impl=impl)
     exp = ref.paged_attention_decode(q.cpu(), kv8[:, 1].cpu(), bt, sl, scale, ks, vs)
     _close(out, exp, 0.02 * max(1.0, exp.abs().max().item()), 0.02, "decode fp8")
 
