@@ -12,6 +12,7 @@ import torch
 
 SHAPES = {  # name: (K, N) of y[T, N] = x[T, K] . w[N, K]^T
     "1b": {"qkv": (2048, 3072), "o": (2048, 2048), "gate_up": (2048, 16384), "down": (8192, 2048)},
+    "1b_lm": {"lm_head": (2048, 128256)},
     "8b": {"qkv": (4096, 6144), "o": (4096, 4096), "gate_up": (4096, 28672), "down": (14336, 4096)},
 }
 
