@@ -372,21 +372,35 @@ typedef float f32x4d_t __attribute__((ext_vector_type(4)));
 
 // KV bytes are read once per step: non-temporal loads keep them from evicting the weights and block
 // tables from L2 / MALL (as in the VALU kernel)
+// The prefetch registers hold the raw cache bytes (fp8: half the VGPRs of bf16); they are widened
+// to bf16 right before the MFMA that consumes them.
 typedef unsigned int u32x2d_t __attribute__((ext_vector_type(2)));
 template <int EB>
-__device__ __forceinline__ uint4 ld_k8(const char* p) {
-  if constexpr (EB == 2)
+struct MfmaKV;
+template <>
+struct MfmaKV<2> {
+  using K8 = uint4;  // 8 bf16 K dims
+  using V4 = uint2;  // 4 bf16 V tokens
+  __device__ static K8 ldk(const char* p) {
     return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p)));
-  else
-    return fp8x8_to_bf16x8(__builtin_bit_cast(uint2, __builtin_nontemporal_load(reinterpret_cast<const u32x2d_t*>(p))));
-}
-template <int EB>
-__device__ __forceinline__ uint2 ld_v4(const char* p) {
-  if constexpr (EB == 2)
+  }
+  __device__ static V4 ldv(const char* p) {
     return __builtin_bit_cast(uint2, __builtin_nontemporal_load(reinterpret_cast<const u32x2d_t*>(p)));
-  else
-    return fp8x4_to_bf16x4(__builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p)));
-}
+  }
+  __device__ static uint4 k(const K8& v) { return v; }
+  __device__ static uint2 v(const V4& v) { return v; }
+};
+template <>
+struct MfmaKV<1> {
+  using K8 = uint2;     // 8 fp8 K dims
+  using V4 = uint32_t;  // 4 fp8 V tokens
+  __device__ static K8 ldk(const char* p) {
+    return __builtin_bit_cast(uint2, __builtin_nontemporal_load(reinterpret_cast<const u32x2d_t*>(p)));
+  }
+  __device__ static V4 ldv(const char* p) { return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p)); }
+  __device__ static uint4 k(const K8& v) { return fp8x8_to_bf16x8(v); }
+  __device__ static uint2 v(const V4& v) { return fp8x4_to_bf16x4(v); }
+};
 
 template <int D, int G, int EB>
 __global__ void __launch_bounds__(256) paged_decode_mfma_kernel(
@@ -446,9 +460,10 @@ __global__ void __launch_bounds__(256) paged_decode_mfma_kernel(
   for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4d_t{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, lsum = 0.f;
 
-  uint4 ka[2][KS];
-  uint2 va[DT][2];
-  auto load = [&](int it, uint4 (&kd)[2][KS], uint2 (&vd)[DT][2]) {
+  using KVT = MfmaKV<EB>;
+  typename KVT::K8 ka[2][KS];
+  typename KVT::V4 va[DT][2];
+  auto load = [&](int it, typename KVT::K8 (&kd)[2][KS], typename KVT::V4 (&vd)[DT][2]) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int bi = (it * kWaves + wid) * 2 + b;
@@ -456,17 +471,24 @@ __global__ void __launch_bounds__(256) paged_decode_mfma_kernel(
       // the partition's last block instead: valid memory, and their tokens are masked or skipped
       const long off = static_cast<long>(btp[blk0 + min(bi, nblk - 1)]) * bsb;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) kd[b][ks] = ld_k8<EB>(kbase + off + (c * D + 32 * ks + 8 * qd) * EB);
+      for (int ks = 0; ks < KS; ++ks) kd[b][ks] = KVT::ldk(kbase + off + (c * D + 32 * ks + 8 * qd) * EB);
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) vd[dt][b] = ld_v4<EB>(vbase + off + ((16 * dt + c) * kBS + 4 * qd) * EB);
+      for (int dt = 0; dt < DT; ++dt) vd[dt][b] = KVT::ldv(vbase + off + ((16 * dt + c) * kBS + 4 * qd) * EB);
     }
   };
+  // software pipeline (next pair's loads in flight under this pair's math) unless it costs a wave
+  // of occupancy: D = 128 with an fp8 cache fits 3 waves/SIMD only without the second register set
+  constexpr bool kPrefetch = !(D >= 128 && EB == 1);
   if (niter > 0) load(0, ka, va);
 
   for (int it = 0; it < niter; ++it) {
-    uint4 kn[2][KS];
-    uint2 vn[DT][2];
-    if (it + 1 < niter) load(it + 1, kn, vn);
+    typename KVT::K8 kn[2][KS];
+    typename KVT::V4 vn[DT][2];
+    if constexpr (kPrefetch) {
+      if (it + 1 < niter) load(it + 1, kn, vn);
+    } else {
+      if (it > 0) load(it, ka, va);
+    }
     const int tok0 = (blk0 + (it * kWaves + wid) * 2) * kBS;
     if (tok0 < end) {
       f32x4d_t s[2];
@@ -475,8 +497,8 @@ __global__ void __launch_bounds__(256) paged_decode_mfma_kernel(
         s[b] = f32x4d_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks)
-          s[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8d_t, ka[b][ks]), qf[ks], s[b], 0,
-                                                          0, 0);
+          s[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8d_t, KVT::k(ka[b][ks])), qf[ks],
+                                                          s[b], 0, 0, 0);
       }
       const bool tail = tok0 + 32 > end;
       if (tail) {
@@ -506,26 +528,22 @@ __global__ void __launch_bounds__(256) paged_decode_mfma_kernel(
         pf[j] = pb;
         lsum += static_cast<float>(pb);  // the row sum sees exactly the weights P V uses
       }
-      if (tail) {  // unwritten cache bytes past the end (possibly NaN) never reach the sum
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (tok0 + 16 * b + 4 * qd + i >= end) {
-#pragma unroll
-              for (int dt = 0; dt < DT; ++dt) {
-                uint32_t& w = (i < 2) ? va[dt][b].x : va[dt][b].y;
-                w &= (i & 1) ? 0x0000FFFFu : 0xFFFF0000u;
-              }
-            }
-      }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        const uint4 a = make_uint4(va[dt][0].x, va[dt][0].y, va[dt][1].x, va[dt][1].y);
+        uint2 v0 = KVT::v(va[dt][0]), v1 = KVT::v(va[dt][1]);
+        if (tail) {  // unwritten cache bytes past the end (possibly NaN) never reach the sum
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t keep = (i & 1) ? 0x0000FFFFu : 0xFFFF0000u;
+            if (tok0 + 4 * qd + i >= end) (i < 2 ? v0.x : v0.y) &= keep;
+            if (tok0 + 16 + 4 * qd + i >= end) (i < 2 ? v1.x : v1.y) &= keep;
+          }
+        }
+        const uint4 a = make_uint4(v0.x, v0.y, v1.x, v1.y);
         o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8d_t, a), pf, o[dt], 0, 0, 0);
       }
     }
-    if (it + 1 < niter) {
+    if (kPrefetch && it + 1 < niter) {
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
