@@ -18,7 +18,7 @@ from .kv_manager import KVCacheManager
 from .model_runner import ModelRunner
 from .request import Request, SamplingParams, Status
 from .scheduler import Scheduler
-from ..utils.tracing import ROCTX
+from ..utils.tracing import ROCTX, StepProfiler
 
 log = logging.getLogger(__name__)
 
@@ -53,6 +53,7 @@ class LLMEngine:
         # async scheduling: the launched-but-not-collected step (scheduler output, runner handle)
         self.async_scheduling = bool(args.async_scheduling)
         self._inflight: Optional[tuple] = None
+        self.profiler = StepProfiler()  # MXS_TORCH_PROFILE="start:count:path"
 
     # ------------------------------------------------------------------ requests
     def add_request(self, prompt_token_ids: list, sampling: Optional[SamplingParams] = None,
@@ -112,6 +113,16 @@ class LLMEngine:
         """One engine iteration.  Synchronous: schedule, run, land.  Async: schedule and launch
         step N+1 first, then land step N (whose GPU work finished while the host was busy), so the
         GPU queue never drains between steps."""
+        if self.profiler.enabled:
+            step_no = self.num_steps
+            self.profiler.step_begin(step_no)
+            try:
+                return self._step()
+            finally:
+                self.profiler.step_end(step_no)
+        return self._step()
+
+    def _step(self) -> list[StepOutput]:
         so = self.scheduler.schedule()
         handle = None
         if not so.is_empty:

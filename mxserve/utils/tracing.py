@@ -95,6 +95,45 @@ class _Roctx:
 ROCTX = _Roctx()
 
 
+# ----------------------------------------------------------------------------- torch.profiler
+class StepProfiler:
+    """Python + GPU-launch view of a window of engine steps (SURVEY.md §5.1 "torch.profiler for the
+    Python side"): MXS_TORCH_PROFILE="start:count:path" records steps [start, start + count) with
+    torch.profiler (CPU + HIP activities) and writes a Chrome trace to `path`."""
+
+    def __init__(self, spec: Optional[str] = None):
+        spec = os.environ.get("MXS_TORCH_PROFILE", "") if spec is None else spec
+        self.start = self.count = -1
+        self.path = ""
+        self._prof = None
+        self.done = False
+        if spec:
+            a, b, path = spec.split(":", 2)
+            self.start, self.count, self.path = int(a), int(b), path
+
+    @property
+    def enabled(self) -> bool:
+        return self.count > 0 and not self.done
+
+    def step_begin(self, step: int) -> None:
+        if self.enabled and self._prof is None and step >= self.start:
+            import torch
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if torch.cuda.is_available():
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            self._prof = torch.profiler.profile(activities=acts, record_shapes=False)
+            self._prof.__enter__()
+            self._first = step
+
+    def step_end(self, step: int) -> None:
+        if self._prof is not None and step >= self._first + self.count - 1:
+            self._prof.__exit__(None, None, None)
+            self._prof.export_chrome_trace(self.path)
+            log.info("torch.profiler: steps %d..%d -> %s", self._first, step, self.path)
+            self._prof = None
+            self.done = True
+
+
 # ----------------------------------------------------------------------------- faults
 class Faults:
     def __init__(self, spec: Optional[str] = None):

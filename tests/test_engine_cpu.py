@@ -185,3 +185,15 @@ def test_fp8_kv_cache_engine():
     assert all(len(x) == 12 for x in b)
     same = sum(x == y for pa, pb in zip(a, b) for x, y in zip(pa, pb))
     assert same >= 0.6 * 36, (a, b)  # tiny random model: fp8 rounding flips some near-ties
+
+
+def test_torch_profiler_window(tmp_path):
+    """MXS_TORCH_PROFILE-style window: steps [2, 5) are recorded and a Chrome trace is written."""
+    import json
+    from mxserve.utils.tracing import StepProfiler
+    eng = _engine(True)
+    path = tmp_path / "trace.json"
+    eng.profiler = StepProfiler(f"2:3:{path}")
+    eng.generate([list(range(5, 30))], SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
+    assert eng.profiler.done and path.exists()
+    assert json.loads(path.read_text())["traceEvents"]
