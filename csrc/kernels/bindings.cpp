@@ -32,7 +32,9 @@ void launch_moe_align(int*, int*, const int*, int, int, int, int*, hipStream_t);
 void launch_moe_combine(bf16_t*, const bf16_t*, const float*, const int*, int, int, int, hipStream_t);
 bool launch_skinny_gemm(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, hipStream_t);
 bool launch_moe_grouped_gemm(bf16_t*, const bf16_t*, const bf16_t*, const int*, int, int, int, int, int, bool,
-                             hipStream_t);
+                             int, float*, hipStream_t);
+void launch_moe_combine_partials(bf16_t*, const float*, const float*, const int*, int, int, int, int, long,
+                                 hipStream_t);
 }  // namespace mxs
 
 namespace {
@@ -221,14 +223,21 @@ bool skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w) {
 
 // y[r] = x[r] . w[e(r)]^T over expert-sorted rows (offs = moe_align offsets); silu: w rows are
 // [gate; up] and y = silu(gate) * up (width N/2).  False if the shape is unsupported.
-bool moe_grouped_gemm(at::Tensor y, at::Tensor x, at::Tensor w, at::Tensor offs, bool silu) {
+bool moe_grouped_gemm(at::Tensor y, at::Tensor x, at::Tensor w, at::Tensor offs, bool silu, int64_t split,
+                      std::optional<at::Tensor> partial) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y); CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
   TORCH_CHECK(w.dim() == 3 && x.dim() == 2 && y.dim() == 2, "w [E, N, K], x [rows, K], y [rows, N']");
   TORCH_CHECK(offs.scalar_type() == at::kInt && offs.numel() == w.size(0) + 1, "offs: int32 [E + 1]");
   const int N = w.size(1), K = w.size(2);
   TORCH_CHECK(x.size(1) == K && y.size(0) == x.size(0) && y.size(1) == (silu ? N / 2 : N), "shape mismatch");
+  float* pp = nullptr;
+  if (split > 1) {
+    TORCH_CHECK(partial.has_value() && partial->scalar_type() == at::kFloat && partial->is_contiguous() &&
+                    partial->numel() >= split * x.size(0) * N, "partial: fp32 [split, rows, N]");
+    pp = partial->data_ptr<float>();
+  }
   return mxs::launch_moe_grouped_gemm(bf(y), bf(x), bf(w), offs.data_ptr<int>(), w.size(0), x.size(0), N, K,
-                                      y.size(1), silu, stream());
+                                      y.size(1), silu, static_cast<int>(split), pp, stream());
 }
 
 void moe_topk_softmax(at::Tensor w, at::Tensor ids, at::Tensor logits) {
@@ -289,7 +298,19 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("e_lo"), pybind11::arg("e_local"), pybind11::arg("inv") = pybind11::none());
   m.def("moe_combine", &moe_combine);
   m.def("skinny_gemm", &skinny_gemm);
-  m.def("moe_grouped_gemm", &moe_grouped_gemm);
+  m.def("moe_grouped_gemm", &moe_grouped_gemm, pybind11::arg("y"), pybind11::arg("x"), pybind11::arg("w"),
+        pybind11::arg("offs"), pybind11::arg("silu"), pybind11::arg("split") = 1,
+        pybind11::arg("partial") = pybind11::none());
+  m.def("moe_combine_partials", [](at::Tensor out, at::Tensor part, at::Tensor topk_w, at::Tensor inv) {
+    CHECK_CUDA(part); CHECK_BF16(out); CHECK_CONTIG(out);
+    TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3, "part fp32 [S, R, H]");
+    TORCH_CHECK(topk_w.scalar_type() == at::kFloat && topk_w.is_contiguous() && topk_w.dim() == 2, "topk_w");
+    TORCH_CHECK(inv.scalar_type() == at::kInt && inv.is_contiguous() && inv.numel() == topk_w.numel(), "inv");
+    const int T = topk_w.size(0), K = topk_w.size(1), H = part.size(2);
+    TORCH_CHECK(K <= 8 && H % 4 == 0 && out.size(0) == T && out.size(1) == H, "shapes");
+    mxs::launch_moe_combine_partials(bf(out), part.data_ptr<float>(), topk_w.data_ptr<float>(), inv.data_ptr<int>(),
+                                     T, K, H, part.size(0), part.size(1) * static_cast<long>(H), stream());
+  });
   m.def("decode_num_partitions", &mxs::decode_num_partitions);
   m.def("decode_plan", [](int B, int Hkv, int max_seq_len) {
     int P = 1, len = 0;

@@ -139,4 +139,41 @@ void launch_moe_combine(bf16_t* out, const bf16_t* ys, const float* topk_w, cons
   MXS_CHECK_LAUNCH();
 }
 
+// Split-K variant: the expert rows are S fp32 partial slices [S][rows][H] (moe_grouped_gemm split).
+__global__ void __launch_bounds__(256) moe_combine_partials_kernel(bf16_t* __restrict__ out,
+                                                                   const float* __restrict__ part,
+                                                                   const float* __restrict__ topk_w,
+                                                                   const int* __restrict__ inv, int K, int H, int S,
+                                                                   long slice) {
+  const int t = blockIdx.x;
+  int rows[8];
+  float ws[8];
+  for (int k = 0; k < K; ++k) {
+    rows[k] = inv[t * K + k];
+    ws[k] = topk_w[t * K + k];
+  }
+  for (int c = threadIdx.x; c < H / 4; c += blockDim.x) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < K; ++k) {
+      if (rows[k] < 0) continue;
+      const float* p = part + static_cast<size_t>(rows[k]) * H + c * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int z = 0; z < S; ++z) {
+        const float4 u = *reinterpret_cast<const float4*>(p + z * slice);
+        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+      }
+      acc.x += ws[k] * v.x; acc.y += ws[k] * v.y; acc.z += ws[k] * v.z; acc.w += ws[k] * v.w;
+    }
+    *reinterpret_cast<uint2*>(out + static_cast<size_t>(t) * H + c * 4) = make_uint2(pack2(acc.x, acc.y),
+                                                                                     pack2(acc.z, acc.w));
+  }
+}
+
+void launch_moe_combine_partials(bf16_t* out, const float* part, const float* topk_w, const int* inv, int T, int K,
+                                 int H, int S, long slice, hipStream_t s) {
+  if (T == 0) return;
+  hipLaunchKernelGGL(moe_combine_partials_kernel, dim3(T), dim3(256), 0, s, out, part, topk_w, inv, K, H, S, slice);
+  MXS_CHECK_LAUNCH();
+}
+
 }  // namespace mxs

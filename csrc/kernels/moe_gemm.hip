@@ -13,6 +13,10 @@
 // Expert scheduling is on the device: a workgroup derives (expert, row block) from the
 // moe_align offsets itself (prefix over ceil(count_e / 128)), so the launch needs no host sync and is
 // hipGraph-capturable; the grid is sized for the worst case and surplus workgroups exit.
+// Split-K (plain variant, gridDim.z > 1): decode routes a few rows per expert, so the down
+// projection (N 4,096, K 14,336) has only N/128 x experts workgroups, each streaming a 3.7 MB weight
+// slice through 224 K-steps -- one workgroup per CU, latency-bound.  With split-K each z-slice
+// streams K/z and writes fp32 partials [z][row][n]; the combine kernel sums the slices.
 #include "common.h"
 
 namespace mxs {
@@ -30,7 +34,7 @@ template <bool SILU>
 __global__ void __launch_bounds__(256) moe_grouped_gemm_kernel(bf16_t* __restrict__ Y, const bf16_t* __restrict__ X,
                                                                const bf16_t* __restrict__ W,
                                                                const int* __restrict__ offs, int E, int N, int K,
-                                                               int ldy) {
+                                                               int ldy, float* __restrict__ partial, int rows_cap) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][kGBN * 128];  // [stage][W | X][rows x 128 B]
   // ---- which expert / row block is this workgroup's
   int tile = blockIdx.y, e = -1, r0 = 0, r1 = 0;
@@ -87,13 +91,15 @@ __global__ void __launch_bounds__(256) moe_grouped_gemm_kernel(bf16_t* __restric
       for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
 
   const int i32 = lane & 31, h = lane >> 5;
-  const int nk = K / kGBK;
-  gload(0);
+  const int nk_all = K / kGBK, S = gridDim.z, z = blockIdx.z;
+  const int ks_lo = nk_all * z / S, nk = nk_all * (z + 1) / S - ks_lo;
+  const int k_lo = ks_lo * kGBK;
+  gload(k_lo);
   sstore(0);
   __syncthreads();
   for (int ks = 0; ks < nk; ++ks) {
     const int st = ks & 1;
-    if (ks + 1 < nk) gload((ks + 1) * kGBK);  // next stage in flight under this stage's MFMAs
+    if (ks + 1 < nk) gload(k_lo + (ks + 1) * kGBK);  // next stage in flight under this stage's MFMAs
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {  // 16-k MFMA steps; lane half h takes chunk 2 kk + h
       bf16x8_t af[2], bf[2];
@@ -122,6 +128,23 @@ __global__ void __launch_bounds__(256) moe_grouped_gemm_kernel(bf16_t* __restric
   // ---- epilogue.  acc[a][b][reg]: weight row nh*64 + a*32 + (reg&3) + 8*(reg>>2) + 4h,
   //                                 token row  mh*64 + b*32 + lane%32
   if constexpr (!SILU) {
+    if (S > 1) {  // fp32 partial slice z: [z][row][n], summed by the combine kernel
+      float* pz = partial + static_cast<size_t>(z) * rows_cap * N;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int m = r0 + mh * 64 + b * 32 + i32;
+        if (m >= r1) continue;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n = n0 + nh * 64 + a * 32 + 8 * g + 4 * h;
+            *reinterpret_cast<float4*>(pz + static_cast<size_t>(m) * N + n) =
+                make_float4(acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]);
+          }
+      }
+      return;
+    }
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int m = r0 + mh * 64 + b * 32 + i32;
@@ -183,16 +206,20 @@ __global__ void __launch_bounds__(256) moe_grouped_gemm_kernel(bf16_t* __restric
 }
 
 // rows_upper: upper bound on the routed rows (T * top_k); the grid covers the worst case.
+// split > 1 (plain variant only): fp32 partials into partial[split][rows_upper][N] instead of Y.
 bool launch_moe_grouped_gemm(bf16_t* Y, const bf16_t* X, const bf16_t* W, const int* offs, int E, int rows_upper,
-                             int N, int K, int ldy, bool silu, hipStream_t s) {
+                             int N, int K, int ldy, bool silu, int split, float* partial, hipStream_t s) {
   if (K % kGBK != 0) return false;
   if (silu ? ((N / 2) % (kGBN / 2) != 0 || N % 2) : (N % kGBN != 0)) return false;
+  if (split < 1 || split > K / kGBK || (split > 1 && (silu || partial == nullptr))) return false;
   const int max_tiles = (rows_upper + kGBM - 1) / kGBM + E;
-  dim3 grid(silu ? (N / 2) / (kGBN / 2) : N / kGBN, max_tiles), blk(256);
+  dim3 grid(silu ? (N / 2) / (kGBN / 2) : N / kGBN, max_tiles, split), blk(256);
   if (silu)
-    hipLaunchKernelGGL(moe_grouped_gemm_kernel<true>, grid, blk, 0, s, Y, X, W, offs, E, N, K, ldy);
+    hipLaunchKernelGGL(moe_grouped_gemm_kernel<true>, grid, blk, 0, s, Y, X, W, offs, E, N, K, ldy, partial,
+                       rows_upper);
   else
-    hipLaunchKernelGGL(moe_grouped_gemm_kernel<false>, grid, blk, 0, s, Y, X, W, offs, E, N, K, ldy);
+    hipLaunchKernelGGL(moe_grouped_gemm_kernel<false>, grid, blk, 0, s, Y, X, W, offs, E, N, K, ldy, partial,
+                       rows_upper);
   MXS_CHECK_LAUNCH();
   return true;
 }

@@ -91,9 +91,17 @@ def fused_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: 
     xs = x.index_select(0, tok)  # rows past the routed count are ignored by the GEMMs
     h = torch.empty(T * K, two_i // 2, dtype=x.dtype, device=dev)
     ys = torch.empty(T * K, H, dtype=x.dtype, device=dev)
+    # split-K for the down projection when the routed rows leave too few workgroups to stream the
+    # weights (decode; one expert per rank under EP): aim at ~1024 workgroups
+    tiles = min(e_local, T * K) + -(-T * K // 128)
+    split = max(1, min(8, (two_i // 2) // 64, -(-1024 // ((H // 128) * tiles))))
+    part = torch.empty(split, T * K, H, dtype=torch.float32, device=dev) if split > 1 else None
     if not (ext().moe_grouped_gemm(h, xs, w13.contiguous(), offs, True)
-            and ext().moe_grouped_gemm(ys, h, w2.contiguous(), offs, False)):
+            and ext().moe_grouped_gemm(ys, h, w2.contiguous(), offs, False, split, part)):
         return _fused_experts_loop(x, w13, w2, topk_w, topk_ids, expert_offset)
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
-    ext().moe_combine(out, ys, topk_w.float().contiguous(), inv)  # K17
+    if part is not None:
+        ext().moe_combine_partials(out, part, topk_w.float().contiguous(), inv)  # K17 over the K slices
+    else:
+        ext().moe_combine(out, ys, topk_w.float().contiguous(), inv)  # K17
     return out

@@ -367,6 +367,30 @@ def test_moe_align(gpu):
     assert (iv[~local] == -1).all()
 
 
+@pytest.mark.parametrize("split", [2, 3, 6])  # K = 384: 6 K-steps of 64
+def test_moe_grouped_gemm_split_k(gpu, split):
+    """Split-K down projection: the fp32 slices summed by moe_combine_partials equal the unsplit
+    GEMM followed by moe_combine."""
+    T, K, E, H, I = 37, 2, 4, 256, 384
+    ids = torch.randint(0, E, (T, K), device=gpu, dtype=torch.int32)
+    offs = torch.empty(E + 1, dtype=torch.int32, device=gpu)
+    perm = torch.full((T * K,), -1, dtype=torch.int32, device=gpu)
+    inv = torch.empty(T * K, dtype=torch.int32, device=gpu)
+    ops.ext().moe_align(offs, perm, ids, 0, E, inv)
+    h = torch.randn(T * K, I, device=gpu, dtype=torch.bfloat16)
+    w2 = torch.randn(E, H, I, device=gpu, dtype=torch.bfloat16) * 0.05
+    w = torch.rand(T, K, device=gpu)
+    ys = torch.empty(T * K, H, device=gpu, dtype=torch.bfloat16)
+    assert ops.ext().moe_grouped_gemm(ys, h, w2, offs, False)
+    ref_out = torch.empty(T, H, device=gpu, dtype=torch.bfloat16)
+    ops.ext().moe_combine(ref_out, ys, w, inv)
+    part = torch.empty(split, T * K, H, device=gpu, dtype=torch.float32)
+    assert ops.ext().moe_grouped_gemm(ys, h, w2, offs, False, split, part)
+    out = torch.empty(T, H, device=gpu, dtype=torch.bfloat16)
+    ops.ext().moe_combine_partials(out, part, w, inv)
+    _close(out, ref_out, 0.02, 0.02, f"split-K {split}")
+
+
 def test_moe_combine(gpu):
     """K17: each token sums its top-k expert rows (gathered through the inverse permutation) with
     the routing weights; rows owned by other ranks (inv < 0) contribute nothing."""
