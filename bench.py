@@ -314,6 +314,7 @@ def main():
     from mxserve.engine.request import SamplingParams
 
     args = EngineArgs(model=a.model, device="cuda" if on_gpu else "cpu", max_num_seqs=a.max_num_seqs,
+                      cuda_graph_max_bs=a.max_num_seqs,
                       max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=a.max_model_len,
                       enforce_eager=a.enforce_eager, seed=a.seed, kv_cache_dtype=a.kv_cache_dtype)
     if not on_gpu:  # plumbing run only (CPU container): keep it tiny
