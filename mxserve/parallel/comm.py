@@ -61,9 +61,11 @@ def init_distributed(tp_size: int, backend: Optional[str] = None, device: Option
     st = ParallelState(tp_rank=dist.get_rank(), tp_size=world, group=dist.group.WORLD)
     # scheduler metadata goes rank0 -> TP ranks over a CPU (gloo) group, never a GPU collective
     st.cpu_group = dist.new_group(backend="gloo") if backend != "gloo" else st.group
-    # custom IPC all-reduce: validated between processes sharing one GPU (tests/test_custom_ar_gpu.py);
-    # opt-in until it has run across a real xGMI mesh
-    if enable_custom_ar and backend == "nccl" and os.environ.get("MXS_CUSTOM_AR", "0") == "1":
+    # custom IPC all-reduce: validated between processes sharing one GPU (tests/test_custom_ar_gpu.py,
+    # tests/test_tp_gpu.py, where the ranks' group is gloo); opt-in until it has run across a real
+    # xGMI mesh
+    on_gpu = backend == "nccl" or (device is not None and torch.device(device).type == "cuda")
+    if enable_custom_ar and on_gpu and os.environ.get("MXS_CUSTOM_AR", "0") == "1":
         try:
             from .custom_allreduce import CustomAllReduce
             st.custom_ar = CustomAllReduce.create(st.group, device, cpu_group=st.cpu_group)

@@ -50,10 +50,10 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, group, out_splits=None, in_splits
 def _gather_slices(out_s: torch.Tensor, T: int, n: int, group) -> torch.Tensor:
     if n == 1:
         return out_s[:T]
-    if out_s.is_cuda:
+    if out_s.is_cuda and dist.get_backend(group) != "gloo":
         full = torch.empty(n * out_s.shape[0], out_s.shape[1], dtype=out_s.dtype, device=out_s.device)
         dist.all_gather_into_tensor(full, out_s.contiguous(), group=group)
-    else:  # gloo
+    else:  # gloo (CPU runs, and GPU ranks sharing one device in tests)
         parts = [torch.empty_like(out_s) for _ in range(n)]
         dist.all_gather(parts, out_s.contiguous(), group=group)
         full = torch.cat(parts)
