@@ -35,6 +35,7 @@ bool launch_moe_grouped_gemm(bf16_t*, const bf16_t*, const bf16_t*, const int*, 
                              int, float*, hipStream_t);
 void launch_moe_combine_partials(bf16_t*, const float*, const float*, const int*, int, int, int, int, long,
                                  hipStream_t);
+void launch_silu_mul_partials(bf16_t*, const float*, int, int, int, long, hipStream_t);
 }  // namespace mxs
 
 namespace {
@@ -229,7 +230,9 @@ bool moe_grouped_gemm(at::Tensor y, at::Tensor x, at::Tensor w, at::Tensor offs,
   TORCH_CHECK(w.dim() == 3 && x.dim() == 2 && y.dim() == 2, "w [E, N, K], x [rows, K], y [rows, N']");
   TORCH_CHECK(offs.scalar_type() == at::kInt && offs.numel() == w.size(0) + 1, "offs: int32 [E + 1]");
   const int N = w.size(1), K = w.size(2);
-  TORCH_CHECK(x.size(1) == K && y.size(0) == x.size(0) && y.size(1) == (silu ? N / 2 : N), "shape mismatch");
+  // split > 1 writes the fp32 partials only: y is not touched (may be empty)
+  TORCH_CHECK(x.size(1) == K && (split > 1 || (y.size(0) == x.size(0) && y.size(1) == (silu ? N / 2 : N))),
+              "shape mismatch");
   float* pp = nullptr;
   if (split > 1) {
     TORCH_CHECK(partial.has_value() && partial->scalar_type() == at::kFloat && partial->is_contiguous() &&
@@ -301,6 +304,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_grouped_gemm", &moe_grouped_gemm, pybind11::arg("y"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("offs"), pybind11::arg("silu"), pybind11::arg("split") = 1,
         pybind11::arg("partial") = pybind11::none());
+  m.def("silu_mul_partials", [](at::Tensor h, at::Tensor part) {
+    CHECK_CUDA(part); CHECK_BF16(h); CHECK_CONTIG(h);
+    TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3, "part fp32 [S, R, 2I]");
+    const int R = part.size(1), I = part.size(2) / 2;
+    TORCH_CHECK(I % 4 == 0 && h.size(0) == R && h.size(1) == I, "shapes");
+    mxs::launch_silu_mul_partials(bf(h), part.data_ptr<float>(), R, I, part.size(0),
+                                  part.size(1) * static_cast<long>(part.size(2)), stream());
+  });
   m.def("moe_combine_partials", [](at::Tensor out, at::Tensor part, at::Tensor topk_w, at::Tensor inv) {
     CHECK_CUDA(part); CHECK_BF16(out); CHECK_CONTIG(out);
     TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3, "part fp32 [S, R, H]");

@@ -169,6 +169,37 @@ __global__ void __launch_bounds__(256) moe_combine_partials_kernel(bf16_t* __res
   }
 }
 
+// Split-K gate_up: h[r, j] = silu(sum_z P[z][r][j]) * sum_z P[z][r][I + j]  (P: [S][rows][2I] fp32)
+__global__ void silu_mul_partials_kernel(bf16_t* __restrict__ h, const float* __restrict__ part, int rows, int I,
+                                         int S, long slice) {
+  const long total = static_cast<long>(rows) * (I / 4);
+  for (long idx = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; idx < total;
+       idx += static_cast<long>(gridDim.x) * blockDim.x) {
+    const long r = idx / (I / 4);
+    const int j = static_cast<int>(idx - r * (I / 4)) * 4;
+    const float* pg = part + r * 2 * I + j;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f), u = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int z = 0; z < S; ++z) {
+      const float4 a = *reinterpret_cast<const float4*>(pg + z * slice);
+      const float4 b = *reinterpret_cast<const float4*>(pg + z * slice + I);
+      g.x += a.x; g.y += a.y; g.z += a.z; g.w += a.w;
+      u.x += b.x; u.y += b.y; u.z += b.z; u.w += b.w;
+    }
+    const float o0 = g.x / (1.f + __expf(-g.x)) * u.x, o1 = g.y / (1.f + __expf(-g.y)) * u.y;
+    const float o2 = g.z / (1.f + __expf(-g.z)) * u.z, o3 = g.w / (1.f + __expf(-g.w)) * u.w;
+    *reinterpret_cast<uint2*>(h + r * I + j) = make_uint2(pack2(o0, o1), pack2(o2, o3));
+  }
+}
+
+void launch_silu_mul_partials(bf16_t* h, const float* part, int rows, int I, int S, long slice, hipStream_t s) {
+  const long total = static_cast<long>(rows) * (I / 4);
+  if (total == 0) return;
+  long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(silu_mul_partials_kernel, dim3(blocks), dim3(256), 0, s, h, part, rows, I, S, slice);
+  MXS_CHECK_LAUNCH();
+}
+
 void launch_moe_combine_partials(bf16_t* out, const float* part, const float* topk_w, const int* inv, int T, int K,
                                  int H, int S, long slice, hipStream_t s) {
   if (T == 0) return;

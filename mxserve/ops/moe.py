@@ -96,8 +96,17 @@ def fused_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: 
     tiles = min(e_local, T * K) + -(-T * K // 128)
     split = max(1, min(8, (two_i // 2) // 64, -(-1024 // ((H // 128) * tiles))))
     part = torch.empty(split, T * K, H, dtype=torch.float32, device=dev) if split > 1 else None
-    if not (ext().moe_grouped_gemm(h, xs, w13.contiguous(), offs, True)
-            and ext().moe_grouped_gemm(ys, h, w2.contiguous(), offs, False, split, part)):
+    # gate_up likewise (fp32 slices over [gate; up], SiLU*mul applied when they are summed) when its
+    # grid is small too: one local expert per rank
+    split13 = max(1, min(4, H // 64, -(-1024 // ((two_i // 128) * tiles))))
+    if split13 > 1:
+        part13 = torch.empty(split13, T * K, two_i, dtype=torch.float32, device=dev)
+        ok13 = ext().moe_grouped_gemm(ys.new_empty(0, two_i), xs, w13.contiguous(), offs, False, split13, part13)
+        if ok13:
+            ext().silu_mul_partials(h, part13)
+    else:
+        ok13 = ext().moe_grouped_gemm(h, xs, w13.contiguous(), offs, True)
+    if not (ok13 and ext().moe_grouped_gemm(ys, h, w2.contiguous(), offs, False, split, part)):
         return _fused_experts_loop(x, w13, w2, topk_w, topk_ids, expert_offset)
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
     if part is not None:

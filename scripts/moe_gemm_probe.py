@@ -49,8 +49,19 @@ def main():
         offs1 = torch.tensor([0, T * K // 4], dtype=torch.int32, device=dev)
         t1 = {sp: timeit(lambda: ops.ext().moe_grouped_gemm(ys, h, w2[:1].contiguous(), offs1, False, sp, part))
               for sp in (1, 4, 8)}
+        w1 = w13[:1].contiguous()
+        x1 = torch.randn(T * K // 4, H, device=dev, dtype=torch.bfloat16)
+        h1 = torch.empty(T * K // 4, I, device=dev, dtype=torch.bfloat16)
+        p13 = torch.empty(4, T * K // 4, 2 * I, device=dev, dtype=torch.float32)
+
+        def gu_split():
+            ops.ext().moe_grouped_gemm(h1.new_empty(0, 2 * I), x1, w1, offs1, False, 4, p13)
+            ops.ext().silu_mul_partials(h1, p13)
+        t1["gate_up_silu"] = timeit(lambda: ops.ext().moe_grouped_gemm(h1, x1, w1, offs1, True))
+        t1["gate_up_split4_then_silu"] = timeit(gu_split)
         print(json.dumps({"T": T, "ep8_one_expert_rows": T * K // 4,
-                          **{f"down_split{sp}_ms": round(v, 4) for sp, v in t1.items()}}), flush=True)
+                          **{(f"down_split{sp}_ms" if isinstance(sp, int) else f"{sp}_ms"): round(v, 4)
+                             for sp, v in t1.items()}}), flush=True)
 
 
 if __name__ == "__main__":

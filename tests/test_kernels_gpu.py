@@ -391,6 +391,26 @@ def test_moe_grouped_gemm_split_k(gpu, split):
     _close(out, ref_out, 0.02, 0.02, f"split-K {split}")
 
 
+@pytest.mark.parametrize("split", [2, 4])
+def test_moe_gate_up_split_k(gpu, split):
+    """Split-K gate_up: fp32 slices over [gate; up] + silu_mul_partials equal the fused SiLU GEMM."""
+    T, K, E, H, I = 29, 2, 3, 256, 384
+    ids = torch.randint(0, E, (T, K), device=gpu, dtype=torch.int32)
+    offs = torch.empty(E + 1, dtype=torch.int32, device=gpu)
+    perm = torch.full((T * K,), -1, dtype=torch.int32, device=gpu)
+    ops.ext().moe_align(offs, perm, ids, 0, E)
+    xs = torch.randn(T * K, H, device=gpu, dtype=torch.bfloat16)
+    w13 = torch.randn(E, 2 * I, H, device=gpu, dtype=torch.bfloat16) * 0.05
+    h_ref = torch.empty(T * K, I, device=gpu, dtype=torch.bfloat16)
+    assert ops.ext().moe_grouped_gemm(h_ref, xs, w13, offs, True)
+    part = torch.empty(split, T * K, 2 * I, device=gpu, dtype=torch.float32)
+    assert ops.ext().moe_grouped_gemm(h_ref.new_empty(0, 2 * I), xs, w13, offs, False, split, part)
+    h = torch.empty_like(h_ref)
+    ops.ext().silu_mul_partials(h, part)
+    rows = int(offs[-1])
+    _close(h[:rows], h_ref[:rows], 0.02, 0.02, f"gate_up split {split}")
+
+
 def test_moe_combine(gpu):
     """K17: each token sums its top-k expert rows (gathered through the inverse permutation) with
     the routing weights; rows owned by other ranks (inv < 0) contribute nothing."""
