@@ -166,11 +166,17 @@ def run_agg(a, eng, sp, drv, barrier) -> float:
             drv.wait_next()
             for rid, toks in drv.due():
                 eng.add_request(toks, sp, request_id=rid)
+        t0 = time.perf_counter()
         outs = eng.step()
         now = time.perf_counter()
         for o in outs:
             drv.token(o.request_id, now, o.finished)
+        if eng.step_times is not None:
+            eng.step_times["engine_step"] = eng.step_times.get("engine_step", 0.0) + now - t0
+            eng.step_times["loop"] = eng.step_times.get("loop", 0.0) + time.perf_counter() - t_loop[0]
+        t_loop[0] = time.perf_counter()
 
+    t_loop = [time.perf_counter()]
     return timed_phases(a, step, barrier, drv)
 
 
@@ -399,6 +405,10 @@ def main():
                        "graphs": sorted(eng.runner.graphs) if on_gpu else []},
         }
         print(json.dumps(line), flush=True)
+        if eng.step_times is not None and eng.step_times["steps"]:
+            n = eng.step_times["steps"]
+            print(json.dumps({"host_ms_per_step": {k: round(v / n * 1e3, 4) for k, v in eng.step_times.items()
+                                                   if k != "steps"}, "steps": n}), file=sys.stderr, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -6,6 +6,7 @@ from __future__ import annotations
 import asyncio
 import collections
 import logging
+import os
 import threading
 import time
 import uuid
@@ -54,6 +55,9 @@ class LLMEngine:
         self.async_scheduling = bool(args.async_scheduling)
         self._inflight: Optional[tuple] = None
         self.profiler = StepProfiler()  # MXS_TORCH_PROFILE="start:count:path"
+        # MXS_STEP_TIMING=1: host seconds per phase (schedule / launch / collect wait / land)
+        self.step_times: Optional[dict] = ({"schedule": 0.0, "launch": 0.0, "collect": 0.0, "land": 0.0,
+                                            "steps": 0} if os.environ.get("MXS_STEP_TIMING") == "1" else None)
 
     # ------------------------------------------------------------------ requests
     def add_request(self, prompt_token_ids: list, sampling: Optional[SamplingParams] = None,
@@ -123,7 +127,12 @@ class LLMEngine:
         return self._step()
 
     def _step(self) -> list[StepOutput]:
+        tm = self.step_times
+        t0 = time.perf_counter() if tm is not None else 0.0
         so = self.scheduler.schedule()
+        if tm is not None:
+            t1 = time.perf_counter()
+            tm["schedule"] += t1 - t0
         handle = None
         if not so.is_empty:
             if ROCTX.lib is not None:  # MXS_ROCTX=1: named ranges on the rocprofv3 timeline
@@ -134,6 +143,9 @@ class LLMEngine:
             for s in so.prefills:
                 self.num_prompt_computed += s.num_new_tokens
             self.num_steps += 1
+        if tm is not None:
+            t2 = time.perf_counter()
+            tm["launch"] += t2 - t1
         if self.async_scheduling:
             done, self._inflight = self._inflight, ((so, handle) if handle is not None else None)
         else:
@@ -142,7 +154,14 @@ class LLMEngine:
             return []
         dso, dh = done
         sampled = self.runner.collect(dh)
-        return self._land(dso, sampled, dh.get("logprobs"))
+        if tm is None:
+            return self._land(dso, sampled, dh.get("logprobs"))
+        t3 = time.perf_counter()
+        out = self._land(dso, sampled, dh.get("logprobs"))
+        tm["collect"] += t3 - t2
+        tm["land"] += time.perf_counter() - t3
+        tm["steps"] += 1
+        return out
 
     def _land(self, so, sampled: dict, logprobs: Optional[dict] = None) -> list[StepOutput]:
         emitted = self.scheduler.update(so, sampled)
