@@ -60,9 +60,9 @@ def parse():
     ap.add_argument("--model", default="meta-llama/Llama-3.2-1B-Instruct")
     ap.add_argument("--isl", type=int, default=4000)
     ap.add_argument("--osl", type=int, default=500)
-    ap.add_argument("--qps", type=float, default=float(os.environ.get("MXS_BENCH_QPS", "40")),
+    ap.add_argument("--qps", type=float, default=float(os.environ.get("MXS_BENCH_QPS", "42")),
                     help="Poisson arrival rate per GPU (requests/s)")
-    ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--max-num-seqs", type=int, default=384)
     ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--enforce-eager", action="store_true")
