@@ -197,3 +197,20 @@ def test_torch_profiler_window(tmp_path):
     eng.generate([list(range(5, 30))], SamplingParams(max_tokens=8, temperature=0.0, ignore_eos=True))
     assert eng.profiler.done and path.exists()
     assert json.loads(path.read_text())["traceEvents"]
+
+
+def test_step_timing(monkeypatch):
+    """MXS_STEP_TIMING=1: every landed step is counted and each phase accumulates host time; the
+    timed engine emits the same tokens as an untimed one."""
+    monkeypatch.setenv("MXS_STEP_TIMING", "1")
+    eng = _engine(True)
+    assert eng.step_times is not None
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    out = eng.generate([list(range(5, 30)), list(range(40, 52))], sp)
+    st = eng.step_times
+    assert st["steps"] >= 6 and all(st[k] >= 0.0 for k in ("schedule", "launch", "collect", "land"))
+    assert st["launch"] > 0.0
+    monkeypatch.delenv("MXS_STEP_TIMING")
+    ref = _engine(True)
+    assert ref.step_times is None
+    assert ref.generate([list(range(5, 30)), list(range(40, 52))], sp) == out
