@@ -8,7 +8,7 @@ out=gpurun_out/qps_check.jsonl; : > $out
 for cfg in ${QPS_CFGS:-"44 384 3000" "42 384 3000"}; do
   set -- $(echo $cfg | tr ',' ' ')
   echo "== qps $1 seqs $2 steps $3"
-  timeout -k 10 400 python bench.py --qps $1 --max-num-seqs $2 --steps $3 --warmup 1500 \
+  timeout -k 10 400 python bench.py --qps $1 --max-num-seqs $2 --steps $3 --warmup 1500 ${BENCH_ARGS:-} \
     > gpurun_out/qc.log 2>&1 || { tail -30 gpurun_out/qc.log; exit 1; }
   tail -2 gpurun_out/qc.log | tee -a $out | cut -c1-120
 done
