@@ -2,35 +2,44 @@
 """Headline benchmark: output tok/s (node) + p50 TTFT at a fixed QPS, Llama-3.2-1B-Instruct,
 aggregated vs disaggregated serving (BASELINE.json metric / configs 2-3).
 
---mode agg (default): each rank (one per GPU, launched by torch.distributed.run) runs an
-  independent engine replica -- the reference scales Llama-3.2-1B by `replicas:` of single-GPU
-  workers behind the frontend router -- driven by an open-loop Poisson arrival
-  process at --qps requests/s per GPU (weak scaling).
---mode disagg (N even): ranks [0, N/2) are prefill workers, ranks [N/2, N) decode workers, paired
-  1P:1D (the reference's vllm/disagg.yaml graph).  Requests arrive at the decode rank (2 x --qps per
-  pair, so the per-GPU rate matches agg); it reserves KV blocks and hands the prompt to its prefill
-  rank, which computes it, pushes the blocks straight into the decode rank's pool with the IPC copy
-  kernel (xGMI between GPUs; mxserve/disagg/kv_transfer.py) and returns the first token.  TTFT
-  there includes the KV transfer.
+Launch: `python bench.py --gpus N` spawns N ranks itself (torch.distributed.run, one process per
+GPU) before anything touches the GPU; under an external launcher WORLD_SIZE must equal --gpus.
 
-Workload shape: ISL 4000 / OSL 500, the only request shape the reference quantifies
-(examples/dgdr/trtllm/dgdr.yaml:22-26).  Prompts are synthetic random token ids and the weights are
-random-init of the real architecture (no network on the GPU box); every request generates exactly
-OSL tokens (ignore_eos).
+Phases (--mode auto: agg for N = 1, agg then disagg for N >= 2, both in the one JSON line):
+  agg     each rank runs an independent engine replica -- the reference scales Llama-3.2-1B by
+          `replicas:` of single-GPU workers behind the frontend router (examples/deploy/vllm/agg.yaml:14,21;
+          SURVEY.md §2.4 P01) -- under an open-loop Poisson arrival process of --qps requests/s
+          per GPU (weak scaling).  `value` is this phase.
+  disagg  ranks [0, N/2) prefill, [N/2, N) decode, paired 1P:1D (examples/deploy/vllm/disagg.yaml:18-57).
+          Requests arrive at the decode rank at 2 x --qps per pair (same node QPS as agg); it
+          reserves KV blocks and hands the prompt to its prefill rank, which computes it, pushes
+          the blocks into the decode rank's staging arena with the IPC copy kernel (xGMI between
+          GPUs; mxserve/disagg/kv_transfer.py) and returns the first token.  TTFT includes the
+          KV transfer.
 
-A "step" is one engine iteration (continuous batching: decodes + chunked prefill under the token
-budget) of a rank that owns requests (every rank in agg, the decode ranks in disagg).  W warmup
-steps fill the pipeline; then exactly K steps are timed between a barrier + device sync on both
-sides.  value = output tokens produced in the timed window summed over ranks / the slowest rank's
-window.  TTFT is measured from each request's scheduled Poisson arrival (queueing included) for
-requests whose first token lands in the window.
+Workload: ISL 4000 / OSL 500, the only request shape the reference quantifies
+(examples/dgdr/trtllm/dgdr.yaml:22-26).  Synthetic random prompt token ids, random-init weights of
+the real architecture (no network on the GPU box); every request generates exactly OSL tokens.
+
+Steps and steady state.  A step is one engine iteration (continuous batching: decodes + chunked
+prefill under the token budget) of a request-owning rank.  The warmup runs at least W steps and
+until the open-loop system is in steady state on every rank: over the last two windows the mean
+running set is flat and completions match arrivals (or --max-warmup-s passes; reported).  Then a
+short soak collects TTFT samples in steady state, and exactly K steps are timed between a
+barrier + device sync on both sides.  value = output tokens produced in the timed window summed
+over ranks / the slowest rank's window.  TTFT is measured from each request's scheduled Poisson
+arrival (queueing included) for first tokens landing in the steady-state soak + timed window.
 """
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -51,18 +60,20 @@ def vlog(msg: str) -> None:
               flush=True)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1500)
-    ap.add_argument("--warmup", type=int, default=1500)
-    ap.add_argument("--mode", choices=["agg", "disagg"], default=os.environ.get("MXS_BENCH_MODE", "agg"))
+    ap.add_argument("--warmup", type=int, default=500)
+    ap.add_argument("--mode", choices=["auto", "agg", "disagg", "both"], default=os.environ.get("MXS_BENCH_MODE", "auto"))
     ap.add_argument("--model", default="meta-llama/Llama-3.2-1B-Instruct")
     ap.add_argument("--isl", type=int, default=4000)
     ap.add_argument("--osl", type=int, default=500)
     ap.add_argument("--qps", type=float, default=float(os.environ.get("MXS_BENCH_QPS", "42")),
                     help="Poisson arrival rate per GPU (requests/s)")
     ap.add_argument("--max-num-seqs", type=int, default=384)
+    ap.add_argument("--disagg-max-num-seqs", type=int, default=512,
+                    help="decode ranks of the disagg phase carry 2x the per-GPU request rate")
     ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--enforce-eager", action="store_true")
@@ -71,19 +82,48 @@ def parse():
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--device", default="auto")
-    ap.add_argument("--max-warmup-s", type=float, default=120.0,
-                    help="cap on the extra warmup that waits for the first finished request")
-    return ap.parse_args()
+    ap.add_argument("--max-warmup-s", type=float, default=90.0,
+                    help="cap on the warmup that waits for steady state")
+    ap.add_argument("--steady-window-s", type=float, default=2.5,
+                    help="length of each of the two windows compared by the steady-state test")
+    ap.add_argument("--min-ttft-samples", type=int, default=40,
+                    help="TTFT samples per request-owning rank collected in steady state before timing")
+    ap.add_argument("--phase-timeout-s", type=float, default=float(os.environ.get("MXS_BENCH_PHASE_TIMEOUT", "420")),
+                    help="a disagg phase that has not finished by then is reported as failed")
+    return ap.parse_args(argv)
 
 
+# ---------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a) -> int:
+    """`--gpus N` without an external launcher: run N ranks under torch.distributed.run as a CHILD
+    process (nothing here has touched the GPU; the parent never execs) and return its exit code."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (the only mode the host driver has)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    vlog("launching: " + " ".join(cmd))
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------------- load + bookkeeping
 class Driver:
-    """Open-loop Poisson load on one request-owning rank + latency bookkeeping."""
+    """Open-loop Poisson load on one request-owning rank, steady-state detection and latency
+    bookkeeping."""
 
     def __init__(self, a, rank: int, vocab: int, qps: float):
         rng = np.random.default_rng(1234 + rank)
-        self.horizon = 4096
+        self.qps = qps
+        self.horizon = 65536
         self.arrivals = np.cumsum(rng.exponential(1.0 / qps, size=self.horizon))
-        self.prompts = rng.integers(100, vocab - 100, size=(self.horizon, a.isl), dtype=np.int64)
+        self.isl = a.isl
+        self.vocab = vocab
+        self.rng = rng
         self.rank = rank
         self.nxt = 0
         self.t_start = 0.0
@@ -91,10 +131,18 @@ class Driver:
         self.first_tok: dict = {}
         self.last_tok: dict = {}
         self.itls: list = []
-        self.record = False
+        self.record_ttft = False  # steady state reached: TTFT samples count from here
+        self.record = False  # timed window: tokens + ITL
         self.finished = 0
         self.warmup_steps = 0
+        self.warmup_s = 0.0
+        self.steady = False
         self.c = {"ttft": [], "tokens": 0}
+        # per-step samples for the steady-state test: (time, running set, arrivals, finished)
+        self.hist: list = []
+
+    def prompt(self) -> list:
+        return self.rng.integers(100, self.vocab - 100, size=self.isl, dtype=np.int64).tolist()
 
     def due(self) -> list:
         """(request_id, prompt) for every arrival whose time has come."""
@@ -103,19 +151,19 @@ class Driver:
         while self.nxt < self.horizon and self.arrivals[self.nxt] <= now_rel:
             rid = f"r{self.rank}-{self.nxt}"
             self.arrival_of[rid] = self.t_start + self.arrivals[self.nxt]
-            out.append((rid, self.prompts[self.nxt].tolist()))
+            out.append((rid, self.prompt()))
             self.nxt += 1
         return out
 
     def wait_next(self) -> None:
         if self.nxt < self.horizon:
-            time.sleep(max(0.0, self.t_start + self.arrivals[self.nxt] - time.perf_counter()))
+            time.sleep(max(0.0, min(0.05, self.t_start + self.arrivals[self.nxt] - time.perf_counter())))
 
     def token(self, rid: str, now: float, finished: bool = False) -> None:
         self.finished += finished
         if rid not in self.first_tok:
             self.first_tok[rid] = now
-            if self.record:
+            if self.record_ttft:
                 self.c["ttft"].append(now - self.arrival_of[rid])
         elif self.record:
             self.itls.append(now - self.last_tok[rid])
@@ -123,33 +171,81 @@ class Driver:
         if self.record:
             self.c["tokens"] += 1
 
+    def sample(self, running: int) -> None:
+        self.hist.append((time.perf_counter(), running, self.nxt, self.finished))
+
+    def is_steady(self, window: float) -> bool:
+        """Running set flat over two consecutive windows and completions ~= arrivals in the last."""
+        if not self.hist or self.finished == 0:
+            return False
+        t_now = self.hist[-1][0]
+        if t_now - self.t_start < 2 * window:
+            return False
+        h = np.asarray(self.hist, dtype=np.float64)
+        a_mask = (h[:, 0] >= t_now - 2 * window) & (h[:, 0] < t_now - window)
+        b_mask = h[:, 0] >= t_now - window
+        if a_mask.sum() < 5 or b_mask.sum() < 5:
+            return False
+        ra, rb = h[a_mask, 1].mean(), h[b_mask, 1].mean()
+        b = h[b_mask]
+        arr = b[-1, 2] - b[0, 2]
+        fin = b[-1, 3] - b[0, 3]
+        flat = abs(rb - ra) <= 0.08 * rb + 1.0
+        balanced = arr > 0 and abs(fin - arr) <= 0.2 * arr + 2
+        return bool(flat and balanced)
+
     def stats(self, dt: float) -> list:
         ttft = np.array(self.c["ttft"]) if self.c["ttft"] else np.array([np.nan])
         itl = np.array(self.itls) if self.itls else np.array([np.nan])
+        running = float(np.mean([x[1] for x in self.hist[-200:]])) if self.hist else 0.0
         return [dt, float(self.c["tokens"]), float(np.nanmedian(ttft)), float(np.nanmedian(itl)),
-                float(len(self.c["ttft"])), float(self.warmup_steps)]
+                float(len(self.c["ttft"])), float(self.warmup_steps), float(self.warmup_s), float(self.steady),
+                running, float(np.nanpercentile(ttft, 90)), float(np.nanpercentile(itl, 90))]
 
 
-def timed_phases(a, step, barrier, drv, on_phase=lambda phase: None) -> float:
-    """W untimed steps, then exactly K steps between barrier + device sync; returns the window."""
+_STAT_NAN = [0.0, 0.0, float("nan"), float("nan"), 0.0, float("nan"), float("nan"), float("nan"), float("nan"),
+             float("nan"), float("nan")]
+
+
+def timed_phases(a, step, barrier, agree, drv, running, on_phase=lambda phase: None) -> float:
+    """Warm up to steady state (agreed by every request-owning rank), soak for TTFT samples, then
+    exactly K steps between barrier + device sync; returns the timed window."""
     on_phase("warmup")
     barrier()
     vlog("warmup")
     drv.t_start = time.perf_counter()
+    check_every = 25
     i = 0
-    while i < a.warmup or (drv.finished == 0 and time.perf_counter() - drv.t_start < a.max_warmup_s):
+    while True:
         step()
-        if i % 200 == 0:
-            vlog(f"warmup step {i}: {drv.nxt} arrivals, {len(drv.first_tok)} first tokens")
+        drv.sample(running())
+        i += 1
+        if i % check_every == 0:
+            timed_out = time.perf_counter() - drv.t_start > a.max_warmup_s
+            mine = i >= a.warmup and (drv.is_steady(a.steady_window_s) or timed_out)
+            if i % 200 == 0:
+                vlog(f"warmup step {i}: {drv.nxt} arrivals, {drv.finished} finished, running {running()}")
+            if agree(mine):
+                drv.steady = not timed_out or drv.is_steady(a.steady_window_s)
+                break
+    # steady state: count TTFTs from here; soak until this rank has enough samples (bounded)
+    drv.record_ttft = True
+    t_soak = time.perf_counter()
+    soak_cap = max(2.0, 3.0 * a.min_ttft_samples / max(drv.qps, 1e-3))
+    while len(drv.c["ttft"]) < a.min_ttft_samples and time.perf_counter() - t_soak < soak_cap:
+        step()
+        drv.sample(running())
         i += 1
     drv.warmup_steps = i
+    drv.warmup_s = time.perf_counter() - drv.t_start
     on_phase("timed")
     barrier()
-    vlog("timed")
+    vlog(f"timed (warmup {i} steps, {drv.warmup_s:.1f}s, steady={drv.steady})")
     drv.record = True
     t0 = time.perf_counter()
     for i in range(a.steps):
         step()
+        drv.sample(running())
         if i % 200 == 0:
             vlog(f"timed step {i}: {drv.c['tokens']} tokens")
     on_phase("stop")
@@ -158,7 +254,7 @@ def timed_phases(a, step, barrier, drv, on_phase=lambda phase: None) -> float:
     return time.perf_counter() - t0
 
 
-def run_agg(a, eng, sp, drv, barrier) -> float:
+def run_agg(a, eng, sp, drv, barrier, agree) -> float:
     def step():
         for rid, toks in drv.due():
             eng.add_request(toks, sp, request_id=rid)
@@ -166,6 +262,8 @@ def run_agg(a, eng, sp, drv, barrier) -> float:
             drv.wait_next()
             for rid, toks in drv.due():
                 eng.add_request(toks, sp, request_id=rid)
+            if not eng.has_unfinished():
+                return
         t0 = time.perf_counter()
         outs = eng.step()
         now = time.perf_counter()
@@ -177,15 +275,16 @@ def run_agg(a, eng, sp, drv, barrier) -> float:
         t_loop[0] = time.perf_counter()
 
     t_loop = [time.perf_counter()]
-    return timed_phases(a, step, barrier, drv)
+    sch = eng.scheduler
+    return timed_phases(a, step, barrier, agree, drv, lambda: len(sch.running) + len(sch.waiting))
 
 
-def _pair_conn(rank: int, world: int, is_decode: bool):
+def _pair_conn(rank: int, world: int, is_decode: bool, base_port: int):
     """Host control channel between a prefill rank and its decode rank (same node)."""
     from multiprocessing.connection import Client, Listener
     half = world // 2
     pair = rank - half if is_decode else rank
-    port = int(os.environ.get("MASTER_PORT", "29500")) + 101 + pair
+    port = base_port + pair
     if is_decode:
         lst = Listener(("127.0.0.1", port), authkey=b"mxs-bench")
         conn = lst.accept()
@@ -199,14 +298,14 @@ def _pair_conn(rank: int, world: int, is_decode: bool):
     raise RuntimeError("could not reach the decode rank")
 
 
-def run_disagg_decode(a, eng, sp, drv, barrier, conn) -> float:
+def run_disagg_decode(a, eng, sp, drv, barrier, agree, conn) -> float:
     from mxserve.disagg.kv_transfer import KVTransferAgent
     agent = KVTransferAgent(eng.runner, "xgmi")
     conn.send(("desc", agent.descriptor()))
-    # the prefill rank maps the pool now, while this rank idles in a plain socket wait
+    # the prefill rank maps the arena now, while this rank idles in a plain socket wait
     ack = conn.recv()
     assert ack[0] == "mapped", ack
-    vlog("decode pool mapped by the prefill rank")
+    vlog("decode arena mapped by the prefill rank")
     bs = eng.args.block_size
     backlog: list = []
     inflight: dict = {}
@@ -219,12 +318,12 @@ def run_disagg_decode(a, eng, sp, drv, barrier, conn) -> float:
         while backlog:
             rid, toks = backlog[0]
             req = eng.reserve_remote_prefill(toks, sp, rid)
-            if req is None:  # decode pool full: retry next step
+            if req is None:  # decode pool or batch full: retry next step
                 break
-            backlog.pop(0)
             skip = req.num_cached_tokens // bs
             dst = list(req.block_ids[skip:-(-len(toks) // bs)])
             start = agent.acquire(len(dst))  # None: host-staged transfer for this request
+            backlog.pop(0)
             conn.send(("prefill", rid, toks, dst, skip, start))
             inflight[rid] = (dst, start)
         now = time.perf_counter()
@@ -233,19 +332,22 @@ def run_disagg_decode(a, eng, sp, drv, barrier, conn) -> float:
             dst, start = inflight.pop(rid)
             if start is not None:  # staging extent -> pool blocks, ordered before the next step
                 agent.land(start, dst)
-            elif data is not None:  # host-staged transfer (CPU plumbing runs)
+            elif data is not None:  # host-staged transfer
                 agent.write_blocks(dst, data)
-            eng.complete_remote_prefill(rid, tok)
-            drv.token(rid, now)
+            out = eng.complete_remote_prefill(rid, tok)
+            drv.token(rid, now, out.finished)
         if eng.has_unfinished():
             outs = eng.step()
             now = time.perf_counter()
             for o in outs:
                 drv.token(o.request_id, now, o.finished)
         elif inflight:  # nothing to decode yet: block until a prefill lands (or an arrival is due)
-            conn.poll(0.05)
+            conn.poll(0.02)
 
-    return timed_phases(a, step, barrier, drv, on_phase=lambda ph: conn.send(("phase", ph)))
+    sch = eng.scheduler
+    return timed_phases(a, step, barrier, agree, drv,
+                        lambda: len(sch.running) + len(sch.remote) + len(backlog),
+                        on_phase=lambda ph: conn.send(("phase", ph)))
 
 
 def run_disagg_prefill(eng, temperature: float, barrier, conn) -> int:
@@ -258,7 +360,7 @@ def run_disagg_prefill(eng, temperature: float, barrier, conn) -> int:
     if agent.backend == "xgmi" and target["backend"] == "xgmi":
         agent.connect(target)
     conn.send(("mapped",))
-    vlog(f"prefill rank serving (decode pool backend {target['backend']})")
+    vlog(f"prefill rank serving (decode arena backend {target['backend']})")
     pending: dict = {}
     moved = 0
     while True:
@@ -273,12 +375,12 @@ def run_disagg_prefill(eng, temperature: float, barrier, conn) -> int:
             _, rid, toks, dst, skip, start = msg
             eng.add_request(toks, SamplingParams(max_tokens=1, temperature=temperature, ignore_eos=True),
                             request_id=rid, disagg_role="prefill_only")
-            vlog(f"prefill {rid}: {len(toks)} tokens -> {len(dst)} blocks")
             pending[rid] = (dst, skip, start)
         if stop:
+            agent.close()
             return moved
         if not eng.has_unfinished():
-            time.sleep(0.0002)
+            conn.poll(0.0005)
             continue
         for o in eng.step():
             if not o.finished or o.request_id not in pending:
@@ -287,8 +389,7 @@ def run_disagg_prefill(eng, temperature: float, barrier, conn) -> int:
             src = list(eng.requests[o.request_id].block_ids[skip:skip + len(dst)])
             data = None
             if start is not None:
-                secs = agent.push_xgmi(src, target, start)
-                vlog(f"pushed {o.request_id}: {len(src)} blocks in {secs * 1e3:.2f} ms")
+                agent.push_xgmi(src, target, start)
             else:
                 data = agent.read_blocks(src)
             moved += len(src)
@@ -296,122 +397,267 @@ def run_disagg_prefill(eng, temperature: float, barrier, conn) -> int:
             conn.send(("done", o.request_id, o.token_id, data))
 
 
-def main():
-    a = parse()
-    import torch
-    import torch.distributed as dist
+# ---------------------------------------------------------------------------- phases
+class Ctx:
+    """Per-rank process context shared by the phases."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    on_gpu = torch.cuda.is_available() and a.device != "cpu"
-    disagg = a.mode == "disagg"
-    if disagg and (world < 2 or world % 2):
-        raise SystemExit("--mode disagg needs an even number of ranks (1 prefill : 1 decode pairs)")
-    if on_gpu:
-        torch.cuda.set_device(local % torch.cuda.device_count())
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # disagg ranks exchange only host messages + barriers (and may share a GPU in functional runs)
-        dist.init_process_group("nccl" if on_gpu and not disagg else "gloo")
+    def __init__(self, a):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.on_gpu = torch.cuda.is_available() and a.device != "cpu"
+        self.ndev = torch.cuda.device_count() if self.on_gpu else 0
+        self.shared_gpu = self.on_gpu and self.ndev < self.world
+        if self.on_gpu:
+            torch.cuda.set_device(self.local % self.ndev)
+        self.pg_decode = None
+        if self.world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            # control plane only (barriers, steady-state votes, stats): replicas share no tensors,
+            # and the P->D KV moves over IPC, so a CPU group keeps RCCL out of the measurement
+            dist.init_process_group("gloo")
+            if self.world % 2 == 0:
+                self.pg_decode = dist.new_group(list(range(self.world // 2, self.world)), backend="gloo")
+        self.sync = torch.cuda.synchronize if self.on_gpu else (lambda: None)
 
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+        self.sync()
+
+    def agree_fn(self, group, size: int):
+        """All request-owning ranks stop warming up at the same step: every rank votes, MIN wins."""
+        torch, dist = self.torch, self.dist
+
+        def agree(flag: bool) -> bool:
+            if size <= 1:
+                return bool(flag)
+            t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+            return bool(t.item())
+        return agree
+
+    def gather(self, vals: list) -> np.ndarray:
+        torch, dist = self.torch, self.dist
+        t = torch.tensor(vals, dtype=torch.float64)
+        if self.world > 1:
+            parts = [torch.zeros_like(t) for _ in range(self.world)]
+            dist.all_gather(parts, t)
+            return torch.stack(parts).numpy()
+        return t.unsqueeze(0).numpy()
+
+
+def engine_args(a, ctx, **kw):
     from mxserve.config import EngineArgs
-    from mxserve.engine.engine import LLMEngine
-    from mxserve.engine.request import SamplingParams
-
-    args = EngineArgs(model=a.model, device="cuda" if on_gpu else "cpu", max_num_seqs=a.max_num_seqs,
+    args = EngineArgs(model=a.model, device="cuda" if ctx.on_gpu else "cpu", max_num_seqs=a.max_num_seqs,
                       cuda_graph_max_bs=a.max_num_seqs,
                       max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=a.max_model_len,
                       enforce_eager=a.enforce_eager, seed=a.seed, kv_cache_dtype=a.kv_cache_dtype)
-    if not on_gpu:  # plumbing run only (CPU container): keep it tiny
+    if kw:
+        args = args.replace(**kw)
+    if not ctx.on_gpu:  # plumbing run only (CPU container): keep it tiny
         args = args.replace(model="tiny-llama", max_model_len=1024, cpu_num_blocks=4096)
-        a.isl, a.osl = min(a.isl, 200), min(a.osl, 20)
-    is_prefill = disagg and rank < world // 2
-    if disagg:
-        args = args.replace(disagg_mode="prefill" if is_prefill else "decode")
-        if on_gpu and torch.cuda.device_count() < world:  # functional run: ranks share a GPU
-            args = args.replace(num_gpu_blocks=int(os.environ.get("MXS_BENCH_SHARED_BLOCKS", "40000")))
-    vlog("building engine")
-    eng = LLMEngine(args)
-    vlog(f"engine ready ({eng.runner.num_blocks} KV blocks)")
-    sp = SamplingParams(max_tokens=a.osl, temperature=a.temperature, ignore_eos=True)
+    elif ctx.shared_gpu:  # functional run: ranks share a GPU, split its memory
+        args = args.replace(num_gpu_blocks=int(os.environ.get("MXS_BENCH_SHARED_BLOCKS", "40000")))
+    return args
 
-    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        sync()
+def free_engine(eng, ctx) -> None:
+    eng.close()
+    del eng
+    gc.collect()
+    if ctx.on_gpu:
+        ctx.torch.cuda.synchronize()
+        ctx.torch.cuda.empty_cache()
 
-    if not disagg:
-        drv = Driver(a, rank, eng.model_config.vocab_size, a.qps)
-        local_stats = drv.stats(run_agg(a, eng, sp, drv, barrier))
-    else:
-        conn = _pair_conn(rank, world, not is_prefill)
-        vlog("paired")
-        if is_prefill:
-            run_disagg_prefill(eng, a.temperature, barrier, conn)
-            local_stats = [0.0, 0.0, float("nan"), float("nan"), 0.0, float("nan")]
-        else:
-            drv = Driver(a, rank, eng.model_config.vocab_size, 2 * a.qps)
-            local_stats = drv.stats(run_disagg_decode(a, eng, sp, drv, barrier, conn))
-        conn.close()
 
-    local_stats = torch.tensor(local_stats, dtype=torch.float64)
-    if world > 1:
-        gathered = [torch.zeros_like(local_stats) for _ in range(world)]
-        dist.all_gather_object(gathered, local_stats)
-        allst = torch.stack(gathered)
-    else:
-        allst = local_stats.unsqueeze(0)
-    if rank == 0:
-        col = allst.numpy()
-        t_max = float(col[:, 0].max())
-        value = float(col[:, 1].sum()) / t_max
+def summarize(col: np.ndarray, steps: int, owners: list) -> dict:
+    """Whole-job numbers from the per-rank stat rows of the request-owning ranks."""
+    col = col[owners]
+    t_max = float(col[:, 0].max())
+    value = float(col[:, 1].sum()) / t_max if t_max > 0 else 0.0
 
-        def med(c):
-            v = col[:, c][~np.isnan(col[:, c])]
-            return float(np.median(v)) * 1e3 if len(v) else None
+    def med(c):
+        v = col[:, c][~np.isnan(col[:, c])]
+        return float(np.median(v)) * 1e3 if len(v) else None
 
-        ttft_p50, itl_p50 = med(2), med(3)
-        st = eng.stats()
-        line = {
-            "metric": BASELINE_METRIC,
-            "value": round(value, 2),
-            "unit": "tok/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "warmup_steps_executed": int(np.nanmax(col[:, 5])),
-            "ms_per_step": round(t_max / a.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16" if on_gpu else "fp32",
-            "data": "synthetic (random prompt token ids, random-init weights, Poisson arrivals)",
-            "config": {"model": args.model if on_gpu else "tiny-llama (CPU plumbing run)",
-                       "global_batch": int(world * a.max_num_seqs), "seq_len": a.isl + a.osl,
-                       "parallelism": f"disagg {world // 2}P+{world // 2}D" if disagg else f"dp{world}",
-                       "mode": a.mode, "isl": a.isl, "osl": a.osl,
-                       "qps_per_gpu": a.qps, "qps_node": a.qps * world,
-                       "kv_cache_dtype": "fp8_e4m3fn" if eng.runner.kv_fp8 else ("bf16" if on_gpu else "fp32")},
-            "ttft_p50_ms": None if ttft_p50 is None else round(ttft_p50, 2),
-            "itl_p50_ms": None if itl_p50 is None else round(itl_p50, 3),
+    r = lambda x, n=2: None if x is None else round(x, n)  # noqa: E731
+    ttft, itl = med(2), med(3)
+    return {"value": round(value, 2), "ms_per_step": round(t_max / steps * 1e3, 4),
+            "ttft_p50_ms": r(ttft), "ttft_p90_ms": r(med(9)), "itl_p50_ms": r(itl, 3), "itl_p90_ms": r(med(10), 3),
             "requests_with_first_token": int(col[:, 4].sum()),
-            "sla_isl4000_osl500": {"ttft_ms<=600": ttft_p50 is not None and ttft_p50 <= 600,
-                                   "itl_ms<=25": itl_p50 is not None and itl_p50 <= 25},
-            "engine": {"kv_blocks": st["num_blocks"], "running_at_end": st["num_running"],
-                       "waiting_at_end": st["num_waiting"], "preemptions": st["num_preemptions"],
-                       "graphs": sorted(eng.runner.graphs) if on_gpu else []},
-        }
-        print(json.dumps(line), flush=True)
-        if eng.step_times is not None and eng.step_times["steps"]:
-            n = eng.step_times["steps"]
-            print(json.dumps({"host_ms_per_step": {k: round(v / n * 1e3, 4) for k, v in eng.step_times.items()
-                                                   if k != "steps"}, "steps": n}), file=sys.stderr, flush=True)
+            "warmup_steps_executed": int(np.nanmax(col[:, 5])), "warmup_s": round(float(np.nanmax(col[:, 6])), 1),
+            "steady_state": bool(np.all(col[:, 7] > 0)), "running_mean": round(float(np.nanmean(col[:, 8])), 1),
+            "sla_isl4000_osl500": {"ttft_ms<=600": ttft is not None and ttft <= 600,
+                                   "itl_ms<=25": itl is not None and itl <= 25}}
+
+
+def phase_agg(a, ctx) -> tuple:
+    from mxserve.engine.engine import LLMEngine
+    from mxserve.engine.request import SamplingParams
+    args = engine_args(a, ctx)
+    isl, osl = (a.isl, a.osl) if ctx.on_gpu else (min(a.isl, 200), min(a.osl, 20))
+    a2 = argparse.Namespace(**{**vars(a), "isl": isl, "osl": osl})
+    vlog("agg: building engine")
+    eng = LLMEngine(args)
+    vlog(f"agg: engine ready ({eng.runner.num_blocks} KV blocks)")
+    sp = SamplingParams(max_tokens=osl, temperature=a.temperature, ignore_eos=True)
+    drv = Driver(a2, ctx.rank, eng.model_config.vocab_size, a.qps)
+    group = None
+    agree = ctx.agree_fn(group, ctx.world)
+    st = drv.stats(run_agg(a2, eng, sp, drv, ctx.barrier, agree))
+    info = {"kv_blocks": eng.runner.num_blocks, "graphs": sorted(eng.runner.graphs) if ctx.on_gpu else [],
+            "preemptions": eng.stats()["num_preemptions"], "model": args.model,
+            "kv_cache_dtype": "fp8_e4m3fn" if eng.runner.kv_fp8 else ("bf16" if ctx.on_gpu else "fp32"),
+            "isl": isl, "osl": osl}
+    host = None
+    if eng.step_times is not None and eng.step_times["steps"]:
+        n = eng.step_times["steps"]
+        host = {k: round(v / n * 1e3, 4) for k, v in eng.step_times.items() if k != "steps"}
+    free_engine(eng, ctx)
+    return ctx.gather(st), info, host
+
+
+def phase_disagg(a, ctx, base_port: int) -> tuple:
+    from mxserve.engine.engine import LLMEngine
+    from mxserve.engine.request import SamplingParams
+    world, rank = ctx.world, ctx.rank
+    is_prefill = rank < world // 2
+    isl, osl = (a.isl, a.osl) if ctx.on_gpu else (min(a.isl, 200), min(a.osl, 20))
+    a2 = argparse.Namespace(**{**vars(a), "isl": isl, "osl": osl})
+    if is_prefill:  # prefill-only steps never replay decode graphs
+        args = engine_args(a, ctx, disagg_mode="prefill", enforce_eager=True)
+    else:
+        mns = a.disagg_max_num_seqs
+        args = engine_args(a, ctx, disagg_mode="decode", max_num_seqs=mns, cuda_graph_max_bs=mns)
+    vlog("disagg: building engine")
+    eng = LLMEngine(args)
+    vlog(f"disagg: engine ready ({eng.runner.num_blocks} KV blocks)")
+    conn = _pair_conn(rank, world, not is_prefill, base_port)
+    if is_prefill:
+        run_disagg_prefill(eng, a.temperature, ctx.barrier, conn)
+        st = list(_STAT_NAN)
+    else:
+        sp = SamplingParams(max_tokens=osl, temperature=a.temperature, ignore_eos=True)
+        drv = Driver(a2, rank, eng.model_config.vocab_size, 2 * a.qps)
+        agree = ctx.agree_fn(ctx.pg_decode, world // 2)
+        st = drv.stats(run_disagg_decode(a2, eng, sp, drv, ctx.barrier, agree, conn))
+    conn.close()
+    info = {"decode_max_num_seqs": a.disagg_max_num_seqs}
+    free_engine(eng, ctx)
+    return ctx.gather(st), info
+
+
+def main():
+    a = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and a.gpus > 1:
+        return launch_ranks(a)
+    world = int(world_env or "1")
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; run `python bench.py --gpus N` "
+                         "(it spawns the ranks) or launch exactly N ranks")
+    mode = a.mode if a.mode != "auto" else ("agg" if world == 1 else "both")
+    if mode in ("disagg", "both") and (world < 2 or world % 2):
+        raise SystemExit("bench.py: the disagg phase needs an even number of GPUs (1 prefill : 1 decode pairs)")
+    ctx = Ctx(a)
+    base_port = int(os.environ.get("MASTER_PORT", "29500")) + 101
+
+    agg = dis = info = None
+    if mode in ("agg", "both"):
+        col, info, host = phase_agg(a, ctx)
+        agg = summarize(col, a.steps, list(range(world)))
+        if host and ctx.rank == 0:
+            print(json.dumps({"host_ms_per_step": host}), file=sys.stderr, flush=True)
+    if mode in ("disagg", "both"):
+        dis = run_guarded(lambda: phase_disagg(a, ctx, base_port), a.phase_timeout_s, ctx, agg_info=info,
+                          agg=agg, a=a, mode=mode)
+        col_d, info_d = dis
+        dis = summarize(col_d, a.steps, list(range(world // 2, world)))
+        dis.update(info_d, parallelism=f"disagg {world // 2}P+{world // 2}D", qps_per_pair=2 * a.qps)
+        if agg is None:
+            info = {"kv_blocks": None, "graphs": [], "preemptions": None, "model": a.model,
+                    "kv_cache_dtype": "bf16", "isl": a.isl, "osl": a.osl}
+    if ctx.rank == 0:
+        print(json.dumps(build_line(a, ctx, mode, agg, dis, info)), flush=True)
     if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        ctx.dist.barrier()
+        ctx.dist.destroy_process_group()
+    return 0
+
+
+def build_line(a, ctx, mode, agg, dis, info) -> dict:
+    head = agg if agg is not None else dis
+    world = ctx.world
+    on_gpu = ctx.on_gpu
+    line = {
+        "metric": BASELINE_METRIC,
+        "value": head["value"],
+        "unit": "tok/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": head["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if on_gpu else "fp32",
+        "data": "synthetic (random prompt token ids, random-init weights, Poisson arrivals)",
+        "config": {"model": info["model"] if on_gpu else "tiny-llama (CPU plumbing run)",
+                   "global_batch": int(world * a.max_num_seqs), "seq_len": info["isl"] + info["osl"],
+                   "parallelism": f"dp{world}" if agg is not None else f"disagg {world // 2}P+{world // 2}D",
+                   "mode": mode, "isl": info["isl"], "osl": info["osl"],
+                   "qps_per_gpu": a.qps, "qps_node": a.qps * world, "kv_cache_dtype": info["kv_cache_dtype"],
+                   "shared_gpu": ctx.shared_gpu},
+    }
+    for k in ("ttft_p50_ms", "ttft_p90_ms", "itl_p50_ms", "itl_p90_ms", "requests_with_first_token",
+              "warmup_steps_executed", "warmup_s", "steady_state", "running_mean", "sla_isl4000_osl500"):
+        line[k] = head[k]
+    line["ttft_window"] = "steady state: post-warmup soak + timed steps"
+    if agg is not None and dis is not None:
+        line["agg"] = {k: agg[k] for k in ("value", "ttft_p50_ms", "itl_p50_ms", "ms_per_step")}
+    if dis is not None:
+        line["disagg"] = dis
+    line["engine"] = {"kv_blocks": info["kv_blocks"], "preemptions": info["preemptions"], "graphs": info["graphs"]}
+    return line
+
+
+def run_guarded(fn, timeout_s: float, ctx, **kw):
+    """Run a phase with a watchdog: if it has not returned by timeout_s (e.g. an IPC mapping that
+    never completes across GPUs), rank 0 prints the line it has, marking the phase failed, and
+    every rank exits instead of hanging the job."""
+    done = threading.Event()
+
+    def watchdog():
+        if done.wait(timeout_s):
+            return
+        if ctx.rank == 0 and kw.get("agg") is not None:
+            line = build_line(kw["a"], ctx, kw["mode"], kw["agg"], None, kw["agg_info"])
+            line["disagg"] = {"status": "failed", "error": f"phase did not finish within {timeout_s:.0f}s"}
+            print(json.dumps(line), flush=True)
+        print(f"bench.py rank {ctx.rank}: disagg phase timed out after {timeout_s:.0f}s", file=sys.stderr, flush=True)
+        os._exit(0 if kw.get("agg") is not None else 3)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        return fn()
+    except BaseException as e:  # noqa: BLE001 - one rank failing must not hang the others in a barrier
+        import traceback
+        traceback.print_exc()
+        if kw.get("agg") is None:
+            raise
+        if ctx.rank == 0:
+            line = build_line(kw["a"], ctx, kw["mode"], kw["agg"], None, kw["agg_info"])
+            line["disagg"] = {"status": "failed", "error": repr(e)[:300]}
+            print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+    finally:
+        done.set()
 
 
 if __name__ == "__main__":

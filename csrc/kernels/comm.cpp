@@ -155,7 +155,8 @@ void register_comm(pybind11::module_& m) {
         pybind11::arg("err_ptr"), pybind11::arg("two_shot") = false);
   m.def("ipc_all_to_all", &ipc_all_to_all);
   m.def("ipc_export_pool", &export_pool);
-  m.def("ipc_open_pool", &open_pool);
+  // may block on the peer driver: let watchdog threads run meanwhile
+  m.def("ipc_open_pool", &open_pool, pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("ipc_close_all", &close_all);
   m.def("copy_blocks", &copy_blocks);
 }

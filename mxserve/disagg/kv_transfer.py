@@ -165,6 +165,17 @@ class KVTransferAgent:
         if self.is_gpu:
             torch.cuda.synchronize(self.kv.device)
 
+    def close(self) -> None:
+        """Unmap every opened peer arena and drop the local one (bench phases rebuild engines)."""
+        if self._opened:
+            from .. import ops
+            if self._stream is not None:
+                self._stream.synchronize()
+            ops.ext().ipc_close_all()
+            self._opened.clear()
+        self.staging = None
+        self._desc = None
+
     # -------------------------------------------------------------- prefill side
     def _remote_ptr(self, target: dict) -> int:
         if target.get("pid") == os.getpid():  # same process: plain device pointer

@@ -197,6 +197,14 @@ class LLMEngine:
     def shutdown(self) -> None:
         self.runner.shutdown_followers()
 
+    def close(self) -> None:
+        """Drop every device allocation (graphs, KV pool, weights) so another engine can be built
+        in this process (bench phases)."""
+        self.shutdown()
+        self._inflight = None
+        self.requests.clear()
+        self.runner.close()
+
 
 class AsyncEngine:
     """Engine loop on a dedicated thread.  The asyncio side never takes a lock that the step holds:

@@ -66,11 +66,14 @@ class KVCacheManager:
         req.block_ids.extend(self.pool.allocate(need_blocks))
         return True
 
-    def cache_computed_blocks(self, req: Request) -> None:
-        """Register hashes of blocks whose tokens are all computed (becomes reusable by others)."""
+    def cache_computed_blocks(self, req: Request, upto: int | None = None) -> None:
+        """Register hashes of blocks whose tokens are all computed (becomes reusable by others).
+        `upto` caps the computed-token count: with async scheduling num_computed_tokens already
+        counts the step still in flight, whose KV is not written yet."""
         if not self.caching:
             return
-        full = req.num_computed_tokens // self.block_size
+        done = req.num_computed_tokens if upto is None else min(upto, req.num_computed_tokens)
+        full = done // self.block_size
         if full <= req.num_registered_blocks:
             return
         self._update_hashes(req)

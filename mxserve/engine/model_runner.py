@@ -363,8 +363,9 @@ class ModelRunner:
         tp = get_tp()
         if tp.tp_size > 1:
             self._steps += 1
-            if tp.custom_ar is not None and not tp.custom_ar.disabled and self._steps % 512 == 0 \
-                    and not tp.custom_ar.check():
+            # error words are host-mapped uncached memory: a few 4-byte reads, so check every step
+            # (a peer timeout surfaces within the steps still in flight, not 512 steps later)
+            if tp.custom_ar is not None and not tp.custom_ar.disabled and not tp.custom_ar.check():
                 meta["car_disable"] = True
                 self._disable_custom_ar()
             tp_broadcast_object(("step", self.buf.host_bytes(), meta))
@@ -437,6 +438,8 @@ class ModelRunner:
             _, host_bytes, meta = msg
             if meta.get("car_disable"):
                 self._disable_custom_ar()
+            # the previous step's non_blocking H2D copy may still be reading the pinned buffer
+            self.buf.wait_free()
             self.buf.load_host_bytes(host_bytes)
             self.execute_host(meta)
 
@@ -557,6 +560,14 @@ class ModelRunner:
         log.info("captured %d decode graphs (%s) in %.1fs", len(buckets), buckets, time.time() - t0)
 
     # ------------------------------------------------------------------ misc
+    def close(self) -> None:
+        if self.is_gpu:
+            torch.cuda.synchronize(self.device)
+        self.graphs.clear()
+        self._logits = None
+        for name in ("kv_cache", "model", "bt_dev", "last_tok", "hist", "_pen_counts", "buf"):
+            setattr(self, name, None)
+
     def kv_stats(self) -> dict:
         return {"num_blocks": self.num_blocks, "block_bytes": self.block_bytes,
                 "kv_bytes": self.num_blocks * self.block_bytes}

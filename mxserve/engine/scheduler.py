@@ -84,9 +84,17 @@ class Scheduler:
         return bool(self.waiting or self.running)
 
     # ------------------------------------------------------------------ disaggregation (decode side)
+    def num_slots_used(self) -> int:
+        """Batch rows held: running requests plus remote-prefill reservations (each becomes a
+        running request when its KV lands, so both count against max_num_seqs)."""
+        return len(self.running) + len(self.remote)
+
     def reserve_remote(self, req: Request) -> bool:
         """Allocate KV blocks for the whole prompt of a request whose prefill runs remotely.
-        Locally cached prefix blocks are reused (only the rest must be transferred)."""
+        Locally cached prefix blocks are reused (only the rest must be transferred).  Refused
+        (False) when the batch is full: the model runner has max_num_seqs rows."""
+        if self.num_slots_used() >= self.max_num_seqs:
+            return False
         req.num_cached_tokens = self.kv.get_computed_blocks(req)
         req.num_computed_tokens = req.num_cached_tokens
         if not self.kv.allocate_slots(req, req.num_prompt_tokens - req.num_computed_tokens):
@@ -163,7 +171,7 @@ class Scheduler:
             budget -= n
             i += 1
 
-        while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs and not out.preempted:
+        while self.waiting and budget > 0 and self.num_slots_used() < self.max_num_seqs and not out.preempted:
             req = self.waiting[0]
             if req.num_pending:  # preempted with a sample still in flight: wait for it
                 break
@@ -208,9 +216,10 @@ class Scheduler:
             req = s.req
             if req.is_finished:  # aborted / finished while this step was in flight
                 continue
+            landed = s.start + s.num_new_tokens  # KV written by THIS step (not the one in flight)
             if not s.sample:
-                if min(req.num_computed_tokens, req.num_known_tokens) // bs > req.num_registered_blocks:
-                    self.kv.cache_computed_blocks(req)
+                if min(landed, req.num_known_tokens) // bs > req.num_registered_blocks:
+                    self.kv.cache_computed_blocks(req, landed)
                 continue
             req.num_pending -= 1
             tok = sampled.get(req.request_id)
@@ -219,8 +228,8 @@ class Scheduler:
             req.output_token_ids.append(int(tok))
             if req.first_token_time is None:
                 req.first_token_time = now
-            if min(req.num_computed_tokens, req.num_known_tokens) // bs > req.num_registered_blocks:
-                self.kv.cache_computed_blocks(req)
+            if min(landed, req.num_known_tokens) // bs > req.num_registered_blocks:
+                self.kv.cache_computed_blocks(req, landed)
             st = req.check_stop(self.max_model_len)
             if req.disagg_role == "prefill_only" and st is None:
                 st = Status.FINISHED_LENGTH

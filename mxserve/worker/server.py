@@ -145,6 +145,7 @@ class Worker:
         target["skip_blocks"] = skip
         target["arena_start"] = start
         payload = {"request_id": rid, "token_ids": toks, "sampling": _sp_dict(sp), "kv_target": target}
+        completed = False
         try:
             sess = await self.http()
             async with sess.post(purl.rstrip("/") + "/prefill", json=payload) as r:
@@ -158,7 +159,7 @@ class Worker:
                 return self.engine.complete_remote_prefill(rid, tok, res.get("logprob"), res.get("top_logprobs"))
 
             out = await self.aeng.submit(land_and_complete, int(res["first_token"]))
-            start = None
+            completed = True  # the landing copy now owns (and recycles) the extent
             self.aeng.push(out)
             if "transfer_s" in res:
                 self.metrics.kv_xfer_lat.labels(self.model).observe(float(res["transfer_s"]))
@@ -167,11 +168,16 @@ class Worker:
             return q
         except Exception as e:  # noqa: BLE001 - SURVEY §5.3: fall back to local prefill
             log.warning("remote prefill failed for %s (%r); prefilling locally", rid, e)
-            if start is not None:
-                self.agent.release(start, len(dst))
-            await self.aeng.submit(self.engine.abort, rid)
-            self.aeng._queues.pop(rid, None)
             return None
+        finally:
+            # any non-completion -- an error above, or the client/frontend going away mid-POST
+            # (CancelledError is a BaseException): give back the arena extent, the reserved KV
+            # blocks and the token queue, or they leak until every reservation fails
+            if not completed:
+                if start is not None:
+                    self.agent.release(start, len(dst))
+                self.aeng.submit_nowait(self.engine.abort, rid)
+                self.aeng._queues.pop(rid, None)
 
     async def _prefill(self, body: dict) -> dict:
         """Prefill side: compute, push KV into the decode worker's pool, return the first token."""

@@ -359,3 +359,48 @@ def test_mid_stream_migration_keeps_greedy_output():
         fs.stop()
         a.aeng.shutdown()
         b.aeng.shutdown()
+
+
+def test_remote_prefill_cancel_releases_reservation():
+    """A client that goes away while the decode worker awaits the prefill POST (CancelledError)
+    must not leak the reserved KV blocks, the remote slot or the token queue."""
+    import asyncio
+    import socket
+    import threading
+    import time
+
+    lst = socket.socket()
+    lst.bind(("127.0.0.1", 0))
+    lst.listen(4)
+    held = []
+    threading.Thread(target=lambda: held.append(lst.accept()), daemon=True).start()  # accepts, never answers
+    w, _ = _worker(None, role="decode")
+    eng = w.engine
+    free0 = eng.kv.num_free()
+
+    async def go():
+        from mxserve.engine.request import SamplingParams
+        t = asyncio.ensure_future(w._remote_prefill("rq", list(range(40)), SamplingParams(max_tokens=4),
+                                                   f"http://127.0.0.1:{lst.getsockname()[1]}"))
+        for _ in range(200):
+            await asyncio.sleep(0.01)
+            if held:
+                break
+        assert "rq" in eng.scheduler.remote and eng.kv.num_free() < free0
+        t.cancel()
+        with pytest.raises(asyncio.CancelledError):
+            await t
+        if w._http is not None:
+            await w._http.close()
+
+    try:
+        asyncio.run(go())
+        for _ in range(200):  # the abort runs on the engine thread
+            if not eng.scheduler.remote and eng.kv.num_free() == free0:
+                break
+            time.sleep(0.01)
+        assert not eng.scheduler.remote and eng.kv.num_free() == free0
+        assert "rq" not in w.aeng._queues and "rq" not in eng.requests
+    finally:
+        w.aeng.shutdown()
+        lst.close()

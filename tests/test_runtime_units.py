@@ -170,6 +170,43 @@ def test_remote_prefill_reserve_and_complete():
     assert done and done[0].output_token_ids[0] == 11 and kv.num_free() == 32
 
 
+def test_remote_reservations_count_against_max_num_seqs():
+    """A decode worker never holds more than max_num_seqs requests (running + remote-prefill
+    reservations): the model runner has max_num_seqs rows."""
+    kv = KVCacheManager(256, 16)
+    s = Scheduler(kv, max_num_seqs=4, max_model_len=1024)
+    reqs = [_req(f"d{i}", 40, max_tokens=3) for i in range(6)]
+    ok = [s.reserve_remote(r) for r in reqs]
+    assert ok == [True] * 4 + [False] * 2
+    assert kv.num_free() == 256 - 4 * 3  # refused reservations hold no blocks
+    for r in reqs[:4]:
+        s.complete_remote(r.request_id, 7)
+    assert len(s.running) == 4
+    # local admissions respect the cap too, while reservations are outstanding
+    s2 = Scheduler(KVCacheManager(256, 16), max_num_seqs=3, max_model_len=1024)
+    assert s2.reserve_remote(_req("x", 40)) and s2.reserve_remote(_req("y", 40))
+    for i in range(3):
+        s2.add(_req(f"w{i}", 20))
+    out = s2.schedule()
+    assert len(out.prefills) == 1 and len(s2.waiting) == 2
+
+
+def test_prefix_registration_stops_at_landed_step():
+    """With async scheduling num_computed_tokens already counts the step in flight; landing step N
+    must only register blocks whose KV step N wrote."""
+    kv = KVCacheManager(64, 16)
+    s = Scheduler(kv, max_num_batched_tokens=32, max_model_len=1024)
+    s.add(_req("a", 64, max_tokens=2))
+    o1 = s.schedule()  # tokens [0, 32)
+    o2 = s.schedule()  # tokens [32, 64) scheduled before step 1 lands
+    r = o1.prefills[0].req
+    assert r.num_computed_tokens == 64
+    s.update(o1, {})
+    assert r.num_registered_blocks == 2  # not 4: step 2's KV is not written yet
+    s.update(o2, {"a": 5})
+    assert r.num_registered_blocks == 4
+
+
 # ----------------------------------------------------------------------------- router
 def test_kv_router_prefers_cached_worker():
     from mxserve.router.router import Registry, Router, WorkerInfo

@@ -150,28 +150,43 @@ def test_run_benchmarks_sh(local_frontend, tmp_path):
     assert (tmp_path / "plots" / "summary.md").exists()
 
 
-@pytest.mark.parametrize("mode,nproc", [("agg", 1), ("agg", 2), ("disagg", 2)])
-def test_bench_contract_cpu(mode, nproc, tmp_path):
-    """bench.py prints exactly one JSON line with the driver's contract fields (CPU plumbing run;
-    world 2 goes through torch.distributed.run like the driver's multi-GPU launch)."""
+@pytest.mark.parametrize("mode,nproc,launcher", [("agg", 1, "self"), ("auto", 2, "self"), ("disagg", 2, "torchrun")])
+def test_bench_contract_cpu(mode, nproc, launcher, tmp_path):
+    """bench.py prints exactly one JSON line with the driver's contract fields (CPU plumbing run).
+    `--gpus N` alone spawns the N ranks itself; under torch.distributed.run (the driver's multi-GPU
+    launch) WORLD_SIZE must match.  N >= 2 in auto mode reports agg and disagg in the one line."""
     import json
     import socket
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "12", "--warmup", "8", "--qps", "20",
-           "--mode", mode, "--device", "cpu"]
-    if nproc > 1:
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "12", "--warmup", "8", "--qps", "8",
+           "--mode", mode, "--device", "cpu", "--gpus", str(nproc), "--max-warmup-s", "8",
+           "--steady-window-s", "1", "--min-ttft-samples", "5"]
+    if launcher == "torchrun":
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-               "--master-addr", "127.0.0.1", "--master-port", str(port)] + cmd[1:] + ["--gpus", str(nproc)]
+               "--master-addr", "127.0.0.1", "--master-port", str(port)] + cmd[1:]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
-                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+                       env=dict(env, OMP_NUM_THREADS="1"))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
-              "vs_baseline", "dtype", "data", "config"):
+              "vs_baseline", "dtype", "data", "config", "ttft_p50_ms", "requests_with_first_token", "steady_state"):
         assert k in d, k
     assert d["n_gpus"] == nproc and d["steps"] == 12 and d["warmup"] == 8 and d["value"] > 0
-    assert d["config"]["mode"] == mode
+    assert d["requests_with_first_token"] >= 5
+    want = {"auto": "agg" if nproc == 1 else "both"}.get(mode, mode)
+    assert d["config"]["mode"] == want
+    if want == "both":
+        assert d["agg"]["value"] == d["value"] and d["disagg"]["value"] > 0
+        assert d["disagg"]["parallelism"] == "disagg 1P+1D"
+
+
+def test_bench_rejects_world_mismatch(tmp_path):
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu"],
+                       capture_output=True, text=True, timeout=120, cwd=str(tmp_path), env=env)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
