@@ -144,8 +144,8 @@ def _attend(q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, q_pos0: int, scal
     Kf = K.float().repeat_interleave(g, dim=1)  # [n, Hq, D]
     Vf = V.float().repeat_interleave(g, dim=1)
     s = torch.einsum("mhd,nhd->hmn", q.float(), Kf) * scale
-    qpos = torch.arange(m).unsqueeze(1) + q_pos0
-    kpos = torch.arange(n).unsqueeze(0)
+    qpos = torch.arange(m, device=q.device).unsqueeze(1) + q_pos0
+    kpos = torch.arange(n, device=q.device).unsqueeze(0)
     s = s.masked_fill((kpos > qpos).unsqueeze(0), float("-inf"))
     p = torch.softmax(s, dim=-1)
     return torch.einsum("hmn,nhd->mhd", p, Vf)

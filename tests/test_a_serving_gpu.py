@@ -22,7 +22,8 @@ MODEL = "small-llama"
 
 
 def _worker(role: str, fe_url: str, port: int, log):
-    cmd = [sys.executable, "-m", "dynamo.vllm", "--model", MODEL, f"--is-{role}-worker", "--frontend-url", fe_url,
+    flag = [] if role == "agg" else [f"--is-{role}-worker"]
+    cmd = [sys.executable, "-m", "dynamo.vllm", "--model", MODEL] + flag + ["--frontend-url", fe_url,
            "--host", "127.0.0.1", "--port", str(port), "--num-gpu-blocks-override", "4096", "--max-model-len",
            "4096", "--max-num-seqs", "16", "--enforce-eager", "--worker-id", f"{role}-0"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MXS_KV_STAGING_BYTES=str(1 << 30),
@@ -38,15 +39,17 @@ def test_disaggregated_chat_over_ipc(tmp_path):
         pytest.skip("HIP already initialised in the test process; run this file on its own")
     fe = Frontend(router_mode="kv", ttl=60)
     fs = Server(fe.app).start()
-    logs = {r: open(tmp_path / f"{r}.log", "w") for r in ("prefill", "decode")}
+    fe_agg = Frontend(router_mode="kv", ttl=60)  # an aggregated worker (same seed) for greedy parity
+    fs_agg = Server(fe_agg.app).start()
+    logs = {r: open(tmp_path / f"{r}.log", "w") for r in ("prefill", "decode", "agg")}
     ports = {r: free_port() for r in logs}
-    procs = {r: _worker(r, fs.url, ports[r], logs[r]) for r in logs}
+    procs = {r: _worker(r, fs_agg.url if r == "agg" else fs.url, ports[r], logs[r]) for r in logs}
     try:
         def ready():
             for r, p in procs.items():
                 if p.poll() is not None:
                     raise RuntimeError(f"{r} worker exited:\n" + (tmp_path / f"{r}.log").read_text()[-4000:])
-            return len(fe.registry.list()) == 2
+            return len(fe.registry.list()) == 2 and len(fe_agg.registry.list()) == 1
         wait_for(ready, timeout=240, interval=1.0)
         body = {"model": MODEL, "messages": [{"role": "user", "content": "disaggregated " * 40}], "max_tokens": 24,
                 "temperature": 0, "ignore_eos": True}
@@ -59,6 +62,11 @@ def test_disaggregated_chat_over_ipc(tmp_path):
         moved = [ln for ln in m.splitlines()
                  if ln.startswith("dynamo_component_kv_transfer_bytes_total") and 'backend="xgmi"' in ln]
         assert moved and float(moved[0].split()[-1]) > 0, m[-2000:]
+        # greedy parity: the disaggregated answer (prefill GPU -> KV over IPC -> decode) is token for
+        # token the aggregated one
+        ra = httpx.post(fs_agg.url + "/v1/chat/completions", json=body, timeout=120)
+        assert ra.status_code == 200, ra.text
+        assert ra.json()["choices"][0]["message"]["content"] == d["choices"][0]["message"]["content"]
         # streaming through the same path, several requests at once
         t0 = time.time()
         outs = []
@@ -77,5 +85,6 @@ def test_disaggregated_chat_over_ipc(tmp_path):
                 p.kill()
                 p.wait()
         fs.stop()
+        fs_agg.stop()
         for f in logs.values():
             f.close()

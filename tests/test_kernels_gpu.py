@@ -526,3 +526,45 @@ def test_moe_experts_uses_grouped_kernel(gpu, monkeypatch):
     assert not called and out is not None
     exp = ref.moe_experts(x.cpu(), w13.cpu(), w2.cpu(), tw.cpu(), tid.cpu(), 2)
     _close(out, exp, 0.02, 0.03, "moe ep")
+
+
+# ---- serving shapes: the bench runs 4000-token prompts in chunks of up to 8192 tokens and decodes up
+# to max_model_len 8192; the fp32 reference runs on the GPU at these sizes
+@pytest.mark.parametrize("D,G,hkv", [(64, 4, 2), (128, 4, 1)])
+def test_paged_prefill_serving_shape(gpu, D, G, hkv):
+    """A 4k cached prefix + an 8k chunk, next to a fresh 1k prompt and a 1-token tail."""
+    specs = [(4096, 8192), (0, 1000), (777, 1)]
+    seq_lens = [c + n for c, n in specs]
+    kv, bt = _paged_setup(seq_lens, hkv, D, device=gpu)
+    qsl = [0]
+    for _, n in specs:
+        qsl.append(qsl[-1] + n)
+    q = torch.randn(qsl[-1], hkv * G, D, device=gpu, dtype=torch.bfloat16)
+    qsl_t = torch.tensor(qsl, dtype=torch.int32)
+    sl = torch.tensor(seq_lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    out = ops.paged_attention_prefill(q, kv[:, 1], bt.to(gpu), qsl_t.to(gpu), sl.to(gpu), scale,
+                                      max(n for _, n in specs))
+    exp = ref.paged_attention(q, kv[:, 1], bt.to(gpu), qsl_t, sl, scale)
+    _close(out, exp, 0.03, 0.03, "prefill 4k+8k")
+
+
+@pytest.mark.parametrize("impl", [1, 2])
+@pytest.mark.parametrize("kv_dtype", ["bf16", "fp8"])
+@pytest.mark.parametrize("D,G", [(64, 4), (128, 4), (128, 8)])
+def test_paged_decode_max_model_len(gpu, D, G, kv_dtype, impl):
+    """Contexts up to max_model_len 8192, launched as the decode graphs launch them."""
+    hkv, lens = 2, [8192, 8191, 4097, 1, 5000, 16, 6001, 8177]
+    kv, bt = _paged_setup(lens, hkv, D, device=gpu)
+    ks = vs = 1.0
+    if kv_dtype == "fp8":
+        ks, vs = 0.02, 0.05
+        kv = _fp8_cache(kv * (ks * 4), ks)
+    q = torch.randn(len(lens), hkv * G, D, device=gpu, dtype=torch.bfloat16)
+    sl = torch.tensor(lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    out = ops.paged_attention_decode(q, kv[:, 1], bt.to(gpu), sl.to(gpu), scale, 8192, k_scale=ks, v_scale=vs,
+                                     impl=impl)
+    exp = ref.paged_attention_decode(q, kv[:, 1], bt.to(gpu), sl, scale, ks, vs)
+    tol = 0.02 * max(1.0, exp.abs().max().item()) if kv_dtype == "fp8" else 0.02
+    _close(out, exp, tol, 0.02, f"decode 8k {kv_dtype}")

@@ -108,3 +108,42 @@ def test_engine_greedy_matches_hf_generate():
             g = hf.generate(torch.tensor([p]), max_new_tokens=8, do_sample=False, eos_token_id=None,
                             pad_token_id=0)[0, len(p):].tolist()
         assert o == g
+
+
+@pytest.mark.parametrize("name,tp", [("tiny-llama", 2), ("tiny-llama", 4), ("tiny-qwen3", 2), ("tiny-mixtral", 2)])
+def test_sharded_safetensors_load_matches_full_load(name, tp, tmp_path):
+    """The shard-aware loader reads only this rank's slices from HF safetensors files (no full
+    tensor on the host) and produces exactly what load_full_state keeps after sharding."""
+    from safetensors.torch import save_file
+
+    from mxserve.models.weights import load_sharded_safetensors
+    from mxserve.parallel.comm import ParallelState, get_tp, set_tp
+    cfg = get_model_config(name)
+    sd = {k: v.float().contiguous() for k, v in _hf_state(_hf_model(cfg), cfg).items()}
+    if cfg.tie_word_embeddings:
+        sd.pop("lm_head.weight", None)
+    keys = sorted(sd)  # two files, like a real multi-shard checkpoint
+    save_file({k: sd[k] for k in keys[::2]}, str(tmp_path / "model-00001-of-00002.safetensors"))
+    save_file({k: sd[k] for k in keys[1::2]}, str(tmp_path / "model-00002-of-00002.safetensors"))
+    total = sum(v.numel() * 4 for v in sd.values())
+    prev = get_tp()
+    try:
+        read = 0
+        for rank in range(tp):
+            set_tp(ParallelState(tp_rank=rank, tp_size=tp))
+            full = TransformerLM(cfg, "cpu", torch.float32)
+            full.load_full_state(hf_to_internal(cfg, sd))
+            part = TransformerLM(cfg, "cpu", torch.float32)
+            n = load_sharded_safetensors(part, str(tmp_path))
+            read += n
+            assert set(part.w) == set(full.w)
+            for k in full.w:
+                assert torch.equal(part.w[k], full.w[k]), (rank, k)
+        # replicated tensors (embedding, norms, router) are read by every rank; the rest once in total
+        # (k/v projections are read once per KV-head replica when tp > num_kv_heads)
+        repl = sum(v.numel() * 4 for k, v in sd.items() if "norm" in k or "embed" in k or k.endswith("gate.weight"))
+        kv = sum(v.numel() * 4 for k, v in sd.items() if k.endswith(("k_proj.weight", "v_proj.weight")))
+        kv_copies = max(1, tp // cfg.num_kv_heads)
+        assert read <= total - repl - kv + tp * repl + kv_copies * kv + 1024
+    finally:
+        set_tp(prev)
