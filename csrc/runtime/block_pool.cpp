@@ -5,6 +5,8 @@
 //                    workers compute byte-identical hashes so KV events line up.
 //   * KvIndexer    - router-side index block-hash -> set of workers holding it, answering
 //                    "longest cached prefix per worker" for KV-aware routing.
+//   * ShmRing      - /dev/shm ring that carries each step's inputs from TP rank 0 to the other
+//                    ranks (shm_ring.cpp).
 // Upstream Dynamo keeps these in Rust (dynamo-llm kv_router indexer) and vLLM keeps the block pool
 // in Python; SURVEY.md §2.3 N05 and §7.4 item 7 size them for ~0.5 M blocks x 8 workers, which is
 // why they are C++ here.
@@ -14,11 +16,15 @@
 #include "kv_runtime.h"
 
 namespace py = pybind11;
+namespace mxs_rt {
+void register_shm_ring(py::module_& m);  // shm_ring.cpp
+}
 using mxs_rt::BlockPool;
 using mxs_rt::KvIndexer;
 
 PYBIND11_MODULE(_rt, m) {
-  m.doc() = "mxserve native host runtime: block pool, block hashing, KV indexer";
+  m.doc() = "mxserve native host runtime: block pool, block hashing, KV indexer, shared-memory ring";
+  mxs_rt::register_shm_ring(m);
   m.def("block_hashes", &mxs_rt::block_hashes, py::arg("tokens"), py::arg("block_size"), py::arg("extra") = 0,
         py::arg("parent") = 0, "Chained hashes of the full blocks of `tokens`.");
   py::class_<BlockPool>(m, "BlockPool")

@@ -45,9 +45,12 @@ watch_args='[]'
 [[ "$NAMESPACE_RESTRICTED_OPERATOR" == "true" ]] && watch_args="[\"--namespace\", \"${NAMESPACE}\"]"
 sed -e "s#IMAGE_PLACEHOLDER#${MXS_IMAGE}#g" -e "s#NAMESPACE_PLACEHOLDER#${NAMESPACE}#g" \
     -e "s#WATCH_ARGS_PLACEHOLDER#${watch_args}#" -e "s#GPU_RESOURCE_PLACEHOLDER#${GPU_RESOURCE}#" \
+    -e "s#PROMETHEUS_ENDPOINT_PLACEHOLDER#${PROMETHEUS_ENDPOINT}#" \
     "$HERE/deploy/operator/operator.yaml" | kubectl apply -n "$NAMESPACE" -f -
 kubectl -n "$NAMESPACE" rollout status deploy/mxserve-operator --timeout=600s
-say "metrics: workers expose /metrics via PodMonitors; Prometheus at ${PROMETHEUS_ENDPOINT}"
+# the operator hands PROMETHEUS_ENDPOINT to the SLA planners it runs (reference: prometheusEndpoint
+# Helm value of the platform chart); workers and frontends are scraped through PodMonitors
+say "metrics: PodMonitors per DGD; planners query Prometheus at ${PROMETHEUS_ENDPOINT}"
 
 case "$GPU_OPERATOR_MODE" in
   operator)
@@ -57,6 +60,10 @@ case "$GPU_OPERATOR_MODE" in
     helm repo update >/dev/null
     helm upgrade --install "$GPU_OPERATOR_RELEASE" "$AMD_HELM_REPO_NAME/gpu-operator-charts" \
       -n "$GPU_OPERATOR_NS" --create-namespace --wait --timeout "$GPU_OPERATOR_HELM_TIMEOUT"
+    say "DeviceConfig: device plugin + node labeller + device-metrics-exporter (ServiceMonitor)"
+    for f in metrics-exporter-config.yaml deviceconfig.yaml; do
+      sed -e "s#GPU_OPERATOR_NS_PLACEHOLDER#${GPU_OPERATOR_NS}#g" "$HERE/deploy/amd-gpu/$f" | kubectl apply -f -
+    done
     ;;
   device-plugin)
     say "ROCm k8s-device-plugin DaemonSet"

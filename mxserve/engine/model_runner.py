@@ -27,7 +27,7 @@ from ..config import EngineArgs
 from ..models.config import ModelConfig
 from ..models.llama import AttnMetadata, build_model
 from ..models.weights import load_weights
-from ..parallel.comm import get_tp, tp_broadcast_object
+from ..parallel.comm import collectives_capturable, get_tp, setup_meta_ring, tp_broadcast_object
 from .scheduler import SchedulerOutput
 
 log = logging.getLogger(__name__)
@@ -155,6 +155,9 @@ class ModelRunner:
         self.buf = InputBuffers(self.max_tokens_per_step, n_rows,
                                 self.max_tokens_per_step // self.bs + 4 * self.max_blocks_per_seq + n_rows,
                                 self.device, pin=self.is_gpu)
+        # per-step inputs to the other TP ranks: the InputBuffers image + meta through a /dev/shm ring
+        if get_tp().tp_size > 1:
+            setup_meta_ring(self.buf.nbytes + (4 << 20))
         # sampled ids come back through two alternating pinned buffers (step N's result is read
         # while step N+1, launched just before, may already be writing the other one)
         self._out_slot = 0
@@ -523,7 +526,14 @@ class ModelRunner:
 
     def _capture_graphs(self) -> None:
         maxb = min(self.args.cuda_graph_max_bs, self.args.max_num_seqs)
-        buckets = _graph_buckets(maxb)
+        m = self.model
+        # largest collective message of a decode step at batch b: the all-reduces of [b, H] and the
+        # logits all-gather ([b, vocab/tp] per rank)
+        msg = lambda b: b * max(self.cfg.hidden_size, m.vocab_local) * 2  # noqa: E731
+        buckets = [b for b in _graph_buckets(maxb) if collectives_capturable(msg(b))]
+        if not buckets:
+            log.warning("no decode bucket has graph-capturable collectives; decode runs eagerly")
+            return
         self._arange = torch.arange(max(buckets), dtype=torch.int64, device=self.device)
         # benign contents for capture: every row is a 1-token sequence that writes nowhere
         h = self.buf.hn

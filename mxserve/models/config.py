@@ -194,6 +194,12 @@ def find_local_model_dir(name: str) -> Optional[str]:
 
 
 def get_model_config(name: str) -> ModelConfig:
+    """`name@layers=N` keeps a model's real shapes with only its first N layers (tests and probes of
+    big models on one GPU, e.g. Llama-3-70B TP=8 with 8 ranks sharing the test box's GPU)."""
+    if "@layers=" in name:
+        base, n = name.split("@layers=", 1)
+        cfg = get_model_config(base)
+        return dataclasses.replace(cfg, num_layers=int(n), name=name)
     local = find_local_model_dir(name)
     if local is not None:
         with open(os.path.join(local, "config.json")) as f:

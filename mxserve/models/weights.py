@@ -16,16 +16,17 @@ from .config import ModelConfig, find_local_model_dir
 
 
 def random_full_state(cfg: ModelConfig, seed: int = 0, std: float = 0.02,
-                      dtype: torch.dtype = torch.float32) -> dict[str, torch.Tensor]:
-    """Unsharded random weights on the host in our naming (small models / tests only)."""
-    g = torch.Generator().manual_seed(seed)
+                      dtype: torch.dtype = torch.float32, device="cpu") -> dict[str, torch.Tensor]:
+    """Unsharded random weights in our naming (small models / tests; device="cuda" generates big
+    shapes on the GPU, identically in every process with the same seed)."""
+    g = torch.Generator(device=device).manual_seed(seed)
     H, D, I = cfg.hidden_size, cfg.head_dim, cfg.intermediate_size
 
     def rnd(*shape):
-        return (torch.randn(*shape, generator=g) * std).to(dtype)
+        return (torch.randn(*shape, generator=g, device=device) * std).to(dtype)
 
     def norm(n):
-        return (1.0 + 0.1 * torch.randn(n, generator=g)).to(dtype)
+        return (1.0 + 0.1 * torch.randn(n, generator=g, device=device)).to(dtype)
 
     sd = {"embed": rnd(cfg.vocab_size, H), "norm": norm(H)}
     if not cfg.tie_word_embeddings:

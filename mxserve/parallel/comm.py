@@ -22,6 +22,7 @@ class ParallelState:
     group: Optional[object] = None
     custom_ar: Optional[object] = None  # CustomAllReduce when enabled
     cpu_group: Optional[object] = None  # gloo group for host-side metadata
+    meta_ring: Optional[object] = None  # MetaRing: per-step metadata over /dev/shm
 
     @property
     def is_first(self) -> bool:
@@ -61,11 +62,12 @@ def init_distributed(tp_size: int, backend: Optional[str] = None, device: Option
     st = ParallelState(tp_rank=dist.get_rank(), tp_size=world, group=dist.group.WORLD)
     # scheduler metadata goes rank0 -> TP ranks over a CPU (gloo) group, never a GPU collective
     st.cpu_group = dist.new_group(backend="gloo") if backend != "gloo" else st.group
-    # custom IPC all-reduce: validated between processes sharing one GPU (tests/test_custom_ar_gpu.py,
-    # tests/test_tp_gpu.py, where the ranks' group is gloo); opt-in until it has run across a real
-    # xGMI mesh
+    # custom IPC all-reduce (one-shot / two-shot over peer-mapped buffers, bounded spins, RCCL
+    # fallback on a peer timeout): on by default for TP <= 8 (its rank limit); validated with 2-8
+    # ranks sharing one GPU (tests/test_custom_ar_gpu.py, tests/test_b_tp_gpu.py); MXS_CUSTOM_AR=0
+    # keeps every all-reduce on RCCL
     on_gpu = backend == "nccl" or (device is not None and torch.device(device).type == "cuda")
-    if enable_custom_ar and on_gpu and os.environ.get("MXS_CUSTOM_AR", "0") == "1":
+    if enable_custom_ar and on_gpu and os.environ.get("MXS_CUSTOM_AR", "1" if world <= 8 else "0") == "1":
         try:
             from .custom_allreduce import CustomAllReduce
             st.custom_ar = CustomAllReduce.create(st.group, device, cpu_group=st.cpu_group)
@@ -90,15 +92,126 @@ def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
     st = _STATE
     if st.tp_size == 1:
         return x
+    car = st.custom_ar
+    if car is not None and x.is_cuda and dim in (-1, x.dim() - 1):
+        # every rank pushes its shard to every peer through the IPC all-to-all (one xGMI hop per
+        # link, graph-capturable whatever the process group's backend)
+        rep = x.contiguous().unsqueeze(0).expand(st.tp_size, *x.shape).contiguous()
+        if car.can_all_to_all(rep):
+            out = torch.empty_like(rep)
+            car.all_to_all(out, rep)  # out[r] = rank r's shard
+            return out.movedim(0, -2).reshape(*x.shape[:-1], st.tp_size * x.shape[-1])
     parts = [torch.empty_like(x) for _ in range(st.tp_size)]
     dist.all_gather(parts, x.contiguous(), group=st.group)
     return torch.cat(parts, dim=dim)
+
+
+class MetaRing:
+    """Per-step scheduler metadata rank 0 -> TP ranks through the native /dev/shm ring
+    (csrc/runtime/shm_ring.cpp) instead of a pickled gloo broadcast per step.
+    A message larger than a slot, or a node without usable /dev/shm, goes over gloo."""
+
+    _GLOO = b"\x00mxs-gloo"
+
+    def __init__(self, ring, rank: int):
+        self.ring, self.rank = ring, rank
+        self.steps = 0
+        self.gloo_fallbacks = 0
+
+    def send(self, obj) -> None:
+        import pickle
+        data = pickle.dumps(obj, protocol=5)
+        self.steps += 1
+        if len(data) > self.ring.slot_bytes:
+            self.gloo_fallbacks += 1
+            self._push(self._GLOO)
+            _gloo_broadcast(obj)
+            return
+        self._push(data)
+
+    def _push(self, data: bytes) -> None:
+        while not self.ring.push(data, 10.0):  # a follower is still busy with an old step
+            import logging
+            logging.getLogger(__name__).warning("TP metadata ring full for 10 s; waiting for followers")
+
+    def recv(self):
+        import pickle
+        ppid = os.getppid()
+        while True:
+            data = self.ring.pop(self.rank - 1, 1.0)
+            if data is not None:
+                break
+            if os.getppid() != ppid:  # the driver rank (our parent) is gone
+                return ("shutdown", None, None)
+        self.steps += 1
+        if data == self._GLOO:
+            return _gloo_broadcast(None)
+        return pickle.loads(data)
+
+
+def setup_meta_ring(slot_bytes: int, nslots: int = 2) -> Optional[MetaRing]:
+    """Collective over the TP group's CPU group: rank 0 creates the ring, every rank attaches, then
+    the name is unlinked (nothing stays in /dev/shm whatever happens to the processes later)."""
+    st = _STATE
+    if st.tp_size == 1 or os.environ.get("MXS_TP_META_RING", "1") != "1":
+        return None
+    from .. import _native
+    rt = _native.rt()
+    name = None
+    ring = None
+    if st.tp_rank == 0:
+        name = f"/mxs-tp-{os.getpid()}-{int.from_bytes(os.urandom(4), 'little'):08x}"
+        try:
+            ring = rt.ShmRing(name, True, int(slot_bytes), int(nslots), st.tp_size - 1)
+        except Exception as e:  # noqa: BLE001 - no /dev/shm (or too small): stay on gloo
+            import logging
+            logging.getLogger(__name__).warning("TP metadata ring unavailable (%r); using gloo", e)
+            name = None
+    name = _gloo_broadcast(name)
+    ok = 1
+    if name is not None and st.tp_rank > 0:
+        try:
+            ring = rt.ShmRing(name, False)
+        except Exception:  # noqa: BLE001
+            ok = 0
+    t = torch.tensor([ok], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=st.cpu_group or st.group)
+    if st.tp_rank == 0 and ring is not None:
+        ring.unlink()
+    if name is None or not int(t.item()):
+        st.meta_ring = None
+        return None
+    st.meta_ring = MetaRing(ring, st.tp_rank)
+    return st.meta_ring
+
+
+def _gloo_broadcast(obj, src: int = 0):
+    st = _STATE
+    box = [obj]
+    dist.broadcast_object_list(box, src=src, group=st.cpu_group or st.group)
+    return box[0]
+
+
+def collectives_capturable(max_message_bytes: int) -> bool:
+    """Can a hipGraph capture this group's collectives for messages up to max_message_bytes?  RCCL
+    is capturable; a gloo group (ranks sharing a GPU in functional runs) only through the custom
+    IPC kernels, within their slot size."""
+    st = _STATE
+    if st.tp_size == 1:
+        return True
+    if dist.get_backend(st.group) == "nccl":
+        return True
+    car = st.custom_ar
+    return car is not None and not car.disabled and max_message_bytes <= car.max_bytes
 
 
 def tp_broadcast_object(obj, src: int = 0):
     st = _STATE
     if st.tp_size == 1:
         return obj
-    box = [obj]
-    dist.broadcast_object_list(box, src=src, group=st.cpu_group or st.group)
-    return box[0]
+    if st.meta_ring is not None and src == 0:
+        if st.tp_rank == 0:
+            st.meta_ring.send(obj)
+            return obj
+        return st.meta_ring.recv()
+    return _gloo_broadcast(obj, src)

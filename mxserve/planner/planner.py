@@ -20,6 +20,7 @@ reconciles the Deployments.  `--dry-run` only logs.
 from __future__ import annotations
 
 import argparse
+import os
 import logging
 import math
 import re
@@ -207,12 +208,41 @@ def http_scraper(url: str) -> Callable[[], dict[str, float]]:
     return scrape
 
 
+PLANNER_METRICS = ("dynamo_frontend_requests_total", "dynamo_frontend_input_sequence_tokens_count",
+                   "dynamo_frontend_input_sequence_tokens_sum", "dynamo_frontend_output_sequence_tokens_count",
+                   "dynamo_frontend_output_sequence_tokens_sum", "dynamo_frontend_time_to_first_token_seconds_count",
+                   "dynamo_frontend_time_to_first_token_seconds_sum",
+                   "dynamo_frontend_inter_token_latency_seconds_count",
+                   "dynamo_frontend_inter_token_latency_seconds_sum")
+
+
+def prometheus_scraper(endpoint: str, namespace: str) -> Callable[[], dict[str, float]]:
+    """Counters of the frontend(s) of `namespace` through the Prometheus HTTP API -- the endpoint
+    the platform installer hands over (PROMETHEUS_ENDPOINT; install-dynamo-1node.sh in the
+    reference passes it to the platform chart as prometheusEndpoint, :214-218).  Same {name: total}
+    shape as http_scraper, summed over every frontend replica Prometheus scrapes."""
+    import httpx
+    names = "|".join(PLANNER_METRICS)
+    query = f'sum by (__name__) ({{__name__=~"{names}", namespace="{namespace}"}})'
+
+    def scrape():
+        r = httpx.get(endpoint.rstrip("/") + "/api/v1/query", params={"query": query}, timeout=10)
+        r.raise_for_status()
+        d = r.json()
+        if d.get("status") != "success":
+            raise RuntimeError(f"prometheus query failed: {d}")
+        return {res["metric"]["__name__"]: float(res["value"][1]) for res in d["data"]["result"]}
+    return scrape
+
+
 def main(argv=None) -> None:
     ap = argparse.ArgumentParser(description="mxserve SLA planner")
     ap.add_argument("--namespace", required=True)
     ap.add_argument("--dgd", required=True)
     ap.add_argument("--model", required=True)
-    ap.add_argument("--frontend-url", required=True)
+    ap.add_argument("--frontend-url", default=None, help="scrape this frontend's /metrics directly")
+    ap.add_argument("--prometheus-endpoint", default=os.environ.get("PROMETHEUS_ENDPOINT"),
+                    help="query Prometheus instead (every frontend replica of the namespace)")
     ap.add_argument("--ttft", type=float, default=600.0, help="ms")
     ap.add_argument("--itl", type=float, default=25.0, help="ms")
     ap.add_argument("--interval", type=float, default=30.0)
@@ -226,4 +256,10 @@ def main(argv=None) -> None:
     from ..k8s.client import KubeClient
     cfg = PlannerConfig(namespace=a.namespace, dgd=a.dgd, model=a.model, ttft_ms=a.ttft, itl_ms=a.itl,
                         interval_s=a.interval, cooldown_s=a.cooldown, max_gpus=a.max_gpus, dry_run=a.dry_run)
-    Planner(cfg, KubeClient(a.server), http_scraper(a.frontend_url)).run()
+    if a.frontend_url:
+        scrape = http_scraper(a.frontend_url)
+    elif a.prometheus_endpoint:
+        scrape = prometheus_scraper(a.prometheus_endpoint, a.namespace)
+    else:
+        ap.error("one of --frontend-url / --prometheus-endpoint (or PROMETHEUS_ENDPOINT) is required")
+    Planner(cfg, KubeClient(a.server), scrape).run()

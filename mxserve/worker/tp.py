@@ -47,8 +47,18 @@ def start_tp_group(args, device_ids=None) -> None:
     if use_gpu:
         torch.cuda.set_device(0)
         dev = torch.device("cuda:0")
-    init_distributed(n, backend="nccl" if use_gpu else "gloo", device=dev)
+    init_distributed(n, backend=_backend(use_gpu, n), device=dev)
     log.info("TP group of %d ranks up", n)
+
+
+def _backend(use_gpu: bool, n: int) -> str:
+    """RCCL when every rank has its own GPU.  Ranks that must share a device (a functional run on a
+    box with fewer GPUs than ranks; RCCL refuses duplicate devices) use gloo, with the custom IPC
+    all-reduce carrying the model's collectives."""
+    import torch
+    if not use_gpu:
+        return "gloo"
+    return "nccl" if torch.cuda.device_count() >= n else "gloo"
 
 
 def stop_tp_group() -> None:
@@ -73,9 +83,9 @@ def follower_main() -> None:
     use_gpu = args.resolved_device() == "cuda"
     dev = None
     if use_gpu:
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)))
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)) % torch.cuda.device_count())
         dev = torch.device("cuda", torch.cuda.current_device())
-    init_distributed(args.tensor_parallel_size, backend="nccl" if use_gpu else "gloo", device=dev)
+    init_distributed(args.tensor_parallel_size, backend=_backend(use_gpu, args.tensor_parallel_size), device=dev)
     runner = ModelRunner(args, get_model_config(args.model))
     runner.follower_loop()
 

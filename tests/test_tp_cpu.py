@@ -36,7 +36,9 @@ def _rank(rank, world, port, model, q, moe_dispatch="allreduce"):
         eng = LLMEngine(_args(model, world, moe_dispatch))
         out = eng.generate(PROMPTS, SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True))
         eng.shutdown()
-        q.put(out)
+        from mxserve.parallel.comm import get_tp
+        ring = get_tp().meta_ring
+        q.put((out, ring.steps if ring else 0, ring.gloo_fallbacks if ring else -1))
     else:
         from mxserve.engine.model_runner import ModelRunner
         from mxserve.models.config import get_model_config
@@ -57,8 +59,10 @@ def test_tp2_matches_tp1(model, moe_dispatch):
     procs = [ctx.Process(target=_rank, args=(r, 2, port, model, q, moe_dispatch)) for r in range(2)]
     for p in procs:
         p.start()
-    out = q.get(timeout=240)
+    out, ring_steps, fallbacks = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert out == ref
+    # every step's inputs went to the follower through the /dev/shm ring, none over gloo
+    assert ring_steps > 6 and fallbacks == 0
