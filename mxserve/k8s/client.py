@@ -14,7 +14,7 @@ import yaml
 
 PLURALS = {
     "Deployment": ("apps/v1", "deployments"), "Service": ("v1", "services"), "ConfigMap": ("v1", "configmaps"),
-    "Secret": ("v1", "secrets"), "Pod": ("v1", "pods"), "Namespace": ("v1", "namespaces"), "Node": ("v1", "nodes"),
+    "Secret": ("v1", "secrets"), "Pod": ("v1", "pods"), "Endpoints": ("v1", "endpoints"), "Namespace": ("v1", "namespaces"), "Node": ("v1", "nodes"),
     "PersistentVolumeClaim": ("v1", "persistentvolumeclaims"), "Job": ("batch/v1", "jobs"),
     "PodMonitor": ("monitoring.coreos.com/v1", "podmonitors"),
     "DynamoGraphDeployment": ("nvidia.com/v1alpha1", "dynamographdeployments"),

@@ -9,7 +9,8 @@ Steps: validate -> warn if no allocatable amd.com/gpu -> ensure namespace -> hf-
 HF_TOKEN, HUGGING_FACE_HUB_TOKEN, token; "dummy" when no token) -> apply the manifest as-is ->
 find Deployments by `nvidia.com/dynamo-namespace=<ns>-<dgd>` and Services by `<dgd>-` prefix ->
 NodePort for every non-headless Service (fixed port for the frontend if given) -> wait for every
-Deployment ready (all replicas, not just the first pod) -> print the quick test.
+Deployment ready (all replicas, not just the first pod) -> wait for the frontend's Endpoints ->
+print the quick test.  With a token, every DGD service gets envFromSecret: hf-token-secret.
 Fixes the reference quirks listed in SURVEY.md Appendix B items 2, 3 and 5.
 """
 from __future__ import annotations
@@ -99,6 +100,13 @@ def run(a: argparse.Namespace, k: Optional[KubeClient] = None) -> dict:
     dgds = []
     for d in docs:
         d.setdefault("metadata", {})["namespace"] = ns
+        if d.get("kind") == "DynamoGraphDeployment" and a.hf_token:
+            # reference :233-247 + :648-655 (envFromSecret patch, then `kubectl set env
+            # --from=secret`): every service of THIS graph gets the token secret (the reference's
+            # fixed service names added stray services to SGLang/TRT-LLM graphs, Appendix B item 2),
+            # and the operator renders it as envFrom on the pods
+            for svc in ((d.get("spec") or {}).get("services") or {}).values():
+                svc.setdefault("envFromSecret", "hf-token-secret")
         k.apply(d)
         if d.get("kind") == "DynamoGraphDeployment":
             dgds.append(d["metadata"]["name"])
@@ -127,6 +135,13 @@ def run(a: argparse.Namespace, k: Optional[KubeClient] = None) -> dict:
                 return all(int((d.get("status") or {}).get("readyReplicas", 0) or 0) >= int(d["spec"].get("replicas", 1))
                            for d in ds) and ds
             _poll(ready, a.pods_timeout, a.poll, f"all pods of {g} ready")
+            # reference wait_endpoints (:94-108, :573): the frontend Service routes to a ready pod
+            fe_name = fe[0]["metadata"]["name"]
+
+            def has_endpoints():
+                ep = k.get("Endpoints", fe_name, ns) or {}
+                return any(ss.get("addresses") for ss in ep.get("subsets") or [])
+            _poll(has_endpoints, a.endpoints_timeout, a.poll, f"endpoints of {fe_name}")
         result["graphs"][g] = {"deployments": sorted(d["metadata"]["name"] for d in deps),
                                "services": sorted(s["metadata"]["name"] for s in svcs),
                                "frontend": fe[0]["metadata"]["name"], "nodeports": ports}

@@ -50,6 +50,7 @@ class FakeApiServer:
                  gpu_resource: str = "amd.com/gpu"):
         self.store: dict[tuple, dict] = {}  # (group/version, plural, ns, name) -> obj
         self.auto_ready = auto_ready
+        self.endpoints_ready = True  # tests flip it to simulate pods that never become endpoints
         self.log: list = []
         self._rv = itertools.count(1)
         for i in range(nodes):
@@ -76,6 +77,15 @@ class FakeApiServer:
                     p["nodePort"] = next(n for n in range(30000, 32768) if n not in used)
                     used.add(p["nodePort"])
         self.store[(gv, plural, ns, meta["name"])] = obj
+        if plural == "services" and self.auto_ready and obj.get("spec", {}).get("selector"):
+            # the endpoints controller: a ready address per selected pod (one, here)
+            ports = [{"name": p.get("name"), "port": p.get("targetPort", p.get("port"))}
+                     for p in obj["spec"].get("ports", [])]
+            self.store[("v1", "endpoints", ns, meta["name"])] = {
+                "apiVersion": "v1", "kind": "Endpoints",
+                "metadata": {"name": meta["name"], "namespace": ns, "uid": str(uuid.uuid4()),
+                             "resourceVersion": str(next(self._rv))},
+                "subsets": [{"addresses": [{"ip": "10.244.0.10"}], "ports": ports}] if self.endpoints_ready else []}
         return obj
 
     def objects(self, plural: str, ns: str | None = None) -> list:

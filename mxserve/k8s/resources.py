@@ -30,6 +30,8 @@ TYPE_LABEL = "nvidia.com/dynamo-component-type"
 SUBTYPE_LABEL = "nvidia.com/dynamo-sub-component-type"
 GPU_RESOURCE = os.environ.get("MXS_GPU_RESOURCE", "amd.com/gpu")
 DEFAULT_IMAGE = os.environ.get("MXS_DEFAULT_IMAGE", "ghcr.io/mxserve/mxserve-rocm:0.1.0")
+# set on the operator Deployment by install-dynamo-1node.sh; passed to every component it renders
+PROMETHEUS_ENDPOINT = os.environ.get("PROMETHEUS_ENDPOINT", "")
 FRONTEND_PORT = 8000
 WORKER_PORT = 8081
 
@@ -154,13 +156,36 @@ def render_dcds(g: GraphSpec) -> list[dict]:
     return out
 
 
+def _served_model(g: GraphSpec) -> str:
+    """The model a graph's workers serve, read from their flag dialects (planner sizing)."""
+    for s in g.services:
+        args = [str(a) for a in (s.args or [])]
+        for flag in ("--served-model-name", "--model", "--model-path"):
+            if flag in args and args.index(flag) + 1 < len(args):
+                return args[args.index(flag) + 1]
+    return "meta-llama/Llama-3.2-1B-Instruct"
+
+
+def _default_command(g: GraphSpec, s: ServiceSpec) -> list:
+    if s.component_type == "frontend":
+        return ["python3", "-m", "dynamo.frontend"]
+    if s.component_type == "planner":
+        # SLA planner: reads the frontend counters from Prometheus (PROMETHEUS_ENDPOINT, handed down
+        # by the operator from the installer) and scales this graph's worker replicas
+        return ["python3", "-m", "mxserve.planner.planner", "--namespace", g.namespace, "--dgd", g.name,
+                "--model", _served_model(g)]
+    return ["python3", "-m", "mxserve.worker"]
+
+
 def _container(g: GraphSpec, s: ServiceSpec) -> dict:
     is_fe = s.component_type == "frontend"
     port = FRONTEND_PORT if is_fe else WORKER_PORT
-    cmd = s.command or (["python3", "-m", "dynamo.frontend"] if is_fe else ["python3", "-m", "mxserve.worker"])
+    cmd = s.command or _default_command(g, s)
     env = [{"name": "DYN_NAMESPACE", "value": f"{g.namespace}-{g.name}"},
            {"name": "POD_IP", "valueFrom": {"fieldRef": {"fieldPath": "status.podIP"}}},
            {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}]
+    if PROMETHEUS_ENDPOINT:
+        env.append({"name": "PROMETHEUS_ENDPOINT", "value": PROMETHEUS_ENDPOINT})
     if is_fe:
         env.append({"name": "DYN_HTTP_PORT", "value": str(FRONTEND_PORT)})
     else:

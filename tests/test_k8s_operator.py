@@ -184,3 +184,83 @@ def test_grafana_dashboard_is_generated_and_uses_exported_metrics():
     exported = set(re.findall(r'"(dynamo_[a-z_]+)"', src))
     base = {re.sub(r"_(sum|count|bucket|total)$", "", u) for u in used}
     assert base <= exported, sorted(base - exported)
+
+
+def test_dashboard_gpu_series_come_from_the_exporter_config():
+    """The dashboard's AMD GPU panels plot only gauges the device-metrics-exporter is configured to
+    publish (deploy/amd-gpu/metrics-exporter-config.yaml, field name lower-cased), and the
+    installer's DeviceConfig enables that exporter with this config."""
+    import json
+    import re
+    from pathlib import Path
+
+    import yaml
+
+    from mxserve.k8s import dashboard
+    root = Path(__file__).resolve().parents[1]
+    cm = yaml.safe_load((root / "deploy/amd-gpu/metrics-exporter-config.yaml").read_text())
+    fields = {f.lower() for f in json.loads(cm["data"]["config.json"])["GPUConfig"]["Fields"]}
+    exprs = " ".join(e for _, _, ts in dashboard.PANELS for e, _ in ts)
+    gpu = set(re.findall(r"\bgpu_[a-z_]+", exprs))
+    assert gpu and gpu <= fields, sorted(gpu - fields)
+    dc = yaml.safe_load((root / "deploy/amd-gpu/deviceconfig.yaml").read_text())
+    assert dc["kind"] == "DeviceConfig" and dc["spec"]["metricsExporter"]["enable"] is True
+    assert dc["spec"]["metricsExporter"]["config"]["name"] == cm["metadata"]["name"]
+    assert dc["spec"]["metricsExporter"]["prometheus"]["serviceMonitor"]["enable"] is True
+    inst = (root / "install-dynamo-1node.sh").read_text()
+    assert "deploy/amd-gpu/$f" in inst and "PROMETHEUS_ENDPOINT_PLACEHOLDER" in inst
+
+
+def test_prometheus_endpoint_reaches_rendered_components(monkeypatch):
+    """PROMETHEUS_ENDPOINT (installer -> operator env) is passed to every rendered component, and a
+    planner service gets the planner command, which queries that endpoint."""
+    from mxserve.k8s import resources
+    monkeypatch.setattr(resources, "PROMETHEUS_ENDPOINT", "http://prom.monitoring:9090")
+    dgd = {"apiVersion": resources.API_VERSION, "kind": resources.DGD_KIND, "metadata": {"name": "g"},
+           "spec": {"services": {
+               "Frontend": {"componentType": "frontend"},
+               "Planner": {"componentType": "planner"},
+               "W": {"componentType": "worker", "resources": {"limits": {"gpu": "1"}},
+                     "extraPodSpec": {"mainContainer": {"args": ["--model", "Qwen/Qwen3-0.6B"]}}}}}}
+    g = resources.parse_dgd(dgd, "ns")
+    deps = {o["metadata"]["name"]: o for o in resources.render_children(g) if o["kind"] == "Deployment"}
+    for d in deps.values():
+        env = {e["name"]: e.get("value") for e in d["spec"]["template"]["spec"]["containers"][0]["env"]}
+        assert env["PROMETHEUS_ENDPOINT"] == "http://prom.monitoring:9090"
+    cmd = deps["g-planner"]["spec"]["template"]["spec"]["containers"][0]["command"]
+    assert cmd[:3] == ["python3", "-m", "mxserve.planner.planner"] and "Qwen/Qwen3-0.6B" in cmd
+
+
+def test_planner_prometheus_scraper():
+    """The planner's Prometheus scraper issues one instant query for the frontend counters of its
+    namespace and returns the same {name: total} map as the direct /metrics scraper."""
+    import json as _json
+    import threading
+    from http.server import BaseHTTPRequestHandler, HTTPServer
+    from urllib.parse import parse_qs, urlparse
+
+    from mxserve.planner.planner import PLANNER_METRICS, prometheus_scraper
+    seen = {}
+
+    class H(BaseHTTPRequestHandler):
+        def do_GET(self):  # noqa: N802
+            q = parse_qs(urlparse(self.path).query)["query"][0]
+            seen["q"] = q
+            res = [{"metric": {"__name__": n}, "value": [0, str(float(i + 1))]} for i, n in enumerate(PLANNER_METRICS)]
+            body = _json.dumps({"status": "success", "data": {"resultType": "vector", "result": res}}).encode()
+            self.send_response(200)
+            self.send_header("content-type", "application/json")
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+
+    srv = HTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        got = prometheus_scraper(f"http://127.0.0.1:{srv.server_port}", "dyn-ns")()
+    finally:
+        srv.shutdown()
+    assert got["dynamo_frontend_requests_total"] == 1.0 and len(got) == len(PLANNER_METRICS)
+    assert 'namespace="dyn-ns"' in seen["q"] and "dynamo_frontend_requests_total" in seen["q"]

@@ -75,6 +75,28 @@ def test_deploy_incluster(cluster):
     assert k.get("Service", "vllm-disagg-vllmdecodeworker", "dynamo-system")["spec"].get("type") != "NodePort"
 
 
+def test_deploy_incluster_token_and_endpoints(cluster):
+    """With --hf-token every service of the graph gets the secret (operator -> envFrom), and the
+    deploy waits for the frontend's Endpoints; without endpoints it times out (ENDPOINTS_TIMEOUT)."""
+    fake, k, url = cluster
+    r = subprocess.run([os.path.join(ROOT, "deploy-incluster.sh"), "--manifest", "examples/deploy/sglang/agg.yaml",
+                        "--hf-token", "hf_abc", "--namespace", "tok"], cwd=ROOT, env=_env(url),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    dgd = k.get("DynamoGraphDeployment", "sglang-agg", "tok")
+    assert all(s.get("envFromSecret") == "hf-token-secret" for s in dgd["spec"]["services"].values())
+    assert set(dgd["spec"]["services"]) == {"Frontend", "decode"}  # no stray services (Appendix B.2)
+    fake.endpoints_ready = False
+    for key in list(fake.store):
+        if key[1] == "endpoints" and key[2] == "tok":
+            fake.store[key]["subsets"] = []
+    r = subprocess.run([os.path.join(ROOT, "deploy-incluster.sh"), "--manifest", "examples/deploy/sglang/agg.yaml",
+                        "--namespace", "tok"], cwd=ROOT, env=_env(url, ENDPOINTS_TIMEOUT="1"),
+                       capture_output=True, text=True, timeout=120)
+    fake.endpoints_ready = True
+    assert r.returncode != 0 and "endpoints of sglang-agg-frontend" in r.stderr, r.stderr
+
+
 def test_deploy_incluster_rejects_bad_nodeport(cluster):
     _, _, url = cluster
     r = subprocess.run([os.path.join(ROOT, "deploy-incluster.sh"), "--manifest", "examples/deploy/vllm/agg.yaml",
