@@ -99,6 +99,14 @@ pybind11::tuple car_alloc(int64_t bytes) {
 
 void car_free(int64_t ptr) { (void)hipFree(reinterpret_cast<void*>(ptr)); }
 
+// Page-lock an existing host mapping (the /dev/shm KV staging arena shared by a prefill and a decode
+// worker of one pod): DMA copies to/from it then run at full PCIe/Infinity-Fabric rate.
+void host_register(int64_t ptr, int64_t bytes) {
+  hip_check(hipHostRegister(reinterpret_cast<void*>(ptr), static_cast<size_t>(bytes), hipHostRegisterDefault),
+            "hipHostRegister");
+}
+void host_unregister(int64_t ptr) { (void)hipHostUnregister(reinterpret_cast<void*>(ptr)); }
+
 int64_t car_read_u32(int64_t ptr) {  // synchronous 4-byte device -> host read (error word)
   unsigned v = 0;
   hip_check(hipMemcpy(&v, reinterpret_cast<void*>(ptr), sizeof(v), hipMemcpyDeviceToHost), "hipMemcpy");
@@ -150,6 +158,8 @@ void register_comm(pybind11::module_& m) {
   m.def("car_alloc", &car_alloc);
   m.def("car_free", &car_free);
   m.def("car_read_u32", &car_read_u32);
+  m.def("host_register", &host_register);
+  m.def("host_unregister", &host_unregister);
   m.def("custom_allreduce", &custom_allreduce, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("recv_ptrs"),
         pybind11::arg("flag_ptrs"), pybind11::arg("rank"), pybind11::arg("slot_elems"), pybind11::arg("epochs_ptr"),
         pybind11::arg("err_ptr"), pybind11::arg("two_shot") = false);

@@ -16,9 +16,17 @@ Backends
         19.5 GiB serving pool hang), so the exported allocation is a fixed, IPC-safe size rather
         than whatever the pool happens to be; the extra on-GPU scatter costs ~30-60 us per
         4000-token prompt.
-  host  staged through host memory over the control plane (CPU backend, or GPUs without a shared
-        IPC namespace): the prefill side ships the block bytes, the decode side writes them.
-Block layout is identical on both sides ([L, 2, Hkv, 16, D] per block).
+  shm   the decode worker also owns a HOST staging arena in /dev/shm (MXS_KV_SHM_BYTES, 2 GiB by
+        default), page-locked with hipHostRegister.  A prefill worker that shares the host's
+        /dev/shm (the P/D pair pod the operator renders, or the same node with hostIPC) but cannot
+        map the GPU arena copies the request's blocks D2H into an extent of it; the decode worker
+        copies them H2D into its pool.  Two DMA copies at host-link speed instead of a msgpack body
+        over HTTP.
+  host  staged through the control plane (no shared /dev/shm either): the prefill side ships the
+        block bytes in the HTTP body, the decode side writes them.
+The decode side reserves an extent in each arena it has; the prefill side uses the first that works
+(xgmi, then shm, then host) and says which; the decode side lands from that one and recycles the
+others.  Block layout is identical on both sides ([L, 2, Hkv, 16, D] per block).
 """
 from __future__ import annotations
 
@@ -36,7 +44,108 @@ import torch
 log = logging.getLogger(__name__)
 
 STAGING_BYTES = int(os.environ.get("MXS_KV_STAGING_BYTES", str(4 << 30)))
+SHM_BYTES = int(os.environ.get("MXS_KV_SHM_BYTES", str(2 << 30)))
 _GIB = 1 << 30
+
+
+class Extents:
+    """First-fit allocator of contiguous block extents in a staging arena; an extent is recycled
+    only once the copy that reads it has finished (an event, or None for immediately)."""
+
+    def __init__(self, n: int):
+        self.n = n
+        self._free: list[list[int]] = [[0, n]] if n > 0 else []
+        self._draining: list[tuple[int, int, object]] = []
+        self._lock = threading.Lock()
+
+    def acquire(self, k: int) -> Optional[int]:
+        if k <= 0 or k > self.n:
+            return None
+        with self._lock:
+            still = []
+            for start, n, ev in self._draining:
+                if ev is None or ev.query():
+                    self._put(start, n)
+                else:
+                    still.append((start, n, ev))
+            self._draining = still
+            for ext in self._free:
+                if ext[1] >= k:
+                    start = ext[0]
+                    ext[0] += k
+                    ext[1] -= k
+                    if ext[1] == 0:
+                        self._free.remove(ext)
+                    return start
+            return None
+
+    def release(self, start: int, n: int, after=None) -> None:
+        with self._lock:
+            self._draining.append((start, n, after))
+
+    def _put(self, start: int, n: int) -> None:
+        f = self._free
+        f.append([start, n])
+        f.sort()
+        merged = [f[0]]
+        for s0, n0 in f[1:]:
+            if merged[-1][0] + merged[-1][1] == s0:
+                merged[-1][1] += n0
+            else:
+                merged.append([s0, n0])
+        self._free = merged
+
+    def free_blocks(self) -> int:
+        with self._lock:
+            return sum(n for _, n in self._free) + sum(n for _, n, _ in self._draining)
+
+
+def _unlink_quiet(path: str) -> None:
+    try:
+        os.unlink(path)
+    except FileNotFoundError:
+        pass
+
+
+class ShmArena:
+    """KV blocks in /dev/shm shared by the workers of one pod / host (the `shm` backend)."""
+
+    def __init__(self, name: str, nblocks: int, block_shape: tuple, dtype: torch.dtype, create: bool,
+                 pin: bool):
+        import mmap
+        self.name, self.nblocks = name, nblocks
+        esz = torch.empty(0, dtype=dtype).element_size()
+        self.block_bytes = int(np.prod(block_shape)) * esz
+        nbytes = nblocks * self.block_bytes
+        path = "/dev/shm" + name
+        flags = os.O_RDWR | (os.O_CREAT | os.O_EXCL if create else 0)
+        fd = os.open(path, flags, 0o600)
+        try:
+            if create:
+                os.ftruncate(fd, nbytes)
+            self._mm = mmap.mmap(fd, nbytes, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        finally:
+            os.close(fd)
+        self.owner = create
+        if create:  # a worker that exits without close() still removes its name from /dev/shm
+            import atexit
+            atexit.register(_unlink_quiet, path)
+        arr = np.frombuffer(self._mm, dtype=np.uint8)
+        self.t = torch.from_numpy(arr).view(dtype).view(nblocks, *block_shape)
+        self._pinned = False
+        if pin:
+            from .. import ops
+            ops.ext().host_register(int(self.t.data_ptr()), nbytes)
+            self._pinned = True
+
+    def close(self) -> None:
+        if self._pinned:
+            from .. import ops
+            ops.ext().host_unregister(int(self.t.data_ptr()))
+            self._pinned = False
+        self.t = None
+        if self.owner:
+            _unlink_quiet("/dev/shm" + self.name)
 
 
 def ipc_safe_blocks(k: int, block_bytes: int) -> int:
@@ -70,9 +179,13 @@ class KVTransferAgent:
         self.arena_blocks = max(math.ceil(mtok / bs), STAGING_BYTES // bb)
         self.arena_blocks = ipc_safe_blocks(self.arena_blocks, bb)
         self.staging: Optional[torch.Tensor] = None
-        self._free: list[list[int]] = []  # sorted free extents [start, length]
-        self._draining: list[tuple[int, int, object]] = []  # (start, n, event) until landed
+        self._ext: Optional[Extents] = None
         self._desc: Optional[dict] = None
+        # host staging arena in /dev/shm (decode side creates, prefill side attaches by name)
+        self.shm: Optional[ShmArena] = None
+        self._shm_ext: Optional[Extents] = None
+        self._shm_peers: dict[str, ShmArena] = {}
+        self.shm_blocks = max(math.ceil(mtok / bs), SHM_BYTES // bb) if SHM_BYTES > 0 else 0
 
     # -------------------------------------------------------------- decode side
     def _ensure_staging(self) -> None:
@@ -80,9 +193,24 @@ class KVTransferAgent:
             return
         self.staging = torch.empty((self.arena_blocks,) + tuple(self.kv.shape[1:]), dtype=self.kv.dtype,
                                    device=self.kv.device)
-        self._free = [[0, self.arena_blocks]]
+        self._ext = Extents(self.arena_blocks)
         log.info("KV staging arena: %d blocks (%.2f GB)", self.arena_blocks,
                  self.arena_blocks * self.block_bytes / 1e9)
+
+    def _ensure_shm(self) -> None:
+        if self.shm is not None or self.shm_blocks <= 0:
+            return
+        name = f"/mxs-kv-{os.getpid()}-{int.from_bytes(os.urandom(4), 'little'):08x}"
+        try:
+            self.shm = ShmArena(name, self.shm_blocks, tuple(self.kv.shape[1:]), self.kv.dtype, create=True,
+                                pin=self.is_gpu)
+        except OSError as e:  # no (big enough) /dev/shm: the host backend remains
+            log.warning("no /dev/shm KV staging arena (%r)", e)
+            self.shm_blocks = 0
+            return
+        self._shm_ext = Extents(self.shm_blocks)
+        log.info("KV shm staging arena %s: %d blocks (%.2f GB)", name, self.shm_blocks,
+                 self.shm_blocks * self.block_bytes / 1e9)
 
     def descriptor(self, host_url: Optional[str] = None) -> dict:
         if self._desc is not None:
@@ -96,51 +224,46 @@ class KVTransferAgent:
             handle, off = ops.ext().ipc_export_pool(self.staging)
             d.update(handle=base64.b64encode(handle).decode(), offset=int(off), device=self.kv.device.index,
                      data_ptr=int(self.staging.data_ptr()), arena_blocks=self.arena_blocks)
+        self._ensure_shm()
+        if self.shm is not None:
+            d.update(shm_name=self.shm.name, shm_blocks=self.shm_blocks)
         self._desc = d
         return dict(d)
 
-    def _reclaim(self) -> None:
-        still = []
-        for start, n, ev in self._draining:
-            if ev is None or ev.query():
-                self._free_extent(start, n)
-            else:
-                still.append((start, n, ev))
-        self._draining = still
-
-    def _free_extent(self, start: int, n: int) -> None:
-        f = self._free
-        f.append([start, n])
-        f.sort()
-        merged = [f[0]]
-        for s0, n0 in f[1:]:
-            if merged[-1][0] + merged[-1][1] == s0:
-                merged[-1][1] += n0
-            else:
-                merged.append([s0, n0])
-        self._free = merged
-
     def acquire(self, n: int) -> Optional[int]:
-        """Offset of a free extent of n arena blocks, or None (caller transfers via the host)."""
+        """Offset of a free extent of n GPU-arena blocks, or None (xgmi unavailable or full)."""
         if self.backend != "xgmi" or n <= 0:
             return None
         self._ensure_staging()
-        with self._lock:
-            self._reclaim()
-            for ext in self._free:
-                if ext[1] >= n:
-                    start = ext[0]
-                    ext[0] += n
-                    ext[1] -= n
-                    if ext[1] == 0:
-                        self._free.remove(ext)
-                    return start
-            return None
+        return self._ext.acquire(n)
 
     def release(self, start: int, n: int, after=None) -> None:
-        """Recycle an extent; `after` (a recorded event) delays it until the landing copy is done."""
-        with self._lock:
-            self._draining.append((start, n, after))
+        """Recycle a GPU-arena extent; `after` (a recorded event) delays it until the landing copy
+        is done."""
+        self._ext.release(start, n, after)
+
+    def acquire_shm(self, n: int) -> Optional[int]:
+        self._ensure_shm()
+        return self._shm_ext.acquire(n) if self._shm_ext is not None else None
+
+    def release_shm(self, start: int, n: int, after=None) -> None:
+        self._shm_ext.release(start, n, after)
+
+    def land_shm(self, start: int, dst_ids: list[int]) -> None:
+        """Host arena extent -> pool blocks on the current stream (H2D DMA from page-locked shm)."""
+        n = len(dst_ids)
+        ev = None
+        if n:
+            src = self.shm.t[start:start + n]
+            idx = torch.tensor(dst_ids, dtype=torch.long)
+            if self.is_gpu:
+                self.kv.index_copy_(0, idx.to(self.kv.device, non_blocking=True),
+                                    src.to(self.kv.device, non_blocking=True))
+                ev = torch.cuda.Event()
+                ev.record()
+            else:
+                self.kv.index_copy_(0, idx, src)
+        self.release_shm(start, n, ev)
 
     def land(self, start: int, dst_ids: list[int]) -> None:
         """Scatter a filled extent into the pool blocks on the CURRENT stream (call it on the engine's
@@ -166,15 +289,48 @@ class KVTransferAgent:
             torch.cuda.synchronize(self.kv.device)
 
     def close(self) -> None:
-        """Unmap every opened peer arena and drop the local one (bench phases rebuild engines)."""
+        """Unmap every opened peer arena and drop the local ones (bench phases rebuild engines)."""
+        if self._stream is not None:
+            self._stream.synchronize()
         if self._opened:
             from .. import ops
-            if self._stream is not None:
-                self._stream.synchronize()
             ops.ext().ipc_close_all()
             self._opened.clear()
+        for a in list(self._shm_peers.values()) + ([self.shm] if self.shm is not None else []):
+            a.close()
+        self._shm_peers.clear()
+        self.shm = None
         self.staging = None
         self._desc = None
+
+    def push_shm(self, src_ids: list[int], target: dict, start: int) -> float:
+        """Prefill side: copy blocks into the decode worker's /dev/shm arena (same pod / host);
+        blocking, returns seconds.  Raises OSError when that arena is not visible here."""
+        if not src_ids:
+            return 0.0
+        name = target["shm_name"]
+        if start < 0 or start + len(src_ids) > int(target["shm_blocks"]):
+            raise ValueError(f"extent [{start}, +{len(src_ids)}) outside the shm arena")
+        t0 = time.perf_counter()
+        with self._lock:
+            arena = self._shm_peers.get(name)
+            if arena is None:
+                arena = ShmArena(name, int(target["shm_blocks"]), tuple(self.kv.shape[1:]), self.kv.dtype,
+                                 create=False, pin=self.is_gpu)
+                self._shm_peers[name] = arena
+        if arena.block_bytes != self.block_bytes:
+            raise ValueError("KV block layout mismatch between prefill and decode workers")
+        idx = torch.tensor(src_ids, dtype=torch.long, device=self.kv.device)
+        if self.is_gpu:
+            self._stream.wait_stream(torch.cuda.current_stream(self.kv.device))
+            with torch.cuda.stream(self._stream):
+                arena.t[start:start + len(src_ids)].copy_(self.kv.index_select(0, idx), non_blocking=True)
+            self._stream.synchronize()
+        else:
+            arena.t[start:start + len(src_ids)].copy_(self.kv.index_select(0, idx))
+        self.bytes_moved += len(src_ids) * self.block_bytes
+        self.transfers += 1
+        return time.perf_counter() - t0
 
     # -------------------------------------------------------------- prefill side
     def _remote_ptr(self, target: dict) -> int:

@@ -219,7 +219,9 @@ class Frontend:
             w, overlap = self.router.pick(decode, ids)
             purl = None
             if w.role == "decode" and prefill:
-                pw, _ = self.router.pick(prefill, ids)
+                # a prefill worker in the decode worker's own pair pod can reach its GPU arena
+                mates = [p for p in prefill if w.pair and p.pair == w.pair]
+                pw, _ = self.router.pick(mates or prefill, ids)
                 purl = pw.url
             if overlap:
                 self.metrics.kv_hit.labels(model).inc(overlap)
@@ -592,7 +594,7 @@ class Frontend:
             info = WorkerInfo(worker_id=d["worker_id"], url=d["url"], model=d["model"], role=d.get("role", "agg"),
                               block_size=int(d.get("block_size", 16)),
                               kv_total_blocks=int(d.get("kv_total_blocks", 1) or 1), tp=int(d.get("tp", 1)),
-                              max_model_len=int(d.get("max_model_len", 0) or 0))
+                              max_model_len=int(d.get("max_model_len", 0) or 0), pair=str(d.get("pair") or ""))
             fe.registry.register(info)
             log.info("registered worker %s (%s) for %s at %s", info.worker_id, info.role, info.model, info.url)
             return {"ok": True, "index": info.index}

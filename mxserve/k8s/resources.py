@@ -13,6 +13,7 @@ lists the fields honoured here.  Rendering (pure functions, unit-tested without 
 from __future__ import annotations
 
 import copy
+import json
 import os
 import re
 from dataclasses import dataclass, field
@@ -213,10 +214,56 @@ def _container(g: GraphSpec, s: ServiceSpec) -> dict:
     return c
 
 
+PAIR_LABEL = "mxserve.io/pd-pair"
+
+
+def pd_pairs(g: GraphSpec) -> Optional[tuple]:
+    """(decode service, prefill service) to co-locate, or None.  MXS_PD_POD_MODE=pair (default)
+    renders each decode replica with a prefill worker in one pod that holds both groups of GPUs
+    (SURVEY.md §5.8 mitigation #1; mxserve/worker/pair.py); =split keeps the reference's two-pod
+    form (then the KV crosses pods over hostIPC, the /dev/shm arena or HTTP)."""
+    if os.environ.get("MXS_PD_POD_MODE", "pair") != "pair":
+        return None
+    dec = [s for s in g.services if s.component_type == "worker" and s.sub_component_type == "decode"]
+    pre = [s for s in g.services if s.component_type == "worker" and s.sub_component_type == "prefill"]
+    if not dec or not pre:
+        return None
+    return dec[0], pre[0]
+
+
+def _full_command(g: GraphSpec, s: ServiceSpec) -> list:
+    return [str(c) for c in (s.command or _default_command(g, s))] + [str(a) for a in (s.args or [])]
+
+
+def _pair_container(g: GraphSpec, d: ServiceSpec, p: ServiceSpec) -> dict:
+    c = _container(g, d)
+    c["command"] = ["python3", "-m", "mxserve.worker.pair"]
+    c.pop("args", None)
+    have = {e["name"] for e in c["env"]}
+    c["env"] += [dict(e) for e in p.envs if e["name"] not in have]
+    c["env"] += [{"name": "MXS_PAIR_DECODE_CMD", "value": json.dumps(_full_command(g, d))},
+                 {"name": "MXS_PAIR_PREFILL_CMD", "value": json.dumps(_full_command(g, p))},
+                 {"name": "POD_NAME", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}}]
+    c["ports"].append({"name": "prefill", "containerPort": WORKER_PORT + 1})
+    n = (d.gpus or 1) + (p.gpus or 1)
+    c["resources"] = {"limits": {GPU_RESOURCE: str(n)}, "requests": {GPU_RESOURCE: str(n)}}
+    mounts = {m["mountPath"] for m in c.get("volumeMounts", [])}
+    for vm in p.volume_mounts:
+        if vm["mountPoint"] not in mounts:
+            c.setdefault("volumeMounts", []).append({"name": vm["name"], "mountPath": vm["mountPoint"]})
+    if not p.env_from_secret or p.env_from_secret == d.env_from_secret:
+        return c
+    c.setdefault("envFrom", []).append({"secretRef": {"name": p.env_from_secret, "optional": True}})
+    return c
+
+
 def render_children(g: GraphSpec, dcd_uids: Optional[dict] = None) -> list[dict]:
-    """Deployment + Service (+ PodMonitor) per service, owned by its DCD."""
+    """Deployment + Service (+ PodMonitor) per service, owned by its DCD.  With P/D pairing the
+    decode service's Deployment runs pair pods and the prefill service's keeps only the prefill
+    replicas beyond the decode count."""
     objs = []
     dcd_uids = dcd_uids or {}
+    pair = pd_pairs(g)
     for s in g.services:
         name = f"{g.name}-{s.dns_name}"
         labels = {NS_LABEL: f"{g.namespace}-{g.name}", COMPONENT_LABEL: s.key, TYPE_LABEL: s.component_type,
@@ -224,20 +271,34 @@ def render_children(g: GraphSpec, dcd_uids: Optional[dict] = None) -> list[dict]
         if s.sub_component_type:
             labels[SUBTYPE_LABEL] = s.sub_component_type
         owner = _owner(DCD_KIND, name, dcd_uids.get(name))
-        pod_spec = {"containers": [_container(g, s)], "terminationGracePeriodSeconds": 30}
-        vols = [{"name": vm["name"], "persistentVolumeClaim": {"claimName": vm["name"]}} for vm in s.volume_mounts]
-        if s.gpus:
+        replicas = s.replicas
+        paired = pair is not None and s is pair[0]
+        if paired:
+            labels[PAIR_LABEL] = f"{pair[0].key}+{pair[1].key}"
+            container = _pair_container(g, pair[0], pair[1])
+        else:
+            container = _container(g, s)
+            if pair is not None and s is pair[1]:
+                replicas = max(0, s.replicas - pair[0].replicas)
+        pod_spec = {"containers": [container], "terminationGracePeriodSeconds": 30}
+        vms = list(s.volume_mounts) + (list(pair[1].volume_mounts) if paired else [])
+        vols = []
+        for vm in vms:
+            if vm["name"] not in {v["name"] for v in vols}:
+                vols.append({"name": vm["name"], "persistentVolumeClaim": {"claimName": vm["name"]}})
+        if s.gpus or paired:
             vols.append({"name": "dshm", "emptyDir": {"medium": "Memory"}})
-            if s.sub_component_type in ("prefill", "decode"):
-                # xGMI KV transfer between prefill and decode pods opens the peer's KV pool with
-                # hipIpcOpenMemHandle: the pods need a shared IPC namespace
+            if s.sub_component_type in ("prefill", "decode") and not paired:
+                # two-pod form: the xGMI KV transfer between prefill and decode pods opens the
+                # peer's staging arena with hipIpcOpenMemHandle; the pods need a shared IPC
+                # namespace (SURVEY.md §5.8 mitigation #2)
                 pod_spec["hostIPC"] = True
         if vols:
             pod_spec["volumes"] = vols
         objs.append({
             "apiVersion": "apps/v1", "kind": "Deployment",
             "metadata": {"name": name, "namespace": g.namespace, "labels": dict(labels), "ownerReferences": owner},
-            "spec": {"replicas": s.replicas, "selector": {"matchLabels": {"app.kubernetes.io/name": name}},
+            "spec": {"replicas": replicas, "selector": {"matchLabels": {"app.kubernetes.io/name": name}},
                      "template": {"metadata": {"labels": dict(labels)}, "spec": pod_spec}}})
         is_fe = s.component_type == "frontend"
         svc_spec = {"selector": {"app.kubernetes.io/name": name},

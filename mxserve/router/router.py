@@ -31,6 +31,7 @@ class WorkerInfo:
     kv_total_blocks: int = 1
     tp: int = 1
     max_model_len: int = 0  # 0 = unknown
+    pair: str = ""  # P/D pair pod id: a decode worker takes prefill workers of its own pair first
     index: int = -1
     last_seen: float = field(default_factory=time.monotonic)
     num_running: int = 0

@@ -137,13 +137,16 @@ class Worker:
         nblk = -(-len(toks) // self.args.block_size)
         dst = list(req.block_ids[skip:nblk])
         target = self.agent.descriptor(self.url)
-        # xgmi: reserve an extent of the IPC-mapped staging arena; none free -> host-staged this time
+        # reserve an extent in every staging arena this worker has (GPU arena over xGMI IPC, host
+        # arena in /dev/shm); the prefill worker uses the first it can reach and says which
         start = self.agent.acquire(len(dst)) if target["backend"] == "xgmi" else None
+        shm_start = self.agent.acquire_shm(len(dst)) if target.get("shm_name") else None
         if start is None:
             target["backend"] = "host"
         target["block_ids"] = dst
         target["skip_blocks"] = skip
         target["arena_start"] = start
+        target["shm_start"] = shm_start
         payload = {"request_id": rid, "token_ids": toks, "sampling": _sp_dict(sp), "kv_target": target}
         completed = False
         try:
@@ -153,18 +156,27 @@ class Worker:
                     raise RuntimeError(f"prefill worker returned {r.status}: {await r.text()}")
                 res = await r.json()
 
+            via = res.get("via", target["backend"])
+
             def land_and_complete(tok: int):
-                if start is not None:  # staging extent -> pool blocks, on the engine's stream
+                # the arena the prefill worker wrote -> pool blocks, on the engine's stream (ordered
+                # before the next step); the other extents are recycled unused
+                if via == "xgmi":
                     self.agent.land(start, dst)
+                elif start is not None:
+                    self.agent.release(start, len(dst))
+                if via == "shm":
+                    self.agent.land_shm(shm_start, dst)
+                elif shm_start is not None:
+                    self.agent.release_shm(shm_start, len(dst))
                 return self.engine.complete_remote_prefill(rid, tok, res.get("logprob"), res.get("top_logprobs"))
 
             out = await self.aeng.submit(land_and_complete, int(res["first_token"]))
-            completed = True  # the landing copy now owns (and recycles) the extent
+            completed = True  # the landing copies now own (and recycle) the extents
             self.aeng.push(out)
             if "transfer_s" in res:
                 self.metrics.kv_xfer_lat.labels(self.model).observe(float(res["transfer_s"]))
-                self.metrics.kv_xfer_bytes.labels(self.model, target["backend"]).inc(
-                    len(target["block_ids"]) * self.agent.block_bytes)
+                self.metrics.kv_xfer_bytes.labels(self.model, via).inc(len(target["block_ids"]) * self.agent.block_bytes)
             return q
         except Exception as e:  # noqa: BLE001 - SURVEY §5.3: fall back to local prefill
             log.warning("remote prefill failed for %s (%r); prefilling locally", rid, e)
@@ -176,6 +188,8 @@ class Worker:
             if not completed:
                 if start is not None:
                     self.agent.release(start, len(dst))
+                if shm_start is not None:
+                    self.agent.release_shm(shm_start, len(dst))
                 self.aeng.submit_nowait(self.engine.abort, rid)
                 self.aeng._queues.pop(rid, None)
 
@@ -196,13 +210,27 @@ class Worker:
         dst = list(target["block_ids"])
         src = list(req.block_ids[skip:skip + len(dst)]) if req is not None else []
         xfer_s = 0.0
+        via = None
+        loop = asyncio.get_running_loop()
         try:
             if len(src) != len(dst):
                 raise RuntimeError(f"block count mismatch: {len(src)} local vs {len(dst)} remote")
-            if target["backend"] == "xgmi" and self.agent.backend == "xgmi":
-                xfer_s = await asyncio.get_running_loop().run_in_executor(None, self.agent.push_xgmi, src, target,
-                                                                          int(target["arena_start"]))
-            else:
+            if target["backend"] == "xgmi" and self.agent.backend == "xgmi" and target.get("arena_start") is not None:
+                try:
+                    xfer_s = await loop.run_in_executor(None, self.agent.push_xgmi, src, target,
+                                                        int(target["arena_start"]))
+                    via = "xgmi"
+                except (RuntimeError, OSError) as e:  # the decode GPU's arena cannot be mapped here
+                    log.warning("xGMI push to %s failed (%r); trying the shm / host paths", target.get("url"), e)
+            if via is None and target.get("shm_start") is not None:
+                try:
+                    xfer_s = await loop.run_in_executor(None, self.agent.push_shm, src, target,
+                                                        int(target["shm_start"]))
+                    via = "shm"
+                except OSError:  # the decode worker's /dev/shm is not ours (another pod / host)
+                    pass
+            if via is None:
+                via = "host"
                 t0 = time.perf_counter()
                 data = await asyncio.get_running_loop().run_in_executor(None, self.agent.read_blocks, src)
                 sess = await self.http()
@@ -215,7 +243,7 @@ class Worker:
         finally:
             self.aeng.submit_nowait(self.engine.release_prefill_blocks, rid)
         res = {"first_token": first, "num_cached_tokens": req.num_cached_tokens if req else 0,
-               "transfer_s": xfer_s, "blocks": len(dst)}
+               "transfer_s": xfer_s, "blocks": len(dst), "via": via}
         if first_lp is not None and first_lp.logprob is not None:
             res.update(logprob=first_lp.logprob, top_logprobs=first_lp.top_logprobs or [])
         return res
@@ -286,7 +314,8 @@ class Worker:
         st = self.aeng.last_stats
         return {"worker_id": self.worker_id, "url": self.url, "model": self.model, "role": self.role,
                 "block_size": self.args.block_size, "kv_total_blocks": st.get("kv_total_blocks", 0),
-                "tp": self.args.tensor_parallel_size, "max_model_len": self.args.max_model_len}
+                "tp": self.args.tensor_parallel_size, "max_model_len": self.args.max_model_len,
+                "pair": os.environ.get("MXS_PAIR_ID", "")}
 
     async def _heartbeat_loop(self) -> None:
         base = self.wargs.frontend_url.rstrip("/")
@@ -330,6 +359,10 @@ def serve(wargs: WorkerArgs) -> None:
     import uvicorn
     from ..utils.logs import setup_logging
     setup_logging()
+    off = int(os.environ.get("MXS_DEVICE_OFFSET", "0"))
+    if off and wargs.engine.resolved_device() == "cuda":  # second worker of a P/D pair pod
+        import torch
+        torch.cuda.set_device(off % torch.cuda.device_count())  # (a 1-GPU functional run shares GPU 0)
     if wargs.engine.tensor_parallel_size > 1:
         from .tp import start_tp_group
         start_tp_group(wargs.engine)

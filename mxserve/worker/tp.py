@@ -44,9 +44,10 @@ def start_tp_group(args, device_ids=None) -> None:
         _children.append(subprocess.Popen([sys.executable, "-m", "mxserve.worker.tp"], env=env))
     use_gpu = args.resolved_device() == "cuda"
     dev = None
-    if use_gpu:
-        torch.cuda.set_device(0)
-        dev = torch.device("cuda:0")
+    if use_gpu:  # GPUs [offset, offset + n): offset > 0 for the prefill half of a P/D pair pod
+        off = int(os.environ.get("MXS_DEVICE_OFFSET", "0"))
+        torch.cuda.set_device(off)
+        dev = torch.device("cuda", off)
     init_distributed(n, backend=_backend(use_gpu, n), device=dev)
     log.info("TP group of %d ranks up", n)
 
@@ -58,7 +59,7 @@ def _backend(use_gpu: bool, n: int) -> str:
     import torch
     if not use_gpu:
         return "gloo"
-    return "nccl" if torch.cuda.device_count() >= n else "gloo"
+    return "nccl" if torch.cuda.device_count() >= n + int(os.environ.get("MXS_DEVICE_OFFSET", "0")) else "gloo"
 
 
 def stop_tp_group() -> None:
@@ -83,7 +84,8 @@ def follower_main() -> None:
     use_gpu = args.resolved_device() == "cuda"
     dev = None
     if use_gpu:
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)) % torch.cuda.device_count())
+        off = int(os.environ.get("MXS_DEVICE_OFFSET", "0"))
+        torch.cuda.set_device((off + int(os.environ.get("LOCAL_RANK", rank))) % torch.cuda.device_count())
         dev = torch.device("cuda", torch.cuda.current_device())
     init_distributed(args.tensor_parallel_size, backend=_backend(use_gpu, args.tensor_parallel_size), device=dev)
     runner = ModelRunner(args, get_model_config(args.model))

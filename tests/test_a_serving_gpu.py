@@ -88,3 +88,53 @@ def test_disaggregated_chat_over_ipc(tmp_path):
         fs_agg.stop()
         for f in logs.values():
             f.close()
+
+
+def test_pd_pair_pod_launcher(tmp_path):
+    """The P/D pair pod the operator renders: `python -m mxserve.worker.pair` runs the decode and
+    the prefill worker (commands from MXS_PAIR_*_CMD) in one container; both register under one pair
+    id, the frontend sends the decode worker its own prefill worker and the KV moves over IPC."""
+    import json
+    import torch
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    if torch.cuda.is_initialized():
+        pytest.skip("HIP already initialised in the test process")
+    fe = Frontend(router_mode="kv", ttl=60)
+    fs = Server(fe.app).start()
+    common = ["--model", MODEL, "--frontend-url", fs.url, "--host", "127.0.0.1", "--num-gpu-blocks-override", "4096",
+              "--max-model-len", "4096", "--max-num-seqs", "16", "--enforce-eager"]
+    port = free_port()  # the decode worker's; the prefill worker takes port + 1
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MXS_KV_STAGING_BYTES=str(1 << 30), DYN_SYSTEM_PORT=str(port),
+               POD_NAME="pairpod-0", PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""),
+               MXS_PAIR_DECODE_CMD=json.dumps([sys.executable, "-m", "dynamo.vllm", "--is-decode-worker"] + common),
+               MXS_PAIR_PREFILL_CMD=json.dumps([sys.executable, "-m", "dynamo.vllm", "--is-prefill-worker"] + common))
+    env.pop("MXS_WORKER_ID", None)
+    log = open(tmp_path / "pair.log", "w")
+    proc = subprocess.Popen([sys.executable, "-m", "mxserve.worker.pair"], cwd=ROOT, env=env, stdout=log,
+                            stderr=subprocess.STDOUT)
+    try:
+        def ready():
+            if proc.poll() is not None:
+                raise RuntimeError("pair launcher exited:\n" + (tmp_path / "pair.log").read_text()[-4000:])
+            return len(fe.registry.list()) == 2
+        wait_for(ready, timeout=240, interval=1.0)
+        ws = fe.registry.list()
+        assert {w.role for w in ws} == {"prefill", "decode"} and {w.pair for w in ws} == {"pairpod-0"}
+        body = {"model": MODEL, "messages": [{"role": "user", "content": "pair pod " * 50}], "max_tokens": 12,
+                "temperature": 0, "ignore_eos": True}
+        r = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=120)
+        assert r.status_code == 200 and r.json()["usage"]["completion_tokens"] == 12, r.text
+        m = httpx.get(f"http://127.0.0.1:{port}/metrics", timeout=10).text
+        moved = [ln for ln in m.splitlines()
+                 if ln.startswith("dynamo_component_kv_transfer_bytes_total") and 'backend="xgmi"' in ln]
+        assert moved and float(moved[0].split()[-1]) > 0, m[-2000:]
+    finally:
+        proc.terminate()
+        try:
+            proc.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+            proc.wait()
+        fs.stop()
+        log.close()

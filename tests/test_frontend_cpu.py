@@ -231,8 +231,14 @@ def test_reasoning_parser_fields(agg_stack):
         fe.reasoning_parser = None
 
 
-def test_disaggregated_matches_aggregated():
-    """Prefill worker + decode worker (host-staged KV transfer) give the agg result token for token."""
+@pytest.mark.parametrize("via", ["shm", "host"])
+def test_disaggregated_matches_aggregated(via, monkeypatch):
+    """Prefill worker + decode worker give the agg result token for token, with the KV moved
+    through the decode worker's /dev/shm staging arena (same host) or, without one, in the HTTP
+    body."""
+    from mxserve.disagg import kv_transfer
+    if via == "host":
+        monkeypatch.setattr(kv_transfer, "SHM_BYTES", 0)
     fe = Frontend(router_mode="round_robin", ttl=30)
     fs = Server(fe.app).start()
     pw, ps = _worker(fs.url, role="prefill")
@@ -248,7 +254,9 @@ def test_disaggregated_matches_aggregated():
         disagg = r.json()["choices"][0]["message"]["content"]
         assert pw.agent.backend == "host"
         # the decode worker really received the prompt's KV from the prefill worker
-        assert dw.metrics.kv_xfer_bytes.labels(MODEL, "host")._value.get() > 0
+        assert dw.metrics.kv_xfer_bytes.labels(MODEL, via)._value.get() > 0
+        if via == "shm":  # every staging extent came back once the copies landed
+            assert dw.agent._shm_ext.free_blocks() == dw.agent.shm_blocks
         # aggregated reference with the same weights (same seed)
         agg, ags = _worker(None, role="agg")
         ags.start()
@@ -267,6 +275,8 @@ def test_disaggregated_matches_aggregated():
         fs.stop()
         pw.aeng.shutdown()
         dw.aeng.shutdown()
+        pw.agent.close()
+        dw.agent.close()
 
 
 def test_request_trace_by_x_request_id(agg_stack):

@@ -49,7 +49,9 @@ def test_every_example_manifest_parses(base):
             assert r.isl == 4000 and r.ttft_ms == 600
 
 
-def test_render_contract():
+def test_render_contract(monkeypatch):
+    """The reference's two-pod P/D form (MXS_PD_POD_MODE=split)."""
+    monkeypatch.setenv("MXS_PD_POD_MODE", "split")
     with open(os.path.join(ROOT, "examples/deploy/vllm/disagg.yaml")) as f:
         g = parse_dgd(yaml.safe_load(f), "dynamo-system")
     dcds = render_dcds(g)
@@ -71,6 +73,49 @@ def test_render_contract():
     assert fe_svc["spec"]["ports"][0]["port"] == 8000 and "clusterIP" not in fe_svc["spec"]
     wk_svc = next(o for o in kids if o["kind"] == "Service" and o["metadata"]["name"].endswith("prefillworker"))
     assert wk_svc["spec"]["clusterIP"] == "None"
+
+
+@pytest.mark.parametrize("manifest", ["examples/deploy/vllm/disagg.yaml", "examples/deploy/sglang/disagg.yaml",
+                                      "examples/deploy/trtllm/disagg.yaml"])
+def test_render_pd_pair_pod(manifest):
+    """Default: each decode replica is ONE pod holding the decode and the prefill worker (both
+    services' GPUs), so the prefill process can IPC-map the decode GPU's staging arena (SURVEY.md §5.8
+    mitigation #1); the prefill Deployment keeps only prefill replicas beyond the decode count."""
+    import json as _json
+
+    from mxserve.k8s.resources import PAIR_LABEL, WORKER_PORT
+    with open(os.path.join(ROOT, manifest)) as f:
+        g = parse_dgd(yaml.safe_load(f), "dynamo-system")
+    dec = next(s for s in g.services if s.sub_component_type == "decode")
+    pre = next(s for s in g.services if s.sub_component_type == "prefill")
+    deps = {d["metadata"]["name"]: d for d in render_children(g) if d["kind"] == "Deployment"}
+    pod = deps[f"{g.name}-{dec.dns_name}"]
+    spec = pod["spec"]["template"]["spec"]
+    assert len(spec["containers"]) == 1 and "hostIPC" not in spec  # one container, no host IPC needed
+    c = spec["containers"][0]
+    assert c["command"] == ["python3", "-m", "mxserve.worker.pair"] and "args" not in c
+    assert c["resources"]["limits"] == {"amd.com/gpu": str(dec.gpus + pre.gpus)}
+    env = {e["name"]: e.get("value") for e in c["env"]}
+    dcmd, pcmd = _json.loads(env["MXS_PAIR_DECODE_CMD"]), _json.loads(env["MXS_PAIR_PREFILL_CMD"])
+    assert dcmd[:len(dec.command or [])] == list(dec.command or []) and dcmd[-len(dec.args):] == list(map(str, dec.args))
+    assert pcmd[-len(pre.args):] == list(map(str, pre.args))
+    assert {p["containerPort"] for p in c["ports"]} == {WORKER_PORT, WORKER_PORT + 1}
+    assert any(v.get("emptyDir", {}).get("medium") == "Memory" for v in spec["volumes"])  # shared /dev/shm
+    assert pod["metadata"]["labels"][PAIR_LABEL] == f"{dec.key}+{pre.key}"
+    assert pod["spec"]["replicas"] == dec.replicas
+    assert deps[f"{g.name}-{pre.dns_name}"]["spec"]["replicas"] == max(0, pre.replicas - dec.replicas)
+
+
+def test_pair_launcher_envs():
+    """The pair launcher gives the decode worker GPUs [0, tp_d) and the pod's system port, the
+    prefill worker the next GPUs and port + 1, both the same pair id."""
+    from mxserve.worker.pair import child_envs
+    dec, pre = child_envs({"DYN_SYSTEM_PORT": "9090", "POD_NAME": "g-decode-abc"},
+                          ["python3", "-m", "dynamo.sglang", "--tp", "2"], ["python3", "-m", "dynamo.sglang"])
+    assert (dec["MXS_DEVICE_OFFSET"], dec["DYN_SYSTEM_PORT"]) == ("0", "9090")
+    assert (pre["MXS_DEVICE_OFFSET"], pre["DYN_SYSTEM_PORT"]) == ("2", "9091")
+    assert dec["MXS_PAIR_ID"] == pre["MXS_PAIR_ID"] == "g-decode-abc"
+    assert dec["MXS_WORKER_ID"] != pre["MXS_WORKER_ID"]
 
 
 def test_invalid_specs_rejected():
