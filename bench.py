@@ -593,8 +593,12 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
     head = agg if agg is not None else dis
     world = ctx.world
     on_gpu = ctx.on_gpu
+    model = info["model"] if on_gpu else a.model
+    metric = BASELINE_METRIC
+    if model != "meta-llama/Llama-3.2-1B-Instruct":  # a labelled side data point, not the headline
+        metric = BASELINE_METRIC.replace("Llama-3.2-1B", model.split("/")[-1])
     line = {
-        "metric": BASELINE_METRIC,
+        "metric": metric,
         "value": head["value"],
         "unit": "tok/s",
         "n_gpus": world,
