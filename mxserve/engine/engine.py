@@ -308,6 +308,20 @@ class AsyncEngine:
             if self._queues.pop(request_id, None) is not None:  # client went away mid-stream
                 self.submit_nowait(self.engine.abort, request_id)
 
+    async def stream_batches(self, request_id: str, q: asyncio.Queue):
+        """Like stream(), but yields every output already queued at once (a list)."""
+        try:
+            while True:
+                outs = [await q.get()]
+                while not outs[-1].finished and not q.empty():
+                    outs.append(q.get_nowait())
+                yield outs
+                if outs[-1].finished:
+                    return
+        finally:
+            if self._queues.pop(request_id, None) is not None:  # client went away mid-stream
+                self.submit_nowait(self.engine.abort, request_id)
+
     async def generate(self, prompt_token_ids: list, sampling: SamplingParams, request_id: Optional[str] = None,
                        disagg_role: Optional[str] = None):
         """Async iterator of StepOutput for one request."""

@@ -194,9 +194,20 @@ class Frontend:
                 if not line.strip():
                     continue
                 d = json.loads(line)
-                if d["t"] < 0:
-                    raise RuntimeError("worker failed the request")
-                yield TokenEvent(d["t"], d["f"], d["r"], d["p"], d["c"], d.get("lp"), d.get("tlp"))
+                toks = d["t"]
+                if not isinstance(toks, list):  # one token per line
+                    if toks < 0:
+                        raise RuntimeError("worker failed the request")
+                    yield TokenEvent(toks, d["f"], d["r"], d["p"], d["c"], d.get("lp"), d.get("tlp"))
+                    continue
+                # a batch: every token that was waiting when the worker wrote the line
+                n = len(toks)
+                lps, tlps = d.get("lp") or [None] * n, d.get("tlp") or [None] * n
+                for i, t in enumerate(toks):
+                    if t < 0:
+                        raise RuntimeError("worker failed the request")
+                    last = i == n - 1
+                    yield TokenEvent(t, d["f"] and last, d["r"] if last else None, d["p"], d["c"], lps[i], tlps[i])
 
     async def generate_tokens(self, model: str, token_ids: list, sampling: dict, rid: str) -> AsyncIterator[TokenEvent]:
         """Route + stream.  A worker that fails before the first token is retried elsewhere; one that
@@ -369,7 +380,7 @@ class Frontend:
             """Yields (text_delta, finish_reason|None, logprob events).  With stop strings, text that
             could still be the start of a stop string is held back until it is disambiguated; the
             log-probs of the tokens behind held-back text travel with the next delta."""
-            detok = IncrementalDetokenizer(tok)
+            detok = IncrementalDetokenizer(tok, prompt_tail=prompt_ids[-5:])
             full, emitted = "", 0
             hold = max((len(x) for x in stops if x), default=1) - 1
             lps: list = []

@@ -57,6 +57,21 @@ def _line(o: StepOutput) -> bytes:
     return (json.dumps(d) + "\n").encode()
 
 
+def _batch_line(outs: list) -> bytes:
+    """Every token of a request that is ready when the stream writes: one NDJSON line (a list of
+    ids).  A consumer that keeps up still gets one token per line; one that falls behind (a busy
+    frontend at tens of thousands of tokens/s) gets fewer, larger lines instead of a backlog."""
+    if len(outs) == 1:
+        return _line(outs[0])
+    last = outs[-1]
+    d = {"t": [o.token_id for o in outs], "f": last.finished, "r": last.finish_reason, "p": last.num_prompt_tokens,
+         "c": last.num_cached_tokens}
+    if any(o.logprob is not None for o in outs):
+        d["lp"] = [o.logprob for o in outs]
+        d["tlp"] = [o.top_logprobs or [] for o in outs]
+    return (json.dumps(d) + "\n").encode()
+
+
 class Worker:
     def __init__(self, wargs: WorkerArgs, engine: Optional[LLMEngine] = None):
         self.wargs = wargs
@@ -114,17 +129,27 @@ class Worker:
         if purl and self.role == "decode":
             q = await self._remote_prefill(rid, toks, sp, purl)
             if q is not None:
-                async for o in self.aeng.stream(rid, q):
-                    yield _line(o)
+                async for outs in self.aeng.stream_batches(rid, q):
+                    yield _batch_line(outs)
                 return
         drop = self.faults.hit("drop_stream")
-        n = 0
-        async for o in self.aeng.generate(toks, sp, rid):
-            n += 1
-            if drop and n > 1:  # fault injection: abort mid-stream
-                await self.aeng.submit(self.engine.abort, rid)
-                raise ConnectionError("fault injection: stream dropped")
-            yield _line(o)
+        if drop:
+            n = 0
+            async for o in self.aeng.generate(toks, sp, rid):
+                n += 1
+                if n > 1:  # fault injection: abort mid-stream
+                    await self.aeng.submit(self.engine.abort, rid)
+                    raise ConnectionError("fault injection: stream dropped")
+                yield _line(o)
+            return
+        q = self.aeng.open_stream(rid)
+        try:
+            await self.aeng.submit(self.engine.add_request, toks, sp, rid, None)
+        except BaseException:
+            self.aeng._queues.pop(rid, None)
+            raise
+        async for outs in self.aeng.stream_batches(rid, q):
+            yield _batch_line(outs)
 
     async def _remote_prefill(self, rid: str, toks: list, sp: SamplingParams, purl: str):
         """Decode side of the disaggregated protocol.  Returns the token queue, or None to fall

@@ -414,3 +414,43 @@ def test_remote_prefill_cancel_releases_reservation():
     finally:
         w.aeng.shutdown()
         lst.close()
+
+
+def test_batched_ndjson_token_lines():
+    """A worker that writes several tokens per NDJSON line (a consumer fell behind) is parsed
+    token by token: same completion text, usage and finish reason as one token per line."""
+    from fastapi import FastAPI
+    from fastapi.responses import StreamingResponse
+
+    from mxserve.engine.engine import StepOutput
+    from mxserve.router.router import WorkerInfo
+    from mxserve.worker.server import _batch_line
+    toks = [ord(c) for c in "hello batched world"]  # byte tokenizer ids (tiny-llama vocab covers ASCII)
+    outs = [StepOutput("x", t, i == len(toks) - 1, "length" if i == len(toks) - 1 else None, 7, 0, i + 1)
+            for i, t in enumerate(toks)]
+    app = FastAPI()
+
+    @app.post("/generate")
+    async def gen():
+        async def body():
+            yield _batch_line(outs[:1])
+            yield _batch_line(outs[1:6])
+            yield _batch_line(outs[6:])
+        return StreamingResponse(body(), media_type="application/x-ndjson")
+
+    ws = Server(app).start()
+    fe = Frontend(router_mode="round_robin")
+    fs = Server(fe.app).start()
+    try:
+        fe.registry.register(WorkerInfo(worker_id="fake", url=ws.url, model=MODEL))
+        r = httpx.post(fs.url + "/v1/completions", json={"model": MODEL, "prompt": "p", "max_tokens": len(toks)},
+                       timeout=30)
+        assert r.status_code == 200, r.text
+        d = r.json()
+        assert d["usage"]["completion_tokens"] == len(toks)
+        assert d["choices"][0]["finish_reason"] == "length"
+        tok = fe.tokenizer(MODEL)
+        assert d["choices"][0]["text"] == tok.decode(toks)
+    finally:
+        fs.stop()
+        ws.stop()

@@ -243,6 +243,16 @@ def test_byte_tokenizer_and_templates():
     d = IncrementalDetokenizer(tok)
     out = "".join(d.add(t) for t in tok.encode("日本語 ok")) + d.flush()
     assert out == "日本語 ok"
+    # windowed decode: same text as one full decode, and the work per token does not grow with n
+    long = "streaming détokenizer, ünïcödé 🙂 " * 40
+    calls = []
+    orig = tok.decode
+    tok.decode = lambda ids, **kw: (calls.append(len(ids)), orig(ids, **kw))[1]
+    d = IncrementalDetokenizer(tok, prompt_tail=tok.encode("prompt "))
+    out = "".join(d.add(t) for t in tok.encode(long)) + d.flush()
+    tok.decode = orig
+    assert out == long
+    assert max(calls) <= 16, max(calls)
     q = render("chatml", [{"role": "user", "content": "hi"}])
     assert q == "<|im_start|>user\nhi<|im_end|>\n<|im_start|>assistant\n"
     assert render("mistral", [{"role": "user", "content": "x"}]) == "<s>[INST] x [/INST]"
