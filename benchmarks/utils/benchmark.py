@@ -67,7 +67,28 @@ async def one_request(sess, url: str, model: str, prompt, osl: int, t_sched: flo
         return {"ok": False, "error": err or "no tokens"}
     out_tokens = usage["completion_tokens"] if usage else n_chunks
     return {"ok": True, "ttft": first - t_sched, "e2e": last - t_sched, "itl": gaps, "out": out_tokens,
-            "in": usage["prompt_tokens"] if usage else None, "start": t0}
+            "in": usage["prompt_tokens"] if usage else None, "start": t0, "sched": t_sched, "first": first,
+            "last": last}
+
+
+def steady_window(results: list, t_a: float, t_b: float) -> dict:
+    """Open-loop steady state: output tokens emitted inside [t_a, t_b] (each request's tokens spread
+    evenly over [first token, last token]) and TTFT of requests scheduled inside it -- the ramp-up
+    before t_a and the drain after the last arrival are excluded, as in bench.py's timed window."""
+    ok = [r for r in results if r["ok"]]
+    toks = 0.0
+    for r in ok:
+        lo, hi = max(r["first"], t_a), min(r["last"], t_b)
+        if hi <= lo:
+            continue
+        span = max(r["last"] - r["first"], 1e-9)
+        toks += (r["out"] - 1) * (hi - lo) / span + (1 if t_a <= r["first"] <= t_b else 0)
+    ttft = [r["ttft"] for r in ok if t_a <= r["sched"] <= t_b]
+    itl = [g for r in ok if t_a <= r["sched"] <= t_b for g in r["itl"]]
+    pct = lambda xs, q: float(np.percentile(xs, q)) * 1e3 if xs else None  # noqa: E731
+    return {"steady_window_s": t_b - t_a, "steady_output_tok_per_s": toks / max(t_b - t_a, 1e-9),
+            "steady_requests": len(ttft), "steady_ttft_ms_p50": pct(ttft, 50), "steady_ttft_ms_p90": pct(ttft, 90),
+            "steady_itl_ms_p50": pct(itl, 50)}
 
 
 def summarize(results: list, wall: float, label: dict) -> dict:
@@ -102,7 +123,7 @@ async def run_concurrency(url, model, conc, n, isl, osl, token_ids, vocab, seed)
     return summarize(results, wall, {"mode": "concurrency", "concurrency": conc, "isl": isl, "osl": osl})
 
 
-async def run_rate(url, model, rate, n, isl, osl, token_ids, vocab, seed):
+async def run_rate(url, model, rate, n, isl, osl, token_ids, vocab, seed, warmup_s: float = 0.0):
     rng = random.Random(seed)
     prompts = [synth_prompt(rng, isl, token_ids, vocab) for _ in range(n)]
     gaps = np.random.default_rng(seed).exponential(1.0 / rate, size=n)
@@ -115,9 +136,13 @@ async def run_rate(url, model, rate, n, isl, osl, token_ids, vocab, seed):
             t += g
             await asyncio.sleep(max(0.0, t - time.perf_counter()))
             tasks.append(asyncio.create_task(one_request(sess, url, model, p, osl, t)))
+        t_arrivals_end = time.perf_counter()
         results = await asyncio.gather(*tasks)
         wall = time.perf_counter() - t0
-    return summarize(list(results), wall, {"mode": "request_rate", "request_rate": rate, "isl": isl, "osl": osl})
+    s = summarize(list(results), wall, {"mode": "request_rate", "request_rate": rate, "isl": isl, "osl": osl})
+    if warmup_s > 0 and t0 + warmup_s < t_arrivals_end:
+        s.update(steady_window(list(results), t0 + warmup_s, t_arrivals_end))
+    return s
 
 
 def _endpoint(url: str) -> str:
@@ -145,6 +170,9 @@ def main(argv=None) -> None:
     ap.add_argument("--token-ids", action="store_true", help="send prompts as token-id lists (exact ISL)")
     ap.add_argument("--vocab", type=int, default=32000)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--warmup-s", type=float, default=float(os.environ.get("BENCH_WARMUP_S", "0")),
+                    help="request-rate points: also report steady-state numbers from this many seconds after "
+                         "the first arrival to the last one (ramp-up and drain excluded)")
     a = ap.parse_args(argv)
     url = _endpoint(a.endpoint_url)
     out_dir = os.path.join(a.output_dir, a.benchmark_name)
@@ -159,7 +187,8 @@ def main(argv=None) -> None:
         print(json.dumps({k: v for k, v in s.items() if k != "errors"}), flush=True)
     for r in [float(x) for x in a.request_rate.split(",") if x.strip()]:
         n = a.num_requests or max(int(r * 30), 16)
-        s = asyncio.run(run_rate(url, a.model, r, n, a.isl, a.osl, a.token_ids, a.vocab, a.seed + int(r * 100)))
+        s = asyncio.run(run_rate(url, a.model, r, n, a.isl, a.osl, a.token_ids, a.vocab, a.seed + int(r * 100),
+                                 a.warmup_s))
         points.append(s)
         with open(os.path.join(out_dir, f"rate_{r:g}.json"), "w") as f:
             json.dump(s, f, indent=2)

@@ -259,14 +259,20 @@ class AsyncEngine:
             self._deliver(outs)
 
     def _deliver(self, outs) -> None:
+        """One cross-thread wakeup per event loop per step (not per token): at ~20k tokens/s a
+        call_soon_threadsafe per token costs the serving process a self-pipe write each and fights
+        the engine thread for the GIL."""
+        by_loop: dict = {}
         for o in outs:
             ent = self._queues.get(o.request_id)
             if ent is None:
                 continue
             loop, q = ent
-            loop.call_soon_threadsafe(q.put_nowait, o)
+            by_loop.setdefault(loop, []).append((q, o))
             if o.finished:
                 self._queues.pop(o.request_id, None)
+        for loop, items in by_loop.items():
+            loop.call_soon_threadsafe(_put_many, items)
 
     def _fail_all(self) -> list:
         self.engine._inflight = None  # the failed step's results are never collected
@@ -339,6 +345,11 @@ class AsyncEngine:
         self._stop = True
         self._wake.set()
         self._thread.join(timeout=5)
+
+
+def _put_many(items: list) -> None:
+    for q, o in items:
+        q.put_nowait(o)
 
 
 def _set_result(fut: asyncio.Future, r, e) -> None:
