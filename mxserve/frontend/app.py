@@ -41,6 +41,24 @@ log = logging.getLogger("mxserve.frontend")
 MAX_N = 16  # choices per request (`n`)
 
 
+def _parse_token_line(d: dict, out: list) -> None:
+    """One NDJSON line of the worker's /generate stream -> TokenEvents (a line holds one token, or a
+    list of every token that was ready when the worker wrote it)."""
+    toks = d["t"]
+    if not isinstance(toks, list):
+        if toks < 0:
+            raise RuntimeError("worker failed the request")
+        out.append(TokenEvent(toks, d["f"], d["r"], d["p"], d["c"], d.get("lp"), d.get("tlp")))
+        return
+    n = len(toks)
+    lps, tlps = d.get("lp") or [None] * n, d.get("tlp") or [None] * n
+    for i, t in enumerate(toks):
+        if t < 0:
+            raise RuntimeError("worker failed the request")
+        last = i == n - 1
+        out.append(TokenEvent(t, d["f"] and last, d["r"] if last else None, d["p"], d["c"], lps[i], tlps[i]))
+
+
 async def _merge(gens: list):
     """Interleave async generators as items arrive: yields (generator index, item).  The first
     exception ends the merge and is raised; the other generators are closed."""
@@ -110,11 +128,17 @@ class LocalWorker:
         self.aeng = aeng
         self.model = model
 
-    async def generate(self, token_ids, sampling: dict, request_id: str, prefill_url=None) -> AsyncIterator[TokenEvent]:
+    async def generate(self, token_ids, sampling: dict, request_id: str, prefill_url=None) -> AsyncIterator[list]:
         from ..worker.server import _sampling
-        async for o in self.aeng.generate(token_ids, _sampling(sampling), request_id):
-            yield TokenEvent(o.token_id, o.finished, o.finish_reason, o.num_prompt_tokens, o.num_cached_tokens,
-                             o.logprob, o.top_logprobs)
+        q = self.aeng.open_stream(request_id)
+        try:
+            await self.aeng.submit(self.aeng.engine.add_request, token_ids, _sampling(sampling), request_id, None)
+        except BaseException:
+            self.aeng._queues.pop(request_id, None)
+            raise
+        async for outs in self.aeng.stream_batches(request_id, q):
+            yield [TokenEvent(o.token_id, o.finished, o.finish_reason, o.num_prompt_tokens, o.num_cached_tokens,
+                              o.logprob, o.top_logprobs) for o in outs]
 
 
 class Frontend:
@@ -178,10 +202,13 @@ class Frontend:
 
     # ---------------------------------------------------------------- request plane
     async def _worker_stream(self, w: WorkerInfo, token_ids, sampling: dict, rid: str,
-                             prefill_url: Optional[str]) -> AsyncIterator[TokenEvent]:
+                             prefill_url: Optional[str]) -> AsyncIterator[list]:
+        """Yields LISTS of TokenEvent: everything that arrived since the last read.  While the
+        frontend keeps up that is one token; when it falls behind, a batch flows through the rest of
+        the pipeline (detokenize, one SSE chunk) at the cost of one."""
         if w.url.startswith("local://"):
-            async for ev in self.local[w.model].generate(token_ids, sampling, rid, prefill_url):
-                yield ev
+            async for evs in self.local[w.model].generate(token_ids, sampling, rid, prefill_url):
+                yield evs
             return
         sess = await self.http()
         body = {"request_id": rid, "token_ids": token_ids, "sampling": sampling}
@@ -190,24 +217,20 @@ class Frontend:
         async with sess.post(w.url.rstrip("/") + "/generate", json=body) as r:
             if r.status != 200:
                 raise ConnectionError(f"worker {w.worker_id} returned {r.status}")
-            async for line in r.content:
-                if not line.strip():
-                    continue
-                d = json.loads(line)
-                toks = d["t"]
-                if not isinstance(toks, list):  # one token per line
-                    if toks < 0:
-                        raise RuntimeError("worker failed the request")
-                    yield TokenEvent(toks, d["f"], d["r"], d["p"], d["c"], d.get("lp"), d.get("tlp"))
-                    continue
-                # a batch: every token that was waiting when the worker wrote the line
-                n = len(toks)
-                lps, tlps = d.get("lp") or [None] * n, d.get("tlp") or [None] * n
-                for i, t in enumerate(toks):
-                    if t < 0:
-                        raise RuntimeError("worker failed the request")
-                    last = i == n - 1
-                    yield TokenEvent(t, d["f"] and last, d["r"] if last else None, d["p"], d["c"], lps[i], tlps[i])
+            buf = b""
+            async for data in r.content.iter_any():
+                buf += data
+                *lines, buf = buf.split(b"\n")
+                evs = []
+                for line in lines:
+                    if line.strip():
+                        _parse_token_line(json.loads(line), evs)
+                if evs:
+                    yield evs
+            if buf.strip():
+                evs = []
+                _parse_token_line(json.loads(buf), evs)
+                yield evs
 
     async def generate_tokens(self, model: str, token_ids: list, sampling: dict, rid: str) -> AsyncIterator[TokenEvent]:
         """Route + stream.  A worker that fails before the first token is retried elsewhere; one that
@@ -238,10 +261,10 @@ class Frontend:
                 self.metrics.kv_hit.labels(model).inc(overlap)
             w.inflight += 1
             try:
-                async for ev in self._worker_stream(w, ids, sp, rid, purl):
-                    generated.append(ev.token_id)
-                    yield ev
-                    if ev.finished:
+                async for evs in self._worker_stream(w, ids, sp, rid, purl):
+                    generated.extend(ev.token_id for ev in evs)
+                    yield evs
+                    if evs[-1].finished:
                         return
                 raise ConnectionError(f"worker {w.worker_id} ended the stream early")
             except _STREAM_ERRORS as e:
@@ -385,12 +408,14 @@ class Frontend:
             hold = max((len(x) for x in stops if x), default=1) - 1
             lps: list = []
             sub_rid, sub_sp = sub_request(idx)
-            async for ev in self.generate_tokens(model, prompt_ids, sub_sp, sub_rid):
-                on_token(idx)
-                eos_hit = ev.finished and ev.finish_reason == "stop" and ev.token_id in tok.eos_token_ids
-                full += "" if eos_hit else detok.add(ev.token_id)
-                if want_lp and not eos_hit and ev.logprob is not None:
-                    lps.append(ev)
+            async for evs in self.generate_tokens(model, prompt_ids, sub_sp, sub_rid):
+                for ev in evs:  # a batch becomes one delta
+                    on_token(idx)
+                    eos_hit = ev.finished and ev.finish_reason == "stop" and ev.token_id in tok.eos_token_ids
+                    full += "" if eos_hit else detok.add(ev.token_id)
+                    if want_lp and not eos_hit and ev.logprob is not None:
+                        lps.append(ev)
+                ev = evs[-1]
                 if ev.finished:
                     full += detok.flush()
                 reason = ("stop" if ev.finish_reason == "abort" else ev.finish_reason) if ev.finished else None
