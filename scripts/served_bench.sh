@@ -36,3 +36,13 @@ B=$!
     echo "$(date +%s) $(ps -o pcpu= -p "$FE") $(ps -o pcpu= -p "$W") $(ps -o pcpu= -p "$B")"; sleep 5
   done ) > "$OUT/cpu_fe_worker_client.txt" &
 wait "$B"
+curl -sf "http://127.0.0.1:$FE_PORT/metrics" > "$OUT/frontend_metrics.txt" || true
+python3 - "$OUT/frontend_metrics.txt" <<'PY'
+import sys
+from mxserve.planner.planner import parse_prometheus
+m = parse_prometheus(open(sys.argv[1]).read())
+n = m.get("dynamo_frontend_time_to_first_token_seconds_count", 0)
+if n:
+    print("[served] frontend-side mean TTFT %.1f ms over %d requests (request received -> first token out)"
+          % (1e3 * m["dynamo_frontend_time_to_first_token_seconds_sum"] / n, n))
+PY
