@@ -17,6 +17,8 @@ PLURALS = {
     "Secret": ("v1", "secrets"), "Pod": ("v1", "pods"), "Endpoints": ("v1", "endpoints"), "Namespace": ("v1", "namespaces"), "Node": ("v1", "nodes"),
     "PersistentVolumeClaim": ("v1", "persistentvolumeclaims"), "Job": ("batch/v1", "jobs"),
     "PodMonitor": ("monitoring.coreos.com/v1", "podmonitors"),
+    "ServiceAccount": ("v1", "serviceaccounts"), "Role": ("rbac.authorization.k8s.io/v1", "roles"),
+    "RoleBinding": ("rbac.authorization.k8s.io/v1", "rolebindings"),
     "DynamoGraphDeployment": ("nvidia.com/v1alpha1", "dynamographdeployments"),
     "DynamoGraphDeploymentRequest": ("nvidia.com/v1alpha1", "dynamographdeploymentrequests"),
     "DynamoComponentDeployment": ("nvidia.com/v1alpha1", "dynamocomponentdeployments"),

@@ -7,6 +7,8 @@ from __future__ import annotations
 import argparse
 import copy
 import itertools
+import os
+import threading
 import time
 import uuid
 
@@ -51,6 +53,11 @@ class FakeApiServer:
         self.store: dict[tuple, dict] = {}  # (group/version, plural, ns, name) -> obj
         self.auto_ready = auto_ready
         self.endpoints_ready = True  # tests flip it to simulate pods that never become endpoints
+        # Jobs: `job_runner(job)` runs in a thread when a Job is created (default: run the mxserve
+        # profiler's command in-process against this server, needs `url`), then the Job succeeds
+        self.url: str | None = None
+        self.job_runner = self._run_profiler_job
+        self.jobs_run: list = []
         self.log: list = []
         self._rv = itertools.count(1)
         for i in range(nodes):
@@ -88,6 +95,36 @@ class FakeApiServer:
                 "subsets": [{"addresses": [{"ip": "10.244.0.10"}], "ports": ports}] if self.endpoints_ready else []}
         return obj
 
+    def _run_profiler_job(self, job: dict) -> None:
+        cmd = job["spec"]["template"]["spec"]["containers"][0]["command"]
+        if cmd[:3] != ["python3", "-m", "mxserve.profiler.sla"] or self.url is None:
+            return
+        args = list(cmd[3:])
+        try:
+            import torch
+            if "--measure" in args and not torch.cuda.is_available():
+                args.remove("--measure")  # CPU test box: the roofline stands in for the live timings
+        except ImportError:
+            pass
+        os.environ["MXS_KUBE_SERVER"] = self.url
+        from ..profiler import sla
+        sla.main(args)
+
+    def _start_job(self, gv, ns, job: dict) -> None:
+        name = job["metadata"]["name"]
+
+        def run():
+            ok = True
+            try:
+                self.job_runner(copy.deepcopy(job))
+            except BaseException:  # noqa: BLE001 - a failing Job
+                ok = False
+            self.jobs_run.append((name, ok))
+            cur = self.store.get((gv, "jobs", ns, name))
+            if cur is not None:
+                cur["status"] = {"succeeded": 1} if ok else {"failed": 2}
+        threading.Thread(target=run, daemon=True).start()
+
     def objects(self, plural: str, ns: str | None = None) -> list:
         return [o for (gv, p, n, _), o in self.store.items() if p == plural and (ns is None or n == ns)]
 
@@ -108,7 +145,10 @@ class FakeApiServer:
                     nm = body["metadata"]["name"]
                     if (gv, plural, ns, nm) in srv.store:
                         return 409, {"kind": "Status", "reason": "AlreadyExists", "message": f"{nm} exists"}
-                    return 201, copy.deepcopy(srv._put(gv, plural, ns, copy.deepcopy(body)))
+                    obj = srv._put(gv, plural, ns, copy.deepcopy(body))
+                    if plural == "jobs" and srv.job_runner is not None:
+                        srv._start_job(gv, ns, obj)
+                    return 201, copy.deepcopy(obj)
                 return 405, {}
             cur = srv.store.get(key)
             if cur is None:

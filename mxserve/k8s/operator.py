@@ -2,8 +2,11 @@
 controller-manager).
 
 Level-triggered polling reconcile (robust to missed events, no watch-resume bookkeeping):
-  DGDR -> SLA profiler (mxserve.profiler.sla, MI355X roofline) -> DGD rendered from the request's
-          ConfigMap template (+ workersImage override) -> applied if autoApply; results in status
+  DGDR -> profiling Job from `profilerImage` running mxserve.profiler.sla (live timings on one GPU
+          when useAiConfigurator is false, else the MI355X roofline), results published in a
+          ConfigMap (state Profiling until the Job ends) -> DGD rendered from the request's ConfigMap
+          template (+ workersImage override) -> applied if autoApply; results in status.
+          MXS_PROFILER_MODE=inline (or no profilerImage) runs the roofline in the operator instead.
   DGD  -> DCD per service -> Deployment + Service + PodMonitor; DGD status.state = successful once
           every Deployment has its replicas ready
 Orphans (children whose DGD is gone) are deleted, as the Kubernetes garbage collector would via
@@ -12,7 +15,9 @@ ownerReferences.  `python -m mxserve.k8s.operator [--namespace NS] [--interval S
 from __future__ import annotations
 
 import argparse
+import json
 import logging
+import os
 import time
 from typing import Optional
 
@@ -21,7 +26,8 @@ import yaml
 from ..profiler import sla
 from .client import ApiError, KubeClient
 from .resources import (API_VERSION, DCD_KIND, DGD_KIND, DGDR_KIND, NS_LABEL, ValidationError,
-                        apply_plan_to_template, parse_dgd, parse_dgdr, render_children, render_dcds)
+                        apply_plan_to_template, parse_dgd, parse_dgdr, render_children, render_dcds,
+                        render_profiler_job)
 
 log = logging.getLogger("mxserve.operator")
 
@@ -97,7 +103,13 @@ class Operator:
             st = {"state": "Failed", "message": str(e)}
             self.k.patch_status(DGDR_KIND, obj["metadata"]["name"], ns, st)
             return st
-        p = sla.plan(r.model, r.isl, r.osl, r.ttft_ms, r.itl_ms, system="mi355x")
+        if r.profiler_image and os.environ.get("MXS_PROFILER_MODE", "job") == "job":
+            p = self._profiling_job(r, ns)
+            if isinstance(p, dict) and "state" in p:  # still profiling, or the Job failed
+                self.k.patch_status(DGDR_KIND, r.name, ns, p)
+                return p
+        else:
+            p = sla.plan(r.model, r.isl, r.osl, r.ttft_ms, r.itl_ms, system="mi355x")
         if not p["feasible"]:
             st = {"state": "Failed", "message": "SLA not reachable on one node", "profilingResults": p}
             self.k.patch_status(DGDR_KIND, r.name, ns, st)
@@ -127,6 +139,26 @@ class Operator:
             self.k.apply(dgd)
         self.k.patch_status(DGDR_KIND, r.name, ns, st)
         return st
+
+    def _profiling_job(self, r, ns: str) -> dict:
+        """Start the DGDR's profiling Job once; return its results, or a status while it runs."""
+        job_name, cm_name = f"{r.name}-profile", f"{r.name}-profiling-results"
+        job = self.k.get("Job", job_name, ns)
+        if job is None:
+            for obj in render_profiler_job(r, job_name, cm_name):
+                self.k.apply(obj)
+            log.info("DGDR %s/%s: profiling Job %s started (%s)", ns, r.name, job_name,
+                     "live on 1 GPU" if r.measure else "roofline")
+            return {"state": "Profiling", "message": f"Job {job_name} started", "profilingJob": job_name}
+        js = job.get("status") or {}
+        if int(js.get("succeeded") or 0) >= 1:
+            cm = self.k.get("ConfigMap", cm_name, ns)
+            if cm is None or "results.json" not in (cm.get("data") or {}):
+                return {"state": "Failed", "message": f"Job {job_name} succeeded without publishing {cm_name}"}
+            return json.loads(cm["data"]["results.json"])
+        if int(js.get("failed") or 0) > int((job.get("spec") or {}).get("backoffLimit", 1)):
+            return {"state": "Failed", "message": f"profiling Job {job_name} failed", "profilingJob": job_name}
+        return {"state": "Profiling", "message": f"Job {job_name} running", "profilingJob": job_name}
 
     # ------------------------------------------------------------------ loop
     def gc_orphans(self) -> None:

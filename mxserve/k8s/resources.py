@@ -336,6 +336,8 @@ class RequestSpec:
     workers_image: Optional[str]
     auto_apply: bool
     uid: Optional[str] = None
+    profiler_image: Optional[str] = None
+    measure: bool = False  # live profiling on a GPU (useAiConfigurator: false) vs the roofline model
 
 
 def parse_dgdr(obj: dict, namespace: Optional[str] = None) -> RequestSpec:
@@ -359,7 +361,46 @@ def parse_dgdr(obj: dict, namespace: Optional[str] = None) -> RequestSpec:
         isl=int(sla.get("isl", 4000)), osl=int(sla.get("osl", 500)), ttft_ms=float(sla.get("ttft", 600)),
         itl_ms=float(sla.get("itl", 25)), system=str(sweep.get("aicSystem", "mi355x")),
         workers_image=(spec.get("deploymentOverrides") or {}).get("workersImage"),
-        auto_apply=bool(spec.get("autoApply", False)), uid=meta.get("uid"))
+        auto_apply=bool(spec.get("autoApply", False)), uid=meta.get("uid"),
+        profiler_image=pc.get("profilerImage"),
+        measure="useAiConfigurator" in sweep and not bool(sweep.get("useAiConfigurator")))
+
+
+PROFILER_SA = "mxserve-profiler"
+
+
+def render_profiler_job(r: RequestSpec, job: str, results_cm: str) -> list[dict]:
+    """The DGDR profiling Job (reference: the Dynamo operator's profiling job from `profilerImage`,
+    examples/dgdr/trtllm/dgdr.yaml:14-31) and the RBAC it needs to publish its results ConfigMap.
+    A live (`measure`) run takes one GPU and times this engine; otherwise it runs the roofline."""
+    owner = _owner(DGDR_KIND, r.name, r.uid)
+    ns = r.namespace
+    cmd = ["python3", "-m", "mxserve.profiler.sla", "--model", r.model, "--isl", str(r.isl), "--osl", str(r.osl),
+           "--ttft", f"{r.ttft_ms:g}", "--itl", f"{r.itl_ms:g}", "--system", r.system,
+           "--output-configmap", results_cm, "--namespace", ns]
+    if r.measure:
+        cmd.append("--measure")
+    c = {"name": "profiler", "image": r.profiler_image or DEFAULT_IMAGE, "command": cmd,
+         "env": [{"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}]}
+    if r.measure:
+        c["resources"] = {"limits": {GPU_RESOURCE: "1"}, "requests": {GPU_RESOURCE: "1"}}
+    labels = {"app.kubernetes.io/managed-by": "mxserve-operator", "mxserve.io/dgdr": r.name}
+    return [
+        {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": PROFILER_SA, "namespace": ns}},
+        {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "Role",
+         "metadata": {"name": PROFILER_SA, "namespace": ns},
+         "rules": [{"apiGroups": [""], "resources": ["configmaps"], "verbs": ["get", "create", "update", "patch"]}]},
+        {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "RoleBinding",
+         "metadata": {"name": PROFILER_SA, "namespace": ns},
+         "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "Role", "name": PROFILER_SA},
+         "subjects": [{"kind": "ServiceAccount", "name": PROFILER_SA, "namespace": ns}]},
+        {"apiVersion": "batch/v1", "kind": "Job",
+         "metadata": {"name": job, "namespace": ns, "labels": labels, "ownerReferences": owner},
+         "spec": {"backoffLimit": 1, "ttlSecondsAfterFinished": 3600,
+                  "template": {"metadata": {"labels": labels},
+                               "spec": {"restartPolicy": "Never", "serviceAccountName": PROFILER_SA,
+                                        "containers": [c]}}}},
+    ]
 
 
 def apply_plan_to_template(template: dict, plan: dict, req: RequestSpec) -> dict:

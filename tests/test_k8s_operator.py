@@ -2,6 +2,7 @@
 example manifest (ours, and the reference's when mounted)."""
 import glob
 import os
+import time
 
 import pytest
 import yaml
@@ -140,6 +141,7 @@ def test_invalid_specs_rejected():
 def cluster():
     fake = FakeApiServer()
     srv = Server(fake.app).start()
+    fake.url = srv.url
     yield fake, KubeClient(server=srv.url)
     srv.stop()
 
@@ -184,6 +186,23 @@ def test_reconcile_dgdr_autoapply(cluster):
     req["metadata"]["namespace"] = ns
     k.create(req)
     op = Operator(k)
+    op.reconcile_all()
+    # the operator started the profiling Job (live timings on one GPU: useAiConfigurator false) with
+    # the profilerImage and the RBAC to publish its results; state Profiling until the Job ends
+    st = k.get("DynamoGraphDeploymentRequest", "qwen-trtllm", ns)["status"]
+    assert st["state"] == "Profiling", st
+    job = k.get("Job", "qwen-trtllm-profile", ns)
+    c = job["spec"]["template"]["spec"]["containers"][0]
+    assert c["image"] == req["spec"]["profilingConfig"]["profilerImage"]
+    assert c["command"][:3] == ["python3", "-m", "mxserve.profiler.sla"] and "--measure" in c["command"]
+    assert c["resources"]["limits"] == {"amd.com/gpu": "1"}
+    assert k.get("RoleBinding", "mxserve-profiler", ns) is not None
+    for _ in range(200):  # the fake cluster runs the Job's command in-process
+        if fake.jobs_run:
+            break
+        time.sleep(0.05)
+    assert fake.jobs_run == [("qwen-trtllm-profile", True)]
+    assert "results.json" in k.get("ConfigMap", "qwen-trtllm-profiling-results", ns)["data"]
     op.reconcile_all()
     st = k.get("DynamoGraphDeploymentRequest", "qwen-trtllm", ns)["status"]
     assert st["state"] == "Successful", st

@@ -88,3 +88,20 @@ def test_planner_agg_graph_and_dry_run(api):
     rec = p.step()
     assert rec["changes"]["W"] == 8  # capped by the node's GPUs
     assert api.get("DynamoGraphDeployment", "g", "ns")["spec"]["services"]["W"]["replicas"] == 1  # dry run
+
+
+def test_sla_plan_from_measurements():
+    """--measure results replace the roofline: the measured TTFT and ITL(batch) curve decide the
+    plan; a slower measured decode yields a smaller batch at the same ITL target."""
+    from mxserve.profiler import sla
+    fast = {"ttft_ms": 60.0, "decode_itl_ms": {"1": 2.0, "64": 4.0, "256": 10.0}}
+    slow = {"ttft_ms": 60.0, "decode_itl_ms": {"1": 2.0, "64": 8.0, "256": 30.0}}
+    pf = sla.plan("Qwen/Qwen3-0.6B", 4000, 500, 600, 25, measured=fast)
+    ps = sla.plan("Qwen/Qwen3-0.6B", 4000, 500, 600, 25, measured=slow)
+    assert pf["source"] == "measured" and pf["measurements"] == fast and pf["feasible"]
+    assert pf["agg"]["ttft_ms"] == 60.0 and pf["disagg"]["prefill"]["ttft_ms"] == 60.0
+    assert ps["agg"]["batch"] < pf["agg"]["batch"]
+    m = sla.Measured(slow)
+    assert m.itl(64) == 8.0 / 1e3 and abs(m.itl(160) - 19e-3) < 1e-9 and m.itl(512) > m.itl(256)
+    # a TTFT target below the measured prefill split over 8 GPUs is infeasible
+    assert not sla.plan("Qwen/Qwen3-0.6B", 4000, 500, 5, 25, measured=fast)["feasible"]

@@ -35,6 +35,7 @@ def test_shell_syntax():
 def cluster():
     fake = FakeApiServer()
     srv = Server(fake.app).start()
+    fake.url = srv.url
     k = KubeClient(server=srv.url)
     op = Operator(k)
     stop = threading.Event()
