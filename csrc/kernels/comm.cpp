@@ -28,7 +28,10 @@ void launch_custom_allreduce(unsigned short*, const unsigned short*, long, const
 void launch_custom_allreduce_2shot(unsigned short*, const unsigned short*, long, const ArPeers&, int, int, long,
                                    unsigned*, unsigned*, hipStream_t);
 void launch_ipc_all_to_all(void*, const void*, long, const ArPeers&, int, int, long, unsigned*, unsigned*,
-                           hipStream_t);
+                           hipStream_t, const int*, long);
+void launch_ep_route(int*, int*, int*, const int*, int, int, int, int, int, int, hipStream_t);
+void launch_ep_gather_rows(unsigned short*, const unsigned short*, const int*, int, int, int, hipStream_t);
+void launch_ep_segment_rows(int*, const int*, int, int, hipStream_t);
 }
 
 namespace {
@@ -133,7 +136,8 @@ void custom_allreduce(at::Tensor out, at::Tensor x, std::vector<int64_t> recv_pt
 
 // equal splits: out/in hold N segments of seg_bytes each; segment d of `in` goes to rank d
 void ipc_all_to_all(at::Tensor out, at::Tensor in, std::vector<int64_t> recv_ptrs, std::vector<int64_t> flag_ptrs,
-                    int64_t rank, int64_t slot_bytes, int64_t epochs_ptr, int64_t err_ptr) {
+                    int64_t rank, int64_t slot_bytes, int64_t epochs_ptr, int64_t err_ptr,
+                    c10::optional<at::Tensor> push_rows, int64_t row_bytes) {
   TORCH_CHECK(in.is_cuda() && in.is_contiguous() && out.is_contiguous(), "contiguous GPU tensors");
   TORCH_CHECK(in.scalar_type() == out.scalar_type() && in.numel() == out.numel(), "in/out shape");
   const int n = static_cast<int>(recv_ptrs.size());
@@ -147,9 +151,52 @@ void ipc_all_to_all(at::Tensor out, at::Tensor in, std::vector<int64_t> recv_ptr
     peers.recv[r] = reinterpret_cast<char*>(recv_ptrs[r]);
     peers.flags[r] = reinterpret_cast<unsigned*>(flag_ptrs[r]);
   }
+  const int* pr = nullptr;
+  if (push_rows.has_value()) {
+    const at::Tensor& t = *push_rows;
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kInt && t.numel() == n && t.is_contiguous(),
+                "push_rows: int32 GPU tensor, one count per rank");
+    TORCH_CHECK(row_bytes > 0 && seg % row_bytes == 0 && row_bytes % 4 == 0, "row_bytes must divide the segment");
+    pr = t.data_ptr<int>();
+  }
   mxs::launch_ipc_all_to_all(out.data_ptr(), in.data_ptr(), seg, peers, static_cast<int>(rank), n, slot_bytes,
                              reinterpret_cast<unsigned*>(epochs_ptr), reinterpret_cast<unsigned*>(err_ptr),
+                             c10::hip::getCurrentHIPStream().stream(), pr, row_bytes);
+}
+
+// ---- EP dispatch (csrc/kernels/ep.hip)
+void ep_route(at::Tensor slot, at::Tensor send_e, at::Tensor counts, at::Tensor topk_ids, int64_t valid_rows,
+              int64_t e_local, int64_t nranks, int64_t C) {
+  TORCH_CHECK(topk_ids.is_cuda() && topk_ids.scalar_type() == at::kInt && topk_ids.dim() == 2 &&
+                  topk_ids.is_contiguous(), "topk_ids: int32 [S, k] GPU tensor");
+  const int P = topk_ids.numel(), k = topk_ids.size(1);
+  TORCH_CHECK(nranks >= 1 && nranks <= 8 && e_local >= 1 && C >= 0, "1..8 ranks");
+  TORCH_CHECK(slot.scalar_type() == at::kInt && slot.numel() == P, "slot: int32 [P]");
+  TORCH_CHECK(send_e.scalar_type() == at::kInt && send_e.numel() == nranks * C, "send_e: int32 [nranks * C]");
+  TORCH_CHECK(counts.scalar_type() == at::kInt && counts.numel() == nranks, "counts: int32 [nranks]");
+  mxs::launch_ep_route(slot.data_ptr<int>(), send_e.data_ptr<int>(), counts.data_ptr<int>(), topk_ids.data_ptr<int>(),
+                       P, k, static_cast<int>(valid_rows), static_cast<int>(e_local), static_cast<int>(nranks),
+                       static_cast<int>(C), c10::hip::getCurrentHIPStream().stream());
+}
+
+void ep_gather_rows(at::Tensor send_x, at::Tensor hs, at::Tensor slot, int64_t k) {
+  TORCH_CHECK(send_x.is_cuda() && hs.is_cuda() && slot.is_cuda(), "GPU tensors");
+  TORCH_CHECK(send_x.scalar_type() == at::kBFloat16 && hs.scalar_type() == at::kBFloat16, "bf16 rows");
+  TORCH_CHECK(send_x.is_contiguous() && hs.is_contiguous() && slot.scalar_type() == at::kInt, "layout");
+  const int H = hs.size(1);
+  TORCH_CHECK(H % 8 == 0 && send_x.size(1) == H && slot.numel() == hs.size(0) * k, "shapes");
+  mxs::launch_ep_gather_rows(reinterpret_cast<unsigned short*>(send_x.data_ptr()),
+                             reinterpret_cast<const unsigned short*>(hs.data_ptr()), slot.data_ptr<int>(),
+                             static_cast<int>(slot.numel()), static_cast<int>(k), H,
                              c10::hip::getCurrentHIPStream().stream());
+}
+
+void ep_segment_rows(at::Tensor counts, at::Tensor ids, int64_t C) {
+  TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kInt && counts.scalar_type() == at::kInt, "int32 GPU");
+  const int nseg = counts.numel();
+  TORCH_CHECK(ids.numel() == nseg * C, "ids: [nseg * C]");
+  mxs::launch_ep_segment_rows(counts.data_ptr<int>(), ids.data_ptr<int>(), nseg, static_cast<int>(C),
+                              c10::hip::getCurrentHIPStream().stream());
 }
 
 }  // namespace
@@ -163,7 +210,12 @@ void register_comm(pybind11::module_& m) {
   m.def("custom_allreduce", &custom_allreduce, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("recv_ptrs"),
         pybind11::arg("flag_ptrs"), pybind11::arg("rank"), pybind11::arg("slot_elems"), pybind11::arg("epochs_ptr"),
         pybind11::arg("err_ptr"), pybind11::arg("two_shot") = false);
-  m.def("ipc_all_to_all", &ipc_all_to_all);
+  m.def("ipc_all_to_all", &ipc_all_to_all, pybind11::arg("out"), pybind11::arg("in"), pybind11::arg("recv_ptrs"),
+        pybind11::arg("flag_ptrs"), pybind11::arg("rank"), pybind11::arg("slot_bytes"), pybind11::arg("epochs_ptr"),
+        pybind11::arg("err_ptr"), pybind11::arg("push_rows") = pybind11::none(), pybind11::arg("row_bytes") = 0);
+  m.def("ep_route", &ep_route);
+  m.def("ep_gather_rows", &ep_gather_rows);
+  m.def("ep_segment_rows", &ep_segment_rows);
   m.def("ipc_export_pool", &export_pool);
   // may block on the peer driver: let watchdog threads run meanwhile
   m.def("ipc_open_pool", &open_pool, pybind11::call_guard<pybind11::gil_scoped_release>());

@@ -220,10 +220,13 @@ void launch_custom_allreduce_2shot(bf16_t* out, const bf16_t* x, long n, const A
 // of the output is read from this rank's slot [par][r].  Every rank pushes on all N-1 links at
 // once.  Same epochs / flags / parity rule as the all-reduce kernels (calls of both kinds may
 // interleave: every rank issues the same sequence).  V = uint4 when segments are 16-byte multiples.
+// push_rows (optional, device): segment d carries only its first push_rows[d] rows of row_v vectors
+// over the link (variable-size EP dispatch: the rest of the segment is capacity, not payload).
 template <typename V>
 __global__ void __launch_bounds__(512) ipc_all_to_all_kernel(V* __restrict__ out, const V* __restrict__ in,
                                                              long seg_v, ArPeers peers, int rank, int nranks,
-                                                             long slot_bytes, unsigned* epochs, unsigned* err) {
+                                                             long slot_bytes, unsigned* epochs, unsigned* err,
+                                                             const int* __restrict__ push_rows, long row_v) {
   const int b = blockIdx.x;
   const long per = (seg_v + gridDim.x - 1) / gridDim.x;
   const long v0 = b * per, v1 = min(seg_v, v0 + per);
@@ -235,7 +238,8 @@ __global__ void __launch_bounds__(512) ipc_all_to_all_kernel(V* __restrict__ out
   for (int d = 0; d < nranks; ++d) {
     V* dst = reinterpret_cast<V*>(peers.recv[d] + (static_cast<long>(par) * nranks + rank) * slot_bytes);
     const V* src = in + d * seg_v;
-    for (long v = v0 + threadIdx.x; v < v1; v += blockDim.x) dst[v] = src[v];
+    const long lim = push_rows == nullptr ? v1 : min(v1, static_cast<long>(push_rows[d]) * row_v);
+    for (long v = v0 + threadIdx.x; v < lim; v += blockDim.x) dst[v] = src[v];
   }
   __threadfence_system();
   __syncthreads();
@@ -252,14 +256,16 @@ __global__ void __launch_bounds__(512) ipc_all_to_all_kernel(V* __restrict__ out
 }
 
 void launch_ipc_all_to_all(void* out, const void* in, long seg_bytes, const ArPeers& peers, int rank, int nranks,
-                           long slot_bytes, unsigned* epochs, unsigned* err, hipStream_t s) {
-  if (seg_bytes % 16 == 0)
+                           long slot_bytes, unsigned* epochs, unsigned* err, hipStream_t s, const int* push_rows,
+                           long row_bytes) {
+  if (seg_bytes % 16 == 0 && (push_rows == nullptr || row_bytes % 16 == 0))
     hipLaunchKernelGGL(ipc_all_to_all_kernel<uint4>, dim3(kArMaxBlocks), dim3(512), 0, s, static_cast<uint4*>(out),
-                       static_cast<const uint4*>(in), seg_bytes / 16, peers, rank, nranks, slot_bytes, epochs, err);
+                       static_cast<const uint4*>(in), seg_bytes / 16, peers, rank, nranks, slot_bytes, epochs, err,
+                       push_rows, row_bytes / 16);
   else
     hipLaunchKernelGGL(ipc_all_to_all_kernel<uint32_t>, dim3(kArMaxBlocks), dim3(512), 0, s,
                        static_cast<uint32_t*>(out), static_cast<const uint32_t*>(in), seg_bytes / 4, peers, rank,
-                       nranks, slot_bytes, epochs, err);
+                       nranks, slot_bytes, epochs, err, push_rows, row_bytes / 4);
   MXS_CHECK_LAUNCH();
 }
 

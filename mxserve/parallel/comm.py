@@ -93,13 +93,15 @@ def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
     if st.tp_size == 1:
         return x
     car = st.custom_ar
-    if car is not None and x.is_cuda and dim in (-1, x.dim() - 1):
+    if car is not None and x.is_cuda and dim in (0, -1, x.dim() - 1):
         # every rank pushes its shard to every peer through the IPC all-to-all (one xGMI hop per
         # link, graph-capturable whatever the process group's backend)
         rep = x.contiguous().unsqueeze(0).expand(st.tp_size, *x.shape).contiguous()
         if car.can_all_to_all(rep):
             out = torch.empty_like(rep)
             car.all_to_all(out, rep)  # out[r] = rank r's shard
+            if dim == 0:
+                return out.reshape(st.tp_size * x.shape[0], *x.shape[1:])
             return out.movedim(0, -2).reshape(*x.shape[:-1], st.tp_size * x.shape[-1])
     parts = [torch.empty_like(x) for _ in range(st.tp_size)]
     dist.all_gather(parts, x.contiguous(), group=st.group)

@@ -87,12 +87,15 @@ class CustomAllReduce:
         return (not self.disabled and x.is_cuda and x.is_contiguous() and nbytes % self.world == 0
                 and (nbytes // self.world) % 4 == 0 and nbytes // self.world <= self.max_bytes)
 
-    def all_to_all(self, out: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    def all_to_all(self, out: torch.Tensor, x: torch.Tensor, push_rows: Optional[torch.Tensor] = None,
+                   row_bytes: int = 0) -> torch.Tensor:
         """Equal-split all-to-all (segment d of x -> rank d; segment r of out <- rank r) by direct
-        peer pushes into the IPC slots (EP dispatch / combine, graph-capturable)."""
+        peer pushes into the IPC slots (EP dispatch / combine, graph-capturable).  With push_rows
+        (int32 [world] on the device) only the first push_rows[d] rows of segment d cross the link:
+        the rest of each segment is capacity (its content in `out` is unspecified)."""
         from .. import ops
         ops.ext().ipc_all_to_all(out, x, self.recv_ptrs, self.flag_ptrs, self.rank, self.max_bytes,
-                                 self.epochs_ptr, self.err_ptr)
+                                 self.epochs_ptr, self.err_ptr, push_rows, row_bytes)
         return out
 
     def check(self) -> bool:

@@ -11,7 +11,12 @@ attention layer sees the full batch again.  Per rank and layer the wire traffic 
 k*T/N*H (dispatch) + k*T/N*H (combine) + (N-1)/N*T*H (gather) instead of the ring all-reduce's
 2(N-1)/N*T*H, and no rank computes routing or experts for tokens it does not own.
 
-Two dispatch layouts:
+Three dispatch layouts:
+  ipc       with the custom all-reduce's IPC slots mapped (default for EP <= 8): routing, the
+            per-destination stable slot assignment, the row gather and the weighted combine are HIP
+            kernels (csrc/kernels/ep.hip, K17 moe_combine) and the all-to-alls push only each
+            destination's real rows (counts stay on the device: no host sync, no N x over-send,
+            hipGraph-capturable); the slices are all-gathered through the same slots;
   fixed     every destination gets a capacity of C = k * ceil(T/N) rows (the worst case), so all
             splits are equal, nothing is read back to the host and the step stays
             hipGraph-capturable -- decode batches;
@@ -47,9 +52,28 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, group, out_splits=None, in_splits
     return out
 
 
+def _ipc_a2a(group, h: torch.Tensor):
+    """The custom all-reduce (its IPC slots carry the EP all-to-alls) when it serves this group."""
+    if not h.is_cuda:
+        return None
+    from .comm import get_tp
+    tp = get_tp()
+    car = tp.custom_ar
+    if car is None or car.disabled or not (group is None or group is tp.group):
+        return None
+    return car
+
+
 def _gather_slices(out_s: torch.Tensor, T: int, n: int, group) -> torch.Tensor:
     if n == 1:
         return out_s[:T]
+    if out_s.is_cuda:
+        from .comm import get_tp, tp_all_gather
+        tp = get_tp()
+        if tp.custom_ar is not None and (group is None or group is tp.group):
+            rep = n * out_s.numel() * out_s.element_size()
+            if rep // n <= tp.custom_ar.max_bytes and not tp.custom_ar.disabled:
+                return tp_all_gather(out_s, dim=0)[:T]
     if out_s.is_cuda and dist.get_backend(group) != "gloo":
         full = torch.empty(n * out_s.shape[0], out_s.shape[1], dtype=out_s.dtype, device=out_s.device)
         dist.all_gather_into_tensor(full, out_s.contiguous(), group=group)
@@ -81,7 +105,42 @@ def moe_a2a(h: torch.Tensor, gate_w: torch.Tensor, w13: torch.Tensor, w2: torch.
     pair_ok = row_ok.repeat_interleave(top_k)
     local_eid = (tid.long().reshape(P) - dest * e_local).to(torch.int32)
     tok = torch.arange(P, device=dev) // top_k
-    layout = force_layout or ("fixed" if P <= FIXED_MAX_PAIRS else "variable")
+    car = _ipc_a2a(group, h)
+    C = P
+    if force_layout is not None:
+        layout = force_layout
+    elif n > 1 and car is not None and C * H * h.element_size() <= car.max_bytes:
+        layout = "ipc"  # one destination segment (capacity C rows) fits an IPC slot
+    else:
+        layout = "fixed" if P <= FIXED_MAX_PAIRS else "variable"
+
+    if layout == "ipc":
+        ext = ops.ext()
+        tid32 = tid.to(torch.int32).contiguous()
+        slot = torch.empty(P, dtype=torch.int32, device=dev)
+        send_e = torch.empty(n * C, dtype=torch.int32, device=dev)
+        counts = torch.empty(n, dtype=torch.int32, device=dev)
+        ext.ep_route(slot, send_e, counts, tid32, hi - lo, e_local, n, C)
+        send_x = torch.empty(n * C, H, dtype=h.dtype, device=dev)  # rows past a segment's count unused
+        ext.ep_gather_rows(send_x, hs, slot, top_k)
+        recv_e = torch.empty_like(send_e)
+        recv_x = torch.empty_like(send_x)
+        if n > 1:
+            car.all_to_all(recv_e, send_e)  # the ids travel whole (-1 past each count): tiny
+            car.all_to_all(recv_x, send_x, counts, H * h.element_size())
+        else:
+            recv_e, recv_x = send_e, send_x
+        ones = torch.ones(n * C, 1, dtype=torch.float32, device=dev)
+        y = ops.moe_experts(recv_x, w13, w2, ones, recv_e.unsqueeze(1), 0)
+        rcounts = torch.empty(n, dtype=torch.int32, device=dev)
+        ext.ep_segment_rows(rcounts, recv_e, C)
+        back = y
+        if n > 1:
+            back = torch.empty_like(y)
+            car.all_to_all(back, y, rcounts, H * h.element_size())
+        out_s = torch.empty(S, H, dtype=h.dtype, device=dev)
+        ext.moe_combine(out_s, back, tw.float().contiguous(), slot)  # K17: weighted gather, fp32 accumulate
+        return _gather_slices(out_s, T, n, group)
 
     if layout == "fixed":
         C = P

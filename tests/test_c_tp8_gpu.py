@@ -21,6 +21,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MODEL_70B_2L = "meta-llama/Meta-Llama-3-70B-Instruct@layers=2"
+MIXTRAL_2L = "mistralai/Mixtral-8x7B-Instruct-v0.1@layers=2"
 
 
 def _md(n, dev):
@@ -35,12 +36,12 @@ def _md(n, dev):
         num_prefill_tokens=n, max_query_len=n, max_seq_len=n, prefill_query_start_loc=qsl)
 
 
-def _logits(full, n=40):
+def _logits(full, n=40, model=MODEL_70B_2L, moe_dispatch="allreduce"):
     import torch
     from mxserve.models.config import get_model_config
     from mxserve.models.llama import build_model
-    cfg = get_model_config(MODEL_70B_2L)
-    m = build_model(cfg, torch.device("cuda:0"), torch.bfloat16)
+    cfg = get_model_config(model)
+    m = build_model(cfg, torch.device("cuda:0"), torch.bfloat16, moe_dispatch)
     m.load_full_state(full)
     ids = torch.randint(3, cfg.vocab_size, (n,), generator=torch.Generator().manual_seed(2)).to("cuda:0")
     kv = torch.zeros(4, cfg.num_layers, 2, m.nkv, 16, cfg.head_dim, dtype=torch.bfloat16, device="cuda:0")
@@ -50,7 +51,7 @@ def _logits(full, n=40):
     return out
 
 
-def _rank(rank, world, port, q):
+def _rank(rank, world, port, q, model=MODEL_70B_2L, moe_dispatch="allreduce"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
         os.environ.pop("MXS_CUSTOM_AR", None)  # the default
@@ -61,14 +62,14 @@ def _rank(rank, world, port, q):
         from mxserve.parallel import comm
         st = comm.init_distributed(world, backend="gloo", device=torch.device("cuda:0"))
         assert st.custom_ar is not None, "custom all-reduce should be on by default for TP <= 8"
-        cfg = get_model_config(MODEL_70B_2L)
+        cfg = get_model_config(model)
         full = random_full_state(cfg, seed=4, std=0.02, dtype=torch.bfloat16, device="cuda:0")
-        got = _logits(full)
+        got = _logits(full, model=model, moe_dispatch=moe_dispatch)
         assert st.custom_ar.check(), "custom all-reduce timed out"
         ref = None
         if rank == 0:
             comm.set_tp(comm.ParallelState())  # the same weights unsharded, in this process
-            ref = _logits(full)
+            ref = _logits(full, model=model, moe_dispatch="allreduce")
             comm.set_tp(st)
         del full
         torch.distributed.barrier()
@@ -77,7 +78,10 @@ def _rank(rank, world, port, q):
         q.put((rank, None, None, traceback.format_exc()))
 
 
-def test_tp8_llama70b_shapes_on_one_gpu_matches_tp1():
+@pytest.mark.parametrize("model,moe_dispatch", [(MODEL_70B_2L, "allreduce"), (MIXTRAL_2L, "a2a")])
+def test_tp8_shapes_on_one_gpu_match_tp1(model, moe_dispatch):
+    """Llama-3-70B TP=8 (1 KV head per rank) and Mixtral-8x7B EP=8 (one expert per rank, tokens
+    dispatched by the device-side IPC all-to-all) with the real layer shapes, 2 layers."""
     import torch
     if torch.cuda.is_initialized():
         pytest.skip("HIP already initialised in the test process")
@@ -90,7 +94,7 @@ def test_tp8_llama70b_shapes_on_one_gpu_matches_tp1():
     world = 8
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_rank, args=(r, world, port, q, model, moe_dispatch)) for r in range(world)]
     for p in ps:
         p.start()
     try:
@@ -110,8 +114,9 @@ def test_tp8_llama70b_shapes_on_one_gpu_matches_tp1():
     for r in range(world):
         got = torch.from_numpy(res[r][0])
         row_err = (got - ref).abs().amax(-1)
-        # bf16: 8-way sharded GEMMs + the all-reduce sum order vs one unsharded GEMM
-        assert (row_err < 0.05 * scale).float().mean().item() > 0.99, row_err
+        # bf16: 8-way sharded GEMMs + the all-reduce sum order vs one unsharded GEMM (MoE: a near-tied
+        # router score may pick another expert for a token)
+        assert (row_err < 0.05 * scale).float().mean().item() > (0.9 if moe_dispatch == "a2a" else 0.99), row_err
         assert (got.argmax(-1) == ref.argmax(-1)).float().mean().item() > 0.9
 
 

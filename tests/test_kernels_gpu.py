@@ -439,7 +439,7 @@ def test_moe_experts_gpu_vs_ref(gpu, T):
     _close(out, exp, 0.02, 0.03, "moe")
 
 
-@pytest.mark.parametrize("layout", ["fixed", "variable"])
+@pytest.mark.parametrize("layout", ["fixed", "variable", "ipc"])
 def test_moe_a2a_dispatch_gpu(gpu, layout):
     """All-to-all expert dispatch (mxserve/parallel/expert.py) on one rank: slice/route/dispatch/
     grouped-GEMM/combine through the HIP kernels vs the fp32 reference MoE."""
@@ -568,3 +568,41 @@ def test_paged_decode_max_model_len(gpu, D, G, kv_dtype, impl):
     exp = ref.paged_attention_decode(q, kv[:, 1], bt.to(gpu), sl, scale, ks, vs)
     tol = 0.02 * max(1.0, exp.abs().max().item()) if kv_dtype == "fp8" else 0.02
     _close(out, exp, tol, 0.02, f"decode 8k {kv_dtype}")
+
+
+@pytest.mark.parametrize("n,e_local,S,k,valid", [(8, 1, 100, 2, 97), (4, 2, 700, 2, 700), (2, 4, 33, 2, 1),
+                                                 (8, 1, 2048, 2, 2000)])
+def test_ep_route_kernel(gpu, n, e_local, S, k, valid):
+    """EP routing on the device: each valid pair's slot is dest * C + (its rank among earlier pairs
+    with the same destination) -- a stable, deterministic order --, padding rows get -1, the
+    segment ids carry the local expert ids then -1, and the counts match."""
+    E = n * e_local
+    tid = torch.randint(0, E, (S, k), device=gpu, dtype=torch.int32)
+    P, C = S * k, S * k
+    slot = torch.empty(P, dtype=torch.int32, device=gpu)
+    send_e = torch.full((n * C,), 77, dtype=torch.int32, device=gpu)
+    counts = torch.empty(n, dtype=torch.int32, device=gpu)
+    ops.ext().ep_route(slot, send_e, counts, tid, valid, e_local, n, C)
+    ids = tid.cpu().reshape(-1).tolist()
+    exp_slot, exp_e, cnt = [], [-1] * (n * C), [0] * n
+    for p, e in enumerate(ids):
+        if p // k >= valid:
+            exp_slot.append(-1)
+            continue
+        d = e // e_local
+        exp_slot.append(d * C + cnt[d])
+        exp_e[d * C + cnt[d]] = e - d * e_local
+        cnt[d] += 1
+    assert slot.cpu().tolist() == exp_slot
+    assert send_e.cpu().tolist() == exp_e
+    assert counts.cpu().tolist() == cnt
+    rc = torch.empty(n, dtype=torch.int32, device=gpu)
+    ops.ext().ep_segment_rows(rc, send_e, C)
+    assert rc.cpu().tolist() == cnt
+    # rows land at their slots
+    hs = torch.randn(S, 64, device=gpu, dtype=torch.bfloat16)
+    send_x = torch.zeros(n * C, 64, device=gpu, dtype=torch.bfloat16)
+    ops.ext().ep_gather_rows(send_x, hs, slot, k)
+    for p in range(0, P, max(1, P // 50)):
+        if exp_slot[p] >= 0:
+            assert torch.equal(send_x[exp_slot[p]], hs[p // k])
