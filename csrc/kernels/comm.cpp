@@ -30,7 +30,7 @@ void launch_custom_allreduce_2shot(unsigned short*, const unsigned short*, long,
 void launch_ipc_all_to_all(void*, const void*, long, const ArPeers&, int, int, long, unsigned*, unsigned*,
                            hipStream_t, const int*, long);
 void launch_ep_route(int*, int*, int*, const int*, int, int, int, int, int, int, hipStream_t);
-void launch_ep_gather_rows(unsigned short*, const unsigned short*, const int*, int, int, int, hipStream_t);
+void launch_ep_gather_rows(unsigned short*, const unsigned short*, const int*, int, int, int, int, hipStream_t);
 void launch_ep_segment_rows(int*, const int*, int, int, hipStream_t);
 }
 
@@ -188,7 +188,7 @@ void ep_gather_rows(at::Tensor send_x, at::Tensor hs, at::Tensor slot, int64_t k
   mxs::launch_ep_gather_rows(reinterpret_cast<unsigned short*>(send_x.data_ptr()),
                              reinterpret_cast<const unsigned short*>(hs.data_ptr()), slot.data_ptr<int>(),
                              static_cast<int>(slot.numel()), static_cast<int>(k), H,
-                             c10::hip::getCurrentHIPStream().stream());
+                             static_cast<int>(send_x.size(0)), c10::hip::getCurrentHIPStream().stream());
 }
 
 void ep_segment_rows(at::Tensor counts, at::Tensor ids, int64_t C) {

@@ -9,6 +9,7 @@ namespace mxs {
 __global__ void __launch_bounds__(256) copy_blocks_kernel(char* __restrict__ dst, const char* __restrict__ src,
                                                           const int* __restrict__ src_ids,
                                                           const int* __restrict__ dst_ids, long block_bytes) {
+  MXS_KCHECK(src_ids[blockIdx.x] >= 0 && dst_ids[blockIdx.x] >= 0);
   const long s = static_cast<long>(src_ids[blockIdx.x]) * block_bytes;
   const long d = static_cast<long>(dst_ids[blockIdx.x]) * block_bytes;
   const uint4* sp = reinterpret_cast<const uint4*>(src + s);

@@ -5,6 +5,24 @@
 
 #define MXS_CHECK_LAUNCH() (void)hipGetLastError()
 
+// Kernel bounds checks.  `MXS_DEBUG_KERNELS=1 python setup_ext.py` compiles every
+// kernel with -DMXS_DEBUG_KERNELS into build/obj-debug: a failing MXS_KCHECK prints the condition,
+// file, line and block, then traps (the launch fails instead of reading or writing out of bounds).
+// Release builds compile the checks away.
+#ifdef MXS_DEBUG_KERNELS
+#include <stdio.h>
+#define MXS_KCHECK(cond)                                                                                   \
+  do {                                                                                                     \
+    if (!(cond)) {                                                                                         \
+      printf("MXS_KCHECK failed %s:%d block %d thread %d: %s\n", __FILE__, __LINE__, (int)blockIdx.x,       \
+             (int)threadIdx.x, #cond);                                                                      \
+      __builtin_trap();                                                                                    \
+    }                                                                                                      \
+  } while (0)
+#else
+#define MXS_KCHECK(cond) ((void)0)
+#endif
+
 namespace mxs {
 
 constexpr int kWave = 64;

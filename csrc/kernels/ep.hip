@@ -50,6 +50,7 @@ __global__ void __launch_bounds__(1024) ep_route_kernel(int* __restrict__ slot, 
       int pre = base[d];
       for (int w = 0; w < wid; ++w) pre += wave_tot[w][d];
       const int pos = pre + my_pos;
+      MXS_KCHECK(pos < C);
       slot[p] = d * C + pos;
       send_e[d * C + pos] = le;
     } else if (p < P) {
@@ -67,10 +68,11 @@ __global__ void __launch_bounds__(1024) ep_route_kernel(int* __restrict__ slot, 
 }
 
 __global__ void __launch_bounds__(256) ep_gather_rows_kernel(bf16_t* __restrict__ send_x, const bf16_t* __restrict__ hs,
-                                                             const int* __restrict__ slot, int k, int H) {
+                                                             const int* __restrict__ slot, int k, int H, int nrows) {
   const int p = blockIdx.x;
   const int s = slot[p];
   if (s < 0) return;
+  MXS_KCHECK(s < nrows);
   const uint4* src = reinterpret_cast<const uint4*>(hs + static_cast<size_t>(p / k) * H);
   uint4* dst = reinterpret_cast<uint4*>(send_x + static_cast<size_t>(s) * H);
   for (int c = threadIdx.x; c < H / 8; c += blockDim.x) dst[c] = src[c];
@@ -95,9 +97,10 @@ void launch_ep_route(int* slot, int* send_e, int* counts, const int* topk_ids, i
   MXS_CHECK_LAUNCH();
 }
 
-void launch_ep_gather_rows(bf16_t* send_x, const bf16_t* hs, const int* slot, int P, int k, int H, hipStream_t s) {
+void launch_ep_gather_rows(bf16_t* send_x, const bf16_t* hs, const int* slot, int P, int k, int H, int nrows,
+                           hipStream_t s) {
   if (P == 0) return;
-  hipLaunchKernelGGL(ep_gather_rows_kernel, dim3(P), dim3(256), 0, s, send_x, hs, slot, k, H);
+  hipLaunchKernelGGL(ep_gather_rows_kernel, dim3(P), dim3(256), 0, s, send_x, hs, slot, k, H, nrows);
   MXS_CHECK_LAUNCH();
 }
 

@@ -35,6 +35,7 @@ class StepOutput:
     num_output_tokens: int
     logprob: Optional[float] = None  # of token_id, when the request asked for logprobs
     top_logprobs: Optional[list] = None  # [(token_id, logprob)] best first
+    timing: Optional[dict] = None  # on a request's first token: where its time to first token went
 
 
 class LLMEngine:
@@ -172,7 +173,8 @@ class LLMEngine:
             outs.append(StepOutput(req.request_id, req.output_token_ids[-1], fin,
                                    req.status.value if fin else None, req.num_prompt_tokens,
                                    req.num_cached_tokens, len(req.output_token_ids),
-                                   lp[0] if lp else None, lp[1] if lp else None))
+                                   lp[0] if lp else None, lp[1] if lp else None,
+                                   _first_token_timing(req) if len(req.output_token_ids) == 1 else None))
             self.num_generated += 1
             if fin:
                 self.runner.release(req.request_id)
@@ -345,6 +347,14 @@ class AsyncEngine:
         self._stop = True
         self._wake.set()
         self._thread.join(timeout=5)
+
+
+def _first_token_timing(req) -> dict:
+    """Worker-side spans of a request's time to first token (ms): waiting for admission, then the
+    prefill steps up to the sampled token."""
+    sched = req.scheduled_time if req.scheduled_time is not None else req.arrival_time
+    first = req.first_token_time if req.first_token_time is not None else sched
+    return {"queue_ms": round((sched - req.arrival_time) * 1e3, 3), "prefill_ms": round((first - sched) * 1e3, 3)}
 
 
 def _put_many(items: list) -> None:

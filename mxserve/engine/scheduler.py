@@ -186,6 +186,8 @@ class Scheduler:
             if not self.kv.allocate_slots(req, n):
                 break
             self.waiting.popleft()
+            if req.scheduled_time is None:
+                req.scheduled_time = time.monotonic()
             req.status = Status.RUNNING
             self.running.append(req)
             scheduled.append(ScheduledReq(req, n, req.num_computed_tokens + n >= req.num_tokens))

@@ -15,6 +15,7 @@ and retries a request on another worker if its worker fails before the first tok
 from __future__ import annotations
 
 import asyncio
+import contextvars
 import contextlib
 import json
 import logging
@@ -48,7 +49,7 @@ def _parse_token_line(d: dict, out: list) -> None:
     if not isinstance(toks, list):
         if toks < 0:
             raise RuntimeError("worker failed the request")
-        out.append(TokenEvent(toks, d["f"], d["r"], d["p"], d["c"], d.get("lp"), d.get("tlp")))
+        out.append(TokenEvent(toks, d["f"], d["r"], d["p"], d["c"], d.get("lp"), d.get("tlp"), d.get("tm")))
         return
     n = len(toks)
     lps, tlps = d.get("lp") or [None] * n, d.get("tlp") or [None] * n
@@ -56,7 +57,8 @@ def _parse_token_line(d: dict, out: list) -> None:
         if t < 0:
             raise RuntimeError("worker failed the request")
         last = i == n - 1
-        out.append(TokenEvent(t, d["f"] and last, d["r"] if last else None, d["p"], d["c"], lps[i], tlps[i]))
+        out.append(TokenEvent(t, d["f"] and last, d["r"] if last else None, d["p"], d["c"], lps[i], tlps[i],
+                              d.get("tm") if i == 0 else None))
 
 
 async def _merge(gens: list):
@@ -119,6 +121,11 @@ class TokenEvent:
     num_cached_tokens: int
     logprob: Optional[float] = None
     top_logprobs: Optional[list] = None  # [(token_id, logprob)]
+    timing: Optional[dict] = None  # worker-side spans of the time to first token (first event)
+
+
+# the request trace of the task serving a request (route / first-token marks deeper in the stack)
+_TRACE: contextvars.ContextVar = contextvars.ContextVar("mxs_trace", default=None)
 
 
 class LocalWorker:
@@ -138,7 +145,7 @@ class LocalWorker:
             raise
         async for outs in self.aeng.stream_batches(request_id, q):
             yield [TokenEvent(o.token_id, o.finished, o.finish_reason, o.num_prompt_tokens, o.num_cached_tokens,
-                              o.logprob, o.top_logprobs) for o in outs]
+                              o.logprob, o.top_logprobs, o.timing) for o in outs]
 
 
 class Frontend:
@@ -251,6 +258,10 @@ class Frontend:
                 sp = dict(sampling, max_tokens=max_tokens - len(generated),
                           min_tokens=max(0, int(sampling.get("min_tokens") or 0) - len(generated)))
             w, overlap = self.router.pick(decode, ids)
+            tr = _TRACE.get()
+            if tr is not None and attempt == 0:
+                tr.mark("routed")
+                tr.attrs["worker"] = w.worker_id
             purl = None
             if w.role == "decode" and prefill:
                 # a prefill worker in the decode worker's own pair pod can reach its GPU arena
@@ -344,7 +355,7 @@ class Frontend:
                 "logprobs": self._logprobs_arg(body, chat), **pens}
 
     async def _run(self, endpoint: str, body: dict, prompt_ids: list, model: str, chat: bool,
-                   xrid: Optional[str] = None):
+                   xrid: Optional[str] = None, t_recv: Optional[float] = None):
         stream = bool(body.get("stream", False))
         rtype = "stream" if stream else "unary"
         sampling = self._sampling(body, model, len(prompt_ids), chat)
@@ -355,8 +366,14 @@ class Frontend:
             stops = [stops]
         rid = ("chatcmpl-" if chat else "cmpl-") + uuid.uuid4().hex
         trace = TRACER.start(xrid or rid)
+        if t_recv is not None:  # spans count from the request's arrival, before templating/tokenizing
+            trace.t0 = t_recv
+            trace.spans.append(("received", 0.0))
+            trace.mark("tokenized")
+        else:
+            trace.mark("received")
         trace.attrs.update(model=model, endpoint=endpoint, prompt_tokens=len(prompt_ids), stream=stream)
-        trace.mark("received")
+        _TRACE.set(trace)
         created = int(time.time())
         tok = self.tokenizer(model)
         m = self.metrics
@@ -409,6 +426,8 @@ class Frontend:
             lps: list = []
             sub_rid, sub_sp = sub_request(idx)
             async for evs in self.generate_tokens(model, prompt_ids, sub_sp, sub_rid):
+                if evs[0].timing and "worker_ms" not in trace.attrs:
+                    trace.attrs["worker_ms"] = evs[0].timing  # queue / prefill / kv transfer on the worker
                 for ev in evs:  # a batch becomes one delta
                     on_token(idx)
                     eos_hit = ev.finished and ev.finish_reason == "stop" and ev.token_id in tok.eos_token_ids
@@ -576,6 +595,7 @@ class Frontend:
                 return _err(400, "invalid JSON body")
             if not isinstance(body, dict) or "messages" not in body:
                 return _err(400, "`messages` is required")
+            t_recv = time.perf_counter()
             model = fe.resolve_model(body.get("model"))
             try:
                 text = render(fe.model_cfg(model).chat_template, body["messages"])
@@ -583,7 +603,7 @@ class Frontend:
                 return _err(400, str(e))
             ids = fe.tokenizer(model).encode(text)
             return await fe._run("chat_completions", body, ids, model, chat=True,
-                                 xrid=request.headers.get("x-request-id"))
+                                 xrid=request.headers.get("x-request-id"), t_recv=t_recv)
 
         @app.post("/v1/completions")
         async def completions(request: HTTPRequest):
@@ -591,6 +611,7 @@ class Frontend:
                 body = await request.json()
             except Exception:  # noqa: BLE001
                 return _err(400, "invalid JSON body")
+            t_recv = time.perf_counter()
             model = fe.resolve_model(body.get("model"))
             p = body.get("prompt")
             if isinstance(p, list) and p and isinstance(p[0], int):
@@ -600,7 +621,7 @@ class Frontend:
             else:
                 return _err(400, "`prompt` must be a string or a list of token ids")
             return await fe._run("completions", body, ids, model, chat=False,
-                                 xrid=request.headers.get("x-request-id"))
+                                 xrid=request.headers.get("x-request-id"), t_recv=t_recv)
 
         @app.get("/debug/traces")
         async def traces(n: int = 100):

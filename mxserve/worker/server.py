@@ -54,6 +54,8 @@ def _line(o: StepOutput) -> bytes:
     if o.logprob is not None:
         d["lp"] = o.logprob
         d["tlp"] = o.top_logprobs or []
+    if o.timing:
+        d["tm"] = o.timing
     return (json.dumps(d) + "\n").encode()
 
 
@@ -69,6 +71,9 @@ def _batch_line(outs: list) -> bytes:
     if any(o.logprob is not None for o in outs):
         d["lp"] = [o.logprob for o in outs]
         d["tlp"] = [o.top_logprobs or [] for o in outs]
+    tm = next((o.timing for o in outs if o.timing), None)
+    if tm:
+        d["tm"] = tm
     return (json.dumps(d) + "\n").encode()
 
 
@@ -174,6 +179,7 @@ class Worker:
         target["shm_start"] = shm_start
         payload = {"request_id": rid, "token_ids": toks, "sampling": _sp_dict(sp), "kv_target": target}
         completed = False
+        t_post = time.perf_counter()
         try:
             sess = await self.http()
             async with sess.post(purl.rstrip("/") + "/prefill", json=payload) as r:
@@ -198,6 +204,10 @@ class Worker:
 
             out = await self.aeng.submit(land_and_complete, int(res["first_token"]))
             completed = True  # the landing copies now own (and recycle) the extents
+            xfer_ms = 1e3 * float(res.get("transfer_s", 0.0))
+            out.timing = {"remote_prefill_ms": round((time.perf_counter() - t_post) * 1e3 - xfer_ms, 3),
+                          "kv_transfer_ms": round(xfer_ms, 3), "kv_path": via,
+                          **{f"prefill_worker_{k}": v for k, v in (res.get("timing") or {}).items()}}
             self.aeng.push(out)
             if "transfer_s" in res:
                 self.metrics.kv_xfer_lat.labels(self.model).observe(float(res["transfer_s"]))
@@ -229,6 +239,7 @@ class Worker:
         first = first_lp = None
         async for o in self.aeng.generate(toks, sp, rid, disagg_role="prefill_only"):
             first, first_lp = o.token_id, o
+        timing = first_lp.timing if first_lp is not None else None
         req = self.engine.requests.get(rid)
         target = body["kv_target"]
         skip = int(target.get("skip_blocks", 0))
@@ -268,7 +279,7 @@ class Worker:
         finally:
             self.aeng.submit_nowait(self.engine.release_prefill_blocks, rid)
         res = {"first_token": first, "num_cached_tokens": req.num_cached_tokens if req else 0,
-               "transfer_s": xfer_s, "blocks": len(dst), "via": via}
+               "transfer_s": xfer_s, "blocks": len(dst), "via": via, "timing": timing}
         if first_lp is not None and first_lp.logprob is not None:
             res.update(logprob=first_lp.logprob, top_logprobs=first_lp.top_logprobs or [])
         return res

@@ -19,7 +19,9 @@ import sys
 import sysconfig
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-BUILD = os.path.join(ROOT, "build", "obj")
+# MXS_DEBUG_KERNELS=1: bounds-checked kernels (MXS_KCHECK, csrc/kernels/common.h), separate objects
+DEBUG_KERNELS = os.environ.get("MXS_DEBUG_KERNELS", "0") == "1"
+BUILD = os.path.join(ROOT, "build", "obj-debug" if DEBUG_KERNELS else "obj")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
@@ -87,7 +89,8 @@ def build_C(force: bool = False, jobs: int = 8) -> str:
         objs.append(obj)
         if force or _stale(obj, [src, *headers]):
             jobs_list.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
-                              "-munsafe-fp-atomics", "-c", src, "-o", obj])
+                              "-munsafe-fp-atomics", *(["-DMXS_DEBUG_KERNELS"] if DEBUG_KERNELS else []),
+                              "-c", src, "-o", obj])
     for src in cpp_srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)

@@ -255,6 +255,11 @@ def test_disaggregated_matches_aggregated(via, monkeypatch):
         assert pw.agent.backend == "host"
         # the decode worker really received the prompt's KV from the prefill worker
         assert dw.metrics.kv_xfer_bytes.labels(MODEL, via)._value.get() > 0
+        # the request trace carries the disaggregated spans: remote prefill + KV transfer by path
+        tr = httpx.get(fs.url + "/debug/traces").json()["traces"][-1]
+        wm = tr["worker_ms"]
+        assert wm["kv_path"] == via and wm["kv_transfer_ms"] >= 0 and wm["remote_prefill_ms"] >= 0
+        assert wm["prefill_worker_prefill_ms"] >= 0
         if via == "shm":  # every staging extent came back once the copies landed
             assert dw.agent._shm_ext.free_blocks() == dw.agent.shm_blocks
         # aggregated reference with the same weights (same seed)
@@ -287,7 +292,10 @@ def test_request_trace_by_x_request_id(agg_stack):
     tr = [t for t in httpx.get(fs.url + "/debug/traces").json()["traces"] if t["request_id"] == "trace-me-1"]
     assert tr and tr[0]["status"] == "success"
     spans = tr[0]["spans_ms"]
-    assert spans["received"] <= spans["first_token"] <= spans["done"]
+    # receive -> tokenize -> route -> (worker: queue -> prefill) -> first token -> done
+    assert spans["received"] <= spans["tokenized"] <= spans["routed"] <= spans["first_token"] <= spans["done"]
+    wm = tr[0]["worker_ms"]
+    assert wm["queue_ms"] >= 0 and wm["prefill_ms"] >= 0 and tr[0]["worker"] == "agg-w"
 
 
 def test_retry_on_dead_worker_before_first_token(agg_stack):
