@@ -28,7 +28,7 @@ from typing import AsyncIterator, Optional
 from fastapi import FastAPI, Request as HTTPRequest
 from fastapi.responses import JSONResponse, Response, StreamingResponse
 
-from ..models.config import get_model_config
+from ..models.config import find_local_model_dir, get_model_config
 from ..router.router import Registry, Router, WorkerInfo
 from ..utils.tracing import TRACER
 from .chat_template import render
@@ -598,7 +598,8 @@ class Frontend:
             t_recv = time.perf_counter()
             model = fe.resolve_model(body.get("model"))
             try:
-                text = render(fe.model_cfg(model).chat_template, body["messages"])
+                cfg = fe.model_cfg(model)
+                text = render(cfg.chat_template, body["messages"], find_local_model_dir(cfg.name))
             except ValueError as e:
                 return _err(400, str(e))
             ids = fe.tokenizer(model).encode(text)

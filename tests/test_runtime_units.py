@@ -363,3 +363,42 @@ def test_debug_kernel_build_compiles(tmp_path):
         asm = out.read_text()
         assert ("s_trap" in asm) == (mode == "debug"), mode
     shutil.rmtree(tmp_path, ignore_errors=True)
+
+
+_LLAMA3_JINJA = ("{% set loop_messages = messages %}{% for message in loop_messages %}{% set content = "
+                 "'<|start_header_id|>' + message['role'] + '<|end_header_id|>\\n\\n'+ message['content'] | trim + "
+                 "'<|eot_id|>' %}{% if loop.index0 == 0 %}{% set content = bos_token + content %}{% endif %}"
+                 "{{ content }}{% endfor %}{% if add_generation_prompt %}"
+                 "{{ '<|start_header_id|>assistant<|end_header_id|>\\n\\n' }}{% endif %}")
+_CHATML_JINJA = ("{% for message in messages %}{{'<|im_start|>' + message['role'] + '\\n' + message['content'] + "
+                 "'<|im_end|>' + '\\n'}}{% endfor %}{% if add_generation_prompt %}{{ '<|im_start|>assistant\\n' }}"
+                 "{% endif %}")
+
+
+@pytest.mark.parametrize("form", ["string", "list"])
+def test_chat_template_from_tokenizer_config(tmp_path, form):
+    """A model directory's own Jinja chat_template (tokenizer_config.json) is what the frontend
+    renders; for the public Llama-3 / ChatML templates that equals the built-in renderers."""
+    import json
+
+    from mxserve.frontend.chat_template import load_hf_template, render
+    msgs = [{"role": "system", "content": "  Be brief. "}, {"role": "user", "content": "héllo"},
+            {"role": "assistant", "content": "hi"}, {"role": "user", "content": "again"}]
+    for name, tpl, bos, builtin in (("l3", _LLAMA3_JINJA, "<|begin_of_text|>", "llama3"),
+                                    ("cm", _CHATML_JINJA, None, "chatml")):
+        d = tmp_path / name
+        d.mkdir()
+        (d / "config.json").write_text("{}")
+        cfg = {"bos_token": {"content": bos} if bos else None, "eos_token": "<|eot_id|>"}
+        cfg["chat_template"] = tpl if form == "string" else [{"name": "tool_use", "template": "x"},
+                                                             {"name": "default", "template": tpl}]
+        (d / "tokenizer_config.json").write_text(json.dumps(cfg))
+        load_hf_template.cache_clear()
+        assert render(builtin, msgs, str(d)) == render(builtin, msgs)
+    bad = tmp_path / "bad"
+    bad.mkdir()
+    (bad / "tokenizer_config.json").write_text(json.dumps(
+        {"chat_template": "{{ raise_exception('roles must alternate') }}"}))
+    load_hf_template.cache_clear()
+    with pytest.raises(ValueError, match="alternate"):
+        render("llama3", msgs, str(bad))
