@@ -30,7 +30,8 @@ void launch_penalties(void*, bool, int, int, long, const int*, long, const int64
 void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStream_t);
 void launch_moe_align(int*, int*, const int*, int, int, int, int*, hipStream_t);
 void launch_moe_combine(bf16_t*, const bf16_t*, const float*, const int*, int, int, int, hipStream_t);
-bool launch_skinny_gemm(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, hipStream_t);
+bool launch_decode_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int,
+                        int, hipStream_t);
 bool launch_moe_grouped_gemm(bf16_t*, const bf16_t*, const bf16_t*, const int*, int, int, int, int, int, bool,
                              int, float*, hipStream_t);
 void launch_moe_combine_partials(bf16_t*, const float*, const float*, const int*, int, int, int, int, long,
@@ -212,14 +213,26 @@ void apply_penalties(at::Tensor logits, at::Tensor hist, at::Tensor srows, at::T
                         counts.data_ptr<int>(), stream());
 }
 
-// out[M,N] = x[M,K] . w[N,K]^T for M <= 256; false if the shape is unsupported (caller falls back)
-bool skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w) {
+// Decode projection (csrc/kernels/gemm_decode.hip): out = x . w^T (epi 0, out [M, N]) or
+// out = SiLU(x . w_gate^T) * (x . w_up^T) with w = [gate; up] (epi 1, out [M, N/2]).  `part` is the
+// fp32 split-K workspace (>= splitk * M * N floats) when splitk > 1.  False if the configuration
+// does not tile the shape (the caller keeps hipBLASLt).
+bool decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> part, int64_t mf, int64_t nf,
+                 int64_t wm, int64_t splitk, int64_t epi) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
-  TORCH_CHECK(x.size(1) == w.size(1) && out.size(0) == x.size(0) && out.size(1) == w.size(0), "shape mismatch");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == (epi == 1 ? N / 2 : N), "shape mismatch");
+  TORCH_CHECK(epi == 0 || epi == 1, "epi 0 (none) | 1 (silu*mul)");
   if (x.stride(1) != 1 || out.stride(1) != 1) return false;
-  return mxs::launch_skinny_gemm(bf(out), bf(x), bf(w), x.size(0), w.size(0), w.size(1), x.stride(0),
-                                 out.stride(0), stream());
+  float* p = nullptr;
+  if (splitk > 1) {
+    TORCH_CHECK(part.has_value() && part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->numel() >= splitk * M * N, "split-K needs an fp32 workspace of splitk * M * N");
+    p = part->data_ptr<float>();
+  }
+  return mxs::launch_decode_gemm(bf(out), p, bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), mf, nf, wm, splitk,
+                                 epi, stream());
 }
 
 // y[r] = x[r] . w[e(r)]^T over expert-sorted rows (offs = moe_align offsets); silu: w rows are
@@ -300,7 +313,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_align", &moe_align, pybind11::arg("expert_offsets"), pybind11::arg("perm"), pybind11::arg("topk_ids"),
         pybind11::arg("e_lo"), pybind11::arg("e_local"), pybind11::arg("inv") = pybind11::none());
   m.def("moe_combine", &moe_combine);
-  m.def("skinny_gemm", &skinny_gemm);
+  m.def("decode_gemm", &decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
+        pybind11::arg("part"), pybind11::arg("mf"), pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"),
+        pybind11::arg("epi"));
   m.def("moe_grouped_gemm", &moe_grouped_gemm, pybind11::arg("y"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("offs"), pybind11::arg("silu"), pybind11::arg("split") = 1,
         pybind11::arg("partial") = pybind11::none());

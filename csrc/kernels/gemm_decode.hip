@@ -1,0 +1,196 @@
+// K05-K09 decode projections: Y[M, N] = X[M, K] . W[N, K]^T for M <= 256 (the decode batch), on MFMA.
+//
+// Decode steps (batch B = M rows) stream every weight byte once; at B = 64-256 the library GEMMs tile
+// for large M and leave the narrow projections (Llama-3.2-1B qkv 3072, o 2048, down 2048 columns)
+// with a dozen workgroups on a 256-CU chip.  This kernel is shaped for the decode regime:
+//
+//   * v_mfma_f32_16x16x32_bf16 with A = a 16-row slice of W (16 output columns x 32 k) and B = X^T
+//     (32 k x 16 tokens): a lane's accumulator holds Y[token][4 consecutive columns], so the store
+//     is one 8-byte write and no transpose is needed;
+//   * a wave owns MF x NF fragments (up to 64 tokens x 64 columns): 16 MFMAs per k-step against
+//     MF + NF 16-byte fragment loads, both operands straight from global memory into registers
+//     (W streamed once, non-temporal; X, ~1 MB, stays in L2), the next k-step's fragments in flight
+//     while the current ones are multiplied;
+//   * a workgroup is WM x WN waves; split-K over gridDim.z fills the chip when there are few column
+//     tiles (o / down at N = 2048), fp32 partial slabs summed by a reduce kernel that also applies
+//     the epilogue;
+//   * EPI_SILU (gate_up): each wave holds the gate columns n and the matching up columns I + n in
+//     the same lane positions, so SiLU(gate) * up is applied in registers and only the [M, I]
+//     activation is written (no [M, 2I] round trip, no separate SiLU*mul kernel).
+// The Python side (mxserve/ops/decode_gemm.py) times these configurations against hipBLASLt per
+// (graph bucket, projection) when the decode graphs are captured and keeps the faster one.
+#include <algorithm>
+
+#include "common.h"
+
+namespace mxs {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int EPI_NONE = 0;
+constexpr int EPI_SILU = 1;
+
+__device__ __forceinline__ bf16x8_t as_bf16x8(const u32x4& v) { return __builtin_bit_cast(bf16x8_t, v); }
+__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+
+template <int MF, int NF, int WM, int WN, int EPI>
+__global__ void __launch_bounds__(256) decode_gemm_kernel(bf16_t* __restrict__ Y, float* __restrict__ part,
+                                                          const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                          int M, int N, int K, int ldx, int ldy, int kslice,
+                                                          int inter) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int i = lane & 15, kq = lane >> 4;
+  constexpr int NH = EPI == EPI_SILU ? NF / 2 : NF;  // output fragments per wave
+  const int m0 = (blockIdx.y * WM + wm) * MF * 16;
+  const int c0 = (blockIdx.x * WN + wn) * NH * 16;  // first OUTPUT column of the wave
+  const int kbeg = blockIdx.z * kslice;
+
+  // weight rows (output columns) of each fragment; gate_up: fragment j < NH is gate column
+  // c0 + 16 j, fragment NH + j the matching up column inter + c0 + 16 j
+  const bf16_t* wp[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int col = (EPI == EPI_SILU && j >= NH) ? inter + c0 + 16 * (j - NH) : c0 + 16 * (j % NH);
+    wp[j] = W + static_cast<size_t>(col + i) * K + kbeg + 8 * kq;
+  }
+  const bf16_t* xp[MF];
+  bool xv[MF];
+#pragma unroll
+  for (int t = 0; t < MF; ++t) {
+    const int m = m0 + 16 * t + i;
+    xv[t] = m < M;
+    xp[t] = X + static_cast<size_t>(xv[t] ? m : 0) * ldx + kbeg + 8 * kq;
+  }
+  float4_ acc[MF][NF];
+#pragma unroll
+  for (int t = 0; t < MF; ++t)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[t][j] = float4_{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 a[NF], b[MF];
+  auto load = [&](int k, u32x4 (&ad)[NF], u32x4 (&bd)[MF]) {
+#pragma unroll
+    for (int j = 0; j < NF; ++j) ad[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wp[j] + k));
+#pragma unroll
+    for (int t = 0; t < MF; ++t)
+      bd[t] = xv[t] ? *reinterpret_cast<const u32x4*>(xp[t] + k) : u32x4{0u, 0u, 0u, 0u};
+  };
+  load(0, a, b);
+  for (int k = 0; k < kslice; k += 32) {
+    u32x4 an[NF], bn[MF];
+    const bool more = k + 32 < kslice;
+    if (more) load(k + 32, an, bn);
+#pragma unroll
+    for (int t = 0; t < MF; ++t)
+#pragma unroll
+      for (int j = 0; j < NF; ++j)
+        acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[j]), as_bf16x8(b[t]), acc[t][j], 0, 0, 0);
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < NF; ++j) a[j] = an[j];
+#pragma unroll
+      for (int t = 0; t < MF; ++t) b[t] = bn[t];
+    }
+  }
+
+  // lane (i, kq) holds Y[m0 + 16 t + i][col_j + 4 kq + r], r = 0..3
+#pragma unroll
+  for (int t = 0; t < MF; ++t) {
+    if (!xv[t]) continue;
+    const int m = m0 + 16 * t + i;
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      const int n = c0 + 16 * j + 4 * kq;
+      if (part != nullptr) {  // split-K: fp32 slab, raw (pre-epilogue) columns
+        const size_t row = (static_cast<size_t>(blockIdx.z) * M + m) * static_cast<size_t>(N);
+        *reinterpret_cast<float4_*>(part + row + n) = acc[t][j];
+        if constexpr (EPI == EPI_SILU) *reinterpret_cast<float4_*>(part + row + inter + n) = acc[t][j + NH];
+        continue;
+      }
+      float v[4];
+      if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = silu(acc[t][j][r]) * acc[t][j + NH][r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[t][j][r];
+      }
+      uint2 o;
+      o.x = pack2(v[0], v[1]);
+      o.y = pack2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(Y + static_cast<size_t>(m) * ldy + n) = o;
+    }
+  }
+}
+
+// Sum S fp32 slabs [S][M][N] and apply the epilogue: Y[m][n] (EPI_NONE, N columns) or
+// Y[m][n] = SiLU(sum gate[n]) * sum up[inter + n] (EPI_SILU, inter columns).
+template <int EPI>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__ Y, const float* __restrict__ part,
+                                                            int M, int N, int S, int ldy, int inter) {
+  const int ncols = EPI == EPI_SILU ? inter : N;
+  const long total4 = static_cast<long>(M) * ncols / 4;
+  for (long q = blockIdx.x * static_cast<long>(blockDim.x) + threadIdx.x; q < total4;
+       q += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int m = static_cast<int>((q * 4) / ncols), n = static_cast<int>((q * 4) % ncols);
+    float4_ g = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < S; ++s) {
+      const float* row = part + (static_cast<size_t>(s) * M + m) * static_cast<size_t>(N);
+      g += *reinterpret_cast<const float4_*>(row + n);
+      if (EPI == EPI_SILU) u += *reinterpret_cast<const float4_*>(row + inter + n);
+    }
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = EPI == EPI_SILU ? silu(g[r]) * u[r] : g[r];
+    uint2 o;
+    o.x = pack2(v[0], v[1]);
+    o.y = pack2(v[2], v[3]);
+    *reinterpret_cast<uint2*>(Y + static_cast<size_t>(m) * ldy + n) = o;
+  }
+}
+
+// config id = ((MF-1) * 2 + (NF/2-1)) * 3 + wave layout {0: 1x4, 1: 2x2, 2: 4x1}; MF in {1, 2, 4}
+// returns false when the configuration does not tile the shape (the caller keeps hipBLASLt).
+bool launch_decode_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx,
+                        int ldy, int MF, int NF, int WM, int splitk, int epi, hipStream_t s) {
+  const int WN = 4 / WM;
+  if (M <= 0 || M > 256 || splitk < 1 || K % (32 * splitk) != 0 || ldx % 8 != 0 || ldy % 4 != 0) return false;
+  const int outN = epi == EPI_SILU ? N / 2 : N;
+  const int NH = epi == EPI_SILU ? NF / 2 : NF;
+  const int BM = WM * MF * 16, BN = WN * NH * 16;
+  if (outN % BN != 0 || (epi == EPI_SILU && N % 2 != 0)) return false;
+  if (splitk > 1 && part == nullptr) return false;
+  const int kslice = K / splitk;
+  dim3 grid(outN / BN, (M + BM - 1) / BM, splitk), blk(256);
+  float* p = splitk > 1 ? part : nullptr;
+#define MXS_DG(mf, nf, wm, e)                                                                                  \
+  if (MF == mf && NF == nf && WM == wm && epi == e) {                                                        \
+    hipLaunchKernelGGL((decode_gemm_kernel<mf, nf, wm, 4 / wm, e>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, \
+                       ldy, kslice, N / 2);                                                                  \
+    launched = true;                                                                                         \
+  }
+  bool launched = false;
+#define MXS_DG_WM(mf, nf, e) MXS_DG(mf, nf, 1, e) MXS_DG(mf, nf, 2, e) MXS_DG(mf, nf, 4, e)
+  MXS_DG_WM(1, 2, 0) MXS_DG_WM(1, 4, 0) MXS_DG_WM(2, 2, 0) MXS_DG_WM(2, 4, 0) MXS_DG_WM(4, 2, 0) MXS_DG_WM(4, 4, 0)
+  MXS_DG_WM(1, 2, 1) MXS_DG_WM(1, 4, 1) MXS_DG_WM(2, 2, 1) MXS_DG_WM(2, 4, 1) MXS_DG_WM(4, 2, 1) MXS_DG_WM(4, 4, 1)
+#undef MXS_DG_WM
+#undef MXS_DG
+  if (!launched) return false;
+  MXS_CHECK_LAUNCH();
+  if (splitk > 1) {
+    const long total4 = static_cast<long>(M) * outN / 4;
+    const int blocks = static_cast<int>(std::min<long>((total4 + 255) / 256, 1024));
+    if (epi == EPI_SILU)
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_SILU>, dim3(blocks), dim3(256), 0, s, Y, part, M, N, splitk, ldy,
+                         N / 2);
+    else
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_NONE>, dim3(blocks), dim3(256), 0, s, Y, part, M, N, splitk, ldy,
+                         0);
+    MXS_CHECK_LAUNCH();
+  }
+  return true;
+}
+
+}  // namespace mxs

@@ -534,6 +534,14 @@ class ModelRunner:
         if not buckets:
             log.warning("no decode bucket has graph-capturable collectives; decode runs eagerly")
             return
+        # decode projection GEMMs: hand-written MFMA kernel vs hipBLASLt, measured per bucket
+        from ..ops import decode_gemm
+        w = m.w
+        shapes = {"qkv": (w["l0.qkv"], 0), "o": (w["l0.o"], 0), "lm_head": (m.lm_head_weight(), 0)}
+        if not self.cfg.is_moe:
+            shapes.update(gate_up=(w["l0.gate_up"], 1), down=(w["l0.down"], 0))
+        with torch.inference_mode():
+            self.decode_gemm_report = decode_gemm.tune(shapes, buckets, self.device, self.dtype)
         self._arange = torch.arange(max(buckets), dtype=torch.int64, device=self.device)
         # benign contents for capture: every row is a 1-token sequence that writes nowhere
         h = self.buf.hn

@@ -234,7 +234,7 @@ class TransformerLM:
             tw, tid = ops.moe_topk_softmax(router, self.cfg.num_experts_per_tok)
             out = ops.moe_experts(h, w[p + "w13"], w[p + "w2"], tw, tid, self.e_offset)
         else:
-            a = ops.silu_mul(ops.linear(h, w[p + "gate_up"]))
+            a = ops.gate_up_silu(h, w[p + "gate_up"])
             out = ops.linear(a, w[p + "down"])
         return tp_all_reduce(out)
 

@@ -53,22 +53,31 @@ def _gpu(t: torch.Tensor) -> bool:
 
 
 # ----------------------------------------------------------------------------- GEMM
-SKINNY_MAX_M = 256
-
-
-_SKINNY = os.environ.get("MXS_SKINNY_GEMM", "0") == "1"
-
-
 def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """y = x @ w.T.  hipBLASLt by default.  MXS_SKINNY_GEMM=1 routes decode-sized GEMMs (M <= 256)
-    to the weight-streaming MFMA kernel (csrc/kernels/gemm_skinny.hip).  Measured inside hipGraphs
-    (profiles/r1_v4_microbench_gemm.jsonl) it only ties hipBLASLt at M <= 16 and loses at larger M
-    (no LDS reuse of the activation tile yet), so it is opt-in."""
-    if _SKINNY and _gpu(x) and x.dim() == 2 and x.shape[0] <= SKINNY_MAX_M:
-        out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-        if ext().skinny_gemm(out, x, w):
-            return out
+    """y = x @ w.T.  Decode-sized GEMMs (M <= 256) run the hand-written MFMA kernel where the
+    tuning pass at graph capture measured it faster than hipBLASLt for that batch bucket and
+    projection (mxserve/ops/decode_gemm.py); everything else is hipBLASLt."""
+    if _gpu(x) and x.dim() == 2 and x.shape[0] <= 256:
+        from .decode_gemm import TABLE
+        cfg = TABLE.lookup(x.shape[0], w.shape[0], w.shape[1], 0)
+        if cfg is not None:
+            out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+            if TABLE.run(out, x, w, cfg, 0):
+                return out
     return torch.nn.functional.linear(x, w)
+
+
+def gate_up_silu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """silu(x @ gate.T) * (x @ up.T) with w = [gate; up] (K07 + K10).  Decode-sized: one MFMA kernel
+    with SiLU*mul in its epilogue when tuned faster; otherwise hipBLASLt + the SiLU*mul kernel."""
+    if _gpu(x) and x.dim() == 2 and x.shape[0] <= 256:
+        from .decode_gemm import TABLE
+        cfg = TABLE.lookup(x.shape[0], w.shape[0], w.shape[1], 1)
+        if cfg is not None:
+            out = torch.empty(x.shape[0], w.shape[0] // 2, dtype=x.dtype, device=x.device)
+            if TABLE.run(out, x, w, cfg, 1):
+                return out
+    return silu_mul(linear(x, w))
 
 
 # ----------------------------------------------------------------------------- norms / act

@@ -103,6 +103,29 @@ def main():
         return ops.sample(lg, temp, torch.ones(B, device=dev), torch.zeros(B, dtype=torch.int32, device=dev),
                           torch.arange(B, device=dev), torch.zeros(B, dtype=torch.int64, device=dev))
 
+    # decode projection GEMMs: the graph-time tuner picks the MFMA kernel or hipBLASLt per projection
+    from mxserve.ops import decode_gemm
+    wd = m.w
+    with torch.inference_mode():
+        rows = decode_gemm.tune({"qkv": (wd["l0.qkv"], 0), "o": (wd["l0.o"], 0), "gate_up": (wd["l0.gate_up"], 1),
+                                 "down": (wd["l0.down"], 0), "lm_head": (m.lm_head_weight(), 0)}, [B], dev)
+    for r in rows:
+        out.append(dict(r, op="decode_gemm_tune"))
+    mode = decode_gemm.MODE
+    decode_gemm.MODE = "off"
+    with torch.inference_mode():
+        g0 = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            step()
+        torch.cuda.current_stream().wait_stream(s)
+        with torch.cuda.graph(g0):
+            step()
+        tg0 = timeit(g0.replay, iters=20)
+    decode_gemm.MODE = mode
+    out.append({"op": "decode_step_hipblaslt_only", "B": B, "ctx": ctx, "graph_ms": tg0})
+    del g0
     with torch.inference_mode():
         te = timeit(step, iters=10)
         g = torch.cuda.CUDAGraph()
@@ -178,8 +201,8 @@ def main():
             x = torch.randn(Mrows, K, dtype=torch.bfloat16, device=dev)
             w = torch.randn(N, K, dtype=torch.bfloat16, device=dev)
             impls = {"hipblaslt": lambda: F.linear(x, w)}
-            if Mrows <= ops.SKINNY_MAX_M:
-                impls["skinny"] = lambda: ops.linear(x, w)
+            if Mrows <= 256:
+                impls["decode_gemm_tuned"] = lambda: ops.linear(x, w)
             for impl, fn in impls.items():
                 tt = timeit_graph(fn)
                 out.append({"op": f"gemm_{name}", "impl": impl, "M": Mrows, "N": N, "K": K, "ms": tt,

@@ -467,26 +467,50 @@ def test_copy_blocks(gpu):
     assert dst[1].abs().sum().item() == 0
 
 
-@pytest.mark.parametrize("N,K", [(3072, 2048), (2048, 8192), (16384, 2048), (6144, 4096), (1056, 1024)])
-@pytest.mark.parametrize("M", [1, 3, 16, 24, 33, 64, 100, 256])
-def test_skinny_gemm(gpu, M, N, K):
-    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
-    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
-    w = (torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.02).to(torch.bfloat16)
-    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    assert ops.ext().skinny_gemm(out, x, w), "shape unexpectedly unsupported"
-    want = x.float() @ w.float().t()
-    _close(out, want, atol=2e-2, rtol=2e-2, name=f"skinny {M}x{N}x{K}")
+@pytest.mark.parametrize("N,K,epi", [(3072, 2048, 0), (2048, 8192, 0), (16384, 2048, 1), (2048, 2048, 0),
+                                     (28672, 4096, 1), (128256, 2048, 0)])
+@pytest.mark.parametrize("M", [1, 3, 16, 24, 33, 64, 100, 192, 256])
+def test_decode_gemm_all_configs(gpu, M, N, K, epi):
+    """Every tiling / split-K configuration of the decode projection kernel vs an fp32 reference,
+    plain (qkv / o / down / lm_head) and with SiLU*mul fused (gate_up: w = [gate; up])."""
+    from mxserve.ops import decode_gemm
+    x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu) * K ** -0.5).to(torch.bfloat16)
+    y = x.float() @ w.float().t()
+    want = torch.nn.functional.silu(y[:, :N // 2]) * y[:, N // 2:] if epi else y
+    cands = decode_gemm.candidates(M, N, K, epi)
+    assert cands
+    part = torch.empty(8 * M * N, dtype=torch.float32, device=gpu)
+    for mf, nf, wm, sk in cands:
+        out = torch.full((M, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
+        assert ops.ext().decode_gemm(out, x, w, part, mf, nf, wm, sk, epi)
+        _close(out, want, atol=2e-2, rtol=2e-2, name=f"decode gemm {M}x{N}x{K} epi{epi} cfg {(mf, nf, wm, sk)}")
 
 
-def test_skinny_gemm_strided_input_and_fallback(gpu):
-    x = torch.randn(8, 4096, device="cuda", dtype=torch.bfloat16)[:, :2048]  # row stride 4096
-    w = torch.randn(512, 2048, device="cuda", dtype=torch.bfloat16) * 0.02
-    _close(ops.linear(x, w), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2, name="strided")
-    w_odd = torch.randn(100, 2048, device="cuda", dtype=torch.bfloat16)  # N % 16 != 0 -> hipBLASLt
-    out = torch.empty(8, 100, device="cuda", dtype=torch.bfloat16)
-    assert not ops.ext().skinny_gemm(out, x.contiguous(), w_odd)
-    _close(ops.linear(x, w_odd), x.float() @ w_odd.float().t(), atol=0.3, rtol=2e-2, name="fallback")
+def test_decode_gemm_tuner_and_dispatch(gpu, monkeypatch):
+    """The graph-time tuner times the kernel against hipBLASLt per (bucket, projection), keeps a winner
+    only when it matches hipBLASLt, and ops.linear / ops.gate_up_silu then follow the table."""
+    from mxserve.ops import decode_gemm
+    monkeypatch.setattr(decode_gemm, "MODE", "auto")
+    w1 = (torch.randn(2048, 2048, device=gpu) * 0.02).to(torch.bfloat16)
+    w2 = (torch.randn(2 * 8192, 2048, device=gpu) * 0.02).to(torch.bfloat16)
+    rows = decode_gemm.tune({"o": (w1, 0), "gate_up": (w2, 1)}, [8, 64, 256], gpu)
+    assert len(rows) == 6 and all(r["us"] <= r["hipblaslt_us"] for r in rows)
+    x = torch.randn(64, 2048, device=gpu, dtype=torch.bfloat16)
+    _close(ops.linear(x, w1), x.float() @ w1.float().t(), 2e-2, 2e-2, "tuned linear")
+    y = x.float() @ w2.float().t()
+    _close(ops.gate_up_silu(x, w2), torch.nn.functional.silu(y[:, :8192]) * y[:, 8192:], 2e-2, 2e-2, "tuned gate_up")
+
+
+def test_decode_gemm_rejects_untiled_shapes(gpu):
+    x = torch.randn(8, 1000, device=gpu, dtype=torch.bfloat16)  # K not a multiple of 32
+    w = torch.randn(1056, 1000, device=gpu, dtype=torch.bfloat16)
+    out = torch.empty(8, 1056, device=gpu, dtype=torch.bfloat16)
+    assert not ops.ext().decode_gemm(out, x, w, None, 1, 2, 1, 1, 0)
+    w2 = torch.randn(1000, 1024, device=gpu, dtype=torch.bfloat16)  # N not a multiple of the tile
+    x2 = torch.randn(8, 1024, device=gpu, dtype=torch.bfloat16)
+    assert not ops.ext().decode_gemm(torch.empty(8, 1000, device=gpu, dtype=torch.bfloat16), x2, w2, None, 1, 4, 1,
+                                     1, 0)
 
 
 @pytest.mark.parametrize("counts", [[0, 5, 300, 1], [128, 129, 0, 3], [1, 1, 1, 1]])
