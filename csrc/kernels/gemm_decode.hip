@@ -34,6 +34,9 @@ constexpr int EPI_SILU = 1;
 __device__ __forceinline__ bf16x8_t as_bf16x8(const u32x4& v) { return __builtin_bit_cast(bf16x8_t, v); }
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
+// k-steps per load group: ~8-12 fragments of 16 B per lane in flight per group (x2 with the next one)
+__host__ __device__ constexpr int decode_gemm_unroll(int mf, int nf) { return mf + nf <= 3 ? 8 : (mf + nf <= 6 ? 4 : 2); }
+
 template <int MF, int NF, int WM, int WN, int EPI>
 __global__ void __launch_bounds__(256) decode_gemm_kernel(bf16_t* __restrict__ Y, float* __restrict__ part,
                                                           const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
@@ -55,13 +58,15 @@ __global__ void __launch_bounds__(256) decode_gemm_kernel(bf16_t* __restrict__ Y
     const int col = (EPI == EPI_SILU && j >= NH) ? inter + c0 + 16 * (j - NH) : c0 + 16 * (j % NH);
     wp[j] = W + static_cast<size_t>(col + i) * K + kbeg + 8 * kq;
   }
+  // rows past M read row M-1 (never stored: an output element depends only on its own token row);
+  // unconditional loads keep hipcc from branching around each one and draining vmcnt per load
   const bf16_t* xp[MF];
   bool xv[MF];
 #pragma unroll
   for (int t = 0; t < MF; ++t) {
     const int m = m0 + 16 * t + i;
     xv[t] = m < M;
-    xp[t] = X + static_cast<size_t>(xv[t] ? m : 0) * ldx + kbeg + 8 * kq;
+    xp[t] = X + static_cast<size_t>(min(m, M - 1)) * ldx + kbeg + 8 * kq;
   }
   float4_ acc[MF][NF];
 #pragma unroll
@@ -69,29 +74,42 @@ __global__ void __launch_bounds__(256) decode_gemm_kernel(bf16_t* __restrict__ Y
 #pragma unroll
     for (int j = 0; j < NF; ++j) acc[t][j] = float4_{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 a[NF], b[MF];
-  auto load = [&](int k, u32x4 (&ad)[NF], u32x4 (&bd)[MF]) {
+  // U k-steps per group, all their loads issued back to back (enough bytes in flight per CU to
+  // stream HBM); the next group's loads are in flight while this group's MFMAs run
+  constexpr int U = decode_gemm_unroll(MF, NF);
+  u32x4 a[U][NF], b[U][MF];
+  auto load = [&](int k, u32x4 (&ad)[U][NF], u32x4 (&bd)[U][MF]) {
 #pragma unroll
-    for (int j = 0; j < NF; ++j) ad[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wp[j] + k));
-#pragma unroll
-    for (int t = 0; t < MF; ++t)
-      bd[t] = xv[t] ? *reinterpret_cast<const u32x4*>(xp[t] + k) : u32x4{0u, 0u, 0u, 0u};
-  };
-  load(0, a, b);
-  for (int k = 0; k < kslice; k += 32) {
-    u32x4 an[NF], bn[MF];
-    const bool more = k + 32 < kslice;
-    if (more) load(k + 32, an, bn);
-#pragma unroll
-    for (int t = 0; t < MF; ++t)
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int j = 0; j < NF; ++j)
-        acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[j]), as_bf16x8(b[t]), acc[t][j], 0, 0, 0);
+        ad[u][j] = *reinterpret_cast<const u32x4*>(wp[j] + k + 32 * u);
+#pragma unroll
+      for (int t = 0; t < MF; ++t)
+        bd[u][t] = *reinterpret_cast<const u32x4*>(xp[t] + k + 32 * u);
+    }
+  };
+  load(0, a, b);
+  for (int k = 0; k < kslice; k += 32 * U) {
+    u32x4 an[U][NF], bn[U][MF];
+    const bool more = k + 32 * U < kslice;
+    if (more) load(k + 32 * U, an, bn);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int t = 0; t < MF; ++t)
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[u][j]), as_bf16x8(b[u][t]), acc[t][j], 0,
+                                                              0, 0);
     if (more) {
 #pragma unroll
-      for (int j = 0; j < NF; ++j) a[j] = an[j];
+      for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int t = 0; t < MF; ++t) b[t] = bn[t];
+        for (int j = 0; j < NF; ++j) a[u][j] = an[u][j];
+#pragma unroll
+        for (int t = 0; t < MF; ++t) b[u][t] = bn[u][t];
+      }
     }
   }
 
@@ -156,7 +174,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
 bool launch_decode_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx,
                         int ldy, int MF, int NF, int WM, int splitk, int epi, hipStream_t s) {
   const int WN = 4 / WM;
-  if (M <= 0 || M > 256 || splitk < 1 || K % (32 * splitk) != 0 || ldx % 8 != 0 || ldy % 4 != 0) return false;
+  if (M <= 0 || M > 256 || splitk < 1 || ldx % 8 != 0 || ldy % 4 != 0) return false;
+  if (K % (32 * decode_gemm_unroll(MF, NF) * splitk) != 0) return false;
   const int outN = epi == EPI_SILU ? N / 2 : N;
   const int NH = epi == EPI_SILU ? NF / 2 : NF;
   const int BM = WM * MF * 16, BN = WN * NH * 16;

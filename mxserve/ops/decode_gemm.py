@@ -31,9 +31,21 @@ def _mf(M: int) -> int:
     return 1 if M <= 16 else (2 if M <= 32 else 4)
 
 
-def candidates(M: int, N: int, K: int, epi: int) -> list[tuple]:
-    """(mf, nf, wm, splitk) configurations that tile the shape."""
-    mf = _mf(M)
+def unroll(mf: int, nf: int) -> int:
+    """k-steps per load group (csrc/kernels/gemm_decode.hip decode_gemm_unroll)."""
+    return 8 if mf + nf <= 3 else (4 if mf + nf <= 6 else 2)
+
+
+def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False) -> list[tuple]:
+    """(mf, nf, wm, splitk) configurations that tile the shape (wave row tile MF x 16 sized to M
+    unless all_mf: then every MF, i.e. more row tiles re-reading the weights from L2)."""
+    out = []
+    for mf in ((1, 2, 4) if all_mf else (_mf(M),)):
+        out += _candidates_mf(M, N, K, epi, mf)
+    return out
+
+
+def _candidates_mf(M: int, N: int, K: int, epi: int, mf: int) -> list[tuple]:
     out = []
     for wm in (1, 2, 4):
         if wm > 1 and (wm // 2) * mf * 16 >= M:  # waves with no rows at all
@@ -45,7 +57,7 @@ def candidates(M: int, N: int, K: int, epi: int) -> list[tuple]:
             if outN % (wn * nh * 16):
                 continue
             for sk in (1, 2, 4, 8):
-                if K % (32 * sk) or K // sk < 128:
+                if K % (32 * unroll(mf, nf) * sk):
                     continue
                 out.append((mf, nf, wm, sk))
     return out
