@@ -24,6 +24,10 @@ import torch
 log = logging.getLogger(__name__)
 
 MAX_M = 256
+# buckets the capture-time tuner measures: above this the register-staged kernel measured 1.3-2.5x
+# behind hipBLASLt for every projection (profiles/r2_decode_gemm_probe_vs_hipblaslt.jsonl), so the
+# engine does not spend startup time timing them
+MAX_TUNE_M = int(os.environ.get("MXS_DECODE_GEMM_TUNE_MAX_M", "64"))
 MODE = os.environ.get("MXS_DECODE_GEMM", "auto")  # auto | off | force
 
 
@@ -129,7 +133,7 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
         return []
     from . import ext, silu_mul
     t0 = time.time()
-    bks = sorted(b for b in buckets if b <= MAX_M)
+    bks = sorted(b for b in buckets if b <= min(MAX_M, MAX_TUNE_M))
     if not bks:
         return []
     # workspace for the largest split-K any candidate may pick

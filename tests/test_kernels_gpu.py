@@ -492,6 +492,7 @@ def test_decode_gemm_tuner_and_dispatch(gpu, monkeypatch):
     only when it matches hipBLASLt, and ops.linear / ops.gate_up_silu then follow the table."""
     from mxserve.ops import decode_gemm
     monkeypatch.setattr(decode_gemm, "MODE", "auto")
+    monkeypatch.setattr(decode_gemm, "MAX_TUNE_M", 256)
     w1 = (torch.randn(2048, 2048, device=gpu) * 0.02).to(torch.bfloat16)
     w2 = (torch.randn(2 * 8192, 2048, device=gpu) * 0.02).to(torch.bfloat16)
     rows = decode_gemm.tune({"o": (w1, 0), "gate_up": (w2, 1)}, [8, 64, 256], gpu)
