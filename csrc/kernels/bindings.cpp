@@ -31,7 +31,7 @@ void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStre
 void launch_moe_align(int*, int*, const int*, int, int, int, int*, hipStream_t);
 void launch_moe_combine(bf16_t*, const bf16_t*, const float*, const int*, int, int, int, hipStream_t);
 bool launch_decode_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int,
-                        int, hipStream_t);
+                        int, hipStream_t, const int* = nullptr, int = 0, int = 0);
 bool launch_moe_grouped_gemm(bf16_t*, const bf16_t*, const bf16_t*, const int*, int, int, int, int, int, bool,
                              int, float*, hipStream_t);
 void launch_moe_combine_partials(bf16_t*, const float*, const float*, const int*, int, int, int, int, long,
@@ -235,6 +235,33 @@ bool decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::T
                                  epi, stream());
 }
 
+// Grouped decode form of decode_gemm (K16 at decode batches): w [E, N, K], x = routed rows sorted by
+// expert (offs = moe_align offsets), rows_max = the most rows one expert can hold (tokens).  Output
+// as moe_grouped_gemm: out [rows, N or N/2] (splitk 1) or fp32 partials [splitk, rows, N].
+bool moe_decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor offs, c10::optional<at::Tensor> part,
+                     int64_t rows_max, int64_t mf, int64_t nf, int64_t wm, int64_t splitk, int64_t epi) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(x);
+  TORCH_CHECK(w.dim() == 3 && x.dim() == 2, "w [E, N, K], x [rows, K]");
+  TORCH_CHECK(offs.scalar_type() == at::kInt && offs.is_contiguous() && offs.numel() == w.size(0) + 1,
+              "offs: int32 [E + 1]");
+  TORCH_CHECK(epi == 0 || epi == 1, "epi 0 (none) | 1 (silu*mul)");
+  const int64_t R = x.size(0), E = w.size(0), N = w.size(1), K = w.size(2);
+  TORCH_CHECK(x.size(1) == K, "shape mismatch");
+  TORCH_CHECK(rows_max >= 1 && rows_max <= R, "rows_max in [1, rows]");
+  float* p = nullptr;
+  int64_t ldy = epi == 1 ? N / 2 : N;
+  if (splitk > 1) {
+    TORCH_CHECK(part.has_value() && part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->numel() >= splitk * R * N, "split-K needs an fp32 workspace of splitk * rows * N");
+    p = part->data_ptr<float>();
+  } else {
+    CHECK_BF16(out); CHECK_CONTIG(out);
+    TORCH_CHECK(out.dim() == 2 && out.size(0) == R && out.size(1) == ldy, "out [rows, N or N/2]");
+  }
+  return mxs::launch_decode_gemm(splitk > 1 ? nullptr : bf(out), p, bf(x), bf(w), R, N, K, K, ldy, mf, nf, wm, splitk,
+                                 epi, stream(), offs.data_ptr<int>(), E, rows_max);
+}
+
 // y[r] = x[r] . w[e(r)]^T over expert-sorted rows (offs = moe_align offsets); silu: w rows are
 // [gate; up] and y = silu(gate) * up (width N/2).  False if the shape is unsupported.
 bool moe_grouped_gemm(at::Tensor y, at::Tensor x, at::Tensor w, at::Tensor offs, bool silu, int64_t split,
@@ -316,6 +343,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("decode_gemm", &decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("part"), pybind11::arg("mf"), pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"),
         pybind11::arg("epi"));
+  m.def("moe_decode_gemm", &moe_decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
+        pybind11::arg("offs"), pybind11::arg("part"), pybind11::arg("rows_max"), pybind11::arg("mf"),
+        pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"), pybind11::arg("epi"));
   m.def("moe_grouped_gemm", &moe_grouped_gemm, pybind11::arg("y"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("offs"), pybind11::arg("silu"), pybind11::arg("split") = 1,
         pybind11::arg("partial") = pybind11::none());

@@ -19,6 +19,13 @@
 //     activation is written (no [M, 2I] round trip, no separate SiLU*mul kernel).
 // The Python side (mxserve/ops/decode_gemm.py) times these configurations against hipBLASLt per
 // (graph bucket, projection) when the decode graphs are captured and keeps the faster one.
+//
+// Grouped form (G = true, K16 at decode batches): W is [E, N, K] per-expert weights and X holds the
+// routed rows sorted by expert (moe_align offsets `offs`); blockIdx.y = expert * rt + row tile, so
+// every expert with routed rows streams its weights once and an expert nobody picked costs nothing.
+// Mixtral decode routes ~2T/8 rows per expert: the wave tile is sized to those rows, not to the
+// 128-row tiles of the prefill grouped GEMM (moe_gemm.hip), which streams weights through LDS with
+// 2 workgroups per CU and leaves the HBM pipe half empty at that size.
 #include <algorithm>
 
 #include "common.h"
@@ -37,16 +44,25 @@ __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); 
 // k-steps per load group: ~8-12 fragments of 16 B per lane in flight per group (x2 with the next one)
 __host__ __device__ constexpr int decode_gemm_unroll(int mf, int nf) { return mf + nf <= 3 ? 8 : (mf + nf <= 6 ? 4 : 2); }
 
-template <int MF, int NF, int WM, int WN, int EPI>
+template <int MF, int NF, int WM, int WN, int EPI, bool G>
 __global__ void __launch_bounds__(256) decode_gemm_kernel(bf16_t* __restrict__ Y, float* __restrict__ part,
                                                           const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                           int M, int N, int K, int ldx, int ldy, int kslice,
-                                                          int inter) {
+                                                          int inter, const int* __restrict__ offs, int rt) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int i = lane & 15, kq = lane >> 4;
   constexpr int NH = EPI == EPI_SILU ? NF / 2 : NF;  // output fragments per wave
-  const int m0 = (blockIdx.y * WM + wm) * MF * 16;
+  int m0 = (blockIdx.y * WM + wm) * MF * 16;
+  int mlim = M;  // rows [.., mlim) are this wave's to store; M stays the split-K slab row count
+  if constexpr (G) {
+    const int e = blockIdx.y / rt, r = blockIdx.y - e * rt;
+    const int lo = offs[e], hi = offs[e + 1];
+    m0 = lo + (r * WM + wm) * MF * 16;
+    if (m0 >= hi) return;  // no barriers in this kernel: a wave without rows just leaves
+    mlim = hi;
+    W += static_cast<size_t>(e) * N * K;
+  }
   const int c0 = (blockIdx.x * WN + wn) * NH * 16;  // first OUTPUT column of the wave
   const int kbeg = blockIdx.z * kslice;
 
@@ -65,8 +81,8 @@ __global__ void __launch_bounds__(256) decode_gemm_kernel(bf16_t* __restrict__ Y
 #pragma unroll
   for (int t = 0; t < MF; ++t) {
     const int m = m0 + 16 * t + i;
-    xv[t] = m < M;
-    xp[t] = X + static_cast<size_t>(min(m, M - 1)) * ldx + kbeg + 8 * kq;
+    xv[t] = m < mlim;
+    xp[t] = X + static_cast<size_t>(min(m, mlim - 1)) * ldx + kbeg + 8 * kq;
   }
   float4_ acc[MF][NF];
 #pragma unroll
@@ -171,10 +187,14 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
 
 // config id = ((MF-1) * 2 + (NF/2-1)) * 3 + wave layout {0: 1x4, 1: 2x2, 2: 4x1}; MF in {1, 2, 4}
 // returns false when the configuration does not tile the shape (the caller keeps hipBLASLt).
+// Grouped form: offs != nullptr, E experts (W [E, N, K]), M = routed rows (slab rows), rows_max = the
+// most rows one expert can get (T tokens: an expert appears at most once in a token's top-k).
 bool launch_decode_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx,
-                        int ldy, int MF, int NF, int WM, int splitk, int epi, hipStream_t s) {
+                        int ldy, int MF, int NF, int WM, int splitk, int epi, hipStream_t s, const int* offs,
+                        int E, int rows_max) {
   const int WN = 4 / WM;
-  if (M <= 0 || M > 256 || splitk < 1 || ldx % 8 != 0 || ldy % 4 != 0) return false;
+  if (M <= 0 || splitk < 1 || ldx % 8 != 0 || ldy % 4 != 0) return false;
+  if (offs == nullptr ? M > 256 : (E < 1 || rows_max < 1 || rows_max > 256 || WM > 2)) return false;
   if (K % (32 * decode_gemm_unroll(MF, NF) * splitk) != 0) return false;
   const int outN = epi == EPI_SILU ? N / 2 : N;
   const int NH = epi == EPI_SILU ? NF / 2 : NF;
@@ -182,23 +202,26 @@ bool launch_decode_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W
   if (outN % BN != 0 || (epi == EPI_SILU && N % 2 != 0)) return false;
   if (splitk > 1 && part == nullptr) return false;
   const int kslice = K / splitk;
-  dim3 grid(outN / BN, (M + BM - 1) / BM, splitk), blk(256);
+  const int rt = offs == nullptr ? 1 : (rows_max + BM - 1) / BM;
+  dim3 grid(outN / BN, offs == nullptr ? (M + BM - 1) / BM : E * rt, splitk), blk(256);
   float* p = splitk > 1 ? part : nullptr;
-#define MXS_DG(mf, nf, wm, e)                                                                                  \
-  if (MF == mf && NF == nf && WM == wm && epi == e) {                                                        \
-    hipLaunchKernelGGL((decode_gemm_kernel<mf, nf, wm, 4 / wm, e>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, \
-                       ldy, kslice, N / 2);                                                                  \
-    launched = true;                                                                                         \
+  const bool g = offs != nullptr;
+#define MXS_DG(mf, nf, wm, e, gr)                                                                                   \
+  if (MF == mf && NF == nf && WM == wm && epi == e && g == gr) {                                                  \
+    hipLaunchKernelGGL((decode_gemm_kernel<mf, nf, wm, 4 / wm, e, gr>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, \
+                       ldy, kslice, N / 2, offs, rt);                                                             \
+    launched = true;                                                                                              \
   }
   bool launched = false;
-#define MXS_DG_WM(mf, nf, e) MXS_DG(mf, nf, 1, e) MXS_DG(mf, nf, 2, e) MXS_DG(mf, nf, 4, e)
+#define MXS_DG_WM(mf, nf, e) \
+  MXS_DG(mf, nf, 1, e, false) MXS_DG(mf, nf, 2, e, false) MXS_DG(mf, nf, 4, e, false) MXS_DG(mf, nf, 1, e, true) MXS_DG(mf, nf, 2, e, true)
   MXS_DG_WM(1, 2, 0) MXS_DG_WM(1, 4, 0) MXS_DG_WM(2, 2, 0) MXS_DG_WM(2, 4, 0) MXS_DG_WM(4, 2, 0) MXS_DG_WM(4, 4, 0)
   MXS_DG_WM(1, 2, 1) MXS_DG_WM(1, 4, 1) MXS_DG_WM(2, 2, 1) MXS_DG_WM(2, 4, 1) MXS_DG_WM(4, 2, 1) MXS_DG_WM(4, 4, 1)
 #undef MXS_DG_WM
 #undef MXS_DG
   if (!launched) return false;
   MXS_CHECK_LAUNCH();
-  if (splitk > 1) {
+  if (splitk > 1 && offs == nullptr) {  // grouped: the MoE combine / silu_mul_partials kernels sum the slabs
     const long total4 = static_cast<long>(M) * outN / 4;
     const int blocks = static_cast<int>(std::min<long>((total4 + 255) / 256, 1024));
     if (epi == EPI_SILU)

@@ -54,47 +54,67 @@ void launch_moe_topk_softmax(float* w, int* ids, const bf16_t* logits, int T, in
 // Counting sort of the T*K (token, slot) assignments by expert, stable in assignment order.
 // Outputs: expert_offsets[E_local+1] (row ranges in the permuted order), perm[] = flat (t*K + k)
 // index of each permuted row.  Only experts in [e_lo, e_lo + E_local) are kept (expert parallel).
-// One workgroup: per 64-assignment chunk every wave-lane learns its rank among equal experts from
-// one ballot per local expert (E_local <= 64 on every config here).
 // inv (optional): inv[i] = permuted row of assignment i, -1 when its expert is not local.
-__global__ void __launch_bounds__(64) moe_align_kernel(int* __restrict__ expert_offsets, int* __restrict__ perm,
-                                                       const int* __restrict__ topk_ids, int TK, int e_lo,
-                                                       int E_local, int* __restrict__ inv) {
-  __shared__ int cnt[257];
-  const int lane = threadIdx.x;
+// One 1024-thread workgroup (a prefill chunk of 8192 tokens x top-2 is 16 passes, not 256):
+//   counts   LDS atomics, then an exclusive scan by thread 0 (E_local <= 256);
+//   ranks    per 1024-assignment pass, one ballot per local expert gives each lane its rank among
+//            equal experts in its wave; a wave's offset is the sum of the earlier waves' counts
+//            (kept per wave in LDS), so the order stays the assignment order with no atomics.
+constexpr int kAlignMaxE = 256;
+constexpr int kAlignWaves = 16;
+
+__global__ void __launch_bounds__(1024) moe_align_kernel(int* __restrict__ expert_offsets, int* __restrict__ perm,
+                                                         const int* __restrict__ topk_ids, int TK, int e_lo,
+                                                         int E_local, int* __restrict__ inv) {
+  __shared__ int base[kAlignMaxE + 1];
+  __shared__ int wave_tot[kAlignWaves][kAlignMaxE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  for (int e = lane; e <= E_local; e += 64) cnt[e] = 0;
+  for (int e = tid; e <= E_local; e += blockDim.x) base[e] = 0;
   __syncthreads();
-  for (int i = lane; i < TK; i += 64) {
+  for (int i = tid; i < TK; i += blockDim.x) {
     const int e = topk_ids[i] - e_lo;
-    if (e >= 0 && e < E_local) atomicAdd(&cnt[e + 1], 1);
+    if (e >= 0 && e < E_local) atomicAdd(&base[e + 1], 1);
   }
   __syncthreads();
-  if (lane == 0) {
-    for (int e = 0; e < E_local; ++e) cnt[e + 1] += cnt[e];
-    for (int e = 0; e <= E_local; ++e) expert_offsets[e] = cnt[e];
+  if (tid == 0) {
+    for (int e = 0; e < E_local; ++e) base[e + 1] += base[e];
+    for (int e = 0; e <= E_local; ++e) expert_offsets[e] = base[e];
   }
   __syncthreads();
-  for (int base = 0; base < TK; base += 64) {
-    const int i = base + lane;
-    const int e = i < TK ? topk_ids[i] - e_lo : -1;
-    int dst = -1;
+  for (int p0 = 0; p0 < TK; p0 += blockDim.x) {
+    const int i = p0 + tid;
+    int e = i < TK ? topk_ids[i] - e_lo : -1;
+    if (e >= E_local) e = -1;
+    int rank = 0;
     for (int x = 0; x < E_local; ++x) {
       const unsigned long long m = __ballot(e == x);
-      if (m == 0ull) continue;
-      if (e == x) dst = cnt[x] + __popcll(m & lt);
-      __syncthreads();
-      if (lane == 0) cnt[x] += __popcll(m);
-      __syncthreads();
+      if (e == x) rank = __popcll(m & lt);
+      if (lane == 0) wave_tot[wid][x] = __popcll(m);
     }
-    if (dst >= 0) perm[dst] = i;
+    __syncthreads();
+    int dst = -1;
+    if (e >= 0) {
+      dst = base[e] + rank;
+      for (int w = 0; w < wid; ++w) dst += wave_tot[w][e];
+      perm[dst] = i;
+    }
     if (inv != nullptr && i < TK) inv[i] = dst;
+    __syncthreads();
+    const int nw = blockDim.x >> 6;
+    for (int x = tid; x < E_local; x += blockDim.x) {
+      int t = 0;
+      for (int w = 0; w < nw; ++w) t += wave_tot[w][x];
+      base[x] += t;
+    }
+    __syncthreads();
   }
 }
 
 void launch_moe_align(int* expert_offsets, int* perm, const int* topk_ids, int TK, int e_lo, int E_local,
                       int* inv, hipStream_t s) {
-  hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(64), 0, s, expert_offsets, perm, topk_ids, TK, e_lo,
+  if (E_local < 1 || E_local > kAlignMaxE) return;
+  hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(1024), 0, s, expert_offsets, perm, topk_ids, TK, e_lo,
                      E_local, inv);
   MXS_CHECK_LAUNCH();
 }

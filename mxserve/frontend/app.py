@@ -47,6 +47,8 @@ def _parse_token_line(d: dict, out: list) -> None:
     list of every token that was ready when the worker wrote it)."""
     toks = d["t"]
     if not isinstance(toks, list):
+        if toks == -2:  # the worker dropped the stream (fault injection on the mux plane)
+            raise ConnectionError("worker dropped the stream")
         if toks < 0:
             raise RuntimeError("worker failed the request")
         out.append(TokenEvent(toks, d["f"], d["r"], d["p"], d["c"], d.get("lp"), d.get("tlp"), d.get("tm")))
@@ -54,6 +56,8 @@ def _parse_token_line(d: dict, out: list) -> None:
     n = len(toks)
     lps, tlps = d.get("lp") or [None] * n, d.get("tlp") or [None] * n
     for i, t in enumerate(toks):
+        if t == -2:
+            raise ConnectionError("worker dropped the stream")
         if t < 0:
             raise RuntimeError("worker failed the request")
         last = i == n - 1
@@ -93,6 +97,76 @@ async def _merge(gens: list):
     finally:
         for t in tasks:
             t.cancel()
+
+
+REQUEST_PLANE = os.environ.get("MXS_REQUEST_PLANE", "mux")  # mux | stream
+
+
+class MuxClient:
+    """This frontend process's end of one worker's multiplexed request plane (worker/server.py
+    POST /mux): one long-lived NDJSON channel carries the tokens of every request this process sends
+    to the worker, one line per engine step, demultiplexed here into per-request queues.  Requests
+    join with POST /submit and leave early with POST /abort.  If the channel breaks, every request
+    on it sees a ConnectionError (retry / migration, as for a broken /generate stream)."""
+
+    HELLO_TIMEOUT = 10.0
+
+    def __init__(self, url: str):
+        self.url = url.rstrip("/")
+        self.sid = uuid.uuid4().hex
+        self.queues: dict[str, asyncio.Queue] = {}
+        self.task: Optional[asyncio.Task] = None
+        self.ready: Optional[asyncio.Future] = None
+        self.unsupported = False  # the worker has no /mux: use /generate streams
+
+    async def ensure(self, sess) -> None:
+        if self.task is None or self.task.done():
+            self.ready = asyncio.get_running_loop().create_future()
+            self.task = asyncio.ensure_future(self._read(sess, self.ready))
+        await asyncio.wait_for(asyncio.shield(self.ready), self.HELLO_TIMEOUT)
+
+    def reset(self) -> None:
+        if self.task is not None and not self.task.done():
+            self.task.cancel()
+        self.task = None
+
+    async def _read(self, sess, ready: asyncio.Future) -> None:
+        err: BaseException = ConnectionError(f"request channel to {self.url} closed")
+        try:
+            async with sess.post(self.url + "/mux", json={"sid": self.sid}) as r:
+                if r.status == 404:
+                    self.unsupported = True
+                if r.status != 200:
+                    raise ConnectionError(f"request channel to {self.url}: HTTP {r.status}")
+                buf = b""
+                queues = self.queues
+                async for data in r.content.iter_any():
+                    buf += data
+                    *lines, buf = buf.split(b"\n")
+                    for line in lines:
+                        if not line:
+                            continue
+                        d = json.loads(line)
+                        b = d.get("b")
+                        if b is None:
+                            if "hello" in d and not ready.done():
+                                ready.set_result(True)
+                            continue
+                        for rid, payload in b:
+                            q = queues.get(rid)
+                            if q is not None:
+                                q.put_nowait(payload)
+        except asyncio.CancelledError:
+            err = ConnectionError(f"request channel to {self.url} closed")
+            raise
+        except BaseException as e:  # noqa: BLE001 - handed to every request on the channel
+            err = e if isinstance(e, _STREAM_ERRORS) else ConnectionError(f"request channel failed: {e!r}")
+        finally:
+            if not ready.done():
+                ready.set_exception(err)
+            for q in self.queues.values():
+                q.put_nowait(err)
+            self.queues.clear()
 
 
 class APIError(Exception):
@@ -163,6 +237,8 @@ class Frontend:
         self._tok = {}
         self._cfg = {}
         self.local: dict[str, LocalWorker] = {}
+        self._mux: dict[str, MuxClient] = {}
+        self._bg: set = set()  # fire-and-forget tasks (aborts), referenced until done
         self._http = None
         self.started = time.time()
         self.app = self._build_app()
@@ -221,6 +297,20 @@ class Frontend:
         body = {"request_id": rid, "token_ids": token_ids, "sampling": sampling}
         if prefill_url:
             body["prefill_url"] = prefill_url
+        if REQUEST_PLANE == "mux":
+            mc = self._mux.get(w.url)
+            if mc is None:
+                mc = self._mux[w.url] = MuxClient(w.url)
+            if not mc.unsupported:
+                try:
+                    await mc.ensure(sess)
+                except _STREAM_ERRORS:
+                    if not mc.unsupported:
+                        raise
+                if not mc.unsupported:
+                    async for evs in self._mux_stream(sess, mc, body, rid):
+                        yield evs
+                    return
         async with sess.post(w.url.rstrip("/") + "/generate", json=body) as r:
             if r.status != 200:
                 raise ConnectionError(f"worker {w.worker_id} returned {r.status}")
@@ -238,6 +328,47 @@ class Frontend:
                 evs = []
                 _parse_token_line(json.loads(buf), evs)
                 yield evs
+
+    async def _mux_stream(self, sess, mc: MuxClient, body: dict, rid: str) -> AsyncIterator[list]:
+        q: asyncio.Queue = asyncio.Queue()
+        mc.queues[rid] = q
+        done = False
+        try:
+            async with sess.post(mc.url + "/submit", json=dict(body, sid=mc.sid)) as r:
+                if r.status == 404:  # the worker no longer knows this channel (restarted): reopen
+                    mc.reset()
+                if r.status != 200:
+                    raise ConnectionError(f"submit to {mc.url} returned {r.status}")
+            while True:
+                item = await q.get()
+                if isinstance(item, BaseException):
+                    raise item
+                evs: list = []
+                _parse_token_line(item, evs)
+                while not evs[-1].finished and not q.empty():
+                    item = q.get_nowait()
+                    if isinstance(item, BaseException):
+                        raise item
+                    _parse_token_line(item, evs)
+                if evs[-1].finished:
+                    done = True
+                yield evs
+                if done:
+                    return
+        finally:
+            mc.queues.pop(rid, None)
+            if not done:  # client gone, or the stream failed: free the worker's slot
+                t = asyncio.ensure_future(self._post_abort(sess, mc.url, rid))
+                self._bg.add(t)
+                t.add_done_callback(self._bg.discard)
+
+    @staticmethod
+    async def _post_abort(sess, url: str, rid: str) -> None:
+        try:
+            async with sess.post(url + "/abort", json={"request_id": rid}) as r:
+                await r.read()
+        except Exception:  # noqa: BLE001 - the worker is gone: nothing to free
+            pass
 
     async def generate_tokens(self, model: str, token_ids: list, sampling: dict, rid: str) -> AsyncIterator[TokenEvent]:
         """Route + stream.  A worker that fails before the first token is retried elsewhere; one that
@@ -679,6 +810,8 @@ class Frontend:
         task = asyncio.get_running_loop().create_task(reaper())
         yield
         task.cancel()
+        for mc in self._mux.values():
+            mc.reset()
         if self._http is not None:
             await self._http.close()
             self._http = None

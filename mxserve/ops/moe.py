@@ -11,10 +11,22 @@ otherwise) for shapes the grouped kernel does not tile.
 """
 from __future__ import annotations
 
+import bisect
+import logging
+import os
+import time
+
 import torch
 import torch.nn.functional as F
 
+log = logging.getLogger(__name__)
+
 DENSE_MAX_TOKENS = 256
+# decode batches (T tokens <= this, graph-captured): both expert GEMMs on the grouped form of the
+# decode GEMM kernel (gemm_decode.hip: weights streamed through registers, wave tile sized to the
+# few rows each expert gets) instead of the 128-row LDS tiles of moe_gemm.hip
+DECODE = os.environ.get("MXS_MOE_DECODE_GEMM", "1") != "0"
+DECODE_MAX_TOKENS = 256
 # grouped kernel up to this many tokens (decode / mixed steps, graph-capturable); above it the
 # per-expert hipBLASLt GEMMs over sorted rows are faster (profiles/r1_moe_layer_mixtral.jsonl:
 # grouped 0.82 / 0.86 ms vs 0.89 / 1.22 ms at T = 64 / 256; 2.77 vs 2.01 ms at T = 2048)
@@ -69,6 +81,85 @@ def _fused_experts_loop(x, w13, w2, topk_w, topk_ids, expert_offset):
     return out.to(x.dtype)
 
 
+# measured at graph capture (tune()): (H, I, E_local, top_k) -> sorted [(T bucket, cfg13, cfg2)];
+# cfg13 None = the LDS-tiled grouped GEMM measured faster for that bucket
+TABLE: dict = {}
+
+
+def _table_cfg(T: int, H: int, I: int, e_local: int, top_k: int):
+    ent = TABLE.get((H, I, e_local, top_k))
+    if not ent:
+        return False
+    i = bisect.bisect_left(ent, (T,))
+    if i == len(ent):
+        return None
+    return ent[i][1], ent[i][2]
+
+
+def decode_cfg(T: int, N: int, K: int, epi: int, e_local: int, top_k: int = 2) -> tuple | None:
+    """Untuned default (mf, nf, wm, splitk) of the grouped decode kernel for T tokens: the wave's row
+    tile covers the average rows per expert (T * top_k / experts), enough split-K to put ~1024
+    workgroups on the chip.  tune() replaces it per bucket with measured choices
+    (scripts/moe_decode_probe.py prints every configuration)."""
+    from .decode_gemm import unroll
+    avg = -(-T * top_k // max(1, e_local))
+    mf = 1 if avg <= 16 else (2 if avg <= 32 else 4)
+    nf = 2 if epi else 4
+    nh = nf // 2 if epi else nf
+    out_n = N // 2 if epi else N
+    bn = 4 * nh * 16
+    if out_n % bn:
+        return None
+    tiles = (out_n // bn) * min(e_local, T * top_k)
+    best = None
+    for sk in (1, 2, 4, 8):
+        if K % (32 * unroll(mf, nf) * sk) == 0:
+            best = (mf, nf, 1, sk)
+            if tiles * sk >= 1024:
+                break
+    return best
+
+
+def _fused_experts_decode(x, w13, w2, topk_w, offs, inv, xs, expert_offset) -> torch.Tensor | None:
+    from . import ext
+    T, H = x.shape
+    K = topk_w.shape[1]
+    e_local, two_i, _ = w13.shape
+    R = T * K
+    tuned = _table_cfg(T, H, two_i // 2, e_local, K)
+    if tuned is False:  # not tuned for this shape: defaults
+        c13 = decode_cfg(T, two_i, H, 1, e_local, K)
+        c2 = decode_cfg(T, H, two_i // 2, 0, e_local, K)
+    elif tuned is None:
+        return None
+    else:
+        c13, c2 = tuned
+    if c13 is None or c2 is None:
+        return None
+    dev = x.device
+    h = torch.empty(R, two_i // 2, dtype=x.dtype, device=dev)
+    if c13[3] > 1:
+        p13 = torch.empty(c13[3], R, two_i, dtype=torch.float32, device=dev)
+        if not ext().moe_decode_gemm(h, xs, w13, offs, p13, T, *c13, 1):
+            return None
+        ext().silu_mul_partials(h, p13)
+    elif not ext().moe_decode_gemm(h, xs, w13, offs, None, T, *c13, 1):
+        return None
+    out = torch.empty(T, H, dtype=x.dtype, device=dev)
+    tw = topk_w.float().contiguous()
+    if c2[3] > 1:
+        p2 = torch.empty(c2[3], R, H, dtype=torch.float32, device=dev)
+        if not ext().moe_decode_gemm(h, h, w2, offs, p2, T, *c2, 0):
+            return None
+        ext().moe_combine_partials(out, p2, tw, inv)
+    else:
+        ys = torch.empty(R, H, dtype=x.dtype, device=dev)
+        if not ext().moe_decode_gemm(ys, h, w2, offs, None, T, *c2, 0):
+            return None
+        ext().moe_combine(out, ys, tw, inv)
+    return out
+
+
 def fused_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
                   topk_ids: torch.Tensor, expert_offset: int = 0) -> torch.Tensor:
     """K15 align -> gather -> K16 grouped GEMM (gate_up with SiLU*mul fused in its epilogue) ->
@@ -89,6 +180,10 @@ def fused_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: 
     rows = perm.clamp(min=0).long()
     tok = rows // K
     xs = x.index_select(0, tok)  # rows past the routed count are ignored by the GEMMs
+    if DECODE and T <= DECODE_MAX_TOKENS and w13.is_contiguous() and w2.is_contiguous():
+        out = _fused_experts_decode(x, w13, w2, topk_w, offs, inv, xs, expert_offset)
+        if out is not None:
+            return out
     h = torch.empty(T * K, two_i // 2, dtype=x.dtype, device=dev)
     ys = torch.empty(T * K, H, dtype=x.dtype, device=dev)
     # split-K for the down projection when the routed rows leave too few workgroups to stream the
@@ -114,3 +209,80 @@ def fused_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: 
     else:
         ext().moe_combine(out, ys, topk_w.float().contiguous(), inv)  # K17
     return out
+
+
+def tune(w13: torch.Tensor, w2: torch.Tensor, buckets: list, top_k: int, n_experts: int, expert_offset: int = 0,
+         device=None) -> list:
+    """Per decode bucket T: time every configuration of the grouped decode kernel for both expert
+    GEMMs (hipGraph-replayed, synthetic uniform routing over all n_experts), then the whole layer
+    on the tuned kernel vs the LDS-tiled grouped GEMM, and keep the faster (TABLE).  Returns the
+    report rows."""
+    global DECODE
+    from . import ext
+    from .decode_gemm import _graph_time, candidates
+    if not DECODE:
+        return []
+    e_local, two_i, H = w13.shape
+    I = two_i // 2
+    dev = device or w13.device
+    g = torch.Generator(device=dev).manual_seed(0)
+    bks = sorted(b for b in buckets if b <= DECODE_MAX_TOKENS)
+    t0 = time.time()
+    rows, ent = [], []
+    key = (H, I, e_local, top_k)
+    TABLE.pop(key, None)
+    for T in bks:
+        R = T * top_k
+        x = torch.randn(T, H, device=dev, generator=g).to(w13.dtype)
+        logits = torch.randn(T, n_experts, device=dev, generator=g)
+        tw, ids = torch.topk(torch.softmax(logits, -1), top_k, dim=-1)
+        tw, ids = (tw / tw.sum(-1, keepdim=True)).float().contiguous(), ids.to(torch.int32).contiguous()
+        offs = torch.empty(e_local + 1, dtype=torch.int32, device=dev)
+        perm = torch.full((R,), -1, dtype=torch.int32, device=dev)
+        inv = torch.empty(R, dtype=torch.int32, device=dev)
+        ext().moe_align(offs, perm, ids, expert_offset, e_local, inv)
+        xs = x.index_select(0, perm.clamp(min=0).long() // top_k)
+        h = torch.empty(R, I, dtype=w13.dtype, device=dev)
+        ys = torch.empty(R, H, dtype=w13.dtype, device=dev)
+        part = torch.empty(8 * R * max(two_i, H), dtype=torch.float32, device=dev)
+        best = {}
+        for name, w, epi, N, K, o, xin in (("w13", w13, 1, two_i, H, h, xs), ("w2", w2, 0, H, I, ys, h)):
+            bt, bc = None, None
+            for cfg in candidates(T, N, K, epi, all_mf=True):
+                mf, nf, wm, sk = cfg
+                if wm > 2:
+                    continue
+                pp = part[: sk * R * N].view(sk, R, N) if sk > 1 else None
+                if not ext().moe_decode_gemm(o, xin, w, offs, pp, T, mf, nf, wm, sk, epi):
+                    continue
+                t = _graph_time(lambda: ext().moe_decode_gemm(o, xin, w, offs, pp, T, mf, nf, wm, sk, epi))
+                if bt is None or t < bt:
+                    bt, bc = t, cfg
+            best[name] = bc
+        if best["w13"] is None or best["w2"] is None:
+            ent.append((T, None, None))
+            continue
+        DECODE = False
+        t_lds = _graph_time(lambda: fused_experts(x, w13, w2, tw, ids, expert_offset))
+        ref = fused_experts(x, w13, w2, tw, ids, expert_offset)
+        DECODE = True
+        TABLE[key] = ent + [(T, best["w13"], best["w2"])]
+        t_dec = _graph_time(lambda: fused_experts(x, w13, w2, tw, ids, expert_offset))
+        out = fused_experts(x, w13, w2, tw, ids, expert_offset)
+        err = (out.float() - ref.float()).abs().max().item()
+        ok = err <= 0.03 * max(1.0, ref.float().abs().max().item())
+        use = ok and t_dec < t_lds * 0.98
+        ent.append((T, best["w13"], best["w2"]) if use else (T, None, None))
+        rows.append({"T": T, "cfg_w13": best["w13"], "cfg_w2": best["w2"], "layer_decode_us": round(t_dec, 1),
+                     "layer_grouped_lds_us": round(t_lds, 1), "chosen": "decode" if use else "grouped_lds",
+                     "max_abs_err": err})
+    TABLE[key] = ent
+    path = os.environ.get("MXS_MOE_GEMM_REPORT")
+    if path:
+        import json
+        with open(path, "w") as f:
+            for r in rows:
+                f.write(json.dumps(r) + "\n")
+    log.info("MoE decode GEMM tuning: decode kernel chosen for %d of %d buckets in %.1fs",
+             sum(r["chosen"] == "decode" for r in rows), len(bks), time.time() - t0)
+    return rows

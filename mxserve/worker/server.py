@@ -4,6 +4,11 @@ Replaces `python3 -m dynamo.{vllm,sglang,trtllm}` (examples/deploy/*/agg.yaml:29
   POST /generate   token-level request plane used by the frontend: NDJSON stream of token ids
                    (`prefill_url` set on a decode worker = disaggregated: reserve blocks, ask the
                    prefill worker to fill them over xGMI, then decode; falls back to local prefill)
+  POST /mux        the multiplexed form: one long-lived NDJSON channel per frontend process that
+  POST /submit     carries every request's tokens, one line per engine step ({"b": [[rid, batch],
+  POST /abort      ...]}); requests join a channel with /submit and leave early with /abort.  At
+                   ~200 running requests this is one write per step instead of 200 streamed
+                   responses, so the HTTP side stops competing with the engine thread for the GIL
   POST /prefill    prefill worker: compute the prompt, push its KV blocks into the decode worker's
                    pool, return the first token
   POST /kv_write   host-staged KV backend (decode side)
@@ -65,6 +70,10 @@ def _batch_line(outs: list) -> bytes:
     frontend at tens of thousands of tokens/s) gets fewer, larger lines instead of a backlog."""
     if len(outs) == 1:
         return _line(outs[0])
+    return (json.dumps(_batch_dict(outs)) + "\n").encode()
+
+
+def _batch_dict(outs: list) -> dict:
     last = outs[-1]
     d = {"t": [o.token_id for o in outs], "f": last.finished, "r": last.finish_reason, "p": last.num_prompt_tokens,
          "c": last.num_cached_tokens}
@@ -74,7 +83,77 @@ def _batch_line(outs: list) -> bytes:
     tm = next((o.timing for o in outs if o.timing), None)
     if tm:
         d["tm"] = tm
-    return (json.dumps(d) + "\n").encode()
+    return d
+
+
+class _MuxSink:
+    """Stands in for a request's asyncio.Queue in AsyncEngine._queues: outputs go to its channel
+    (put_nowait runs on the event loop, from AsyncEngine._deliver's one wakeup per step)."""
+    __slots__ = ("ch",)
+
+    def __init__(self, ch: "MuxChannel"):
+        self.ch = ch
+
+    def put_nowait(self, o) -> None:
+        self.ch.pending.append(o)
+        self.ch.wake.set()
+
+
+class _DropSink(_MuxSink):
+    """Fault injection (MXS_FAULT drop_stream) on the mux plane: after the first token the request
+    is aborted and its stream ends with a "dropped" marker (token -2), which the frontend treats as
+    a lost connection (retry / migrate)."""
+    __slots__ = ("n", "on_drop")
+
+    def __init__(self, ch: "MuxChannel", on_drop):
+        super().__init__(ch)
+        self.n = 0
+        self.on_drop = on_drop
+
+    def put_nowait(self, o) -> None:
+        self.n += 1
+        if self.n == 1:
+            super().put_nowait(o)
+        elif self.n == 2:
+            super().put_nowait(StepOutput(o.request_id, -2, True, "abort", 0, 0, 0))
+            self.on_drop(o.request_id)
+
+
+class MuxChannel:
+    """One frontend process's request-plane channel (POST /mux): the tokens of all its requests,
+    one NDJSON line per wakeup (one engine step): {"b": [[request_id, batch], ...]}, where batch is
+    the /generate line format."""
+
+    def __init__(self, sid: str):
+        self.sid = sid
+        self.pending: list = []
+        self.wake = asyncio.Event()
+        self.rids: set = set()
+        self.closed = False
+
+    async def lines(self, aeng: AsyncEngine):
+        try:
+            yield (json.dumps({"hello": self.sid}) + "\n").encode()
+            while True:
+                await self.wake.wait()
+                self.wake.clear()
+                outs, self.pending = self.pending, []
+                by_rid: dict = {}
+                for o in outs:
+                    by_rid.setdefault(o.request_id, []).append(o)
+                batch = []
+                for rid, os_ in by_rid.items():
+                    batch.append([rid, _batch_dict(os_)])
+                    if os_[-1].finished:
+                        self.rids.discard(rid)
+                if batch:
+                    yield (json.dumps({"b": batch}) + "\n").encode()
+        finally:  # the frontend went away: its requests have nobody to stream to
+            self.closed = True
+            for rid in list(self.rids):
+                if aeng._queues.pop(rid, None) is not None:
+                    aeng.submit_nowait(aeng.engine.abort, rid)
+            self.rids.clear()
 
 
 class Worker:
@@ -98,6 +177,7 @@ class Worker:
         self.aeng.on_step = self._on_step
         self.ready = True
         self._http = None
+        self._channels: dict[str, MuxChannel] = {}
         self.app = self._build_app()
 
     # ---------------------------------------------------------------- engine-thread hook
@@ -156,13 +236,46 @@ class Worker:
         async for outs in self.aeng.stream_batches(rid, q):
             yield _batch_line(outs)
 
-    async def _remote_prefill(self, rid: str, toks: list, sp: SamplingParams, purl: str):
-        """Decode side of the disaggregated protocol.  Returns the token queue, or None to fall
-        back to local prefill."""
+    async def _submit(self, body: dict) -> dict:
+        """Multiplexed request plane: start a request whose tokens go to channel body["sid"]."""
+        ch = self._channels.get(body.get("sid", ""))
+        if ch is None or ch.closed:
+            return {"error": "unknown channel"}
+        rid = body.get("request_id") or uuid.uuid4().hex
+        toks = list(body["token_ids"])
+        sp = _sampling(body.get("sampling", {}))
+        purl = body.get("prefill_url")
+        sink = _DropSink(ch, self._abort) if self.faults.hit("drop_stream") else _MuxSink(ch)
+        ch.rids.add(rid)
+        if purl and self.role == "decode":
+            if await self._remote_prefill(rid, toks, sp, purl, sink=sink) is not None:
+                return {"ok": True}
+        self.aeng._queues[rid] = (asyncio.get_running_loop(), sink)
+        try:
+            await self.aeng.submit(self.engine.add_request, toks, sp, rid, None)
+        except BaseException:
+            self.aeng._queues.pop(rid, None)
+            ch.rids.discard(rid)
+            raise
+        return {"ok": True}
+
+    def _abort(self, rid: str) -> bool:
+        if self.aeng._queues.pop(rid, None) is None:
+            return False
+        self.aeng.submit_nowait(self.engine.abort, rid)
+        return True
+
+    async def _remote_prefill(self, rid: str, toks: list, sp: SamplingParams, purl: str, sink=None):
+        """Decode side of the disaggregated protocol.  Returns the token queue (or `sink`, the
+        request's mux channel sink, when given), or None to fall back to local prefill."""
         req = await self.aeng.submit(self.engine.reserve_remote_prefill, toks, sp, rid)
         if req is None:
             return None
-        q = self.aeng.open_stream(rid)
+        if sink is not None:
+            self.aeng._queues[rid] = (asyncio.get_running_loop(), sink)
+            q = sink
+        else:
+            q = self.aeng.open_stream(rid)
         skip = req.num_cached_tokens // self.args.block_size
         nblk = -(-len(toks) // self.args.block_size)
         dst = list(req.block_ids[skip:nblk])
@@ -293,6 +406,33 @@ class Worker:
         async def generate(request: HTTPRequest):
             body = await request.json()
             return StreamingResponse(w._generate_stream(body), media_type="application/x-ndjson")
+
+        @app.post("/mux")
+        async def mux(request: HTTPRequest):
+            body = await request.json()
+            sid = str(body.get("sid") or uuid.uuid4().hex)
+            old = w._channels.get(sid)
+            if old is not None:
+                old.closed = True
+            ch = w._channels[sid] = MuxChannel(sid)
+
+            async def lines():
+                try:
+                    async for line in ch.lines(w.aeng):
+                        yield line
+                finally:
+                    if w._channels.get(sid) is ch:
+                        w._channels.pop(sid, None)
+            return StreamingResponse(lines(), media_type="application/x-ndjson")
+
+        @app.post("/submit")
+        async def submit(request: HTTPRequest):
+            res = await w._submit(await request.json())
+            return JSONResponse(res, status_code=404 if "error" in res else 200)
+
+        @app.post("/abort")
+        async def abort(request: HTTPRequest):
+            return {"aborted": w._abort(str((await request.json()).get("request_id", "")))}
 
         @app.post("/prefill")
         async def prefill(request: HTTPRequest):

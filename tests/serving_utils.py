@@ -9,6 +9,21 @@ import httpx
 
 
 def free_port() -> int:
+    """A free port BELOW the kernel's ephemeral range (32768+): the port is closed again before the
+    test binds it, and an ephemeral one can be handed to some other connection in between."""
+    import os
+    import random
+    rng = random.Random(os.getpid() ^ time.monotonic_ns())
+    for _ in range(200):
+        p = rng.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]

@@ -3,7 +3,6 @@ CPU/gloo: every rank's MoE output must equal the unsharded reference MoE over th
 both dispatch layouts (fixed-capacity / exact counts), world sizes 1, 2 and 4, and batches smaller
 than the world (empty token slices)."""
 import os
-import socket
 
 import pytest
 import torch
@@ -13,11 +12,8 @@ E, K, H, I = 8, 2, 32, 48
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from tests.serving_utils import free_port
+    return free_port()
 
 
 def _weights():

@@ -538,6 +538,74 @@ def test_moe_grouped_gemm(gpu, counts, silu):
     assert torch.all(y[o[-1]:] == 7.0), "rows past the routed count were written"
 
 
+@pytest.mark.parametrize("counts", [[0, 5, 70, 1], [16, 17, 0, 33], [1, 1, 1, 1], [130, 0, 0, 2]])
+@pytest.mark.parametrize("silu", [False, True])
+def test_moe_decode_gemm_all_configs(gpu, counts, silu):
+    """Grouped form of the decode GEMM kernel (K16 at decode batches) in every configuration the
+    launcher takes: each expert's rows vs fp32, rows past the routed count untouched, split-K slabs."""
+    from mxserve.ops import decode_gemm as dg
+    E, N, K = len(counts), 512, 1024
+    R = sum(counts) + 9
+    rows_max = max(counts)
+    g = torch.Generator(device="cuda").manual_seed(sum(counts) + silu)
+    x = torch.randn(R, K, device=gpu, dtype=torch.bfloat16, generator=g)
+    w = (torch.randn(E, N, K, device=gpu, dtype=torch.bfloat16, generator=g) * 0.05).to(torch.bfloat16)
+    offs = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=gpu)
+    o = offs.tolist()
+    refs = {}
+    for e in range(E):
+        a, b = o[e], o[e + 1]
+        if b > a:
+            refs[e] = x[a:b].float() @ w[e].float().t()
+    epi = int(silu)
+    ran = 0
+    for cfg in dg.candidates(rows_max, N, K, epi, all_mf=True):
+        mf, nf, wm, sk = cfg
+        if wm > 2:
+            continue
+        y = torch.full((R, N // 2 if silu else N), 7.0, device=gpu, dtype=torch.bfloat16)
+        part = torch.zeros(sk, R, N, device=gpu, dtype=torch.float32) if sk > 1 else None
+        assert ops.ext().moe_decode_gemm(y, x, w, offs, part, rows_max, mf, nf, wm, sk, epi), cfg
+        ran += 1
+        for e, r in refs.items():
+            a, b = o[e], o[e + 1]
+            if sk > 1:
+                got = part[:, a:b].sum(0)
+                _close(got, r, atol=3e-2, rtol=3e-2, name=f"expert {e} cfg {cfg} slabs")
+                continue
+            exp = r
+            if silu:
+                gt, up = r[:, :N // 2], r[:, N // 2:]
+                exp = gt * torch.sigmoid(gt) * up
+            _close(y[a:b], exp, atol=3e-2, rtol=3e-2, name=f"expert {e} cfg {cfg}")
+        if sk == 1:
+            assert torch.all(y[o[-1]:] == 7.0), f"rows past the routed count were written ({cfg})"
+    assert ran >= 6
+
+
+@pytest.mark.parametrize("T,offset", [(1, 0), (7, 0), (64, 0), (200, 0), (40, 2)])
+def test_moe_experts_decode_kernel_path(gpu, monkeypatch, T, offset):
+    """fused_experts at decode batches runs both expert GEMMs on the grouped decode kernel (split-K
+    slabs summed by silu_mul_partials / moe_combine_partials) and matches the fp32 reference MoE."""
+    from mxserve.ops import moe as moe_mod
+    monkeypatch.setattr(moe_mod, "DECODE", True)
+    real = moe_mod._fused_experts_decode
+    used = []
+    monkeypatch.setattr(moe_mod, "_fused_experts_decode", lambda *a: used.append(1) or real(*a))
+    H, I, E, K = 512, 1024, 4, 2
+    e_local = E if offset == 0 else 2
+    g = torch.Generator(device="cuda").manual_seed(T)
+    x = torch.randn(T, H, device=gpu, dtype=torch.bfloat16, generator=g)
+    w13 = (torch.randn(E, 2 * I, H, device=gpu, generator=g) * 0.05).to(torch.bfloat16)
+    w2 = (torch.randn(E, H, I, device=gpu, generator=g) * 0.05).to(torch.bfloat16)
+    tw, tid = ops.moe_topk_softmax(torch.randn(T, E, device=gpu, dtype=torch.bfloat16, generator=g), K)
+    w13l, w2l = w13[offset:offset + e_local].contiguous(), w2[offset:offset + e_local].contiguous()
+    out = moe_mod.fused_experts(x, w13l, w2l, tw, tid, offset)
+    assert used and out is not None
+    exp = ref.moe_experts(x.cpu(), w13l.cpu(), w2l.cpu(), tw.cpu(), tid.cpu(), offset)
+    _close(out, exp, 0.02, 0.03, "moe decode kernel")
+
+
 def test_moe_experts_uses_grouped_kernel(gpu, monkeypatch):
     from mxserve.ops import moe as moe_mod
     called = []

@@ -1,7 +1,6 @@
 """Tensor parallelism on CPU (gloo, world size 2): a TP=2 engine (driver + follower process) must
 produce the same greedy tokens as TP=1 with the same unsharded weights."""
 import os
-import socket
 
 import pytest
 import torch
@@ -9,11 +8,8 @@ import torch.multiprocessing as mp
 
 
 def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from tests.serving_utils import free_port
+    return free_port()
 
 
 PROMPTS = [[5, 9, 13, 200, 31, 7, 77, 8, 100, 3] * 3, [44, 45, 46], list(range(60, 140))]
