@@ -31,7 +31,7 @@ void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStre
 void launch_moe_align(int*, int*, const int*, int, int, int, int*, hipStream_t);
 void launch_moe_combine(bf16_t*, const bf16_t*, const float*, const int*, int, int, int, hipStream_t);
 bool launch_decode_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int,
-                        int, hipStream_t, const int* = nullptr, int = 0, int = 0);
+                        int, hipStream_t, const int* = nullptr, int = 0, int = 0, int = 0);
 bool launch_moe_grouped_gemm(bf16_t*, const bf16_t*, const bf16_t*, const int*, int, int, int, int, int, bool,
                              int, float*, hipStream_t);
 void launch_moe_combine_partials(bf16_t*, const float*, const float*, const int*, int, int, int, int, long,
@@ -218,7 +218,7 @@ void apply_penalties(at::Tensor logits, at::Tensor hist, at::Tensor srows, at::T
 // fp32 split-K workspace (>= splitk * M * N floats) when splitk > 1.  False if the configuration
 // does not tile the shape (the caller keeps hipBLASLt).
 bool decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> part, int64_t mf, int64_t nf,
-                 int64_t wm, int64_t splitk, int64_t epi) {
+                 int64_t wm, int64_t splitk, int64_t epi, int64_t lu) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
   const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
@@ -232,14 +232,15 @@ bool decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::T
     p = part->data_ptr<float>();
   }
   return mxs::launch_decode_gemm(bf(out), p, bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), mf, nf, wm, splitk,
-                                 epi, stream());
+                                 epi, stream(), nullptr, 0, 0, lu);
 }
 
 // Grouped decode form of decode_gemm (K16 at decode batches): w [E, N, K], x = routed rows sorted by
 // expert (offs = moe_align offsets), rows_max = the most rows one expert can hold (tokens).  Output
 // as moe_grouped_gemm: out [rows, N or N/2] (splitk 1) or fp32 partials [splitk, rows, N].
 bool moe_decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor offs, c10::optional<at::Tensor> part,
-                     int64_t rows_max, int64_t mf, int64_t nf, int64_t wm, int64_t splitk, int64_t epi) {
+                     int64_t rows_max, int64_t mf, int64_t nf, int64_t wm, int64_t splitk, int64_t epi,
+                     int64_t lu) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_CONTIG(w); CHECK_CONTIG(x);
   TORCH_CHECK(w.dim() == 3 && x.dim() == 2, "w [E, N, K], x [rows, K]");
   TORCH_CHECK(offs.scalar_type() == at::kInt && offs.is_contiguous() && offs.numel() == w.size(0) + 1,
@@ -259,7 +260,7 @@ bool moe_decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, at::Tensor offs
     TORCH_CHECK(out.dim() == 2 && out.size(0) == R && out.size(1) == ldy, "out [rows, N or N/2]");
   }
   return mxs::launch_decode_gemm(splitk > 1 ? nullptr : bf(out), p, bf(x), bf(w), R, N, K, K, ldy, mf, nf, wm, splitk,
-                                 epi, stream(), offs.data_ptr<int>(), E, rows_max);
+                                 epi, stream(), offs.data_ptr<int>(), E, rows_max, lu);
 }
 
 // y[r] = x[r] . w[e(r)]^T over expert-sorted rows (offs = moe_align offsets); silu: w rows are
@@ -342,10 +343,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_combine", &moe_combine);
   m.def("decode_gemm", &decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("part"), pybind11::arg("mf"), pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"),
-        pybind11::arg("epi"));
+        pybind11::arg("epi"), pybind11::arg("lu") = 0);
   m.def("moe_decode_gemm", &moe_decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("offs"), pybind11::arg("part"), pybind11::arg("rows_max"), pybind11::arg("mf"),
-        pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"), pybind11::arg("epi"));
+        pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"), pybind11::arg("epi"),
+        pybind11::arg("lu") = 0);
   m.def("moe_grouped_gemm", &moe_grouped_gemm, pybind11::arg("y"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("offs"), pybind11::arg("silu"), pybind11::arg("split") = 1,
         pybind11::arg("partial") = pybind11::none());

@@ -159,6 +159,141 @@ __global__ void __launch_bounds__(256) decode_gemm_kernel(bf16_t* __restrict__ Y
   }
 }
 
+// LDS form: the same wave tiles (4 waves side by side over N, all on the workgroup's MF x 16 rows),
+// but the X tile of each U-step group is loaded ONCE per workgroup (each thread a few 16-byte
+// chunks, coalesced row segments) and written to LDS in MFMA-fragment order, where every wave reads
+// its B fragments with conflict-free ds_read_b128 (lane l reads 16 bytes at 16 l).  The register
+// kernel above has every wave load the X fragments itself: 4x the X traffic from L2, which at
+// 32-64 rows per tile (MoE experts at decode, M >= 64 dense) is as many bytes as the weights.
+// One barrier per group: the group's X chunks and W fragments for the NEXT group are issued before
+// this group's MFMAs (X first, so the wait before the LDS write leaves the W loads in flight).
+template <int MF, int NF, int U, int EPI, bool G>
+__global__ void __launch_bounds__(256) decode_gemm_lds_kernel(bf16_t* __restrict__ Y, float* __restrict__ part,
+                                                              const bf16_t* __restrict__ X,
+                                                              const bf16_t* __restrict__ W, int M, int N, int K,
+                                                              int ldx, int ldy, int kslice, int inter,
+                                                              const int* __restrict__ offs, int rt) {
+  constexpr int KG = 32 * U;                 // k per group
+  constexpr int BM = MF * 16;                // rows of the workgroup
+  constexpr int XCH = BM * KG / 8;           // 16-byte chunks of one X tile
+  constexpr int XPT = (XCH + 255) / 256;     // chunks per thread
+  constexpr int NH = EPI == EPI_SILU ? NF / 2 : NF;
+  __shared__ __attribute__((aligned(16))) u32x4 xs[2][XCH];
+  const int tid = threadIdx.x, lane = tid & 63, wn = tid >> 6;
+  const int i = lane & 15, kq = lane >> 4;
+  int m0 = blockIdx.y * BM;
+  int mlim = M;
+  if constexpr (G) {
+    const int e = blockIdx.y / rt, r = blockIdx.y - e * rt;
+    const int lo = offs[e], hi = offs[e + 1];
+    m0 = lo + r * BM;
+    if (m0 >= hi) return;  // uniform over the workgroup
+    mlim = hi;
+    W += static_cast<size_t>(e) * N * K;
+  }
+  const int c0 = (blockIdx.x * 4 + wn) * NH * 16;
+  const int kbeg = blockIdx.z * kslice;
+  const bf16_t* wp[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int col = (EPI == EPI_SILU && j >= NH) ? inter + c0 + 16 * (j - NH) : c0 + 16 * (j % NH);
+    wp[j] = W + static_cast<size_t>(col + i) * K + kbeg + 8 * kq;
+  }
+  // X chunk q of the tile <-> LDS slot q = ((t * U + u) * 64 + kq' * 16 + i'): row m0 + 16 t + i',
+  // k offset 32 u + 8 kq' (rows past the limit re-read row mlim - 1: loaded, never stored)
+  const bf16_t* xsrc[XPT];
+#pragma unroll
+  for (int s2 = 0; s2 < XPT; ++s2) {
+    const int q = tid + 256 * s2;
+    const int ii = q & 15, kk = (q >> 4) & 3, tu = q >> 6;
+    const int t = tu / U, u = tu - t * U;
+    const int row = min(m0 + 16 * t + ii, mlim - 1);
+    xsrc[s2] = X + static_cast<size_t>(row) * ldx + kbeg + 32 * u + 8 * kk;
+  }
+  auto load_x = [&](int k, u32x4 (&xr)[XPT]) {
+#pragma unroll
+    for (int s2 = 0; s2 < XPT; ++s2)
+      if (XCH % 256 == 0 || tid + 256 * s2 < XCH) xr[s2] = *reinterpret_cast<const u32x4*>(xsrc[s2] + k);
+  };
+  auto store_x = [&](int buf, const u32x4 (&xr)[XPT]) {
+#pragma unroll
+    for (int s2 = 0; s2 < XPT; ++s2)
+      if (XCH % 256 == 0 || tid + 256 * s2 < XCH) xs[buf][tid + 256 * s2] = xr[s2];
+  };
+  auto load_w = [&](int k, u32x4 (&ad)[U][NF]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) ad[u][j] = *reinterpret_cast<const u32x4*>(wp[j] + k + 32 * u);
+  };
+  float4_ acc[MF][NF];
+#pragma unroll
+  for (int t = 0; t < MF; ++t)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[t][j] = float4_{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 a[U][NF], xr[XPT];
+  load_x(0, xr);
+  load_w(0, a);
+  store_x(0, xr);
+  __syncthreads();
+  int cur = 0;
+  for (int k = 0; k < kslice; k += KG) {
+    const bool more = k + KG < kslice;
+    u32x4 an[U][NF];
+    if (more) {
+      load_x(k + KG, xr);
+      load_w(k + KG, an);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int t = 0; t < MF; ++t) {
+        const u32x4 b = xs[cur][(t * U + u) * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[u][j]), as_bf16x8(b), acc[t][j], 0, 0, 0);
+      }
+    if (more) {
+      store_x(cur ^ 1, xr);
+      __syncthreads();
+      cur ^= 1;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) a[u][j] = an[u][j];
+    }
+  }
+
+#pragma unroll
+  for (int t = 0; t < MF; ++t) {
+    const int m = m0 + 16 * t + i;
+    if (m >= mlim) continue;
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      const int n = c0 + 16 * j + 4 * kq;
+      if (part != nullptr) {
+        const size_t row = (static_cast<size_t>(blockIdx.z) * M + m) * static_cast<size_t>(N);
+        *reinterpret_cast<float4_*>(part + row + n) = acc[t][j];
+        if constexpr (EPI == EPI_SILU) *reinterpret_cast<float4_*>(part + row + inter + n) = acc[t][j + NH];
+        continue;
+      }
+      float v[4];
+      if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = silu(acc[t][j][r]) * acc[t][j + NH][r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[t][j][r];
+      }
+      uint2 o;
+      o.x = pack2(v[0], v[1]);
+      o.y = pack2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(Y + static_cast<size_t>(m) * ldy + n) = o;
+    }
+  }
+}
+
 // Sum S fp32 slabs [S][M][N] and apply the epilogue: Y[m][n] (EPI_NONE, N columns) or
 // Y[m][n] = SiLU(sum gate[n]) * sum up[inter + n] (EPI_SILU, inter columns).
 template <int EPI>
@@ -191,11 +326,13 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
 // most rows one expert can get (T tokens: an expert appears at most once in a token's top-k).
 bool launch_decode_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx,
                         int ldy, int MF, int NF, int WM, int splitk, int epi, hipStream_t s, const int* offs,
-                        int E, int rows_max) {
+                        int E, int rows_max, int LU) {
+  if (LU > 0) WM = 1;  // LDS form: 4 waves side by side over N
   const int WN = 4 / WM;
   if (M <= 0 || splitk < 1 || ldx % 8 != 0 || ldy % 4 != 0) return false;
   if (offs == nullptr ? M > 256 : (E < 1 || rows_max < 1 || rows_max > 256 || WM > 2)) return false;
-  if (K % (32 * decode_gemm_unroll(MF, NF) * splitk) != 0) return false;
+  if (LU != 0 && LU != 2 && LU != 4) return false;
+  if (K % (32 * (LU > 0 ? LU : decode_gemm_unroll(MF, NF)) * splitk) != 0) return false;
   const int outN = epi == EPI_SILU ? N / 2 : N;
   const int NH = epi == EPI_SILU ? NF / 2 : NF;
   const int BM = WM * MF * 16, BN = WN * NH * 16;
@@ -213,10 +350,27 @@ bool launch_decode_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W
     launched = true;                                                                                              \
   }
   bool launched = false;
+#define MXS_DGL(mf, nf, lu, e, gr)                                                                                 \
+  if (LU == lu && MF == mf && NF == nf && epi == e && g == gr) {                                                  \
+    hipLaunchKernelGGL((decode_gemm_lds_kernel<mf, nf, lu, e, gr>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy, \
+                       kslice, N / 2, offs, rt);                                                                  \
+    launched = true;                                                                                              \
+  }
+#define MXS_DGL_ALL(mf, nf, e) \
+  MXS_DGL(mf, nf, 2, e, false) MXS_DGL(mf, nf, 4, e, false) MXS_DGL(mf, nf, 2, e, true) MXS_DGL(mf, nf, 4, e, true)
+  if (LU > 0) {
+    MXS_DGL_ALL(1, 2, 0) MXS_DGL_ALL(1, 4, 0) MXS_DGL_ALL(2, 2, 0) MXS_DGL_ALL(2, 4, 0) MXS_DGL_ALL(4, 2, 0)
+    MXS_DGL_ALL(4, 4, 0) MXS_DGL_ALL(1, 2, 1) MXS_DGL_ALL(1, 4, 1) MXS_DGL_ALL(2, 2, 1) MXS_DGL_ALL(2, 4, 1)
+    MXS_DGL_ALL(4, 2, 1) MXS_DGL_ALL(4, 4, 1)
+  }
+#undef MXS_DGL_ALL
+#undef MXS_DGL
 #define MXS_DG_WM(mf, nf, e) \
   MXS_DG(mf, nf, 1, e, false) MXS_DG(mf, nf, 2, e, false) MXS_DG(mf, nf, 4, e, false) MXS_DG(mf, nf, 1, e, true) MXS_DG(mf, nf, 2, e, true)
-  MXS_DG_WM(1, 2, 0) MXS_DG_WM(1, 4, 0) MXS_DG_WM(2, 2, 0) MXS_DG_WM(2, 4, 0) MXS_DG_WM(4, 2, 0) MXS_DG_WM(4, 4, 0)
-  MXS_DG_WM(1, 2, 1) MXS_DG_WM(1, 4, 1) MXS_DG_WM(2, 2, 1) MXS_DG_WM(2, 4, 1) MXS_DG_WM(4, 2, 1) MXS_DG_WM(4, 4, 1)
+  if (LU == 0) {
+    MXS_DG_WM(1, 2, 0) MXS_DG_WM(1, 4, 0) MXS_DG_WM(2, 2, 0) MXS_DG_WM(2, 4, 0) MXS_DG_WM(4, 2, 0) MXS_DG_WM(4, 4, 0)
+    MXS_DG_WM(1, 2, 1) MXS_DG_WM(1, 4, 1) MXS_DG_WM(2, 2, 1) MXS_DG_WM(2, 4, 1) MXS_DG_WM(4, 2, 1) MXS_DG_WM(4, 4, 1)
+  }
 #undef MXS_DG_WM
 #undef MXS_DG
   if (!launched) return false;

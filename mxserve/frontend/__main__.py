@@ -23,6 +23,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--local-model", default=os.environ.get("MXS_LOCAL_MODEL"),
                     help="also serve this model from an in-process engine")
     ap.add_argument("--local-device", default=os.environ.get("MXS_LOCAL_DEVICE", "auto"))
+    ap.add_argument("--num-procs", type=int, default=int(os.environ.get("MXS_FRONTEND_PROCS", "1")),
+                    help="frontend processes sharing the port (SO_REUSEPORT); >1 spreads the per-token "
+                         "streaming work over cores (frontend/multiproc.py)")
     return ap
 
 
@@ -32,6 +35,13 @@ def main(argv=None) -> None:
     a = build_parser().parse_args(argv)
     from ..utils.logs import setup_logging
     setup_logging()
+    if a.num_procs > 1:
+        if a.local_model:
+            raise SystemExit("--local-model runs the engine in the frontend process: use --num-procs 1")
+        from .multiproc import serve
+        raise SystemExit(serve({"host": a.http_host, "port": a.http_port, "router_mode": a.router_mode,
+                                "ttl": a.lease_ttl, "namespace": a.namespace,
+                                "reasoning_parser": a.reasoning_parser}, a.num_procs))
     fe = Frontend(router_mode=a.router_mode, ttl=a.lease_ttl, namespace=a.namespace,
                   reasoning_parser=a.reasoning_parser)
     if a.local_model:

@@ -65,6 +65,17 @@ def _parse_token_line(d: dict, out: list) -> None:
                               d.get("tm") if i == 0 else None))
 
 
+def _observe_zeros(hist_child, k: int) -> None:
+    """k observations of 0.0 in one histogram child: one bucket increment instead of k observe()
+    calls (prometheus_client keeps a child's bucket counters in `_buckets`, lowest bound first)."""
+    b = getattr(hist_child, "_buckets", None)
+    if b:
+        b[0].inc(k)
+    else:  # pragma: no cover - other client versions
+        for _ in range(k):
+            hist_child.observe(0.0)
+
+
 async def _merge(gens: list):
     """Interleave async generators as items arrive: yields (generator index, item).  The first
     exception ends the merge and is raised; the other generators are closed."""
@@ -238,10 +249,34 @@ class Frontend:
         self._cfg = {}
         self.local: dict[str, LocalWorker] = {}
         self._mux: dict[str, MuxClient] = {}
+        self.bus = None  # multi-process frontend: discovery messages to/from the sibling processes
         self._bg: set = set()  # fire-and-forget tasks (aborts), referenced until done
         self._http = None
         self.started = time.time()
         self.app = self._build_app()
+
+    # ---------------------------------------------------------------- discovery
+    def apply_register(self, d: dict) -> WorkerInfo:
+        info = WorkerInfo(worker_id=d["worker_id"], url=d["url"], model=d["model"], role=d.get("role", "agg"),
+                          block_size=int(d.get("block_size", 16)),
+                          kv_total_blocks=int(d.get("kv_total_blocks", 1) or 1), tp=int(d.get("tp", 1)),
+                          max_model_len=int(d.get("max_model_len", 0) or 0), pair=str(d.get("pair") or ""))
+        self.registry.register(info)
+        log.info("registered worker %s (%s) for %s at %s", info.worker_id, info.role, info.model, info.url)
+        return info
+
+    def apply_heartbeat(self, d: dict) -> bool:
+        return self.registry.heartbeat(d["worker_id"], d.get("load", {}), d.get("stored", ()), d.get("removed", ()))
+
+    def apply_peer(self, kind: str, d: dict) -> None:
+        """A discovery message another process of this frontend received (frontend/multiproc.py)."""
+        try:
+            if kind == "register":
+                self.apply_register(d)
+            elif kind == "heartbeat":
+                self.apply_heartbeat(d)
+        except Exception:  # noqa: BLE001
+            log.exception("bad peer discovery message")
 
     # ---------------------------------------------------------------- model info
     def tokenizer(self, model: str):
@@ -513,19 +548,24 @@ class Frontend:
         m.isl.labels(model).observe(len(prompt_ids))
         t0 = time.perf_counter()
         state = {"first": None, "last": {}, "n": 0, "queued": True}
+        m_itl = m.itl.labels(model)
 
-        def on_token(idx: int):
+        def on_tokens(idx: int, n: int):
+            """n tokens of choice idx arrived together (one worker batch)."""
             now = time.perf_counter()
+            last = state["last"]
             if state["first"] is None:
                 state["first"] = now
                 trace.mark("first_token")
                 m.ttft.labels(model).observe(now - t0)
                 m.queued.labels(model).dec()
                 state["queued"] = False
-            elif idx in state["last"]:
-                m.itl.labels(model).observe(now - state["last"][idx])
-            state["last"][idx] = now
-            state["n"] += 1
+            elif idx in last:
+                m_itl.observe(now - last[idx])
+            if n > 1:  # the rest of a batch arrived with its first token: n-1 zero intervals
+                _observe_zeros(m_itl, n - 1)
+            last[idx] = now
+            state["n"] += n
 
         def finish(status: str):
             m.requests.labels(model, endpoint, rtype, status).inc()
@@ -556,16 +596,17 @@ class Frontend:
             hold = max((len(x) for x in stops if x), default=1) - 1
             lps: list = []
             sub_rid, sub_sp = sub_request(idx)
+            eos_ids = tok.eos_token_ids
             async for evs in self.generate_tokens(model, prompt_ids, sub_sp, sub_rid):
                 if evs[0].timing and "worker_ms" not in trace.attrs:
                     trace.attrs["worker_ms"] = evs[0].timing  # queue / prefill / kv transfer on the worker
-                for ev in evs:  # a batch becomes one delta
-                    on_token(idx)
-                    eos_hit = ev.finished and ev.finish_reason == "stop" and ev.token_id in tok.eos_token_ids
-                    full += "" if eos_hit else detok.add(ev.token_id)
-                    if want_lp and not eos_hit and ev.logprob is not None:
-                        lps.append(ev)
-                ev = evs[-1]
+                on_tokens(idx, len(evs))
+                ev = evs[-1]  # a batch becomes one delta; only its last event can finish the request
+                eos_hit = ev.finished and ev.finish_reason == "stop" and ev.token_id in eos_ids
+                body = evs[:-1] if eos_hit else evs
+                full += detok.add_many([e.token_id for e in body])
+                if want_lp:
+                    lps.extend(e for e in body if e.logprob is not None)
                 if ev.finished:
                     full += detok.flush()
                 reason = ("stop" if ev.finish_reason == "abort" else ev.finish_reason) if ev.finished else None
@@ -651,8 +692,21 @@ class Frontend:
         splitters = ([ReasoningSplitter(self.reasoning_parser) for _ in range(n_choices)]
                      if chat and self.reasoning_parser else None)
 
+        fast: dict = {}  # idx -> (prefix, suffix) of a plain content chunk: only the delta is encoded
+
         def chunk(delta: Optional[str], reason: Optional[str], first: bool = False, evs: tuple = (),
                   idx: int = 0, reasoning: Optional[str] = None) -> bytes:
+            if delta and reason is None and not first and not reasoning and not want_lp:
+                ps = fast.get(idx)
+                if ps is None:
+                    ch0 = ({"index": idx, "delta": {"content": "\x00"}, "finish_reason": None} if chat else
+                           {"index": idx, "text": "\x00", "logprobs": None, "finish_reason": None})
+                    t = "data: " + json.dumps({"id": rid, "object": chunk_obj, "created": created, "model": model,
+                                               "choices": [ch0]}) + "\n\n"
+                    ps = fast[idx] = tuple(t.split('"\\u0000"'))
+                if not chat:
+                    sent[idx] += len(delta)
+                return (ps[0] + json.dumps(delta) + ps[1]).encode()
             if chat:
                 d = {}
                 if first:
@@ -780,18 +834,17 @@ class Frontend:
         @app.post("/internal/register")
         async def register(request: HTTPRequest):
             d = await request.json()
-            info = WorkerInfo(worker_id=d["worker_id"], url=d["url"], model=d["model"], role=d.get("role", "agg"),
-                              block_size=int(d.get("block_size", 16)),
-                              kv_total_blocks=int(d.get("kv_total_blocks", 1) or 1), tp=int(d.get("tp", 1)),
-                              max_model_len=int(d.get("max_model_len", 0) or 0), pair=str(d.get("pair") or ""))
-            fe.registry.register(info)
-            log.info("registered worker %s (%s) for %s at %s", info.worker_id, info.role, info.model, info.url)
+            info = fe.apply_register(d)
+            if fe.bus is not None:  # the sibling processes of a multi-process frontend
+                fe.bus.publish("register", d)
             return {"ok": True, "index": info.index}
 
         @app.post("/internal/heartbeat")
         async def heartbeat(request: HTTPRequest):
             d = await request.json()
-            ok = fe.registry.heartbeat(d["worker_id"], d.get("load", {}), d.get("stored", ()), d.get("removed", ()))
+            ok = fe.apply_heartbeat(d)
+            if fe.bus is not None:
+                fe.bus.publish("heartbeat", d)
             return JSONResponse({"ok": ok}, status_code=200 if ok else 404)
 
         @app.get("/internal/workers")
@@ -808,6 +861,8 @@ class Frontend:
                 for wid in self.registry.expire():
                     log.warning("worker %s lease expired", wid)
         task = asyncio.get_running_loop().create_task(reaper())
+        if self.bus is not None:
+            self.bus.start(asyncio.get_running_loop(), self.apply_peer)
         yield
         task.cancel()
         for mc in self._mux.values():

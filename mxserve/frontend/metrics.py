@@ -6,6 +6,8 @@
 plus inflight / queued gauges and worker-side dynamo_component_* KV stats."""
 from __future__ import annotations
 
+import os
+
 from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest
 
 _LAT = (0.001, 0.0025, 0.005, 0.0075, 0.01, 0.015, 0.02, 0.025, 0.035, 0.05, 0.075, 0.1, 0.15, 0.25, 0.35, 0.5,
@@ -14,15 +16,24 @@ _DUR = (0.05, 0.1, 0.25, 0.5, 1.0, 2.0, 4.0, 8.0, 15.0, 30.0, 60.0, 120.0, 300.0
 _TOK = (1, 8, 32, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 131072)
 
 
+def _multiproc() -> bool:
+    """prometheus_client multiprocess mode (a multi-process frontend, frontend/multiproc.py)."""
+    return bool(os.environ.get("PROMETHEUS_MULTIPROC_DIR"))
+
+
 class FrontendMetrics:
     def __init__(self, registry: CollectorRegistry | None = None):
         self.registry = registry or CollectorRegistry()
         r = self.registry
+        mp = _multiproc()
+        sum_kw = {"multiprocess_mode": "livesum"} if mp else {}
+        max_kw = {"multiprocess_mode": "livemax"} if mp else {}
         self.requests = Counter("dynamo_frontend_requests", "Frontend requests",
                                 ["model", "endpoint", "request_type", "status"], registry=r)
-        self.inflight = Gauge("dynamo_frontend_inflight_requests", "In-flight requests", ["model"], registry=r)
+        self.inflight = Gauge("dynamo_frontend_inflight_requests", "In-flight requests", ["model"], registry=r,
+                              **sum_kw)
         self.queued = Gauge("dynamo_frontend_queued_requests", "Requests waiting for first token", ["model"],
-                            registry=r)
+                            registry=r, **sum_kw)
         self.ttft = Histogram("dynamo_frontend_time_to_first_token_seconds", "TTFT", ["model"], buckets=_LAT,
                               registry=r)
         self.itl = Histogram("dynamo_frontend_inter_token_latency_seconds", "ITL", ["model"], buckets=_LAT,
@@ -31,13 +42,19 @@ class FrontendMetrics:
                                   buckets=_DUR, registry=r)
         self.isl = Histogram("dynamo_frontend_input_sequence_tokens", "ISL", ["model"], buckets=_TOK, registry=r)
         self.osl = Histogram("dynamo_frontend_output_sequence_tokens", "OSL", ["model"], buckets=_TOK, registry=r)
-        self.workers = Gauge("dynamo_frontend_workers", "Registered workers", ["model", "role"], registry=r)
+        # every process sees every worker: the max over processes, not the sum
+        self.workers = Gauge("dynamo_frontend_workers", "Registered workers", ["model", "role"], registry=r, **max_kw)
         self.kv_hit = Counter("dynamo_frontend_kv_router_overlap_blocks", "Prefix blocks matched by the KV router",
                               ["model"], registry=r)
         self.migrations = Counter("dynamo_frontend_request_migrations", "Streams moved to another worker mid-request",
                                   ["model"], registry=r)
 
     def render(self) -> bytes:
+        if _multiproc():
+            from prometheus_client import multiprocess
+            reg = CollectorRegistry()
+            multiprocess.MultiProcessCollector(reg)
+            return generate_latest(reg)
         return generate_latest(self.registry)
 
 

@@ -39,6 +39,7 @@ class ByteTokenizer:
         self.eos_token_ids = list(cfg.eos_token_ids)
         self.bos_token_id = cfg.bos_token_id
         self._sorted_specials = sorted(self.special_to_id, key=len, reverse=True)
+        self._pieces: dict = {}
 
     def encode(self, text: str, add_special_tokens: bool = False) -> list[int]:
         ids: list[int] = []
@@ -63,6 +64,14 @@ class ByteTokenizer:
         return ids
 
     def _piece(self, t: int, skip_special: bool) -> bytes:
+        p = self._pieces.get((t, skip_special))
+        if p is None:
+            p = self._pieces[(t, skip_special)] = self._make_piece(t, skip_special)
+            if len(self._pieces) > 1 << 18:
+                self._pieces.clear()
+        return p
+
+    def _make_piece(self, t: int, skip_special: bool) -> bytes:
         if self.byte0 <= t < self.byte0 + 256:
             return bytes([t - self.byte0])
         if t in self.id_to_special:
@@ -75,7 +84,8 @@ class ByteTokenizer:
         return (" " + w).encode()
 
     def decode(self, ids: list[int], skip_special_tokens: bool = True) -> str:
-        return b"".join(self._piece(int(t), skip_special_tokens) for t in ids).decode("utf-8", errors="replace")
+        piece = self._piece
+        return b"".join([piece(t, skip_special_tokens) for t in ids]).decode("utf-8", errors="replace")
 
     def convert_special(self, name: str) -> Optional[int]:
         return self.special_to_id.get(name)
@@ -130,6 +140,17 @@ class IncrementalDetokenizer:
 
     def add(self, token_id: int) -> str:
         self.ids.append(int(token_id))
+        return self._advance()
+
+    def add_many(self, token_ids: list) -> str:
+        """A batch of tokens that arrived together: one window decode instead of one per token
+        (the same text as adding them one by one)."""
+        if not token_ids:
+            return ""
+        self.ids.extend(int(t) for t in token_ids)
+        return self._advance()
+
+    def _advance(self) -> str:
         prefix_text = self._decode(self.prefix, self.read)
         new_text = self._decode(self.prefix)
         if len(new_text) <= len(prefix_text) or new_text.endswith("\ufffd"):

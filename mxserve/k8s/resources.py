@@ -187,8 +187,9 @@ def _container(g: GraphSpec, s: ServiceSpec) -> dict:
            {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}]
     if PROMETHEUS_ENDPOINT:
         env.append({"name": "PROMETHEUS_ENDPOINT", "value": PROMETHEUS_ENDPOINT})
-    if is_fe:
-        env.append({"name": "DYN_HTTP_PORT", "value": str(FRONTEND_PORT)})
+    if is_fe:  # 4 frontend processes on the port: one Python process streams ~20 k tokens/s at most
+        env += [{"name": "DYN_HTTP_PORT", "value": str(FRONTEND_PORT)},
+                {"name": "MXS_FRONTEND_PROCS", "value": os.environ.get("MXS_FRONTEND_PROCS", "4")}]
     else:
         env += [{"name": "MXS_FRONTEND_URL", "value": frontend_url(g)},
                 {"name": "DYN_SYSTEM_PORT", "value": str(WORKER_PORT)}]

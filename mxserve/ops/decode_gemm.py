@@ -40,12 +40,29 @@ def unroll(mf: int, nf: int) -> int:
     return 8 if mf + nf <= 3 else (4 if mf + nf <= 6 else 2)
 
 
-def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False) -> list[tuple]:
-    """(mf, nf, wm, splitk) configurations that tile the shape (wave row tile MF x 16 sized to M
-    unless all_mf: then every MF, i.e. more row tiles re-reading the weights from L2)."""
+def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool = True) -> list[tuple]:
+    """(mf, nf, wm, splitk, lu) configurations that tile the shape (wave row tile MF x 16 sized to M
+    unless all_mf: then every MF, i.e. more row tiles re-reading the weights from L2).  lu = 0: the
+    register kernel (wm waves over M); lu = 2 / 4: the LDS form (X tile shared by the workgroup's 4
+    waves through LDS, lu k-steps per group)."""
     out = []
     for mf in ((1, 2, 4) if all_mf else (_mf(M),)):
         out += _candidates_mf(M, N, K, epi, mf)
+        if lds and mf > 1:  # one 16-row tile: the X fragment is as small as one W fragment
+            out += _candidates_lds(N, K, epi, mf)
+    return out
+
+
+def _candidates_lds(N: int, K: int, epi: int, mf: int) -> list[tuple]:
+    out = []
+    for nf in (2, 4):
+        nh = nf // 2 if epi else nf
+        if (N // 2 if epi else N) % (4 * nh * 16):
+            continue
+        for lu in (2, 4):
+            for sk in (1, 2, 4, 8):
+                if K % (32 * lu * sk) == 0:
+                    out.append((mf, nf, 1, sk, lu))
     return out
 
 
@@ -63,7 +80,7 @@ def _candidates_mf(M: int, N: int, K: int, epi: int, mf: int) -> list[tuple]:
             for sk in (1, 2, 4, 8):
                 if K % (32 * unroll(mf, nf) * sk):
                     continue
-                out.append((mf, nf, wm, sk))
+                out.append((mf, nf, wm, sk, 0))
     return out
 
 
@@ -89,7 +106,8 @@ class DecodeGemmTable:
 
     def run(self, out: torch.Tensor, x: torch.Tensor, w: torch.Tensor, cfg: tuple, epi: int) -> bool:
         from . import ext
-        mf, nf, wm, sk = cfg
+        mf, nf, wm, sk = cfg[:4]
+        lu = cfg[4] if len(cfg) > 4 else 0
         part = None
         if sk > 1:
             need = sk * x.shape[0] * w.shape[0]
@@ -98,7 +116,7 @@ class DecodeGemmTable:
                     return False  # never allocate inside a capture (tune() sizes it beforehand)
                 self.part = torch.empty(need, dtype=torch.float32, device=x.device)
             part = self.part
-        return bool(ext().decode_gemm(out, x, w, part, mf, nf, wm, sk, epi))
+        return bool(ext().decode_gemm(out, x, w, part, mf, nf, wm, sk, epi, lu))
 
 
 TABLE = DecodeGemmTable()

@@ -114,10 +114,17 @@ def decode_cfg(T: int, N: int, K: int, epi: int, e_local: int, top_k: int = 2) -
     best = None
     for sk in (1, 2, 4, 8):
         if K % (32 * unroll(mf, nf) * sk) == 0:
-            best = (mf, nf, 1, sk)
+            best = (mf, nf, 1, sk, 0)
             if tiles * sk >= 1024:
                 break
     return best
+
+
+def _mdg(out, x, w, offs, part, rows_max: int, cfg: tuple, epi: int) -> bool:
+    from . import ext
+    mf, nf, wm, sk = cfg[:4]
+    return bool(ext().moe_decode_gemm(out, x, w, offs, part, rows_max, mf, nf, wm, sk, epi,
+                                      cfg[4] if len(cfg) > 4 else 0))
 
 
 def _fused_experts_decode(x, w13, w2, topk_w, offs, inv, xs, expert_offset) -> torch.Tensor | None:
@@ -140,21 +147,21 @@ def _fused_experts_decode(x, w13, w2, topk_w, offs, inv, xs, expert_offset) -> t
     h = torch.empty(R, two_i // 2, dtype=x.dtype, device=dev)
     if c13[3] > 1:
         p13 = torch.empty(c13[3], R, two_i, dtype=torch.float32, device=dev)
-        if not ext().moe_decode_gemm(h, xs, w13, offs, p13, T, *c13, 1):
+        if not _mdg(h, xs, w13, offs, p13, T, c13, 1):
             return None
         ext().silu_mul_partials(h, p13)
-    elif not ext().moe_decode_gemm(h, xs, w13, offs, None, T, *c13, 1):
+    elif not _mdg(h, xs, w13, offs, None, T, c13, 1):
         return None
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
     tw = topk_w.float().contiguous()
     if c2[3] > 1:
         p2 = torch.empty(c2[3], R, H, dtype=torch.float32, device=dev)
-        if not ext().moe_decode_gemm(h, h, w2, offs, p2, T, *c2, 0):
+        if not _mdg(h, h, w2, offs, p2, T, c2, 0):
             return None
         ext().moe_combine_partials(out, p2, tw, inv)
     else:
         ys = torch.empty(R, H, dtype=x.dtype, device=dev)
-        if not ext().moe_decode_gemm(ys, h, w2, offs, None, T, *c2, 0):
+        if not _mdg(ys, h, w2, offs, None, T, c2, 0):
             return None
         ext().moe_combine(out, ys, tw, inv)
     return out
@@ -249,13 +256,13 @@ def tune(w13: torch.Tensor, w2: torch.Tensor, buckets: list, top_k: int, n_exper
         for name, w, epi, N, K, o, xin in (("w13", w13, 1, two_i, H, h, xs), ("w2", w2, 0, H, I, ys, h)):
             bt, bc = None, None
             for cfg in candidates(T, N, K, epi, all_mf=True):
-                mf, nf, wm, sk = cfg
-                if wm > 2:
+                sk = cfg[3]
+                if cfg[2] > 2:
                     continue
                 pp = part[: sk * R * N].view(sk, R, N) if sk > 1 else None
-                if not ext().moe_decode_gemm(o, xin, w, offs, pp, T, mf, nf, wm, sk, epi):
+                if not _mdg(o, xin, w, offs, pp, T, cfg, epi):
                     continue
-                t = _graph_time(lambda: ext().moe_decode_gemm(o, xin, w, offs, pp, T, mf, nf, wm, sk, epi))
+                t = _graph_time(lambda: _mdg(o, xin, w, offs, pp, T, cfg, epi))
                 if bt is None or t < bt:
                     bt, bc = t, cfg
             best[name] = bc

@@ -260,8 +260,11 @@ class Worker:
         return {"ok": True}
 
     def _abort(self, rid: str) -> bool:
-        if self.aeng._queues.pop(rid, None) is None:
+        ent = self.aeng._queues.pop(rid, None)
+        if ent is None:
             return False
+        if isinstance(ent[1], _MuxSink):
+            ent[1].ch.rids.discard(rid)
         self.aeng.submit_nowait(self.engine.abort, rid)
         return True
 

@@ -120,9 +120,17 @@ def fake_worker(port: int, frontend: str, step_ms: float) -> None:
 
 
 def cpu_seconds(pid: int) -> float:
-    with open(f"/proc/{pid}/stat") as f:
-        parts = f.read().rsplit(")", 1)[1].split()
-    return (int(parts[11]) + int(parts[12])) / os.sysconf("SC_CLK_TCK")
+    """CPU time of the frontend process and its children (a multi-process frontend)."""
+    import psutil
+    root = psutil.Process(pid)
+    tot = 0.0
+    for p in [root] + root.children(recursive=True):
+        try:
+            t = p.cpu_times()
+            tot += t.user + t.system
+        except psutil.NoSuchProcess:
+            pass
+    return tot
 
 
 def main():
@@ -135,6 +143,7 @@ def main():
     ap.add_argument("--osl", type=int, default=500)
     ap.add_argument("--step-ms", type=float, default=10.0)
     ap.add_argument("--plane", default="mux")
+    ap.add_argument("--procs", type=int, default=1, help="frontend processes (--num-procs)")
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--out", default="/tmp/fe_probe")
     a = ap.parse_args()
@@ -145,7 +154,7 @@ def main():
     fe_port, w_port = free_port(), free_port()
     env = dict(os.environ, PYTHONPATH=ROOT, MXS_REQUEST_PLANE=a.plane)
     fe_cmd = [sys.executable] + (["-m", "cProfile", "-o", f"{a.out}/frontend.prof"] if a.profile else []) + [
-        "-m", "mxserve.frontend", "--http-host", "127.0.0.1", "--http-port", str(fe_port)]
+        "-m", "mxserve.frontend", "--http-host", "127.0.0.1", "--http-port", str(fe_port), "--num-procs", str(a.procs)]
     fe = subprocess.Popen(fe_cmd, env=env)
     w = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--role", "worker", "--port", str(w_port),
                           "--frontend", f"http://127.0.0.1:{fe_port}", "--step-ms", str(a.step_ms)], env=env)
@@ -172,7 +181,7 @@ def main():
             if fn.startswith("rate_"):
                 res = json.load(open(os.path.join(d, fn)))
         toks = a.requests * a.osl
-        print(json.dumps({"plane": a.plane, "qps": a.qps, "frontend_cpu_s": round(c1 - c0, 2), "wall_s": round(t1 - t0, 1),
+        print(json.dumps({"plane": a.plane, "procs": a.procs, "qps": a.qps, "frontend_cpu_s": round(c1 - c0, 2), "wall_s": round(t1 - t0, 1),
                           "frontend_cpu_ms_per_1k_tokens": round(1e3 * (c1 - c0) / toks * 1e3, 2),
                           "ttft_ms_p50": res.get("ttft_ms_p50"), "itl_ms_p50": res.get("itl_ms_p50"),
                           "steady_ttft_ms_p50": res.get("steady_ttft_ms_p50"),

@@ -56,13 +56,13 @@ def main():
             xin = xs if name == "w13" else h
             res = []
             for cfg in dg.candidates(min(T, 256), N, K, epi, all_mf=True):
-                mf, nf, wm, sk = cfg
-                if wm > 2:
+                sk = cfg[3]
+                if cfg[2] > 2:
                     continue
                 pp = part[: sk * R * N].view(sk, R, N) if sk > 1 else None
-                if not ext().moe_decode_gemm(o, xin, w, offs, pp, T, mf, nf, wm, sk, epi):
+                if not moe._mdg(o, xin, w, offs, pp, T, cfg, epi):
                     continue
-                us = dg._graph_time(lambda: ext().moe_decode_gemm(o, xin, w, offs, pp, T, mf, nf, wm, sk, epi))
+                us = dg._graph_time(lambda: moe._mdg(o, xin, w, offs, pp, T, cfg, epi))
                 res.append((cfg, us))
             res.sort(key=lambda r: r[1])
             for c, us in res[: a.top]:

@@ -13,7 +13,7 @@ FE_PORT="${FE_PORT:-18000}"
 W_PORT="${W_PORT:-18081}"
 mkdir -p "$OUT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0 PYTHONPATH="$PWD" MXS_CUDA_GRAPH_MAX_BS=384
-python3 -m dynamo.frontend --http-port "$FE_PORT" > "$OUT/frontend.log" 2>&1 &
+python3 -m dynamo.frontend --http-port "$FE_PORT" --num-procs "${FE_PROCS:-4}" > "$OUT/frontend.log" 2>&1 &
 FE=$!
 python3 -m dynamo.vllm --model "$MODEL" --frontend-url "http://127.0.0.1:$FE_PORT" --host 127.0.0.1 \
   --port "$W_PORT" --max-num-seqs 384 --max-num-batched-tokens 8192 > "$OUT/worker.log" 2>&1 &
@@ -31,9 +31,10 @@ python3 -m benchmarks.utils.benchmark --benchmark-name served --endpoint-url "ht
   --model "$MODEL" --output-dir "$OUT" --concurrency "" --request-rate "$QPS" --num-requests "$N" \
   --isl 4000 --osl 500 --token-ids --vocab 128256 --warmup-s 15 &
 B=$!
-# CPU of each process over the run (frontend / worker / load generator): which one is the limit
+# CPU of each process over the run (frontend parent / frontend processes summed / worker / load
+# generator): which one is the limit
 ( while kill -0 "$B" 2>/dev/null; do
-    echo "$(date +%s) $(ps -o pcpu= -p "$FE") $(ps -o pcpu= -p "$W") $(ps -o pcpu= -p "$B")"; sleep 5
+    echo "$(date +%s) $(ps -o pcpu= -p "$FE") $(ps -o pcpu= --ppid "$FE" | awk '{s+=$1} END {print s+0}') $(ps -o pcpu= -p "$W") $(ps -o pcpu= -p "$B")"; sleep 5
   done ) > "$OUT/cpu_fe_worker_client.txt" &
 wait "$B"
 curl -sf "http://127.0.0.1:$FE_PORT/metrics" > "$OUT/frontend_metrics.txt" || true

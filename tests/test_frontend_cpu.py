@@ -462,3 +462,87 @@ def test_batched_ndjson_token_lines():
     finally:
         fs.stop()
         ws.stop()
+
+
+def test_mux_plane_client_disconnect_aborts(agg_stack):
+    """On the multiplexed request plane a client that goes away mid-stream makes the frontend POST
+    /abort: the worker drops the request (engine, channel membership, sink)."""
+    import time
+    fe, fs, w = agg_stack
+    with httpx.Client(timeout=60) as c:
+        with c.stream("POST", fs.url + "/v1/completions",
+                      json={"model": MODEL, "prompt": "tell me", "max_tokens": 400, "stream": True,
+                            "ignore_eos": True}) as r:
+            n = 0
+            for line in r.iter_lines():
+                if line.startswith("data: {"):
+                    n += 1
+                if n >= 3:
+                    break
+    for _ in range(300):
+        if not w.engine.requests and not w.aeng._queues and all(not ch.rids for ch in w._channels.values()):
+            break
+        time.sleep(0.02)
+    assert not w.engine.requests and not w.aeng._queues
+    assert w._channels and all(not ch.rids for ch in w._channels.values())
+
+
+def test_stream_plane_fallback(agg_stack, monkeypatch):
+    """MXS_REQUEST_PLANE=stream: one /generate NDJSON response per request (the pre-mux protocol,
+    also what the frontend falls back to for a worker without /mux)."""
+    from mxserve.frontend import app as app_mod
+    monkeypatch.setattr(app_mod, "REQUEST_PLANE", "stream")
+    _, fs, _ = agg_stack
+    body = {"model": MODEL, "prompt": "same prompt", "max_tokens": 6, "temperature": 0}
+    a = httpx.post(fs.url + "/v1/completions", json=body, timeout=60).json()
+    monkeypatch.setattr(app_mod, "REQUEST_PLANE", "mux")
+    b = httpx.post(fs.url + "/v1/completions", json=body, timeout=60).json()
+    assert a["choices"][0]["text"] == b["choices"][0]["text"]
+    assert a["usage"]["completion_tokens"] == b["usage"]["completion_tokens"] == 6
+
+
+def test_multiprocess_frontend_shares_discovery_and_metrics(tmp_path):
+    """`--num-procs 2`: both processes serve the port, a worker registered through one of them is
+    routable from either, and /metrics sums the processes' counters."""
+    import os
+    import subprocess
+    import sys
+    import time
+    from tests.serving_utils import free_port
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root)
+    env.pop("PROMETHEUS_MULTIPROC_DIR", None)
+    fp, wp = free_port(), free_port()
+    fe = subprocess.Popen([sys.executable, "-m", "mxserve.frontend", "--http-host", "127.0.0.1", "--http-port", str(fp),
+                           "--num-procs", "2"], env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    wk = subprocess.Popen([sys.executable, os.path.join(root, "scripts", "frontend_cpu_probe.py"), "--role", "worker",
+                           "--port", str(wp), "--frontend", f"http://127.0.0.1:{fp}", "--step-ms", "2"], env=env,
+                          stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    url = f"http://127.0.0.1:{fp}"
+    model = "meta-llama/Llama-3.2-1B-Instruct"
+    try:
+        seen = 0
+        for _ in range(300):  # fresh connections land on either process; all must know the worker
+            try:
+                ok = all(model in httpx.get(url + "/v1/models", timeout=2).text for _ in range(8))
+            except httpx.HTTPError:
+                ok = False
+            seen = seen + 1 if ok else 0
+            if seen >= 3:
+                break
+            time.sleep(0.1)
+        assert seen >= 3, "worker not visible from every frontend process"
+        for i in range(8):
+            r = httpx.post(url + "/v1/completions", json={"model": model, "prompt": [1, 2, 3], "max_tokens": 5},
+                           timeout=30)
+            assert r.status_code == 200, r.text
+            assert r.json()["usage"]["completion_tokens"] == 5
+        from mxserve.planner.planner import parse_prometheus
+        m = parse_prometheus(httpx.get(url + "/metrics", timeout=5).text)
+        total = sum(v for k, v in m.items() if k.startswith("dynamo_frontend_requests_total"))
+        assert total == 8, m
+    finally:
+        wk.terminate()
+        fe.terminate()
+        wk.wait(timeout=20)
+        fe.wait(timeout=30)

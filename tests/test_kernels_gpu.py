@@ -481,10 +481,11 @@ def test_decode_gemm_all_configs(gpu, M, N, K, epi):
     cands = decode_gemm.candidates(M, N, K, epi)
     assert cands
     part = torch.empty(8 * M * N, dtype=torch.float32, device=gpu)
-    for mf, nf, wm, sk in cands:
+    assert any(c[4] for c in cands) or M <= 16, "LDS-form configurations are among the candidates"
+    for mf, nf, wm, sk, lu in cands:
         out = torch.full((M, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
-        assert ops.ext().decode_gemm(out, x, w, part, mf, nf, wm, sk, epi)
-        _close(out, want, atol=2e-2, rtol=2e-2, name=f"decode gemm {M}x{N}x{K} epi{epi} cfg {(mf, nf, wm, sk)}")
+        assert ops.ext().decode_gemm(out, x, w, part, mf, nf, wm, sk, epi, lu)
+        _close(out, want, atol=2e-2, rtol=2e-2, name=f"decode gemm {M}x{N}x{K} epi{epi} cfg {(mf, nf, wm, sk, lu)}")
 
 
 def test_decode_gemm_tuner_and_dispatch(gpu, monkeypatch):
@@ -560,12 +561,12 @@ def test_moe_decode_gemm_all_configs(gpu, counts, silu):
     epi = int(silu)
     ran = 0
     for cfg in dg.candidates(rows_max, N, K, epi, all_mf=True):
-        mf, nf, wm, sk = cfg
+        mf, nf, wm, sk, lu = cfg
         if wm > 2:
             continue
         y = torch.full((R, N // 2 if silu else N), 7.0, device=gpu, dtype=torch.bfloat16)
         part = torch.zeros(sk, R, N, device=gpu, dtype=torch.float32) if sk > 1 else None
-        assert ops.ext().moe_decode_gemm(y, x, w, offs, part, rows_max, mf, nf, wm, sk, epi), cfg
+        assert ops.ext().moe_decode_gemm(y, x, w, offs, part, rows_max, mf, nf, wm, sk, epi, lu), cfg
         ran += 1
         for e, r in refs.items():
             a, b = o[e], o[e + 1]
@@ -580,7 +581,7 @@ def test_moe_decode_gemm_all_configs(gpu, counts, silu):
             _close(y[a:b], exp, atol=3e-2, rtol=3e-2, name=f"expert {e} cfg {cfg}")
         if sk == 1:
             assert torch.all(y[o[-1]:] == 7.0), f"rows past the routed count were written ({cfg})"
-    assert ran >= 6
+    assert ran >= 6 and any(c[4] for c in dg.candidates(rows_max, N, K, epi, all_mf=True))
 
 
 @pytest.mark.parametrize("T,offset", [(1, 0), (7, 0), (64, 0), (200, 0), (40, 2)])
