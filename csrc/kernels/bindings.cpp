@@ -32,6 +32,8 @@ void launch_moe_align(int*, int*, const int*, int, int, int, int*, hipStream_t);
 void launch_moe_combine(bf16_t*, const bf16_t*, const float*, const int*, int, int, int, hipStream_t);
 bool launch_decode_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int,
                         int, hipStream_t, const int* = nullptr, int = 0, int = 0, int = 0);
+bool launch_prefill_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int,
+                         hipStream_t);
 bool launch_moe_grouped_gemm(bf16_t*, const bf16_t*, const bf16_t*, const int*, int, int, int, int, int, bool,
                              int, float*, hipStream_t);
 void launch_moe_combine_partials(bf16_t*, const float*, const float*, const int*, int, int, int, int, long,
@@ -235,6 +237,25 @@ bool decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::T
                                  epi, stream(), nullptr, 0, 0, lu);
 }
 
+// K05-K08 at prefill sizes (csrc/kernels/gemm_prefill.hip): out [M, N] = x [M, K] . w [N, K]^T.
+// bm in {64, 128}; splitk > 1 needs an fp32 workspace of splitk * M * N.  False if unsupported.
+bool prefill_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> part, int64_t bm,
+                  int64_t splitk) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == N, "shape mismatch");
+  if (x.stride(1) != 1 || out.stride(1) != 1) return false;
+  float* p = nullptr;
+  if (splitk > 1) {
+    TORCH_CHECK(part.has_value() && part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->numel() >= splitk * M * N, "split-K needs an fp32 workspace of splitk * M * N");
+    p = part->data_ptr<float>();
+  }
+  return mxs::launch_prefill_gemm(bf(out), p, bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), bm, splitk,
+                                  stream());
+}
+
 // Grouped decode form of decode_gemm (K16 at decode batches): w [E, N, K], x = routed rows sorted by
 // expert (offs = moe_align offsets), rows_max = the most rows one expert can hold (tokens).  Output
 // as moe_grouped_gemm: out [rows, N or N/2] (splitk 1) or fp32 partials [splitk, rows, N].
@@ -344,6 +365,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("decode_gemm", &decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("part"), pybind11::arg("mf"), pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"),
         pybind11::arg("epi"), pybind11::arg("lu") = 0);
+  m.def("prefill_gemm", &prefill_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
+        pybind11::arg("part"), pybind11::arg("bm"), pybind11::arg("splitk"));
   m.def("moe_decode_gemm", &moe_decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("offs"), pybind11::arg("part"), pybind11::arg("rows_max"), pybind11::arg("mf"),
         pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"), pybind11::arg("epi"),

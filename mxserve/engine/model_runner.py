@@ -542,6 +542,8 @@ class ModelRunner:
             shapes.update(gate_up=(w["l0.gate_up"], 1), down=(w["l0.down"], 0))
         with torch.inference_mode():
             self.decode_gemm_report = decode_gemm.tune(shapes, buckets, self.device, self.dtype)
+            self.prefill_gemm_report = decode_gemm.tune_prefill(
+                {k: v for k, (v, epi) in shapes.items() if epi == 0 and k != "lm_head"}, self.device, self.dtype)
             if self.cfg.is_moe and "l0.w13" in w:  # expert GEMMs at decode batches (local experts)
                 from ..ops import moe as moe_ops
                 self.moe_gemm_report = moe_ops.tune(w["l0.w13"], w["l0.w2"], buckets, self.cfg.num_experts_per_tok,

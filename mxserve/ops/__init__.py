@@ -57,14 +57,44 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """y = x @ w.T.  Decode-sized GEMMs (M <= 256) run the hand-written MFMA kernel where the
     tuning pass at graph capture measured it faster than hipBLASLt for that batch bucket and
     projection (mxserve/ops/decode_gemm.py); everything else is hipBLASLt."""
-    if _gpu(x) and x.dim() == 2 and x.shape[0] <= 256:
-        from .decode_gemm import TABLE
-        cfg = TABLE.lookup(x.shape[0], w.shape[0], w.shape[1], 0)
-        if cfg is not None:
-            out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-            if TABLE.run(out, x, w, cfg, 0):
-                return out
+    if _gpu(x) and x.dim() == 2:
+        M = x.shape[0]
+        if M <= 256:
+            from .decode_gemm import TABLE
+            cfg = TABLE.lookup(M, w.shape[0], w.shape[1], 0)
+            if cfg is not None:
+                out = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
+                if TABLE.run(out, x, w, cfg, 0):
+                    return out
+        else:  # small prefill chunks: the 64/128-row tile kernel where it was measured faster
+            from .decode_gemm import PREFILL_TABLE
+            cfg = PREFILL_TABLE.lookup(M, w.shape[0], w.shape[1])
+            if cfg is not None:
+                out = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
+                if prefill_gemm(out, x, w, cfg):
+                    return out
     return torch.nn.functional.linear(x, w)
+
+
+_PG_PART: dict = {}
+
+
+def prefill_gemm_configs(M: int, N: int, K: int) -> list:
+    """(bm, splitk) configurations of the prefill GEMM kernel (csrc/kernels/gemm_prefill.hip)."""
+    if N % 128:
+        return []
+    return [(bm, sk) for bm in (64, 128) for sk in (1, 2, 4) if K % (64 * sk) == 0]
+
+
+def prefill_gemm(out: torch.Tensor, x: torch.Tensor, w: torch.Tensor, cfg: tuple) -> bool:
+    bm, sk = cfg
+    part = None
+    if sk > 1:
+        need = sk * x.shape[0] * w.shape[0]
+        part = _PG_PART.get(x.device)
+        if part is None or part.numel() < need:
+            part = _PG_PART[x.device] = torch.empty(need, dtype=torch.float32, device=x.device)
+    return bool(ext().prefill_gemm(out, x, w, part, bm, sk))
 
 
 def gate_up_silu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:

@@ -198,3 +198,74 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
             for r in rows:
                 f.write(json.dumps(r) + "\n")
     return rows
+
+
+class PrefillGemmTable:
+    """Prefill-sized GEMMs (256 < M <= PREFILL_MAX_M) on the tile kernel of gemm_prefill.hip where
+    the startup measurement found it faster than hipBLASLt: (N, K) -> sorted [(M bucket, cfg|None)].
+    Above PREFILL_MAX_M the library's 256 x 256 tiles fill the chip and win
+    (profiles/r2_prefill_gemm_probe_v1.jsonl)."""
+
+    def __init__(self):
+        self.entries: dict = {}
+        self.report: list = []
+
+    def lookup(self, M: int, N: int, K: int):
+        if MODE == "off" or M > PREFILL_MAX_M:
+            return None
+        ent = self.entries.get((N, K))
+        if not ent:
+            return None
+        i = bisect.bisect_left(ent, (M,))
+        return ent[i][1] if i < len(ent) else None
+
+
+PREFILL_MAX_M = int(os.environ.get("MXS_PREFILL_GEMM_MAX_M", "768"))
+PREFILL_TABLE = PrefillGemmTable()
+
+
+def _event_time(fn, iters: int = 10) -> float:
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
+def tune_prefill(weights: dict, device, dtype=torch.bfloat16, buckets=(384, 512, 768)) -> list:
+    """weights: {name: [N, K] tensor}.  Per M bucket: every tile / split-K configuration of the
+    prefill kernel vs hipBLASLt (eager launches, as prefill runs), correctness-gated."""
+    if MODE != "auto":
+        return []
+    from .. import ops
+    rows = []
+    for name, w in weights.items():
+        N, K = w.shape
+        ent = []
+        for M in sorted(b for b in buckets if 256 < b <= PREFILL_MAX_M):
+            x = (torch.randn(M, K, device=device) * 0.5).to(dtype)
+            ref = torch.nn.functional.linear(x, w)
+            t_lib = _event_time(lambda: torch.nn.functional.linear(x, w))
+            best, best_t = None, t_lib
+            out = torch.empty(M, N, dtype=dtype, device=device)
+            for cfg in ops.prefill_gemm_configs(M, N, K):
+                if not ops.prefill_gemm(out, x, w, cfg):
+                    continue
+                t = _event_time(lambda: ops.prefill_gemm(out, x, w, cfg))
+                if t < best_t * 0.97:
+                    best, best_t = cfg, t
+            if best is not None:
+                ops.prefill_gemm(out, x, w, best)
+                err = (out.float() - ref.float()).abs().max().item()
+                if not err <= 0.02 * max(1.0, ref.float().abs().max().item()):
+                    best, best_t = None, t_lib
+            ent.append((M, best))
+            rows.append({"proj": name, "M": M, "N": N, "K": K, "hipblaslt_us": round(t_lib, 2),
+                         "chosen": "hipblaslt" if best is None else "mfma", "cfg": best, "us": round(best_t, 2)})
+        PREFILL_TABLE.entries[(N, K)] = ent
+    PREFILL_TABLE.report = rows
+    return rows

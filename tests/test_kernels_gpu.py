@@ -700,3 +700,39 @@ def test_ep_route_kernel(gpu, n, e_local, S, k, valid):
     for p in range(0, P, max(1, P // 50)):
         if exp_slot[p] >= 0:
             assert torch.equal(send_x[exp_slot[p]], hs[p // k])
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 2048, 2048), (100, 3072, 2048), (777, 2048, 8192), (2048, 2048, 2048),
+                                   (4096, 3072, 2048), (1000, 16384, 2048)])
+def test_prefill_gemm_all_configs(gpu, M, N, K):
+    """Prefill projection GEMM kernel (csrc/kernels/gemm_prefill.hip), every tile / split-K
+    configuration vs an fp32 reference, including row counts that are not tile multiples."""
+    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=gpu) * 2 - 1) * K ** -0.5).to(torch.bfloat16)
+    want = x.float() @ w.float().t()
+    cfgs = ops.prefill_gemm_configs(M, N, K)
+    assert len(cfgs) >= 4
+    for cfg in cfgs:
+        out = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+        assert ops.prefill_gemm(out, x, w, cfg), cfg
+        _close(out, want, atol=2e-2, rtol=2e-2, name=f"prefill gemm {M}x{N}x{K} cfg {cfg}")
+
+
+def test_prefill_gemm_tuner_and_dispatch(gpu, monkeypatch):
+    """Startup tuner for small prefill chunks: hipBLASLt vs the tile kernel per M bucket, and
+    ops.linear follows the table (the kernel runs when it was chosen) with correct results."""
+    from mxserve.ops import decode_gemm
+    monkeypatch.setattr(decode_gemm, "MODE", "auto")
+    monkeypatch.setattr(decode_gemm.PREFILL_TABLE, "entries", {})
+    w = ((torch.rand(2048, 2048, device=gpu) * 2 - 1) * 0.02).to(torch.bfloat16)
+    rows = decode_gemm.tune_prefill({"o": w}, gpu, buckets=(384, 512))
+    assert len(rows) == 2 and all(r["us"] <= r["hipblaslt_us"] for r in rows)
+    calls = []
+    real = ops.prefill_gemm
+    monkeypatch.setattr(ops, "prefill_gemm", lambda *a: calls.append(1) or real(*a))
+    for M in (300, 500):
+        x = torch.randn(M, 2048, device=gpu, dtype=torch.bfloat16)
+        _close(ops.linear(x, w), x.float() @ w.float().t(), 2e-2, 2e-2, f"tuned prefill linear M={M}")
+    assert len(calls) == sum(r["chosen"] == "mfma" for r in rows)
+    x = torch.randn(1000, 2048, device=gpu, dtype=torch.bfloat16)  # above PREFILL_MAX_M: hipBLASLt
+    _close(ops.linear(x, w), x.float() @ w.float().t(), 2e-2, 2e-2, "prefill linear M=1000")
