@@ -173,7 +173,8 @@ def test_run_benchmarks_sh(local_frontend, tmp_path):
     assert (tmp_path / "plots" / "summary.md").exists()
 
 
-@pytest.mark.parametrize("mode,nproc,launcher", [("agg", 1, "self"), ("auto", 2, "self"), ("disagg", 2, "torchrun")])
+@pytest.mark.parametrize("mode,nproc,launcher", [("agg", 1, "self"), ("auto", 2, "self"), ("disagg", 2, "torchrun"),
+                                                  ("auto", 4, "self")])
 def test_bench_contract_cpu(mode, nproc, launcher, tmp_path):
     """bench.py prints exactly one JSON line with the driver's contract fields (CPU plumbing run).
     `--gpus N` alone spawns the N ranks itself; under torch.distributed.run (the driver's multi-GPU
@@ -205,7 +206,7 @@ def test_bench_contract_cpu(mode, nproc, launcher, tmp_path):
     assert d["config"]["mode"] == want
     if want == "both":
         assert d["agg"]["value"] == d["value"] and d["disagg"]["value"] > 0
-        assert d["disagg"]["parallelism"] == "disagg 1P+1D"
+        assert d["disagg"]["parallelism"] == f"disagg {nproc // 2}P+{nproc // 2}D"
 
 
 def test_bench_rejects_world_mismatch(tmp_path):
