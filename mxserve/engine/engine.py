@@ -354,7 +354,11 @@ def _first_token_timing(req) -> dict:
     prefill steps up to the sampled token."""
     sched = req.scheduled_time if req.scheduled_time is not None else req.arrival_time
     first = req.first_token_time if req.first_token_time is not None else sched
-    return {"queue_ms": round((sched - req.arrival_time) * 1e3, 3), "prefill_ms": round((first - sched) * 1e3, 3)}
+    t = {"queue_ms": round((sched - req.arrival_time) * 1e3, 3), "prefill_ms": round((first - sched) * 1e3, 3),
+         "emit_unix": time.time()}  # the consumer's receive time minus this = delivery latency (same host)
+    if req.submit_time is not None:  # waiting in the engine thread's inbox for a step boundary
+        t["inbox_ms"] = round((req.arrival_time - req.submit_time) * 1e3, 3)
+    return t
 
 
 def _put_many(items: list) -> None:

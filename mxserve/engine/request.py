@@ -88,6 +88,7 @@ class Request:
     block_hashes: list = field(default_factory=list)
     num_registered_blocks: int = 0
     seed: int = 0
+    submit_time: Optional[float] = None  # monotonic: the serving layer received it (before the engine inbox)
     scheduled_time: Optional[float] = None  # first admitted into a step (queue time ends)
     first_token_time: Optional[float] = None
     finish_time: Optional[float] = None

@@ -599,7 +599,11 @@ class Frontend:
             eos_ids = tok.eos_token_ids
             async for evs in self.generate_tokens(model, prompt_ids, sub_sp, sub_rid):
                 if evs[0].timing and "worker_ms" not in trace.attrs:
-                    trace.attrs["worker_ms"] = evs[0].timing  # queue / prefill / kv transfer on the worker
+                    tm = dict(evs[0].timing)  # queue / prefill / kv transfer on the worker
+                    emit = tm.pop("emit_unix", None)
+                    if emit is not None:  # worker emitted the first token -> this process has it
+                        tm["delivery_ms"] = round((time.time() - emit) * 1e3, 3)
+                    trace.attrs["worker_ms"] = tm
                 on_tokens(idx, len(evs))
                 ev = evs[-1]  # a batch becomes one delta; only its last event can finish the request
                 eos_hit = ev.finished and ev.finish_reason == "stop" and ev.token_id in eos_ids

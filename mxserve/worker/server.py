@@ -229,7 +229,7 @@ class Worker:
             return
         q = self.aeng.open_stream(rid)
         try:
-            await self.aeng.submit(self.engine.add_request, toks, sp, rid, None)
+            await self.aeng.submit(self._add_request, toks, sp, rid, time.monotonic())
         except BaseException:
             self.aeng._queues.pop(rid, None)
             raise
@@ -252,12 +252,18 @@ class Worker:
                 return {"ok": True}
         self.aeng._queues[rid] = (asyncio.get_running_loop(), sink)
         try:
-            await self.aeng.submit(self.engine.add_request, toks, sp, rid, None)
+            await self.aeng.submit(self._add_request, toks, sp, rid, time.monotonic())
         except BaseException:
             self.aeng._queues.pop(rid, None)
             ch.rids.discard(rid)
             raise
         return {"ok": True}
+
+    def _add_request(self, toks: list, sp: SamplingParams, rid: str, t_in: float):
+        """Engine thread: add the request, stamping when the HTTP layer received it."""
+        req = self.engine.add_request(toks, sp, rid, None)
+        req.submit_time = t_in
+        return req
 
     def _abort(self, rid: str) -> bool:
         ent = self.aeng._queues.pop(rid, None)
@@ -535,9 +541,14 @@ def advertise_url(wargs: WorkerArgs, port: int) -> str:
 
 
 def serve(wargs: WorkerArgs) -> None:
+    import sys
     import uvicorn
     from ..utils.logs import setup_logging
     setup_logging()
+    # the engine thread and the HTTP event loop share the GIL: a thread that wants it waits up to
+    # the switch interval (5 ms by default) while the other runs Python -- a whole decode step at
+    # the headline point.  A shorter interval bounds the engine thread's wait.
+    sys.setswitchinterval(float(os.environ.get("MXS_GIL_SWITCH_MS", "0.5")) / 1e3)
     off = int(os.environ.get("MXS_DEVICE_OFFSET", "0"))
     if off and wargs.engine.resolved_device() == "cuda":  # second worker of a P/D pair pod
         import torch

@@ -38,6 +38,32 @@ B=$!
   done ) > "$OUT/cpu_fe_worker_client.txt" &
 wait "$B"
 curl -sf "http://127.0.0.1:$FE_PORT/metrics" > "$OUT/frontend_metrics.txt" || true
+# request traces (per frontend process: a few fetches land on different processes)
+for i in 1 2 3 4 5 6 7 8; do curl -sf "http://127.0.0.1:$FE_PORT/debug/traces?n=300" > "$OUT/traces_$i.json" || true; done
+python3 - "$OUT" <<'PY'
+import glob, json, statistics, sys
+seen, rows = set(), []
+for f in glob.glob(sys.argv[1] + "/traces_*.json"):
+    try:
+        for t in json.load(open(f))["traces"]:
+            if t["request_id"] not in seen and "first_token" in t.get("spans_ms", {}):
+                seen.add(t["request_id"])
+                rows.append(t)
+    except (OSError, ValueError, KeyError):
+        pass
+if rows:
+    med = lambda xs: round(statistics.median(xs), 2) if xs else None
+    sp = [r["spans_ms"] for r in rows]
+    wk = [r.get("worker_ms") or {} for r in rows]
+    out = {"traces": len(rows), "routed_ms_p50": med([s.get("routed", 0) for s in sp]),
+           "first_token_ms_p50": med([s["first_token"] for s in sp]),
+           "worker_queue_ms_p50": med([w["queue_ms"] for w in wk if "queue_ms" in w]),
+           "worker_prefill_ms_p50": med([w["prefill_ms"] for w in wk if "prefill_ms" in w]),
+           "worker_inbox_ms_p50": med([w["inbox_ms"] for w in wk if "inbox_ms" in w]),
+           "delivery_ms_p50": med([w["delivery_ms"] for w in wk if "delivery_ms" in w])}
+    print("[served] TTFT breakdown (median over %d traces): %s" % (len(rows), json.dumps(out)))
+    json.dump(out, open(sys.argv[1] + "/ttft_breakdown.json", "w"))
+PY
 python3 - "$OUT/frontend_metrics.txt" <<'PY'
 import sys
 from mxserve.planner.planner import parse_prometheus
