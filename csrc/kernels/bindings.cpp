@@ -378,7 +378,7 @@ PYBIND11_MODULE(_C, m) {
     CHECK_CUDA(part); CHECK_BF16(h); CHECK_CONTIG(h);
     TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3, "part fp32 [S, R, 2I]");
     const int R = part.size(1), I = part.size(2) / 2;
-    TORCH_CHECK(I % 4 == 0 && h.size(0) == R && h.size(1) == I, "shapes");
+    TORCH_CHECK(I % 4 == 0 && h.size(0) == R && h.size(1) == I && part.size(0) <= 8, "shapes (at most 8 slabs)");
     mxs::launch_silu_mul_partials(bf(h), part.data_ptr<float>(), R, I, part.size(0),
                                   part.size(1) * static_cast<long>(part.size(2)), stream());
   });
@@ -388,7 +388,8 @@ PYBIND11_MODULE(_C, m) {
     TORCH_CHECK(topk_w.scalar_type() == at::kFloat && topk_w.is_contiguous() && topk_w.dim() == 2, "topk_w");
     TORCH_CHECK(inv.scalar_type() == at::kInt && inv.is_contiguous() && inv.numel() == topk_w.numel(), "inv");
     const int T = topk_w.size(0), K = topk_w.size(1), H = part.size(2);
-    TORCH_CHECK(K <= 8 && H % 4 == 0 && out.size(0) == T && out.size(1) == H, "shapes");
+    TORCH_CHECK(K <= 8 && H % 4 == 0 && out.size(0) == T && out.size(1) == H && part.size(0) <= 8,
+                "shapes (top-k <= 8, at most 8 slabs)");
     mxs::launch_moe_combine_partials(bf(out), part.data_ptr<float>(), topk_w.data_ptr<float>(), inv.data_ptr<int>(),
                                      T, K, H, part.size(0), part.size(1) * static_cast<long>(H), stream());
   });

@@ -160,33 +160,37 @@ void launch_moe_combine(bf16_t* out, const bf16_t* ys, const float* topk_w, cons
 }
 
 // Split-K variant: the expert rows are S fp32 partial slices [S][rows][H] (moe_grouped_gemm split).
+// One thread per (token, 4 columns): grid (T, H / 1024), every K x S slab load of the thread issued
+// back to back (the loops are unrolled to their bounds, K <= 8 and S <= 8, with guards), so a decode
+// batch of ~100 tokens is 400 workgroups of independent loads instead of 100 workgroups walking
+// their rows with one dependent load at a time.
 __global__ void __launch_bounds__(256) moe_combine_partials_kernel(bf16_t* __restrict__ out,
                                                                    const float* __restrict__ part,
                                                                    const float* __restrict__ topk_w,
                                                                    const int* __restrict__ inv, int K, int H, int S,
                                                                    long slice) {
   const int t = blockIdx.x;
-  int rows[8];
-  float ws[8];
-  for (int k = 0; k < K; ++k) {
-    rows[k] = inv[t * K + k];
-    ws[k] = topk_w[t * K + k];
-  }
-  for (int c = threadIdx.x; c < H / 4; c += blockDim.x) {
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k = 0; k < K; ++k) {
-      if (rows[k] < 0) continue;
-      const float* p = part + static_cast<size_t>(rows[k]) * H + c * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int z = 0; z < S; ++z) {
-        const float4 u = *reinterpret_cast<const float4*>(p + z * slice);
-        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
-      }
-      acc.x += ws[k] * v.x; acc.y += ws[k] * v.y; acc.z += ws[k] * v.z; acc.w += ws[k] * v.w;
+  const int c = blockIdx.y * blockDim.x + threadIdx.x;
+  if (c >= H / 4) return;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (k >= K) break;
+    const int row = inv[t * K + k];
+    if (row < 0) continue;
+    const float w = topk_w[t * K + k];
+    const float* p = part + static_cast<size_t>(row) * H + c * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int z = 0; z < 8; ++z) {
+      if (z >= S) break;
+      const float4 u = *reinterpret_cast<const float4*>(p + z * slice);
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
     }
-    *reinterpret_cast<uint2*>(out + static_cast<size_t>(t) * H + c * 4) = make_uint2(pack2(acc.x, acc.y),
-                                                                                     pack2(acc.z, acc.w));
+    acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
   }
+  *reinterpret_cast<uint2*>(out + static_cast<size_t>(t) * H + c * 4) = make_uint2(pack2(acc.x, acc.y),
+                                                                                   pack2(acc.z, acc.w));
 }
 
 // Split-K gate_up: h[r, j] = silu(sum_z P[z][r][j]) * sum_z P[z][r][I + j]  (P: [S][rows][2I] fp32)
@@ -199,7 +203,9 @@ __global__ void silu_mul_partials_kernel(bf16_t* __restrict__ h, const float* __
     const int j = static_cast<int>(idx - r * (I / 4)) * 4;
     const float* pg = part + r * 2 * I + j;
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f), u = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int z = 0; z < S; ++z) {
+#pragma unroll
+    for (int z = 0; z < 8; ++z) {  // S <= 8: unrolled so the slab loads are in flight together
+      if (z >= S) break;
       const float4 a = *reinterpret_cast<const float4*>(pg + z * slice);
       const float4 b = *reinterpret_cast<const float4*>(pg + z * slice + I);
       g.x += a.x; g.y += a.y; g.z += a.z; g.w += a.w;
@@ -223,7 +229,9 @@ void launch_silu_mul_partials(bf16_t* h, const float* part, int rows, int I, int
 void launch_moe_combine_partials(bf16_t* out, const float* part, const float* topk_w, const int* inv, int T, int K,
                                  int H, int S, long slice, hipStream_t s) {
   if (T == 0) return;
-  hipLaunchKernelGGL(moe_combine_partials_kernel, dim3(T), dim3(256), 0, s, out, part, topk_w, inv, K, H, S, slice);
+  if (K > 8 || S > 8) return;  // callers: top-k <= 8, split-K <= 8 (checked in the bindings)
+  hipLaunchKernelGGL(moe_combine_partials_kernel, dim3(T, (H / 4 + 255) / 256), dim3(256), 0, s, out, part, topk_w,
+                     inv, K, H, S, slice);
   MXS_CHECK_LAUNCH();
 }
 

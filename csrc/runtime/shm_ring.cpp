@@ -143,6 +143,7 @@ class ShmRing {
   template <class F>
   static bool wait_until(F&& cond, double timeout_s) {
     if (cond()) return true;
+    if (timeout_s <= 0.0) return false;  // a poll: no spinning
     const auto t0 = std::chrono::steady_clock::now();
     for (int spin = 0;; ++spin) {
       if (cond()) return true;

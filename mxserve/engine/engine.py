@@ -221,6 +221,7 @@ class AsyncEngine:
         self._queues: dict[str, tuple[asyncio.AbstractEventLoop, asyncio.Queue]] = {}
         self._stop = False
         self.on_step = None  # optional callback(list[StepOutput]) run on the engine thread
+        self._ring = None  # (cmd ring, out ring, handler): a streamer process owns the request plane
         self.last_stats: dict = engine.stats()
         self._thread = threading.Thread(target=self._loop, name="mxs-engine", daemon=True)
         self._thread.start()
@@ -242,9 +243,14 @@ class AsyncEngine:
     def _loop(self) -> None:
         while not self._stop:
             self._drain()
+            if self._ring is not None:
+                self._drain_ring(0.0)
             if not self.engine.has_unfinished():
                 self.last_stats = self.engine.stats()
-                self._wake.wait(0.05)
+                if self._ring is not None and not self._wake.is_set():
+                    self._drain_ring(0.005)  # idle: a ring command wakes the loop at once
+                else:
+                    self._wake.wait(0.05)
                 self._wake.clear()
                 continue
             try:
@@ -263,18 +269,48 @@ class AsyncEngine:
     def _deliver(self, outs) -> None:
         """One cross-thread wakeup per event loop per step (not per token): at ~20k tokens/s a
         call_soon_threadsafe per token costs the serving process a self-pipe write each and fights
-        the engine thread for the GIL."""
+        the engine thread for the GIL.  Requests of the streamer process (attach_ring) go out as
+        ONE ring message per step, written here on the engine thread."""
         by_loop: dict = {}
+        ring_outs = []
         for o in outs:
             ent = self._queues.get(o.request_id)
             if ent is None:
                 continue
             loop, q = ent
-            by_loop.setdefault(loop, []).append((q, o))
+            if loop is None:
+                ring_outs.append(o)
+            else:
+                by_loop.setdefault(loop, []).append((q, o))
             if o.finished:
                 self._queues.pop(o.request_id, None)
         for loop, items in by_loop.items():
             loop.call_soon_threadsafe(_put_many, items)
+        if ring_outs:
+            self._ring[2].emit(ring_outs)
+
+    # ---------------------------------------------------------------- streamer process (ring)
+    def attach_ring(self, handler) -> None:
+        """Hand the token request plane to a streamer process (mxserve/worker/streamer.py):
+        handler.poll(timeout) -> command or None, handler.command(cmd) runs it (engine thread),
+        handler.emit(outs) writes one step's outputs.  Set before traffic arrives."""
+        self._ring = (None, None, handler)
+
+    def _drain_ring(self, timeout: float) -> None:
+        h = self._ring[2]
+        while True:
+            cmd = h.poll(timeout)
+            if cmd is None:
+                return
+            timeout = 0.0
+            try:
+                h.command(cmd)
+            except Exception:  # noqa: BLE001 - a bad command must not stop the engine loop
+                log.exception("streamer command failed")
+
+    def own_by_ring(self, request_id: str) -> None:
+        """Route this request's outputs to the streamer ring (engine thread or before the loop sees it)."""
+        self._queues[request_id] = (None, None)
 
     def _fail_all(self) -> list:
         self.engine._inflight = None  # the failed step's results are never collected
@@ -302,8 +338,12 @@ class AsyncEngine:
         return q
 
     def push(self, out: StepOutput) -> None:
-        """Deliver an output produced outside a step (e.g. a remotely prefilled first token)."""
-        self._deliver([out])
+        """Deliver an output produced outside a step (e.g. a remotely prefilled first token).  With a
+        streamer ring the engine thread is the ring's only producer: queue it there."""
+        if self._ring is not None and threading.current_thread() is not self._thread:
+            self.submit_nowait(self._deliver, [out])
+        else:
+            self._deliver([out])
 
     async def stream(self, request_id: str, q: asyncio.Queue):
         try:

@@ -260,7 +260,8 @@ class Frontend:
         info = WorkerInfo(worker_id=d["worker_id"], url=d["url"], model=d["model"], role=d.get("role", "agg"),
                           block_size=int(d.get("block_size", 16)),
                           kv_total_blocks=int(d.get("kv_total_blocks", 1) or 1), tp=int(d.get("tp", 1)),
-                          max_model_len=int(d.get("max_model_len", 0) or 0), pair=str(d.get("pair") or ""))
+                          max_model_len=int(d.get("max_model_len", 0) or 0), pair=str(d.get("pair") or ""),
+                          stream_url=str(d.get("stream_url") or ""))
         self.registry.register(info)
         log.info("registered worker %s (%s) for %s at %s", info.worker_id, info.role, info.model, info.url)
         return info
@@ -333,9 +334,10 @@ class Frontend:
         if prefill_url:
             body["prefill_url"] = prefill_url
         if REQUEST_PLANE == "mux":
-            mc = self._mux.get(w.url)
+            murl = w.stream_url or w.url  # the worker's streamer process, if it runs one
+            mc = self._mux.get(murl)
             if mc is None:
-                mc = self._mux[w.url] = MuxClient(w.url)
+                mc = self._mux[murl] = MuxClient(murl)
             if not mc.unsupported:
                 try:
                     await mc.ensure(sess)

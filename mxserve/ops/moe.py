@@ -181,12 +181,13 @@ def fused_experts(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: 
     dev = x.device
     ids = topk_ids.to(torch.int32).contiguous()
     offs = torch.empty(e_local + 1, dtype=torch.int32, device=dev)
-    perm = torch.full((T * K,), -1, dtype=torch.int32, device=dev)
+    perm = torch.empty(T * K, dtype=torch.int32, device=dev)
     inv = torch.empty(T * K, dtype=torch.int32, device=dev)
     ext().moe_align(offs, perm, ids, expert_offset, e_local, inv)
-    rows = perm.clamp(min=0).long()
-    tok = rows // K
-    xs = x.index_select(0, tok)  # rows past the routed count are ignored by the GEMMs
+    # xs[inv[p]] = x[p // K] in one kernel; rows past the routed count stay unset (never read as data)
+    x = x.contiguous()
+    xs = torch.empty(T * K, H, dtype=x.dtype, device=dev)
+    ext().ep_gather_rows(xs, x, inv, K)
     if DECODE and T <= DECODE_MAX_TOKENS and w13.is_contiguous() and w2.is_contiguous():
         out = _fused_experts_decode(x, w13, w2, topk_w, offs, inv, xs, expert_offset)
         if out is not None:

@@ -32,6 +32,7 @@ class WorkerInfo:
     tp: int = 1
     max_model_len: int = 0  # 0 = unknown
     pair: str = ""  # P/D pair pod id: a decode worker takes prefill workers of its own pair first
+    stream_url: str = ""  # the worker's streamer process (token request plane), when it has one
     index: int = -1
     last_seen: float = field(default_factory=time.monotonic)
     num_running: int = 0

@@ -86,6 +86,9 @@ def _batch_dict(outs: list) -> dict:
     return d
 
 
+_RING = object()  # sink marker: the request's outputs go to the streamer ring
+
+
 class _MuxSink:
     """Stands in for a request's asyncio.Queue in AsyncEngine._queues: outputs go to its channel
     (put_nowait runs on the event loop, from AsyncEngine._deliver's one wakeup per step)."""
@@ -178,6 +181,9 @@ class Worker:
         self.ready = True
         self._http = None
         self._channels: dict[str, MuxChannel] = {}
+        self.stream_url: Optional[str] = None  # the streamer process's request plane (attach_streamer)
+        self.loop: Optional[asyncio.AbstractEventLoop] = None
+        self._ring_plane = None
         self.app = self._build_app()
 
     # ---------------------------------------------------------------- engine-thread hook
@@ -265,6 +271,24 @@ class Worker:
         req.submit_time = t_in
         return req
 
+    # ---------------------------------------------------------------- streamer process
+    def attach_streamer(self, cmd_ring, out_ring, stream_url: str) -> None:
+        """The token request plane moves to the streamer process (worker/streamer.py)."""
+        from .streamer import RingPlane
+        self._ring_plane = RingPlane(self, cmd_ring, out_ring)
+        self.stream_url = stream_url
+        self.aeng.attach_ring(self._ring_plane)
+
+    def start_remote_ring(self, rid: str, toks: list, sp: SamplingParams, purl: str, t_in: float) -> None:
+        """Event loop: a streamer request with a prefill URL (disaggregated decode)."""
+        t = asyncio.ensure_future(self._remote_ring(rid, toks, sp, purl, t_in))
+        t.add_done_callback(lambda f: f.cancelled() or f.exception() is None or
+                            log.error("remote prefill of %s failed: %r", rid, f.exception()))
+
+    async def _remote_ring(self, rid: str, toks: list, sp: SamplingParams, purl: str, t_in: float) -> None:
+        if await self._remote_prefill(rid, toks, sp, purl, sink=_RING) is None:  # prefill locally
+            self.aeng.submit_nowait(self._ring_plane.add_local, toks, sp, rid, t_in)
+
     def _abort(self, rid: str) -> bool:
         ent = self.aeng._queues.pop(rid, None)
         if ent is None:
@@ -280,7 +304,10 @@ class Worker:
         req = await self.aeng.submit(self.engine.reserve_remote_prefill, toks, sp, rid)
         if req is None:
             return None
-        if sink is not None:
+        if sink is _RING:
+            self.aeng.own_by_ring(rid)
+            q = sink
+        elif sink is not None:
             self.aeng._queues[rid] = (asyncio.get_running_loop(), sink)
             q = sink
         else:
@@ -484,6 +511,7 @@ class Worker:
 
     @contextlib.asynccontextmanager
     async def _lifespan(self, app):
+        self.loop = asyncio.get_running_loop()
         task = None
         if self.wargs.frontend_url:
             task = asyncio.get_running_loop().create_task(self._heartbeat_loop())
@@ -500,7 +528,7 @@ class Worker:
         return {"worker_id": self.worker_id, "url": self.url, "model": self.model, "role": self.role,
                 "block_size": self.args.block_size, "kv_total_blocks": st.get("kv_total_blocks", 0),
                 "tp": self.args.tensor_parallel_size, "max_model_len": self.args.max_model_len,
-                "pair": os.environ.get("MXS_PAIR_ID", "")}
+                "pair": os.environ.get("MXS_PAIR_ID", ""), "stream_url": self.stream_url}
 
     async def _heartbeat_loop(self) -> None:
         base = self.wargs.frontend_url.rstrip("/")
@@ -549,6 +577,16 @@ def serve(wargs: WorkerArgs) -> None:
     # the switch interval (5 ms by default) while the other runs Python -- a whole decode step at
     # the headline point.  A shorter interval bounds the engine thread's wait.
     sys.setswitchinterval(float(os.environ.get("MXS_GIL_SWITCH_MS", "0.5")) / 1e3)
+    # the token request plane in a streamer process (agg / decode workers), started before anything
+    # here touches the GPU: a fresh interpreter, not a fork of a GPU process
+    streamer = None
+    if wargs.engine.disagg_mode != "prefill" and os.environ.get("MXS_STREAMER", "1") == "1":
+        from .streamer import start_streamer
+        sport = int(os.environ.get("MXS_STREAM_PORT", str(wargs.port + 100)))
+        try:
+            streamer = start_streamer(wargs.host, sport, wargs.engine.max_model_len) + (sport,)
+        except Exception as e:  # noqa: BLE001 - no /dev/shm: the worker serves the plane itself
+            log.warning("streamer process unavailable (%r); serving /mux in the worker", e)
     off = int(os.environ.get("MXS_DEVICE_OFFSET", "0"))
     if off and wargs.engine.resolved_device() == "cuda":  # second worker of a P/D pair pod
         import torch
@@ -558,6 +596,18 @@ def serve(wargs: WorkerArgs) -> None:
         start_tp_group(wargs.engine)
     w = Worker(wargs)
     w.url = advertise_url(wargs, wargs.port)
+    if streamer is not None:
+        proc, cmd_ring, out_ring, sport = streamer
+        w.attach_streamer(cmd_ring, out_ring, advertise_url(wargs, sport))
+        log.info("token request plane: streamer process %d at %s", proc.pid, w.stream_url)
     log.info("worker %s (%s, %s) serving %s on %s", w.worker_id, w.role, w.agent.backend, w.model, w.url)
-    uvicorn.run(w.app, host=wargs.host, port=wargs.port, log_level="warning", access_log=False)
-    w.engine.shutdown()
+    try:
+        uvicorn.run(w.app, host=wargs.host, port=wargs.port, log_level="warning", access_log=False)
+    finally:
+        w.engine.shutdown()
+        if streamer is not None:
+            streamer[0].terminate()
+            try:
+                streamer[0].wait(timeout=10)
+            except Exception:  # noqa: BLE001
+                streamer[0].kill()

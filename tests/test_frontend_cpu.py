@@ -546,3 +546,67 @@ def test_multiprocess_frontend_shares_discovery_and_metrics(tmp_path):
         fe.terminate()
         wk.wait(timeout=20)
         fe.wait(timeout=30)
+
+
+@pytest.fixture(scope="module")
+def streamer_stack():
+    """Agg worker whose token request plane runs in a streamer process (worker/streamer.py)."""
+    from mxserve.worker.streamer import start_streamer
+    from tests.serving_utils import free_port
+    sport = free_port()
+    proc, cmd, out = start_streamer("127.0.0.1", sport, 1024)
+    fe = Frontend(router_mode="kv", ttl=30)
+    fs = Server(fe.app).start()
+    w, ws = _worker(fs.url)
+    w.attach_streamer(cmd, out, f"http://127.0.0.1:{sport}")
+    def up():
+        try:
+            return httpx.get(f"http://127.0.0.1:{sport}/health", timeout=2).status_code == 200
+        except httpx.HTTPError:
+            return False
+    wait_for(up, timeout=60)
+    ws.start()
+    wait_for(lambda: len(fe.registry.list()) == 1)
+    yield fe, fs, w
+    ws.stop()
+    fs.stop()
+    w.aeng.shutdown()
+    proc.terminate()
+    proc.wait(timeout=20)
+
+
+def test_streamer_process_serves_the_token_plane(streamer_stack, agg_stack):
+    """Greedy completions through the streamer process equal the in-worker plane's; streaming
+    works; the worker registered its stream_url and its own /mux channels stay unused."""
+    fe, fs, w = streamer_stack
+    assert fe.registry.list()[0].stream_url.endswith(str(w.stream_url.rsplit(":", 1)[1]))
+    body = {"model": MODEL, "prompt": "same prompt again", "max_tokens": 9, "temperature": 0}
+    a = httpx.post(fs.url + "/v1/completions", json=body, timeout=60).json()
+    b = httpx.post(agg_stack[1].url + "/v1/completions", json=body, timeout=60).json()
+    assert a["choices"][0]["text"] == b["choices"][0]["text"] and a["usage"]["completion_tokens"] == 9
+    chunks = []
+    with httpx.stream("POST", fs.url + "/v1/completions", json=dict(body, stream=True), timeout=60) as r:
+        for line in r.iter_lines():
+            if line.startswith("data: {"):
+                chunks.append(json.loads(line[6:])["choices"][0]["text"])
+    assert "".join(chunks) == a["choices"][0]["text"]
+    assert not w._channels and w._ring_plane is not None and w._ring_plane.dropped == 0
+
+
+def test_streamer_client_disconnect_aborts(streamer_stack):
+    import time
+    fe, fs, w = streamer_stack
+    with httpx.Client(timeout=60) as c:
+        with c.stream("POST", fs.url + "/v1/completions",
+                      json={"model": MODEL, "prompt": "go on", "max_tokens": 400, "stream": True,
+                            "ignore_eos": True}) as r:
+            n = 0
+            for line in r.iter_lines():
+                n += line.startswith("data: {")
+                if n >= 3:
+                    break
+    for _ in range(300):
+        if not w.engine.requests and not w.aeng._queues:
+            break
+        time.sleep(0.02)
+    assert not w.engine.requests and not w.aeng._queues
