@@ -232,10 +232,11 @@ def test_reasoning_parser_fields(agg_stack):
 
 
 @pytest.mark.parametrize("via", ["shm", "host"])
-def test_disaggregated_matches_aggregated(via, monkeypatch):
+@pytest.mark.parametrize("streamer", [False, True])
+def test_disaggregated_matches_aggregated(via, streamer, monkeypatch):
     """Prefill worker + decode worker give the agg result token for token, with the KV moved
     through the decode worker's /dev/shm staging arena (same host) or, without one, in the HTTP
-    body."""
+    body; with the decode worker's token plane in its own or in a streamer process."""
     from mxserve.disagg import kv_transfer
     if via == "host":
         monkeypatch.setattr(kv_transfer, "SHM_BYTES", 0)
@@ -243,6 +244,20 @@ def test_disaggregated_matches_aggregated(via, monkeypatch):
     fs = Server(fe.app).start()
     pw, ps = _worker(fs.url, role="prefill")
     dw, ds = _worker(fs.url, role="decode")
+    sproc = None
+    if streamer:
+        from mxserve.worker.streamer import start_streamer
+        from tests.serving_utils import free_port
+        sport = free_port()
+        sproc, cmd, out = start_streamer("127.0.0.1", sport, 1024)
+        dw.attach_streamer(cmd, out, f"http://127.0.0.1:{sport}")
+
+        def up():
+            try:
+                return httpx.get(f"http://127.0.0.1:{sport}/health", timeout=2).status_code == 200
+            except httpx.HTTPError:
+                return False
+        wait_for(up, timeout=60)
     ps.start()
     ds.start()
     try:
@@ -282,6 +297,9 @@ def test_disaggregated_matches_aggregated(via, monkeypatch):
         dw.aeng.shutdown()
         pw.agent.close()
         dw.agent.close()
+        if sproc is not None:
+            sproc.terminate()
+            sproc.wait(timeout=20)
 
 
 def test_request_trace_by_x_request_id(agg_stack):
