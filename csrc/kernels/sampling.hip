@@ -159,10 +159,134 @@ __global__ void __launch_bounds__(1024) sample_kernel(int64_t* __restrict__ out,
   if (threadIdx.x == 0) out[row] = r.i;
 }
 
+// Register-resident form (bf16 rows up to 2048 * NV logits, 16-byte aligned): the workgroup loads
+// its row ONCE into registers (NV packed bf16 pairs per thread, 8 consecutive logits per 16-byte
+// load), and every bisection pass of the top-k / top-p thresholds, the max / min and the final
+// Gumbel-max run on those registers.  The memory form above re-reads the row (256 KB at a 128k
+// vocab) for each of up to 64 bisection passes.  Element e of a thread is logit
+// 8 (tid + 1024 (e / 8)) + e % 8; slots past V hold -inf and are skipped.
+template <int NV>
+__global__ void __launch_bounds__(1024) sample_reg_kernel(int64_t* __restrict__ out, const bf16_t* __restrict__ logits,
+                                                          int V, long row_stride, const float* __restrict__ temperature,
+                                                          const float* __restrict__ top_p, const int* __restrict__ top_k,
+                                                          const int64_t* __restrict__ seeds,
+                                                          const int64_t* __restrict__ steps) {
+  constexpr int NQ = NV / 4;  // 16-byte loads per thread
+  constexpr int NE = 2 * NV;  // logits per thread
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const bf16_t* z = logits + row * row_stride;
+  uint32_t r[NV];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int v0 = 8 * (tid + 1024 * q);
+    uint4 w = make_uint4(0xFF80FF80u, 0xFF80FF80u, 0xFF80FF80u, 0xFF80FF80u);  // -inf pairs
+    if (v0 < V) w = *reinterpret_cast<const uint4*>(z + v0);
+    r[4 * q] = w.x;
+    r[4 * q + 1] = w.y;
+    r[4 * q + 2] = w.z;
+    r[4 * q + 3] = w.w;
+  }
+  auto val = [&](int e) -> float { return (e & 1) ? bf2f_hi(r[e >> 1]) : bf2f_lo(r[e >> 1]); };
+  // an empty asm "modifying" the packed row at the top of each pass: keeps hipcc from hoisting all
+  // 2 NV unpacked floats out of the bisection loops (loop-invariant), which would spill
+  auto opaque = [&] {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) asm volatile("" : "+v"(r[i]));
+  };
+  auto idx = [&](int e) -> int { return 8 * (tid + 1024 * (e >> 3)) + (e & 7); };
+  const float t = temperature[row];
+  if (!(t > 0.f)) {
+    ArgMax a{-INFINITY, 0x7FFFFFFF};
+#pragma unroll
+    for (int e = 0; e < NE; ++e)
+      if (idx(e) < V) a = better(a, ArgMax{val(e), idx(e)});
+    ArgMax res = block_argmax(a, sv, si);
+    if (tid == 0) out[row] = res.i;
+    return;
+  }
+  const float invt = 1.f / t;
+  const int k = top_k[row];
+  const float p = top_p[row];
+  float thr = -INFINITY;
+  if ((k > 0 && k < V) || p < 1.f) {
+    float mx = -INFINITY, mn = INFINITY;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const float x = val(e);
+      mx = fmaxf(mx, x);
+      if (x != -INFINITY) mn = fminf(mn, x);
+    }
+    mx = block_max(mx, sv);
+    mn = -block_max(-mn, sv);
+    if (k > 0 && k < V) {  // largest tau with count(z >= tau) >= k
+      float lo = mn, hi = mx;
+      for (int it = 0; it < 32; ++it) {
+        const float mid = 0.5f * (lo + hi);
+        float cnt = 0.f;
+        opaque();
+#pragma unroll
+        for (int e = 0; e < NE; ++e) cnt += val(e) >= mid ? 1.f : 0.f;
+        cnt = block_sum(cnt, sv);
+        if (cnt >= static_cast<float>(k)) lo = mid; else hi = mid;
+      }
+      thr = lo;
+    }
+    if (p < 1.f) {  // largest tau with mass(z >= tau) >= p * total, mass in softmax(z / T)
+      float tot = 0.f;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        tot += __expf((val(e) - mx) * invt);
+        __builtin_amdgcn_sched_barrier(0);  // one element at a time: keeps the row in registers
+      }
+      tot = block_sum(tot, sv);
+      float lo = fmaxf(mn, mx - 88.f * t), hi = mx;
+      for (int it = 0; it < 32; ++it) {
+        const float mid = 0.5f * (lo + hi);
+        float mass = 0.f;
+        opaque();
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const float x = val(e);
+          mass += x >= mid ? __expf((x - mx) * invt) : 0.f;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        mass = block_sum(mass, sv);
+        if (mass >= p * tot) lo = mid; else hi = mid;
+      }
+      thr = fmaxf(thr, lo);
+    }
+  }
+  const uint32_t key = hash_u32(static_cast<uint32_t>(static_cast<uint64_t>(seeds[row]) * 0x9E3779B1ull +
+                                                      static_cast<uint64_t>(steps[row])));
+  ArgMax a{-INFINITY, 0x7FFFFFFF};
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const float x = val(e);
+    const int v = idx(e);
+    if (v < V && x >= thr) a = better(a, ArgMax{x * invt + gumbel(key, v), v});
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  ArgMax res = block_argmax(a, sv, si);
+  if (tid == 0) out[row] = res.i;
+}
+
 void launch_sample(int64_t* out, const void* logits, bool bf16, int B, int V, long row_stride,
                    const float* temperature, const float* top_p, const int* top_k, const int64_t* seeds,
                    const int64_t* steps, hipStream_t s) {
   if (B == 0) return;
+  const bool vec = V % 8 == 0 && row_stride % 8 == 0 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0;
+  if (bf16 && vec && V <= 2048 * 64) {
+    if (V <= 2048 * 16)
+      hipLaunchKernelGGL(sample_reg_kernel<16>, dim3(B), dim3(1024), 0, s, out, static_cast<const bf16_t*>(logits), V,
+                         row_stride, temperature, top_p, top_k, seeds, steps);
+    else
+      hipLaunchKernelGGL(sample_reg_kernel<64>, dim3(B), dim3(1024), 0, s, out, static_cast<const bf16_t*>(logits), V,
+                         row_stride, temperature, top_p, top_k, seeds, steps);
+    MXS_CHECK_LAUNCH();
+    return;
+  }
   if (bf16)
     hipLaunchKernelGGL(sample_kernel<bf16_t>, dim3(B), dim3(1024), 0, s, out, static_cast<const bf16_t*>(logits), V,
                        row_stride, temperature, top_p, top_k, seeds, steps);

@@ -259,10 +259,12 @@ def test_sample_greedy(gpu, dtype, V):
     assert int(ids[3]) == 77
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype,V", [(torch.float32, 32000), (torch.bfloat16, 32000), (torch.bfloat16, 128256)])
 @pytest.mark.parametrize("top_p,top_k", [(1.0, 0), (0.9, 0), (1.0, 50), (0.8, 20)])
-def test_sample_matches_reference(gpu, top_p, top_k, dtype):
-    B, V = 24, 32000
+def test_sample_matches_reference(gpu, top_p, top_k, dtype, V):
+    """bf16 rows take the register-resident kernel (row loaded once, bisection passes on registers;
+    V = 32000 pads the last 16-byte slots), fp32 rows the memory form."""
+    B = 24
     logits = (torch.randn(B, V, device=gpu) * 3).to(dtype)
     t = torch.full((B,), 0.7, device=gpu)
     tp = torch.full((B,), top_p, device=gpu)
@@ -736,3 +738,26 @@ def test_prefill_gemm_tuner_and_dispatch(gpu, monkeypatch):
     assert len(calls) == sum(r["chosen"] == "mfma" for r in rows)
     x = torch.randn(1000, 2048, device=gpu, dtype=torch.bfloat16)  # above PREFILL_MAX_M: hipBLASLt
     _close(ops.linear(x, w), x.float() @ w.float().t(), 2e-2, 2e-2, "prefill linear M=1000")
+
+
+def test_sample_top_p_rate(gpu):
+    """Top-k / top-p sampling at a serving batch (384 rows x 128k vocab, bf16): the register-resident
+    kernel keeps it to a small fraction of a decode step."""
+    B, V = 384, 128256
+    logits = (torch.randn(B, V, device=gpu) * 3).to(torch.bfloat16)
+    t = torch.full((B,), 0.8, device=gpu)
+    tp = torch.full((B,), 0.9, device=gpu)
+    tk = torch.full((B,), 40, dtype=torch.int32, device=gpu)
+    seeds = torch.arange(B, device=gpu)
+    steps = torch.zeros(B, dtype=torch.int64, device=gpu)
+    ops.sample(logits, t, tp, tk, seeds, steps)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        ops.sample(logits, t, tp, tk, seeds, steps)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 5
+    print(f"top-k 40 + top-p 0.9 sampling, 384 x 128256 bf16: {ms:.3f} ms")
+    assert ms < 2.0
