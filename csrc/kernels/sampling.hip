@@ -6,6 +6,8 @@
 //                              graph-capturable, no RNG state).  No sort: the top-k and top-p
 //                              thresholds are found by bisection over value with block reductions.
 // The hash matches mxserve/ops/reference.py::_hash_u32 bit for bit.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace mxs {
@@ -277,7 +279,11 @@ void launch_sample(int64_t* out, const void* logits, bool bf16, int B, int V, lo
                    const int64_t* steps, hipStream_t s) {
   if (B == 0) return;
   const bool vec = V % 8 == 0 && row_stride % 8 == 0 && (reinterpret_cast<uintptr_t>(logits) & 15) == 0;
-  if (bf16 && vec && V <= 2048 * 64) {
+  static const bool reg_ok = [] {  // MXS_SAMPLE_REG=0: the memory form (A/B measurements)
+    const char* e = std::getenv("MXS_SAMPLE_REG");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (reg_ok && bf16 && vec && V <= 2048 * 64) {
     if (V <= 2048 * 16)
       hipLaunchKernelGGL(sample_reg_kernel<16>, dim3(B), dim3(1024), 0, s, out, static_cast<const bf16_t*>(logits), V,
                          row_stride, temperature, top_p, top_k, seeds, steps);
