@@ -133,7 +133,8 @@ class MuxClient:
     async def ensure(self, sess) -> None:
         if self.task is None or self.task.done():
             self.ready = asyncio.get_running_loop().create_future()
-            self.task = asyncio.ensure_future(self._read(sess, self.ready))
+            self.queues = {}  # this channel's requests (the old channel fails only its own)
+            self.task = asyncio.ensure_future(self._read(sess, self.ready, self.queues))
         await asyncio.wait_for(asyncio.shield(self.ready), self.HELLO_TIMEOUT)
 
     def reset(self) -> None:
@@ -141,7 +142,7 @@ class MuxClient:
             self.task.cancel()
         self.task = None
 
-    async def _read(self, sess, ready: asyncio.Future) -> None:
+    async def _read(self, sess, ready: asyncio.Future, queues: dict) -> None:
         err: BaseException = ConnectionError(f"request channel to {self.url} closed")
         try:
             async with sess.post(self.url + "/mux", json={"sid": self.sid}) as r:
@@ -150,7 +151,6 @@ class MuxClient:
                 if r.status != 200:
                     raise ConnectionError(f"request channel to {self.url}: HTTP {r.status}")
                 buf = b""
-                queues = self.queues
                 async for data in r.content.iter_any():
                     buf += data
                     *lines, buf = buf.split(b"\n")
@@ -175,9 +175,9 @@ class MuxClient:
         finally:
             if not ready.done():
                 ready.set_exception(err)
-            for q in self.queues.values():
+            for q in queues.values():
                 q.put_nowait(err)
-            self.queues.clear()
+            queues.clear()
 
 
 class APIError(Exception):
@@ -371,11 +371,19 @@ class Frontend:
         mc.queues[rid] = q
         done = False
         try:
-            async with sess.post(mc.url + "/submit", json=dict(body, sid=mc.sid)) as r:
-                if r.status == 404:  # the worker no longer knows this channel (restarted): reopen
+            for attempt in range(2):
+                async with sess.post(mc.url + "/submit", json=dict(body, sid=mc.sid)) as r:
+                    status = r.status
+                if status == 404 and attempt == 0:  # the worker restarted and lost this channel: reopen
+                    mc.queues.pop(rid, None)
                     mc.reset()
-                if r.status != 200:
-                    raise ConnectionError(f"submit to {mc.url} returned {r.status}")
+                    await mc.ensure(sess)
+                    q = asyncio.Queue()
+                    mc.queues[rid] = q
+                    continue
+                if status != 200:
+                    raise ConnectionError(f"submit to {mc.url} returned {status}")
+                break
             while True:
                 item = await q.get()
                 if isinstance(item, BaseException):

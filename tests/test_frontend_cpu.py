@@ -628,3 +628,35 @@ def test_streamer_client_disconnect_aborts(streamer_stack):
             break
         time.sleep(0.02)
     assert not w.engine.requests and not w.aeng._queues
+
+
+def test_mux_channel_reconnects_after_worker_restart():
+    """The frontend's channel to a worker breaks when the worker restarts on the same address; the
+    next request opens a new channel (the worker answers /submit for an unknown channel with 404,
+    or the dead reader is noticed first) and completes."""
+    from tests.serving_utils import free_port
+    fe = Frontend(router_mode="round_robin", ttl=30)
+    fs = Server(fe.app).start()
+    port = free_port()
+    body = {"model": MODEL, "prompt": "restart me", "max_tokens": 5, "temperature": 0}
+    w1, _ = _worker(None)
+    s1 = Server(w1.app, port=port).start()
+    from mxserve.router.router import WorkerInfo
+    fe.registry.register(WorkerInfo(worker_id="w", url=s1.url, model=MODEL))
+    try:
+        a = httpx.post(fs.url + "/v1/completions", json=body, timeout=60).json()
+        assert a["usage"]["completion_tokens"] == 5
+        s1.stop()
+        w1.aeng.shutdown()
+        w2, _ = _worker(None)
+        s2 = Server(w2.app, port=port).start()
+        try:
+            b = httpx.post(fs.url + "/v1/completions", json=body, timeout=60)
+            assert b.status_code == 200, b.text
+            assert b.json()["choices"][0]["text"] == a["choices"][0]["text"]
+            assert w2._channels  # a new channel was opened on the restarted worker
+        finally:
+            s2.stop()
+            w2.aeng.shutdown()
+    finally:
+        fs.stop()
