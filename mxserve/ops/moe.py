@@ -65,20 +65,20 @@ def _fused_experts_loop(x, w13, w2, topk_w, topk_ids, expert_offset):
     ids = topk_ids.to(torch.int32).contiguous()
     offs = torch.empty(e_local + 1, dtype=torch.int32, device=x.device)
     perm = torch.empty(T * K, dtype=torch.int32, device=x.device)
-    ext().moe_align(offs, perm, ids, expert_offset, e_local)
-    o = offs.tolist()
-    rows = perm[:o[-1]].long()
-    tok = rows // K
-    xs = x.index_select(0, tok)
-    ys = torch.empty(o[-1], H, dtype=x.dtype, device=x.device)
+    inv = torch.empty(T * K, dtype=torch.int32, device=x.device)
+    ext().moe_align(offs, perm, ids, expert_offset, e_local, inv)
+    o = offs.tolist()  # prefill runs eagerly: one host sync for the per-expert slices
+    x = x.contiguous()
+    xs = torch.empty(max(o[-1], 1), H, dtype=x.dtype, device=x.device)
+    ext().ep_gather_rows(xs, x, inv, K)  # xs[inv[p]] = x[p // K]
+    ys = torch.empty(max(o[-1], 1), H, dtype=x.dtype, device=x.device)
     for e in range(e_local):
         a, b = o[e], o[e + 1]
         if b > a:
             ys[a:b] = F.linear(_silu_mul(F.linear(xs[a:b], w13[e])), w2[e])
-    wts = topk_w.reshape(-1).index_select(0, rows).unsqueeze(1)
-    out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
-    out.index_add_(0, tok, ys.float() * wts)
-    return out.to(x.dtype)
+    out = torch.empty(T, H, dtype=x.dtype, device=x.device)
+    ext().moe_combine(out, ys, topk_w.float().contiguous(), inv)  # K17: weighted sum, fp32, one write
+    return out
 
 
 # measured at graph capture (tune()): (H, I, E_local, top_k) -> sorted [(T bucket, cfg13, cfg2)];

@@ -428,8 +428,9 @@ def test_moe_combine(gpu):
     _close(out, exp, 0.02, 0.01, "moe_combine")
 
 
-@pytest.mark.parametrize("T", [64, 300])
+@pytest.mark.parametrize("T", [64, 300, 700])
 def test_moe_experts_gpu_vs_ref(gpu, T):
+    """T = 700 takes the prefill path (per-expert hipBLASLt over gathered rows, K17 combine)."""
     H, I, E, K = 256, 192, 4, 2
     x = torch.randn(T, H, device=gpu, dtype=torch.bfloat16)
     w13 = torch.randn(E, 2 * I, H, device=gpu, dtype=torch.bfloat16) * 0.05
