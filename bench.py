@@ -305,7 +305,8 @@ def run_disagg_decode(a, eng, sp, drv, barrier, agree, conn) -> float:
     # the prefill rank maps the arena now, while this rank idles in a plain socket wait
     ack = conn.recv()
     assert ack[0] == "mapped", ack
-    vlog("decode arena mapped by the prefill rank")
+    arena = bool(ack[1]) if len(ack) > 1 else True
+    vlog(f"decode arena mapped by the prefill rank: {arena}")
     bs = eng.args.block_size
     backlog: list = []
     inflight: dict = {}
@@ -322,16 +323,20 @@ def run_disagg_decode(a, eng, sp, drv, barrier, agree, conn) -> float:
                 break
             skip = req.num_cached_tokens // bs
             dst = list(req.block_ids[skip:-(-len(toks) // bs)])
-            start = agent.acquire(len(dst))  # None: host-staged transfer for this request
+            # GPU arena extent over xGMI, else the page-locked /dev/shm arena, else the pipe
+            start = agent.acquire(len(dst)) if arena else None
+            shm_start = agent.acquire_shm(len(dst)) if start is None else None
             backlog.pop(0)
-            conn.send(("prefill", rid, toks, dst, skip, start))
-            inflight[rid] = (dst, start)
+            conn.send(("prefill", rid, toks, dst, skip, start, shm_start))
+            inflight[rid] = (dst, start, shm_start)
         now = time.perf_counter()
         while conn.poll():
             _, rid, tok, data = conn.recv()
-            dst, start = inflight.pop(rid)
+            dst, start, shm_start = inflight.pop(rid)
             if start is not None:  # staging extent -> pool blocks, ordered before the next step
                 agent.land(start, dst)
+            elif shm_start is not None:
+                agent.land_shm(shm_start, dst)
             elif data is not None:  # host-staged transfer
                 agent.write_blocks(dst, data)
             out = eng.complete_remote_prefill(rid, tok)
@@ -357,10 +362,15 @@ def run_disagg_prefill(eng, temperature: float, barrier, conn) -> int:
     agent = KVTransferAgent(eng.runner, "xgmi")
     kind, target = conn.recv()
     assert kind == "desc", kind
+    arena = False
     if agent.backend == "xgmi" and target["backend"] == "xgmi":
-        agent.connect(target)
-    conn.send(("mapped",))
-    vlog(f"prefill rank serving (decode arena backend {target['backend']})")
+        try:
+            agent.connect(target)
+            arena = True
+        except (RuntimeError, OSError) as e:  # the decode GPU's arena cannot be mapped here
+            vlog(f"decode arena not mappable ({e!r}); KV goes through the /dev/shm arena")
+    conn.send(("mapped", arena))
+    vlog(f"prefill rank serving (decode arena backend {target['backend']}, mapped={arena})")
     pending: dict = {}
     moved = 0
     while True:
@@ -372,10 +382,10 @@ def run_disagg_prefill(eng, temperature: float, barrier, conn) -> int:
                 barrier()
                 stop = msg[1] == "stop"
                 continue
-            _, rid, toks, dst, skip, start = msg
+            _, rid, toks, dst, skip, start, shm_start = msg
             eng.add_request(toks, SamplingParams(max_tokens=1, temperature=temperature, ignore_eos=True),
                             request_id=rid, disagg_role="prefill_only")
-            pending[rid] = (dst, skip, start)
+            pending[rid] = (dst, skip, start, shm_start)
         if stop:
             agent.close()
             return moved
@@ -385,11 +395,13 @@ def run_disagg_prefill(eng, temperature: float, barrier, conn) -> int:
         for o in eng.step():
             if not o.finished or o.request_id not in pending:
                 continue
-            dst, skip, start = pending.pop(o.request_id)
+            dst, skip, start, shm_start = pending.pop(o.request_id)
             src = list(eng.requests[o.request_id].block_ids[skip:skip + len(dst)])
             data = None
             if start is not None:
                 agent.push_xgmi(src, target, start)
+            elif shm_start is not None:
+                agent.push_shm(src, target, shm_start)
             else:
                 data = agent.read_blocks(src)
             moved += len(src)
