@@ -66,6 +66,7 @@ class RingPlane:
         self.cmd = cmd_ring
         self.out = out_ring
         self.dropped = 0
+        self.dead = False  # the streamer stopped reading: drop outputs instead of stalling the engine
 
     def poll(self, timeout: float):
         data = self.cmd.pop(0, timeout)
@@ -112,9 +113,13 @@ class RingPlane:
             self.emit_tuples(tuples[:half])
             self.emit_tuples(tuples[half:])
             return
-        if not self.out.push(data, 2.0):
+        if self.dead:
             self.dropped += 1
-            log.error("streamer output ring full for 2 s (streamer gone?); %d step(s) dropped", self.dropped)
+            return
+        if not self.out.push(data, 0.5):
+            self.dropped += 1
+            self.dead = True  # one stall, then never again: the engine keeps its step rate
+            log.error("streamer output ring full for 0.5 s (streamer process gone?); dropping its outputs")
 
 
 def start_streamer(host: str, port: int, max_prompt_tokens: int) -> tuple:
@@ -125,7 +130,7 @@ def start_streamer(host: str, port: int, max_prompt_tokens: int) -> tuple:
     tag = f"{os.getpid()}-{uuid.uuid4().hex[:8]}"
     cmd_name, out_name = f"/mxs-cmd-{tag}", f"/mxs-out-{tag}"
     cmd_slot = max(64 << 10, 8 * int(max_prompt_tokens) + 4096)
-    cmd = rt.ShmRing(cmd_name, True, cmd_slot, 16, 1)
+    cmd = rt.ShmRing(cmd_name, True, cmd_slot, 64, 1)  # a burst of submits between two engine steps
     out = rt.ShmRing(out_name, True, _OUT_SLOT, 32, 1)
     env = dict(os.environ)
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
