@@ -255,6 +255,11 @@ def timed_phases(a, step, barrier, agree, drv, running, on_phase=lambda phase: N
 
 
 def run_agg(a, eng, sp, drv, barrier, agree) -> float:
+    def admit():  # late admission (engine/pacing.py): arrivals due by the time the next step is scheduled
+        for rid, toks in drv.due():
+            eng.add_request(toks, sp, request_id=rid)
+    eng.admit_hook = admit
+
     def step():
         for rid, toks in drv.due():
             eng.add_request(toks, sp, request_id=rid)
@@ -525,6 +530,10 @@ def phase_agg(a, ctx) -> tuple:
             "preemptions": eng.stats()["num_preemptions"], "model": args.model,
             "kv_cache_dtype": "fp8_e4m3fn" if eng.runner.kv_fp8 else ("bf16" if ctx.on_gpu else "fp32"),
             "isl": isl, "osl": osl}
+    la = getattr(eng, "_late", None)
+    if la is not None:  # engine/pacing.py: how often the host waited for a late admission, and how long
+        info["late_admission"] = {"waits": la.waits, "mean_wait_ms": round(1e3 * la.wait_s / max(1, la.waits), 3),
+                                  "model_updates": la.model.n, "host_lead_ms": round(1e3 * la.host_lead, 3)}
     host = None
     if eng.step_times is not None and eng.step_times["steps"]:
         n = eng.step_times["steps"]
@@ -638,6 +647,8 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
     if dis is not None:
         line["disagg"] = dis
     line["engine"] = {"kv_blocks": info["kv_blocks"], "preemptions": info["preemptions"], "graphs": info["graphs"]}
+    if "late_admission" in info:
+        line["engine"]["late_admission"] = info["late_admission"]
     return line
 
 

@@ -54,6 +54,14 @@ class LLMEngine:
         self.check_invariants = False
         # async scheduling: the launched-but-not-collected step (scheduler output, runner handle)
         self.async_scheduling = bool(args.async_scheduling)
+        # late admission (engine/pacing.py): async steps on the GPU only, and only when the serving
+        # layer provides an admit hook (AsyncEngine, bench.py)
+        self.admit_hook = None
+        self._late = None
+        if (self.async_scheduling and self.runner.is_gpu and
+                os.environ.get("MXS_LATE_ADMISSION", "1") == "1"):
+            from .pacing import LateAdmission
+            self._late = LateAdmission()
         self._inflight: Optional[tuple] = None
         self.profiler = StepProfiler()  # MXS_TORCH_PROFILE="start:count:path"
         # MXS_STEP_TIMING=1: host seconds per phase (schedule / launch / collect wait / land)
@@ -129,6 +137,11 @@ class LLMEngine:
 
     def _step(self) -> list[StepOutput]:
         tm = self.step_times
+        late = self._late
+        if late is not None and self._inflight is not None and self.admit_hook is not None:
+            late.wait(self._inflight[1].get("ev"))  # until the in-flight step is nearly done
+            self.admit_hook()  # requests that arrived meanwhile join the step launched next
+        t_adm = time.perf_counter()
         t0 = time.perf_counter() if tm is not None else 0.0
         so = self.scheduler.schedule()
         if tm is not None:
@@ -147,6 +160,12 @@ class LLMEngine:
         if tm is not None:
             t2 = time.perf_counter()
             tm["launch"] += t2 - t1
+        done_state = None
+        if late is not None:
+            if handle is not None:
+                late.launched(so, t_adm, time.perf_counter())
+            done_state = late.inflight
+            late.rotate()
         if self.async_scheduling:
             done, self._inflight = self._inflight, ((so, handle) if handle is not None else None)
         else:
@@ -154,7 +173,15 @@ class LLMEngine:
         if done is None:
             return []
         dso, dh = done
-        sampled = self.runner.collect(dh)
+        if late is not None:
+            ev = dh.get("ev")
+            pending = ev is not None and not ev.query()
+            sampled = self.runner.collect(dh)
+            t_done = done_state.get("done") if done_state else None
+            late.observe_done(done_state, t_done if t_done is not None else
+                              (time.perf_counter() if pending else None))
+        else:
+            sampled = self.runner.collect(dh)
         if tm is None:
             return self._land(dso, sampled, dh.get("logprobs"))
         t3 = time.perf_counter()
@@ -223,6 +250,7 @@ class AsyncEngine:
         self.on_step = None  # optional callback(list[StepOutput]) run on the engine thread
         self._ring = None  # (cmd ring, out ring, handler): a streamer process owns the request plane
         self.last_stats: dict = engine.stats()
+        engine.admit_hook = self._admit  # late admission: arrivals up to the last moment join the next step
         self._thread = threading.Thread(target=self._loop, name="mxs-engine", daemon=True)
         self._thread.start()
 
@@ -239,6 +267,12 @@ class AsyncEngine:
                     loop.call_soon_threadsafe(_set_result, fut, None, e)
                 else:
                     log.exception("engine command failed")
+
+    def _admit(self) -> None:
+        """Engine thread, right before a step is scheduled: run the commands that arrived since."""
+        self._drain()
+        if self._ring is not None:
+            self._drain_ring(0.0)
 
     def _loop(self) -> None:
         while not self._stop:

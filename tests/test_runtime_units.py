@@ -402,3 +402,45 @@ def test_chat_template_from_tokenizer_config(tmp_path, form):
     load_hf_template.cache_clear()
     with pytest.raises(ValueError, match="alternate"):
         render("llama3", msgs, str(bad))
+
+
+def test_step_time_model_learns_step_composition():
+    """The late-admission predictor fits a step's GPU time from its composition."""
+    import numpy as np
+    from mxserve.engine.pacing import StepTimeModel
+    m = StepTimeModel(lam=0.99, warmup=10)
+    rng = np.random.default_rng(0)
+    true = np.array([0.002, 0.0025, 0.001, 0.004, 0.0005])
+    for _ in range(200):
+        x = np.array([1.0, rng.uniform(0, 8), rng.uniform(0, 3), rng.uniform(0, 3), rng.uniform(0, 9)])
+        m.update(x, float(x @ true))
+    x = np.array([1.0, 4.0, 0.8, 2.0, 8.5])
+    assert abs(m.predict(x) - float(x @ true)) < 1e-4
+
+
+def test_late_admission_wait_stops_at_target_or_completion():
+    import time
+    from mxserve.engine.pacing import LateAdmission
+
+    class Ev:
+        def __init__(self, t_done):
+            self.t_done = t_done
+
+        def query(self):
+            return time.perf_counter() >= self.t_done
+
+    la = LateAdmission()
+    la.host_lead, la.margin = 0.001, 0.0
+    now = time.perf_counter()
+    la.inflight = {"x": None, "t_launch": now, "est_done": now + 0.02, "done": None}
+    t0 = time.perf_counter()
+    la.wait(Ev(now + 1.0))  # predicted done in 20 ms: wake ~1 ms before
+    assert 0.015 <= time.perf_counter() - t0 < 0.05 and la.inflight["done"] is None
+    now = time.perf_counter()
+    la.inflight = {"x": None, "t_launch": now, "est_done": now + 0.5, "done": None}
+    t0 = time.perf_counter()
+    la.wait(Ev(now + 0.01))  # finishes early: proceed at once, completion time recorded
+    assert time.perf_counter() - t0 < 0.1 and la.inflight["done"] is not None
+    la.inflight = {"x": None, "t_launch": now, "est_done": now + 0.5, "done": None}
+    la.wait(Ev(0.0))  # already done when looked at: no wait, completion time unknown
+    assert la.inflight["done"] is None
