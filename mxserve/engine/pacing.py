@@ -17,6 +17,7 @@ times observed whenever the host sees a step finish (see LLMEngine._step).
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Optional
 
@@ -71,7 +72,8 @@ class LateAdmission:
     def __init__(self):
         self.model = StepTimeModel()
         self.host_lead = 1.5e-3  # EMA of admit -> launched host time
-        self.margin = float(__import__("os").environ.get("MXS_LATE_ADMISSION_MARGIN_MS", "1.5")) / 1e3
+        # slack for the prediction error: admitting this much earlier than the host lead requires
+        self.margin = float(os.environ.get("MXS_LATE_ADMISSION_MARGIN_MS", "1.5")) / 1e3
         self.inflight: Optional[dict] = None  # {"x", "t_launch", "est_done", "done"}
         self.last_done: Optional[float] = None  # observed completion of the previous step
         self.waits = 0
