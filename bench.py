@@ -533,7 +533,8 @@ def phase_agg(a, ctx) -> tuple:
     la = getattr(eng, "_late", None)
     if la is not None:  # engine/pacing.py: how often the host waited for a late admission, and how long
         info["late_admission"] = {"waits": la.waits, "mean_wait_ms": round(1e3 * la.wait_s / max(1, la.waits), 3),
-                                  "model_updates": la.model.n, "host_lead_ms": round(1e3 * la.host_lead, 3)}
+                                  "model_updates": la.model.n, "host_lead_ms": round(1e3 * la.host_lead, 3),
+                                  "late_wakes": la.late, "margin_ms": round(1e3 * la.margin, 3)}
     host = None
     if eng.step_times is not None and eng.step_times["steps"]:
         n = eng.step_times["steps"]

@@ -221,6 +221,10 @@ class LLMEngine:
     def stats(self) -> dict:
         s = self.scheduler.stats()
         s.update(num_steps=self.num_steps, num_generated=self.num_generated, **self.runner.kv_stats())
+        la = self._late
+        if la is not None:
+            s["late_admission"] = {"waits": la.waits, "late_wakes": la.late, "margin_ms": round(1e3 * la.margin, 3),
+                                   "host_lead_ms": round(1e3 * la.host_lead, 3), "model_updates": la.model.n}
         return s
 
     def shutdown(self) -> None:

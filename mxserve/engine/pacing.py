@@ -74,6 +74,8 @@ class LateAdmission:
         self.host_lead = 1.5e-3  # EMA of admit -> launched host time
         # slack for the prediction error: admitting this much earlier than the host lead requires
         self.margin = float(os.environ.get("MXS_LATE_ADMISSION_MARGIN_MS", "1.5")) / 1e3
+        self.margin_min = self.margin
+        self.late = 0  # waits the step outlasted (GPU done before the host admitted)
         self.inflight: Optional[dict] = None  # {"x", "t_launch", "est_done", "done"}
         self.last_done: Optional[float] = None  # observed completion of the previous step
         self.waits = 0
@@ -88,12 +90,21 @@ class LateAdmission:
         t0 = now = time.perf_counter()
         if ev is not None and ev.query():  # already done when we looked: completion time unknown
             return
+        finished = False
         while now < target:
             if ev is not None and ev.query():  # seen finishing: a completion time within one poll
                 st["done"] = now
+                finished = True
                 break
             time.sleep(min(2e-4, target - now))
             now = time.perf_counter()
+        # margin control (AIMD): the GPU finishing before the host admits means it idles for the
+        # host's schedule + launch time -- widen the slack at once; shrink it slowly while on time
+        if finished or (ev is not None and ev.query()):
+            self.late += 1
+            self.margin = min(self.margin + 5e-4, 8e-3)
+        else:
+            self.margin = max(self.margin - 2e-5, self.margin_min)
         self.waits += 1
         self.wait_s += time.perf_counter() - t0
 

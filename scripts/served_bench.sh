@@ -38,6 +38,7 @@ B=$!
   done ) > "$OUT/cpu_fe_worker_client.txt" &
 wait "$B"
 curl -sf "http://127.0.0.1:$FE_PORT/metrics" > "$OUT/frontend_metrics.txt" || true
+curl -sf "http://127.0.0.1:$W_PORT/stats" > "$OUT/worker_stats.json" || true
 # request traces (per frontend process: a few fetches land on different processes)
 for i in 1 2 3 4 5 6 7 8; do curl -sf "http://127.0.0.1:$FE_PORT/debug/traces?n=300" > "$OUT/traces_$i.json" || true; done
 python3 - "$OUT" <<'PY'
