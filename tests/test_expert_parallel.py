@@ -44,7 +44,7 @@ def _run(rank, world, port, Ts, layout, q):
         h = torch.randn(T, H, generator=torch.Generator().manual_seed(T))
         out = moe_a2a(h, gate, w13[rank * el:(rank + 1) * el], w2[rank * el:(rank + 1) * el], K, rank, world,
                       dist.group.WORLD, force_layout=layout)
-        res.append(out)
+        res.append(out.numpy())  # by value: a shared-fd tensor dies with this process
     q.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
@@ -68,7 +68,7 @@ def test_moe_a2a_matches_reference(world, layout):
         h = torch.randn(T, H, generator=torch.Generator().manual_seed(T))
         want = _reference(h)
         for r in range(world):
-            torch.testing.assert_close(got[r][i], want, rtol=1e-4, atol=1e-4)
+            torch.testing.assert_close(torch.from_numpy(got[r][i]), want, rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("layout", ["fixed", "variable"])
