@@ -530,6 +530,11 @@ def phase_agg(a, ctx) -> tuple:
             "preemptions": eng.stats()["num_preemptions"], "model": args.model,
             "kv_cache_dtype": "fp8_e4m3fn" if eng.runner.kv_fp8 else ("bf16" if ctx.on_gpu else "fp32"),
             "isl": isl, "osl": osl}
+    rep = getattr(eng.runner, "decode_gemm_report", None)
+    if rep:  # capture-time choice per (bucket, projection): hand-written MFMA kernels vs hipBLASLt
+        info["decode_gemm"] = {"pairs": len(rep), "hand_written": sum(r["chosen"] == "mfma" for r in rep),
+                               "mt_kernel": sum(bool(r["cfg"]) and r["cfg"][0] == "mt" for r in rep),
+                               "tune_s": round(getattr(eng.runner, "decode_gemm_tune_s", 0.0), 1)}
     la = getattr(eng, "_late", None)
     if la is not None:  # engine/pacing.py: how often the host waited for a late admission, and how long
         info["late_admission"] = {"waits": la.waits, "mean_wait_ms": round(1e3 * la.wait_s / max(1, la.waits), 3),
@@ -648,8 +653,9 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
     if dis is not None:
         line["disagg"] = dis
     line["engine"] = {"kv_blocks": info["kv_blocks"], "preemptions": info["preemptions"], "graphs": info["graphs"]}
-    if "late_admission" in info:
-        line["engine"]["late_admission"] = info["late_admission"]
+    for k in ("late_admission", "decode_gemm"):
+        if k in info:
+            line["engine"][k] = info[k]
     return line
 
 

@@ -32,6 +32,8 @@ void launch_moe_align(int*, int*, const int*, int, int, int, int*, hipStream_t);
 void launch_moe_combine(bf16_t*, const bf16_t*, const float*, const int*, int, int, int, hipStream_t);
 bool launch_decode_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int,
                         int, hipStream_t, const int* = nullptr, int = 0, int = 0, int = 0);
+bool launch_mt_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int, int,
+                    int, hipStream_t, int*, int);
 bool launch_prefill_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int,
                          hipStream_t);
 bool launch_moe_grouped_gemm(bf16_t*, const bf16_t*, const bf16_t*, const int*, int, int, int, int, int, bool,
@@ -237,6 +239,35 @@ bool decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::T
                                  epi, stream(), nullptr, 0, 0, lu);
 }
 
+// Medium-M form of the decode projection (gemm_decode.hip mt_gemm_kernel, M = 64-256 and short
+// prefill chunks): WM x WN waves of 32 MR rows x 32 WNF weight rows, same epilogues and workspace rule
+// as decode_gemm; with `cnt` (int32 tile counters, zeroed once, left zero by every launch) the split-K
+// slabs are summed inside the launch.  False if the configuration does not tile the shape.
+bool mt_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> part, int64_t wm, int64_t wn,
+             int64_t mr, int64_t wnf, int64_t splitk, int64_t epi, c10::optional<at::Tensor> cnt) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == (epi == 1 ? N / 2 : N), "shape mismatch");
+  TORCH_CHECK(epi == 0 || epi == 1, "epi 0 (none) | 1 (silu*mul)");
+  if (x.stride(1) != 1 || out.stride(1) != 1) return false;
+  float* p = nullptr;
+  if (splitk > 1) {
+    TORCH_CHECK(part.has_value() && part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->numel() >= splitk * M * N, "split-K needs an fp32 workspace of splitk * M * N");
+    p = part->data_ptr<float>();
+  }
+  int* c = nullptr;
+  int clen = 0;
+  if (cnt.has_value()) {
+    TORCH_CHECK(cnt->is_cuda() && cnt->scalar_type() == at::kInt && cnt->is_contiguous(), "cnt: int32 CUDA tensor");
+    c = cnt->data_ptr<int>();
+    clen = static_cast<int>(std::min<int64_t>(cnt->numel(), 1 << 30));
+  }
+  return mxs::launch_mt_gemm(bf(out), p, bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), wm, wn, mr, wnf, splitk,
+                             epi, stream(), c, clen);
+}
+
 // K05-K08 at prefill sizes (csrc/kernels/gemm_prefill.hip): out [M, N] = x [M, K] . w [N, K]^T.
 // bm in {64, 128}; splitk > 1 needs an fp32 workspace of splitk * M * N.  False if unsupported.
 bool prefill_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> part, int64_t bm,
@@ -365,6 +396,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("decode_gemm", &decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("part"), pybind11::arg("mf"), pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"),
         pybind11::arg("epi"), pybind11::arg("lu") = 0);
+  m.def("mt_gemm", &mt_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("part"),
+        pybind11::arg("wm"), pybind11::arg("wn"), pybind11::arg("mr"), pybind11::arg("wnf"), pybind11::arg("splitk"),
+        pybind11::arg("epi"), pybind11::arg("cnt") = pybind11::none());
   m.def("prefill_gemm", &prefill_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("part"), pybind11::arg("bm"), pybind11::arg("splitk"));
   m.def("moe_decode_gemm", &moe_decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),

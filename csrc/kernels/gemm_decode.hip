@@ -320,6 +320,269 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Medium-M form ("mt"): decode batches of 64-256 rows (and short prefill chunks), where the weight
+// bytes no longer dominate the on-chip traffic: at M = 256 every weight element feeds 512 FLOP, so
+// the MFMA pipe, the LDS read port and the L2 re-reads of X all matter (cdna_hip_programming.md §5,
+// "Projection GEMM at M = 256").  The kernel above re-streams W once per 64-row tile and reads
+// fragment-shaped pieces (16 rows x 64 B per instruction) straight into registers; this one:
+//
+//   * covers up to all 256 rows in ONE workgroup (WM x WN waves, each 32 MR rows x 32 WNF weight
+//     rows = output columns), so each W element is read from HBM once per row tile and shared by the
+//     WM waves through LDS;
+//   * v_mfma_f32_32x32x16_bf16 (A = 32 W rows, B = X^T with 32 tokens), MR x WNF accumulator tiles
+//     per wave: MR + WNF fragment reads feed MR x WNF MFMAs, which keeps the LDS read port (256 B/clk
+//     per CU: 2 KB of fresh operands per 32-cycle MFMA would saturate it) below the MFMA pipe;
+//   * the fragment reads of k-step s + 1 are issued before the MFMAs of step s (counted lgkmcnt);
+//   * stages both operands with global_load_lds_dwordx4 in full 128-byte lines (8 rows x 128 B per
+//     wave instruction, no VGPRs, no ds_write pass) into a ring of as many 64-k stages as the LDS
+//     holds (3-6), one raw s_barrier per k-group, counted vmcnt waits;
+//   * the 16-byte chunks of a row are XOR-swizzled by (row >> 1) & 7 on the SOURCE address (the
+//     LDS image stays lane-linear, as the DMA writes it) and un-swizzled on the ds_read_b128, so the
+//     16 lanes of a read group (16 rows, one chunk) hit 16 distinct bank slots;
+//   * split-K over the grid (fp32 slabs, summed with the epilogue by splitk_reduce_kernel) and an
+//     XCD-aware block order (consecutive blocks of one XCD share their X slice in its L2);
+//   * EPI_SILU: a wave's fragments are gate columns and the matching up columns, so gate_up writes
+//     SiLU(gate) * up directly.
+__device__ __forceinline__ int mt_slot(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+template <int WM, int WN, int MR, int WNF, int EPI>
+__global__ void __launch_bounds__(WM* WN * 64) mt_gemm_kernel(bf16_t* __restrict__ Y, float* __restrict__ part,
+                                                              const bf16_t* __restrict__ X,
+                                                              const bf16_t* __restrict__ W, int M, int N, int K,
+                                                              int ldx, int ldy, int kslice, int inter, int ntm,
+                                                              int ntn, int* __restrict__ cnt) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = 32 * MR * WM, BN = 32 * WNF * WN;  // X rows / W rows of a stage image
+  constexpr int ROWS = BN + BM, STAGE = ROWS * 128;
+  constexpr int NS = (160 * 1024 / STAGE) < 6 ? (160 * 1024 / STAGE) : 6;  // ring depth: the LDS it fits
+  constexpr int NI = ROWS / 8 / NW;  // DMA instructions per wave per k-group
+  constexpr int HF = EPI == EPI_SILU ? WNF / 2 : WNF;  // output fragments per wave
+  constexpr int OUTB = 32 * HF * WN;                    // output columns of the workgroup
+  static_assert(ROWS % (8 * NW) == 0 && (EPI != EPI_SILU || WNF % 2 == 0), "mt tile");
+  static_assert(NS >= 3 && NI * 4 <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tn = wg % ntn, tm = (wg / ntn) % ntm, z = wg / (ntn * ntm);
+  const int m0 = tm * BM, c0 = tn * OUTB, kbeg = z * kslice;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  // DMA sources: instruction j of this wave fills image rows 8 (wid + NW j) .. +7; lane -> row
+  // + (lane >> 3), LDS chunk (lane & 7) <- global chunk (lane & 7) ^ swizzle(row).  W image row
+  // 32 (wn' WNF + f) + i is output column c0 + 32 (wn' HF + f % HF) + i (+ inter for up fragments).
+  const bf16_t* src[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int row = 8 * (wid + NW * j) + (lane >> 3);
+    const int gch = (lane & 7) ^ ((row >> 1) & 7);
+    const bf16_t* base;
+    if (row < BN) {
+      const int wv = row / (32 * WNF), f = (row / 32) % WNF, i = row & 31;
+      const int col = c0 + 32 * (wv * HF + f % HF) + i;
+      base = W + static_cast<size_t>((EPI == EPI_SILU && f >= HF) ? inter + col : col) * K;
+    } else {  // rows past M re-read row M-1: loaded, never stored
+      base = X + static_cast<size_t>(min(m0 + row - BN, M - 1)) * ldx;
+    }
+    src[j] = base + kbeg + 8 * gch;
+  }
+  auto stage = [&](int g, int buf) {
+    char* dst = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(src[j] + 64 * g),
+                                       (__attribute__((address_space(3))) void*)(dst + (wid + NW * j) * 1024), 16, 0,
+                                       0);
+  };
+
+  float16_ acc[MR][WNF];
+#pragma unroll
+  for (int t = 0; t < MR; ++t)
+#pragma unroll
+    for (int f = 0; f < WNF; ++f)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[t][f][e] = 0.f;
+
+  const int r32 = lane & 31, h = lane >> 5;
+  const bool rows = m0 + wm * 32 * MR < M;  // wave-uniform: a wave past M only stages
+  int aoff[WNF], boff[MR];                   // image rows of this lane's fragments
+#pragma unroll
+  for (int f = 0; f < WNF; ++f) aoff[f] = 32 * (wn * WNF + f) + r32;
+#pragma unroll
+  for (int t = 0; t < MR; ++t) boff[t] = BN + 32 * (wm * MR + t) + r32;
+
+  const int ng = kslice / 64;
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < ng) stage(p, p);
+  for (int g = 0; g < ng; ++g) {
+    // this wave's DMA of k-group g has landed (the next min(NS-2, ng-1-g) groups may still fly); the
+    // barrier publishes every wave's, and retires every wave's reads of the buffer read at g - 1,
+    // which the group g + NS - 1 DMA then overwrites
+    const int ahead = min(NS - 2, ng - 1 - g);
+    if (ahead >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * 4) : "memory");
+    else if (ahead == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * 3) : "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * 2) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (g + NS - 1 < ng) stage(g + NS - 1, (g + NS - 1) % NS);
+    const char* b = smem + (g % NS) * STAGE;
+    if (rows) {
+      u32x4 fa[2][WNF], fb[2][MR];
+      auto rd = [&](int s, u32x4 (&a)[WNF], u32x4 (&bb)[MR]) {
+#pragma unroll
+        for (int t = 0; t < MR; ++t) bb[t] = *reinterpret_cast<const u32x4*>(b + mt_slot(boff[t], 2 * s + h));
+#pragma unroll
+        for (int f = 0; f < WNF; ++f) a[f] = *reinterpret_cast<const u32x4*>(b + mt_slot(aoff[f], 2 * s + h));
+      };
+      rd(0, fa[0], fb[0]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (s < 3) rd(s + 1, fa[(s + 1) & 1], fb[(s + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);  // step s + 1's reads fly under step s's MFMAs
+#pragma unroll
+        for (int t = 0; t < MR; ++t)
+#pragma unroll
+          for (int f = 0; f < WNF; ++f)
+            acc[t][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(fa[s & 1][f]), as_bf16x8(fb[s & 1][t]),
+                                                                acc[t][f], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+
+  // lane (r32, h), register e of tile (t, f): token m0 + 32 (wm MR + t) + r32, column 32 f' + 8 (e >> 2)
+  // + 4 h + (e & 3) of the wave's output columns
+  if (rows) {
+#pragma unroll
+    for (int t = 0; t < MR; ++t) {
+      const int m = m0 + 32 * (wm * MR + t) + r32;
+      if (m >= M) continue;
+#pragma unroll
+      for (int f = 0; f < HF; ++f)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int n = c0 + 32 * (wn * HF + f) + 8 * gq + 4 * h;
+          const float16_& a = acc[t][f];
+          if (part != nullptr) {  // split-K: this slice's raw fp32 slab
+            const size_t row = (static_cast<size_t>(z) * M + m) * static_cast<size_t>(N);
+            *reinterpret_cast<float4_*>(part + row + n) =
+                float4_{a[4 * gq], a[4 * gq + 1], a[4 * gq + 2], a[4 * gq + 3]};
+            if constexpr (EPI == EPI_SILU) {
+              const float16_& u = acc[t][f + HF];
+              *reinterpret_cast<float4_*>(part + row + inter + n) =
+                  float4_{u[4 * gq], u[4 * gq + 1], u[4 * gq + 2], u[4 * gq + 3]};
+            }
+            continue;
+          }
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e] = EPI == EPI_SILU ? silu(a[4 * gq + e]) * acc[t][f + HF][4 * gq + e] : a[4 * gq + e];
+          uint2 o;
+          o.x = pack2(v[0], v[1]);
+          o.y = pack2(v[2], v[3]);
+          *reinterpret_cast<uint2*>(Y + static_cast<size_t>(m) * ldy + n) = o;
+        }
+    }
+  }
+  if (part == nullptr || cnt == nullptr) return;  // unsplit, or slabs summed by splitk_reduce_kernel
+
+  // In-launch split-K reduction (cdna_hip_programming.md §5 "Projection GEMM at M = 256" item 2):
+  // every slice publishes its slab with one agent-scope release before drawing a ticket; the slice
+  // that draws S - 1 acquires, sums the S slabs of the tile in slice order (deterministic) and
+  // writes the epilogue, then re-arms the tile's counter for the next launch.  Correct for any
+  // placement of the slices over XCDs.
+  const int S = gridDim.x / (ntm * ntn);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's slab stores are complete; the staging ring is no longer read
+  int* flag = reinterpret_cast<int*>(smem);
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int ticket = __hip_atomic_fetch_add(cnt + tm * ntn + tn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = ticket == S - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      cnt[tm * ntn + tn] = 0;
+    }
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  const int nr = min(BM, M - m0);
+  constexpr int Q4 = OUTB / 4;
+  for (int idx = tid; idx < nr * Q4; idx += NW * 64) {
+    const int m = m0 + idx / Q4, n = c0 + 4 * (idx % Q4);
+    float4_ g = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
+    for (int zz = 0; zz < S; ++zz) {
+      const float* row = part + (static_cast<size_t>(zz) * M + m) * static_cast<size_t>(N);
+      g += *reinterpret_cast<const float4_*>(row + n);
+      if constexpr (EPI == EPI_SILU) u += *reinterpret_cast<const float4_*>(row + inter + n);
+    }
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = EPI == EPI_SILU ? silu(g[e]) * u[e] : g[e];
+    uint2 o;
+    o.x = pack2(v[0], v[1]);
+    o.y = pack2(v[2], v[3]);
+    *reinterpret_cast<uint2*>(Y + static_cast<size_t>(m) * ldy + n) = o;
+  }
+}
+
+// (wm, wn, mr, wnf): WM x WN waves of 32 MR rows x 32 WNF W rows; false when the shape is not tiled
+// or the layout is not built.
+// With a tile-counter array `cnt` (>= tiles ints, zero on first use; every launch leaves it zero) the
+// split-K slabs are summed inside the launch, else by splitk_reduce_kernel.
+bool launch_mt_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx, int ldy,
+                    int wm, int wn, int mr, int wnf, int splitk, int epi, hipStream_t s, int* cnt, int cnt_len) {
+  if (M <= 0 || splitk < 1 || K % (64 * splitk) != 0 || ldx % 8 != 0 || ldy % 4 != 0) return false;
+  if (epi == EPI_SILU && (N % 2 != 0 || wnf % 2 != 0)) return false;
+  if (splitk > 1 && part == nullptr) return false;
+  const int outN = epi == EPI_SILU ? N / 2 : N;
+  const int outb = 32 * (epi == EPI_SILU ? wnf / 2 : wnf) * wn;
+  if (outN % outb != 0) return false;
+  const int bm = 32 * mr * wm;
+  const int ntm = (M + bm - 1) / bm, ntn = outN / outb;
+  const long nwg = static_cast<long>(ntm) * ntn * splitk;
+  if (nwg > (1L << 30)) return false;
+  float* p = splitk > 1 ? part : nullptr;
+  int* cnt_ = splitk > 1 && cnt != nullptr && cnt_len >= ntm * ntn ? cnt : nullptr;
+  const int kslice = K / splitk;
+  bool launched = false;
+#define MXS_MT(a, b, c, d, e)                                                                                  \
+  if (!launched && wm == a && wn == b && mr == c && wnf == d && epi == e) {                                   \
+    hipLaunchKernelGGL((mt_gemm_kernel<a, b, c, d, e>), dim3(nwg), dim3(a * b * 64), 0, s, Y, p, X, W, M, N, K, \
+                       ldx, ldy, kslice, N / 2, ntm, ntn, cnt_);                                              \
+    launched = true;                                                                                          \
+  }
+#define MXS_MT_E(a, b, c, d) MXS_MT(a, b, c, d, EPI_NONE) MXS_MT(a, b, c, d, EPI_SILU)
+  MXS_MT_E(4, 1, 2, 2) MXS_MT_E(4, 2, 2, 2) MXS_MT_E(4, 1, 2, 4) MXS_MT_E(2, 2, 2, 2) MXS_MT_E(2, 2, 2, 4)
+  MXS_MT_E(2, 4, 2, 2) MXS_MT_E(1, 4, 2, 2) MXS_MT_E(1, 2, 2, 2) MXS_MT_E(2, 1, 2, 2) MXS_MT_E(8, 1, 1, 4)
+  MXS_MT_E(4, 2, 1, 2) MXS_MT_E(2, 4, 1, 2)
+#undef MXS_MT_E
+#undef MXS_MT
+  if (!launched) return false;
+  MXS_CHECK_LAUNCH();
+  if (splitk > 1 && cnt_ == nullptr) {
+    const long total4 = static_cast<long>(M) * outN / 4;
+    const int blocks = static_cast<int>(std::min<long>((total4 + 255) / 256, 1024));
+    if (epi == EPI_SILU)
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_SILU>, dim3(blocks), dim3(256), 0, s, Y, part, M, N, splitk, ldy,
+                         N / 2);
+    else
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_NONE>, dim3(blocks), dim3(256), 0, s, Y, part, M, N, splitk, ldy,
+                         0);
+    MXS_CHECK_LAUNCH();
+  }
+  return true;
+}
+
 // config id = ((MF-1) * 2 + (NF/2-1)) * 3 + wave layout {0: 1x4, 1: 2x2, 2: 4x1}; MF in {1, 2, 4}
 // returns false when the configuration does not tile the shape (the caller keeps hipBLASLt).
 // Grouped form: offs != nullptr, E experts (W [E, N, K]), M = routed rows (slab rows), rows_max = the

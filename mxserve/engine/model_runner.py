@@ -541,7 +541,9 @@ class ModelRunner:
         if not self.cfg.is_moe:
             shapes.update(gate_up=(w["l0.gate_up"], 1), down=(w["l0.down"], 0))
         with torch.inference_mode():
+            t0 = time.time()
             self.decode_gemm_report = decode_gemm.tune(shapes, buckets, self.device, self.dtype)
+            self.decode_gemm_tune_s = time.time() - t0
             self.prefill_gemm_report = decode_gemm.tune_prefill(
                 {k: v for k, (v, epi) in shapes.items() if epi == 0 and k != "lm_head"}, self.device, self.dtype)
             if self.cfg.is_moe and "l0.w13" in w:  # expert GEMMs at decode batches (local experts)

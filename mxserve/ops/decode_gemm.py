@@ -24,10 +24,11 @@ import torch
 log = logging.getLogger(__name__)
 
 MAX_M = 256
-# buckets the capture-time tuner measures: above this the register-staged kernel measured 1.3-2.5x
-# behind hipBLASLt for every projection (profiles/r2_decode_gemm_probe_vs_hipblaslt.jsonl), so the
-# engine does not spend startup time timing them
-MAX_TUNE_M = int(os.environ.get("MXS_DECODE_GEMM_TUNE_MAX_M", "64"))
+# buckets the capture-time tuner measures (the whole decode-graph range): up to OLD_FORMS_MAX_M the
+# register / LDS forms compete, above it only the medium-M (mt) kernel, since the register-staged forms
+# measured 1.3-2.5x behind hipBLASLt there (profiles/r2_decode_gemm_probe_vs_hipblaslt.jsonl)
+MAX_TUNE_M = int(os.environ.get("MXS_DECODE_GEMM_TUNE_MAX_M", "256"))
+OLD_FORMS_MAX_M = 64
 MODE = os.environ.get("MXS_DECODE_GEMM", "auto")  # auto | off | force
 
 
@@ -40,16 +41,51 @@ def unroll(mf: int, nf: int) -> int:
     return 8 if mf + nf <= 3 else (4 if mf + nf <= 6 else 2)
 
 
-def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool = True) -> list[tuple]:
+def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool = True,
+               mt: bool = True) -> list[tuple]:
     """(mf, nf, wm, splitk, lu) configurations that tile the shape (wave row tile MF x 16 sized to M
     unless all_mf: then every MF, i.e. more row tiles re-reading the weights from L2).  lu = 0: the
     register kernel (wm waves over M); lu = 2 / 4: the LDS form (X tile shared by the workgroup's 4
-    waves through LDS, lu k-steps per group)."""
+    waves through LDS, lu k-steps per group).  With mt, from M = MT_MIN_M on, also the medium-M
+    kernel's ("mt", wm, wn, wnf, splitk) configurations."""
     out = []
     for mf in ((1, 2, 4) if all_mf else (_mf(M),)):
         out += _candidates_mf(M, N, K, epi, mf)
         if lds and mf > 1:  # one 16-row tile: the X fragment is as small as one W fragment
             out += _candidates_lds(N, K, epi, mf)
+    if mt and M >= MT_MIN_M:  # dense only (the grouped MoE form has no mt kernel)
+        out += mt_candidates(M, N, K, epi)
+    return out
+
+
+MT_MIN_M = 64
+MT_COUNTERS = 1 << 16  # tile counters of the in-launch split-K reduction (every launch leaves them zero)
+# in-launch split-K reduction (last arriver sums the slabs): measured slower than the separate reduce
+# kernel at every decode shape (agent-scope release per workgroup + a serial slab read), so opt-in
+MT_FUSED_REDUCE = os.environ.get("MXS_MT_FUSED_REDUCE", "0") == "1"
+# (WM, WN, MR, WNF) of the medium-M kernel (gemm_decode.hip mt_gemm_kernel): WM x WN waves, each 32 MR
+# rows x 32 WNF weight rows
+MT_LAYOUTS = ((4, 1, 2, 2), (4, 2, 2, 2), (4, 1, 2, 4), (2, 2, 2, 2), (2, 2, 2, 4), (2, 4, 2, 2), (1, 4, 2, 2),
+              (1, 2, 2, 2), (2, 1, 2, 2), (8, 1, 1, 4), (4, 2, 1, 2), (2, 4, 1, 2))
+
+
+def mt_candidates(M: int, N: int, K: int, epi: int, max_blocks: int = 1024) -> list[tuple]:
+    out = []
+    for wm, wn, mr, wnf in MT_LAYOUTS:
+        bm = 32 * mr * wm
+        if bm > 64 and bm >= 2 * M:  # half the tile's rows empty: a smaller WM covers it
+            continue
+        if epi and wnf % 2:
+            continue
+        outb = 32 * (wnf // 2 if epi else wnf) * wn
+        outN = N // 2 if epi else N
+        if outN % outb:
+            continue
+        tiles = -(-M // bm) * (outN // outb)
+        for sk in (1, 2, 4, 8):
+            if K % (64 * sk) or K // sk < 128 or tiles * sk > max_blocks:
+                continue
+            out.append(("mt", wm, wn, mr, wnf, sk))
     return out
 
 
@@ -88,13 +124,14 @@ class DecodeGemmTable:
     def __init__(self):
         self.entries: dict[tuple, list] = {}  # (N, K, epi) -> sorted [(M bucket, cfg or None)]
         self.part: Optional[torch.Tensor] = None  # fp32 split-K workspace (stable for graphs)
+        self.cnt: Optional[torch.Tensor] = None  # mt kernel tile counters (in-launch split-K reduce)
         self.report: list = []
 
     def lookup(self, M: int, N: int, K: int, epi: int) -> Optional[tuple]:
         if MODE == "off" or M > MAX_M:
             return None
         if MODE == "force":
-            c = candidates(M, N, K, epi)
+            c = [x for x in candidates(M, N, K, epi) if x[0] != "mt"]
             return next((x for x in c if x[3] == 1), c[0] if c else None)
         ent = self.entries.get((N, K, epi))
         if not ent:
@@ -106,8 +143,12 @@ class DecodeGemmTable:
 
     def run(self, out: torch.Tensor, x: torch.Tensor, w: torch.Tensor, cfg: tuple, epi: int) -> bool:
         from . import ext
-        mf, nf, wm, sk = cfg[:4]
-        lu = cfg[4] if len(cfg) > 4 else 0
+        mt = cfg[0] == "mt"
+        if mt:
+            _, wm, wn, mr, wnf, sk = cfg
+        else:
+            mf, nf, wm, sk = cfg[:4]
+            lu = cfg[4] if len(cfg) > 4 else 0
         part = None
         if sk > 1:
             need = sk * x.shape[0] * w.shape[0]
@@ -116,24 +157,46 @@ class DecodeGemmTable:
                     return False  # never allocate inside a capture (tune() sizes it beforehand)
                 self.part = torch.empty(need, dtype=torch.float32, device=x.device)
             part = self.part
+        if mt:
+            if sk > 1 and (self.cnt is None or self.cnt.device != x.device):
+                if torch.cuda.is_current_stream_capturing():
+                    return False
+                self.cnt = torch.zeros(MT_COUNTERS, dtype=torch.int32, device=x.device)
+            return bool(ext().mt_gemm(out, x, w, part, wm, wn, mr, wnf, sk, epi, self.cnt if MT_FUSED_REDUCE else None))
         return bool(ext().decode_gemm(out, x, w, part, mf, nf, wm, sk, epi, lu))
 
 
 TABLE = DecodeGemmTable()
 
 
+COLD_BYTES = 512 << 20  # > the 256 MiB Infinity Cache: timed weights come from HBM, as in a decode step
+
+
+def weight_copies(w: torch.Tensor, cold_bytes: int = COLD_BYTES, cap: int = 20) -> list:
+    """[w] plus enough copies that cycling through them streams more bytes than the Infinity Cache
+    holds: a decode step reads every layer's weights once (GBs), so a timing that replays one
+    8-70 MB matrix from the cache ranks kernels on the wrong memory level."""
+    n = max(1, min(cap, -(-cold_bytes // (w.numel() * w.element_size()))))
+    return [w] + [w.clone() for _ in range(n - 1)]
+
+
 def _graph_time(fn, iters: int = 20) -> float:
-    """Microseconds per call of `fn`, from `iters` calls captured in one hipGraph."""
+    """Microseconds per call of `fn`, from `iters` calls captured in one hipGraph.  `fn` may take the
+    call index (to cycle through weight copies)."""
+    import inspect
+    if not inspect.signature(fn).parameters:
+        f0 = fn
+        fn = lambda i: f0()  # noqa: E731
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        fn()
+        fn(0)
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        for _ in range(iters):
-            fn()
+        for i in range(iters):
+            fn(i)
     g.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -157,24 +220,28 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
     # workspace for the largest split-K any candidate may pick
     need = max(8 * max(bks) * w.shape[0] for w, _ in shapes.values())
     TABLE.part = torch.empty(need, dtype=torch.float32, device=device)
+    TABLE.cnt = torch.zeros(MT_COUNTERS, dtype=torch.int32, device=device)
     rows = []
     for name, (w, epi) in shapes.items():
         N, K = w.shape
         ent = []
+        ws = weight_copies(w)  # timed from HBM, as the decode step reads them
         for M in bks:
             x = (torch.randn(M, K, device=device) * 0.5).to(dtype)
             outN = N // 2 if epi else N
             ref_out = silu_mul(torch.nn.functional.linear(x, w)) if epi else torch.nn.functional.linear(x, w)
             if epi:
-                t_lib = _graph_time(lambda: silu_mul(torch.nn.functional.linear(x, w)))
+                t_lib = _graph_time(lambda i: silu_mul(torch.nn.functional.linear(x, ws[i % len(ws)])))
             else:
-                t_lib = _graph_time(lambda: torch.nn.functional.linear(x, w))
+                t_lib = _graph_time(lambda i: torch.nn.functional.linear(x, ws[i % len(ws)]))
             best, best_t = None, t_lib
             out = torch.empty(M, outN, dtype=dtype, device=device)
             for cfg in candidates(M, N, K, epi):
+                if cfg[0] != "mt" and M > OLD_FORMS_MAX_M:
+                    continue
                 if not TABLE.run(out, x, w, cfg, epi):
                     continue
-                t = _graph_time(lambda: TABLE.run(out, x, w, cfg, epi))
+                t = _graph_time(lambda i: TABLE.run(out, x, ws[i % len(ws)], cfg, epi))
                 if t < best_t * 0.97:  # a clear win only
                     best, best_t = cfg, t
             if best is not None:  # correctness gate: the winner must match hipBLASLt's result
@@ -188,6 +255,7 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
             rows.append({"proj": name, "M": M, "N": N, "K": K, "epi": epi, "hipblaslt_us": round(t_lib, 2),
                          "chosen": "hipblaslt" if best is None else "mfma", "cfg": best, "us": round(best_t, 2)})
         TABLE.entries[(N, K, epi)] = ent
+        del ws
     TABLE.report = rows
     won = sum(r["chosen"] == "mfma" for r in rows)
     log.info("decode GEMM tuning: MFMA kernel chosen for %d of %d (bucket, projection) pairs in %.1fs", won,

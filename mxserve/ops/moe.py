@@ -256,7 +256,7 @@ def tune(w13: torch.Tensor, w2: torch.Tensor, buckets: list, top_k: int, n_exper
         best = {}
         for name, w, epi, N, K, o, xin in (("w13", w13, 1, two_i, H, h, xs), ("w2", w2, 0, H, I, ys, h)):
             bt, bc = None, None
-            for cfg in candidates(T, N, K, epi, all_mf=True):
+            for cfg in candidates(T, N, K, epi, all_mf=True, mt=False):
                 sk = cfg[3]
                 if cfg[2] > 2:
                     continue

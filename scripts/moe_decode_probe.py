@@ -55,7 +55,7 @@ def main():
         for name, (w, epi, N, K, o) in {"w13": (w13, 1, 2 * I, H, h), "w2": (w2, 0, H, I, ys)}.items():
             xin = xs if name == "w13" else h
             res = []
-            for cfg in dg.candidates(min(T, 256), N, K, epi, all_mf=True):
+            for cfg in dg.candidates(min(T, 256), N, K, epi, all_mf=True, mt=False):
                 sk = cfg[3]
                 if cfg[2] > 2:
                     continue

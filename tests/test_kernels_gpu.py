@@ -484,11 +484,46 @@ def test_decode_gemm_all_configs(gpu, M, N, K, epi):
     cands = decode_gemm.candidates(M, N, K, epi)
     assert cands
     part = torch.empty(8 * M * N, dtype=torch.float32, device=gpu)
-    assert any(c[4] for c in cands) or M <= 16, "LDS-form configurations are among the candidates"
-    for mf, nf, wm, sk, lu in cands:
+    assert any(c[0] != "mt" and c[4] for c in cands) or M <= 16, "LDS-form configurations are among the candidates"
+    assert any(c[0] == "mt" for c in cands) == (M >= decode_gemm.MT_MIN_M)
+    for c in cands:
         out = torch.full((M, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
-        assert ops.ext().decode_gemm(out, x, w, part, mf, nf, wm, sk, epi, lu)
-        _close(out, want, atol=2e-2, rtol=2e-2, name=f"decode gemm {M}x{N}x{K} epi{epi} cfg {(mf, nf, wm, sk, lu)}")
+        if c[0] == "mt":
+            assert ops.ext().mt_gemm(out, x, w, part, *c[1:], epi)
+        else:
+            assert ops.ext().decode_gemm(out, x, w, part, *c[:4], epi, c[4])
+        _close(out, want, atol=2e-2, rtol=2e-2, name=f"decode gemm {M}x{N}x{K} epi{epi} cfg {c}")
+
+
+@pytest.mark.parametrize("N,K,epi", [(3072, 2048, 0), (2048, 8192, 0), (16384, 2048, 1), (1024, 512, 1)])
+@pytest.mark.parametrize("M", [1, 33, 64, 100, 192, 256, 300, 640])
+def test_mt_gemm_all_layouts(gpu, M, N, K, epi):
+    """Every wave layout and split-K of the medium-M kernel (gemm_decode.hip mt_gemm_kernel, glds
+    staging) vs an fp32 reference, including partial row tiles, several row tiles (prefill-sized M)
+    and a K of 2 k-groups per slice; an asymmetric W catches a transposed store."""
+    from mxserve.ops import decode_gemm
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
+    x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16, generator=g)
+    w = (torch.randn(N, K, device=gpu, generator=g) * K ** -0.5).to(torch.bfloat16)
+    w[:, : K // 2] *= torch.linspace(0.5, 2.0, N, device=gpu).to(torch.bfloat16)[:, None]
+    y = x.float() @ w.float().t()
+    want = torch.nn.functional.silu(y[:, :N // 2]) * y[:, N // 2:] if epi else y
+    part = torch.empty(8 * M * N, dtype=torch.float32, device=gpu)
+    cnt = torch.zeros(1 << 16, dtype=torch.int32, device=gpu)
+    ran = 0
+    for lay in decode_gemm.MT_LAYOUTS:
+        for sk in (1, 2, 4):
+            for fused in ((False, True) if sk > 1 else (False,)):
+                out = torch.full((M, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
+                for _ in range(2 if fused else 1):  # the second launch reuses the counters the first re-armed
+                    if not ops.ext().mt_gemm(out, x, w, part, *lay, sk, epi, cnt if fused else None):
+                        break
+                else:
+                    ran += 1
+                    _close(out, want, atol=2e-2, rtol=2e-2,
+                           name=f"mt gemm {M}x{N}x{K} epi{epi} {lay} sk{sk} fused-reduce {fused}")
+    assert ran >= 8
+    assert int(cnt.abs().sum().item()) == 0, "every launch leaves the tile counters zero"
 
 
 def test_decode_gemm_tuner_and_dispatch(gpu, monkeypatch):
@@ -563,7 +598,7 @@ def test_moe_decode_gemm_all_configs(gpu, counts, silu):
             refs[e] = x[a:b].float() @ w[e].float().t()
     epi = int(silu)
     ran = 0
-    for cfg in dg.candidates(rows_max, N, K, epi, all_mf=True):
+    for cfg in dg.candidates(rows_max, N, K, epi, all_mf=True, mt=False):
         mf, nf, wm, sk, lu = cfg
         if wm > 2:
             continue
@@ -584,7 +619,7 @@ def test_moe_decode_gemm_all_configs(gpu, counts, silu):
             _close(y[a:b], exp, atol=3e-2, rtol=3e-2, name=f"expert {e} cfg {cfg}")
         if sk == 1:
             assert torch.all(y[o[-1]:] == 7.0), f"rows past the routed count were written ({cfg})"
-    assert ran >= 6 and any(c[4] for c in dg.candidates(rows_max, N, K, epi, all_mf=True))
+    assert ran >= 6 and any(c[4] for c in dg.candidates(rows_max, N, K, epi, all_mf=True, mt=False))
 
 
 @pytest.mark.parametrize("T,offset", [(1, 0), (7, 0), (64, 0), (200, 0), (40, 2)])
