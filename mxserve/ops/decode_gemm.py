@@ -53,12 +53,16 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
         out += _candidates_mf(M, N, K, epi, mf)
         if lds and mf > 1:  # one 16-row tile: the X fragment is as small as one W fragment
             out += _candidates_lds(N, K, epi, mf)
-    if mt and M >= MT_MIN_M:  # dense only (the grouped MoE form has no mt kernel)
+    # dense only (the grouped MoE form has no mt kernel); below MT_MIN_M only for large matrices,
+    # where it streams W at 5.3-5.6 TB/s (Llama-3-70B gate_up / down at M = 8-32,
+    # profiles/r2_mt_gemm_probe_70b_cold_weights.jsonl)
+    if mt and (M >= MT_MIN_M or (M >= 8 and N * K * 2 >= MT_SMALL_M_MIN_BYTES)):
         out += mt_candidates(M, N, K, epi)
     return out
 
 
 MT_MIN_M = 64
+MT_SMALL_M_MIN_BYTES = int(os.environ.get("MXS_MT_SMALL_M_MIN_BYTES", str(192 << 20)))
 MT_COUNTERS = 1 << 16  # tile counters of the in-launch split-K reduction (every launch leaves them zero)
 # in-launch split-K reduction (last arriver sums the slabs): measured slower than the separate reduce
 # kernel at every decode shape (agent-scope release per workgroup + a serial slab read), so opt-in

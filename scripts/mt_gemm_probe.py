@@ -19,6 +19,10 @@ SHAPES = {
                      "down": (2048, 8192, 0)},
     "llama-3-8b": {"qkv": (6144, 4096, 0), "o": (4096, 4096, 0), "gate_up": (28672, 4096, 1),
                    "down": (4096, 14336, 0)},
+    "llama-3-70b": {"qkv": (10240, 8192, 0), "o": (8192, 8192, 0), "gate_up": (57344, 8192, 1),
+                    "down": (8192, 28672, 0)},
+    "llama-3-70b-tp8": {"qkv": (1280, 8192, 0), "o": (8192, 1024, 0), "gate_up": (7168, 8192, 1),
+                        "down": (8192, 3584, 0)},
 }
 
 
@@ -30,7 +34,7 @@ def main():
     dev = torch.device("cuda:0")
     Ms = [int(m) for m in (sys.argv[1].split(",") if len(sys.argv) > 1 else "64,128,192,256,384,512".split(","))]
     models = sys.argv[2].split(",") if len(sys.argv) > 2 else list(SHAPES)
-    dg.TABLE.part = torch.empty(8 * max(Ms) * 28672, dtype=torch.float32, device=dev)
+    dg.TABLE.part = torch.empty(8 * max(Ms) * 57344, dtype=torch.float32, device=dev)
     for model in models:
         for name, (N, K, epi) in SHAPES[model].items():
             w = ((torch.rand(N, K, device=dev) * 2 - 1) * K ** -0.5).to(torch.bfloat16)

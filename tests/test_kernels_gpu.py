@@ -485,7 +485,8 @@ def test_decode_gemm_all_configs(gpu, M, N, K, epi):
     assert cands
     part = torch.empty(8 * M * N, dtype=torch.float32, device=gpu)
     assert any(c[0] != "mt" and c[4] for c in cands) or M <= 16, "LDS-form configurations are among the candidates"
-    assert any(c[0] == "mt" for c in cands) == (M >= decode_gemm.MT_MIN_M)
+    big = N * K * 2 >= decode_gemm.MT_SMALL_M_MIN_BYTES
+    assert any(c[0] == "mt" for c in cands) == (M >= decode_gemm.MT_MIN_M or (M >= 8 and big))
     for c in cands:
         out = torch.full((M, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
         if c[0] == "mt":
