@@ -6,13 +6,16 @@ Launch: `python bench.py --gpus N` spawns N ranks itself (torch.distributed.run,
 GPU) before anything touches the GPU; under an external launcher WORLD_SIZE must equal --gpus.
 
 Phases (--mode auto: agg for N = 1, agg then disagg for N >= 2, both in the one JSON line):
+  probe   N >= 2: the multi-GPU probe (mxserve/tools/mgpu_probe.py; TP / EP vs the unsharded model,
+          collectives, peer copies) in processes started before the ranks touch the GPU
   agg     each rank runs an independent engine replica -- the reference scales Llama-3.2-1B by
           `replicas:` of single-GPU workers behind the frontend router (examples/deploy/vllm/agg.yaml:14,21;
           SURVEY.md §2.4 P01) -- under an open-loop Poisson arrival process of --qps requests/s
           per GPU (weak scaling).  `value` is this phase.
   disagg  ranks [0, N/2) prefill, [N/2, N) decode, paired 1P:1D (examples/deploy/vllm/disagg.yaml:18-57).
-          Requests arrive at the decode rank at 2 x --qps per pair (same node QPS as agg); it
-          reserves KV blocks and hands the prompt to its prefill rank, which computes it, pushes
+          Requests arrive at the decode rank at 2 x --disagg-qps per pair (default 32 / GPU, below
+          the agg rate: at ISL 4000 the decode GPU of a 1:1 pair is KV-bandwidth bound at ~78
+          req/s, while its prefill GPU would idle 30-45 %; see --disagg-qps); it reserves KV blocks and hands the prompt to its prefill rank, which computes it, pushes
           the blocks into the decode rank's staging arena with the IPC copy kernel (xGMI between
           GPUs; mxserve/disagg/kv_transfer.py) and returns the first token.  TTFT includes the
           KV transfer.
@@ -74,6 +77,10 @@ def parse(argv=None):
     ap.add_argument("--max-num-seqs", type=int, default=384)
     ap.add_argument("--disagg-max-num-seqs", type=int, default=512,
                     help="decode ranks of the disagg phase carry 2x the per-GPU request rate")
+    ap.add_argument("--disagg-qps", type=float, default=float(os.environ.get("MXS_BENCH_DISAGG_QPS", "32")),
+                    help="disagg phase arrival rate per GPU (a 1P+1D pair takes 2x): a decode GPU streams the "
+                         "KV of every running request each step, so at ISL 4000 it sustains ~39k tok/s (~78 "
+                         "req/s of OSL 500); the agg rate (42/GPU) would overload the decode half of a 1:1 split")
     ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--enforce-eager", action="store_true")
@@ -90,6 +97,8 @@ def parse(argv=None):
                     help="TTFT samples per request-owning rank collected in steady state before timing")
     ap.add_argument("--phase-timeout-s", type=float, default=float(os.environ.get("MXS_BENCH_PHASE_TIMEOUT", "420")),
                     help="a disagg phase that has not finished by then is reported as failed")
+    ap.add_argument("--probe-timeout-s", type=float, default=float(os.environ.get("MXS_BENCH_PROBE_TIMEOUT", "300")),
+                    help="N >= 2: budget of the multi-GPU probe run after the serving phases (0: no probe)")
     return ap.parse_args(argv)
 
 
@@ -98,6 +107,44 @@ def _free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def start_probe(a, world: int):
+    """N >= 2: one multi-GPU probe process per rank (mxserve/tools/mgpu_probe.py: TP / EP against the
+    unsharded model, RCCL and custom all-reduce bandwidth, xGMI peer copies), started BEFORE this rank
+    touches the GPU and idle until finish_probe: a crash or hang there costs only the probe."""
+    if world < 2 or a.probe_timeout_s <= 0:
+        return None
+    root = os.path.dirname(os.path.abspath(__file__))
+    # its own rendezvous: rank 0's probe hosts the store (not torchrun's agent store of this job)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(MASTER_PORT=str(int(os.environ.get("MASTER_PORT", "29500")) + 211),
+               MXS_PROBE_DEVICE="cpu" if a.device == "cpu" else "auto",
+               PYTHONPATH=os.pathsep.join([root] + [x for x in [os.environ.get("PYTHONPATH")] if x]))
+    return subprocess.Popen([sys.executable, "-m", "mxserve.tools.mgpu_probe"], stdin=subprocess.PIPE,
+                            stdout=subprocess.PIPE, env=env, cwd=root)
+
+
+def finish_probe(p, timeout_s: float):
+    """Release the probe (this rank's engine is gone) and wait for it; rank 0's carries the result."""
+    if p is None:
+        return None
+    try:
+        p.stdin.write(b"go\n")
+        p.stdin.close()
+    except OSError:
+        pass
+    p.stdin = None  # closed above: communicate() must not flush it again
+    try:
+        out, _ = p.communicate(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.communicate()
+        return {"status": "failed", "error": f"no result within {timeout_s:.0f}s"}
+    lines = [ln for ln in out.decode(errors="replace").splitlines() if ln.startswith("PROBE ")]
+    if lines:
+        return json.loads(lines[-1][len("PROBE "):])
+    return {"status": "failed", "error": f"probe exited with {p.returncode} and no result"}
 
 
 def launch_ranks(a) -> int:
@@ -569,7 +616,7 @@ def phase_disagg(a, ctx, base_port: int) -> tuple:
         st = list(_STAT_NAN)
     else:
         sp = SamplingParams(max_tokens=osl, temperature=a.temperature, ignore_eos=True)
-        drv = Driver(a2, rank, eng.model_config.vocab_size, 2 * a.qps)
+        drv = Driver(a2, rank, eng.model_config.vocab_size, 2 * a.disagg_qps)
         agree = ctx.agree_fn(ctx.pg_decode, world // 2)
         st = drv.stats(run_disagg_decode(a2, eng, sp, drv, ctx.barrier, agree, conn))
     conn.close()
@@ -590,6 +637,7 @@ def main():
     mode = a.mode if a.mode != "auto" else ("agg" if world == 1 else "both")
     if mode in ("disagg", "both") and (world < 2 or world % 2):
         raise SystemExit("bench.py: the disagg phase needs an even number of GPUs (1 prefill : 1 decode pairs)")
+    probe = start_probe(a, world)  # before Ctx: nothing in this process has touched the GPU yet
     ctx = Ctx(a)
     base_port = int(os.environ.get("MASTER_PORT", "29500")) + 101
 
@@ -604,12 +652,17 @@ def main():
                           agg=agg, a=a, mode=mode)
         col_d, info_d = dis
         dis = summarize(col_d, a.steps, list(range(world // 2, world)))
-        dis.update(info_d, parallelism=f"disagg {world // 2}P+{world // 2}D", qps_per_pair=2 * a.qps)
+        dis.update(info_d, parallelism=f"disagg {world // 2}P+{world // 2}D", qps_per_pair=2 * a.disagg_qps,
+                   qps_node=a.disagg_qps * world)
         if agg is None:
             info = {"kv_blocks": None, "graphs": [], "preemptions": None, "model": a.model,
                     "kv_cache_dtype": "bf16", "isl": a.isl, "osl": a.osl}
+    probe_res = finish_probe(probe, a.probe_timeout_s)
     if ctx.rank == 0:
-        print(json.dumps(build_line(a, ctx, mode, agg, dis, info)), flush=True)
+        line = build_line(a, ctx, mode, agg, dis, info)
+        if probe_res is not None:
+            line["multi_gpu_probe"] = probe_res
+        print(json.dumps(line), flush=True)
     if world > 1:
         ctx.dist.barrier()
         ctx.dist.destroy_process_group()

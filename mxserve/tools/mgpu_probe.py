@@ -1,0 +1,257 @@
+"""Multi-GPU probe: tensor / expert parallelism, collectives and xGMI peer copies measured on the
+node a multi-GPU bench runs on.
+
+bench.py (N >= 2 ranks) starts one probe process per rank BEFORE anything touches the GPU; each
+blocks on stdin until its rank has finished the serving phases and released its engine.  The probes
+then form their own process group -- RCCL when every rank has its own GPU, else gloo with the custom
+IPC all-reduce carrying the model's collectives (ranks sharing one GPU) -- and measure:
+
+  collectives  all-reduce of bf16 buffers 64 KiB - 256 MiB through the process group (RCCL over xGMI
+               on a real node): time, algorithm and bus bandwidth (2 (n-1) / n x bytes / t); the
+               custom IPC all-reduce (one-shot / two-shot) 16 KiB - 8 MiB
+  tp           Llama-3-70B layer shapes (2 layers, random weights) sharded TP=N against the
+               unsharded model on rank 0: logit error, argmax agreement, and the forward time of a
+               64-token batch at TP=N vs TP=1
+  ep           Mixtral-8x7B layer shapes (2 layers), experts sharded EP=N with the device-side IPC
+               token dispatch, against the unsharded model
+  p2p          rank 0: peer copy bandwidth to every other GPU it sees, one link at a time and all
+               links at once (hipMemcpyPeer over xGMI)
+
+A crash or hang in a probe costs only the probe (its rank reports {"status": "failed"}); the
+serving numbers of the bench stand.  Rank 0 prints one line `PROBE {json}` on its original stdout.
+The CPU plumbing run (bench.py --device cpu) uses the tiny configs over gloo.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+import traceback
+
+MODEL_TP = "meta-llama/Meta-Llama-3-70B-Instruct@layers=2"
+MODEL_EP = "mistralai/Mixtral-8x7B-Instruct-v0.1@layers=2"
+
+
+def _md(n, dev):
+    import torch
+    from ..models.llama import AttnMetadata
+    nb = (n + 15) // 16
+    pos = torch.arange(n, device=dev)
+    qsl = torch.tensor([0, n], dtype=torch.int32, device=dev)
+    return AttnMetadata(positions=pos, slot_mapping=pos.clone(), block_tables=torch.arange(
+        nb, dtype=torch.int32, device=dev).unsqueeze(0), seq_lens=torch.tensor([n], dtype=torch.int32, device=dev),
+        query_start_loc=qsl, logits_indices=torch.arange(n, device=dev), num_decodes=0, num_prefills=1,
+        num_prefill_tokens=n, max_query_len=n, max_seq_len=n, prefill_query_start_loc=qsl)
+
+
+class Probe:
+    def __init__(self):
+        import torch
+        self.torch = torch
+        self.rank = int(os.environ["RANK"])
+        self.world = int(os.environ["WORLD_SIZE"])
+        self.local = int(os.environ.get("LOCAL_RANK", self.rank))
+        self.on_gpu = os.environ.get("MXS_PROBE_DEVICE", "auto") != "cpu" and torch.cuda.is_available()
+        self.ndev = torch.cuda.device_count() if self.on_gpu else 0
+        self.shared = self.on_gpu and self.ndev < self.world
+        self.dev = torch.device("cuda", self.local % self.ndev) if self.on_gpu else torch.device("cpu")
+        self.dtype = torch.bfloat16 if self.on_gpu else torch.float32
+        self.backend = "nccl" if self.on_gpu and not self.shared else "gloo"
+
+    # ------------------------------------------------------------------ helpers
+    def sync(self):
+        if self.on_gpu:
+            self.torch.cuda.synchronize()
+
+    def timeit(self, fn, iters: int, warmup: int = 3) -> float:
+        """Median seconds per call (device-synchronised around each call)."""
+        for _ in range(warmup):
+            fn()
+        self.sync()
+        ts = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            fn()
+            self.sync()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return ts[len(ts) // 2]
+
+    def barrier(self):
+        import torch.distributed as dist
+        from ..parallel.comm import get_tp
+        dist.barrier(group=get_tp().cpu_group)
+
+    # ------------------------------------------------------------------ sections
+    def collectives(self) -> dict:
+        import torch.distributed as dist
+        from ..parallel.comm import get_tp
+        torch, n = self.torch, self.world
+        st = get_tp()
+        out = {"backend": self.backend, "all_reduce": [], "custom_all_reduce": []}
+        # RCCL up to 256 MiB (prefill-sized all-reduces); gloo (CPU run, ranks sharing a GPU) small only
+        sizes = [64 << 10, 1 << 20, 16 << 20, 256 << 20] if self.backend == "nccl" else [64 << 10, 1 << 20]
+        for nbytes in sizes:
+            x = torch.ones(nbytes // 2 if self.on_gpu else nbytes // 4, dtype=self.dtype, device=self.dev)
+            t = self.timeit(lambda: dist.all_reduce(x, group=st.group), iters=10 if nbytes >= 16 << 20 else 30)
+            out["all_reduce"].append({"bytes": nbytes, "us": round(t * 1e6, 1), "algbw_GBps": round(nbytes / t / 1e9, 2),
+                                      "busbw_GBps": round(2 * (n - 1) / n * nbytes / t / 1e9, 2)})
+            del x
+        car = st.custom_ar
+        if car is not None:
+            for nbytes in (16 << 10, 256 << 10, 1 << 20, 8 << 20):
+                x = torch.ones(nbytes // 2, dtype=torch.bfloat16, device=self.dev)
+                if not car.should_use(x):
+                    continue
+                y = torch.empty_like(x)
+                t = self.timeit(lambda: car.all_reduce(x, out=y), iters=50)
+                ok = bool(car.check()) and bool((y == float(n)).all().item())
+                out["custom_all_reduce"].append({"bytes": nbytes, "us": round(t * 1e6, 1),
+                                                 "busbw_GBps": round(2 * (n - 1) / n * nbytes / t / 1e9, 2),
+                                                 "correct": ok})
+        return out
+
+    def _logits_and_time(self, model: str, full: dict, moe_dispatch: str, n_tok: int = 64):
+        from ..models.config import get_model_config
+        from ..models.llama import build_model
+        torch = self.torch
+        cfg = get_model_config(model)
+        m = build_model(cfg, self.dev, self.dtype, moe_dispatch)
+        m.load_full_state(full)
+        ids = torch.randint(3, cfg.vocab_size, (n_tok,), generator=torch.Generator().manual_seed(2)).to(self.dev)
+        kv = torch.zeros((n_tok + 15) // 16, cfg.num_layers, 2, m.nkv, 16, cfg.head_dim, dtype=self.dtype,
+                         device=self.dev)
+        md = _md(n_tok, self.dev)
+        with torch.inference_mode():
+            logits = m.compute_logits(m.forward(ids, md, kv)).float().cpu()
+            t = self.timeit(lambda: m.forward(ids, md, kv), iters=10 if self.on_gpu else 3)
+        del m, kv
+        return logits, t
+
+    def sharded_vs_full(self, model: str, moe_dispatch: str) -> dict:
+        from ..models.config import get_model_config
+        from ..models.weights import random_full_state
+        from ..parallel import comm
+        torch = self.torch
+        cfg = get_model_config(model)
+        full = random_full_state(cfg, seed=4, std=0.02, dtype=self.dtype, device=self.dev)
+        got, t_n = self._logits_and_time(model, full, moe_dispatch)
+        st = comm.get_tp()
+        car_ok = st.custom_ar.check() if st.custom_ar is not None else None
+        res = {"model": model, "ranks": self.world, "ms_64_tokens": round(t_n * 1e3, 3),
+               "custom_all_reduce": st.custom_ar is not None, "custom_all_reduce_healthy": car_ok}
+        ref = None
+        if self.rank == 0:  # the same weights unsharded, in this process
+            comm.set_tp(comm.ParallelState())
+            try:
+                ref, t_1 = self._logits_and_time(model, full, "allreduce")
+            finally:
+                comm.set_tp(st)
+            res["ms_64_tokens_unsharded"] = round(t_1 * 1e3, 3)
+            res["speedup_vs_unsharded"] = round(t_1 / t_n, 3)
+        del full
+        if self.on_gpu:
+            torch.cuda.empty_cache()
+        # every rank's logits to rank 0 (host tensors over the CPU group)
+        import torch.distributed as dist
+        parts = [None] * self.world
+        dist.all_gather_object(parts, got.numpy(), group=st.cpu_group)
+        if self.rank == 0:
+            r = ref
+            scale = float(r.abs().max())
+            errs, agree = [], []
+            for p in parts:
+                g = torch.from_numpy(p)
+                errs.append(float((g - r).abs().max()) / scale)
+                agree.append(float((g.argmax(-1) == r.argmax(-1)).float().mean()))
+            res["max_rel_err"] = round(max(errs), 5)
+            res["argmax_agreement_min"] = round(min(agree), 4)
+            res["ranks_consistent"] = all(bool((torch.from_numpy(p) == torch.from_numpy(parts[0])).all()) for p in parts)
+        return res
+
+    def p2p(self) -> dict:
+        torch = self.torch
+        if not self.on_gpu or self.ndev < 2 or self.rank != 0:
+            return {"skipped": "needs >= 2 visible GPUs (rank 0 only)"}
+        nbytes = 256 << 20
+        src = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+        peers = [d for d in range(min(self.ndev, 8)) if d != self.dev.index]
+        dsts = {d: torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{d}") for d in peers}
+        out = {"bytes": nbytes, "per_peer_GBps": {}}
+        for d in peers:
+            t = self.timeit(lambda: dsts[d].copy_(src, non_blocking=True), iters=5, warmup=2)
+            out["per_peer_GBps"][str(d)] = round(nbytes / t / 1e9, 1)
+        streams = {d: torch.cuda.Stream(device=self.dev) for d in peers}
+
+        def all_at_once():
+            for d in peers:
+                with torch.cuda.stream(streams[d]):
+                    dsts[d].copy_(src, non_blocking=True)
+            for d in peers:
+                streams[d].synchronize()
+        t = self.timeit(all_at_once, iters=5, warmup=2)
+        out["all_peers_GBps"] = round(len(peers) * nbytes / t / 1e9, 1)
+        del dsts, src
+        torch.cuda.empty_cache()
+        return out
+
+    # ------------------------------------------------------------------ main
+    def run(self) -> dict:
+        from ..parallel.comm import init_distributed
+        if self.on_gpu:
+            self.torch.cuda.set_device(self.dev)
+        init_distributed(self.world, backend=self.backend, device=self.dev if self.on_gpu else None)
+        res = {"status": "ok", "ranks": self.world, "backend": self.backend, "shared_gpu": self.shared}
+        tp_model = MODEL_TP if self.on_gpu else "tiny-llama"
+        ep_model = MODEL_EP if self.on_gpu else "tiny-mixtral"
+        sections = [("collectives", self.collectives),
+                    ("tp", lambda: self.sharded_vs_full(tp_model, "allreduce")),
+                    ("ep", lambda: self.sharded_vs_full(ep_model, "a2a")),
+                    ("p2p", self.p2p)]
+        from ..models.config import get_model_config
+        for name, fn in sections:
+            if name == "ep" and get_model_config(ep_model).num_experts % self.world:
+                res[name] = {"skipped": f"{self.world} ranks do not divide the experts"}
+                continue
+            t0 = time.perf_counter()
+            try:
+                res[name] = fn()
+            except Exception as e:  # noqa: BLE001 - report, keep the other sections
+                traceback.print_exc()
+                res[name] = {"status": "failed", "error": repr(e)[:300]}
+            if isinstance(res[name], dict):
+                res[name]["wall_s"] = round(time.perf_counter() - t0, 1)
+            self.barrier()
+        return res
+
+
+def main() -> int:
+    # keep this process's stdout for the result line only: library chatter goes to stderr
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    sys.stdout = sys.stderr
+    line = sys.stdin.readline()
+    if line.strip() != "go":  # the bench rank ended (or failed) before its serving phases finished
+        return 0
+    t0 = time.perf_counter()
+    try:
+        p = Probe()
+        res = p.run()
+        res["wall_s"] = round(time.perf_counter() - t0, 1)
+        if p.rank == 0:
+            result_out.write("PROBE " + json.dumps(res) + "\n")
+            result_out.flush()
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        traceback.print_exc()
+        result_out.write("PROBE " + json.dumps({"status": "failed", "error": repr(e)[:300]}) + "\n")
+        result_out.flush()
+        return 1
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

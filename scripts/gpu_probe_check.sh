@@ -1,0 +1,5 @@
+# bench.py --gpus 2 on a 1-GPU box: agg x2 + disagg 1P+1D + the multi-GPU probe (ranks share the GPU)
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 900 python bench.py --gpus 2 --steps 20 --warmup 5 > gpurun_out/s4_bench_g2.json 2> gpurun_out/s4_bench_g2.err && echo BENCH2_OK
+tail -c 3000 gpurun_out/s4_bench_g2.json

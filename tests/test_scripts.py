@@ -186,7 +186,7 @@ def test_bench_contract_cpu(mode, nproc, launcher, tmp_path):
         port = s.getsockname()[1]
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "12", "--warmup", "8", "--qps", "8",
            "--mode", mode, "--device", "cpu", "--gpus", str(nproc), "--max-warmup-s", "8",
-           "--steady-window-s", "1", "--min-ttft-samples", "5"]
+           "--steady-window-s", "1", "--min-ttft-samples", "5", "--disagg-qps", "4"]
     if launcher == "torchrun":
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(port)] + cmd[1:]
@@ -207,6 +207,14 @@ def test_bench_contract_cpu(mode, nproc, launcher, tmp_path):
     if want == "both":
         assert d["agg"]["value"] == d["value"] and d["disagg"]["value"] > 0
         assert d["disagg"]["parallelism"] == f"disagg {nproc // 2}P+{nproc // 2}D"
+    if nproc >= 2:  # the multi-GPU probe (mxserve/tools/mgpu_probe.py) ran after the serving phases
+        pr = d["multi_gpu_probe"]
+        assert pr["status"] == "ok" and pr["ranks"] == nproc, pr
+        assert pr["collectives"]["all_reduce"] and pr["p2p"].get("skipped"), pr
+        for sec in ("tp", "ep"):  # sharded (TP / EP over gloo) vs the unsharded model on rank 0
+            assert pr[sec]["max_rel_err"] < 1e-4 and pr[sec]["argmax_agreement_min"] == 1.0, pr[sec]
+    else:
+        assert "multi_gpu_probe" not in d
 
 
 def test_bench_rejects_world_mismatch(tmp_path):
