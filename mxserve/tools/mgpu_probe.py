@@ -14,6 +14,10 @@ IPC all-reduce carrying the model's collectives (ranks sharing one GPU) -- and m
                64-token batch at TP=N vs TP=1
   ep           Mixtral-8x7B layer shapes (2 layers), experts sharded EP=N with the device-side IPC
                token dispatch, against the unsharded model
+  tp_engine    the full Llama-3-70B (80 layers, random weights; BASELINE config 4) as a TP=N serving
+               engine -- rank 0 schedules, ranks 1..N-1 mirror its steps (ModelRunner.follower_loop),
+               decode in hipGraphs with the custom all-reduce captured -- 64 requests of 512 prompt
+               tokens, 64 output tokens each: median decode step (the ITL at batch 64) and prefill rate
   p2p          rank 0: peer copy bandwidth to every other GPU it sees, one link at a time and all
                links at once (hipMemcpyPeer over xGMI)
 
@@ -31,6 +35,7 @@ import traceback
 
 MODEL_TP = "meta-llama/Meta-Llama-3-70B-Instruct@layers=2"
 MODEL_EP = "mistralai/Mixtral-8x7B-Instruct-v0.1@layers=2"
+MODEL_TP_ENGINE = "meta-llama/Meta-Llama-3-70B-Instruct"
 
 
 def _md(n, dev):
@@ -170,6 +175,66 @@ class Probe:
             res["ranks_consistent"] = all(bool((torch.from_numpy(p) == torch.from_numpy(parts[0])).all()) for p in parts)
         return res
 
+    def tp_engine(self, model: str, batch: int = 64, isl: int = 512, osl: int = 64) -> dict:
+        from ..config import EngineArgs
+        from ..engine.model_runner import ModelRunner
+        from ..models.config import get_model_config
+        torch = self.torch
+        if not self.on_gpu:
+            batch, isl, osl = 8, 48, 8
+        blocks = batch * (-(-(isl + osl) // 16)) + 256
+        args = EngineArgs(model=model, device="cuda" if self.on_gpu else "cpu", tensor_parallel_size=self.world,
+                          max_num_seqs=batch, cuda_graph_max_bs=batch, max_model_len=isl + osl + 64,
+                          num_gpu_blocks=blocks, cpu_num_blocks=blocks, load_format="random", seed=7)
+        if self.rank != 0:  # mirror rank 0's steps until it shuts the group down
+            runner = ModelRunner(args, get_model_config(model))
+            runner.follower_loop()
+            runner.close()
+            del runner
+            if self.on_gpu:
+                torch.cuda.empty_cache()
+            return {}
+        from ..engine.engine import LLMEngine
+        from ..engine.request import SamplingParams
+        t0 = time.perf_counter()
+        eng = LLMEngine(args)
+        t_build = time.perf_counter() - t0
+        g = torch.Generator().manual_seed(3)
+        vocab = eng.model_config.vocab_size
+        sp = SamplingParams(max_tokens=osl, temperature=0.0, ignore_eos=True)
+        for i in range(batch):
+            eng.add_request(torch.randint(100, vocab - 100, (isl,), generator=g).tolist(), sp, request_id=f"tp{i}")
+        steps = []  # (wall seconds since the previous step returned, outputs returned)
+        t_prev = t_start = time.perf_counter()
+        first_all = None
+        seen = set()
+        while eng.has_unfinished():
+            outs = eng.step()
+            now = time.perf_counter()
+            steps.append((now - t_prev, len(outs)))
+            t_prev = now
+            seen.update(o.request_id for o in outs)
+            if first_all is None and len(seen) == batch:
+                first_all = now - t_start
+        total = time.perf_counter() - t_start
+        dec = sorted(dt for dt, n in steps if n == batch)
+        res = {"model": model, "tp": self.world, "batch": batch, "isl": isl, "osl": osl,
+               "engine_build_s": round(t_build, 1), "graphs": sorted(eng.runner.graphs),
+               "decode_steps": len(dec),
+               "decode_step_ms_p50": round(1e3 * dec[len(dec) // 2], 3) if dec else None,
+               "decode_tok_per_s": round(batch / dec[len(dec) // 2], 1) if dec else None,
+               "prefill_tok_per_s": round(batch * isl / first_all, 1) if first_all else None,
+               "total_s": round(total, 2)}
+        st = eng.runner
+        from ..parallel.comm import get_tp
+        car = get_tp().custom_ar
+        res["custom_all_reduce"] = car is not None and not car.disabled
+        eng.close()
+        del eng, st
+        if self.on_gpu:
+            torch.cuda.empty_cache()
+        return res
+
     def p2p(self) -> dict:
         torch = self.torch
         if not self.on_gpu or self.ndev < 2 or self.rank != 0:
@@ -208,6 +273,7 @@ class Probe:
         sections = [("collectives", self.collectives),
                     ("tp", lambda: self.sharded_vs_full(tp_model, "allreduce")),
                     ("ep", lambda: self.sharded_vs_full(ep_model, "a2a")),
+                    ("tp_engine", lambda: self.tp_engine(MODEL_TP_ENGINE if self.on_gpu else "tiny-llama")),
                     ("p2p", self.p2p)]
         from ..models.config import get_model_config
         for name, fn in sections:
