@@ -18,6 +18,8 @@ IPC all-reduce carrying the model's collectives (ranks sharing one GPU) -- and m
                engine -- rank 0 schedules, ranks 1..N-1 mirror its steps (ModelRunner.follower_loop),
                decode in hipGraphs with the custom all-reduce captured -- 64 requests of 512 prompt
                tokens, 64 output tokens each: median decode step (the ITL at batch 64) and prefill rate
+  ep_engine    the full Mixtral-8x7B the same way with its experts sharded EP=N (tokens dispatched to
+               the expert owners by the device-side IPC all-to-all; BASELINE config 5's EP)
   p2p          rank 0: peer copy bandwidth to every other GPU it sees, one link at a time and all
                links at once (hipMemcpyPeer over xGMI)
 
@@ -36,6 +38,7 @@ import traceback
 MODEL_TP = "meta-llama/Meta-Llama-3-70B-Instruct@layers=2"
 MODEL_EP = "mistralai/Mixtral-8x7B-Instruct-v0.1@layers=2"
 MODEL_TP_ENGINE = "meta-llama/Meta-Llama-3-70B-Instruct"
+MODEL_EP_ENGINE = "mistralai/Mixtral-8x7B-Instruct-v0.1"
 
 
 def _md(n, dev):
@@ -175,7 +178,8 @@ class Probe:
             res["ranks_consistent"] = all(bool((torch.from_numpy(p) == torch.from_numpy(parts[0])).all()) for p in parts)
         return res
 
-    def tp_engine(self, model: str, batch: int = 64, isl: int = 512, osl: int = 64) -> dict:
+    def tp_engine(self, model: str, moe_dispatch: str = "allreduce", batch: int = 64, isl: int = 512,
+                  osl: int = 64) -> dict:
         from ..config import EngineArgs
         from ..engine.model_runner import ModelRunner
         from ..models.config import get_model_config
@@ -185,7 +189,8 @@ class Probe:
         blocks = batch * (-(-(isl + osl) // 16)) + 256
         args = EngineArgs(model=model, device="cuda" if self.on_gpu else "cpu", tensor_parallel_size=self.world,
                           max_num_seqs=batch, cuda_graph_max_bs=batch, max_model_len=isl + osl + 64,
-                          num_gpu_blocks=blocks, cpu_num_blocks=blocks, load_format="random", seed=7)
+                          num_gpu_blocks=blocks, cpu_num_blocks=blocks, load_format="random", seed=7,
+                          moe_dispatch=moe_dispatch)
         if self.rank != 0:  # mirror rank 0's steps until it shuts the group down
             runner = ModelRunner(args, get_model_config(model))
             runner.follower_loop()
@@ -218,7 +223,7 @@ class Probe:
                 first_all = now - t_start
         total = time.perf_counter() - t_start
         dec = sorted(dt for dt, n in steps if n == batch)
-        res = {"model": model, "tp": self.world, "batch": batch, "isl": isl, "osl": osl,
+        res = {"model": model, "tp": self.world, "moe_dispatch": moe_dispatch, "batch": batch, "isl": isl, "osl": osl,
                "engine_build_s": round(t_build, 1), "graphs": sorted(eng.runner.graphs),
                "decode_steps": len(dec),
                "decode_step_ms_p50": round(1e3 * dec[len(dec) // 2], 3) if dec else None,
@@ -274,10 +279,11 @@ class Probe:
                     ("tp", lambda: self.sharded_vs_full(tp_model, "allreduce")),
                     ("ep", lambda: self.sharded_vs_full(ep_model, "a2a")),
                     ("tp_engine", lambda: self.tp_engine(MODEL_TP_ENGINE if self.on_gpu else "tiny-llama")),
+                    ("ep_engine", lambda: self.tp_engine(MODEL_EP_ENGINE if self.on_gpu else "tiny-mixtral", "a2a")),
                     ("p2p", self.p2p)]
         from ..models.config import get_model_config
         for name, fn in sections:
-            if name == "ep" and get_model_config(ep_model).num_experts % self.world:
+            if name in ("ep", "ep_engine") and get_model_config(ep_model).num_experts % self.world:
                 res[name] = {"skipped": f"{self.world} ranks do not divide the experts"}
                 continue
             t0 = time.perf_counter()
