@@ -97,6 +97,8 @@ def parse(argv=None):
                     help="TTFT samples per request-owning rank collected in steady state before timing")
     ap.add_argument("--phase-timeout-s", type=float, default=float(os.environ.get("MXS_BENCH_PHASE_TIMEOUT", "420")),
                     help="a disagg phase that has not finished by then is reported as failed")
+    ap.add_argument("--num-gpu-blocks", type=int, default=None,
+                    help="KV pool size per rank (default: what the GPU's free memory allows)")
     ap.add_argument("--probe-timeout-s", type=float, default=float(os.environ.get("MXS_BENCH_PROBE_TIMEOUT", "300")),
                     help="N >= 2: budget of the multi-GPU probe run after the serving phases (0: no probe)")
     return ap.parse_args(argv)
@@ -526,6 +528,8 @@ def engine_args(a, ctx, **kw):
         args = args.replace(model="tiny-llama", max_model_len=1024, cpu_num_blocks=4096)
     elif ctx.shared_gpu:  # functional run: ranks share a GPU, split its memory
         args = args.replace(num_gpu_blocks=int(os.environ.get("MXS_BENCH_SHARED_BLOCKS", "40000")))
+    if a.num_gpu_blocks and ctx.on_gpu:
+        args = args.replace(num_gpu_blocks=a.num_gpu_blocks)
     return args
 
 

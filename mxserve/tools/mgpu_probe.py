@@ -20,6 +20,10 @@ IPC all-reduce carrying the model's collectives (ranks sharing one GPU) -- and m
                tokens, 64 output tokens each: median decode step (the ITL at batch 64) and prefill rate
   ep_engine    the full Mixtral-8x7B the same way with its experts sharded EP=N (tokens dispatched to
                the expert owners by the device-side IPC all-to-all; BASELINE config 5's EP)
+  disagg_8b    Llama-3-8B disaggregated 1P+1D (BASELINE config 3): ranks [0, N/2) prefill, [N/2, N)
+               decode, the KV of each prompt pushed over xGMI into the decode GPU's arena -- bench.py's
+               disagg phase (Poisson arrivals, ISL 4000 / OSL 500, steady-state warmup) at 4 req/s per
+               pair: TTFT (KV transfer included) and ITL
   p2p          rank 0: peer copy bandwidth to every other GPU it sees, one link at a time and all
                links at once (hipMemcpyPeer over xGMI)
 
@@ -39,6 +43,7 @@ MODEL_TP = "meta-llama/Meta-Llama-3-70B-Instruct@layers=2"
 MODEL_EP = "mistralai/Mixtral-8x7B-Instruct-v0.1@layers=2"
 MODEL_TP_ENGINE = "meta-llama/Meta-Llama-3-70B-Instruct"
 MODEL_EP_ENGINE = "mistralai/Mixtral-8x7B-Instruct-v0.1"
+MODEL_DISAGG = "meta-llama/Meta-Llama-3-8B-Instruct"
 
 
 def _md(n, dev):
@@ -240,6 +245,57 @@ class Probe:
             torch.cuda.empty_cache()
         return res
 
+    def disagg(self, model: str, qps_per_gpu: float) -> dict:
+        """bench.py's disaggregated phase on this probe group (each engine TP = 1)."""
+        import torch.distributed as dist
+        from ..parallel import comm
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        if root not in sys.path:
+            sys.path.insert(0, root)
+        import bench
+        st = comm.get_tp()
+        n = self.world
+        if n % 2:
+            return {"skipped": "needs an even number of ranks"}
+        argv = ["--model", model, "--disagg-qps", str(qps_per_gpu), "--steps", "600", "--warmup", "100",
+                "--max-warmup-s", "45", "--steady-window-s", "2.5", "--min-ttft-samples", "25",
+                "--device", "auto" if self.on_gpu else "cpu", "--disagg-max-num-seqs", "64",
+                "--num-gpu-blocks", "40000"]
+        if not self.on_gpu:
+            argv += ["--steps", "12", "--warmup", "8", "--max-warmup-s", "8", "--steady-window-s", "1",
+                     "--min-ttft-samples", "5", "--disagg-qps", "4"]
+        a = bench.parse(argv)
+        probe = self
+        pg_decode = dist.new_group(list(range(n // 2, n)), backend="gloo")
+
+        class Ctx(bench.Ctx):  # the probe's process group instead of a new one; control over gloo
+            def __init__(self):
+                self.torch, self.dist = probe.torch, dist
+                self.world, self.rank, self.local = n, probe.rank, probe.local
+                self.on_gpu, self.ndev, self.shared_gpu = probe.on_gpu, probe.ndev, probe.shared
+                self.pg_decode = pg_decode
+                self.sync = probe.sync
+
+            def barrier(self):
+                dist.barrier(group=st.cpu_group)
+                self.sync()
+
+            def gather(self, vals):
+                import numpy as np
+                t = probe.torch.tensor(vals, dtype=probe.torch.float64)
+                parts = [probe.torch.zeros_like(t) for _ in range(n)]
+                dist.all_gather(parts, t, group=st.cpu_group)
+                return np.stack([p.numpy() for p in parts])
+
+        comm.set_tp(comm.ParallelState())  # every engine here is TP = 1
+        try:
+            col, info = bench.phase_disagg(a, Ctx(), int(os.environ.get("MASTER_PORT", "29500")) + 101)
+        finally:
+            comm.set_tp(st)
+        res = bench.summarize(col, a.steps, list(range(n // 2, n)))
+        res.update(info, model=model, parallelism=f"disagg {n // 2}P+{n // 2}D", qps_per_pair=2 * qps_per_gpu)
+        return res
+
     def p2p(self) -> dict:
         torch = self.torch
         if not self.on_gpu or self.ndev < 2 or self.rank != 0:
@@ -280,6 +336,7 @@ class Probe:
                     ("ep", lambda: self.sharded_vs_full(ep_model, "a2a")),
                     ("tp_engine", lambda: self.tp_engine(MODEL_TP_ENGINE if self.on_gpu else "tiny-llama")),
                     ("ep_engine", lambda: self.tp_engine(MODEL_EP_ENGINE if self.on_gpu else "tiny-mixtral", "a2a")),
+                    ("disagg_8b", lambda: self.disagg(MODEL_DISAGG if self.on_gpu else "tiny-llama", 2.0)),
                     ("p2p", self.p2p)]
         from ..models.config import get_model_config
         for name, fn in sections:
