@@ -339,6 +339,9 @@ class Probe:
                     ("disagg_8b", lambda: self.disagg(MODEL_DISAGG if self.on_gpu else "tiny-llama", 2.0)),
                     ("p2p", self.p2p)]
         from ..models.config import get_model_config
+        only = [x for x in os.environ.get("MXS_PROBE_SECTIONS", "").split(",") if x]
+        if only:  # a subset (GPU tests)
+            sections = [(nm, fn) for nm, fn in sections if nm in only]
         for name, fn in sections:
             if name in ("ep", "ep_engine") and get_model_config(ep_model).num_experts % self.world:
                 res[name] = {"skipped": f"{self.world} ranks do not divide the experts"}

@@ -40,6 +40,9 @@ def _rank(rank, world, port, model, q, moe_dispatch="allreduce"):
         from mxserve.models.config import get_model_config
         runner = ModelRunner(_args(model, world, moe_dispatch), get_model_config(model))
         runner.follower_loop()
+    # tear the gloo group down before the interpreter exits (its threads otherwise can abort at exit)
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
 
 
 @pytest.mark.parametrize("model,moe_dispatch", [("tiny-llama", "allreduce"), ("tiny-mixtral", "allreduce"),
