@@ -24,8 +24,14 @@ Workload: ISL 4000 / OSL 500, the only request shape the reference quantifies
 (examples/dgdr/trtllm/dgdr.yaml:22-26).  Synthetic random prompt token ids, random-init weights of
 the real architecture (no network on the GPU box); every request generates exactly OSL tokens.
 
-Steps and steady state.  A step is one engine iteration (continuous batching: decodes + chunked
-prefill under the token budget) of a request-owning rank.  The warmup runs at least W steps and
+Steps and steady state.  A step is --iters-per-step (default 50) engine iterations (continuous
+batching: decodes + chunked prefill under the token budget) of a request-owning rank.  Under an
+open-loop Poisson load the token rate of a short window follows the running set, which drifts with
+the arrivals of the last request lifetime (~4 s here), and the number of prefill-carrying iterations
+in it: measured on one MI355X at QPS 40-42, 20 windows of 20 iterations (0.2 s) spread 17.3-21.1k
+tok/s and windows of 200 iterations (2 s) 16.9-19.8k, against ~20.3k over 1,500 iterations.  K = 20
+steps of 50 iterations is a ~9 s window, a couple of request lifetimes.  The
+warmup runs at least W steps and
 until the open-loop system is in steady state on every rank: over the last two windows the mean
 running set is flat and completions match arrivals (or --max-warmup-s passes; reported).  Then a
 short soak collects TTFT samples in steady state, and exactly K steps are timed between a
@@ -66,8 +72,11 @@ def vlog(msg: str) -> None:
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1500)
-    ap.add_argument("--warmup", type=int, default=500)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--iters-per-step", type=int, default=int(os.environ.get("MXS_BENCH_ITERS_PER_STEP", "50")),
+                    help="engine iterations per bench step (see the module docstring: a window must span a few "
+                         "request lifetimes for the token rate of an open-loop Poisson load to settle)")
     ap.add_argument("--mode", choices=["auto", "agg", "disagg", "both"], default=os.environ.get("MXS_BENCH_MODE", "auto"))
     ap.add_argument("--model", default="meta-llama/Llama-3.2-1B-Instruct")
     ap.add_argument("--isl", type=int, default=4000)
@@ -271,7 +280,7 @@ def timed_phases(a, step, barrier, agree, drv, running, on_phase=lambda phase: N
         i += 1
         if i % check_every == 0:
             timed_out = time.perf_counter() - drv.t_start > a.max_warmup_s
-            mine = i >= a.warmup and (drv.is_steady(a.steady_window_s) or timed_out)
+            mine = i >= a.warmup * a.iters_per_step and (drv.is_steady(a.steady_window_s) or timed_out)
             if i % 200 == 0:
                 vlog(f"warmup step {i}: {drv.nxt} arrivals, {drv.finished} finished, running {running()}")
             if agree(mine):
@@ -293,9 +302,10 @@ def timed_phases(a, step, barrier, agree, drv, running, on_phase=lambda phase: N
     drv.record = True
     t0 = time.perf_counter()
     for i in range(a.steps):
-        step()
-        drv.sample(running())
-        if i % 200 == 0:
+        for _ in range(a.iters_per_step):  # one bench step = a fixed number of engine iterations
+            step()
+            drv.sample(running())
+        if i % 20 == 0:
             vlog(f"timed step {i}: {drv.c['tokens']} tokens")
     on_phase("stop")
     barrier()
@@ -689,6 +699,7 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": head["ms_per_step"],
+        "engine_iterations_per_step": a.iters_per_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -257,12 +257,12 @@ class Probe:
         n = self.world
         if n % 2:
             return {"skipped": "needs an even number of ranks"}
-        argv = ["--model", model, "--disagg-qps", str(qps_per_gpu), "--steps", "600", "--warmup", "100",
+        argv = ["--model", model, "--disagg-qps", str(qps_per_gpu), "--steps", "60", "--warmup", "10", "--iters-per-step", "10",
                 "--max-warmup-s", "45", "--steady-window-s", "2.5", "--min-ttft-samples", "25",
                 "--device", "auto" if self.on_gpu else "cpu", "--disagg-max-num-seqs", "64",
                 "--num-gpu-blocks", "40000"]
         if not self.on_gpu:
-            argv += ["--steps", "12", "--warmup", "8", "--max-warmup-s", "8", "--steady-window-s", "1",
+            argv += ["--steps", "12", "--warmup", "8", "--iters-per-step", "1", "--max-warmup-s", "8", "--steady-window-s", "1",
                      "--min-ttft-samples", "5", "--disagg-qps", "4"]
         a = bench.parse(argv)
         probe = self

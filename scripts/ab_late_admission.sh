@@ -1,4 +1,5 @@
 #!/usr/bin/env bash
+export MXS_BENCH_ITERS_PER_STEP=${MXS_BENCH_ITERS_PER_STEP:-1}  # the --steps / --warmup counts below are engine iterations
 # Interleaved A/B of late admission (engine/pacing.py) on the headline bench, in one box session:
 # off / on / off / on ... with N timed steps each; one JSON line per run in $OUT/ab.jsonl.
 #   scripts/ab_late_admission.sh [ROUNDS] [STEPS] [OUT]

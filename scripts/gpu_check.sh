@@ -1,4 +1,5 @@
 #!/usr/bin/env bash
+export MXS_BENCH_ITERS_PER_STEP=${MXS_BENCH_ITERS_PER_STEP:-1}  # the --steps / --warmup counts below are engine iterations
 # One gpurun call: kernel numerics, smoke, short bench, rocprofv3 kernel stats.
 set -euo pipefail
 cd "$(dirname "$0")/.."

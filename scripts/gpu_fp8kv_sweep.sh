@@ -1,4 +1,5 @@
 # labelled side data point: the headline workload with an fp8 (e4m3fn) KV cache at higher request rates
+export MXS_BENCH_ITERS_PER_STEP=${MXS_BENCH_ITERS_PER_STEP:-1}  # the --steps / --warmup counts below are engine iterations
 set -o pipefail
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out

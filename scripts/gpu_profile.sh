@@ -1,4 +1,5 @@
 #!/usr/bin/env bash
+export MXS_BENCH_ITERS_PER_STEP=${MXS_BENCH_ITERS_PER_STEP:-1}  # the --steps / --warmup counts below are engine iterations
 # rocprofv3 kernel-trace stats of a bench run (summaries only; traces deleted to stay under 64 MiB).
 set -euo pipefail
 cd "$(dirname "$0")/.."

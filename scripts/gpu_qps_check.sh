@@ -1,4 +1,5 @@
 #!/usr/bin/env bash
+export MXS_BENCH_ITERS_PER_STEP=${MXS_BENCH_ITERS_PER_STEP:-1}  # the --steps / --warmup counts below are engine iterations
 # Longer timed window at the candidate default operating points (steady-state check).
 set -euo pipefail
 cd "$(dirname "$0")/.."

@@ -202,6 +202,7 @@ def test_bench_contract_cpu(mode, nproc, launcher, tmp_path):
         assert k in d, k
     assert d["n_gpus"] == nproc and d["steps"] == 12 and d["warmup"] == 8 and d["value"] > 0
     assert d["requests_with_first_token"] >= 5
+    assert d["engine_iterations_per_step"] == 50
     want = {"auto": "agg" if nproc == 1 else "both"}.get(mode, mode)
     assert d["config"]["mode"] == want
     if want == "both":
