@@ -10,6 +10,10 @@ __global__ void __launch_bounds__(256) copy_blocks_kernel(char* __restrict__ dst
                                                           const int* __restrict__ src_ids,
                                                           const int* __restrict__ dst_ids, long block_bytes) {
   MXS_KCHECK(src_ids[blockIdx.x] >= 0 && dst_ids[blockIdx.x] >= 0);
+  // the source may have been written by ANOTHER GPU over xGMI (a decode worker landing its staging
+  // arena after the prefill GPU's push, published through the host): acquire at system scope so no
+  // stale line of an earlier use of the arena is read from this GPU's caches
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const long s = static_cast<long>(src_ids[blockIdx.x]) * block_bytes;
   const long d = static_cast<long>(dst_ids[blockIdx.x]) * block_bytes;
   const uint4* sp = reinterpret_cast<const uint4*>(src + s);
@@ -25,6 +29,10 @@ __global__ void __launch_bounds__(256) copy_blocks_kernel(char* __restrict__ dst
     dp[i + 768] = e;
   }
   for (; i < n; i += 256) dp[i] = sp[i];
+  // the destination may be another GPU's memory: make the stores visible at system scope before this
+  // wave retires, so the host's completion of the launch means the peer can read them
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 void launch_copy_blocks(char* dst, const char* src, const int* src_ids, const int* dst_ids, int n,
