@@ -254,6 +254,7 @@ class AsyncEngine:
         self.on_step = None  # optional callback(list[StepOutput]) run on the engine thread
         self._ring = None  # (cmd ring, out ring, handler): a streamer process owns the request plane
         self.last_stats: dict = engine.stats()
+        self._stats_t = 0.0
         engine.admit_hook = self._admit  # late admission: arrivals up to the last moment join the next step
         self._thread = threading.Thread(target=self._loop, name="mxs-engine", daemon=True)
         self._thread.start()
@@ -296,7 +297,10 @@ class AsyncEngine:
             except Exception:  # noqa: BLE001 - fail the in-flight requests, keep serving
                 log.exception("engine step failed")
                 outs = self._fail_all()
-            self.last_stats = self.engine.stats()
+            now = time.monotonic()
+            if now - self._stats_t >= 0.02:  # readers (heartbeat load, /metrics) poll far slower
+                self.last_stats = self.engine.stats()
+                self._stats_t = now
             if self.on_step is not None:
                 try:
                     self.on_step(outs)
