@@ -12,11 +12,15 @@ Phases (--mode auto: agg for N = 1, agg then disagg for N >= 2, both in the one 
           `replicas:` of single-GPU workers behind the frontend router (examples/deploy/vllm/agg.yaml:14,21;
           SURVEY.md §2.4 P01) -- under an open-loop Poisson arrival process of --qps requests/s
           per GPU (weak scaling).  `value` is this phase.
-  disagg  ranks [0, N/2) prefill, [N/2, N) decode, paired 1P:1D (examples/deploy/vllm/disagg.yaml:18-57).
-          Requests arrive at the decode rank at 2 x --disagg-qps per pair (default 32 / GPU, below
-          the agg rate: at ISL 4000 the decode GPU of a 1:1 pair is KV-bandwidth bound at ~78
-          req/s, while its prefill GPU would idle 30-45 %; see --disagg-qps); it reserves KV blocks and hands the prompt to its prefill rank, which computes it, pushes
-          the blocks into the decode rank's staging arena with the IPC copy kernel (xGMI between
+  disagg  ranks [0, P) prefill, [P, N) decode (examples/deploy/vllm/disagg.yaml:18-57: separate
+          prefill and decode workers, each scaled by its own `replicas`).  disagg_plan() sizes P:D
+          from the two roles' capacities for this workload (a decode GPU is KV-bandwidth bound at
+          ~76 req/s, a prefill GPU computes ~118 req/s: 1P+1D at N = 2, 2P+2D at 4, 3P+5D at 8)
+          and offers the node the rate that loads the tighter role to 85 % (32 req/s per GPU at
+          N = 2 and 4, 37.6 at 8; the agg rate of 42 would overload a 1:1 split's decode GPU).
+          Requests arrive at the decode ranks; decode rank j hands its prompts to prefill rank
+          (j - P) mod P.  The decode rank reserves KV blocks and hands the prompt to its prefill
+          rank, which computes it, pushes the blocks into the decode rank's staging arena with the IPC copy kernel (xGMI between
           GPUs; mxserve/disagg/kv_transfer.py) and returns the first token.  TTFT includes the
           KV transfer.
 
@@ -86,10 +90,10 @@ def parse(argv=None):
     ap.add_argument("--max-num-seqs", type=int, default=384)
     ap.add_argument("--disagg-max-num-seqs", type=int, default=512,
                     help="decode ranks of the disagg phase carry 2x the per-GPU request rate")
-    ap.add_argument("--disagg-qps", type=float, default=float(os.environ.get("MXS_BENCH_DISAGG_QPS", "32")),
-                    help="disagg phase arrival rate per GPU (a 1P+1D pair takes 2x): a decode GPU streams the "
-                         "KV of every running request each step, so at ISL 4000 it sustains ~39k tok/s (~78 "
-                         "req/s of OSL 500); the agg rate (42/GPU) would overload the decode half of a 1:1 split")
+    ap.add_argument("--disagg-qps", type=float, default=float(os.environ.get("MXS_BENCH_DISAGG_QPS", "0")),
+                    help="disagg phase arrival rate per GPU; 0 = from the capacity model of disagg_plan()")
+    ap.add_argument("--disagg-prefill-ranks", type=int, default=int(os.environ.get("MXS_BENCH_DISAGG_P", "0")),
+                    help="prefill ranks of the disagg phase (the rest decode); 0 = disagg_plan()")
     ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--enforce-eager", action="store_true")
@@ -111,6 +115,30 @@ def parse(argv=None):
     ap.add_argument("--probe-timeout-s", type=float, default=float(os.environ.get("MXS_BENCH_PROBE_TIMEOUT", "300")),
                     help="N >= 2: budget of the multi-GPU probe run after the serving phases (0: no probe)")
     return ap.parse_args(argv)
+
+
+# Capacity of one MI355X in the disagg roles for the headline workload (Llama-3.2-1B, ISL 4000 / OSL
+# 500, bf16): a prefill GPU computes ~476k prompt tok/s in 8192-token chunks (17.2 ms each,
+# profiles/r2_decode_step_microbench/mb_1b_256.jsonl) = ~118 req/s; a decode GPU streams every running
+# request's KV each step (~136 MB at a 4.25k context, ~22 us at 6.1 TB/s) and sustains ~38k tok/s at
+# 512 running = ~76 req/s.
+_CAP_PREFILL, _CAP_DECODE, _DISAGG_UTIL = 118.0, 76.0, 0.85
+
+
+def disagg_plan(a, world: int) -> tuple:
+    """(prefill ranks, decode ranks, arrival rate per GPU) of the disagg phase.  The split follows the
+    two roles' capacities (~3 prefill : 5 decode GPUs for this workload; 1:1 below 4 GPUs), and the
+    node rate loads the tighter role to 85 %.  Other models: a 1:1 split at --qps x 0.76."""
+    p = a.disagg_prefill_ranks
+    headline = a.model == "meta-llama/Llama-3.2-1B-Instruct" and a.isl == 4000 and a.osl == 500
+    if p <= 0:
+        p = max(1, round(world * _CAP_DECODE / (_CAP_PREFILL + _CAP_DECODE))) if headline else world // 2
+    p = min(max(1, p), world - 1)
+    d = world - p
+    qps = a.disagg_qps
+    if qps <= 0:
+        qps = (_DISAGG_UTIL * min(p * _CAP_PREFILL, d * _CAP_DECODE) / world) if headline else 0.76 * a.qps
+    return p, d, qps
 
 
 # ---------------------------------------------------------------------------- launcher
@@ -343,23 +371,28 @@ def run_agg(a, eng, sp, drv, barrier, agree) -> float:
     return timed_phases(a, step, barrier, agree, drv, lambda: len(sch.running) + len(sch.waiting))
 
 
-def _pair_conn(rank: int, world: int, is_decode: bool, base_port: int):
-    """Host control channel between a prefill rank and its decode rank (same node)."""
+def _disagg_conns(rank: int, p: int, world: int, base_port: int) -> list:
+    """Host control channels of the disagg phase: decode rank j (ranks [p, world)) listens on
+    base_port + j; prefill rank i serves the decode ranks j with (j - p) % p == i."""
     from multiprocessing.connection import Client, Listener
-    half = world // 2
-    pair = rank - half if is_decode else rank
-    port = base_port + pair
-    if is_decode:
-        lst = Listener(("127.0.0.1", port), authkey=b"mxs-bench")
+    if rank >= p:
+        lst = Listener(("127.0.0.1", base_port + rank), authkey=b"mxs-bench")
         conn = lst.accept()
         lst.close()
-        return conn
-    for _ in range(1200):
-        try:
-            return Client(("127.0.0.1", port), authkey=b"mxs-bench")
-        except OSError:
-            time.sleep(0.1)
-    raise RuntimeError("could not reach the decode rank")
+        return [conn]
+    conns = []
+    for j in range(p, world):
+        if (j - p) % p != rank:
+            continue
+        for _ in range(1200):
+            try:
+                conns.append(Client(("127.0.0.1", base_port + j), authkey=b"mxs-bench"))
+                break
+            except OSError:
+                time.sleep(0.1)
+        else:
+            raise RuntimeError(f"could not reach decode rank {j}")
+    return conns
 
 
 def run_disagg_decode(a, eng, sp, drv, barrier, agree, conn) -> float:
@@ -419,47 +452,57 @@ def run_disagg_decode(a, eng, sp, drv, barrier, agree, conn) -> float:
                         on_phase=lambda ph: conn.send(("phase", ph)))
 
 
-def run_disagg_prefill(eng, temperature: float, barrier, conn) -> int:
-    """Serve the paired decode rank until it says stop, joining its barriers; returns blocks moved."""
+def run_disagg_prefill(eng, temperature: float, barrier, conns: list) -> int:
+    """Serve this rank's decode ranks until they say stop, joining each of their barriers once (a
+    phase's barrier is entered when every served decode rank has announced it); returns blocks moved."""
     from mxserve.disagg.kv_transfer import KVTransferAgent
     from mxserve.engine.request import SamplingParams
     agent = KVTransferAgent(eng.runner, "xgmi")
-    kind, target = conn.recv()
-    assert kind == "desc", kind
-    arena = False
-    if agent.backend == "xgmi" and target["backend"] == "xgmi":
-        try:
-            agent.connect(target)
-            arena = True
-        except (RuntimeError, OSError) as e:  # the decode GPU's arena cannot be mapped here
-            vlog(f"decode arena not mappable ({e!r}); KV goes through the /dev/shm arena")
-    conn.send(("mapped", arena))
-    vlog(f"prefill rank serving (decode arena backend {target['backend']}, mapped={arena})")
+    targets, arenas = [], []
+    for conn in conns:
+        kind, target = conn.recv()
+        assert kind == "desc", kind
+        arena = False
+        if agent.backend == "xgmi" and target["backend"] == "xgmi":
+            try:
+                agent.connect(target)
+                arena = True
+            except (RuntimeError, OSError) as e:  # the decode GPU's arena cannot be mapped here
+                vlog(f"decode arena not mappable ({e!r}); KV goes through the /dev/shm arena")
+        conn.send(("mapped", arena))
+        targets.append(target)
+        arenas.append(arena)
+    vlog(f"prefill rank serving {len(conns)} decode rank(s) (mapped={arenas})")
     pending: dict = {}
+    announced: dict = {}
     moved = 0
     while True:
         stop = False
-        while conn.poll():
-            msg = conn.recv()
-            if msg[0] == "phase":
-                vlog(f"phase {msg[1]}; {moved} blocks pushed so far")
-                barrier()
-                stop = msg[1] == "stop"
-                continue
-            _, rid, toks, dst, skip, start, shm_start = msg
-            eng.add_request(toks, SamplingParams(max_tokens=1, temperature=temperature, ignore_eos=True),
-                            request_id=rid, disagg_role="prefill_only")
-            pending[rid] = (dst, skip, start, shm_start)
+        for ci, conn in enumerate(conns):
+            while conn.poll():
+                msg = conn.recv()
+                if msg[0] == "phase":
+                    announced[msg[1]] = announced.get(msg[1], 0) + 1
+                    if announced[msg[1]] == len(conns):
+                        vlog(f"phase {msg[1]}; {moved} blocks pushed so far")
+                        barrier()
+                        stop = msg[1] == "stop"
+                    continue
+                _, rid, toks, dst, skip, start, shm_start = msg
+                eng.add_request(toks, SamplingParams(max_tokens=1, temperature=temperature, ignore_eos=True),
+                                request_id=rid, disagg_role="prefill_only")
+                pending[rid] = (ci, dst, skip, start, shm_start)
         if stop:
             agent.close()
             return moved
         if not eng.has_unfinished():
-            conn.poll(0.0005)
+            conns[0].poll(0.0005) if len(conns) == 1 else time.sleep(0.0005)
             continue
         for o in eng.step():
             if not o.finished or o.request_id not in pending:
                 continue
-            dst, skip, start, shm_start = pending.pop(o.request_id)
+            ci, dst, skip, start, shm_start = pending.pop(o.request_id)
+            target = targets[ci]
             src = list(eng.requests[o.request_id].block_ids[skip:skip + len(dst)])
             data = None
             if start is not None:
@@ -470,7 +513,7 @@ def run_disagg_prefill(eng, temperature: float, barrier, conn) -> int:
                 data = agent.read_blocks(src)
             moved += len(src)
             eng.release_prefill_blocks(o.request_id)
-            conn.send(("done", o.request_id, o.token_id, data))
+            conns[ci].send(("done", o.request_id, o.token_id, data))
 
 
 # ---------------------------------------------------------------------------- phases
@@ -495,8 +538,8 @@ class Ctx:
             # control plane only (barriers, steady-state votes, stats): replicas share no tensors,
             # and the P->D KV moves over IPC, so a CPU group keeps RCCL out of the measurement
             dist.init_process_group("gloo")
-            if self.world % 2 == 0:
-                self.pg_decode = dist.new_group(list(range(self.world // 2, self.world)), backend="gloo")
+            p = disagg_plan(a, self.world)[0]
+            self.pg_decode = dist.new_group(list(range(p, self.world)), backend="gloo")
         self.sync = torch.cuda.synchronize if self.on_gpu else (lambda: None)
 
     def barrier(self):
@@ -613,7 +656,8 @@ def phase_disagg(a, ctx, base_port: int) -> tuple:
     from mxserve.engine.engine import LLMEngine
     from mxserve.engine.request import SamplingParams
     world, rank = ctx.world, ctx.rank
-    is_prefill = rank < world // 2
+    p, d, qps = disagg_plan(a, world)
+    is_prefill = rank < p
     isl, osl = (a.isl, a.osl) if ctx.on_gpu else (min(a.isl, 200), min(a.osl, 20))
     a2 = argparse.Namespace(**{**vars(a), "isl": isl, "osl": osl})
     if is_prefill:  # prefill-only steps never replay decode graphs
@@ -624,17 +668,20 @@ def phase_disagg(a, ctx, base_port: int) -> tuple:
     vlog("disagg: building engine")
     eng = LLMEngine(args)
     vlog(f"disagg: engine ready ({eng.runner.num_blocks} KV blocks)")
-    conn = _pair_conn(rank, world, not is_prefill, base_port)
+    conns = _disagg_conns(rank, p, world, base_port)
     if is_prefill:
-        run_disagg_prefill(eng, a.temperature, ctx.barrier, conn)
+        run_disagg_prefill(eng, a.temperature, ctx.barrier, conns)
         st = list(_STAT_NAN)
     else:
         sp = SamplingParams(max_tokens=osl, temperature=a.temperature, ignore_eos=True)
-        drv = Driver(a2, rank, eng.model_config.vocab_size, 2 * a.disagg_qps)
-        agree = ctx.agree_fn(ctx.pg_decode, world // 2)
-        st = drv.stats(run_disagg_decode(a2, eng, sp, drv, ctx.barrier, agree, conn))
-    conn.close()
-    info = {"decode_max_num_seqs": a.disagg_max_num_seqs}
+        drv = Driver(a2, rank, eng.model_config.vocab_size, qps * world / d)  # the node's rate over D ranks
+        agree = ctx.agree_fn(ctx.pg_decode, d)
+        st = drv.stats(run_disagg_decode(a2, eng, sp, drv, ctx.barrier, agree, conns[0]))
+    for c in conns:
+        c.close()
+    info = {"decode_max_num_seqs": a.disagg_max_num_seqs, "prefill_ranks": p, "decode_ranks": d,
+            "qps_per_gpu": round(qps, 2), "qps_node": round(qps * world, 2),
+            "qps_per_decode_rank": round(qps * world / d, 2)}
     free_engine(eng, ctx)
     return ctx.gather(st), info
 
@@ -649,8 +696,8 @@ def main():
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; run `python bench.py --gpus N` "
                          "(it spawns the ranks) or launch exactly N ranks")
     mode = a.mode if a.mode != "auto" else ("agg" if world == 1 else "both")
-    if mode in ("disagg", "both") and (world < 2 or world % 2):
-        raise SystemExit("bench.py: the disagg phase needs an even number of GPUs (1 prefill : 1 decode pairs)")
+    if mode in ("disagg", "both") and world < 2:
+        raise SystemExit("bench.py: the disagg phase needs at least 2 GPUs (prefill and decode ranks)")
     probe = start_probe(a, world)  # before Ctx: nothing in this process has touched the GPU yet
     ctx = Ctx(a)
     base_port = int(os.environ.get("MASTER_PORT", "29500")) + 101
@@ -665,9 +712,9 @@ def main():
         dis = run_guarded(lambda: phase_disagg(a, ctx, base_port), a.phase_timeout_s, ctx, agg_info=info,
                           agg=agg, a=a, mode=mode)
         col_d, info_d = dis
-        dis = summarize(col_d, a.steps, list(range(world // 2, world)))
-        dis.update(info_d, parallelism=f"disagg {world // 2}P+{world // 2}D", qps_per_pair=2 * a.disagg_qps,
-                   qps_node=a.disagg_qps * world)
+        p_d = info_d["prefill_ranks"]
+        dis = summarize(col_d, a.steps, list(range(p_d, world)))
+        dis.update(info_d, parallelism=f"disagg {p_d}P+{world - p_d}D")
         if agg is None:
             info = {"kv_blocks": None, "graphs": [], "preemptions": None, "model": a.model,
                     "kv_cache_dtype": "bf16", "isl": a.isl, "osl": a.osl}
@@ -707,7 +754,7 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
         "data": "synthetic (random prompt token ids, random-init weights, Poisson arrivals)",
         "config": {"model": info["model"] if on_gpu else "tiny-llama (CPU plumbing run)",
                    "global_batch": int(world * a.max_num_seqs), "seq_len": info["isl"] + info["osl"],
-                   "parallelism": f"dp{world}" if agg is not None else f"disagg {world // 2}P+{world // 2}D",
+                   "parallelism": f"dp{world}" if agg is not None else (dis or {}).get("parallelism", "disagg"),
                    "mode": mode, "isl": info["isl"], "osl": info["osl"],
                    "qps_per_gpu": a.qps, "qps_node": a.qps * world, "kv_cache_dtype": info["kv_cache_dtype"],
                    "shared_gpu": ctx.shared_gpu},

@@ -257,7 +257,7 @@ class Probe:
         n = self.world
         if n % 2:
             return {"skipped": "needs an even number of ranks"}
-        argv = ["--model", model, "--disagg-qps", str(qps_per_gpu), "--steps", "60", "--warmup", "10", "--iters-per-step", "10",
+        argv = ["--model", model, "--disagg-qps", str(qps_per_gpu), "--disagg-prefill-ranks", str(n // 2), "--steps", "60", "--warmup", "10", "--iters-per-step", "10",
                 "--max-warmup-s", "45", "--steady-window-s", "2.5", "--min-ttft-samples", "25",
                 "--device", "auto" if self.on_gpu else "cpu", "--disagg-max-num-seqs", "64",
                 "--num-gpu-blocks", "40000"]
@@ -293,7 +293,7 @@ class Probe:
         finally:
             comm.set_tp(st)
         res = bench.summarize(col, a.steps, list(range(n // 2, n)))
-        res.update(info, model=model, parallelism=f"disagg {n // 2}P+{n // 2}D", qps_per_pair=2 * qps_per_gpu)
+        res.update(info, model=model, parallelism=f"disagg {n // 2}P+{n // 2}D")
         return res
 
     def p2p(self) -> dict:
@@ -345,6 +345,9 @@ class Probe:
         for name, fn in sections:
             if name in ("ep", "ep_engine") and get_model_config(ep_model).num_experts % self.world:
                 res[name] = {"skipped": f"{self.world} ranks do not divide the experts"}
+                continue
+            if name in ("tp", "tp_engine") and get_model_config(tp_model).num_heads % self.world:
+                res[name] = {"skipped": f"{self.world} ranks do not divide the attention heads"}
                 continue
             t0 = time.perf_counter()
             try:
