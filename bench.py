@@ -18,9 +18,9 @@ Phases (--mode auto: agg for N = 1, agg then disagg for N >= 2, both in the one 
           ~76 req/s, a prefill GPU computes ~118 req/s: 1P+1D at N = 2, 2P+2D at 4, 3P+5D at 8)
           and offers the node the rate that loads the tighter role to 85 % (32 req/s per GPU at
           N = 2 and 4, 37.6 at 8; the agg rate of 42 would overload a 1:1 split's decode GPU).
-          Requests arrive at the decode ranks; decode rank j hands its prompts to prefill rank
-          (j - P) mod P.  The decode rank reserves KV blocks and hands the prompt to its prefill
-          rank, which computes it, pushes the blocks into the decode rank's staging arena with the IPC copy kernel (xGMI between
+          Requests arrive at the decode ranks; a decode rank reserves KV blocks and hands each
+          prompt to the prefill rank with the fewest prompts in flight, which computes it, pushes
+          the blocks into the decode rank's staging arena with the IPC copy kernel (xGMI between
           GPUs; mxserve/disagg/kv_transfer.py) and returns the first token.  TTFT includes the
           KV transfer.
 
@@ -372,18 +372,16 @@ def run_agg(a, eng, sp, drv, barrier, agree) -> float:
 
 
 def _disagg_conns(rank: int, p: int, world: int, base_port: int) -> list:
-    """Host control channels of the disagg phase: decode rank j (ranks [p, world)) listens on
-    base_port + j; prefill rank i serves the decode ranks j with (j - p) % p == i."""
+    """Host control channels of the disagg phase, one per (prefill rank, decode rank): decode rank j
+    (ranks [p, world)) listens on base_port + j and accepts the p prefill ranks."""
     from multiprocessing.connection import Client, Listener
     if rank >= p:
-        lst = Listener(("127.0.0.1", base_port + rank), authkey=b"mxs-bench")
-        conn = lst.accept()
+        lst = Listener(("127.0.0.1", base_port + rank), authkey=b"mxs-bench", backlog=max(8, p))
+        conns = [lst.accept() for _ in range(p)]
         lst.close()
-        return [conn]
+        return conns
     conns = []
     for j in range(p, world):
-        if (j - p) % p != rank:
-            continue
         for _ in range(1200):
             try:
                 conns.append(Client(("127.0.0.1", base_port + j), authkey=b"mxs-bench"))
@@ -395,18 +393,25 @@ def _disagg_conns(rank: int, p: int, world: int, base_port: int) -> list:
     return conns
 
 
-def run_disagg_decode(a, eng, sp, drv, barrier, agree, conn) -> float:
+def run_disagg_decode(a, eng, sp, drv, barrier, agree, conns: list) -> float:
+    """Decode rank: its arrivals' prompts go to the prefill rank with the fewest prompts in flight
+    (one control channel per prefill rank); the KV lands in this rank's pool before the request
+    decodes here."""
     from mxserve.disagg.kv_transfer import KVTransferAgent
     agent = KVTransferAgent(eng.runner, "xgmi")
-    conn.send(("desc", agent.descriptor()))
-    # the prefill rank maps the arena now, while this rank idles in a plain socket wait
-    ack = conn.recv()
-    assert ack[0] == "mapped", ack
-    arena = bool(ack[1]) if len(ack) > 1 else True
-    vlog(f"decode arena mapped by the prefill rank: {arena}")
+    desc = agent.descriptor()
+    for conn in conns:
+        conn.send(("desc", desc))
+    arenas = []
+    for conn in conns:  # each prefill rank maps the arena now, while this rank idles in a socket wait
+        ack = conn.recv()
+        assert ack[0] == "mapped", ack
+        arenas.append(bool(ack[1]) if len(ack) > 1 else True)
+    vlog(f"decode arena mapped by the prefill ranks: {arenas}")
     bs = eng.args.block_size
     backlog: list = []
     inflight: dict = {}
+    load = [0] * len(conns)
 
     def step():
         backlog.extend(drv.due())
@@ -418,38 +423,48 @@ def run_disagg_decode(a, eng, sp, drv, barrier, agree, conn) -> float:
             req = eng.reserve_remote_prefill(toks, sp, rid)
             if req is None:  # decode pool or batch full: retry next step
                 break
+            k = min(range(len(conns)), key=load.__getitem__)
             skip = req.num_cached_tokens // bs
             dst = list(req.block_ids[skip:-(-len(toks) // bs)])
             # GPU arena extent over xGMI, else the page-locked /dev/shm arena, else the pipe
-            start = agent.acquire(len(dst)) if arena else None
+            start = agent.acquire(len(dst)) if arenas[k] else None
             shm_start = agent.acquire_shm(len(dst)) if start is None else None
             backlog.pop(0)
-            conn.send(("prefill", rid, toks, dst, skip, start, shm_start))
-            inflight[rid] = (dst, start, shm_start)
+            conns[k].send(("prefill", rid, toks, dst, skip, start, shm_start))
+            inflight[rid] = (k, dst, start, shm_start)
+            load[k] += 1
         now = time.perf_counter()
-        while conn.poll():
-            _, rid, tok, data = conn.recv()
-            dst, start, shm_start = inflight.pop(rid)
-            if start is not None:  # staging extent -> pool blocks, ordered before the next step
-                agent.land(start, dst)
-            elif shm_start is not None:
-                agent.land_shm(shm_start, dst)
-            elif data is not None:  # host-staged transfer
-                agent.write_blocks(dst, data)
-            out = eng.complete_remote_prefill(rid, tok)
-            drv.token(rid, now, out.finished)
+        for conn in conns:
+            while conn.poll():
+                _, rid, tok, data = conn.recv()
+                k, dst, start, shm_start = inflight.pop(rid)
+                load[k] -= 1
+                if start is not None:  # staging extent -> pool blocks, ordered before the next step
+                    agent.land(start, dst)
+                elif shm_start is not None:
+                    agent.land_shm(shm_start, dst)
+                elif data is not None:  # host-staged transfer
+                    agent.write_blocks(dst, data)
+                out = eng.complete_remote_prefill(rid, tok)
+                drv.token(rid, now, out.finished)
         if eng.has_unfinished():
             outs = eng.step()
             now = time.perf_counter()
             for o in outs:
                 drv.token(o.request_id, now, o.finished)
         elif inflight:  # nothing to decode yet: block until a prefill lands (or an arrival is due)
-            conn.poll(0.02)
+            if len(conns) == 1:
+                conns[0].poll(0.02)
+            else:
+                time.sleep(0.0005)
+
+    def on_phase(ph):
+        for conn in conns:
+            conn.send(("phase", ph))
 
     sch = eng.scheduler
     return timed_phases(a, step, barrier, agree, drv,
-                        lambda: len(sch.running) + len(sch.remote) + len(backlog),
-                        on_phase=lambda ph: conn.send(("phase", ph)))
+                        lambda: len(sch.running) + len(sch.remote) + len(backlog), on_phase=on_phase)
 
 
 def run_disagg_prefill(eng, temperature: float, barrier, conns: list) -> int:
@@ -676,7 +691,7 @@ def phase_disagg(a, ctx, base_port: int) -> tuple:
         sp = SamplingParams(max_tokens=osl, temperature=a.temperature, ignore_eos=True)
         drv = Driver(a2, rank, eng.model_config.vocab_size, qps * world / d)  # the node's rate over D ranks
         agree = ctx.agree_fn(ctx.pg_decode, d)
-        st = drv.stats(run_disagg_decode(a2, eng, sp, drv, ctx.barrier, agree, conns[0]))
+        st = drv.stats(run_disagg_decode(a2, eng, sp, drv, ctx.barrier, agree, conns))
     for c in conns:
         c.close()
     info = {"decode_max_num_seqs": a.disagg_max_num_seqs, "prefill_ranks": p, "decode_ranks": d,
