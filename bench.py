@@ -157,19 +157,20 @@ def start_probe(a, world: int):
     root = os.path.dirname(os.path.abspath(__file__))
     # its own rendezvous: rank 0's probe hosts the store (not torchrun's agent store of this job)
     env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
-    env.update(MASTER_PORT=str(int(os.environ.get("MASTER_PORT", "29500")) + 211),
-               MXS_PROBE_DEVICE="cpu" if a.device == "cpu" else "auto",
+    env.update(MXS_PROBE_DEVICE="cpu" if a.device == "cpu" else "auto",
                PYTHONPATH=os.pathsep.join([root] + [x for x in [os.environ.get("PYTHONPATH")] if x]))
     return subprocess.Popen([sys.executable, "-m", "mxserve.tools.mgpu_probe"], stdin=subprocess.PIPE,
                             stdout=subprocess.PIPE, env=env, cwd=root)
 
 
-def finish_probe(p, timeout_s: float):
-    """Release the probe (this rank's engine is gone) and wait for it; rank 0's carries the result."""
+def finish_probe(p, timeout_s: float, ctx):
+    """Release the probe (this rank's engine is gone) with the rendezvous port rank 0 picked, and
+    wait for it; rank 0's carries the result."""
     if p is None:
         return None
+    port = ctx.gather([float(_free_port()) if ctx.rank == 0 else 0.0])[0, 0]
     try:
-        p.stdin.write(b"go\n")
+        p.stdin.write(f"go {int(port)}\n".encode())
         p.stdin.close()
     except OSError:
         pass
@@ -371,20 +372,24 @@ def run_agg(a, eng, sp, drv, barrier, agree) -> float:
     return timed_phases(a, step, barrier, agree, drv, lambda: len(sch.running) + len(sch.waiting))
 
 
-def _disagg_conns(rank: int, p: int, world: int, base_port: int) -> list:
-    """Host control channels of the disagg phase, one per (prefill rank, decode rank): decode rank j
-    (ranks [p, world)) listens on base_port + j and accepts the p prefill ranks."""
+def _disagg_conns(rank: int, p: int, world: int, gather) -> list:
+    """Host control channels of the disagg phase, one per (prefill rank, decode rank): every decode
+    rank (ranks [p, world)) listens on a port of its own choosing (published to all ranks through
+    `gather`, so no fixed port can collide) and accepts the p prefill ranks."""
     from multiprocessing.connection import Client, Listener
+    lst = None
     if rank >= p:
-        lst = Listener(("127.0.0.1", base_port + rank), authkey=b"mxs-bench", backlog=max(8, p))
+        lst = Listener(("127.0.0.1", 0), authkey=b"mxs-bench", backlog=max(8, p))
+    ports = gather([float(lst.address[1]) if lst is not None else 0.0])[:, 0].astype(int)
+    if lst is not None:
         conns = [lst.accept() for _ in range(p)]
         lst.close()
         return conns
     conns = []
     for j in range(p, world):
-        for _ in range(1200):
+        for _ in range(600):
             try:
-                conns.append(Client(("127.0.0.1", base_port + j), authkey=b"mxs-bench"))
+                conns.append(Client(("127.0.0.1", int(ports[j])), authkey=b"mxs-bench"))
                 break
             except OSError:
                 time.sleep(0.1)
@@ -667,7 +672,7 @@ def phase_agg(a, ctx) -> tuple:
     return ctx.gather(st), info, host
 
 
-def phase_disagg(a, ctx, base_port: int) -> tuple:
+def phase_disagg(a, ctx) -> tuple:
     from mxserve.engine.engine import LLMEngine
     from mxserve.engine.request import SamplingParams
     world, rank = ctx.world, ctx.rank
@@ -683,7 +688,7 @@ def phase_disagg(a, ctx, base_port: int) -> tuple:
     vlog("disagg: building engine")
     eng = LLMEngine(args)
     vlog(f"disagg: engine ready ({eng.runner.num_blocks} KV blocks)")
-    conns = _disagg_conns(rank, p, world, base_port)
+    conns = _disagg_conns(rank, p, world, ctx.gather)
     if is_prefill:
         run_disagg_prefill(eng, a.temperature, ctx.barrier, conns)
         st = list(_STAT_NAN)
@@ -715,7 +720,6 @@ def main():
         raise SystemExit("bench.py: the disagg phase needs at least 2 GPUs (prefill and decode ranks)")
     probe = start_probe(a, world)  # before Ctx: nothing in this process has touched the GPU yet
     ctx = Ctx(a)
-    base_port = int(os.environ.get("MASTER_PORT", "29500")) + 101
 
     agg = dis = info = None
     if mode in ("agg", "both"):
@@ -724,7 +728,7 @@ def main():
         if host and ctx.rank == 0:
             print(json.dumps({"host_ms_per_step": host}), file=sys.stderr, flush=True)
     if mode in ("disagg", "both"):
-        dis = run_guarded(lambda: phase_disagg(a, ctx, base_port), a.phase_timeout_s, ctx, agg_info=info,
+        dis = run_guarded(lambda: phase_disagg(a, ctx), a.phase_timeout_s, ctx, agg_info=info,
                           agg=agg, a=a, mode=mode)
         col_d, info_d = dis
         p_d = info_d["prefill_ranks"]
@@ -733,7 +737,7 @@ def main():
         if agg is None:
             info = {"kv_blocks": None, "graphs": [], "preemptions": None, "model": a.model,
                     "kv_cache_dtype": "bf16", "isl": a.isl, "osl": a.osl}
-    probe_res = finish_probe(probe, a.probe_timeout_s)
+    probe_res = finish_probe(probe, a.probe_timeout_s, ctx)
     if ctx.rank == 0:
         line = build_line(a, ctx, mode, agg, dis, info)
         if probe_res is not None:

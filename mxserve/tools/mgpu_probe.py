@@ -289,7 +289,7 @@ class Probe:
 
         comm.set_tp(comm.ParallelState())  # every engine here is TP = 1
         try:
-            col, info = bench.phase_disagg(a, Ctx(), int(os.environ.get("MASTER_PORT", "29500")) + 101)
+            col, info = bench.phase_disagg(a, Ctx())
         finally:
             comm.set_tp(st)
         res = bench.summarize(col, a.steps, list(range(n // 2, n)))
@@ -366,9 +366,11 @@ def main() -> int:
     result_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
     sys.stdout = sys.stderr
-    line = sys.stdin.readline()
-    if line.strip() != "go":  # the bench rank ended (or failed) before its serving phases finished
+    line = sys.stdin.readline().split()
+    if not line or line[0] != "go":  # the bench rank ended (or failed) before its serving phases finished
         return 0
+    if len(line) > 1:  # the rendezvous port rank 0's bench process picked
+        os.environ["MASTER_PORT"] = line[1]
     t0 = time.perf_counter()
     try:
         p = Probe()

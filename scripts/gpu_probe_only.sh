@@ -5,7 +5,7 @@ N=${1:-2}
 mkdir -p gpurun_out
 pids=()
 for r in $(seq 0 $((N-1))); do
-  (echo go | env MASTER_ADDR=127.0.0.1 MASTER_PORT=29911 RANK=$r LOCAL_RANK=$r WORLD_SIZE=$N \
+  (echo "go 29911" | env MASTER_ADDR=127.0.0.1 MASTER_PORT=29911 RANK=$r LOCAL_RANK=$r WORLD_SIZE=$N \
      timeout -k 10 600 python -m mxserve.tools.mgpu_probe > gpurun_out/probe_r$r.out 2> gpurun_out/probe_r$r.err) &
   pids+=($!)
 done
