@@ -157,6 +157,9 @@ def start_probe(a, world: int):
     root = os.path.dirname(os.path.abspath(__file__))
     # its own rendezvous: rank 0's probe hosts the store (not torchrun's agent store of this job)
     env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    # no new section starts past 60 % of the timeout: a long section then still ends in time and the
+    # sections already measured are reported instead of a killed probe
+    env.setdefault("MXS_PROBE_BUDGET_S", str(round(0.6 * a.probe_timeout_s)))
     env.update(MXS_PROBE_DEVICE="cpu" if a.device == "cpu" else "auto",
                PYTHONPATH=os.pathsep.join([root] + [x for x in [os.environ.get("PYTHONPATH")] if x]))
     return subprocess.Popen([sys.executable, "-m", "mxserve.tools.mgpu_probe"], stdin=subprocess.PIPE,

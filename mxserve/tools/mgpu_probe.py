@@ -96,6 +96,15 @@ class Probe:
         from ..parallel.comm import get_tp
         dist.barrier(group=get_tp().cpu_group)
 
+    def over_budget(self, elapsed: float, budget: float) -> bool:
+        """Rank 0's clock decides for every rank (the sections run collectives, so all ranks must
+        agree on which ones start)."""
+        import torch.distributed as dist
+        from ..parallel.comm import get_tp
+        flag = [elapsed > budget]
+        dist.broadcast_object_list(flag, src=0, group=get_tp().cpu_group)
+        return bool(flag[0])
+
     # ------------------------------------------------------------------ sections
     def collectives(self) -> dict:
         import torch.distributed as dist
@@ -342,7 +351,12 @@ class Probe:
         only = [x for x in os.environ.get("MXS_PROBE_SECTIONS", "").split(",") if x]
         if only:  # a subset (GPU tests)
             sections = [(nm, fn) for nm, fn in sections if nm in only]
+        budget = float(os.environ.get("MXS_PROBE_BUDGET_S", "0"))  # 0: no limit
+        t_start = time.perf_counter()
         for name, fn in sections:
+            if budget > 0 and self.over_budget(time.perf_counter() - t_start, budget):
+                res[name] = {"skipped": f"probe wall budget of {budget:.0f}s spent"}
+                continue
             if name in ("ep", "ep_engine") and get_model_config(ep_model).num_experts % self.world:
                 res[name] = {"skipped": f"{self.world} ranks do not divide the experts"}
                 continue
