@@ -71,6 +71,16 @@ int64_t open_pool(const std::string& handle, int64_t offset) {
   return reinterpret_cast<int64_t>(reinterpret_cast<char*>(base) + offset);
 }
 
+// Unmap one opened handle: a KV transfer agent closes only the arenas IT opened (the custom
+// all-reduce's peer slots live in the same table and must stay mapped).
+void close_handle(const std::string& handle) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_open.find(handle);
+  if (it == g_open.end()) return;
+  (void)hipIpcCloseMemHandle(it->second);
+  g_open.erase(it);
+}
+
 void close_all() {
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& kv : g_open) (void)hipIpcCloseMemHandle(kv.second);
@@ -220,5 +230,6 @@ void register_comm(pybind11::module_& m) {
   // may block on the peer driver: let watchdog threads run meanwhile
   m.def("ipc_open_pool", &open_pool, pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("ipc_close_all", &close_all);
+  m.def("ipc_close", &close_handle);
   m.def("copy_blocks", &copy_blocks);
 }

@@ -292,9 +292,10 @@ class KVTransferAgent:
         """Unmap every opened peer arena and drop the local ones (bench phases rebuild engines)."""
         if self._stream is not None:
             self._stream.synchronize()
-        if self._opened:
+        if self._opened:  # only this agent's mappings: the custom all-reduce's peer slots stay mapped
             from .. import ops
-            ops.ext().ipc_close_all()
+            for key in self._opened:
+                ops.ext().ipc_close(base64.b64decode(key))
             self._opened.clear()
         for a in list(self._shm_peers.values()) + ([self.shm] if self.shm is not None else []):
             a.close()

@@ -27,9 +27,10 @@ IPC all-reduce carrying the model's collectives (ranks sharing one GPU) -- and m
   p2p          rank 0: peer copy bandwidth to every other GPU it sees, one link at a time and all
                links at once (hipMemcpyPeer over xGMI)
 
-bench.py's own disagg phase stays in the rank processes: hosted here ahead of the other sections,
-it completed, but the custom IPC all-reduce created next in the same processes hit an illegal
-address (profiles/r2_s5_hosted_disagg_fault.txt), so disagg_8b runs last but for p2p.
+bench.py's own disagg phase stays in the rank processes.  Hosted here ahead of the other sections
+it completed, but its KV agent's teardown then unmapped the custom all-reduce's peer slots (an
+ipc_close_all; fixed: agents close only their own mappings), and the next all-reduce hit an
+illegal address (profiles/r2_s5_hosted_disagg_fault.txt).
 
 A crash or hang in a probe costs only the probe (its rank reports {"status": "failed"}); the
 serving numbers of the bench stand.  Rank 0 prints one line `PROBE {json}` on its original stdout.

@@ -78,6 +78,25 @@ def _rank(rank, world, port, q):
             for i, b in enumerate(bufs):
                 if not torch.equal(b.float(), want(b.numel(), 20 + i)):
                     errs.append(f"graph rep {rep} buf {i}")
+        # a KV transfer agent in the same process maps a peer's arena and closes it (engine teardown):
+        # only that mapping goes; the all-reduce's peer slots (same IPC table) must stay mapped
+        from mxserve import ops
+        ext = ops.ext()
+        arena = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda:0")
+        handle, off = ext.ipc_export_pool(arena)
+        handles = [None] * world
+        dist.all_gather_object(handles, (bytes(handle), int(off)))
+        peer_h, peer_off = handles[(rank + 1) % world]
+        ext.ipc_open_pool(peer_h, peer_off)
+        torch.cuda.synchronize()
+        dist.barrier()
+        ext.ipc_close(peer_h)
+        x = inp(4096, 40)
+        out = car.all_reduce(x)
+        torch.cuda.synchronize()
+        if not torch.equal(out.float(), want(4096, 40)):
+            errs.append("all-reduce after an agent's ipc_close")
+        dist.barrier()
         assert car.check(), "error word raised"
         dist.barrier()
         q.put((rank, errs))
