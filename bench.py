@@ -148,10 +148,12 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def start_probe(a, world: int):
+def start_probe(a, world: int, host_disagg: bool = False):
     """N >= 2: one multi-GPU probe process per rank (mxserve/tools/mgpu_probe.py: TP / EP against the
     unsharded model, RCCL and custom all-reduce bandwidth, xGMI peer copies), started BEFORE this rank
-    touches the GPU and idle until finish_probe: a crash or hang there costs only the probe."""
+    touches the GPU and idle until finish_probe: a crash or hang there costs only the probe.
+    host_disagg: the probe processes also run this bench's disagg phase (first, with this bench's
+    arguments), so a fault on the cross-GPU KV path cannot take the aggregated result with it."""
     if world < 2 or a.probe_timeout_s <= 0:
         return None
     root = os.path.dirname(os.path.abspath(__file__))
@@ -160,6 +162,10 @@ def start_probe(a, world: int):
     # no new section starts past 60 % of the timeout: a long section then still ends in time and the
     # sections already measured are reported instead of a killed probe
     env.setdefault("MXS_PROBE_BUDGET_S", str(round(0.6 * a.probe_timeout_s)))
+    if host_disagg:
+        env["MXS_PROBE_DISAGG_ARGV"] = json.dumps(sys.argv[1:])
+    else:
+        env.pop("MXS_PROBE_DISAGG_ARGV", None)
     env.update(MXS_PROBE_DEVICE="cpu" if a.device == "cpu" else "auto",
                PYTHONPATH=os.pathsep.join([root] + [x for x in [os.environ.get("PYTHONPATH")] if x]))
     return subprocess.Popen([sys.executable, "-m", "mxserve.tools.mgpu_probe"], stdin=subprocess.PIPE,
@@ -721,7 +727,9 @@ def main():
     mode = a.mode if a.mode != "auto" else ("agg" if world == 1 else "both")
     if mode in ("disagg", "both") and world < 2:
         raise SystemExit("bench.py: the disagg phase needs at least 2 GPUs (prefill and decode ranks)")
-    probe = start_probe(a, world)  # before Ctx: nothing in this process has touched the GPU yet
+    # the disagg phase runs in the crash-isolated probe processes unless the probe is off
+    host_disagg = mode in ("disagg", "both") and a.probe_timeout_s > 0
+    probe = start_probe(a, world, host_disagg)  # before Ctx: nothing in this process has touched the GPU yet
     ctx = Ctx(a)
 
     agg = dis = info = None
@@ -730,17 +738,25 @@ def main():
         agg = summarize(col, a.steps, list(range(world)))
         if host and ctx.rank == 0:
             print(json.dumps({"host_ms_per_step": host}), file=sys.stderr, flush=True)
-    if mode in ("disagg", "both"):
+    if mode in ("disagg", "both") and not host_disagg:
         dis = run_guarded(lambda: phase_disagg(a, ctx), a.phase_timeout_s, ctx, agg_info=info,
                           agg=agg, a=a, mode=mode)
-        col_d, info_d = dis
-        p_d = info_d["prefill_ranks"]
-        dis = summarize(col_d, a.steps, list(range(p_d, world)))
-        dis.update(info_d, parallelism=f"disagg {p_d}P+{world - p_d}D")
-        if agg is None:
-            info = {"kv_blocks": None, "graphs": [], "preemptions": None, "model": a.model,
-                    "kv_cache_dtype": "bf16", "isl": a.isl, "osl": a.osl}
-    probe_res = finish_probe(probe, a.probe_timeout_s, ctx)
+        dis = disagg_summary(*dis, a, world)
+    # a hosted disagg phase has its own watchdog budget on top of the probe's
+    probe_res = finish_probe(probe, a.probe_timeout_s + (a.phase_timeout_s if host_disagg else 0), ctx)
+    if host_disagg and ctx.rank == 0:
+        r = probe_res.pop("disagg_headline", None) if isinstance(probe_res, dict) else None
+        if isinstance(r, dict) and "col" in r:
+            dis = disagg_summary(np.array(r["col"], dtype=np.float64), r["info"], a, world)
+            dis["ran_in"] = "probe processes (crash-isolated)"
+        else:
+            err = (r or probe_res or {}).get("error", "no result from the probe processes")
+            dis = {"status": "failed", "error": err}
+            if agg is None:
+                raise SystemExit(f"bench.py: disagg phase failed: {err}")
+    if mode in ("disagg", "both") and agg is None:
+        info = {"kv_blocks": None, "graphs": [], "preemptions": None, "model": a.model,
+                "kv_cache_dtype": "bf16", "isl": a.isl, "osl": a.osl}
     if ctx.rank == 0:
         line = build_line(a, ctx, mode, agg, dis, info)
         if probe_res is not None:
@@ -750,6 +766,13 @@ def main():
         ctx.dist.barrier()
         ctx.dist.destroy_process_group()
     return 0
+
+
+def disagg_summary(col_d: np.ndarray, info_d: dict, a, world: int) -> dict:
+    p_d = info_d["prefill_ranks"]
+    dis = summarize(col_d, a.steps, list(range(p_d, world)))
+    dis.update(info_d, parallelism=f"disagg {p_d}P+{world - p_d}D")
+    return dis
 
 
 def build_line(a, ctx, mode, agg, dis, info) -> dict:

@@ -208,6 +208,9 @@ def test_bench_contract_cpu(mode, nproc, launcher, tmp_path):
     if want == "both":
         assert d["agg"]["value"] == d["value"] and d["disagg"]["value"] > 0
         assert d["disagg"]["parallelism"] == f"disagg {nproc // 2}P+{nproc // 2}D"
+    if want in ("both", "disagg"):  # hosted by the crash-isolated probe processes
+        assert d["disagg"]["ran_in"].startswith("probe"), d["disagg"]
+        assert "disagg_headline" not in d["multi_gpu_probe"]
     if want == "disagg" and nproc == 3:  # disagg_plan: 1 prefill rank serving 2 decode ranks
         assert d["disagg"]["prefill_ranks"] == 1 and d["disagg"]["decode_ranks"] == 2, d["disagg"]
         assert d["config"]["parallelism"] == "disagg 1P+2D" and d["value"] > 0
