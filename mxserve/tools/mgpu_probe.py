@@ -6,6 +6,9 @@ blocks on stdin until its rank has finished the serving phases and released its 
 then form their own process group -- RCCL when every rank has its own GPU, else gloo with the custom
 IPC all-reduce carrying the model's collectives (ranks sharing one GPU) -- and measure:
 
+  disagg_headline  (when bench.py hands over its arguments in MXS_PROBE_DISAGG_ARGV) bench.py's own
+               disaggregated phase, run first and outside the section budget; the per-rank stat rows
+               go back to bench.py, which reports them as the line's `disagg`
   collectives  all-reduce of bf16 buffers 64 KiB - 256 MiB through the process group (RCCL over xGMI
                on a real node): time, algorithm and bus bandwidth (2 (n-1) / n x bytes / t); the
                custom IPC all-reduce (one-shot / two-shot) 16 KiB - 8 MiB
@@ -27,10 +30,9 @@ IPC all-reduce carrying the model's collectives (ranks sharing one GPU) -- and m
   p2p          rank 0: peer copy bandwidth to every other GPU it sees, one link at a time and all
                links at once (hipMemcpyPeer over xGMI)
 
-bench.py's own disagg phase stays in the rank processes.  Hosted here ahead of the other sections
-it completed, but its KV agent's teardown then unmapped the custom all-reduce's peer slots (an
-ipc_close_all; fixed: agents close only their own mappings), and the next all-reduce hit an
-illegal address (profiles/r2_s5_hosted_disagg_fault.txt).
+bench.py's own disagg phase runs here first (disagg_headline).  Its first trial faulted the next
+section: the KV agent's teardown unmapped the custom all-reduce's peer slots (an ipc_close_all;
+fixed: agents close only their own mappings; profiles/r2_s5_hosted_disagg_fault.txt).
 
 A crash or hang in a probe costs only the probe (its rank reports {"status": "failed"}); the
 serving numbers of the bench stand.  Rank 0 prints one line `PROBE {json}` on its original stdout.
