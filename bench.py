@@ -60,6 +60,7 @@ import numpy as np
 BASELINE_METRIC = "output tok/s (node) + p50 TTFT at fixed QPS, Llama-3.2-1B agg vs disagg"
 _VERBOSE = os.environ.get("MXS_BENCH_VERBOSE", "0") == "1"
 _T0 = time.perf_counter()
+_WALL0 = time.time()  # the whole-run wall budget (--time-budget-s) counts from here
 
 
 if _VERBOSE:  # stacks of every thread once a minute: where a stalled rank is waiting
@@ -114,7 +115,92 @@ def parse(argv=None):
                     help="KV pool size per rank (default: what the GPU's free memory allows)")
     ap.add_argument("--probe-timeout-s", type=float, default=float(os.environ.get("MXS_BENCH_PROBE_TIMEOUT", "300")),
                     help="N >= 2: budget of the multi-GPU probe run after the serving phases (0: no probe)")
+    ap.add_argument("--time-budget-s", type=float, default=float(os.environ.get("MXS_BENCH_BUDGET_S", "450")),
+                    help="wall budget of the whole run, from process start: the probe and the disagg phase get "
+                         "what the agg phase leaves; at the deadline rank 0 prints the line it has and every "
+                         "rank exits (the driver's own timeout is 600 s)")
     return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------- wall budget
+_RESERVE_S = 25.0  # what the probe leaves the ranks to collect its result and print before the deadline
+
+
+class Guard:
+    """Whole-run deadline of one rank.
+
+    Every rank arms it at start.  The probe processes (and the disagg phase they host) get absolute
+    deadlines derived from it, finish_probe waits only until it, and a watchdog thread enforces it:
+    at the deadline rank 0 prints the best line it has (the provisional agg line, with the phases
+    that did not finish marked), the children are killed with their process groups, and the rank
+    exits 0 (a non-zero worker exit would make torchrun SIGTERM rank 0 before it has printed).  A
+    rank whose parent (torchrun) dies exits too, so nothing outlives a killed launcher."""
+
+    def __init__(self, budget_s: float, rank: int):
+        self.deadline = _WALL0 + budget_s
+        self.rank = rank
+        self.lock = threading.Lock()
+        self.printed = False
+        self.pending = None  # rank 0: the line to print if the budget runs out
+        self.children: list = []
+
+    def remaining(self) -> float:
+        return self.deadline - time.time()
+
+    def emit(self, line: dict) -> bool:
+        with self.lock:
+            if self.printed:
+                return False
+            self.printed = True
+        print(json.dumps(line), flush=True)
+        return True
+
+    def arm(self) -> "Guard":
+        threading.Thread(target=self._watch, daemon=True, name="bench-deadline").start()
+        if os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("WORLD_SIZE"):
+            ppid = os.getppid()
+            threading.Thread(target=self._watch_parent, args=(ppid,), daemon=True, name="bench-ppid").start()
+        return self
+
+    def _watch(self) -> None:
+        # ranks > 0 wait a little longer: rank 0 prints first, whatever the others do
+        slack = 0.0 if self.rank == 0 else 10.0
+        while self.remaining() + slack > 0:
+            time.sleep(min(1.0, max(0.05, self.remaining() + slack)))
+        self.expire(f"time budget of {self.deadline - _WALL0:.0f}s spent")
+
+    def _watch_parent(self, ppid: int) -> None:
+        while os.getppid() == ppid:
+            time.sleep(1.0)
+        self.kill_children()
+        os._exit(1)
+
+    def kill_children(self) -> None:
+        import signal
+        for p in self.children:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except OSError:
+                    p.kill()
+
+    def expire(self, why: str) -> None:
+        print(f"bench.py rank {self.rank}: {why}; killing children and exiting", file=sys.stderr, flush=True)
+        self.kill_children()
+        if self.rank == 0:
+            line = self.pending
+            if line is None:  # not even the agg phase finished: a failure line, not silence
+                line = {"metric": BASELINE_METRIC, "value": None, "unit": "tok/s", "status": "failed",
+                        "error": why, "higher_is_better": True}
+            else:
+                line = dict(line)
+                for k in ("disagg", "multi_gpu_probe"):
+                    if isinstance(line.get(k), dict) and line[k].get("status") == "pending":
+                        line[k] = {"status": "failed", "error": why}
+            self.emit(line)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0 if (self.rank != 0 or self.pending is not None) else 3)
 
 
 # Capacity of one MI355X in the disagg roles for the headline workload (Llama-3.2-1B, ISL 4000 / OSL
@@ -148,33 +234,36 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def start_probe(a, world: int, host_disagg: bool = False):
+def start_probe(a, world: int, guard: Guard, host_disagg: bool = False):
     """N >= 2: one multi-GPU probe process per rank (mxserve/tools/mgpu_probe.py: TP / EP against the
     unsharded model, RCCL and custom all-reduce bandwidth, xGMI peer copies), started BEFORE this rank
     touches the GPU and idle until finish_probe: a crash or hang there costs only the probe.
     host_disagg: the probe processes also run this bench's disagg phase (first, with this bench's
-    arguments), so a fault on the cross-GPU KV path cannot take the aggregated result with it."""
+    arguments), so a fault on the cross-GPU KV path cannot take the aggregated result with it.
+    The probe runs in a session of its own (killed as a group at the deadline), watches this rank
+    (exits when it dies) and reports by an absolute deadline _RESERVE_S ahead of this rank's."""
     if world < 2 or a.probe_timeout_s <= 0:
         return None
     root = os.path.dirname(os.path.abspath(__file__))
     # its own rendezvous: rank 0's probe hosts the store (not torchrun's agent store of this job)
     env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
-    # no new section starts past 60 % of the timeout: a long section then still ends in time and the
-    # sections already measured are reported instead of a killed probe
-    env.setdefault("MXS_PROBE_BUDGET_S", str(round(0.6 * a.probe_timeout_s)))
+    env["MXS_PROBE_DEADLINE"] = repr(guard.deadline - _RESERVE_S)
+    env["MXS_PROBE_TIMEOUT_S"] = repr(a.probe_timeout_s)  # the optional sections' own cap, after disagg
     if host_disagg:
         env["MXS_PROBE_DISAGG_ARGV"] = json.dumps(sys.argv[1:])
     else:
         env.pop("MXS_PROBE_DISAGG_ARGV", None)
     env.update(MXS_PROBE_DEVICE="cpu" if a.device == "cpu" else "auto",
                PYTHONPATH=os.pathsep.join([root] + [x for x in [os.environ.get("PYTHONPATH")] if x]))
-    return subprocess.Popen([sys.executable, "-m", "mxserve.tools.mgpu_probe"], stdin=subprocess.PIPE,
-                            stdout=subprocess.PIPE, env=env, cwd=root)
+    p = subprocess.Popen([sys.executable, "-m", "mxserve.tools.mgpu_probe"], stdin=subprocess.PIPE,
+                         stdout=subprocess.PIPE, env=env, cwd=root, start_new_session=True)
+    guard.children.append(p)
+    return p
 
 
-def finish_probe(p, timeout_s: float, ctx):
+def finish_probe(p, guard: Guard, ctx):
     """Release the probe (this rank's engine is gone) with the rendezvous port rank 0 picked, and
-    wait for it; rank 0's carries the result."""
+    wait for it until the deadline leaves just enough to print; rank 0's carries the result."""
     if p is None:
         return None
     port = ctx.gather([float(_free_port()) if ctx.rank == 0 else 0.0])[0, 0]
@@ -184,12 +273,13 @@ def finish_probe(p, timeout_s: float, ctx):
     except OSError:
         pass
     p.stdin = None  # closed above: communicate() must not flush it again
+    timeout_s = max(1.0, guard.remaining() - 10.0)
     try:
         out, _ = p.communicate(timeout=timeout_s)
     except subprocess.TimeoutExpired:
-        p.kill()
+        guard.kill_children()
         p.communicate()
-        return {"status": "failed", "error": f"no result within {timeout_s:.0f}s"}
+        return {"status": "failed", "error": f"no result within {timeout_s:.0f}s (run deadline)"}
     lines = [ln for ln in out.decode(errors="replace").splitlines() if ln.startswith("PROBE ")]
     if lines:
         return json.loads(lines[-1][len("PROBE "):])
@@ -565,8 +655,10 @@ class Ctx:
         if self.world > 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             # control plane only (barriers, steady-state votes, stats): replicas share no tensors,
-            # and the P->D KV moves over IPC, so a CPU group keeps RCCL out of the measurement
-            dist.init_process_group("gloo")
+            # and the P->D KV moves over IPC, so a CPU group keeps RCCL out of the measurement.
+            # A collective a peer never joins raises after the timeout instead of gloo's 30 min.
+            from datetime import timedelta
+            dist.init_process_group("gloo", timeout=timedelta(seconds=max(60.0, min(300.0, a.time_budget_s))))
             p = disagg_plan(a, self.world)[0]
             self.pg_decode = dist.new_group(list(range(p, self.world)), backend="gloo")
         self.sync = torch.cuda.synchronize if self.on_gpu else (lambda: None)
@@ -727,9 +819,10 @@ def main():
     mode = a.mode if a.mode != "auto" else ("agg" if world == 1 else "both")
     if mode in ("disagg", "both") and world < 2:
         raise SystemExit("bench.py: the disagg phase needs at least 2 GPUs (prefill and decode ranks)")
+    guard = Guard(a.time_budget_s, int(os.environ.get("RANK", "0"))).arm()
     # the disagg phase runs in the crash-isolated probe processes unless the probe is off
     host_disagg = mode in ("disagg", "both") and a.probe_timeout_s > 0
-    probe = start_probe(a, world, host_disagg)  # before Ctx: nothing in this process has touched the GPU yet
+    probe = start_probe(a, world, guard, host_disagg)  # before Ctx: nothing here has touched the GPU yet
     ctx = Ctx(a)
 
     agg = dis = info = None
@@ -738,12 +831,19 @@ def main():
         agg = summarize(col, a.steps, list(range(world)))
         if host and ctx.rank == 0:
             print(json.dumps({"host_ms_per_step": host}), file=sys.stderr, flush=True)
+        if ctx.rank == 0:  # provisional: what the watchdog prints if the rest runs out of time
+            line = build_line(a, ctx, mode, agg, None, info)
+            if mode == "both":
+                line["disagg"] = {"status": "pending"}
+            if probe is not None:
+                line["multi_gpu_probe"] = {"status": "pending"}
+            guard.pending = line
+            vlog(f"agg done: {agg['value']} tok/s; {guard.remaining():.0f}s of the budget left")
     if mode in ("disagg", "both") and not host_disagg:
-        dis = run_guarded(lambda: phase_disagg(a, ctx), a.phase_timeout_s, ctx, agg_info=info,
-                          agg=agg, a=a, mode=mode)
+        dis = run_guarded(lambda: phase_disagg(a, ctx), min(a.phase_timeout_s, max(1.0, guard.remaining() - 15)),
+                          ctx, agg_info=info, agg=agg, a=a, mode=mode, guard=guard)
         dis = disagg_summary(*dis, a, world)
-    # a hosted disagg phase has its own watchdog budget on top of the probe's
-    probe_res = finish_probe(probe, a.probe_timeout_s + (a.phase_timeout_s if host_disagg else 0), ctx)
+    probe_res = finish_probe(probe, guard, ctx)
     if host_disagg and ctx.rank == 0:
         r = probe_res.pop("disagg_headline", None) if isinstance(probe_res, dict) else None
         if isinstance(r, dict) and "col" in r:
@@ -761,7 +861,8 @@ def main():
         line = build_line(a, ctx, mode, agg, dis, info)
         if probe_res is not None:
             line["multi_gpu_probe"] = probe_res
-        print(json.dumps(line), flush=True)
+        line["wall_s"] = round(time.time() - _WALL0, 1)
+        guard.emit(line)
     if world > 1:
         ctx.dist.barrier()
         ctx.dist.destroy_process_group()
@@ -825,14 +926,17 @@ def run_guarded(fn, timeout_s: float, ctx, **kw):
     every rank exits instead of hanging the job."""
     done = threading.Event()
 
+    guard = kw["guard"]
+
     def watchdog():
         if done.wait(timeout_s):
             return
         if ctx.rank == 0 and kw.get("agg") is not None:
             line = build_line(kw["a"], ctx, kw["mode"], kw["agg"], None, kw["agg_info"])
             line["disagg"] = {"status": "failed", "error": f"phase did not finish within {timeout_s:.0f}s"}
-            print(json.dumps(line), flush=True)
+            guard.emit(line)
         print(f"bench.py rank {ctx.rank}: disagg phase timed out after {timeout_s:.0f}s", file=sys.stderr, flush=True)
+        guard.kill_children()
         os._exit(0 if kw.get("agg") is not None else 3)
 
     threading.Thread(target=watchdog, daemon=True).start()
@@ -846,7 +950,8 @@ def run_guarded(fn, timeout_s: float, ctx, **kw):
         if ctx.rank == 0:
             line = build_line(kw["a"], ctx, kw["mode"], kw["agg"], None, kw["agg_info"])
             line["disagg"] = {"status": "failed", "error": repr(e)[:300]}
-            print(json.dumps(line), flush=True)
+            guard.emit(line)
+        guard.kill_children()
         sys.stdout.flush()
         sys.stderr.flush()
         os._exit(0)

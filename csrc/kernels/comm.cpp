@@ -53,7 +53,14 @@ pybind11::tuple export_pool(at::Tensor t) {
 }
 
 std::mutex g_mu;
-std::unordered_map<std::string, void*> g_open;  // handle bytes -> mapped base
+// handle bytes -> (mapped base, users): every open_pool takes a reference and every close_handle
+// drops one, so two users of one mapping in this process (a KV agent and the custom all-reduce, or
+// two agents) cannot unmap it under each other; the last close unmaps
+struct Mapping {
+  void* base;
+  int refs;
+};
+std::unordered_map<std::string, Mapping> g_open;
 
 int64_t open_pool(const std::string& handle, int64_t offset) {
   TORCH_CHECK(handle.size() == sizeof(hipIpcMemHandle_t), "bad IPC handle size");
@@ -61,29 +68,36 @@ int64_t open_pool(const std::string& handle, int64_t offset) {
   auto it = g_open.find(handle);
   void* base = nullptr;
   if (it != g_open.end()) {
-    base = it->second;
+    base = it->second.base;
+    ++it->second.refs;
   } else {
     hipIpcMemHandle_t h;
     std::memcpy(&h, handle.data(), sizeof(h));
     hip_check(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
-    g_open.emplace(handle, base);
+    g_open.emplace(handle, Mapping{base, 1});
   }
   return reinterpret_cast<int64_t>(reinterpret_cast<char*>(base) + offset);
 }
 
-// Unmap one opened handle: a KV transfer agent closes only the arenas IT opened (the custom
-// all-reduce's peer slots live in the same table and must stay mapped).
+// Drop one reference to an opened handle; the mapping goes away with the last one.
 void close_handle(const std::string& handle) {
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_open.find(handle);
   if (it == g_open.end()) return;
-  (void)hipIpcCloseMemHandle(it->second);
+  if (--it->second.refs > 0) return;
+  (void)hipIpcCloseMemHandle(it->second.base);
   g_open.erase(it);
+}
+
+int64_t open_refs(const std::string& handle) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_open.find(handle);
+  return it == g_open.end() ? 0 : it->second.refs;
 }
 
 void close_all() {
   std::lock_guard<std::mutex> lk(g_mu);
-  for (auto& kv : g_open) (void)hipIpcCloseMemHandle(kv.second);
+  for (auto& kv : g_open) (void)hipIpcCloseMemHandle(kv.second.base);
   g_open.clear();
 }
 
@@ -231,5 +245,6 @@ void register_comm(pybind11::module_& m) {
   m.def("ipc_open_pool", &open_pool, pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("ipc_close_all", &close_all);
   m.def("ipc_close", &close_handle);
+  m.def("ipc_open_refs", &open_refs);
   m.def("copy_blocks", &copy_blocks);
 }

@@ -133,10 +133,13 @@ class ShmArena:
         arr = np.frombuffer(self._mm, dtype=np.uint8)
         self.t = torch.from_numpy(arr).view(dtype).view(nblocks, *block_shape)
         self._pinned = False
-        if pin:
+        if pin:  # page-locked for DMA; a pin failure (RLIMIT_MEMLOCK, ...) leaves it pageable
             from .. import ops
-            ops.ext().host_register(int(self.t.data_ptr()), nbytes)
-            self._pinned = True
+            try:
+                ops.ext().host_register(int(self.t.data_ptr()), nbytes)
+                self._pinned = True
+            except RuntimeError as e:
+                log.warning("KV shm arena %s not page-locked (%r); copies go through pageable memory", name, e)
 
     def close(self) -> None:
         if self._pinned:

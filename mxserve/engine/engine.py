@@ -112,6 +112,22 @@ class LLMEngine:
                           req.num_prompt_tokens, req.num_cached_tokens, len(req.output_token_ids), logprob,
                           top_logprobs)
 
+    def detach_remote_prefill(self, request_id: str) -> Optional[Request]:
+        """Decode side, a remote prefill given up while its KV push may still be in flight (the
+        client went away mid-transfer): forget the request -- its id is free again, e.g. for the
+        local-prefill fallback -- but keep its KV blocks allocated until release_detached(), so a
+        late push cannot land in blocks another request already owns."""
+        req = self.scheduler.remote.pop(request_id, None)
+        if req is None:
+            return None
+        self.requests.pop(request_id, None)
+        self.runner.release(request_id)
+        return req
+
+    def release_detached(self, req: Request) -> None:
+        """The prefill side is known to be done with a detached request's blocks: free them."""
+        self.scheduler.release_blocks(req)
+
     def release_prefill_blocks(self, request_id: str) -> None:
         """Prefill side: drop the blocks kept alive for the KV transfer."""
         req = self.requests.pop(request_id, None)

@@ -42,9 +42,10 @@ def set_tp(state: ParallelState) -> None:
 
 
 def init_distributed(tp_size: int, backend: Optional[str] = None, device: Optional[torch.device] = None,
-                     enable_custom_ar: bool = True) -> ParallelState:
+                     enable_custom_ar: bool = True, timeout_s: Optional[float] = None) -> ParallelState:
     """Initialise the default process group from torchrun-style env (RANK/WORLD_SIZE/MASTER_*).
-    The whole world is one TP group (one worker = one TP group)."""
+    The whole world is one TP group (one worker = one TP group).  timeout_s bounds a collective that
+    some rank never joins (gloo raises after it; default: torch's 30 min)."""
     if tp_size <= 1 and not dist.is_initialized():
         set_tp(ParallelState())
         return _STATE
@@ -55,13 +56,20 @@ def init_distributed(tp_size: int, backend: Optional[str] = None, device: Option
         kw = {}
         if backend == "nccl" and device is not None:
             kw["device_id"] = device
+        if timeout_s:
+            from datetime import timedelta
+            kw["timeout"] = timedelta(seconds=timeout_s)
         dist.init_process_group(backend=backend, **kw)
     world = dist.get_world_size()
     if world != tp_size:
         raise ValueError(f"world size {world} != tp_size {tp_size}")
     st = ParallelState(tp_rank=dist.get_rank(), tp_size=world, group=dist.group.WORLD)
     # scheduler metadata goes rank0 -> TP ranks over a CPU (gloo) group, never a GPU collective
-    st.cpu_group = dist.new_group(backend="gloo") if backend != "gloo" else st.group
+    if backend != "gloo":
+        from datetime import timedelta
+        st.cpu_group = dist.new_group(backend="gloo", **({"timeout": timedelta(seconds=timeout_s)} if timeout_s else {}))
+    else:
+        st.cpu_group = st.group
     # custom IPC all-reduce (one-shot / two-shot over peer-mapped buffers, bounded spins, RCCL
     # fallback on a peer timeout): on by default for TP <= 8 (its rank limit); validated with 2-8
     # ranks sharing one GPU (tests/test_custom_ar_gpu.py, tests/test_b_tp_gpu.py); MXS_CUSTOM_AR=0
@@ -131,10 +139,18 @@ class MetaRing:
             return
         self._push(data)
 
+    # a follower that has not taken a step for this long is dead or wedged: fail the driver's engine
+    # (the worker exits non-zero and gets restarted) instead of serving nothing while looking alive
+    PUSH_TIMEOUT_S = float(os.environ.get("MXS_TP_META_TIMEOUT_S", "120"))
+
     def _push(self, data: bytes) -> None:
+        import logging
+        waited = 0.0
         while not self.ring.push(data, 10.0):  # a follower is still busy with an old step
-            import logging
-            logging.getLogger(__name__).warning("TP metadata ring full for 10 s; waiting for followers")
+            waited += 10.0
+            if waited >= self.PUSH_TIMEOUT_S:
+                raise RuntimeError(f"TP metadata ring full for {waited:.0f}s: a follower rank stopped reading")
+            logging.getLogger(__name__).warning("TP metadata ring full for %.0f s; waiting for followers", waited)
 
     def recv(self):
         import pickle

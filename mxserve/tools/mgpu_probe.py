@@ -78,6 +78,8 @@ class Probe:
         self.dev = torch.device("cuda", self.local % self.ndev) if self.on_gpu else torch.device("cpu")
         self.dtype = torch.bfloat16 if self.on_gpu else torch.float32
         self.backend = "nccl" if self.on_gpu and not self.shared else "gloo"
+        self.res: dict = {"status": "starting"}  # filled section by section (the deadline dumps it)
+        self.current = "init"
 
     # ------------------------------------------------------------------ helpers
     def sync(self):
@@ -102,15 +104,6 @@ class Probe:
         import torch.distributed as dist
         from ..parallel.comm import get_tp
         dist.barrier(group=get_tp().cpu_group)
-
-    def over_budget(self, elapsed: float, budget: float) -> bool:
-        """Rank 0's clock decides for every rank (the sections run collectives, so all ranks must
-        agree on which ones start)."""
-        import torch.distributed as dist
-        from ..parallel.comm import get_tp
-        flag = [elapsed > budget]
-        dist.broadcast_object_list(flag, src=0, group=get_tp().cpu_group)
-        return bool(flag[0])
 
     # ------------------------------------------------------------------ sections
     def collectives(self) -> dict:
@@ -346,35 +339,66 @@ class Probe:
         return out
 
     # ------------------------------------------------------------------ main
+    # Wall seconds a section needs to finish on an MI355X node (the r2 2-rank run took 0.2-41 s per
+    # section; engines of the 70B / Mixtral shapes dominate): a section starts only if the deadline
+    # leaves it this much.  CPU plumbing runs use the small number.
+    SECTION_COST_S = {"collectives": 20, "tp": 40, "ep": 40, "p2p": 15, "tp_engine": 120, "ep_engine": 120,
+                      "disagg_8b": 90}
+
+    def section_fits(self, name: str, t_sections: float, deadline: float, cap: float) -> str:
+        """'' if the section may start, else why not.  Rank 0's clock decides for every rank (the
+        sections run collectives, so all ranks must agree on which ones start)."""
+        import torch.distributed as dist
+        from ..parallel.comm import get_tp
+        why = ""
+        need = self.SECTION_COST_S.get(name, 30) if self.on_gpu else 5
+        if deadline and time.time() + need > deadline:
+            why = f"run deadline: {deadline - time.time():.0f}s left, the section needs ~{need}s"
+        elif cap > 0 and time.perf_counter() - t_sections > 0.6 * cap:
+            why = f"probe wall budget of {cap:.0f}s spent"
+        box = [why]
+        dist.broadcast_object_list(box, src=0, group=get_tp().cpu_group)
+        return box[0]
+
     def run(self) -> dict:
         from ..parallel.comm import init_distributed
         if self.on_gpu:
             self.torch.cuda.set_device(self.dev)
-        init_distributed(self.world, backend=self.backend, device=self.dev if self.on_gpu else None)
-        res = {"status": "ok", "ranks": self.world, "backend": self.backend, "shared_gpu": self.shared}
+        # a collective some rank never joins (a section failed on one rank only) raises instead of
+        # waiting gloo's default 30 min
+        init_distributed(self.world, backend=self.backend, device=self.dev if self.on_gpu else None,
+                         timeout_s=float(os.environ.get("MXS_PROBE_PG_TIMEOUT_S", "180")))
+        res = self.res
+        res.update(status="ok", ranks=self.world, backend=self.backend, shared_gpu=self.shared)
         tp_model = MODEL_TP if self.on_gpu else "tiny-llama"
         ep_model = MODEL_EP if self.on_gpu else "tiny-mixtral"
+        # cheapest and most informative first: a run short of time still measures the collectives
+        # and the sharded-vs-unsharded parity before the engine-sized sections
         sections = [("collectives", self.collectives),
                     ("tp", lambda: self.sharded_vs_full(tp_model, "allreduce")),
                     ("ep", lambda: self.sharded_vs_full(ep_model, "a2a")),
+                    ("p2p", self.p2p),
                     ("tp_engine", lambda: self.tp_engine(MODEL_TP_ENGINE if self.on_gpu else "tiny-llama")),
                     ("ep_engine", lambda: self.tp_engine(MODEL_EP_ENGINE if self.on_gpu else "tiny-mixtral", "a2a")),
-                    ("disagg_8b", lambda: self.disagg(MODEL_DISAGG if self.on_gpu else "tiny-llama", 2.0)),
-                    ("p2p", self.p2p)]
+                    ("disagg_8b", lambda: self.disagg(MODEL_DISAGG if self.on_gpu else "tiny-llama", 2.0))]
         from ..models.config import get_model_config
         only = [x for x in os.environ.get("MXS_PROBE_SECTIONS", "").split(",") if x]
         if only:  # a subset (GPU tests)
             sections = [(nm, fn) for nm, fn in sections if nm in only]
         headline = os.environ.get("MXS_PROBE_DISAGG_ARGV")
-        if headline:  # bench.py's own disagg phase first, outside the wall budget
+        if headline:  # bench.py's own disagg phase first, outside the optional sections' cap
             argv = json.loads(headline)
             sections.insert(0, ("disagg_headline", lambda: self.disagg("", 0.0, argv=argv, raw=True)))
-        budget = float(os.environ.get("MXS_PROBE_BUDGET_S", "0"))  # 0: no limit
+        deadline = float(os.environ.get("MXS_PROBE_DEADLINE", "0"))  # absolute (time.time()); 0: none
+        cap = float(os.environ.get("MXS_PROBE_TIMEOUT_S", os.environ.get("MXS_PROBE_BUDGET_S", "0")))
+        if os.environ.get("MXS_PROBE_BUDGET_S"):  # a direct cap on the optional sections (tests)
+            cap = float(os.environ["MXS_PROBE_BUDGET_S"]) / 0.6
         t_start = time.perf_counter()
         for name, fn in sections:
-            if (budget > 0 and name != "disagg_headline"
-                    and self.over_budget(time.perf_counter() - t_start, budget)):
-                res[name] = {"skipped": f"probe wall budget of {budget:.0f}s spent"}
+            self.current = name
+            why = "" if name == "disagg_headline" else self.section_fits(name, t_start, deadline, cap)
+            if why:
+                res[name] = {"skipped": why}
                 continue
             if name in ("ep", "ep_engine") and get_model_config(ep_model).num_experts % self.world:
                 res[name] = {"skipped": f"{self.world} ranks do not divide the experts"}
@@ -383,6 +407,9 @@ class Probe:
                 res[name] = {"skipped": f"{self.world} ranks do not divide the attention heads"}
                 continue
             t0 = time.perf_counter()
+            if os.environ.get("MXS_PROBE_FAULT") == f"hang:{name}":  # tests: a section that never returns
+                while True:
+                    time.sleep(1.0)
             try:
                 res[name] = fn()
             except Exception as e:  # noqa: BLE001 - report, keep the other sections
@@ -391,9 +418,58 @@ class Probe:
             if isinstance(res[name], dict):
                 res[name]["wall_s"] = round(time.perf_counter() - t0, 1)
             self.barrier()
-            if name == "disagg_headline":  # the optional sections' budget starts after it
+            if name == "disagg_headline":  # the optional sections' cap starts after it
                 t_start = time.perf_counter()
+        self.current = "done"
         return res
+
+
+_EMIT_LOCK = None
+_EMITTED = []
+
+
+def _emit(result_out, res: dict) -> None:
+    """Write the one `PROBE {json}` line (the deadline watchdog and the main thread race for it)."""
+    with _EMIT_LOCK:
+        if _EMITTED:
+            return
+        _EMITTED.append(True)
+        try:
+            result_out.write("PROBE " + json.dumps(res, default=str) + "\n")
+            result_out.flush()
+        except (OSError, ValueError):
+            pass
+
+
+def _watch(result_out, probe_box: list, t0: float) -> None:
+    """The probe's own deadline (bench.py hands it MXS_PROBE_DEADLINE) and parent watch: at the
+    deadline rank 0 reports the sections finished so far and names the one that did not; every rank
+    exits.  If the bench rank that started this probe dies, the probe exits at once."""
+    import threading
+    global _EMIT_LOCK
+    _EMIT_LOCK = threading.Lock()
+    deadline = float(os.environ.get("MXS_PROBE_DEADLINE", "0"))
+    ppid = os.getppid()
+
+    def loop():
+        while True:
+            time.sleep(0.5)
+            if os.getppid() != ppid:
+                os._exit(1)
+            if deadline and time.time() > deadline:
+                break
+        p = probe_box[0] if probe_box else None
+        rank = int(os.environ.get("RANK", "0"))
+        print(f"mgpu_probe rank {rank}: deadline reached in section {getattr(p, 'current', 'init')!r}",
+              file=sys.stderr, flush=True)
+        if rank == 0:
+            res = dict(p.res) if p is not None else {}
+            res.update(status="partial", timed_out_section=getattr(p, "current", "init"),
+                       wall_s=round(time.perf_counter() - t0, 1))
+            _emit(result_out, res)
+        sys.stderr.flush()
+        os._exit(0)
+    threading.Thread(target=loop, daemon=True, name="probe-deadline").start()
 
 
 def main() -> int:
@@ -401,6 +477,9 @@ def main() -> int:
     result_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
     sys.stdout = sys.stderr
+    box: list = []
+    t0 = time.perf_counter()
+    _watch(result_out, box, t0)
     line = sys.stdin.readline().split()
     if not line or line[0] != "go":  # the bench rank ended (or failed) before its serving phases finished
         return 0
@@ -409,18 +488,17 @@ def main() -> int:
     t0 = time.perf_counter()
     try:
         p = Probe()
+        box.append(p)
         res = p.run()
         res["wall_s"] = round(time.perf_counter() - t0, 1)
         if p.rank == 0:
-            result_out.write("PROBE " + json.dumps(res) + "\n")
-            result_out.flush()
+            _emit(result_out, res)
         import torch.distributed as dist
         if dist.is_initialized():
             dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001
         traceback.print_exc()
-        result_out.write("PROBE " + json.dumps({"status": "failed", "error": repr(e)[:300]}) + "\n")
-        result_out.flush()
+        _emit(result_out, {"status": "failed", "error": repr(e)[:300]})
         return 1
     return 0
 

@@ -184,6 +184,7 @@ class Worker:
         self.stream_url: Optional[str] = None  # the streamer process's request plane (attach_streamer)
         self.loop: Optional[asyncio.AbstractEventLoop] = None
         self._ring_plane = None
+        self.kv_quarantined = 0  # remote prefills whose extents / blocks wait for the prefill side
         self.app = self._build_app()
 
     # ---------------------------------------------------------------- engine-thread hook
@@ -272,10 +273,10 @@ class Worker:
         return req
 
     # ---------------------------------------------------------------- streamer process
-    def attach_streamer(self, cmd_ring, out_ring, stream_url: str) -> None:
+    def attach_streamer(self, cmd_ring, out_ring, stream_url: str, proc=None) -> None:
         """The token request plane moves to the streamer process (worker/streamer.py)."""
         from .streamer import RingPlane
-        self._ring_plane = RingPlane(self, cmd_ring, out_ring)
+        self._ring_plane = RingPlane(self, cmd_ring, out_ring, proc)
         self.stream_url = stream_url
         self.aeng.attach_ring(self._ring_plane)
 
@@ -315,7 +316,13 @@ class Worker:
         skip = req.num_cached_tokens // self.args.block_size
         nblk = -(-len(toks) // self.args.block_size)
         dst = list(req.block_ids[skip:nblk])
-        target = self.agent.descriptor(self.url)
+        try:
+            target = self.agent.descriptor(self.url)
+        except Exception as e:  # noqa: BLE001 - no staging arena: give the reservation back, prefill here
+            log.warning("KV staging arena unavailable (%r); prefilling %s locally", e, rid)
+            self.aeng._queues.pop(rid, None)
+            self.aeng.submit_nowait(self.engine.abort, rid)
+            return None
         # reserve an extent in every staging arena this worker has (GPU arena over xGMI IPC, host
         # arena in /dev/shm); the prefill worker uses the first it can reach and says which
         start = self.agent.acquire(len(dst)) if target["backend"] == "xgmi" else None
@@ -328,13 +335,22 @@ class Worker:
         target["shm_start"] = shm_start
         payload = {"request_id": rid, "token_ids": toks, "sampling": _sp_dict(sp), "kv_target": target}
         completed = False
+        answered = False  # the prefill worker replied: it no longer writes our extents or blocks
+        post = None
         t_post = time.perf_counter()
         try:
             sess = await self.http()
-            async with sess.post(purl.rstrip("/") + "/prefill", json=payload) as r:
-                if r.status != 200:
-                    raise RuntimeError(f"prefill worker returned {r.status}: {await r.text()}")
-                res = await r.json()
+
+            async def do_post():
+                async with sess.post(purl.rstrip("/") + "/prefill", json=payload) as r:
+                    return r.status, (await r.json() if r.status == 200 else await r.text())
+            # shielded: a client going away cancels this coroutine, not the POST, whose reply is
+            # what tells us the prefill worker has stopped pushing into our extents and blocks
+            post = asyncio.ensure_future(do_post())
+            status, res = await asyncio.shield(post)
+            answered = True
+            if status != 200:
+                raise RuntimeError(f"prefill worker returned {status}: {res}")
 
             via = res.get("via", target["backend"])
 
@@ -367,15 +383,52 @@ class Worker:
             return None
         finally:
             # any non-completion -- an error above, or the client/frontend going away mid-POST
-            # (CancelledError is a BaseException): give back the arena extent, the reserved KV
-            # blocks and the token queue, or they leak until every reservation fails
+            # (CancelledError is a BaseException): give back the arena extents, the reserved KV
+            # blocks and the token queue, or they leak until every reservation fails -- but only
+            # once the prefill worker can no longer push into them (a late push into a
+            # reused extent or block would land the wrong KV in another request)
             if not completed:
-                if start is not None:
-                    self.agent.release(start, len(dst))
-                if shm_start is not None:
-                    self.agent.release_shm(shm_start, len(dst))
-                self.aeng.submit_nowait(self.engine.abort, rid)
                 self.aeng._queues.pop(rid, None)
+                if answered or post is None:
+                    self._release_remote(rid, start, shm_start, len(dst))
+                else:
+                    self._quarantine_remote(rid, post, start, shm_start, len(dst))
+
+    def _release_remote(self, rid: str, start, shm_start, n: int) -> None:
+        if start is not None:
+            self.agent.release(start, n)
+        if shm_start is not None:
+            self.agent.release_shm(shm_start, n)
+        self.aeng.submit_nowait(self.engine.abort, rid)
+
+    # how long extents and blocks of a remote prefill whose POST failed without a reply stay held:
+    # the prefill worker may have received it and still push (a reply settles it at once)
+    QUARANTINE_S = float(os.environ.get("MXS_KV_QUARANTINE_S", "60"))
+
+    def _quarantine_remote(self, rid: str, post: "asyncio.Future", start, shm_start, n: int) -> None:
+        """The POST has no reply yet (cancelled) or failed without one: detach the request now (its
+        id is free for the local fallback) and free its blocks and extents when the prefill worker
+        has replied, or QUARANTINE_S after a reply-less failure."""
+        held: dict = {}
+        self.aeng.submit_nowait(lambda: held.__setitem__("req", self.engine.detach_remote_prefill(rid)))
+        loop = asyncio.get_running_loop()
+
+        def free() -> None:
+            if start is not None:
+                self.agent.release(start, n)
+            if shm_start is not None:
+                self.agent.release_shm(shm_start, n)
+            self.aeng.submit_nowait(lambda: held.get("req") is not None and self.engine.release_detached(held["req"]))
+            self.kv_quarantined -= 1
+
+        def done(f: "asyncio.Future") -> None:
+            replied = not f.cancelled() and f.exception() is None
+            if replied:
+                free()
+            else:
+                loop.call_later(self.QUARANTINE_S, free)
+        self.kv_quarantined += 1
+        post.add_done_callback(done)
 
     async def _prefill(self, body: dict) -> dict:
         """Prefill side: compute, push KV into the decode worker's pool, return the first token."""
@@ -492,6 +545,9 @@ class Worker:
         async def health():
             if not w.ready:
                 return JSONResponse({"status": "starting"}, status_code=503)
+            rp = getattr(w, "_ring_plane", None)
+            if rp is not None and (rp.dead or rp.streamer_exited()):  # its token plane is gone
+                return JSONResponse({"status": "streamer down"}, status_code=503)
             return {"status": "ready", "model": w.model, "role": w.role, "worker_id": w.worker_id}
 
         @app.get("/live")
@@ -534,6 +590,12 @@ class Worker:
         base = self.wargs.frontend_url.rstrip("/")
         registered = False
         while True:
+            rp = self._ring_plane
+            if rp is not None and (rp.dead or rp.streamer_exited()):
+                # the token plane is gone: stop renewing the lease, so the frontend's registry
+                # expires this worker and routes elsewhere (/health fails too)
+                await asyncio.sleep(1.0)
+                continue
             try:
                 sess = await self.http()
                 if not registered:
@@ -598,7 +660,7 @@ def serve(wargs: WorkerArgs) -> None:
     w.url = advertise_url(wargs, wargs.port)
     if streamer is not None:
         proc, cmd_ring, out_ring, sport = streamer
-        w.attach_streamer(cmd_ring, out_ring, advertise_url(wargs, sport))
+        w.attach_streamer(cmd_ring, out_ring, advertise_url(wargs, sport), proc)
         log.info("token request plane: streamer process %d at %s", proc.pid, w.stream_url)
     log.info("worker %s (%s, %s) serving %s on %s", w.worker_id, w.role, w.agent.backend, w.model, w.url)
     try:

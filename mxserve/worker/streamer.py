@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import collections
 import json
 import logging
 import os
@@ -61,14 +62,23 @@ class RingPlane:
     """Engine-process end of the rings (AsyncEngine.attach_ring handler).  poll / command / emit run
     on the engine thread."""
 
-    def __init__(self, worker, cmd_ring, out_ring):
+    # outputs held back while the ring is full (a GC pause or a slow SSE writer in the streamer):
+    # re-sent, in order, ahead of the next step's; past this many messages the streamer is wedged
+    BACKLOG_MAX = 4096
+
+    def __init__(self, worker, cmd_ring, out_ring, proc=None):
         self.w = worker
         self.cmd = cmd_ring
         self.out = out_ring
+        self.proc = proc  # the streamer process: `dead` only once it has exited (or is wedged)
         self.dropped = 0
-        self.dead = False  # the streamer stopped reading: drop outputs instead of stalling the engine
+        self.backlog: collections.deque = collections.deque()
+        self.stalls = 0
+        self.dead = False  # the streamer is gone: /health fails so the worker is replaced
 
     def poll(self, timeout: float):
+        if self.backlog:  # an idle engine still delivers what a stall held back
+            self.flush()
         data = self.cmd.pop(0, timeout)
         return None if data is None else msgpack.unpackb(data, raw=False)
 
@@ -116,10 +126,28 @@ class RingPlane:
         if self.dead:
             self.dropped += 1
             return
-        if not self.out.push(data, 0.5):
-            self.dropped += 1
-            self.dead = True  # one stall, then never again: the engine keeps its step rate
-            log.error("streamer output ring full for 0.5 s (streamer process gone?); dropping its outputs")
+        self.backlog.append(data)
+        self.flush()
+
+    def flush(self) -> None:
+        """Push held-back outputs in order without stalling the engine thread for long: a stall is
+        transient (outputs wait in the backlog, nothing -- finish markers included -- is dropped)
+        unless the streamer process has exited or the backlog overflows."""
+        while self.backlog:
+            if self.out.push(self.backlog[0], 0.002 if len(self.backlog) > 1 else 0.05):
+                self.backlog.popleft()
+                continue
+            self.stalls += 1
+            if self.streamer_exited() or len(self.backlog) > self.BACKLOG_MAX:
+                self.dead = True
+                self.dropped += len(self.backlog)
+                self.backlog.clear()
+                log.error("streamer process %s; dropping its outputs and failing /health",
+                          "exited" if self.streamer_exited() else f"wedged ({self.BACKLOG_MAX} outputs queued)")
+            return
+
+    def streamer_exited(self) -> bool:
+        return self.proc is not None and self.proc.poll() is not None
 
 
 def start_streamer(host: str, port: int, max_prompt_tokens: int) -> tuple:

@@ -88,9 +88,20 @@ def _rank(rank, world, port, q):
         dist.all_gather_object(handles, (bytes(handle), int(off)))
         peer_h, peer_off = handles[(rank + 1) % world]
         ext.ipc_open_pool(peer_h, peer_off)
+        # a second user of the same mapping in this process takes a reference of its own: one
+        # user's close leaves the mapping in place for the other (comm.cpp refcount)
+        p2 = ext.ipc_open_pool(peer_h, peer_off)
+        if ext.ipc_open_refs(peer_h) != 2:
+            errs.append(f"refs after two opens: {ext.ipc_open_refs(peer_h)}")
+        ext.ipc_close(peer_h)
+        if ext.ipc_open_refs(peer_h) != 1:
+            errs.append(f"refs after one close: {ext.ipc_open_refs(peer_h)}")
         torch.cuda.synchronize()
+        del p2
         dist.barrier()
         ext.ipc_close(peer_h)
+        if ext.ipc_open_refs(peer_h) != 0:
+            errs.append("mapping still referenced after the last close")
         x = inp(4096, 40)
         out = car.all_reduce(x)
         torch.cuda.synchronize()

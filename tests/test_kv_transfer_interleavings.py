@@ -126,3 +126,94 @@ def test_kv_transfer_random_interleavings(seed, monkeypatch):
     finally:
         pre_agent.close()
         dec_agent.close()
+
+
+@pytest.mark.parametrize("reply", ["ok", "reset"])
+def test_cancelled_remote_prefill_holds_kv_until_prefill_side_is_done(reply, monkeypatch):
+    """the decode side's /prefill POST is cancelled (the client left) while the
+    prefill worker is still pushing.  The request id is freed at once (a local-prefill fallback can
+    reuse it), but its pool blocks and staging extents stay allocated until the prefill worker has
+    replied -- or, for a reply-less failure, the quarantine delay -- so a late push never lands in
+    blocks or extents another request owns."""
+    import asyncio
+
+    from mxserve.config import EngineArgs
+    from mxserve.disagg import kv_transfer
+    from mxserve.worker.args import WorkerArgs
+    from mxserve.worker.server import Worker
+    monkeypatch.setattr(kv_transfer, "SHM_BYTES", 256 * 2048)
+    ea = EngineArgs(model="tiny-llama", device="cpu", cpu_num_blocks=256, max_model_len=1024, disagg_mode="decode",
+                    load_format="random", seed=7)
+    w = Worker(WorkerArgs(engine=ea, host="127.0.0.1", worker_id="dec"))
+    w.QUARANTINE_S = 0.5
+    kv = w.engine.scheduler.kv
+    posted = []
+
+    class _Resp:
+        status = 200
+
+        async def json(self):
+            return {"first_token": 5, "via": "shm", "transfer_s": 0.0}
+
+    class _Post:
+        def __init__(self, gate):
+            self.gate = gate
+
+        async def __aenter__(self):
+            posted.append(True)
+            await self.gate.wait()  # the prefill worker is still computing / pushing
+            if reply == "reset":
+                raise ConnectionResetError("prefill worker connection reset")
+            return _Resp()
+
+        async def __aexit__(self, *exc):
+            return False
+
+    async def main():
+        gate = asyncio.Event()
+
+        class _Sess:
+            def post(self, url, json=None):
+                return _Post(gate)
+
+        async def http():
+            return _Sess()
+        w.http = http
+        free0, shm0 = kv.num_free(), w.agent._shm_ext.free_blocks()
+        toks = list(range(3, 103))  # 100 tokens = 7 blocks
+        t = asyncio.ensure_future(w._remote_prefill("r1", toks, SamplingParams(max_tokens=4), "http://prefill"))
+        while not posted:
+            await asyncio.sleep(0.01)
+        assert kv.num_free() == free0 - 7 and w.agent._shm_ext.free_blocks() == shm0 - 7
+        t.cancel()
+        with pytest.raises(asyncio.CancelledError):
+            await t
+        for _ in range(100):  # the engine thread runs the detach
+            if "r1" not in w.engine.requests:
+                break
+            await asyncio.sleep(0.01)
+        assert "r1" not in w.engine.requests and "r1" not in w.engine.scheduler.remote
+        await asyncio.sleep(0.2)
+        # still held: the prefill worker may push into them at any moment
+        assert kv.num_free() == free0 - 7 and w.agent._shm_ext.free_blocks() == shm0 - 7
+        assert w.kv_quarantined == 1
+        # the id is reusable right away (the local fallback path re-adds it)
+        await w.aeng.submit(w.engine.add_request, toks, SamplingParams(max_tokens=1), "r1")
+        gate.set()  # the prefill side replies (or its connection drops)
+        for _ in range(300):
+            if w.kv_quarantined == 0:
+                break
+            await asyncio.sleep(0.01)
+        assert w.kv_quarantined == 0
+        for _ in range(300):  # the fallback request finishes; then everything is free again
+            if not w.engine.has_unfinished() and kv.num_free() == free0:
+                break
+            await asyncio.sleep(0.02)
+        assert w.agent._shm_ext.free_blocks() == shm0
+        assert kv.num_free() == free0
+
+    try:
+        asyncio.run(main())
+    finally:
+        w.aeng.shutdown()
+        w.agent.close()

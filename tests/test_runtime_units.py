@@ -444,3 +444,70 @@ def test_late_admission_wait_stops_at_target_or_completion():
     la.inflight = {"x": None, "t_launch": now, "est_done": now + 0.5, "done": None}
     la.wait(Ev(0.0))  # already done when looked at: no wait, completion time unknown
     assert la.inflight["done"] is None
+
+
+def test_streamer_ring_stall_is_transient():
+    """a stalled output ring (GC pause / slow SSE writer in the streamer) must not drop
+    outputs for good.  Held-back messages go out in order once the ring drains; the plane is
+    declared dead only when the streamer process has exited (and then /health fails)."""
+    import msgpack
+
+    from mxserve.worker.streamer import RingPlane
+
+    class _Ring:
+        slot_bytes = 1 << 16
+
+        def __init__(self):
+            self.accept = False
+            self.got = []
+
+        def push(self, data, timeout):
+            if not self.accept:
+                return False
+            self.got.append(msgpack.unpackb(data, raw=False))
+            return True
+
+        def pop(self, i, timeout):
+            return None
+
+    class _Proc:
+        rc = None
+
+        def poll(self):
+            return self.rc
+
+    ring, proc = _Ring(), _Proc()
+    rp = RingPlane(worker=None, cmd_ring=ring, out_ring=ring, proc=proc)
+    rp.emit_tuples([("a", 1, False, None, 0, 0, None, None, None)])
+    rp.emit_tuples([("a", 2, True, "length", 0, 0, None, None, None)])  # the finish marker
+    assert not rp.dead and len(rp.backlog) == 2 and rp.stalls >= 1
+    ring.accept = True
+    assert rp.poll(0.0) is None  # an idle engine loop flushes the backlog
+    assert [m[0][1] for m in ring.got] == [1, 2] and not rp.backlog and rp.dropped == 0
+    ring.accept = False
+    proc.rc = -9  # the streamer died: now the plane is dead
+    rp.emit_tuples([("b", 1, False, None, 0, 0, None, None, None)])
+    assert rp.dead and rp.streamer_exited() and rp.dropped == 1
+
+
+def test_meta_ring_push_is_bounded():
+    """a TP follower that stops reading makes the driver's metadata push raise after
+    MXS_TP_META_TIMEOUT_S instead of retrying forever (the worker then exits and is restarted)."""
+    import pytest as _pt
+
+    from mxserve.parallel.comm import MetaRing
+
+    class _Full:
+        slot_bytes = 1 << 16
+        calls = 0
+
+        def push(self, data, timeout):
+            self.calls += 1
+            return False
+
+    r = _Full()
+    mr = MetaRing(r, 0)
+    mr.PUSH_TIMEOUT_S = 30.0
+    with _pt.raises(RuntimeError, match="stopped reading"):
+        mr.send(("step", 1))
+    assert r.calls == 3

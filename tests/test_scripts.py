@@ -191,8 +191,8 @@ def test_bench_contract_cpu(mode, nproc, launcher, tmp_path):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(port)] + cmd[1:]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=str(tmp_path),
-                       env=dict(env, OMP_NUM_THREADS="1"))
+    from tests.bench_utils import run_group
+    r = run_group(cmd + ["--time-budget-s", "280"], timeout=330, cwd=str(tmp_path), env=dict(env, OMP_NUM_THREADS="1"))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
