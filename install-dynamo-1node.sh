@@ -24,11 +24,29 @@ ROCM_DEVICE_PLUGIN_URL="${ROCM_DEVICE_PLUGIN_URL:-https://raw.githubusercontent.
 GPU_OPERATOR_HELM_TIMEOUT="${GPU_OPERATOR_HELM_TIMEOUT:-15m}"
 GPU_ALLOCATABLE_WAIT_ATTEMPTS="${GPU_ALLOCATABLE_WAIT_ATTEMPTS:-120}"
 GPU_ALLOCATABLE_WAIT_INTERVAL="${GPU_ALLOCATABLE_WAIT_INTERVAL:-5}"
+GPU_OPERATOR_POD_WAIT_ATTEMPTS="${GPU_OPERATOR_POD_WAIT_ATTEMPTS:-180}"
+GPU_OPERATOR_POD_WAIT_INTERVAL="${GPU_OPERATOR_POD_WAIT_INTERVAL:-5}"
+# multi-node gang scheduling (Grove / KAI scheduler): accepted for drop-in compatibility with the
+# reference's flags; a single node needs neither, so they are reported and otherwise no-ops
+ENABLE_GROVE="${ENABLE_GROVE:-false}"
+ENABLE_KAI_SCHEDULER="${ENABLE_KAI_SCHEDULER:-false}"
 
 say() { printf '\n[install] %s\n' "$*"; }
 die() { printf 'ERROR: %s\n' "$*" >&2; exit 1; }
 for c in kubectl; do command -v "$c" >/dev/null || die "missing $c"; done
 kubectl version >/dev/null 2>&1 || die "cannot reach the cluster (KUBECONFIG?)"
+
+say "configuration"
+for v in NAMESPACE RELEASE_VERSION MXS_IMAGE NAMESPACE_RESTRICTED_OPERATOR ENABLE_GROVE ENABLE_KAI_SCHEDULER \
+         PROMETHEUS_ENDPOINT GPU_RESOURCE GPU_OPERATOR_MODE GPU_OPERATOR_NS GPU_OPERATOR_RELEASE GPU_OPERATOR_HELM_TIMEOUT; do
+  echo "  ${v}=${!v}"
+done
+for v in ENABLE_GROVE ENABLE_KAI_SCHEDULER; do
+  if [[ "${!v}" == "true" ]]; then
+    echo "WARNING: ${v}=true has no effect: mxserve targets one node (8 GPUs, SURVEY §2.4 P07), where the" \
+         "operator packs P/D groups into pods itself and no gang scheduler is needed" >&2
+  fi
+done
 
 say "storage: default StorageClass"
 if ! kubectl get storageclass -o jsonpath='{range .items[*]}{.metadata.annotations.storageclass\.kubernetes\.io/is-default-class}{"\n"}{end}' | grep -q true; then
@@ -72,6 +90,18 @@ case "$GPU_OPERATOR_MODE" in
   skip) say "GPU operator installation skipped" ;;
   *) die "GPU_OPERATOR_MODE must be operator|device-plugin|skip" ;;
 esac
+
+if [[ "$GPU_OPERATOR_MODE" == "operator" ]]; then
+  # the device plugin / node labeller DaemonSets must be up before the GPUs show as allocatable
+  say "waiting for the AMD GPU Operator pods in ${GPU_OPERATOR_NS} to be Running/Completed"
+  for ((i = 1; i <= GPU_OPERATOR_POD_WAIT_ATTEMPTS; i++)); do
+    not_ready="$(kubectl get pods -n "$GPU_OPERATOR_NS" --no-headers 2>/dev/null \
+                 | awk '$3 != "Running" && $3 != "Completed" {n++} END {print n + 0}')"
+    [[ "$not_ready" == "0" ]] && break
+    sleep "$GPU_OPERATOR_POD_WAIT_INTERVAL"
+  done
+  kubectl get pods -n "$GPU_OPERATOR_NS" || true
+fi
 
 say "waiting for ${GPU_RESOURCE} to become allocatable"
 for ((i = 1; i <= GPU_ALLOCATABLE_WAIT_ATTEMPTS; i++)); do

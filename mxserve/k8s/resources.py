@@ -216,37 +216,64 @@ def _container(g: GraphSpec, s: ServiceSpec) -> dict:
 
 
 PAIR_LABEL = "mxserve.io/pd-pair"
+SHAPE_LABEL = "mxserve.io/pd-group-shape"
+# GPUs of one node: a P/D group pod never asks for more (single node)
+NODE_GPUS = int(os.environ.get("MXS_NODE_GPUS", "8"))
 
 
 def pd_pairs(g: GraphSpec) -> Optional[tuple]:
-    """(decode service, prefill service) to co-locate, or None.  MXS_PD_POD_MODE=pair (default)
-    renders each decode replica with a prefill worker in one pod that holds both groups of GPUs
+    """(decode service, prefill service) whose workers are packed into P/D group pods, or None.
+    MXS_PD_POD_MODE=group (default; `pair` is accepted as its old name) renders the graph's decode
+    and prefill replicas as pods that each hold several workers of both roles and all their GPUs
     (SURVEY.md §5.8 mitigation #1; mxserve/worker/pair.py); =split keeps the reference's two-pod
-    form (then the KV crosses pods over hostIPC, the /dev/shm arena or HTTP)."""
-    if os.environ.get("MXS_PD_POD_MODE", "pair") != "pair":
+    form (then the KV crosses pods over hostIPC: the host's /dev/shm arena or HTTP)."""
+    if os.environ.get("MXS_PD_POD_MODE", "group") not in ("group", "pair"):
         return None
     dec = [s for s in g.services if s.component_type == "worker" and s.sub_component_type == "decode"]
     pre = [s for s in g.services if s.component_type == "worker" and s.sub_component_type == "prefill"]
-    if not dec or not pre:
+    if not dec or not pre or dec[0].replicas <= 0 or pre[0].replicas <= 0:
         return None
     return dec[0], pre[0]
+
+
+def pd_groups(d: ServiceSpec, p: ServiceSpec, node_gpus: int = 0) -> list:
+    """Pack P prefill and D decode workers (their own `gpu` limits each) into the fewest pods that
+    fit one node's GPUs, spreading both roles evenly so every pod has decode workers and, where
+    there are enough, prefill workers of its own.  Returns [(prefill workers, decode workers)] per
+    pod: the reference's independent counts (examples/deploy/vllm/disagg.yaml:22,42) at any P:D
+    ratio -- 3P+5D is one 8-GPU pod with exactly 3 prefill and 5 decode workers."""
+    node = node_gpus or NODE_GPUS
+    gp, gd = p.gpus or 1, d.gpus or 1
+    P, D = p.replicas, d.replicas
+    if gp > node or gd > node:
+        raise ValidationError(f"a worker asks for more GPUs than a node has ({max(gp, gd)} > {node})")
+    n = max(1, -(-(P * gp + D * gd) // node))
+    while True:
+        groups = [(P // n + (i < P % n), D // n + (i < D % n)) for i in range(n)]
+        if all(pi * gp + di * gd <= node for pi, di in groups):
+            return [gr for gr in groups if gr != (0, 0)]
+        n += 1
 
 
 def _full_command(g: GraphSpec, s: ServiceSpec) -> list:
     return [str(c) for c in (s.command or _default_command(g, s))] + [str(a) for a in (s.args or [])]
 
 
-def _pair_container(g: GraphSpec, d: ServiceSpec, p: ServiceSpec) -> dict:
+def _group_container(g: GraphSpec, d: ServiceSpec, p: ServiceSpec, n_pre: int, n_dec: int) -> dict:
+    """One container running n_dec decode + n_pre prefill workers (mxserve/worker/pair.py assigns
+    each its GPUs and port; decode workers first, so the pod's readiness port is a decode worker)."""
     c = _container(g, d)
     c["command"] = ["python3", "-m", "mxserve.worker.pair"]
     c.pop("args", None)
     have = {e["name"] for e in c["env"]}
     c["env"] += [dict(e) for e in p.envs if e["name"] not in have]
-    c["env"] += [{"name": "MXS_PAIR_DECODE_CMD", "value": json.dumps(_full_command(g, d))},
-                 {"name": "MXS_PAIR_PREFILL_CMD", "value": json.dumps(_full_command(g, p))},
+    spec = ([{"role": "decode", "cmd": _full_command(g, d), "gpus": d.gpus or 1}] * n_dec
+            + [{"role": "prefill", "cmd": _full_command(g, p), "gpus": p.gpus or 1}] * n_pre)
+    c["env"] += [{"name": "MXS_GROUP_SPEC", "value": json.dumps(spec)},
                  {"name": "POD_NAME", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}}]
-    c["ports"].append({"name": "prefill", "containerPort": WORKER_PORT + 1})
-    n = (d.gpus or 1) + (p.gpus or 1)
+    c["ports"] = [{"name": "system" if i == 0 else f"w{i}", "containerPort": WORKER_PORT + i}
+                  for i in range(len(spec))]
+    n = sum(w["gpus"] for w in spec)
     c["resources"] = {"limits": {GPU_RESOURCE: str(n)}, "requests": {GPU_RESOURCE: str(n)}}
     mounts = {m["mountPath"] for m in c.get("volumeMounts", [])}
     for vm in p.volume_mounts:
@@ -258,13 +285,26 @@ def _pair_container(g: GraphSpec, d: ServiceSpec, p: ServiceSpec) -> dict:
     return c
 
 
+def _deployment(g: GraphSpec, name: str, labels: dict, owner: list, replicas: int, pod_spec: dict,
+                extra_selector: Optional[dict] = None) -> dict:
+    sel = {"app.kubernetes.io/name": name, **(extra_selector or {})}
+    return {"apiVersion": "apps/v1", "kind": "Deployment",
+            "metadata": {"name": name if not extra_selector else f"{name}-{extra_selector[SHAPE_LABEL]}",
+                         "namespace": g.namespace, "labels": dict(labels, **(extra_selector or {})),
+                         "ownerReferences": owner},
+            "spec": {"replicas": replicas, "selector": {"matchLabels": sel},
+                     "template": {"metadata": {"labels": dict(labels, **(extra_selector or {}))}, "spec": pod_spec}}}
+
+
 def render_children(g: GraphSpec, dcd_uids: Optional[dict] = None) -> list[dict]:
-    """Deployment + Service (+ PodMonitor) per service, owned by its DCD.  With P/D pairing the
-    decode service's Deployment runs pair pods and the prefill service's keeps only the prefill
-    replicas beyond the decode count."""
+    """Deployment + Service (+ PodMonitor) per service, owned by its DCD.  With P/D grouping the
+    decode service's Deployment(s) run the group pods (pd_groups: one Deployment per distinct
+    group shape) and the prefill service's Deployment keeps 0 replicas (every prefill worker runs
+    inside a group pod)."""
     objs = []
     dcd_uids = dcd_uids or {}
     pair = pd_pairs(g)
+    groups = pd_groups(pair[0], pair[1]) if pair is not None else []
     for s in g.services:
         name = f"{g.name}-{s.dns_name}"
         labels = {NS_LABEL: f"{g.namespace}-{g.name}", COMPONENT_LABEL: s.key, TYPE_LABEL: s.component_type,
@@ -272,35 +312,46 @@ def render_children(g: GraphSpec, dcd_uids: Optional[dict] = None) -> list[dict]
         if s.sub_component_type:
             labels[SUBTYPE_LABEL] = s.sub_component_type
         owner = _owner(DCD_KIND, name, dcd_uids.get(name))
-        replicas = s.replicas
-        paired = pair is not None and s is pair[0]
-        if paired:
-            labels[PAIR_LABEL] = f"{pair[0].key}+{pair[1].key}"
-            container = _pair_container(g, pair[0], pair[1])
-        else:
-            container = _container(g, s)
-            if pair is not None and s is pair[1]:
-                replicas = max(0, s.replicas - pair[0].replicas)
-        pod_spec = {"containers": [container], "terminationGracePeriodSeconds": 30}
-        vms = list(s.volume_mounts) + (list(pair[1].volume_mounts) if paired else [])
+        grouped = pair is not None and s is pair[0]
+        vms = list(s.volume_mounts) + (list(pair[1].volume_mounts) if grouped else [])
         vols = []
         for vm in vms:
             if vm["name"] not in {v["name"] for v in vols}:
                 vols.append({"name": vm["name"], "persistentVolumeClaim": {"claimName": vm["name"]}})
-        if s.gpus or paired:
+        split_pd = pair is None and s.sub_component_type in ("prefill", "decode") and s.component_type == "worker"
+        if (s.gpus or grouped) and not split_pd:
+            # a pod-private /dev/shm for the TP ranks' metadata ring, RCCL and (group pods) the
+            # workers' shared KV staging arena
             vols.append({"name": "dshm", "emptyDir": {"medium": "Memory"}})
-            if s.sub_component_type in ("prefill", "decode") and not paired:
-                # two-pod form: the xGMI KV transfer between prefill and decode pods opens the
-                # peer's staging arena with hipIpcOpenMemHandle; the pods need a shared IPC
-                # namespace (SURVEY.md §5.8 mitigation #2)
-                pod_spec["hostIPC"] = True
-        if vols:
-            pod_spec["volumes"] = vols
-        objs.append({
-            "apiVersion": "apps/v1", "kind": "Deployment",
-            "metadata": {"name": name, "namespace": g.namespace, "labels": dict(labels), "ownerReferences": owner},
-            "spec": {"replicas": replicas, "selector": {"matchLabels": {"app.kubernetes.io/name": name}},
-                     "template": {"metadata": {"labels": dict(labels)}, "spec": pod_spec}}})
+
+        def pod(container: dict) -> dict:
+            spec = {"containers": [container], "terminationGracePeriodSeconds": 30}
+            if split_pd and s.gpus:
+                # two-pod form: the xGMI KV transfer between prefill and decode pods opens the peer's
+                # staging arena with hipIpcOpenMemHandle, and the /dev/shm arena must be the host's:
+                # the pods share the host IPC namespace (SURVEY.md §5.8 mitigation #2) and mount no
+                # private /dev/shm over it
+                spec["hostIPC"] = True
+                container.get("volumeMounts", [])[:] = [m for m in container.get("volumeMounts", [])
+                                                        if m["name"] != "dshm"]
+                if not container.get("volumeMounts"):
+                    container.pop("volumeMounts", None)
+            if vols:
+                spec["volumes"] = [dict(v) for v in vols]
+            return spec
+
+        if grouped:
+            labels[PAIR_LABEL] = f"{pair[0].key}+{pair[1].key}"
+            shapes: dict = {}
+            for gr in groups:
+                shapes[gr] = shapes.get(gr, 0) + 1
+            for k, ((n_pre, n_dec), count) in enumerate(sorted(shapes.items(), key=lambda x: (-x[1], x[0]))):
+                c = _group_container(g, pair[0], pair[1], n_pre, n_dec)
+                objs.append(_deployment(g, name, labels, owner, count, pod(c),
+                                        None if k == 0 else {SHAPE_LABEL: f"g{k + 1}"}))
+        else:
+            replicas = 0 if (pair is not None and s is pair[1]) else s.replicas
+            objs.append(_deployment(g, name, labels, owner, replicas, pod(_container(g, s))))
         is_fe = s.component_type == "frontend"
         svc_spec = {"selector": {"app.kubernetes.io/name": name},
                     "ports": [{"name": "http" if is_fe else "system", "port": FRONTEND_PORT if is_fe else WORKER_PORT,
@@ -311,13 +362,27 @@ def render_children(g: GraphSpec, dcd_uids: Optional[dict] = None) -> list[dict]
                      "metadata": {"name": name, "namespace": g.namespace, "labels": dict(labels),
                                   "ownerReferences": owner},
                      "spec": svc_spec})
+        endpoints = [{"port": "http" if is_fe else "system", "path": "/metrics", "interval": "15s"}]
+        if grouped:  # every worker of a group pod serves its own /metrics
+            n_max = max(a + b for a, b in groups)
+            endpoints += [{"port": f"w{i}", "path": "/metrics", "interval": "15s"} for i in range(1, n_max)]
         objs.append({"apiVersion": "monitoring.coreos.com/v1", "kind": "PodMonitor",
                      "metadata": {"name": name, "namespace": g.namespace, "labels": dict(labels),
                                   "ownerReferences": owner},
                      "spec": {"selector": {"matchLabels": {"app.kubernetes.io/name": name}},
-                              "podMetricsEndpoints": [{"port": "http" if is_fe else "system", "path": "/metrics",
-                                                       "interval": "15s"}]}})
+                              "podMetricsEndpoints": endpoints}})
     return objs
+
+
+def graph_gpus(g: GraphSpec) -> int:
+    """GPUs the rendered graph asks for (what has to fit the node)."""
+    total = 0
+    for o in render_children(g):
+        if o["kind"] != "Deployment":
+            continue
+        c = o["spec"]["template"]["spec"]["containers"][0]
+        total += o["spec"]["replicas"] * int((c.get("resources") or {}).get("limits", {}).get(GPU_RESOURCE, 0))
+    return total
 
 
 # --------------------------------------------------------------------------- DGDR

@@ -1,20 +1,23 @@
-"""P/D pair pod launcher: one decode worker and one prefill worker in ONE container that holds both
-groups of GPUs (cross-pod caveat, mitigation #1).
+"""P/D group pod launcher: several decode and prefill workers in ONE container that holds all their
+GPUs (cross-pod caveat, mitigation #1).
 
-The reference runs prefill and decode as separate services with `gpu: "1"` each
+The reference runs prefill and decode as separate services, each scaled by its own `replicas`
 (examples/deploy/vllm/disagg.yaml:18-57, sglang/disagg.yaml:18-87).  On MI355X the prompt's KV moves
 prefill -> decode by IPC-mapping the decode GPU's staging arena (hipIpcOpenMemHandle) and pushing
 over xGMI; that needs both processes to see both GPUs, which two pods that each own one GPU do not.
-So the operator renders every decode replica of a graph that also has a prefill service as a pair
-pod: `amd.com/gpu: <decode tp> + <prefill tp>`, this launcher as the command, and the two services'
-own commands in MXS_PAIR_DECODE_CMD / MXS_PAIR_PREFILL_CMD.
+So the operator packs a graph's prefill and decode workers into group pods (resources.pd_groups:
+any P:D ratio, as few pods as fit one node -- 3P+5D is one 8-GPU pod) and runs this launcher with
+the workers in MXS_GROUP_SPEC = [{"role": "decode"|"prefill", "cmd": [...], "gpus": n}, ...]:
 
-  decode   GPUs [0, tp_d), port DYN_SYSTEM_PORT (the pod's readiness / metrics port)
-  prefill  GPUs [tp_d, tp_d + tp_p), port DYN_SYSTEM_PORT + 1
-Both register with the frontend under the same pair id (the pod name), and the frontend hands a
-decode worker a prefill worker of its own pair first.  /dev/shm is shared too, so the host-staged
-fallback is the shm arena, not HTTP.  The launcher forwards SIGTERM and exits with the first child
-that exits (k8s then restarts the whole pair).
+  worker i   GPUs [sum of the earlier workers' gpus, + its own), port DYN_SYSTEM_PORT + i
+             (decode workers first: worker 0's port is the pod's readiness / metrics port)
+Every worker registers with the frontend under the same group id (the pod name), and the frontend
+hands a decode worker a prefill worker of its own group first.  /dev/shm is shared too, so the
+host-staged fallback is the shm arena, not HTTP.  The launcher forwards SIGTERM and exits with the
+first child that exits (k8s then restarts the whole group).
+
+The older pair form (MXS_PAIR_DECODE_CMD / MXS_PAIR_PREFILL_CMD: one worker of each role) is still
+accepted.
 """
 from __future__ import annotations
 
@@ -34,21 +37,38 @@ def _tp_of(cmd: list) -> int:
     return 1
 
 
-def child_envs(base: dict, decode_cmd: list, prefill_cmd: list) -> tuple:
+def group_envs(base: dict, spec: list) -> list:
+    """(cmd, env) of every worker of the group: its GPU offset, port and ids."""
     port = int(base.get("DYN_SYSTEM_PORT", base.get("MXS_WORKER_PORT", "8081")))
-    pair = base.get("MXS_PAIR_ID") or base.get("POD_NAME") or socket.gethostname()
-    tp_d = _tp_of(decode_cmd)
-    common = dict(base, MXS_PAIR_ID=pair, HSA_ENABLE_IPC_MODE_LEGACY=base.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
-    dec = dict(common, MXS_DEVICE_OFFSET="0", DYN_SYSTEM_PORT=str(port), MXS_WORKER_ID=f"decode-{pair}")
-    pre = dict(common, MXS_DEVICE_OFFSET=str(tp_d), DYN_SYSTEM_PORT=str(port + 1), MXS_WORKER_ID=f"prefill-{pair}")
+    group = base.get("MXS_PAIR_ID") or base.get("POD_NAME") or socket.gethostname()
+    common = dict(base, MXS_PAIR_ID=group, HSA_ENABLE_IPC_MODE_LEGACY=base.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    out, off, seen = [], 0, {}
+    for i, w in enumerate(spec):
+        cmd = [str(c) for c in w["cmd"]]
+        gpus = int(w.get("gpus") or _tp_of(cmd))
+        role = w["role"]
+        k = seen[role] = seen.get(role, -1) + 1
+        wid = f"{role}-{group}" + (f"-{k}" if k else "")
+        out.append((cmd, dict(common, MXS_DEVICE_OFFSET=str(off), DYN_SYSTEM_PORT=str(port + i),
+                              MXS_WORKER_ID=wid, MXS_STREAM_PORT=str(port + 100 + i))))
+        off += gpus
+    return out
+
+
+def child_envs(base: dict, decode_cmd: list, prefill_cmd: list) -> tuple:
+    """The pair form: decode GPUs [0, tp_d) on the pod's port, prefill the next GPUs on port + 1."""
+    (_, dec), (_, pre) = group_envs(base, [{"role": "decode", "cmd": decode_cmd, "gpus": _tp_of(decode_cmd)},
+                                           {"role": "prefill", "cmd": prefill_cmd, "gpus": _tp_of(prefill_cmd)}])
     return dec, pre
 
 
 def main() -> int:
-    decode_cmd = json.loads(os.environ["MXS_PAIR_DECODE_CMD"])
-    prefill_cmd = json.loads(os.environ["MXS_PAIR_PREFILL_CMD"])
-    dec_env, pre_env = child_envs(dict(os.environ), decode_cmd, prefill_cmd)
-    procs = [subprocess.Popen(decode_cmd, env=dec_env), subprocess.Popen(prefill_cmd, env=pre_env)]
+    if os.environ.get("MXS_GROUP_SPEC"):
+        spec = json.loads(os.environ["MXS_GROUP_SPEC"])
+    else:
+        spec = [{"role": "decode", "cmd": json.loads(os.environ["MXS_PAIR_DECODE_CMD"])},
+                {"role": "prefill", "cmd": json.loads(os.environ["MXS_PAIR_PREFILL_CMD"])}]
+    procs = [subprocess.Popen(cmd, env=env) for cmd, env in group_envs(dict(os.environ), spec)]
 
     def stop(signum, _frame):
         for p in procs:

@@ -90,10 +90,12 @@ def test_disaggregated_chat_over_ipc(tmp_path):
             f.close()
 
 
-def test_pd_pair_pod_launcher(tmp_path):
-    """The P/D pair pod the operator renders: `python -m mxserve.worker.pair` runs the decode and
-    the prefill worker (commands from MXS_PAIR_*_CMD) in one container; both register under one pair
-    id, the frontend sends the decode worker its own prefill worker and the KV moves over IPC."""
+@pytest.mark.parametrize("form", ["pair", "group"])
+def test_pd_pair_pod_launcher(tmp_path, form):
+    """The P/D group pod the operator renders: `python -m mxserve.worker.pair` runs the decode and
+    prefill workers in one container (pair: MXS_PAIR_*_CMD, one of each; group: MXS_GROUP_SPEC, here
+    1 decode + 2 prefill); all register under one group id, the frontend sends the decode worker a
+    prefill worker of its own group and the KV moves over IPC."""
     import json
     import torch
     if torch.cuda.device_count() < 1:
@@ -110,6 +112,13 @@ def test_pd_pair_pod_launcher(tmp_path):
                MXS_PAIR_DECODE_CMD=json.dumps([sys.executable, "-m", "dynamo.vllm", "--is-decode-worker"] + common),
                MXS_PAIR_PREFILL_CMD=json.dumps([sys.executable, "-m", "dynamo.vllm", "--is-prefill-worker"] + common))
     env.pop("MXS_WORKER_ID", None)
+    n_workers = 2
+    if form == "group":
+        pre = {"role": "prefill", "cmd": [sys.executable, "-m", "dynamo.vllm", "--is-prefill-worker"] + common, "gpus": 1}
+        env["MXS_GROUP_SPEC"] = json.dumps(
+            [{"role": "decode", "cmd": [sys.executable, "-m", "dynamo.vllm", "--is-decode-worker"] + common, "gpus": 1},
+             pre, pre])
+        n_workers = 3
     log = open(tmp_path / "pair.log", "w")
     proc = subprocess.Popen([sys.executable, "-m", "mxserve.worker.pair"], cwd=ROOT, env=env, stdout=log,
                             stderr=subprocess.STDOUT)
@@ -117,14 +126,16 @@ def test_pd_pair_pod_launcher(tmp_path):
         def ready():
             if proc.poll() is not None:
                 raise RuntimeError("pair launcher exited:\n" + (tmp_path / "pair.log").read_text()[-4000:])
-            return len(fe.registry.list()) == 2
+            return len(fe.registry.list()) == n_workers
         wait_for(ready, timeout=240, interval=1.0)
         ws = fe.registry.list()
         assert {w.role for w in ws} == {"prefill", "decode"} and {w.pair for w in ws} == {"pairpod-0"}
-        body = {"model": MODEL, "messages": [{"role": "user", "content": "pair pod " * 50}], "max_tokens": 12,
-                "temperature": 0, "ignore_eos": True}
-        r = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=120)
-        assert r.status_code == 200 and r.json()["usage"]["completion_tokens"] == 12, r.text
+        assert len({w.worker_id for w in ws}) == n_workers
+        for i in range(2 if form == "group" else 1):
+            body = {"model": MODEL, "messages": [{"role": "user", "content": f"pair pod {i} " * 50}],
+                    "max_tokens": 12, "temperature": 0, "ignore_eos": True}
+            r = httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=120)
+            assert r.status_code == 200 and r.json()["usage"]["completion_tokens"] == 12, r.text
         m = httpx.get(f"http://127.0.0.1:{port}/metrics", timeout=10).text
         moved = [ln for ln in m.splitlines()
                  if ln.startswith("dynamo_component_kv_transfer_bytes_total") and 'backend="xgmi"' in ln]

@@ -78,10 +78,10 @@ def test_render_contract(monkeypatch):
 
 @pytest.mark.parametrize("manifest", ["examples/deploy/vllm/disagg.yaml", "examples/deploy/sglang/disagg.yaml",
                                       "examples/deploy/trtllm/disagg.yaml"])
-def test_render_pd_pair_pod(manifest):
-    """Default: each decode replica is ONE pod holding the decode and the prefill worker (both
-    services' GPUs), so the prefill process can IPC-map the decode GPU's staging arena (SURVEY.md §5.8
-    mitigation #1); the prefill Deployment keeps only prefill replicas beyond the decode count."""
+def test_render_pd_group_pod(manifest):
+    """Default: the graph's decode and prefill workers run in ONE pod holding both services' GPUs,
+    so a prefill process can IPC-map the decode GPU's staging arena (SURVEY.md §5.8 mitigation #1);
+    the prefill Deployment keeps 0 replicas (its workers live in the group pod)."""
     import json as _json
 
     from mxserve.k8s.resources import PAIR_LABEL, WORKER_PORT
@@ -97,26 +97,110 @@ def test_render_pd_pair_pod(manifest):
     assert c["command"] == ["python3", "-m", "mxserve.worker.pair"] and "args" not in c
     assert c["resources"]["limits"] == {"amd.com/gpu": str(dec.gpus + pre.gpus)}
     env = {e["name"]: e.get("value") for e in c["env"]}
-    dcmd, pcmd = _json.loads(env["MXS_PAIR_DECODE_CMD"]), _json.loads(env["MXS_PAIR_PREFILL_CMD"])
+    grp = _json.loads(env["MXS_GROUP_SPEC"])
+    assert [w["role"] for w in grp] == ["decode", "prefill"]
+    dcmd, pcmd = grp[0]["cmd"], grp[1]["cmd"]
     assert dcmd[:len(dec.command or [])] == list(dec.command or []) and dcmd[-len(dec.args):] == list(map(str, dec.args))
     assert pcmd[-len(pre.args):] == list(map(str, pre.args))
     assert {p["containerPort"] for p in c["ports"]} == {WORKER_PORT, WORKER_PORT + 1}
     assert any(v.get("emptyDir", {}).get("medium") == "Memory" for v in spec["volumes"])  # shared /dev/shm
     assert pod["metadata"]["labels"][PAIR_LABEL] == f"{dec.key}+{pre.key}"
-    assert pod["spec"]["replicas"] == dec.replicas
-    assert deps[f"{g.name}-{pre.dns_name}"]["spec"]["replicas"] == max(0, pre.replicas - dec.replicas)
+    assert pod["spec"]["replicas"] == 1
+    assert deps[f"{g.name}-{pre.dns_name}"]["spec"]["replicas"] == 0
+
+
+def _pd_graph(n_pre: int, n_dec: int, g_pre: int = 1, g_dec: int = 1):
+    with open(os.path.join(ROOT, "examples/deploy/vllm/disagg.yaml")) as f:
+        obj = yaml.safe_load(f)
+    for key, s in obj["spec"]["services"].items():
+        if s.get("subComponentType") == "prefill":
+            s["replicas"], s["resources"] = n_pre, {"limits": {"gpu": str(g_pre)}}
+        elif s.get("subComponentType") == "decode":
+            s["replicas"], s["resources"] = n_dec, {"limits": {"gpu": str(g_dec)}}
+    return parse_dgd(obj, "dynamo-system")
+
+
+@pytest.mark.parametrize("n_pre,n_dec,g_pre,g_dec,pods,gpus", [
+    (3, 5, 1, 1, 1, 8),    # bench.py's capacity model for 8 GPUs: ONE pod, 3 prefill + 5 decode workers
+    (2, 6, 1, 1, 1, 8),    # the reference DGDR example's measured plan (profiles/r2_dgdr_*)
+    (1, 1, 1, 1, 1, 2),
+    (1, 3, 1, 1, 1, 4),
+    (6, 10, 1, 1, 2, 16),  # two nodes' worth: two identical 8-GPU pods
+    (3, 4, 1, 1, 1, 7),
+    (2, 3, 2, 2, 2, 10),   # TP-2 workers: a 5-worker group would need 10 GPUs, so two pods
+])
+def test_pd_groups_any_ratio_fits_the_node(n_pre, n_dec, g_pre, g_dec, pods, gpus):
+    """any P:D ratio deploys on one node at xGMI speed -- the group pods
+    hold exactly the graph's prefill and decode workers, each pod fits 8 GPUs, and nothing else
+    runs prefill."""
+    import json as _json
+
+    from mxserve.k8s.resources import graph_gpus
+    g = _pd_graph(n_pre, n_dec, g_pre, g_dec)
+    deps = [d for d in render_children(g) if d["kind"] == "Deployment"]
+    group_deps = [d for d in deps if "MXS_GROUP_SPEC" in {e["name"] for e in
+                                                           d["spec"]["template"]["spec"]["containers"][0]["env"]}]
+    n_pods = sum(d["spec"]["replicas"] for d in group_deps)
+    assert n_pods == pods
+    roles = {"prefill": 0, "decode": 0}
+    for d in group_deps:
+        c = d["spec"]["template"]["spec"]["containers"][0]
+        grp = _json.loads(next(e["value"] for e in c["env"] if e["name"] == "MXS_GROUP_SPEC"))
+        assert sum(w["gpus"] for w in grp) == int(c["resources"]["limits"]["amd.com/gpu"]) <= 8
+        assert grp[0]["role"] == "decode"  # the readiness port is a decode worker's
+        for w in grp:
+            roles[w["role"]] += d["spec"]["replicas"]
+    assert roles == {"prefill": n_pre, "decode": n_dec}
+    assert graph_gpus(g) == gpus
+    sels = [tuple(sorted(d["spec"]["selector"]["matchLabels"].items())) for d in deps]
+    assert len(sels) == len(set(sels))  # Deployments never share a selector
+
+
+def test_dgdr_reference_plan_renders_within_one_node():
+    """The reference DGDR example's template with the profiler's measured plan (2P + 6D) renders
+    to 8 GPUs (round 2 rendered 12: one prefill per decode replica)."""
+    import json as _json
+
+    from mxserve.k8s.resources import apply_plan_to_template, graph_gpus, parse_dgdr
+    plan = _json.load(open(os.path.join(ROOT, "profiles/r2_dgdr_profiler_measure_qwen3_0.6b.json")))["disagg"]
+    with open(os.path.join(ROOT, "examples/dgdr/trtllm/disagg.yaml")) as f:
+        tmpl = yaml.safe_load(f)
+    with open(os.path.join(ROOT, "examples/dgdr/trtllm/dgdr.yaml")) as f:
+        req = parse_dgdr(yaml.safe_load(f), "dynamo-system")
+    g = parse_dgd(apply_plan_to_template(tmpl, plan, req), "dynamo-system")
+    assert graph_gpus(g) == 8
+
+
+def test_split_pd_pods_share_the_host_shm(monkeypatch):
+    """MXS_PD_POD_MODE=split: prefill and decode pods share the host IPC namespace and mount no
+    private /dev/shm over it, so the /dev/shm KV arena one creates is visible to the other."""
+    from mxserve.k8s.resources import SUBTYPE_LABEL
+    monkeypatch.setenv("MXS_PD_POD_MODE", "split")
+    g = _pd_graph(2, 3)
+    for d in (o for o in render_children(g) if o["kind"] == "Deployment"):
+        if d["metadata"]["labels"].get(SUBTYPE_LABEL) not in ("prefill", "decode"):
+            continue
+        spec = d["spec"]["template"]["spec"]
+        assert spec.get("hostIPC") is True
+        assert not any(v["name"] == "dshm" for v in spec.get("volumes", []))
+        assert not any(m["name"] == "dshm" for m in spec["containers"][0].get("volumeMounts", []))
 
 
 def test_pair_launcher_envs():
-    """The pair launcher gives the decode worker GPUs [0, tp_d) and the pod's system port, the
-    prefill worker the next GPUs and port + 1, both the same pair id."""
-    from mxserve.worker.pair import child_envs
+    """The group launcher gives worker i its GPUs after the earlier workers' and port + i; every
+    worker shares the group id."""
+    from mxserve.worker.pair import child_envs, group_envs
     dec, pre = child_envs({"DYN_SYSTEM_PORT": "9090", "POD_NAME": "g-decode-abc"},
                           ["python3", "-m", "dynamo.sglang", "--tp", "2"], ["python3", "-m", "dynamo.sglang"])
     assert (dec["MXS_DEVICE_OFFSET"], dec["DYN_SYSTEM_PORT"]) == ("0", "9090")
     assert (pre["MXS_DEVICE_OFFSET"], pre["DYN_SYSTEM_PORT"]) == ("2", "9091")
     assert dec["MXS_PAIR_ID"] == pre["MXS_PAIR_ID"] == "g-decode-abc"
     assert dec["MXS_WORKER_ID"] != pre["MXS_WORKER_ID"]
+    spec = [{"role": "decode", "cmd": ["w"], "gpus": 1}] * 5 + [{"role": "prefill", "cmd": ["w"], "gpus": 1}] * 3
+    envs = [e for _, e in group_envs({"DYN_SYSTEM_PORT": "8081", "POD_NAME": "p"}, spec)]
+    assert [e["MXS_DEVICE_OFFSET"] for e in envs] == [str(i) for i in range(8)]
+    assert [e["DYN_SYSTEM_PORT"] for e in envs] == [str(8081 + i) for i in range(8)]
+    assert len({e["MXS_WORKER_ID"] for e in envs}) == 8 and {e["MXS_PAIR_ID"] for e in envs} == {"p"}
 
 
 def test_invalid_specs_rejected():
@@ -328,3 +412,42 @@ def test_planner_prometheus_scraper():
         srv.shutdown()
     assert got["dynamo_frontend_requests_total"] == 1.0 and len(got) == len(PLANNER_METRICS)
     assert 'namespace="dyn-ns"' in seen["q"] and "dynamo_frontend_requests_total" in seen["q"]
+
+
+def test_installer_reports_grove_kai_and_waits_for_gpu_operator_pods(tmp_path):
+    """install-dynamo-1node.sh against stub kubectl / helm: it reports ENABLE_GROVE /
+    ENABLE_KAI_SCHEDULER (warning that they are no-ops on one node, reference
+    install-dynamo-1node.sh:35-36,207-212) and polls the AMD GPU Operator pods until every one is
+    Running/Completed before the allocatable wait (reference :288-297)."""
+    import subprocess
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    state = tmp_path / "polls"
+    (bindir / "kubectl").write_text(f"""#!/usr/bin/env bash
+echo "kubectl $*" >> {tmp_path}/calls
+case "$*" in
+  *"get pods -n kube-amd-gpu --no-headers"*)
+    n=$(cat {state} 2>/dev/null || echo 0); echo $((n + 1)) > {state}
+    if [ "$n" -lt 2 ]; then echo "dp-abc 0/1 ContainerCreating 0 1s"; else echo "dp-abc 1/1 Running 0 9s"; echo "lab-x 0/1 Completed 0 9s"; fi ;;
+  *"get storageclass"*) echo true ;;
+  *"get nodes"*) echo 8 ;;
+  *"--dry-run=client"*) echo "apiVersion: v1" ;;
+esac
+exit 0
+""")
+    (bindir / "helm").write_text(f"#!/usr/bin/env bash\necho \"helm $*\" >> {tmp_path}/calls\nexit 0\n")
+    for f in ("kubectl", "helm"):
+        (bindir / f).chmod(0o755)
+    env = dict(os.environ, PATH=f"{bindir}:{os.environ['PATH']}", ENABLE_GROVE="true", ENABLE_KAI_SCHEDULER="false",
+               GPU_OPERATOR_POD_WAIT_INTERVAL="0", GPU_ALLOCATABLE_WAIT_INTERVAL="0")
+    r = subprocess.run(["bash", str(root / "install-dynamo-1node.sh")], capture_output=True, text=True, env=env,
+                       timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert "ENABLE_GROVE=true" in r.stdout and "ENABLE_KAI_SCHEDULER=false" in r.stdout
+    assert "WARNING: ENABLE_GROVE=true has no effect" in r.stderr and "ENABLE_KAI_SCHEDULER=true" not in r.stderr
+    assert int(state.read_text()) >= 3  # polled until the pods were Running / Completed
+    calls = (tmp_path / "calls").read_text()
+    assert calls.index("get pods -n kube-amd-gpu") < calls.index("get nodes")
+    assert "8 x amd.com/gpu allocatable" in r.stdout
