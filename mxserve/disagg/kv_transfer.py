@@ -345,7 +345,7 @@ class KVTransferAgent:
             ptr = self._opened.get(key)
             if ptr is None:
                 from .. import ops
-                ptr = int(ops.ext().ipc_open_pool(base64.b64decode(key), int(target["offset"])))
+                ptr = ops.ipc_open(base64.b64decode(key), int(target["offset"]))  # deadline: TimeoutError
                 self._opened[key] = ptr
             return ptr
 

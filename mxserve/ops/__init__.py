@@ -42,6 +42,42 @@ def has_ext() -> bool:
         return False
 
 
+# ----------------------------------------------------------------------------- IPC
+# hipIpcOpenMemHandle of a peer GPU's allocation can hang for some sizes (measured r1:
+# profiles/r1_ipc_open_probe.txt; disagg/kv_transfer.py module docstring).  Every open goes through
+# ipc_open(): a deadline, after which IPC is marked broken for this process (the stuck call still
+# holds the native table's lock) and callers fall back -- the KV transfer to the /dev/shm arena or
+# HTTP, the TP all-reduce to RCCL.
+IPC_STATE: dict = {"broken": None}
+
+
+def ipc_open(handle: bytes, offset: int = 0, timeout_s: Optional[float] = None) -> int:
+    """Map a peer's exported allocation (comm.cpp open_pool) within timeout_s seconds (default
+    MXS_IPC_OPEN_TIMEOUT_S, 30); raises TimeoutError (an OSError) past it and on every later call."""
+    import threading
+    if IPC_STATE["broken"]:
+        raise TimeoutError(f"IPC disabled in this process: {IPC_STATE['broken']}")
+    timeout_s = float(os.environ.get("MXS_IPC_OPEN_TIMEOUT_S", "30")) if timeout_s is None else timeout_s
+    box: dict = {}
+    done = threading.Event()
+    fn = ext().ipc_open_pool
+
+    def run():
+        try:
+            box["ptr"] = int(fn(handle, int(offset)))
+        except BaseException as e:  # noqa: BLE001 - re-raised in the caller
+            box["err"] = e
+        finally:
+            done.set()
+    threading.Thread(target=run, name="mxs-ipc-open", daemon=True).start()  # daemon: a hung open never blocks exit
+    if not done.wait(timeout_s):
+        IPC_STATE["broken"] = f"hipIpcOpenMemHandle did not return within {timeout_s:.0f}s"
+        raise TimeoutError(IPC_STATE["broken"])
+    if "err" in box:
+        raise box["err"]
+    return box["ptr"]
+
+
 _PREFILL_VERSION = int(os.environ.get("MXS_PREFILL_KERNEL", "3"))
 
 

@@ -29,6 +29,11 @@ SIGNAL_BYTES = 64 << 10
 _FLAGS_OFF, _EPOCHS_OFF, _ERR_OFF = 0, 4096, 8192
 
 
+def _ipc_stalled(err) -> bool:
+    """A timed-out open still holds the native IPC table's lock: touch nothing IPC after it."""
+    return isinstance(err, TimeoutError)
+
+
 class CustomAllReduce:
     def __init__(self, rank: int, world: int, max_bytes: int, recv_ptrs: list, flag_ptrs: list, own: tuple,
                  device: torch.device):
@@ -58,14 +63,30 @@ class CustomAllReduce:
         handles = [None] * world
         dist.all_gather_object(handles, (recv_h, sig_h), group=cpu_group or group)
         recv_ptrs, flag_ptrs = [], []
-        for r, (rh, sh) in enumerate(handles):
-            if r == rank:
-                recv_ptrs.append(recv_ptr)
-                flag_ptrs.append(sig_ptr)
-            else:
-                recv_ptrs.append(int(ext.ipc_open_pool(rh, 0)))
-                flag_ptrs.append(int(ext.ipc_open_pool(sh, 0)))
-        dist.barrier(group=cpu_group or group)
+        err = None
+        try:  # each open has a deadline (ops.ipc_open): a hung peer mapping fails this rank, not the job
+            for r, (rh, sh) in enumerate(handles):
+                if r == rank:
+                    recv_ptrs.append(recv_ptr)
+                    flag_ptrs.append(sig_ptr)
+                else:
+                    recv_ptrs.append(ops.ipc_open(rh, 0))
+                    flag_ptrs.append(ops.ipc_open(sh, 0))
+        except (RuntimeError, OSError) as e:
+            err = e
+        # every rank agrees: one rank that could not map its peers turns the custom path off for all
+        ok = torch.tensor([0 if err else 1], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=cpu_group or group)
+        if not int(ok.item()):
+            if not _ipc_stalled(err):
+                for r, (rh, sh) in enumerate(handles):
+                    if r != rank and r < len(recv_ptrs):
+                        ext.ipc_close(rh)
+                    if r != rank and r < len(flag_ptrs):
+                        ext.ipc_close(sh)
+                ext.car_free(recv_ptr)
+                ext.car_free(sig_ptr)
+            raise RuntimeError(f"custom all-reduce: peer mapping failed on some rank ({err!r} here)")
         log.info("custom all-reduce ready: rank %d/%d, %d MiB slots", rank, world, max_bytes >> 20)
         return cls(rank, world, max_bytes, recv_ptrs, flag_ptrs, (recv_ptr, sig_ptr), device)
 

@@ -511,3 +511,36 @@ def test_meta_ring_push_is_bounded():
     with _pt.raises(RuntimeError, match="stopped reading"):
         mr.send(("step", 1))
     assert r.calls == 3
+
+
+def test_ipc_open_deadline(monkeypatch):
+    """a hipIpcOpenMemHandle that never returns costs its caller the deadline, not a
+    hang: TimeoutError (an OSError, which the KV agent turns into the shm / HTTP path), and every
+    later open in the process fails fast (the stuck call still holds the native table's lock)."""
+    import threading
+    import time as _time
+
+    from mxserve import ops
+    release = threading.Event()
+
+    class _Ext:
+        calls = 0
+
+        def ipc_open_pool(self, handle, offset):
+            _Ext.calls += 1
+            if handle == b"hang":
+                release.wait(30)
+            return 4096 + offset
+
+    monkeypatch.setattr(ops, "ext", lambda: _Ext())
+    monkeypatch.setitem(ops.IPC_STATE, "broken", None)
+    assert ops.ipc_open(b"ok", 16, timeout_s=5) == 4112
+    t0 = _time.time()
+    import pytest as _pt
+    with _pt.raises(TimeoutError):
+        ops.ipc_open(b"hang", 0, timeout_s=0.3)
+    assert _time.time() - t0 < 2.0
+    with _pt.raises(OSError):  # fails fast from now on, without calling into the native table
+        ops.ipc_open(b"ok", 0, timeout_s=5)
+    assert _Ext.calls == 2
+    release.set()
