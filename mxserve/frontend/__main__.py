@@ -30,8 +30,7 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 def main(argv=None) -> None:
-    import uvicorn
-    from .app import Frontend
+    from .app import Frontend, serve_app
     a = build_parser().parse_args(argv)
     from ..utils.logs import setup_logging
     setup_logging()
@@ -51,7 +50,7 @@ def main(argv=None) -> None:
         kw.update(model=a.local_model, device=a.local_device)
         eng = LLMEngine(EngineArgs(**kw))
         fe.add_local_worker(AsyncEngine(eng), eng.args.name, eng.runner.num_blocks)
-    uvicorn.run(fe.app, host=a.http_host, port=a.http_port, log_level="warning", access_log=False)
+    serve_app(fe, host=a.http_host, port=a.http_port)
 
 
 if __name__ == "__main__":

@@ -180,6 +180,27 @@ class MuxClient:
             queues.clear()
 
 
+class _PushSink:
+    """Stands in for a request's queue in MuxClient.queues: the channel reader's put_nowait(line)
+    runs the request's PushStream right there (fastpath.py); the end or a failure resolves `fut`."""
+    __slots__ = ("ps", "fut")
+
+    def __init__(self, ps, fut: asyncio.Future):
+        self.ps, self.fut = ps, fut
+
+    def put_nowait(self, item) -> None:
+        if self.fut.done():
+            return
+        if isinstance(item, BaseException):
+            self.fut.set_exception(item)
+            return
+        try:
+            if self.ps.on_payload(item):
+                self.fut.set_result(True)
+        except BaseException as e:  # noqa: BLE001 - the request's coroutine handles it
+            self.fut.set_exception(e)
+
+
 class APIError(Exception):
     def __init__(self, status: int, message: str, etype: str = "invalid_request_error"):
         super().__init__(message)
@@ -422,30 +443,11 @@ class Frontend:
         budget, so the client sees one uninterrupted stream."""
         tried: set = set()
         generated: list = []
-        max_tokens = int(sampling.get("max_tokens", 16))
         for attempt in range(4):
-            decode = [w for w in self.registry.list(model) if w.role in ("agg", "decode") and w.worker_id not in tried]
-            prefill = [w for w in self.registry.list(model, "prefill")]
-            if not decode:
+            pick = self._choose(model, token_ids, sampling, generated, tried, attempt)
+            if pick is None:
                 break
-            ids = token_ids + generated
-            sp = sampling
-            if generated:
-                sp = dict(sampling, max_tokens=max_tokens - len(generated),
-                          min_tokens=max(0, int(sampling.get("min_tokens") or 0) - len(generated)))
-            w, overlap = self.router.pick(decode, ids)
-            tr = _TRACE.get()
-            if tr is not None and attempt == 0:
-                tr.mark("routed")
-                tr.attrs["worker"] = w.worker_id
-            purl = None
-            if w.role == "decode" and prefill:
-                # a prefill worker in the decode worker's own pair pod can reach its GPU arena
-                mates = [p for p in prefill if w.pair and p.pair == w.pair]
-                pw, _ = self.router.pick(mates or prefill, ids)
-                purl = pw.url
-            if overlap:
-                self.metrics.kv_hit.labels(model).inc(overlap)
+            w, ids, sp, purl = pick
             w.inflight += 1
             try:
                 async for evs in self._worker_stream(w, ids, sp, rid, purl):
@@ -455,21 +457,124 @@ class Frontend:
                         return
                 raise ConnectionError(f"worker {w.worker_id} ended the stream early")
             except _STREAM_ERRORS as e:
-                if generated and not self.migrate:
-                    raise
-                log.warning("worker %s failed after %d tokens (%r); %s", w.worker_id, len(generated), e,
-                            "migrating" if generated else "retrying")
-                if generated:
-                    self.metrics.migrations.labels(model).inc()
-                tried.add(w.worker_id)
-                try:
-                    import aiohttp
-                    if isinstance(e, aiohttp.ClientConnectionError) and not generated:
-                        self.registry.deregister(w.worker_id)
-                except ImportError:
-                    pass
+                self._attempt_failed(model, w, e, generated, tried)
             finally:
                 w.inflight -= 1
+        self._no_worker_left(model, generated, tried)
+
+    # ---------------------------------------------------------------- push path (fastpath.py)
+    async def run_push(self, model: str, token_ids: list, sampling: dict, rid: str, ps) -> None:
+        """Route + stream one request into a fastpath.PushStream: the retry / migration policy of
+        generate_tokens, with the tokens pushed to `ps.on_events` by the channel reader."""
+        tried: set = set()
+        generated = ps.generated
+        for attempt in range(4):
+            pick = self._choose(model, token_ids, sampling, generated, tried, attempt)
+            if pick is None:
+                break
+            w, ids, sp, purl = pick
+            w.inflight += 1
+            try:
+                await self._push_attempt(w, ids, sp, rid, purl, ps)
+                return
+            except _STREAM_ERRORS as e:
+                from .fastpath import ClientGone
+                if isinstance(e, ClientGone):  # nobody to stream to: no retry
+                    raise
+                self._attempt_failed(model, w, e, generated, tried)
+            finally:
+                w.inflight -= 1
+        self._no_worker_left(model, generated, tried)
+
+    async def _push_attempt(self, w: WorkerInfo, ids: list, sp: dict, rid: str, purl: Optional[str], ps) -> None:
+        sess = await self.http()
+        body = {"request_id": rid, "token_ids": ids, "sampling": sp}
+        if purl:
+            body["prefill_url"] = purl
+        murl = w.stream_url or w.url
+        mc = self._mux.get(murl) if REQUEST_PLANE == "mux" and not w.url.startswith("local://") else None
+        if mc is None and REQUEST_PLANE == "mux" and not w.url.startswith("local://"):
+            mc = self._mux[murl] = MuxClient(murl)
+        if mc is not None and not mc.unsupported:
+            try:
+                await mc.ensure(sess)
+            except _STREAM_ERRORS:
+                if not mc.unsupported:
+                    raise
+        if mc is None or mc.unsupported:  # a worker without the mux plane: pull its stream here
+            async for evs in self._worker_stream(w, ids, sp, rid, purl):
+                if ps.on_events(evs):
+                    return
+            raise ConnectionError(f"worker {w.worker_id} ended the stream early")
+        fut = asyncio.get_running_loop().create_future()
+        sink = _PushSink(ps, fut)
+        mc.queues[rid] = sink
+        try:
+            for attempt in range(2):
+                async with sess.post(mc.url + "/submit", json=dict(body, sid=mc.sid)) as r:
+                    status = r.status
+                if status == 404 and attempt == 0:  # the worker restarted and lost this channel: reopen
+                    mc.queues.pop(rid, None)
+                    mc.reset()
+                    await mc.ensure(sess)
+                    mc.queues[rid] = sink
+                    continue
+                if status != 200:
+                    raise ConnectionError(f"submit to {mc.url} returned {status}")
+                break
+            await fut
+        finally:
+            mc.queues.pop(rid, None)
+            if not ps.worker_done:  # stop string, client gone or failure: free the worker's slot
+                t = asyncio.ensure_future(self._post_abort(sess, mc.url, rid))
+                self._bg.add(t)
+                t.add_done_callback(self._bg.discard)
+
+    def _choose(self, model: str, token_ids: list, sampling: dict, generated: list, tried: set, attempt: int):
+        """(decode / agg worker, token ids, sampling, prefill URL) of the next attempt, or None: the
+        router's pick among the workers not tried yet; after a failure mid-stream the ids are prompt +
+        generated and the budget what is left (migration).  A decode worker gets a prefill worker of
+        its own P/D group pod first (that one can reach its GPU arena)."""
+        decode = [w for w in self.registry.list(model) if w.role in ("agg", "decode") and w.worker_id not in tried]
+        prefill = [w for w in self.registry.list(model, "prefill")]
+        if not decode:
+            return None
+        ids = token_ids + generated
+        sp = sampling
+        if generated:
+            sp = dict(sampling, max_tokens=int(sampling.get("max_tokens", 16)) - len(generated),
+                      min_tokens=max(0, int(sampling.get("min_tokens") or 0) - len(generated)))
+        w, overlap = self.router.pick(decode, ids)
+        tr = _TRACE.get()
+        if tr is not None and attempt == 0:
+            tr.mark("routed")
+            tr.attrs["worker"] = w.worker_id
+        purl = None
+        if w.role == "decode" and prefill:
+            mates = [p for p in prefill if w.pair and p.pair == w.pair]
+            pw, _ = self.router.pick(mates or prefill, ids)
+            purl = pw.url
+        if overlap:
+            self.metrics.kv_hit.labels(model).inc(overlap)
+        return w, ids, sp, purl
+
+    def _attempt_failed(self, model: str, w: WorkerInfo, e: BaseException, generated: list, tried: set) -> None:
+        if generated and not self.migrate:
+            raise e
+        log.warning("worker %s failed after %d tokens (%r); %s", w.worker_id, len(generated), e,
+                    "migrating" if generated else "retrying")
+        if generated:
+            self.metrics.migrations.labels(model).inc()
+        tried.add(w.worker_id)
+        try:
+            import aiohttp
+            if isinstance(e, aiohttp.ClientConnectionError) and not generated:
+                self.registry.deregister(w.worker_id)
+        except ImportError:
+            pass
+
+    @staticmethod
+    def _no_worker_left(model: str, generated: list, tried: set) -> None:
         if generated:
             raise ConnectionError("request could not be migrated: no other worker")
         raise APIError(503, f"no workers available for model {model}" if not tried else "all workers failed",
@@ -884,3 +989,17 @@ class Frontend:
         if self._http is not None:
             await self._http.close()
             self._http = None
+
+
+def serve_app(fe: Frontend, host: str = "0.0.0.0", port: int = 8000, sock=None) -> None:
+    """Serve a Frontend until SIGTERM / SIGINT: our HTTP/1.1 server with the push-streaming fast
+    path (httpd.py + fastpath.py; the default), or uvicorn (MXS_FRONTEND_SERVER=uvicorn)."""
+    if os.environ.get("MXS_FRONTEND_SERVER", "httpd") == "uvicorn":
+        import uvicorn
+        if sock is not None:
+            uvicorn.Server(uvicorn.Config(fe.app, log_level="warning", access_log=False)).run(sockets=[sock])
+        else:
+            uvicorn.run(fe.app, host=host, port=port, log_level="warning", access_log=False)
+        return
+    from . import fastpath, httpd
+    httpd.run(fe.app, host, port, fast=lambda req, conn: fastpath.handle(fe, req, conn), sock=sock)

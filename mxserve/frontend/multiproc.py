@@ -59,16 +59,13 @@ def _listen(host: str, port: int) -> socket.socket:
 
 
 def _child(index: int, args: dict, outbound, inbound) -> None:
-    import uvicorn
     from ..utils.logs import setup_logging
-    from .app import Frontend
+    from .app import Frontend, serve_app
     setup_logging()
     fe = Frontend(router_mode=args["router_mode"], ttl=args["ttl"], namespace=args["namespace"],
                   reasoning_parser=args["reasoning_parser"])
     fe.bus = PeerBus(index, outbound, inbound)
-    sock = _listen(args["host"], args["port"])
-    server = uvicorn.Server(uvicorn.Config(fe.app, log_level="warning", access_log=False))
-    server.run(sockets=[sock])
+    serve_app(fe, sock=_listen(args["host"], args["port"]))
 
 
 def serve(args: dict, nprocs: int) -> int:

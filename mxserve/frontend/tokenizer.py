@@ -125,7 +125,11 @@ class IncrementalDetokenizer:
     (from `prefix` to the end), not the whole output -- a full re-decode per token is O(n^2) over a
     500-token answer, ~10^5 tokens decoded per request at OSL 500.  The window starts a few tokens
     back so byte-fallback / leading-space merges resolve as in a full decode; an incomplete UTF-8
-    sequence (U+FFFD at the tail) is held back until its next byte arrives."""
+    sequence (U+FFFD at the tail) is held back until its next byte arrives.  The window start stays
+    put for up to WINDOW tokens, so the text of [prefix, read) is the previous step's decode: one
+    tokenizer call per token instead of two."""
+
+    WINDOW = 8
 
     def __init__(self, tokenizer, prompt_tail: Optional[list] = None, skip_special_tokens: bool = True):
         self.tok = tokenizer
@@ -133,7 +137,7 @@ class IncrementalDetokenizer:
         self.ids: list[int] = list(prompt_tail or [])[-5:]
         self.prefix = 0  # window start
         self.read = len(self.ids)  # end of the text already emitted
-        self.emitted = ""
+        self._ptext: Optional[str] = None  # decode of ids[prefix:read], when known
 
     def _decode(self, a: int, b: Optional[int] = None) -> str:
         return self.tok.decode(self.ids[a:b], skip_special_tokens=self.skip)
@@ -151,19 +155,23 @@ class IncrementalDetokenizer:
         return self._advance()
 
     def _advance(self) -> str:
-        prefix_text = self._decode(self.prefix, self.read)
+        prefix_text = self._ptext if self._ptext is not None else self._decode(self.prefix, self.read)
         new_text = self._decode(self.prefix)
         if len(new_text) <= len(prefix_text) or new_text.endswith("\ufffd"):
+            self._ptext = prefix_text
             return ""
         delta = new_text[len(prefix_text):]
-        self.prefix, self.read = self.read, len(self.ids)
-        self.emitted += delta
+        if len(self.ids) - self.prefix > self.WINDOW:  # slide: the text of the new window is not known
+            self.prefix, self._ptext = self.read, None
+        else:
+            self._ptext = new_text
+        self.read = len(self.ids)
         return delta
 
     def flush(self) -> str:
-        prefix_text = self._decode(self.prefix, self.read)
+        prefix_text = self._ptext if self._ptext is not None else self._decode(self.prefix, self.read)
         new_text = self._decode(self.prefix)
         delta = new_text[len(prefix_text):] if len(new_text) > len(prefix_text) else ""
         self.prefix = self.read = len(self.ids)
-        self.emitted += delta
+        self._ptext = None
         return delta

@@ -399,7 +399,9 @@ def test_mid_stream_migration_keeps_greedy_output():
 
 def test_remote_prefill_cancel_releases_reservation():
     """A client that goes away while the decode worker awaits the prefill POST (CancelledError)
-    must not leak the reserved KV blocks, the remote slot or the token queue."""
+    must not leak the reserved KV blocks, the remote slot or the token queue -- and must not free
+    the blocks while the prefill worker may still push into them: they are held until its reply,
+    or (the POST failing without one, as here) the quarantine delay."""
     import asyncio
     import socket
     import threading
@@ -411,6 +413,7 @@ def test_remote_prefill_cancel_releases_reservation():
     held = []
     threading.Thread(target=lambda: held.append(lst.accept()), daemon=True).start()  # accepts, never answers
     w, _ = _worker(None, role="decode")
+    w.QUARANTINE_S = 0.5
     eng = w.engine
     free0 = eng.kv.num_free()
 
@@ -426,8 +429,14 @@ def test_remote_prefill_cancel_releases_reservation():
         t.cancel()
         with pytest.raises(asyncio.CancelledError):
             await t
+        await asyncio.sleep(0.1)
+        assert "rq" not in eng.scheduler.remote and eng.kv.num_free() < free0  # detached, still held
         if w._http is not None:
-            await w._http.close()
+            await w._http.close()  # the POST fails without a reply: quarantine, then free
+        for _ in range(100):
+            if w.kv_quarantined == 0:
+                break
+            await asyncio.sleep(0.05)
 
     try:
         asyncio.run(go())

@@ -253,6 +253,19 @@ def test_byte_tokenizer_and_templates():
     tok.decode = orig
     assert out == long
     assert max(calls) <= 16, max(calls)
+    n_tok = len(tok.encode(long))
+    assert len(calls) <= 1.3 * n_tok, (len(calls), n_tok)  # ~one decode per token, not two
+    import random
+    rng = random.Random(5)
+    ids = tok.encode(long)
+    for _ in range(5):  # tokens arriving in random batches: still the full decode's text
+        d = IncrementalDetokenizer(tok)
+        parts, i = [], 0
+        while i < len(ids):
+            k = rng.randint(1, 6)
+            parts.append(d.add_many(ids[i:i + k]) if k > 1 else d.add(ids[i]))
+            i += k
+        assert "".join(parts) + d.flush() == long
     q = render("chatml", [{"role": "user", "content": "hi"}])
     assert q == "<|im_start|>user\nhi<|im_end|>\n<|im_start|>assistant\n"
     assert render("mistral", [{"role": "user", "content": "x"}]) == "<s>[INST] x [/INST]"
