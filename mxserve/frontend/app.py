@@ -1002,4 +1002,14 @@ def serve_app(fe: Frontend, host: str = "0.0.0.0", port: int = 8000, sock=None) 
             uvicorn.run(fe.app, host=host, port=port, log_level="warning", access_log=False)
         return
     from . import fastpath, httpd
-    httpd.run(fe.app, host, port, fast=lambda req, conn: fastpath.handle(fe, req, conn), sock=sock)
+
+    def fast(req, conn):
+        return fastpath.handle(fe, req, conn)
+    prof = os.environ.get("MXS_FRONTEND_PROFILE")  # dev: cProfile of this process -> <path>.<pid>
+    if prof:
+        import cProfile
+        cProfile.runctx("run(app, host, port, fast=fast, sock=sock)", {},
+                        {"run": httpd.run, "app": fe.app, "host": host, "port": port, "fast": fast, "sock": sock},
+                        f"{prof}.{os.getpid()}")
+        return
+    httpd.run(fe.app, host, port, fast=fast, sock=sock)

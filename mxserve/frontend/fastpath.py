@@ -30,12 +30,37 @@ class ClientGone(ConnectionError):
     pass
 
 
-def _observe(child, v: float) -> None:
-    """Histogram.observe without its per-call checks and linear bucket scan (one bisect)."""
-    ub = child._upper_bounds
-    i = bisect.bisect_left(ub, v)
-    child._sum.inc(v)
-    child._buckets[min(i, len(ub) - 1)].inc(1)
+class _LocalHistogram:
+    """One request's share of a prometheus Histogram child, counted locally (a list index per
+    observation) and added to the shared child every FLUSH observations and at the end: the
+    multiprocess-mode child takes a lock and an mmap write per inc()."""
+    FLUSH = 64
+
+    def __init__(self, child):
+        self.child = child
+        self.ub = child._upper_bounds
+        self.counts = [0] * len(self.ub)
+        self.sum = 0.0
+        self.n = 0
+
+    def observe(self, v: float) -> None:
+        i = bisect.bisect_left(self.ub, v)
+        self.counts[i if i < len(self.ub) else -1] += 1
+        self.sum += v
+        self.n += 1
+        if self.n >= self.FLUSH:
+            self.flush()
+
+    def flush(self) -> None:
+        if not self.n:
+            return
+        b = self.child._buckets
+        for i, c in enumerate(self.counts):
+            if c:
+                b[i].inc(c)
+                self.counts[i] = 0
+        self.child._sum.inc(self.sum)
+        self.sum, self.n = 0.0, 0
 
 
 class PushStream:
@@ -69,6 +94,7 @@ class PushStream:
         self.pre, self.post = t.split('"\\u0000"')
         m = fe.metrics
         self.m_itl = m.itl.labels(model)
+        self.itl = _LocalHistogram(self.m_itl)
         self.first = None
         self.last = None
         self.n = 0
@@ -148,10 +174,10 @@ class PushStream:
                     tm["delivery_ms"] = round((time.time() - emit) * 1e3, 3)
                 self.trace.attrs["worker_ms"] = tm
         elif self.last is not None:
-            _observe(self.m_itl, now - self.last)
-        if k > 1:
-            from .app import _observe_zeros
-            _observe_zeros(self.m_itl, k - 1)
+            self.itl.observe(now - self.last)
+        if k > 1:  # the rest of a batch arrived with its first token: k - 1 zero intervals
+            self.itl.counts[0] += k - 1
+            self.itl.n += k - 1
         self.last = now
         self.n += k
         self.generated.extend(toks)
@@ -201,6 +227,7 @@ class PushStream:
         self.conn.write_chunk(("data: " + json.dumps({"error": err}) + "\n\n").encode())
 
     def record(self, status: str, endpoint: str) -> None:
+        self.itl.flush()
         m = self.fe.metrics
         m.requests.labels(self.model, endpoint, "stream", status).inc()
         m.inflight.labels(self.model).dec()

@@ -214,7 +214,7 @@ class Server:
     """`fast(req, conn) -> bool` takes a request over (True) or leaves it to the ASGI `app`."""
 
     def __init__(self, app, fast: Optional[Callable[[Request, Connection], Awaitable[bool]]] = None):
-        self.app = app
+        self.app = app  # None: the fast hook serves every request (no ASGI app, no lifespan)
         self.fast = fast
         self.conns: set = set()
         self._lifespan_q: Optional[asyncio.Queue] = None
@@ -283,6 +283,8 @@ class Server:
 
     # ------------------------------------------------------------------ lifespan
     async def startup(self) -> None:
+        if self.app is None:
+            return
         self._lifespan_q = asyncio.Queue()
         started = asyncio.get_running_loop().create_future()
         stopped = asyncio.get_running_loop().create_future()

@@ -87,6 +87,11 @@ class ByteTokenizer:
         piece = self._piece
         return b"".join([piece(t, skip_special_tokens) for t in ids]).decode("utf-8", errors="replace")
 
+    def piece_bytes(self, t: int, skip_special_tokens: bool = True) -> bytes:
+        """The bytes of one id, independent of its neighbours (what makes an O(1) incremental
+        decode exact for this tokenizer: IncrementalDetokenizer's byte mode)."""
+        return self._piece(t, skip_special_tokens)
+
     def convert_special(self, name: str) -> Optional[int]:
         return self.special_to_id.get(name)
 
@@ -138,11 +143,19 @@ class IncrementalDetokenizer:
         self.prefix = 0  # window start
         self.read = len(self.ids)  # end of the text already emitted
         self._ptext: Optional[str] = None  # decode of ids[prefix:read], when known
+        # tokenizers whose ids map to context-free byte strings: an incremental UTF-8 decoder is
+        # the exact full decode, at one dict lookup per token (no window)
+        self._piece = getattr(tokenizer, "piece_bytes", None)
+        if self._piece is not None:
+            import codecs
+            self._utf8 = codecs.getincrementaldecoder("utf-8")("replace")
 
     def _decode(self, a: int, b: Optional[int] = None) -> str:
         return self.tok.decode(self.ids[a:b], skip_special_tokens=self.skip)
 
     def add(self, token_id: int) -> str:
+        if self._piece is not None:
+            return self._utf8.decode(self._piece(int(token_id), self.skip))
         self.ids.append(int(token_id))
         return self._advance()
 
@@ -151,6 +164,8 @@ class IncrementalDetokenizer:
         (the same text as adding them one by one)."""
         if not token_ids:
             return ""
+        if self._piece is not None:
+            return self._utf8.decode(b"".join(self._piece(int(t), self.skip) for t in token_ids))
         self.ids.extend(int(t) for t in token_ids)
         return self._advance()
 
@@ -169,6 +184,8 @@ class IncrementalDetokenizer:
         return delta
 
     def flush(self) -> str:
+        if self._piece is not None:
+            return self._utf8.decode(b"", final=True)
         prefix_text = self._ptext if self._ptext is not None else self._decode(self.prefix, self.read)
         new_text = self._decode(self.prefix)
         delta = new_text[len(prefix_text):] if len(new_text) > len(prefix_text) else ""

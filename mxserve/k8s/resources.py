@@ -178,6 +178,23 @@ def _default_command(g: GraphSpec, s: ServiceSpec) -> list:
     return ["python3", "-m", "mxserve.worker"]
 
 
+# Streamed tokens per second one MI355X worker produces at the headline point (BENCH: ~20-24 k) and
+# one frontend process forwards with headroom (scripts/frontend_load.py: 125 k tok/s over 4
+# processes at a 17 ms TTFT p50, ~22-26 us of CPU per token: ~38 k/s at 100 % of a core).
+TOKENS_PER_GPU = 24000
+TOKENS_PER_FRONTEND_PROC = 27000
+
+
+def frontend_procs(g: GraphSpec) -> int:
+    """Frontend processes for a graph: enough cores for the tokens its worker GPUs stream (prefill-
+    only workers stream nothing), 2..16; MXS_FRONTEND_PROCS (operator env) overrides."""
+    if os.environ.get("MXS_FRONTEND_PROCS"):
+        return int(os.environ["MXS_FRONTEND_PROCS"])
+    gpus = sum(max(1, s.gpus) * max(0, s.replicas) for s in g.services
+               if s.component_type == "worker" and s.sub_component_type != "prefill")
+    return max(2, min(16, -(-gpus * TOKENS_PER_GPU // TOKENS_PER_FRONTEND_PROC)))
+
+
 def _container(g: GraphSpec, s: ServiceSpec) -> dict:
     is_fe = s.component_type == "frontend"
     port = FRONTEND_PORT if is_fe else WORKER_PORT
@@ -187,9 +204,9 @@ def _container(g: GraphSpec, s: ServiceSpec) -> dict:
            {"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}]
     if PROMETHEUS_ENDPOINT:
         env.append({"name": "PROMETHEUS_ENDPOINT", "value": PROMETHEUS_ENDPOINT})
-    if is_fe:  # 4 frontend processes on the port: one Python process streams ~20 k tokens/s at most
+    if is_fe:  # frontend processes on the port, sized for the graph's GPUs (frontend_procs)
         env += [{"name": "DYN_HTTP_PORT", "value": str(FRONTEND_PORT)},
-                {"name": "MXS_FRONTEND_PROCS", "value": os.environ.get("MXS_FRONTEND_PROCS", "4")}]
+                {"name": "MXS_FRONTEND_PROCS", "value": str(frontend_procs(g))}]
     else:
         env += [{"name": "MXS_FRONTEND_URL", "value": frontend_url(g)},
                 {"name": "DYN_SYSTEM_PORT", "value": str(WORKER_PORT)}]
@@ -208,6 +225,8 @@ def _container(g: GraphSpec, s: ServiceSpec) -> dict:
         c["envFrom"] = [{"secretRef": {"name": s.env_from_secret, "optional": True}}]
     if s.gpus:
         c["resources"] = {"limits": {GPU_RESOURCE: str(s.gpus)}, "requests": {GPU_RESOURCE: str(s.gpus)}}
+    elif is_fe:  # one core per frontend process (the streaming work is per-process CPU)
+        c["resources"] = {"requests": {"cpu": str(frontend_procs(g)), "memory": "2Gi"}}
     if s.volume_mounts:
         c["volumeMounts"] = [{"name": vm["name"], "mountPath": vm["mountPoint"]} for vm in s.volume_mounts]
     if s.gpus:  # shared memory for the TP ranks' host-side metadata and RCCL

@@ -64,3 +64,46 @@ def wait_for(cond, timeout: float = 20.0, interval: float = 0.1) -> None:
 
 def get_json(url: str):
     return httpx.get(url, timeout=30).json()
+
+
+class FrontendServer:
+    """A Frontend served the way `python -m mxserve.frontend` serves it: mxserve/frontend/httpd.py
+    with the push-streaming fast path (fastpath.py), on its own event loop in a thread."""
+
+    def __init__(self, fe, port: int | None = None):
+        self.fe = fe
+        self.port = port or free_port()
+        self.url = f"http://127.0.0.1:{self.port}"
+        self.loop = None
+        self.stop_ev = None
+        self.thread = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self) -> None:
+        import asyncio
+
+        from mxserve.frontend import fastpath, httpd
+        self.loop = asyncio.new_event_loop()
+        asyncio.set_event_loop(self.loop)
+
+        async def main():
+            self.stop_ev = asyncio.Event()
+            srv = httpd.Server(self.fe.app, lambda req, conn: fastpath.handle(self.fe, req, conn))
+            await srv.serve(httpd.listen("127.0.0.1", self.port), stop=self.stop_ev)
+        self.loop.run_until_complete(main())
+
+    def start(self, timeout: float = 20.0) -> "FrontendServer":
+        self.thread.start()
+        t0 = time.time()
+        while True:
+            try:
+                with socket.create_connection(("127.0.0.1", self.port), timeout=0.5):
+                    return self
+            except OSError:
+                if time.time() - t0 > timeout:
+                    raise TimeoutError("frontend did not start")
+                time.sleep(0.05)
+
+    def stop(self) -> None:
+        if self.loop is not None and self.stop_ev is not None:
+            self.loop.call_soon_threadsafe(self.stop_ev.set)
+        self.thread.join(timeout=10)

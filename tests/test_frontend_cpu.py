@@ -10,7 +10,7 @@ from mxserve.config import EngineArgs
 from mxserve.frontend.app import Frontend
 from mxserve.worker.args import WorkerArgs
 from mxserve.worker.server import Worker
-from tests.serving_utils import Server, wait_for
+from tests.serving_utils import FrontendServer, Server, wait_for
 
 MODEL = "tiny-llama"
 
@@ -28,7 +28,7 @@ def _worker(frontend_url, role="agg", seed=7):
 @pytest.fixture(scope="module")
 def agg_stack():
     fe = Frontend(router_mode="kv", ttl=30)
-    fs = Server(fe.app).start()
+    fs = FrontendServer(fe).start()  # httpd + push fast path, as `python -m mxserve.frontend` serves
     w, ws = _worker(fs.url)
     ws.start()
     wait_for(lambda: len(fe.registry.list()) == 1)
@@ -669,3 +669,93 @@ def test_mux_channel_reconnects_after_worker_restart():
             w2.aeng.shutdown()
     finally:
         fs.stop()
+
+
+def _sse_events(url: str, path: str, body: dict) -> list:
+    out = []
+    with httpx.stream("POST", url + path, json=body, timeout=60) as r:
+        assert r.status_code == 200 and r.headers["content-type"].startswith("text/event-stream")
+        for line in r.iter_lines():
+            if line.startswith("data: "):
+                out.append(line[6:])
+    return out
+
+
+def _normalize(events: list) -> dict:
+    """What a stream says, independent of how tokens were grouped into chunks (a consumer that falls
+    behind legitimately merges deltas): the text, the finish reasons, the usage, the chunk schema
+    and the terminator."""
+    text, reasons, usage, shapes, roles = "", [], None, set(), 0
+    for p in events:
+        if p == "[DONE]":
+            continue
+        d = json.loads(p)
+        shapes.add((d["object"], d["model"], tuple(sorted(d))))
+        if not d["choices"]:
+            usage = d.get("usage")
+            continue
+        ch = d["choices"][0]
+        shapes.add(tuple(sorted(ch)))
+        delta = ch.get("delta")
+        if delta is not None:
+            roles += "role" in delta
+            text += delta.get("content") or ""
+        else:
+            text += ch.get("text") or ""
+        if ch.get("finish_reason"):
+            reasons.append(ch["finish_reason"])
+    return {"text": text, "reasons": reasons, "usage": usage, "shapes": shapes, "roles": roles,
+            "done": events[-1] == "[DONE]"}
+
+
+@pytest.mark.parametrize("path,extra", [
+    ("/v1/chat/completions", {"stream_options": {"include_usage": True}}),
+    ("/v1/chat/completions", {"stop": ["\n", "e"]}),
+    ("/v1/completions", {"stop": "a"}),
+    ("/v1/completions", {}),
+])
+def test_push_fast_path_matches_fastapi_path(agg_stack, monkeypatch, path, extra):
+    """The httpd push path (frontend/fastpath.py) streams exactly what the FastAPI route streams:
+    same chunks (content deltas, finish reasons, usage), same [DONE].  The FastAPI side is served
+    by uvicorn from the same Frontend; the fast side must really be the push path."""
+    from mxserve.frontend import fastpath
+    fe, fs, w = agg_stack
+    body = {"model": MODEL, "max_tokens": 12, "temperature": 0, "ignore_eos": True, "stream": True, **extra}
+    if path.endswith("chat/completions"):
+        body["messages"] = [{"role": "user", "content": "push path parity"}]
+    else:
+        body["prompt"] = "push path parity"
+    used = []
+    orig = fastpath.PushStream.head
+    monkeypatch.setattr(fastpath.PushStream, "head", lambda self: (used.append(1), orig(self))[1])
+    fast = _normalize(_sse_events(fs.url, path, body))
+    assert used, "the push fast path did not serve the request"
+    fe2 = Frontend(router_mode="kv", ttl=30)  # its own loop-bound sessions: a second Frontend
+    slow_srv = Server(fe2.app).start()  # uvicorn: the FastAPI route only
+    try:
+        assert httpx.post(slow_srv.url + "/internal/register", json=w.registration(), timeout=10).status_code == 200
+        slow = _normalize(_sse_events(slow_srv.url, path, body))
+    finally:
+        slow_srv.stop()
+    assert fast == slow
+    assert fast["done"] and len(fast["reasons"]) == 1
+
+
+def test_httpd_keep_alive_errors_and_bridge(agg_stack):
+    """One connection, several requests: JSON routes through the ASGI bridge, an error in the app's
+    shape from the fast path, a streamed response, and the connection stays usable throughout."""
+    _, fs, _ = agg_stack
+    with httpx.Client(base_url=fs.url, timeout=60) as c:
+        assert c.get("/v1/models").json()["object"] == "list"
+        r = c.post("/v1/chat/completions", json={"model": "nope", "messages": [], "stream": True})
+        assert r.status_code == 404 and "error" in r.json() and r.json()["error"]["message"]
+        r = c.post("/v1/chat/completions", json={"model": MODEL, "stream": True})
+        assert r.status_code == 400 and "messages" in r.json()["error"]["message"]
+        r = c.post("/v1/chat/completions", content=b"{not json", headers={"content-type": "application/json"})
+        assert r.status_code == 400
+        with c.stream("POST", "/v1/completions", json={"model": MODEL, "prompt": "x", "max_tokens": 3,
+                                                       "stream": True, "temperature": 0}) as s:
+            lines = [ln for ln in s.iter_lines() if ln.startswith("data: ")]
+        assert lines[-1] == "data: [DONE]" and len(lines) >= 2
+        assert c.get("/health").status_code == 200
+        assert "dynamo_frontend_requests_total" in c.get("/metrics").text

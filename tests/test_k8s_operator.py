@@ -451,3 +451,31 @@ exit 0
     calls = (tmp_path / "calls").read_text()
     assert calls.index("get pods -n kube-amd-gpu") < calls.index("get nodes")
     assert "8 x amd.com/gpu allocatable" in r.stdout
+
+
+def test_frontend_sized_for_the_graph(monkeypatch):
+    """the frontend's process count (and CPU request) follows the tokens its graph's
+    decode / agg GPUs stream: 8 single-GPU agg replicas -> 8 processes, 1 GPU -> the floor of 2."""
+    from mxserve.k8s import resources
+    monkeypatch.delenv("MXS_FRONTEND_PROCS", raising=False)
+
+    def graph(replicas, gpus="1"):
+        return resources.parse_dgd({"apiVersion": resources.API_VERSION, "kind": resources.DGD_KIND,
+                                    "metadata": {"name": "g"}, "spec": {"services": {
+                                        "Frontend": {"componentType": "frontend"},
+                                        "W": {"componentType": "worker", "replicas": replicas,
+                                              "resources": {"limits": {"gpu": gpus}}}}}}, "ns")
+
+    def procs(g):
+        d = next(o for o in resources.render_children(g) if o["kind"] == "Deployment" and o["metadata"]["name"] == "g-frontend")
+        c = d["spec"]["template"]["spec"]["containers"][0]
+        env = {e["name"]: e.get("value") for e in c["env"]}
+        assert c["resources"]["requests"]["cpu"] == env["MXS_FRONTEND_PROCS"]
+        return int(env["MXS_FRONTEND_PROCS"])
+    assert procs(graph(8)) == 8
+    assert procs(graph(1)) == 2
+    assert procs(graph(1, "8")) == 8  # one TP-8 worker streams as much as 8 GPUs
+    g = _pd_graph(3, 5)  # prefill workers stream nothing: 5 decode GPUs
+    assert resources.frontend_procs(g) == 5
+    monkeypatch.setenv("MXS_FRONTEND_PROCS", "3")
+    assert procs(graph(8)) == 3

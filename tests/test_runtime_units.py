@@ -246,11 +246,13 @@ def test_byte_tokenizer_and_templates():
     # windowed decode: same text as one full decode, and the work per token does not grow with n
     long = "streaming détokenizer, ünïcödé 🙂 " * 40
     calls = []
-    orig = tok.decode
-    tok.decode = lambda ids, **kw: (calls.append(len(ids)), orig(ids, **kw))[1]
-    d = IncrementalDetokenizer(tok, prompt_tail=tok.encode("prompt "))
+
+    class _Windowed:  # a tokenizer without context-free pieces: the windowed decode path
+        def decode(self, ids, **kw):
+            calls.append(len(ids))
+            return tok.decode(ids, **kw)
+    d = IncrementalDetokenizer(_Windowed(), prompt_tail=tok.encode("prompt "))
     out = "".join(d.add(t) for t in tok.encode(long)) + d.flush()
-    tok.decode = orig
     assert out == long
     assert max(calls) <= 16, max(calls)
     n_tok = len(tok.encode(long))
@@ -258,8 +260,8 @@ def test_byte_tokenizer_and_templates():
     import random
     rng = random.Random(5)
     ids = tok.encode(long)
-    for _ in range(5):  # tokens arriving in random batches: still the full decode's text
-        d = IncrementalDetokenizer(tok)
+    for mode in [tok, _Windowed()] * 3:  # random batches, byte mode and window mode: the full decode's text
+        d = IncrementalDetokenizer(mode)
         parts, i = [], 0
         while i < len(ids):
             k = rng.randint(1, 6)
