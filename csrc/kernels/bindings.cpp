@@ -36,6 +36,7 @@ bool launch_mt_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int
                     int, hipStream_t, int*, int);
 bool launch_prefill_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int,
                          hipStream_t);
+bool launch_gemm_big(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, hipStream_t);
 bool launch_moe_grouped_gemm(bf16_t*, const bf16_t*, const bf16_t*, const int*, int, int, int, int, int, bool,
                              int, float*, hipStream_t);
 void launch_moe_combine_partials(bf16_t*, const float*, const float*, const int*, int, int, int, int, long,
@@ -287,6 +288,17 @@ bool prefill_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::
                                   stream());
 }
 
+// K05-K08 at full prefill chunks (csrc/kernels/gemm_big.hip): epi 0 out [M, N] = x w^T; epi 1 (SwiGLU)
+// w = [gate; up] [2 I, K], out [M, I] = SiLU(x gate^T) * (x up^T).  False if the shape is unsupported.
+bool gemm_big(at::Tensor out, at::Tensor x, at::Tensor w, int64_t epi, int64_t variant) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == (epi == 1 ? N / 2 : N), "shape mismatch");
+  if (x.stride(1) != 1 || out.stride(1) != 1 || M > (1 << 30)) return false;
+  return mxs::launch_gemm_big(bf(out), bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), epi, variant, stream());
+}
+
 // Grouped decode form of decode_gemm (K16 at decode batches): w [E, N, K], x = routed rows sorted by
 // expert (offs = moe_align offsets), rows_max = the most rows one expert can hold (tokens).  Output
 // as moe_grouped_gemm: out [rows, N or N/2] (splitk 1) or fp32 partials [splitk, rows, N].
@@ -401,6 +413,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("epi"), pybind11::arg("cnt") = pybind11::none());
   m.def("prefill_gemm", &prefill_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("part"), pybind11::arg("bm"), pybind11::arg("splitk"));
+  m.def("gemm_big", &gemm_big, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("epi"),
+        pybind11::arg("variant") = 1);
   m.def("moe_decode_gemm", &moe_decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("offs"), pybind11::arg("part"), pybind11::arg("rows_max"), pybind11::arg("mf"),
         pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"), pybind11::arg("epi"),

@@ -79,13 +79,131 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
   }
 }
 
+// Prefill form (no q/k norm): 16 consecutive tokens per workgroup.  The rotation moves 4 pairs per
+// lane (8-byte loads and stores instead of 2-byte ones), and when the 16 tokens fill one run of a
+// block's slots (a prefill chunk's tokens are consecutive slots of their sequence) their V rows are
+// staged in LDS and written as 32-byte runs of the dim-major V block instead of one 2-byte store
+// per (token, dim).  Any other slot pattern falls back to per-element V stores.
+__device__ __forceinline__ void kv_store4(bf16_t* p, const float* x, float) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack2(x[0], x[1]), pack2(x[2], x[3]));
+}
+__device__ __forceinline__ void kv_store4(fp8_t* p, const float* x, float inv) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) p[e] = f2fp8(x[e] * inv);
+}
+
+template <int D, typename KT>
+__global__ void __launch_bounds__(256) rope_cache_t16_kernel(
+    bf16_t* __restrict__ q_out, const bf16_t* __restrict__ qkv, const int64_t* __restrict__ positions,
+    const float* __restrict__ cos_sin, KT* __restrict__ kv, long block_stride, const int64_t* __restrict__ slot_mapping,
+    int Hq, int Hkv, int BS, int T, float k_inv_scale, float v_inv_scale) {
+  constexpr int HALF = D / 2, V4 = HALF / 4, TPB = 16;
+  extern __shared__ __attribute__((aligned(16))) bf16_t vstage[];  // [TPB][Hkv * D]
+  __shared__ int64_t s_slot0;
+  __shared__ int s_fast;
+  const int t0 = blockIdx.x * TPB, nt = min(TPB, T - t0);
+  const int row_stride = (Hq + 2 * Hkv) * D, hkd = Hkv * D;
+  const int per_tok = (Hq + Hkv) * V4;
+  if (threadIdx.x == 0) {
+    const int64_t s0 = slot_mapping[t0];
+    int fast = s0 >= 0 && (s0 % BS) + nt <= BS;
+    for (int k = 1; k < nt && fast; ++k) fast = slot_mapping[t0 + k] == s0 + k;
+    s_slot0 = s0;
+    s_fast = fast;
+  }
+  for (int i = threadIdx.x; i < nt * per_tok; i += blockDim.x) {
+    const int tt = i / per_tok, rem = i - tt * per_tok, head = rem / V4, p = (rem - head * V4) * 4;
+    const int t = t0 + tt;
+    const bf16_t* src = qkv + static_cast<size_t>(t) * row_stride + head * D;
+    const uint2 a = *reinterpret_cast<const uint2*>(src + p), b = *reinterpret_cast<const uint2*>(src + p + HALF);
+    const float* cs = cos_sin + positions[t] * D;
+    const float4 c = *reinterpret_cast<const float4*>(cs + p), sn = *reinterpret_cast<const float4*>(cs + HALF + p);
+    const float x1[4] = {bf2f_lo(a.x), bf2f_hi(a.x), bf2f_lo(a.y), bf2f_hi(a.y)};
+    const float x2[4] = {bf2f_lo(b.x), bf2f_hi(b.x), bf2f_lo(b.y), bf2f_hi(b.y)};
+    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+    float o1[4], o2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o1[e] = x1[e] * cc[e] - x2[e] * ss[e];
+      o2[e] = x2[e] * cc[e] + x1[e] * ss[e];
+    }
+    if (head < Hq) {
+      bf16_t* qo = q_out + (static_cast<size_t>(t) * Hq + head) * D;
+      *reinterpret_cast<uint2*>(qo + p) = make_uint2(pack2(o1[0], o1[1]), pack2(o1[2], o1[3]));
+      *reinterpret_cast<uint2*>(qo + p + HALF) = make_uint2(pack2(o2[0], o2[1]), pack2(o2[2], o2[3]));
+    } else {
+      const int64_t slot = slot_mapping[t];
+      if (slot >= 0) {
+        KT* kd = kv + (slot / BS) * block_stride + (static_cast<size_t>(head - Hq) * BS + slot % BS) * D;
+        kv_store4(kd + p, o1, k_inv_scale);
+        kv_store4(kd + p + HALF, o2, k_inv_scale);
+      }
+    }
+  }
+  __syncthreads();
+  const bf16_t* vbase = qkv + static_cast<size_t>(t0) * row_stride + (Hq + Hkv) * D;
+  if (!s_fast) {  // tokens of different blocks (or unmapped): one store per (token, dim)
+    for (int i = threadIdx.x; i < nt * hkd; i += blockDim.x) {
+      const int tt = i / hkd, j = i - tt * hkd;
+      const int64_t slot = slot_mapping[t0 + tt];
+      if (slot < 0) continue;
+      KT* dst = kv + (slot / BS) * block_stride + static_cast<size_t>(Hkv) * BS * D + static_cast<size_t>(j) * BS +
+                slot % BS;
+      const bf16_t v = vbase[static_cast<size_t>(tt) * row_stride + j];
+      if constexpr (sizeof(KT) == 2) *dst = v;
+      else kv_store(dst, bf2f(v), v_inv_scale);
+    }
+    return;
+  }
+  // stage the nt V rows (16-byte loads), then write each (head, dim) row's run of nt slots
+  for (int i = threadIdx.x; i < nt * (hkd / 8); i += blockDim.x) {
+    const int tt = i / (hkd / 8), j = (i - tt * (hkd / 8)) * 8;
+    *reinterpret_cast<uint4*>(vstage + tt * hkd + j) =
+        *reinterpret_cast<const uint4*>(vbase + static_cast<size_t>(tt) * row_stride + j);
+  }
+  __syncthreads();
+  const int64_t s0 = s_slot0;
+  const int off0 = static_cast<int>(s0 % BS);
+  KT* vblk = kv + (s0 / BS) * block_stride + static_cast<size_t>(Hkv) * BS * D;
+  for (int j = threadIdx.x; j < hkd; j += blockDim.x) {
+    KT* dst = vblk + static_cast<size_t>(j) * BS + off0;
+    if constexpr (sizeof(KT) == 2) {
+      if (nt == TPB && off0 == 0 && BS == TPB) {  // a whole 32-byte row of the block
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          w[k] = static_cast<uint32_t>(vstage[(2 * k) * hkd + j]) | (static_cast<uint32_t>(vstage[(2 * k + 1) * hkd + j]) << 16);
+        *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+        *reinterpret_cast<uint4*>(dst + 8) = make_uint4(w[4], w[5], w[6], w[7]);
+        continue;
+      }
+    }
+    for (int tt = 0; tt < nt; ++tt) {
+      if constexpr (sizeof(KT) == 2) dst[tt] = vstage[tt * hkd + j];
+      else kv_store(dst + tt, bf2f(vstage[tt * hkd + j]), v_inv_scale);
+    }
+  }
+}
+
 template <typename KT>
 static void launch_rope_typed(bf16_t* q_out, const bf16_t* qkv, const int64_t* positions, const float* cos_sin,
                               KT* kv, long block_stride, const int64_t* slot_mapping, const bf16_t* qn,
                               const bf16_t* kn, int T, int Hq, int Hkv, int D, int BS, float eps, float kis, float vis,
                               hipStream_t s) {
-  dim3 g(T), b(256);
   const bool norm = qn != nullptr;
+  if (!norm && T >= 512 && D % 8 == 0 && (D == 64 || D == 128) && Hkv * D * 16 * 2 <= 64 * 1024) {
+    const dim3 g16((T + 15) / 16), b16(256);
+    const size_t lds = static_cast<size_t>(16) * Hkv * D * sizeof(bf16_t);
+    if (D == 64)
+      hipLaunchKernelGGL((rope_cache_t16_kernel<64, KT>), g16, b16, lds, s, q_out, qkv, positions, cos_sin, kv,
+                         block_stride, slot_mapping, Hq, Hkv, BS, T, kis, vis);
+    else
+      hipLaunchKernelGGL((rope_cache_t16_kernel<128, KT>), g16, b16, lds, s, q_out, qkv, positions, cos_sin, kv,
+                         block_stride, slot_mapping, Hq, Hkv, BS, T, kis, vis);
+    MXS_CHECK_LAUNCH();
+    return;
+  }
+  dim3 g(T), b(256);
 #define MXS_ROPE_CASE(DD)                                                                                   \
   if (D == DD) {                                                                                            \
     if (norm)                                                                                               \

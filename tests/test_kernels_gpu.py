@@ -85,6 +85,41 @@ def test_rope_and_cache(gpu, D, hq, hkv, qknorm):
     assert kv[:, 0].abs().sum().item() == 0  # other layer untouched
 
 
+@pytest.mark.parametrize("D,hq,hkv", [(64, 32, 8), (128, 32, 8)])
+@pytest.mark.parametrize("kv_fp8", [False, True])
+def test_rope_and_cache_prefill_t16(gpu, D, hq, hkv, kv_fp8):
+    """Prefill-sized batches take the 16-tokens-per-workgroup kernel: contiguous chunks (V staged in
+    LDS and written as 32-byte block rows, including a chunk that starts mid-block and a short
+    tail), plus scattered slots and an unmapped token (per-element V fallback)."""
+    L, nb = 2, 200
+    # 3 sequences: 700 tokens from slot 0 (block-aligned), 333 from mid-block, 90 scattered
+    seg = [torch.arange(0, 700), torch.arange(64 * 16 + 5, 64 * 16 + 5 + 333), torch.randperm(60 * 16)[:90] + 110 * 16]
+    slots = torch.cat(seg).to(gpu)
+    slots[800] = -1
+    T = slots.shape[0]
+    cos_sin = ref.build_cos_sin_cache(D, 8192, 500000.0, None, device=gpu)
+    qkv = (torch.randn(T, (hq + 2 * hkv) * D, device=gpu) * (3 if kv_fp8 else 1)).to(torch.bfloat16)
+    pos = torch.randint(0, 8000, (T,), device=gpu)
+    dt = torch.uint8 if kv_fp8 else torch.bfloat16
+    kv = torch.zeros(nb, L, 2, hkv, 16, D, device=gpu, dtype=dt)
+    kv_ref = kv.clone().cpu()
+    sc = {"k_scale": 0.05, "v_scale": 0.05} if kv_fp8 else {}
+    q = ops.rope_and_cache(qkv, hq, hkv, D, pos, cos_sin, kv[:, 1], slots, None, None, 1e-6, **sc)
+    qs, ks = hq * D, hkv * D
+    c = qkv.cpu()
+    q_ref = ref.rope_and_cache(c[:, :qs].reshape(T, hq, D), c[:, qs:qs + ks].reshape(T, hkv, D),
+                               c[:, qs + ks:].reshape(T, hkv, D), pos.cpu(), cos_sin.cpu(), kv_ref[:, 1],
+                               slots.cpu(), None, None, 1e-6, **sc)
+    _close(q, q_ref, 0.03, 0.02, "q")
+    if kv_fp8:
+        got = kv.cpu().view(torch.float8_e4m3fn).float()
+        want = kv_ref.view(torch.float8_e4m3fn).float()
+        assert ((got - want).abs() <= 0.07 * want.abs() + 0.05).float().mean() > 0.995
+    else:
+        _close(kv, kv_ref, 0.03, 0.02, "kv cache")
+    assert kv[:, 0].float().abs().sum().item() == 0
+
+
 def _paged_setup(seq_lens, hkv, D, L=2, device="cuda"):
     nbs = [-(-s // 16) for s in seq_lens]
     nb = sum(nbs) + 5
@@ -755,6 +790,43 @@ def test_prefill_gemm_all_configs(gpu, M, N, K):
         out = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
         assert ops.prefill_gemm(out, x, w, cfg), cfg
         _close(out, want, atol=2e-2, rtol=2e-2, name=f"prefill gemm {M}x{N}x{K} cfg {cfg}")
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 256, 64), (300, 3072, 2048), (4133, 2048, 2048), (8192, 2048, 8192),
+                                   (257, 512, 192)])
+def test_gemm_big(gpu, M, N, K):
+    """Full-chunk prefill GEMM (csrc/kernels/gemm_big.hip) vs an fp32 reference, row counts that are
+    not tile multiples included, with an asymmetric W so a transposed store cannot pass."""
+    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=gpu) * 2 - 1) * K ** -0.5).to(torch.bfloat16)
+    w[:, 0] += torch.arange(N, device=gpu, dtype=torch.bfloat16) * 1e-3
+    for variant in (0, 1, 2):
+        out = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+        assert ops.ext().gemm_big(out, x, w, 0, variant)
+        _close(out, x.float() @ w.float().t(), atol=2e-2, rtol=2e-2, name=f"gemm_big v{variant} {M}x{N}x{K}")
+
+
+@pytest.mark.parametrize("M,I,K", [(1, 128, 64), (777, 1024, 2048), (4096, 8192, 2048)])
+def test_gemm_big_swiglu(gpu, M, I, K):
+    """gate_up with SiLU(gate) * up in the epilogue (W rows [gate; up], gathered per tile by the DMA
+    addresses) vs fp32 SiLU(x gate^T) * (x up^T)."""
+    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(2 * I, K, device=gpu) * 2 - 1) * 2 * K ** -0.5).to(torch.bfloat16)
+    gu = x.float() @ w.float().t()
+    want = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
+    for variant in (0, 1, 2):
+        out = torch.full((M, I), float("nan"), device=gpu, dtype=torch.bfloat16)
+        assert ops.ext().gemm_big(out, x, w, 1, variant)
+        _close(out, want, atol=2e-2, rtol=2e-2, name=f"gemm_big v{variant} swiglu {M}x{I}x{K}")
+
+
+def test_gemm_big_rejects_unsupported(gpu):
+    x = torch.randn(64, 2048, device=gpu, dtype=torch.bfloat16)
+    w = torch.randn(3000, 2048, device=gpu, dtype=torch.bfloat16)  # N not a multiple of 256
+    assert not ops.ext().gemm_big(torch.empty(64, 3000, device=gpu, dtype=torch.bfloat16), x, w, 0)
+    w = torch.randn(256, 2000, device=gpu, dtype=torch.bfloat16)  # K not a multiple of 64
+    assert not ops.ext().gemm_big(torch.empty(64, 256, device=gpu, dtype=torch.bfloat16),
+                                  torch.randn(64, 2000, device=gpu, dtype=torch.bfloat16), w, 0)
 
 
 def test_prefill_gemm_tuner_and_dispatch(gpu, monkeypatch):
