@@ -97,6 +97,8 @@ def parse(argv=None):
                     help="prefill ranks of the disagg phase (the rest decode); 0 = disagg_plan()")
     ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
     ap.add_argument("--max-model-len", type=int, default=8192)
+    ap.add_argument("--itl-target-ms", type=float, default=float(os.environ.get("MXS_BENCH_ITL_TARGET_MS", "0")),
+                    help="decode-aware prefill chunk budget (0 = fixed --max-num-batched-tokens chunks)")
     ap.add_argument("--enforce-eager", action="store_true")
     ap.add_argument("--kv-cache-dtype", default=os.environ.get("MXS_BENCH_KV_DTYPE", "auto"),
                     help="auto (bf16, the headline) | fp8 (e4m3fn KV cache: a separate, labelled data point)")
@@ -695,7 +697,8 @@ def engine_args(a, ctx, **kw):
     args = EngineArgs(model=a.model, device="cuda" if ctx.on_gpu else "cpu", max_num_seqs=a.max_num_seqs,
                       cuda_graph_max_bs=a.max_num_seqs,
                       max_num_batched_tokens=a.max_num_batched_tokens, max_model_len=a.max_model_len,
-                      enforce_eager=a.enforce_eager, seed=a.seed, kv_cache_dtype=a.kv_cache_dtype)
+                      enforce_eager=a.enforce_eager, seed=a.seed, kv_cache_dtype=a.kv_cache_dtype,
+                      itl_target_ms=a.itl_target_ms)
     if kw:
         args = args.replace(**kw)
     if not ctx.on_gpu:  # plumbing run only (CPU container): keep it tiny
@@ -759,12 +762,15 @@ def phase_agg(a, ctx) -> tuple:
     if rep:  # capture-time choice per (bucket, projection): hand-written MFMA kernels vs hipBLASLt
         info["decode_gemm"] = {"pairs": len(rep), "hand_written": sum(r["chosen"] == "mfma" for r in rep),
                                "mt_kernel": sum(bool(r["cfg"]) and r["cfg"][0] == "mt" for r in rep),
-                               "tune_s": round(getattr(eng.runner, "decode_gemm_tune_s", 0.0), 1)}
+                               "tune_s": round(getattr(eng.runner, "decode_gemm_tune_s", 0.0), 1),
+                               "from_table": sum(r.get("source") == "table" for r in rep)}
     la = getattr(eng, "_late", None)
     if la is not None:  # engine/pacing.py: how often the host waited for a late admission, and how long
         info["late_admission"] = {"waits": la.waits, "mean_wait_ms": round(1e3 * la.wait_s / max(1, la.waits), 3),
                                   "model_updates": la.model.n, "host_lead_ms": round(1e3 * la.host_lead, 3),
                                   "late_wakes": la.late, "margin_ms": round(1e3 * la.margin, 3)}
+    if eng.scheduler.chunk_budget is not None:
+        info["chunk_budget"] = eng.scheduler.chunk_budget.stats()
     host = None
     if eng.step_times is not None and eng.step_times["steps"]:
         n = eng.step_times["steps"]
@@ -903,7 +909,8 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
                    "parallelism": f"dp{world}" if agg is not None else (dis or {}).get("parallelism", "disagg"),
                    "mode": mode, "isl": info["isl"], "osl": info["osl"],
                    "qps_per_gpu": a.qps, "qps_node": a.qps * world, "kv_cache_dtype": info["kv_cache_dtype"],
-                   "shared_gpu": ctx.shared_gpu},
+                   "shared_gpu": ctx.shared_gpu, "max_num_batched_tokens": a.max_num_batched_tokens,
+                   "itl_target_ms": a.itl_target_ms or None},
     }
     for k in ("ttft_p50_ms", "ttft_p90_ms", "itl_p50_ms", "itl_p90_ms", "requests_with_first_token",
               "warmup_steps_executed", "warmup_s", "steady_state", "running_mean", "sla_isl4000_osl500"):
@@ -914,7 +921,7 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
     if dis is not None:
         line["disagg"] = dis
     line["engine"] = {"kv_blocks": info["kv_blocks"], "preemptions": info["preemptions"], "graphs": info["graphs"]}
-    for k in ("late_admission", "decode_gemm"):
+    for k in ("late_admission", "decode_gemm", "chunk_budget"):
         if k in info:
             line["engine"][k] = info[k]
     return line

@@ -29,6 +29,9 @@ class EngineArgs:
     max_num_seqs: int = 256
     max_num_batched_tokens: int = 8192
     enable_chunked_prefill: bool = True
+    # decode-aware prefill chunking: cap each step's prefill chunks so the step's predicted time
+    # (online step-time model, engine/pacing.py) stays under this inter-token latency (0 = off)
+    itl_target_ms: float = 0.0
     enable_prefix_caching: bool = True
     gpu_memory_utilization: float = 0.90
     num_gpu_blocks: Optional[int] = None  # override the memory-derived count

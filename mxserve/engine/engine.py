@@ -63,6 +63,15 @@ class LLMEngine:
             from .pacing import LateAdmission
             self._late = LateAdmission()
         self._inflight: Optional[tuple] = None
+        # decode-aware prefill chunk budget: priced by the late-admission step-time model, or by an
+        # own model fed with synchronous step times when late admission is off
+        self._budget_model = None
+        if args.itl_target_ms and args.itl_target_ms > 0:
+            from .pacing import ChunkBudget, StepTimeModel
+            model = self._late.model if self._late is not None else StepTimeModel()
+            if self._late is None:
+                self._budget_model = model
+            self.scheduler.chunk_budget = ChunkBudget(model, args.itl_target_ms)
         self.profiler = StepProfiler()  # MXS_TORCH_PROFILE="start:count:path"
         # MXS_STEP_TIMING=1: host seconds per phase (schedule / launch / collect wait / land)
         self.step_times: Optional[dict] = ({"schedule": 0.0, "launch": 0.0, "collect": 0.0, "land": 0.0,
@@ -198,6 +207,9 @@ class LLMEngine:
                               (time.perf_counter() if pending else None))
         else:
             sampled = self.runner.collect(dh)
+            if self._budget_model is not None and not self.async_scheduling:
+                from .pacing import step_features
+                self._budget_model.update(step_features(dso), time.perf_counter() - t_adm)
         if tm is None:
             return self._land(dso, sampled, dh.get("logprobs"))
         t3 = time.perf_counter()
@@ -241,6 +253,8 @@ class LLMEngine:
         if la is not None:
             s["late_admission"] = {"waits": la.waits, "late_wakes": la.late, "margin_ms": round(1e3 * la.margin, 3),
                                    "host_lead_ms": round(1e3 * la.host_lead, 3), "model_updates": la.model.n}
+        if self.scheduler.chunk_budget is not None:
+            s["chunk_budget"] = self.scheduler.chunk_budget.stats()
         return s
 
     def shutdown(self) -> None:

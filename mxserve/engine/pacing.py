@@ -17,6 +17,7 @@ times observed whenever the host sees a step finish (see LLMEngine._step).
 """
 from __future__ import annotations
 
+import math
 import os
 import time
 from typing import Optional
@@ -39,6 +40,18 @@ def step_features(so) -> np.ndarray:
     return np.array([1.0, p / 1e3, pa / 1e7, len(so.decodes) / 1e2, dctx / 1e5])
 
 
+def nonneg_fit(A: np.ndarray, b: np.ndarray) -> Optional[np.ndarray]:
+    """argmin_{theta >= 0} theta' A theta - 2 b' theta for the normal equations (A = X'X, b = X'y):
+    with A = L L' that is the non-negative least squares problem ||L' theta - L^-1 b||."""
+    try:
+        from scipy.optimize import nnls
+        L = np.linalg.cholesky(A + 1e-9 * np.eye(A.shape[0]))
+        theta, _ = nnls(L.T, np.linalg.solve(L, b))
+        return theta
+    except Exception:  # noqa: BLE001 - no scipy / not positive definite: no constrained fit
+        return None
+
+
 class StepTimeModel:
     def __init__(self, lam: float = 0.98, warmup: int = 24):
         self.lam = lam
@@ -46,6 +59,11 @@ class StepTimeModel:
         self.A = np.eye(NF) * 1e-6
         self.b = np.zeros(NF)
         self.theta: Optional[np.ndarray] = None
+        # the same fit with every coefficient >= 0 (a step cannot get faster with more work): prefill
+        # tokens and prefill attention work move together, so the unconstrained fit can trade one
+        # for the other with a negative sign, which is harmless for predicting a whole step but not
+        # for pricing a chunk of a given size (ChunkBudget)
+        self.theta_nn: Optional[np.ndarray] = None
         self.n = 0
 
     def update(self, x: np.ndarray, seconds: float) -> None:
@@ -59,11 +77,82 @@ class StepTimeModel:
                 self.theta = np.linalg.solve(self.A + 1e-9 * np.eye(NF), self.b)
             except np.linalg.LinAlgError:
                 self.theta = None
+            self.theta_nn = nonneg_fit(self.A, self.b)
 
     def predict(self, x: np.ndarray) -> Optional[float]:
         if self.theta is None:
             return None
         return max(0.0, float(x @ self.theta))
+
+
+class ChunkBudget:
+    """Decode-aware prefill chunk budget (--itl-target-ms).
+
+    A fixed token budget (max_num_batched_tokens) makes a step that carries a prefill chunk as long
+    as the decode rows plus the whole chunk: at 250 decode rows and an 8192-token chunk that step,
+    and so every running request's inter-token latency, is ~2.5x a decode-only step.  With a target
+    the scheduler prices the step's decode rows with the same online step-time model late admission
+    fits (StepTimeModel: intercept, decode rows, decode context, prefill tokens, prefill attention
+    work) and gives prefill chunks only the time left under the target.  The first chunk of a step
+    always gets at least `min_tokens`, so prefill never stalls (TTFT stays bounded when decode alone
+    exceeds the target).  The chunk is priced with the model's non-negative fit (theta_nn); until the
+    model is fitted no limit applies.
+    """
+
+    def __init__(self, model: StepTimeModel, target_ms: float, min_tokens: int = 256, align: int = 64):
+        self.model = model
+        self.target = float(target_ms) / 1e3
+        self.min_tokens = int(min_tokens)
+        self.align = int(align)
+        self.steps = 0  # steps that planned with a fitted model
+        self.limited = 0  # prefill chunks cut short by the budget
+        self.cut_tokens = 0
+
+    def begin(self, running) -> Optional[float]:
+        """Seconds left for prefill work in the next step (None = no limit)."""
+        th = self.model.theta_nn
+        if th is None or th[1] + th[2] <= 0.0:
+            return None
+        nd = 0
+        dctx = 0
+        for r in running:
+            c = r.num_computed_tokens
+            if r.num_tokens - c == 1 and c >= r.num_prompt_tokens:
+                nd += 1
+                dctx += c
+        self.steps += 1
+        return self.target - max(0.0, th[0] + th[3] * nd / 1e2 + th[4] * dctx / 1e5)
+
+    def fit(self, left: float, start: int, want: int, first: bool) -> tuple:
+        """Largest chunk <= want (tokens from position `start`) whose predicted cost fits in
+        `left` seconds; returns (tokens, seconds)."""
+        th = self.model.theta_nn
+        c1 = th[1] / 1e3  # s per prefill token
+        c2 = max(0.0, th[2] / 1e7)  # s per token x context token (attention)
+        b = max(c1 + c2 * start, 1e-9)
+        a = 0.5 * c2
+        if left <= 0.0:
+            n = 0
+        elif a > 0.0:
+            n = int((-b + math.sqrt(b * b + 4.0 * a * left)) / (2.0 * a) + 1e-6)
+        else:
+            n = int(left / b + 1e-6)
+        if n < want:
+            if n > self.align:
+                n -= n % self.align
+            if first:
+                n = max(n, self.min_tokens)
+            n = min(n, want)
+            if n < want:
+                self.limited += 1
+                self.cut_tokens += want - n
+        else:
+            n = want
+        return n, n * (b + a * n)
+
+    def stats(self) -> dict:
+        return {"target_ms": round(self.target * 1e3, 2), "planned_steps": self.steps, "limited_chunks": self.limited,
+                "cut_tokens": self.cut_tokens}
 
 
 class LateAdmission:

@@ -60,6 +60,9 @@ class Scheduler:
         self.num_preemptions = 0
         # disaggregated decode: requests whose prompt KV is being written by a prefill worker
         self.remote: dict[str, Request] = {}
+        # decode-aware prefill budget (engine/pacing.py ChunkBudget), set by the engine when an
+        # inter-token latency target is configured
+        self.chunk_budget = None
 
     # ------------------------------------------------------------------ queue ops
     def add(self, req: Request) -> None:
@@ -145,6 +148,9 @@ class Scheduler:
         out = SchedulerOutput()
         budget = self.max_num_batched_tokens
         scheduled: list[ScheduledReq] = []
+        cb = self.chunk_budget
+        left = cb.begin(self.running) if cb is not None else None  # seconds for prefill chunks
+        first = True
         i = 0
         while i < len(self.running) and budget > 0:
             req = self.running[i]
@@ -153,6 +159,13 @@ class Scheduler:
                 i += 1
                 continue
             n = min(n, budget)
+            if left is not None and (n > 1 or req.num_computed_tokens < req.num_prompt_tokens):
+                n, cost = cb.fit(left, req.num_computed_tokens, n, first)
+                first = False
+                if n <= 0:
+                    i += 1
+                    continue
+                left -= cost
             if n < req.num_tokens - req.num_computed_tokens and not self.chunked:
                 break
             while not self.kv.allocate_slots(req, n):
@@ -183,6 +196,10 @@ class Scheduler:
                 if not self.chunked:
                     break
                 n = budget
+            if left is not None and self.chunked:
+                n, cost = cb.fit(left, req.num_computed_tokens, n, first)
+                if n <= 0:
+                    break
             if not self.kv.allocate_slots(req, n):
                 break
             self.waiting.popleft()
@@ -192,6 +209,9 @@ class Scheduler:
             self.running.append(req)
             scheduled.append(ScheduledReq(req, n, req.num_computed_tokens + n >= req.num_tokens))
             budget -= n
+            if left is not None and self.chunked:
+                left -= cost
+                first = False
 
         for s in scheduled:
             r = s.req

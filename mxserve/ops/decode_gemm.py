@@ -85,11 +85,14 @@ def mt_candidates(M: int, N: int, K: int, epi: int, max_blocks: int = 1024) -> l
         outN = N // 2 if epi else N
         if outN % outb:
             continue
-        tiles = -(-M // bm) * (outN // outb)
+        ntm = -(-M // bm)
+        tiles = ntm * (outN // outb)
         for sk in (1, 2, 4, 8):
             if K % (64 * sk) or K // sk < 128 or tiles * sk > max_blocks:
                 continue
             out.append(("mt", wm, wn, mr, wnf, sk))
+            if ntm > 1:  # row tiles fastest: the tiles sharing a weight slice run together on one XCD
+                out.append(("mt", wm, wn, mr, wnf, sk, 1))
     return out
 
 
@@ -130,6 +133,7 @@ class DecodeGemmTable:
         self.part: Optional[torch.Tensor] = None  # fp32 split-K workspace (stable for graphs)
         self.cnt: Optional[torch.Tensor] = None  # mt kernel tile counters (in-launch split-K reduce)
         self.report: list = []
+        self.store_stats: dict = {}
 
     def lookup(self, M: int, N: int, K: int, epi: int) -> Optional[tuple]:
         if MODE == "off" or M > MAX_M:
@@ -149,7 +153,8 @@ class DecodeGemmTable:
         from . import ext
         mt = cfg[0] == "mt"
         if mt:
-            _, wm, wn, mr, wnf, sk = cfg
+            wm, wn, mr, wnf, sk = cfg[1:6]
+            order = cfg[6] if len(cfg) > 6 else 0
         else:
             mf, nf, wm, sk = cfg[:4]
             lu = cfg[4] if len(cfg) > 4 else 0
@@ -166,7 +171,8 @@ class DecodeGemmTable:
                 if torch.cuda.is_current_stream_capturing():
                     return False
                 self.cnt = torch.zeros(MT_COUNTERS, dtype=torch.int32, device=x.device)
-            return bool(ext().mt_gemm(out, x, w, part, wm, wn, mr, wnf, sk, epi, self.cnt if MT_FUSED_REDUCE else None))
+            return bool(ext().mt_gemm(out, x, w, part, wm, wn, mr, wnf, sk, epi, self.cnt if MT_FUSED_REDUCE else None,
+                                      order))
         return bool(ext().decode_gemm(out, x, w, part, mf, nf, wm, sk, epi, lu))
 
 
@@ -212,15 +218,47 @@ def _graph_time(fn, iters: int = 20) -> float:
     return e0.elapsed_time(e1) * 1e3 / iters
 
 
+FINALISTS = 3  # candidates re-timed after the screening pass
+ROUNDS = 3  # interleaved timing rounds of the finalists and hipBLASLt; the median decides
+WIN_MARGIN = 0.97  # a kernel replaces hipBLASLt only when its median is 3 % lower
+
+
+def pick(lib_fn, cand_fns: dict) -> tuple:
+    """Robust choice between hipBLASLt (`lib_fn`) and candidate kernels ({cfg: fn}): one screening
+    timing per candidate, then FINALISTS candidates and the library re-timed in ROUNDS interleaved
+    rounds; returns (cfg or None, median us of the choice, median us of hipBLASLt)."""
+    from .tuned import median
+    screen = sorted(((_graph_time(fn), cfg) for cfg, fn in cand_fns.items()), key=lambda t: t[0])
+    finals = [cfg for _, cfg in screen[:FINALISTS]]
+    times: dict = {None: []}
+    for cfg in finals:
+        times[cfg] = []
+    for _ in range(ROUNDS):
+        times[None].append(_graph_time(lib_fn))
+        for cfg in finals:
+            times[cfg].append(_graph_time(cand_fns[cfg]))
+    med = {cfg: median(v) for cfg, v in times.items()}
+    t_lib = med[None]
+    best, best_t = None, t_lib
+    for cfg in finals:
+        if med[cfg] < t_lib * WIN_MARGIN and (best is None or med[cfg] < best_t):
+            best, best_t = cfg, med[cfg]
+    return best, best_t, t_lib
+
+
 def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
-    """shapes: {name: (weight tensor [N, K], epi)}.  Fills TABLE; returns the report rows."""
+    """shapes: {name: (weight tensor [N, K], epi)}.  Fills TABLE; returns the report rows.  Choices
+    come from the persisted table (ops/tuned.py) when it has the (shape, bucket); otherwise they are
+    measured (pick()) and added to it."""
     if MODE != "auto":
         return []
-    from . import ext, silu_mul
+    from . import silu_mul
+    from .tuned import TunedStore, device_tag
     t0 = time.time()
     bks = sorted(b for b in buckets if b <= min(MAX_M, MAX_TUNE_M))
     if not bks:
         return []
+    store = TunedStore("decode_gemm", device_tag(device))
     # workspace for the largest split-K any candidate may pick
     need = max(8 * max(bks) * w.shape[0] for w, _ in shapes.values())
     TABLE.part = torch.empty(need, dtype=torch.float32, device=device)
@@ -229,25 +267,35 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
     for name, (w, epi) in shapes.items():
         N, K = w.shape
         ent = []
-        ws = weight_copies(w)  # timed from HBM, as the decode step reads them
+        ws = None
         for M in bks:
             x = (torch.randn(M, K, device=device) * 0.5).to(dtype)
             outN = N // 2 if epi else N
             ref_out = silu_mul(torch.nn.functional.linear(x, w)) if epi else torch.nn.functional.linear(x, w)
-            if epi:
-                t_lib = _graph_time(lambda i: silu_mul(torch.nn.functional.linear(x, ws[i % len(ws)])))
-            else:
-                t_lib = _graph_time(lambda i: torch.nn.functional.linear(x, ws[i % len(ws)]))
-            best, best_t = None, t_lib
             out = torch.empty(M, outN, dtype=dtype, device=device)
-            for cfg in candidates(M, N, K, epi):
-                if cfg[0] != "mt" and M > OLD_FORMS_MAX_M:
-                    continue
-                if not TABLE.run(out, x, w, cfg, epi):
-                    continue
-                t = _graph_time(lambda i: TABLE.run(out, x, ws[i % len(ws)], cfg, epi))
-                if t < best_t * 0.97:  # a clear win only
-                    best, best_t = cfg, t
+            key = f"{N}x{K}x{epi}@{M}"
+            st = store.get(key)
+            source = "table"
+            if st is not None:
+                best, best_t, t_lib = st.get("cfg"), st.get("us"), st.get("hipblaslt_us")
+                if best is not None and not TABLE.run(out, x, w, best, epi):
+                    best = None  # no longer tiles this shape: hipBLASLt
+            else:
+                source = "measured"
+                if ws is None:
+                    ws = weight_copies(w)  # timed from HBM, as the decode step reads them
+                if epi:
+                    lib_fn = lambda i: silu_mul(torch.nn.functional.linear(x, ws[i % len(ws)]))  # noqa: E731
+                else:
+                    lib_fn = lambda i: torch.nn.functional.linear(x, ws[i % len(ws)])  # noqa: E731
+                fns = {}
+                for cfg in candidates(M, N, K, epi):
+                    if cfg[0] != "mt" and M > OLD_FORMS_MAX_M:
+                        continue
+                    if not TABLE.run(out, x, w, cfg, epi):
+                        continue
+                    fns[cfg] = (lambda c: (lambda i: TABLE.run(out, x, ws[i % len(ws)], c, epi)))(cfg)
+                best, best_t, t_lib = pick(lib_fn, fns) if fns else (None, None, _graph_time(lib_fn))
             if best is not None:  # correctness gate: the winner must match hipBLASLt's result
                 TABLE.run(out, x, w, best, epi)
                 err = (out.float() - ref_out.float()).abs().max().item()
@@ -255,15 +303,21 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
                 if not err <= tol:
                     log.warning("decode GEMM %s M=%d cfg %s mismatches hipBLASLt (%.3g); not used", name, M, best, err)
                     best, best_t = None, t_lib
+            if source == "measured":
+                store.put(key, {"cfg": best, "us": round(best_t, 2) if best_t else None,
+                                "hipblaslt_us": round(t_lib, 2) if t_lib else None})
             ent.append((M, best))
-            rows.append({"proj": name, "M": M, "N": N, "K": K, "epi": epi, "hipblaslt_us": round(t_lib, 2),
-                         "chosen": "hipblaslt" if best is None else "mfma", "cfg": best, "us": round(best_t, 2)})
+            rows.append({"proj": name, "M": M, "N": N, "K": K, "epi": epi, "hipblaslt_us": t_lib and round(t_lib, 2),
+                         "chosen": "hipblaslt" if best is None else "mfma", "cfg": best,
+                         "us": best_t and round(best_t, 2), "source": source})
         TABLE.entries[(N, K, epi)] = ent
         del ws
     TABLE.report = rows
+    TABLE.store_stats = {"table_hits": store.hits, "measured": store.misses, "device": store.tag}
+    store.save()
     won = sum(r["chosen"] == "mfma" for r in rows)
-    log.info("decode GEMM tuning: MFMA kernel chosen for %d of %d (bucket, projection) pairs in %.1fs", won,
-             len(rows), time.time() - t0)
+    log.info("decode GEMM tuning: MFMA kernel chosen for %d of %d (bucket, projection) pairs in %.1fs "
+             "(%d from the persisted table)", won, len(rows), time.time() - t0, store.hits)
     path = os.environ.get("MXS_DECODE_GEMM_REPORT")
     if path:
         with open(path, "w") as f:
@@ -310,10 +364,13 @@ def _event_time(fn, iters: int = 10) -> float:
 
 def tune_prefill(weights: dict, device, dtype=torch.bfloat16, buckets=(384, 512, 768)) -> list:
     """weights: {name: [N, K] tensor}.  Per M bucket: every tile / split-K configuration of the
-    prefill kernel vs hipBLASLt (eager launches, as prefill runs), correctness-gated."""
+    prefill kernel vs hipBLASLt (eager launches, as prefill runs), correctness-gated; the choice is
+    persisted like the decode table's (median of ROUNDS timings of the finalists)."""
     if MODE != "auto":
         return []
     from .. import ops
+    from .tuned import TunedStore, device_tag, median
+    store = TunedStore("prefill_gemm", device_tag(device))
     rows = []
     for name, w in weights.items():
         N, K = w.shape
@@ -321,23 +378,42 @@ def tune_prefill(weights: dict, device, dtype=torch.bfloat16, buckets=(384, 512,
         for M in sorted(b for b in buckets if 256 < b <= PREFILL_MAX_M):
             x = (torch.randn(M, K, device=device) * 0.5).to(dtype)
             ref = torch.nn.functional.linear(x, w)
-            t_lib = _event_time(lambda: torch.nn.functional.linear(x, w))
-            best, best_t = None, t_lib
             out = torch.empty(M, N, dtype=dtype, device=device)
-            for cfg in ops.prefill_gemm_configs(M, N, K):
-                if not ops.prefill_gemm(out, x, w, cfg):
-                    continue
-                t = _event_time(lambda: ops.prefill_gemm(out, x, w, cfg))
-                if t < best_t * 0.97:
-                    best, best_t = cfg, t
+            key = f"{N}x{K}@{M}"
+            st = store.get(key)
+            if st is not None:
+                best, best_t, t_lib = st.get("cfg"), st.get("us"), st.get("hipblaslt_us")
+                if best is not None and not ops.prefill_gemm(out, x, w, best):
+                    best = None
+                source = "table"
+            else:
+                source = "measured"
+                cands = [cfg for cfg in ops.prefill_gemm_configs(M, N, K) if ops.prefill_gemm(out, x, w, cfg)]
+                screen = sorted((_event_time(lambda: ops.prefill_gemm(out, x, w, c)), c) for c in cands)
+                finals = [c for _, c in screen[:FINALISTS]]
+                tl, tc = [], {c: [] for c in finals}
+                for _ in range(ROUNDS):
+                    tl.append(_event_time(lambda: torch.nn.functional.linear(x, w)))
+                    for c in finals:
+                        tc[c].append(_event_time(lambda: ops.prefill_gemm(out, x, w, c)))
+                t_lib = median(tl)
+                best, best_t = None, t_lib
+                for c in finals:
+                    t = median(tc[c])
+                    if t < t_lib * WIN_MARGIN and (best is None or t < best_t):
+                        best, best_t = c, t
             if best is not None:
                 ops.prefill_gemm(out, x, w, best)
                 err = (out.float() - ref.float()).abs().max().item()
                 if not err <= 0.02 * max(1.0, ref.float().abs().max().item()):
                     best, best_t = None, t_lib
+            if source == "measured":
+                store.put(key, {"cfg": best, "us": round(best_t, 2), "hipblaslt_us": round(t_lib, 2)})
             ent.append((M, best))
-            rows.append({"proj": name, "M": M, "N": N, "K": K, "hipblaslt_us": round(t_lib, 2),
-                         "chosen": "hipblaslt" if best is None else "mfma", "cfg": best, "us": round(best_t, 2)})
+            rows.append({"proj": name, "M": M, "N": N, "K": K, "hipblaslt_us": t_lib and round(t_lib, 2),
+                         "chosen": "hipblaslt" if best is None else "mfma", "cfg": best,
+                         "us": best_t and round(best_t, 2), "source": source})
         PREFILL_TABLE.entries[(N, K)] = ent
     PREFILL_TABLE.report = rows
+    store.save()
     return rows

@@ -55,6 +55,8 @@ def _parser(dialect: str) -> argparse.ArgumentParser:
                     default=None)
     ap.add_argument("--max-num-batched-tokens", "--chunked-prefill-size", "--max-num-tokens",
                     dest="max_num_batched_tokens", type=int, default=None)
+    ap.add_argument("--itl-target-ms", dest="itl_target_ms", type=float, default=None,
+                    help="decode-aware prefill chunking: keep each step's predicted time under this ITL")
     ap.add_argument("--gpu-memory-utilization", "--mem-fraction-static", "--free-gpu-memory-fraction",
                     dest="gpu_memory_utilization", type=float, default=None)
     ap.add_argument("--num-gpu-blocks-override", dest="num_gpu_blocks", type=int, default=None)
@@ -95,7 +97,7 @@ _YAML_MAP = {
     "enable_chunked_prefill": "enable_chunked_prefill", "tokens_per_block": "block_size",
     "max_model_len": "max_model_len", "max_num_seqs": "max_num_seqs", "block_size": "block_size",
     "gpu_memory_utilization": "gpu_memory_utilization", "enforce_eager": "enforce_eager",
-    "moe_dispatch": "moe_dispatch",
+    "moe_dispatch": "moe_dispatch", "itl_target_ms": "itl_target_ms",
 }
 
 
@@ -131,7 +133,7 @@ def parse_worker_args(argv: list[str], dialect: str = "vllm") -> WorkerArgs:
         "model": a.model, "served_model_name": a.served_model_name, "dtype": a.dtype, "load_format": a.load_format,
         "seed": a.seed, "tensor_parallel_size": a.tp, "block_size": a.block_size, "max_model_len": a.max_model_len,
         "max_num_seqs": a.max_num_seqs, "max_num_batched_tokens": a.max_num_batched_tokens,
-        "gpu_memory_utilization": a.gpu_memory_utilization, "num_gpu_blocks": a.num_gpu_blocks,
+        "itl_target_ms": a.itl_target_ms, "gpu_memory_utilization": a.gpu_memory_utilization, "num_gpu_blocks": a.num_gpu_blocks,
         "enforce_eager": a.enforce_eager, "enable_prefix_caching": a.enable_prefix_caching,
         "enable_chunked_prefill": a.enable_chunked_prefill, "device": a.device,
         "async_scheduling": a.async_scheduling, "moe_dispatch": a.moe_dispatch,

@@ -1,0 +1,153 @@
+"""Decode-aware prefill chunk budget (engine/pacing.py ChunkBudget, --itl-target-ms): the scheduler
+caps prefill chunks so a step's predicted time stays under the target, always gives the first
+chunk of a step its minimum, and leaves decodes alone.  CPU only."""
+import numpy as np
+import pytest
+
+from mxserve.engine.kv_manager import KVCacheManager
+from mxserve.engine.pacing import ChunkBudget, StepTimeModel, step_features
+from mxserve.engine.request import Request, SamplingParams
+from mxserve.engine.scheduler import Scheduler
+
+
+def _model(theta):
+    m = StepTimeModel()
+    m.theta = np.asarray(theta, dtype=float)
+    m.theta_nn = m.theta
+    return m
+
+
+# 2 ms intercept, 2 ms per 1000 prefill tokens, no attention term, 4 ms per 100 decode rows
+THETA = [2e-3, 2e-3, 0.0, 4e-3, 0.0]
+
+
+def _req(i, n_prompt):
+    return Request(f"r{i}", list(range(1, n_prompt + 1)), SamplingParams(max_tokens=64, ignore_eos=True))
+
+
+def _sched(target_ms, theta=THETA, budget=8192):
+    s = Scheduler(KVCacheManager(4096, 16, False), max_num_seqs=256, max_num_batched_tokens=budget,
+                  max_model_len=8192)
+    if target_ms:
+        s.chunk_budget = ChunkBudget(_model(theta), target_ms)
+    return s
+
+
+def _to_decode(s, n):
+    """n requests that have finished their prefill and sit in the running batch as decodes."""
+    cb, s.chunk_budget = s.chunk_budget, None
+    for i in range(n):
+        s.add(_req(1000 + i, 32))
+    so = s.schedule()
+    s.update(so, {x.req.request_id: 5 for x in so.all() if x.sample})
+    s.chunk_budget = cb
+    assert all(r.num_computed_tokens >= r.num_prompt_tokens for r in s.running)
+
+
+def test_no_target_uses_token_budget():
+    s = _sched(0)
+    s.add(_req(0, 6000))
+    so = s.schedule()
+    assert so.prefills[0].num_new_tokens == 6000
+
+
+def test_budget_caps_prefill_chunk():
+    s = _sched(20.0)
+    s.add(_req(0, 6000))
+    so = s.schedule()
+    # 20 ms - 2 ms intercept = 18 ms at 2 us/token -> 9000 tokens: whole prompt fits
+    assert so.prefills[0].num_new_tokens == 6000
+    s = _sched(10.0)
+    s.add(_req(0, 6000))
+    so = s.schedule()
+    # 8 ms / 2 us = 4000 tokens, rounded down to a multiple of 64
+    assert so.prefills[0].num_new_tokens == 3968
+    assert s.chunk_budget.limited == 1 and s.chunk_budget.cut_tokens == 2032
+
+
+def test_decodes_take_their_share_first():
+    s = _sched(10.0)
+    _to_decode(s, 100)  # 100 decode rows: 4 ms
+    s.add(_req(0, 6000))
+    so = s.schedule()
+    assert len(so.decodes) == 100
+    # 10 - 2 - 4 = 4 ms -> 2000 tokens -> 1984
+    assert so.prefills[0].num_new_tokens == 1984
+    x = step_features(so)
+    assert float(x @ np.asarray(THETA)) <= 10e-3 + 1e-9
+
+
+def test_first_chunk_gets_minimum_when_decode_exceeds_target():
+    s = _sched(5.0)
+    _to_decode(s, 100)  # decode alone: 6 ms > 5 ms
+    s.add(_req(0, 6000))
+    s.add(_req(1, 3000))
+    so = s.schedule()
+    assert len(so.decodes) == 100
+    assert [p.num_new_tokens for p in so.prefills] == [256]  # min_tokens, and the second waits
+
+
+def test_running_chunked_prefill_continues_under_budget():
+    s = _sched(10.0)
+    s.add(_req(0, 8000))
+    first = s.schedule()
+    assert first.prefills[0].num_new_tokens == 3968
+    s.update(first, {})
+    second = s.schedule()
+    assert second.prefills[0].start == 3968 and second.prefills[0].num_new_tokens == 3968
+
+
+def test_attention_term_shrinks_late_chunks():
+    # attention 1 ms per 1e7 token*context: a chunk deep into a long prompt costs more per token
+    theta = [2e-3, 2e-3, 1e-3, 0.0, 0.0]
+    cb = ChunkBudget(_model(theta), 10.0)
+    n0, c0 = cb.fit(8e-3, 0, 8000, True)
+    n1, c1 = cb.fit(8e-3, 6000, 8000, True)
+    assert n1 < n0
+    assert c0 <= 8e-3 + 1e-9 and c1 <= 8e-3 + 1e-9
+
+
+def test_unfitted_or_degenerate_model_means_no_limit():
+    s = _sched(10.0, theta=[2e-3, -1e-3, 0, 0, 0])
+    s.add(_req(0, 6000))
+    assert s.schedule().prefills[0].num_new_tokens == 6000
+    s = _sched(0)
+    s.chunk_budget = ChunkBudget(StepTimeModel(), 10.0)  # theta None: not fitted yet
+    s.add(_req(0, 6000))
+    assert s.schedule().prefills[0].num_new_tokens == 6000
+
+
+def test_engine_wires_target_from_args():
+    from mxserve.config import EngineArgs
+    from mxserve.engine.engine import LLMEngine
+    eng = LLMEngine(EngineArgs(model="tiny-llama", device="cpu", cpu_num_blocks=256, max_model_len=512,
+                               itl_target_ms=50.0, async_scheduling=False))
+    assert eng.scheduler.chunk_budget is not None
+    sp = SamplingParams(max_tokens=4, ignore_eos=True)
+    outs = eng.generate([list(range(1, 40)) for _ in range(30)], sp)
+    assert all(len(o) == 4 for o in outs)
+    assert eng._budget_model.n > 0
+    assert eng.stats()["chunk_budget"]["target_ms"] == 50.0
+
+
+def test_cli_flag():
+    from mxserve.worker.args import parse_worker_args
+    wa = parse_worker_args(["--model", "tiny-llama", "--itl-target-ms", "25"])
+    assert wa.engine.itl_target_ms == 25.0
+
+
+def test_nonneg_fit_on_collinear_steps():
+    """Prefill tokens and prefill attention work move together in real traffic; the constrained fit
+    keeps every coefficient >= 0 and still predicts the steps."""
+    rng = np.random.default_rng(0)
+    m = StepTimeModel()
+    true = np.array([3e-3, 2.5e-3, 0.4e-3, 4e-3, 1e-3])
+    for _ in range(400):
+        p = rng.choice([0, 0, 8192, 4096]) + rng.integers(0, 64)
+        start = rng.integers(0, 4000)
+        x = np.array([1.0, p / 1e3, p * (start + p / 2) / 1e7, rng.integers(50, 300) / 1e2,
+                      rng.integers(50, 300) * 4000 / 1e5])
+        m.update(x, float(x @ true) * (1 + 0.02 * rng.standard_normal()))
+    assert m.theta_nn is not None and (m.theta_nn >= 0).all()
+    x = np.array([1.0, 8.192, 8192 * 6096 / 1e7, 2.0, 8.0])
+    assert abs(float(x @ m.theta_nn) - float(x @ true)) < 0.05 * float(x @ true)

@@ -525,7 +525,7 @@ def test_decode_gemm_all_configs(gpu, M, N, K, epi):
     for c in cands:
         out = torch.full((M, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
         if c[0] == "mt":
-            assert ops.ext().mt_gemm(out, x, w, part, *c[1:], epi)
+            assert ops.ext().mt_gemm(out, x, w, part, *c[1:6], epi, None, c[6] if len(c) > 6 else 0)
         else:
             assert ops.ext().decode_gemm(out, x, w, part, *c[:4], epi, c[4])
         _close(out, want, atol=2e-2, rtol=2e-2, name=f"decode gemm {M}x{N}x{K} epi{epi} cfg {c}")
@@ -549,15 +549,15 @@ def test_mt_gemm_all_layouts(gpu, M, N, K, epi):
     ran = 0
     for lay in decode_gemm.MT_LAYOUTS:
         for sk in (1, 2, 4):
-            for fused in ((False, True) if sk > 1 else (False,)):
+            for fused, order in (((False, 0), (True, 0), (False, 1), (True, 1)) if sk > 1 else ((False, 0), (False, 1))):
                 out = torch.full((M, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
                 for _ in range(2 if fused else 1):  # the second launch reuses the counters the first re-armed
-                    if not ops.ext().mt_gemm(out, x, w, part, *lay, sk, epi, cnt if fused else None):
+                    if not ops.ext().mt_gemm(out, x, w, part, *lay, sk, epi, cnt if fused else None, order):
                         break
                 else:
                     ran += 1
                     _close(out, want, atol=2e-2, rtol=2e-2,
-                           name=f"mt gemm {M}x{N}x{K} epi{epi} {lay} sk{sk} fused-reduce {fused}")
+                           name=f"mt gemm {M}x{N}x{K} epi{epi} {lay} sk{sk} fused-reduce {fused} order {order}")
     assert ran >= 8
     assert int(cnt.abs().sum().item()) == 0, "every launch leaves the tile counters zero"
 
