@@ -92,7 +92,8 @@ def parse(argv=None):
     ap.add_argument("--disagg-max-num-seqs", type=int, default=512,
                     help="decode ranks of the disagg phase carry 2x the per-GPU request rate")
     ap.add_argument("--disagg-qps", type=float, default=float(os.environ.get("MXS_BENCH_DISAGG_QPS", "0")),
-                    help="disagg phase arrival rate per GPU; 0 = from the capacity model of disagg_plan()")
+                    help="disagg phase arrival rate per GPU; 0 = the agg rate (like-for-like) when the split "
+                         "can carry it, else the capacity rate; < 0 = the capacity rate of disagg_plan()")
     ap.add_argument("--disagg-prefill-ranks", type=int, default=int(os.environ.get("MXS_BENCH_DISAGG_P", "0")),
                     help="prefill ranks of the disagg phase (the rest decode); 0 = disagg_plan()")
     ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
@@ -224,8 +225,14 @@ def disagg_plan(a, world: int) -> tuple:
     p = min(max(1, p), world - 1)
     d = world - p
     qps = a.disagg_qps
-    if qps <= 0:
-        qps = (_DISAGG_UTIL * min(p * _CAP_PREFILL, d * _CAP_DECODE) / world) if headline else 0.76 * a.qps
+    cap = (_DISAGG_UTIL * min(p * _CAP_PREFILL, d * _CAP_DECODE) / world) if headline else 0.76 * a.qps
+    if qps == 0:
+        # like-for-like with the agg phase (the same arrival rate per GPU) unless this split cannot
+        # carry it (1P+1D on 2 GPUs has one decode GPU for twice its share): then the capacity rate
+        full = min(p * _CAP_PREFILL, d * _CAP_DECODE) / world if headline else a.qps
+        qps = a.qps if a.qps <= 0.95 * full + 1e-9 else cap
+    elif qps < 0:  # capacity-derived: the tighter role loaded to 85 %
+        qps = cap
     return p, d, qps
 
 
@@ -882,6 +889,21 @@ def disagg_summary(col_d: np.ndarray, info_d: dict, a, world: int) -> dict:
     return dis
 
 
+def compare_modes(agg: dict, dis: dict, agg_qps: float) -> dict:
+    """Agg vs disagg on the same node: the arrival rate each ran at (like-for-like when equal) and
+    which mode is better on each serving metric."""
+    keys = (("value", True), ("ttft_p50_ms", False), ("ttft_p90_ms", False), ("itl_p50_ms", False),
+            ("itl_p90_ms", False))
+    out = {"qps_per_gpu": {"agg": agg_qps, "disagg": dis.get("qps_per_gpu")},
+           "like_for_like": dis.get("qps_per_gpu") is not None and abs(float(dis["qps_per_gpu"]) - agg_qps) < 0.01}
+    for k, higher in keys:
+        va, vd = agg.get(k), dis.get(k)
+        if va is None or vd is None:
+            continue
+        out[k] = {"agg": va, "disagg": vd, "better": ("agg" if (va > vd) == higher else "disagg") if va != vd else "tie"}
+    return out
+
+
 def build_line(a, ctx, mode, agg, dis, info) -> dict:
     head = agg if agg is not None else dis
     world = ctx.world
@@ -918,6 +940,7 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
     line["ttft_window"] = "steady state: post-warmup soak + timed steps"
     if agg is not None and dis is not None:
         line["agg"] = {k: agg[k] for k in ("value", "ttft_p50_ms", "itl_p50_ms", "ms_per_step")}
+        line["agg_vs_disagg"] = compare_modes(agg, dis, a.qps)
     if dis is not None:
         line["disagg"] = dis
     line["engine"] = {"kv_blocks": info["kv_blocks"], "preemptions": info["preemptions"], "graphs": info["graphs"]}

@@ -65,10 +65,14 @@ class StepTimeModel:
         # for pricing a chunk of a given size (ChunkBudget)
         self.theta_nn: Optional[np.ndarray] = None
         self.n = 0
+        self.prefill_samples: list = []  # last few (features, seconds) of steps with prefill (stats)
 
     def update(self, x: np.ndarray, seconds: float) -> None:
         if not (0.0 < seconds < 5.0):
             return
+        if x[1] > 0:
+            self.prefill_samples = self.prefill_samples[-7:] + [[round(float(v), 4) for v in x[1:]] +
+                                                                [round(1e3 * seconds, 3)]]
         self.A = self.lam * self.A + np.outer(x, x)
         self.b = self.lam * self.b + x * seconds
         self.n += 1
@@ -151,8 +155,14 @@ class ChunkBudget:
         return n, n * (b + a * n)
 
     def stats(self) -> dict:
+        th = self.model.theta_nn
         return {"target_ms": round(self.target * 1e3, 2), "planned_steps": self.steps, "limited_chunks": self.limited,
-                "cut_tokens": self.cut_tokens}
+                "cut_tokens": self.cut_tokens, "model_updates": self.model.n,
+                # fitted costs: ms per step, per 1k prefill tokens, per 1e7 token x context, per 100
+                # decode rows, per 1e5 decode context tokens
+                "theta_nn_ms": None if th is None else [round(1e3 * float(v), 4) for v in th],
+                "theta_ms": None if self.model.theta is None else [round(1e3 * float(v), 4) for v in self.model.theta],
+                "prefill_samples": self.model.prefill_samples}
 
 
 class LateAdmission:

@@ -16,7 +16,9 @@ Three dispatch layouts:
             per-destination stable slot assignment, the row gather and the weighted combine are HIP
             kernels (csrc/kernels/ep.hip, K17 moe_combine) and the all-to-alls push only each
             destination's real rows (counts stay on the device: no host sync, no N x over-send,
-            hipGraph-capturable); the slices are all-gathered through the same slots;
+            hipGraph-capturable); the slices are all-gathered through the same slots.  A slice
+            whose worst-case segment exceeds a slot (prefill chunks: Mixtral at EP = 8 above 4,096
+            tokens) runs as several slot-sized chunks, still without a host sync;
   fixed     every destination gets a capacity of C = k * ceil(T/N) rows (the worst case), so all
             splits are equal, nothing is read back to the host and the step stays
             hipGraph-capturable -- decode batches;
@@ -84,6 +86,41 @@ def _gather_slices(out_s: torch.Tensor, T: int, n: int, group) -> torch.Tensor:
     return full[:T]
 
 
+def _ipc_chunk(out_c: torch.Tensor, hs: torch.Tensor, tw: torch.Tensor, tid: torch.Tensor, valid: int,
+               w13: torch.Tensor, w2: torch.Tensor, top_k: int, n: int, car) -> None:
+    """One chunk of a rank's token slice through the IPC dispatch: route (per-destination stable
+    slots, csrc/kernels/ep.hip), gather rows, push each destination's real rows into its slot, run
+    the local experts over what arrived, push the results back, weighted-combine into out_c."""
+    ext = ops.ext()
+    dev, H = hs.device, hs.shape[1]
+    e_local = w13.shape[0]
+    C = hs.shape[0] * top_k  # segment capacity: every pair of the chunk to one destination
+    P = C
+    tid32 = tid.to(torch.int32).contiguous()
+    slot = torch.empty(P, dtype=torch.int32, device=dev)
+    send_e = torch.empty(n * C, dtype=torch.int32, device=dev)
+    counts = torch.empty(n, dtype=torch.int32, device=dev)
+    ext.ep_route(slot, send_e, counts, tid32, valid, e_local, n, C)
+    send_x = torch.empty(n * C, H, dtype=hs.dtype, device=dev)  # rows past a segment's count unused
+    ext.ep_gather_rows(send_x, hs, slot, top_k)
+    recv_e = torch.empty_like(send_e)
+    recv_x = torch.empty_like(send_x)
+    if n > 1:
+        car.all_to_all(recv_e, send_e)  # the ids travel whole (-1 past each count): tiny
+        car.all_to_all(recv_x, send_x, counts, H * hs.element_size())
+    else:
+        recv_e, recv_x = send_e, send_x
+    ones = torch.ones(n * C, 1, dtype=torch.float32, device=dev)
+    y = ops.moe_experts(recv_x, w13, w2, ones, recv_e.unsqueeze(1), 0)
+    rcounts = torch.empty(n, dtype=torch.int32, device=dev)
+    ext.ep_segment_rows(rcounts, recv_e, C)
+    back = y
+    if n > 1:
+        back = torch.empty_like(y)
+        car.all_to_all(back, y, rcounts, H * hs.element_size())
+    ext.moe_combine(out_c, back, tw.float().contiguous(), slot)  # K17: weighted gather, fp32 accumulate
+
+
 def moe_a2a(h: torch.Tensor, gate_w: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, top_k: int,
             rank: int, world: int, group=None, force_layout: str | None = None) -> torch.Tensor:
     """h [T, H] replicated on every rank -> MoE output [T, H] replicated on every rank.
@@ -106,40 +143,24 @@ def moe_a2a(h: torch.Tensor, gate_w: torch.Tensor, w13: torch.Tensor, w2: torch.
     local_eid = (tid.long().reshape(P) - dest * e_local).to(torch.int32)
     tok = torch.arange(P, device=dev) // top_k
     car = _ipc_a2a(group, h)
-    C = P
     if force_layout is not None:
         layout = force_layout
-    elif n > 1 and car is not None and C * H * h.element_size() <= car.max_bytes:
-        layout = "ipc"  # one destination segment (capacity C rows) fits an IPC slot
+    elif n > 1 and car is not None and top_k * H * h.element_size() <= car.max_bytes:
+        layout = "ipc"  # device-side dispatch, in slot-sized chunks of the slice
     else:
         layout = "fixed" if P <= FIXED_MAX_PAIRS else "variable"
 
     if layout == "ipc":
-        ext = ops.ext()
-        tid32 = tid.to(torch.int32).contiguous()
-        slot = torch.empty(P, dtype=torch.int32, device=dev)
-        send_e = torch.empty(n * C, dtype=torch.int32, device=dev)
-        counts = torch.empty(n, dtype=torch.int32, device=dev)
-        ext.ep_route(slot, send_e, counts, tid32, hi - lo, e_local, n, C)
-        send_x = torch.empty(n * C, H, dtype=h.dtype, device=dev)  # rows past a segment's count unused
-        ext.ep_gather_rows(send_x, hs, slot, top_k)
-        recv_e = torch.empty_like(send_e)
-        recv_x = torch.empty_like(send_x)
-        if n > 1:
-            car.all_to_all(recv_e, send_e)  # the ids travel whole (-1 past each count): tiny
-            car.all_to_all(recv_x, send_x, counts, H * h.element_size())
-        else:
-            recv_e, recv_x = send_e, send_x
-        ones = torch.ones(n * C, 1, dtype=torch.float32, device=dev)
-        y = ops.moe_experts(recv_x, w13, w2, ones, recv_e.unsqueeze(1), 0)
-        rcounts = torch.empty(n, dtype=torch.int32, device=dev)
-        ext.ep_segment_rows(rcounts, recv_e, C)
-        back = y
-        if n > 1:
-            back = torch.empty_like(y)
-            car.all_to_all(back, y, rcounts, H * h.element_size())
+        # one destination segment of a chunk (k x rows pairs) must fit an IPC slot: a prefill slice
+        # larger than that runs as several chunks, every one on the device (no host sync), the same
+        # number on every rank (S is equal everywhere)
+        sc = S if force_layout == "ipc" and n == 1 else max(1, car.max_bytes // (top_k * H * h.element_size()))
         out_s = torch.empty(S, H, dtype=h.dtype, device=dev)
-        ext.moe_combine(out_s, back, tw.float().contiguous(), slot)  # K17: weighted gather, fp32 accumulate
+        valid = hi - lo
+        for c0 in range(0, S, sc):
+            c1 = min(S, c0 + sc)
+            _ipc_chunk(out_s[c0:c1], hs[c0:c1], tw[c0:c1], tid[c0:c1], max(0, min(valid - c0, c1 - c0)),
+                       w13, w2, top_k, n, car)
         return _gather_slices(out_s, T, n, group)
 
     if layout == "fixed":

@@ -134,6 +134,66 @@ class Probe:
                                                  "correct": ok})
         return out
 
+    def graph_collectives(self) -> dict:
+        """The decode graphs' collectives, captured in a hipGraph and replayed with fresh inputs: the
+        lm_head logits all-gather at a bucket above the IPC slot (RCCL inside the graph on a real
+        node), a 1 MiB one (IPC all-to-all), and a 16 MiB RCCL all-reduce.  Each replay's result is
+        checked against the rank-dependent fill."""
+        from ..parallel.comm import collectives_capturable, get_tp, tp_all_gather
+        import torch.distributed as dist
+        torch, n = self.torch, self.world
+        if not self.on_gpu:
+            return {"skipped": "no GPU"}
+        st = get_tp()
+        out = {"backend": self.backend, "cases": []}
+        cols = 16032  # Llama-3-70B vocab shard at TP 8
+        for op, nbytes in (("all_gather", 1 << 20), ("all_gather", 16 << 20), ("all_reduce", 16 << 20)):
+            case = {"op": op, "bytes": nbytes}
+            if not collectives_capturable(nbytes):
+                case["skipped"] = "not capturable on this group (gloo beyond the IPC slot)"
+                out["cases"].append(case)
+                continue
+            rows = max(1, nbytes // 2 // (cols if op == "all_gather" else 4096))
+            x = torch.zeros(rows, cols if op == "all_gather" else 4096, dtype=torch.bfloat16, device=self.dev)
+
+            def body():
+                if op == "all_gather":
+                    return tp_all_gather(x, dim=-1)
+                dist.all_reduce(x, group=st.group)
+                return x
+
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):  # warm-up outside the capture (communicator set-up)
+                body()
+            torch.cuda.current_stream().wait_stream(s)
+            self.sync()
+            self.barrier()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                y = body()
+            ok = True
+            for it in (1, 2, 3):
+                x.fill_(float((self.rank + 1) * it))
+                g.replay()
+                self.sync()
+                if op == "all_gather":
+                    got = y.view(rows, n, cols)[0, :, :8].float().cpu()
+                    want = torch.tensor([[(r + 1) * it] * 8 for r in range(n)], dtype=torch.float32)
+                else:
+                    got = y[0, :8].float().cpu()
+                    want = torch.full((8,), float(it * n * (n + 1) // 2))
+                ok = ok and bool(torch.equal(got, want))
+            t = self.timeit(g.replay, iters=10)
+            car = st.custom_ar
+            # tp_all_gather pushes each peer one x-sized segment through the IPC all-to-all when it fits
+            ipc = op == "all_gather" and car is not None and not car.disabled and x.numel() * 2 <= car.max_bytes
+            case.update(correct=ok, replay_us=round(t * 1e6, 1),
+                        path="ipc" if ipc else ("rccl" if self.backend == "nccl" else "gloo"))
+            out["cases"].append(case)
+            del g, x
+        return out
+
     def _logits_and_time(self, model: str, full: dict, moe_dispatch: str, n_tok: int = 64):
         from ..models.config import get_model_config
         from ..models.llama import build_model
@@ -342,7 +402,7 @@ class Probe:
     # Wall seconds a section needs to finish on an MI355X node (the r2 2-rank run took 0.2-41 s per
     # section; engines of the 70B / Mixtral shapes dominate): a section starts only if the deadline
     # leaves it this much.  CPU plumbing runs use the small number.
-    SECTION_COST_S = {"collectives": 20, "tp": 40, "ep": 40, "p2p": 15, "tp_engine": 120, "ep_engine": 120,
+    SECTION_COST_S = {"collectives": 20, "graph_collectives": 15, "tp": 40, "ep": 40, "p2p": 15, "tp_engine": 120, "ep_engine": 120,
                       "disagg_8b": 90}
 
     def section_fits(self, name: str, t_sections: float, deadline: float, cap: float) -> str:
@@ -375,6 +435,7 @@ class Probe:
         # cheapest and most informative first: a run short of time still measures the collectives
         # and the sharded-vs-unsharded parity before the engine-sized sections
         sections = [("collectives", self.collectives),
+                    ("graph_collectives", self.graph_collectives),
                     ("tp", lambda: self.sharded_vs_full(tp_model, "allreduce")),
                     ("ep", lambda: self.sharded_vs_full(ep_model, "a2a")),
                     ("p2p", self.p2p),

@@ -13,3 +13,4 @@ tail -c 700 gpurun_out/mt/bench_table.json
 MX="--model mistralai/Mixtral-8x7B-Instruct-v0.1 --qps 4 --max-num-seqs 128 --iters-per-step 50 --steps 10 --warmup 3"
 MXS_TUNED_SAVE=1 MXS_TUNED_DIR=gpurun_out/tuned timeout -k 10 420 python3 bench.py $MX --itl-target-ms 40 > gpurun_out/mt/mixtral_t40.json 2> gpurun_out/mt/mixtral_t40.err || exit 1
 tail -c 1200 gpurun_out/mt/mixtral_t40.json
+timeout -k 10 600 python -u -m pytest tests/test_c_tp8_gpu.py tests/test_mgpu_probe_gpu.py tests/test_kernels_gpu.py -x -v --timeout 300 --timeout-method thread -k "ep8_moe_layer or probe_two_ranks or moe_a2a_dispatch" > gpurun_out/mt/ep_tests.log 2>&1; rc=$?; tail -8 gpurun_out/mt/ep_tests.log; [ $rc -eq 0 ] || exit $rc

@@ -115,3 +115,34 @@ def test_killed_launcher_leaves_no_process(tmp_path, victim):
                 os.kill(q, signal.SIGKILL)
             except OSError:
                 pass
+
+
+def _ns(**kw):
+    import argparse
+    d = dict(model="meta-llama/Llama-3.2-1B-Instruct", isl=4000, osl=500, qps=42.0, disagg_qps=0.0,
+             disagg_prefill_ranks=0)
+    d.update(kw)
+    return argparse.Namespace(**d)
+
+
+def test_disagg_plan_like_for_like():
+    """The disagg phase runs at the agg phase's arrival rate whenever its P:D split can carry it
+    (3P+5D on 8 GPUs), and falls back to the capacity rate when it cannot (1P+1D on 2 GPUs)."""
+    import bench
+    p, d, q = bench.disagg_plan(_ns(), 8)
+    assert (p, d) == (3, 5) and q == 42.0
+    p, d, q = bench.disagg_plan(_ns(), 2)
+    assert (p, d) == (1, 1) and q < 42.0
+    assert bench.disagg_plan(_ns(disagg_qps=-1), 8)[2] < 42.0
+    assert bench.disagg_plan(_ns(disagg_qps=30.0), 8)[2] == 30.0
+
+
+def test_compare_modes_marks_winners():
+    import bench
+    agg = {"value": 20000.0, "ttft_p50_ms": 35.0, "ttft_p90_ms": 60.0, "itl_p50_ms": 9.0, "itl_p90_ms": 22.0}
+    dis = {"value": 19800.0, "ttft_p50_ms": 50.0, "ttft_p90_ms": 80.0, "itl_p50_ms": 12.0, "itl_p90_ms": 13.0,
+           "qps_per_gpu": 42.0}
+    c = bench.compare_modes(agg, dis, 42.0)
+    assert c["like_for_like"] is True
+    assert c["value"]["better"] == "agg" and c["itl_p90_ms"]["better"] == "disagg"
+    assert c["ttft_p50_ms"]["better"] == "agg"

@@ -120,6 +120,110 @@ def test_tp8_shapes_on_one_gpu_match_tp1(model, moe_dispatch):
         assert (got.argmax(-1) == ref.argmax(-1)).float().mean().item() > 0.9
 
 
+def _ep_rank(rank, world, port, q, T):
+    """One EP rank of a Mixtral-shaped MoE layer (H 4096, I 14336, 8 experts, top-2): this rank owns
+    expert `rank`; the reference (rank 0) recomputes every slice's routing with the very same router
+    call the rank made (same rows, same kernel), so routing is identical by construction and the only
+    differences left are bf16 expert GEMMs vs an fp32 reference."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        os.environ.pop("MXS_CUSTOM_AR", None)
+        import torch
+        import torch.nn.functional as F
+        torch.cuda.set_device(0)
+        from mxserve import ops
+        from mxserve.parallel import comm
+        from mxserve.parallel.expert import moe_a2a
+        st = comm.init_distributed(world, backend="gloo", device=torch.device("cuda:0"))
+        assert st.custom_ar is not None
+        H, I, E, K = 4096, 14336, 8, 2
+        g = torch.Generator(device="cuda:0").manual_seed(11)
+        x = (torch.randn(T, H, device="cuda:0", generator=g) * 0.5).to(torch.bfloat16)
+        gate = (torch.randn(E, H, device="cuda:0", generator=g) * H ** -0.5).to(torch.bfloat16)
+
+        def expert(e):
+            ge = torch.Generator(device="cuda:0").manual_seed(100 + e)
+            w13 = (torch.randn(2 * I, H, device="cuda:0", generator=ge) * H ** -0.5).to(torch.bfloat16)
+            w2 = (torch.randn(H, I, device="cuda:0", generator=ge) * I ** -0.5).to(torch.bfloat16)
+            return w13, w2
+
+        w13, w2 = expert(rank)
+        with torch.inference_mode():
+            got = moe_a2a(x, gate, w13.unsqueeze(0).contiguous(), w2.unsqueeze(0).contiguous(), K, rank, world,
+                          st.group)
+        torch.cuda.synchronize()
+        assert st.custom_ar.check(), "custom all-reduce timed out"
+        ref = None
+        if rank == 0:
+            S = (T + world - 1) // world
+            tws, tids = [], []
+            with torch.inference_mode():
+                for r in range(world):  # the router exactly as each rank ran it on its padded slice
+                    lo, hi = min(T, r * S), min(T, r * S + S)
+                    hs = torch.zeros(S, H, dtype=x.dtype, device=x.device)
+                    hs[:hi - lo] = x[lo:hi]
+                    tw, tid = ops.moe_topk_softmax(F.linear(hs, gate), K)
+                    tws.append(tw[:hi - lo].float())
+                    tids.append(tid[:hi - lo].long())
+                tw, tid = torch.cat(tws), torch.cat(tids)
+                ref = torch.zeros(T, H, device=x.device)
+                xf = x.float()
+                for e in range(E):
+                    rows, j = (tid == e).nonzero(as_tuple=True)
+                    if rows.numel() == 0:
+                        continue
+                    a, b = expert(e)
+                    hgu = xf[rows] @ a.float().t()
+                    act = F.silu(hgu[:, :I]) * hgu[:, I:]
+                    ref.index_add_(0, rows, (act @ b.float().t()) * tw[rows, j].unsqueeze(1))
+                ref = ref.cpu().numpy()
+        torch.distributed.barrier()
+        q.put((rank, got.float().cpu().numpy(), ref, None))
+    except BaseException:  # noqa: BLE001
+        q.put((rank, None, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("T", [600, 6000])
+def test_ep8_moe_layer_identical_routing(T):
+    """Mixtral EP = 8 MoE layer (8 ranks on GPU 0, device-side IPC dispatch): with routing identical
+    by construction every row must match the fp32 reference within bf16 GEMM error -- no row may be
+    off (a misrouted row is off by O(1)).  T = 6000 puts 750 tokens in each rank's slice: two
+    slot-sized dispatch chunks (the prefill path above 4,096 tokens)."""
+    import numpy as np
+    import torch
+    if torch.cuda.is_initialized():
+        pytest.skip("HIP already initialised in the test process")
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_ep_rank, args=(r, world, port, q, T)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        res = {}
+        for _ in range(world):
+            r, g, ref, err = q.get(timeout=300)
+            res[r] = (g, ref, err)
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert res[r][2] is None, res[r][2]
+    ref = res[0][1]
+    scale = np.abs(ref).max()
+    for r in range(world):
+        got = res[r][0]
+        assert got.shape == ref.shape
+        row_err = np.abs(got - ref).max(-1)
+        assert row_err.max() < 0.02 * scale, (r, float(row_err.max() / scale), int(row_err.argmax()))
+
+
 _ENGINE_SCRIPT = r"""
 import json, os, sys
 sys.path.insert(0, os.environ["MXS_ROOT"])

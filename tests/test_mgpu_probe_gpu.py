@@ -25,7 +25,7 @@ def test_probe_two_ranks_on_one_gpu(tmp_path):
     for r in range(2):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
                    WORLD_SIZE="2", PYTHONPATH=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0",
-                   MXS_PROBE_SECTIONS="collectives,tp,ep")
+                   MXS_PROBE_SECTIONS="collectives,graph_collectives,tp,ep")
         procs.append(subprocess.Popen([sys.executable, "-m", "mxserve.tools.mgpu_probe"], stdin=subprocess.PIPE,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, cwd=ROOT))
     outs = []
@@ -47,6 +47,11 @@ def test_probe_two_ranks_on_one_gpu(tmp_path):
     assert d["status"] == "ok" and d["shared_gpu"] and d["backend"] == "gloo", d
     car = d["collectives"]["custom_all_reduce"]
     assert car and all(c["correct"] for c in car), car
+    # gloo group: the 1 MiB logits all-gather is captured through the IPC all-to-all; the 16 MiB cases
+    # need RCCL (an 8-GPU node) and are reported as skipped here
+    gc = {(c["op"], c["bytes"]): c for c in d["graph_collectives"]["cases"]}
+    assert gc[("all_gather", 1 << 20)]["correct"] and gc[("all_gather", 1 << 20)]["path"] == "ipc", gc
+    assert "skipped" in gc[("all_reduce", 16 << 20)], gc
     for sec in ("tp", "ep"):
         r = d[sec]
         assert r["custom_all_reduce"] and r["custom_all_reduce_healthy"] and r["ranks_consistent"], r
