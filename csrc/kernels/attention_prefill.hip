@@ -375,14 +375,21 @@ __global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
     for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
   float m = -INFINITY, l = 0.f;
 
+  // Scores are accumulated relative to the running max: the QK^T accumulator starts at -m (the
+  // row's max so far), so exp2 reads the MFMA output directly and the per-element subtraction is
+  // gone from the VALU stream (at D = 64 the softmax VALU, not the MFMA pipe, bounds a tile).  The
+  // first tile of a row starts at 0 and sets m from its own max; later tiles only move m (lazy
+  // rescale) when their max exceeds it by more than 2^8.
   auto compute = [&](int buf, int k0) {
     const char* kl = lds[buf];
     const char* vl = lds[buf] + KBYTES;
+    const bool first = k0 == 0;
+    const float off = first ? 0.f : -m;
     float16_ sacc[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[kt][i] = 0.f;
+      for (int i = 0; i < 16; ++i) sacc[kt][i] = off;
       const int key = kt * 32 + c;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -399,22 +406,32 @@ __global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
           if (kk > qpos) sacc[kt][i] = -INFINITY;
         }
     }
-    float mx = sacc[0][0];
+    float mx = sacc[0][0];  // relative to m (absolute on the first tile)
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[kt][i]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const bool bump = mx > m + 8.f;  // lazy rescale, as in v2
+    // first tile: m := its max; later: lazy rescale when the tile raises the max by more than 2^8.
+    // Both halves of a row see the same mx, hence the same decision.
+    const bool bump = first || mx > 8.f;
     if (__ballot(bump)) {
-      const float mn = bump ? mx : m;
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);
-      m = mn;
-      l *= alpha;
+      const float d = bump ? mx : 0.f;  // how far m moves (relative)
+      if (!first) {
+        const float alpha = __builtin_amdgcn_exp2f(-d);
+        l *= alpha;
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
+        for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+          for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+        m += d;
+      } else {
+        m = d;
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[kt][i] -= d;
     }
     float ps = 0.f;
     bf16x8_t pf[2][2];
@@ -422,7 +439,7 @@ __global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(sacc[kt][i] - m);
+        const float p = __builtin_amdgcn_exp2f(sacc[kt][i]);
         ps += p;
         pf[kt][i >> 3][i & 7] = static_cast<__bf16>(p);
       }

@@ -31,9 +31,13 @@ void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStre
 void launch_moe_align(int*, int*, const int*, int, int, int, int*, hipStream_t);
 void launch_moe_combine(bf16_t*, const bf16_t*, const float*, const int*, int, int, int, hipStream_t);
 bool launch_decode_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int,
-                        int, hipStream_t, const int* = nullptr, int = 0, int = 0, int = 0);
+                        int, hipStream_t, const int* = nullptr, int = 0, int = 0, int = 0, int = 1);
 bool launch_mt_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int, int,
-                    int, hipStream_t, int*, int);
+                    int, hipStream_t, int*, int, int = 0, int = 1);
+void launch_splitk_add_rms_norm(bf16_t*, bf16_t*, const float*, int, int, int, const bf16_t*, float, hipStream_t);
+bool launch_splitk_rope_and_cache(bf16_t*, const float*, int, const int64_t*, const float*, void*, bool, long,
+                                  const int64_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, float, float,
+                                  float, hipStream_t);
 bool launch_prefill_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int,
                          hipStream_t);
 bool launch_gemm_big(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, hipStream_t);
@@ -64,6 +68,18 @@ void rms_norm(at::Tensor out, at::Tensor x, at::Tensor w, double eps) {
   const int rows = x.numel() / H;
   const int x_stride = x.dim() >= 2 ? x.stride(-2) : H;
   mxs::launch_rms_norm(bf(out), bf(x), bf(w), rows, H, x_stride, static_cast<float>(eps), stream());
+}
+
+// Split-K slabs [S][M][H] of a residual-stream projection -> residual += their sum (bf16-rounded),
+// out = RMSNorm(residual) * w (norm_act.hip splitk_add_rmsnorm_kernel).
+void splitk_add_rms_norm(at::Tensor out, at::Tensor residual, at::Tensor part, int64_t S, at::Tensor w, double eps) {
+  CHECK_CUDA(out); CHECK_BF16(out); CHECK_BF16(residual); CHECK_BF16(w); CHECK_CONTIG(out); CHECK_CONTIG(residual);
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous(), "part: fp32 CUDA slabs");
+  const int64_t H = residual.size(-1), M = residual.numel() / H;
+  TORCH_CHECK(out.numel() == M * H && w.numel() == H && H % 8 == 0, "shape mismatch");
+  TORCH_CHECK(S >= 1 && part.numel() >= S * M * H, "part holds fewer than S slabs of [M, H]");
+  mxs::launch_splitk_add_rms_norm(bf(out), bf(residual), part.data_ptr<float>(), static_cast<int>(S),
+                                  static_cast<int>(M), static_cast<int>(H), bf(w), static_cast<float>(eps), stream());
 }
 
 void fused_add_rms_norm(at::Tensor out, at::Tensor x, at::Tensor residual, at::Tensor w, double eps) {
@@ -119,6 +135,27 @@ void rope_and_cache(at::Tensor q_out, at::Tensor qkv, at::Tensor positions, at::
                              kv.data_ptr(), fp8, kv.stride(0), slot_mapping.data_ptr<int64_t>(), qnp, knp, qkv.size(0),
                              Hq, Hkv, D, 16, static_cast<float>(eps), static_cast<float>(k_scale),
                              static_cast<float>(v_scale), stream());
+}
+
+// rope_and_cache reading the qkv row from S unreduced fp32 split-K slabs [S][T][(Hq + 2 Hkv) D]
+bool splitk_rope_and_cache(at::Tensor q_out, at::Tensor part, int64_t S, int64_t T, at::Tensor positions,
+                           at::Tensor cos_sin, at::Tensor kv, at::Tensor slot_mapping, std::optional<at::Tensor> qn,
+                           std::optional<at::Tensor> kn, int64_t Hq, int64_t Hkv, int64_t D, double eps, double k_scale,
+                           double v_scale) {
+  CHECK_CUDA(part); CHECK_CONTIG(q_out);
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous(), "part: fp32 slabs");
+  TORCH_CHECK(part.numel() >= S * T * (Hq + 2 * Hkv) * D, "part holds fewer than S slabs of [T, qkv]");
+  TORCH_CHECK(positions.scalar_type() == at::kLong && slot_mapping.scalar_type() == at::kLong, "int64 indices");
+  TORCH_CHECK(positions.numel() >= T && slot_mapping.numel() >= T && q_out.numel() == T * Hq * D, "shape mismatch");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == D, "cos_sin must be fp32 [P, D]");
+  const bool fp8 = check_kv(kv, Hkv, D);
+  const bf16_t* qnp = qn.has_value() ? bf(*qn) : nullptr;
+  const bf16_t* knp = kn.has_value() ? bf(*kn) : nullptr;
+  return mxs::launch_splitk_rope_and_cache(bf(q_out), part.data_ptr<float>(), static_cast<int>(S),
+                                           positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(), kv.data_ptr(), fp8,
+                                           kv.stride(0), slot_mapping.data_ptr<int64_t>(), qnp, knp,
+                                           static_cast<int>(T), Hq, Hkv, D, 16, static_cast<float>(eps),
+                                           static_cast<float>(k_scale), static_cast<float>(v_scale), stream());
 }
 
 void paged_attention_decode(at::Tensor out, at::Tensor q, at::Tensor kv, at::Tensor block_tables,
@@ -223,7 +260,7 @@ void apply_penalties(at::Tensor logits, at::Tensor hist, at::Tensor srows, at::T
 // fp32 split-K workspace (>= splitk * M * N floats) when splitk > 1.  False if the configuration
 // does not tile the shape (the caller keeps hipBLASLt).
 bool decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> part, int64_t mf, int64_t nf,
-                 int64_t wm, int64_t splitk, int64_t epi, int64_t lu) {
+                 int64_t wm, int64_t splitk, int64_t epi, int64_t lu, bool reduce) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
   const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
@@ -237,7 +274,7 @@ bool decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::T
     p = part->data_ptr<float>();
   }
   return mxs::launch_decode_gemm(bf(out), p, bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), mf, nf, wm, splitk,
-                                 epi, stream(), nullptr, 0, 0, lu);
+                                 epi, stream(), nullptr, 0, 0, lu, reduce ? 1 : 0);
 }
 
 // Medium-M form of the decode projection (gemm_decode.hip mt_gemm_kernel, M = 64-256 and short
@@ -245,7 +282,8 @@ bool decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::T
 // as decode_gemm; with `cnt` (int32 tile counters, zeroed once, left zero by every launch) the split-K
 // slabs are summed inside the launch.  False if the configuration does not tile the shape.
 bool mt_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> part, int64_t wm, int64_t wn,
-             int64_t mr, int64_t wnf, int64_t splitk, int64_t epi, c10::optional<at::Tensor> cnt) {
+             int64_t mr, int64_t wnf, int64_t splitk, int64_t epi, c10::optional<at::Tensor> cnt, int64_t order,
+             bool reduce) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
   const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
@@ -266,7 +304,7 @@ bool mt_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tenso
     clen = static_cast<int>(std::min<int64_t>(cnt->numel(), 1 << 30));
   }
   return mxs::launch_mt_gemm(bf(out), p, bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), wm, wn, mr, wnf, splitk,
-                             epi, stream(), c, clen);
+                             epi, stream(), c, clen, static_cast<int>(order), reduce ? 1 : 0);
 }
 
 // K05-K08 at prefill sizes (csrc/kernels/gemm_prefill.hip): out [M, N] = x [M, K] . w [N, K]^T.
@@ -384,6 +422,8 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "mxserve gfx950 HIP kernels";
   m.def("rms_norm", &rms_norm);
   m.def("fused_add_rms_norm", &fused_add_rms_norm);
+  m.def("splitk_add_rms_norm", &splitk_add_rms_norm);
+  m.def("splitk_rope_and_cache", &splitk_rope_and_cache);
   m.def("silu_mul", &silu_mul);
   m.def("embed_rms_norm", &embed_rms_norm);
   m.def("rope_and_cache", &rope_and_cache, pybind11::arg("q_out"), pybind11::arg("qkv"), pybind11::arg("positions"),
@@ -407,10 +447,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_combine", &moe_combine);
   m.def("decode_gemm", &decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("part"), pybind11::arg("mf"), pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"),
-        pybind11::arg("epi"), pybind11::arg("lu") = 0);
+        pybind11::arg("epi"), pybind11::arg("lu") = 0, pybind11::arg("reduce") = true);
   m.def("mt_gemm", &mt_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("part"),
         pybind11::arg("wm"), pybind11::arg("wn"), pybind11::arg("mr"), pybind11::arg("wnf"), pybind11::arg("splitk"),
-        pybind11::arg("epi"), pybind11::arg("cnt") = pybind11::none());
+        pybind11::arg("epi"), pybind11::arg("cnt") = pybind11::none(), pybind11::arg("order") = 0,
+        pybind11::arg("reduce") = true);
   m.def("prefill_gemm", &prefill_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("part"), pybind11::arg("bm"), pybind11::arg("splitk"));
   m.def("gemm_big", &gemm_big, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("epi"),

@@ -351,7 +351,7 @@ __global__ void __launch_bounds__(WM* WN * 64) mt_gemm_kernel(bf16_t* __restrict
                                                               const bf16_t* __restrict__ X,
                                                               const bf16_t* __restrict__ W, int M, int N, int K,
                                                               int ldx, int ldy, int kslice, int inter, int ntm,
-                                                              int ntn, int* __restrict__ cnt) {
+                                                              int ntn, int* __restrict__ cnt, int order) {
   constexpr int NW = WM * WN;
   constexpr int BM = 32 * MR * WM, BN = 32 * WNF * WN;  // X rows / W rows of a stage image
   constexpr int ROWS = BN + BM, STAGE = ROWS * 128;
@@ -365,7 +365,10 @@ __global__ void __launch_bounds__(WM* WN * 64) mt_gemm_kernel(bf16_t* __restrict
 
   const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tn = wg % ntn, tm = (wg / ntn) % ntm, z = wg / (ntn * ntm);
+  // order 0: column tiles fastest; 1: row tiles fastest, so the row tiles sharing a weight slice run
+  // back to back on one XCD and the slice is read from HBM once (its second read hits that L2)
+  const int tn = order ? (wg / ntm) % ntn : wg % ntn, tm = order ? wg % ntm : (wg / ntn) % ntm;
+  const int z = wg / (ntn * ntm);
   const int m0 = tm * BM, c0 = tn * OUTB, kbeg = z * kslice;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -540,7 +543,8 @@ __global__ void __launch_bounds__(WM* WN * 64) mt_gemm_kernel(bf16_t* __restrict
 // With a tile-counter array `cnt` (>= tiles ints, zero on first use; every launch leaves it zero) the
 // split-K slabs are summed inside the launch, else by splitk_reduce_kernel.
 bool launch_mt_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx, int ldy,
-                    int wm, int wn, int mr, int wnf, int splitk, int epi, hipStream_t s, int* cnt, int cnt_len) {
+                    int wm, int wn, int mr, int wnf, int splitk, int epi, hipStream_t s, int* cnt, int cnt_len,
+                    int order, int reduce) {
   if (M <= 0 || splitk < 1 || K % (64 * splitk) != 0 || ldx % 8 != 0 || ldy % 4 != 0) return false;
   if (epi == EPI_SILU && (N % 2 != 0 || wnf % 2 != 0)) return false;
   if (splitk > 1 && part == nullptr) return false;
@@ -552,13 +556,13 @@ bool launch_mt_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, in
   const long nwg = static_cast<long>(ntm) * ntn * splitk;
   if (nwg > (1L << 30)) return false;
   float* p = splitk > 1 ? part : nullptr;
-  int* cnt_ = splitk > 1 && cnt != nullptr && cnt_len >= ntm * ntn ? cnt : nullptr;
+  int* cnt_ = splitk > 1 && reduce && cnt != nullptr && cnt_len >= ntm * ntn ? cnt : nullptr;
   const int kslice = K / splitk;
   bool launched = false;
 #define MXS_MT(a, b, c, d, e)                                                                                  \
   if (!launched && wm == a && wn == b && mr == c && wnf == d && epi == e) {                                   \
     hipLaunchKernelGGL((mt_gemm_kernel<a, b, c, d, e>), dim3(nwg), dim3(a * b * 64), 0, s, Y, p, X, W, M, N, K, \
-                       ldx, ldy, kslice, N / 2, ntm, ntn, cnt_);                                              \
+                       ldx, ldy, kslice, N / 2, ntm, ntn, cnt_, order);                                       \
     launched = true;                                                                                          \
   }
 #define MXS_MT_E(a, b, c, d) MXS_MT(a, b, c, d, EPI_NONE) MXS_MT(a, b, c, d, EPI_SILU)
@@ -569,7 +573,7 @@ bool launch_mt_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, in
 #undef MXS_MT
   if (!launched) return false;
   MXS_CHECK_LAUNCH();
-  if (splitk > 1 && cnt_ == nullptr) {
+  if (splitk > 1 && cnt_ == nullptr && reduce) {  // !reduce: the caller's epilogue kernel sums the slabs
     const long total4 = static_cast<long>(M) * outN / 4;
     const int blocks = static_cast<int>(std::min<long>((total4 + 255) / 256, 1024));
     if (epi == EPI_SILU)
@@ -589,7 +593,7 @@ bool launch_mt_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, in
 // most rows one expert can get (T tokens: an expert appears at most once in a token's top-k).
 bool launch_decode_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx,
                         int ldy, int MF, int NF, int WM, int splitk, int epi, hipStream_t s, const int* offs,
-                        int E, int rows_max, int LU) {
+                        int E, int rows_max, int LU, int reduce) {
   if (LU > 0) WM = 1;  // LDS form: 4 waves side by side over N
   const int WN = 4 / WM;
   if (M <= 0 || splitk < 1 || ldx % 8 != 0 || ldy % 4 != 0) return false;
@@ -638,7 +642,7 @@ bool launch_decode_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W
 #undef MXS_DG
   if (!launched) return false;
   MXS_CHECK_LAUNCH();
-  if (splitk > 1 && offs == nullptr) {  // grouped: the MoE combine / silu_mul_partials kernels sum the slabs
+  if (splitk > 1 && offs == nullptr && reduce) {  // grouped: the MoE combine / silu_mul_partials kernels sum the slabs
     const long total4 = static_cast<long>(M) * outN / 4;
     const int blocks = static_cast<int>(std::min<long>((total4 + 255) / 256, 1024));
     if (epi == EPI_SILU)

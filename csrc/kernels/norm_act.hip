@@ -103,6 +103,91 @@ void launch_fused_add_rms_norm(bf16_t* out, const bf16_t* x, bf16_t* residual, c
   launch_rmsnorm_t<true>(out, x, residual, w, rows, H, H, eps, s);
 }
 
+// Split-K epilogue of a projection that feeds the residual stream (o_proj, down_proj at TP = 1):
+// y = sum of the S fp32 slabs [S][M][N] the GEMM left (gemm_decode.hip, reduce skipped), rounded to
+// bf16 as the GEMM's own output would be; residual += y (in place); out = RMSNorm(residual) * w.
+// One launch instead of the split-K reduce kernel plus the fused add + RMSNorm kernel, and the
+// projection output never makes a bf16 round trip through memory.  One workgroup per row, the row
+// in registers between the reduction and the scaled write.
+template <int NV>
+__global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(bf16_t* __restrict__ out, bf16_t* __restrict__ residual,
+                                                                  const float* __restrict__ part, int S, int M,
+                                                                  int H, const bf16_t* __restrict__ w, float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  bf16_t* rr = residual + static_cast<size_t>(row) * H;
+  const int nvec = H >> 3;
+  const size_t slab = static_cast<size_t>(M) * H;
+  uint4 v[NV];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nvec) {
+      const float* p = part + static_cast<size_t>(row) * H + c * 8;
+      float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+      for (int s = 1; s < S; ++s) {
+        const float4 a2 = *reinterpret_cast<const float4*>(p + s * slab);
+        const float4 b2 = *reinterpret_cast<const float4*>(p + s * slab + 4);
+        a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
+        b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
+      }
+      const float y[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      const uint4 rv = *reinterpret_cast<const uint4*>(rr + c * 8);
+      const uint32_t* pr = reinterpret_cast<const uint32_t*>(&rv);
+      uint4 o;
+      uint32_t* po = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)  // bf16(y) + residual, rounded as the unfused path rounds it
+        po[k] = pack2(bf2f(f2bf(y[2 * k])) + bf2f_lo(pr[k]), bf2f(f2bf(y[2 * k + 1])) + bf2f_hi(pr[k]));
+      *reinterpret_cast<uint4*>(rr + c * 8) = o;
+      v[i] = o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float lo = bf2f_lo(po[k]), hi = bf2f_hi(po[k]);
+        ss += lo * lo + hi * hi;
+      }
+    }
+  }
+  const float inv = rsqrtf(block_sum(ss, scratch) / static_cast<float>(H) + eps);
+  bf16_t* orow = out + static_cast<size_t>(row) * H;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nvec) {
+      const uint4 wv = *reinterpret_cast<const uint4*>(w + c * 8);
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(&v[i]);
+      const uint32_t* pw = reinterpret_cast<const uint32_t*>(&wv);
+      uint4 o;
+      uint32_t* po = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        po[k] = pack2(bf2f_lo(p[k]) * inv * bf2f_lo(pw[k]), bf2f_hi(p[k]) * inv * bf2f_hi(pw[k]));
+      *reinterpret_cast<uint4*>(orow + c * 8) = o;
+    }
+  }
+}
+
+void launch_splitk_add_rms_norm(bf16_t* out, bf16_t* residual, const float* part, int S, int M, int H, const bf16_t* w,
+                                float eps, hipStream_t s) {
+  if (M == 0) return;
+  const int nvec = H / 8;
+  const int threads = nvec <= 1024 ? ((nvec + 63) / 64) * 64 : 1024;
+  const int nv = (nvec + threads - 1) / threads;
+#define MXS_SKR(NVV)                                                                                        \
+  hipLaunchKernelGGL((splitk_add_rmsnorm_kernel<NVV>), dim3(M), dim3(threads), 0, s, out, residual, part, S, M, \
+                     H, w, eps)
+  switch (nv) {
+    case 1: MXS_SKR(1); break;
+    case 2: MXS_SKR(2); break;
+    case 3: MXS_SKR(3); break;
+    case 4: MXS_SKR(4); break;
+    default: MXS_SKR(8); break;
+  }
+#undef MXS_SKR
+  MXS_CHECK_LAUNCH();
+}
+
 // out[t, i] = silu(gu[t, i]) * gu[t, I + i]; 8 elements per thread, grid-stride.
 __global__ void silu_mul_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ gu, int rows, int I) {
   const int vec_per_row = I >> 3;

@@ -9,16 +9,39 @@
 
 namespace mxs {
 
-template <int D, bool QKNORM, typename KT>
+// Source of the fused QKV row: the projection's bf16 output, or (SLABS) the S fp32 split-K slabs
+// [S][T][row_stride] a decode GEMM left unreduced, summed here and rounded to bf16 as the GEMM's own
+// output would be -- the reduce kernel and the bf16 round trip of the qkv row disappear.
+template <bool SLABS>
+struct QkvRow {
+  const bf16_t* row;
+  const float* prow;
+  int S;
+  size_t slab;
+  __device__ __forceinline__ float operator[](int j) const {
+    if constexpr (SLABS) {
+      float a = prow[j];
+      for (int s = 1; s < S; ++s) a += prow[s * slab + j];
+      return bf2f(f2bf(a));
+    } else {
+      return bf2f(row[j]);
+    }
+  }
+};
+
+template <int D, bool QKNORM, typename KT, bool SLABS = false>
 __global__ void __launch_bounds__(256) rope_cache_kernel(
     bf16_t* __restrict__ q_out, const bf16_t* __restrict__ qkv, const int64_t* __restrict__ positions,
     const float* __restrict__ cos_sin, KT* __restrict__ kv, long block_stride,
     const int64_t* __restrict__ slot_mapping, const bf16_t* __restrict__ qn, const bf16_t* __restrict__ kn,
-    int Hq, int Hkv, int BS, float eps, float k_inv_scale, float v_inv_scale) {
+    int Hq, int Hkv, int BS, float eps, float k_inv_scale, float v_inv_scale, const float* __restrict__ part = nullptr,
+    int S = 1, int T = 0) {
   constexpr int HALF = D / 2;
   const int t = blockIdx.x;
   const int row_stride = (Hq + 2 * Hkv) * D;
-  const bf16_t* src = qkv + static_cast<size_t>(t) * row_stride;
+  QkvRow<SLABS> src{qkv + static_cast<size_t>(t) * row_stride,
+                    SLABS ? part + static_cast<size_t>(t) * row_stride : nullptr, S,
+                    static_cast<size_t>(T) * row_stride};
   const long pos = positions[t];
   const long slot = slot_mapping[t];
   const float* cs = cos_sin + pos * D;
@@ -37,8 +60,8 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
     const int p = i % HALF;
     float x1 = 0.f, x2 = 0.f;
     if (active) {
-      x1 = bf2f(src[head * D + p]);
-      x2 = bf2f(src[head * D + p + HALF]);
+      x1 = src[head * D + p];
+      x2 = src[head * D + p + HALF];
     }
     if (QKNORM) {
       float ss = x1 * x1 + x2 * x2;
@@ -67,15 +90,15 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
   }
   if (!kblk) return;
   // V: copy into the dim-major half of the block
-  const bf16_t* vsrc = src + (Hq + Hkv) * D;
+  const int v0 = (Hq + Hkv) * D;
   KT* vblk = kblk + static_cast<size_t>(Hkv) * BS * D;
   for (int j = threadIdx.x; j < Hkv * D; j += blockDim.x) {
     const int h = j / D, d = j % D;
     KT* dst = vblk + (static_cast<size_t>(h) * D + d) * BS + off;
-    if constexpr (sizeof(KT) == 2)
-      *dst = vsrc[j];  // bf16 -> bf16: bit copy
+    if constexpr (sizeof(KT) == 2 && !SLABS)
+      *dst = src.row[v0 + j];  // bf16 -> bf16: bit copy
     else
-      kv_store(dst, bf2f(vsrc[j]), v_inv_scale);
+      kv_store(dst, src[v0 + j], v_inv_scale);
   }
 }
 
@@ -219,6 +242,44 @@ static void launch_rope_typed(bf16_t* q_out, const bf16_t* qkv, const int64_t* p
   MXS_ROPE_CASE(128)
   MXS_ROPE_CASE(32)
 #undef MXS_ROPE_CASE
+}
+
+template <typename KT>
+static void launch_rope_slabs_typed(bf16_t* q_out, const float* part, int S, const int64_t* positions,
+                                    const float* cos_sin, KT* kv, long block_stride, const int64_t* slot_mapping,
+                                    const bf16_t* qn, const bf16_t* kn, int T, int Hq, int Hkv, int D, int BS, float eps,
+                                    float kis, float vis, hipStream_t s) {
+  dim3 g(T), b(256);
+#define MXS_ROPE_SLAB(DD)                                                                                      \
+  if (D == DD) {                                                                                               \
+    if (qn != nullptr)                                                                                         \
+      hipLaunchKernelGGL((rope_cache_kernel<DD, true, KT, true>), g, b, 0, s, q_out, nullptr, positions, cos_sin, \
+                         kv, block_stride, slot_mapping, qn, kn, Hq, Hkv, BS, eps, kis, vis, part, S, T);        \
+    else                                                                                                       \
+      hipLaunchKernelGGL((rope_cache_kernel<DD, false, KT, true>), g, b, 0, s, q_out, nullptr, positions,       \
+                         cos_sin, kv, block_stride, slot_mapping, qn, kn, Hq, Hkv, BS, eps, kis, vis, part, S, T); \
+    MXS_CHECK_LAUNCH();                                                                                        \
+    return;                                                                                                    \
+  }
+  MXS_ROPE_SLAB(64)
+  MXS_ROPE_SLAB(128)
+#undef MXS_ROPE_SLAB
+}
+
+// rope_and_cache from the unreduced split-K slabs of the qkv projection (decode batches)
+bool launch_splitk_rope_and_cache(bf16_t* q_out, const float* part, int S, const int64_t* positions,
+                                  const float* cos_sin, void* kv, bool kv_fp8, long block_stride,
+                                  const int64_t* slot_mapping, const bf16_t* qn, const bf16_t* kn, int T, int Hq,
+                                  int Hkv, int D, int BS, float eps, float k_scale, float v_scale, hipStream_t s) {
+  if (T == 0) return true;
+  if (D != 64 && D != 128) return false;
+  if (kv_fp8)
+    launch_rope_slabs_typed(q_out, part, S, positions, cos_sin, static_cast<fp8_t*>(kv), block_stride, slot_mapping,
+                            qn, kn, T, Hq, Hkv, D, BS, eps, 1.f / k_scale, 1.f / v_scale, s);
+  else
+    launch_rope_slabs_typed(q_out, part, S, positions, cos_sin, static_cast<bf16_t*>(kv), block_stride,
+                            slot_mapping, qn, kn, T, Hq, Hkv, D, BS, eps, 1.f, 1.f, s);
+  return true;
 }
 
 // kv_fp8: the cache holds e4m3fn bytes (block_stride in elements = bytes); k/v_scale: stored = x / scale

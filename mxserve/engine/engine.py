@@ -173,6 +173,7 @@ class LLMEngine:
             t1 = time.perf_counter()
             tm["schedule"] += t1 - t0
         handle = None
+        t_begin = time.perf_counter()
         if not so.is_empty:
             if ROCTX.lib is not None:  # MXS_ROCTX=1: named ranges on the rocprofv3 timeline
                 with ROCTX.range(f"step {self.num_steps} d{len(so.decodes)} p{len(so.prefills)}"):
@@ -188,7 +189,7 @@ class LLMEngine:
         done_state = None
         if late is not None:
             if handle is not None:
-                late.launched(so, t_adm, time.perf_counter())
+                late.launched(so, t_adm, time.perf_counter(), t_begin)
             done_state = late.inflight
             late.rotate()
         if self.async_scheduling:
@@ -204,7 +205,7 @@ class LLMEngine:
             sampled = self.runner.collect(dh)
             t_done = done_state.get("done") if done_state else None
             late.observe_done(done_state, t_done if t_done is not None else
-                              (time.perf_counter() if pending else None))
+                              (time.perf_counter() if pending else None), dh.get("gpu_s"))
         else:
             sampled = self.runner.collect(dh)
             if self._budget_model is not None and not self.async_scheduling:

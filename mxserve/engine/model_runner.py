@@ -164,7 +164,11 @@ class ModelRunner:
         self._steps = 0
         if self.is_gpu:
             self._out_pinned = [torch.zeros(n_rows, dtype=torch.int64, pin_memory=True) for _ in range(2)]
-            self._out_events = [torch.cuda.Event(), torch.cuda.Event()]
+            # timing-enabled: with the start events below they give each step's GPU time (engine/pacing.py
+            # fits its step-time model on them; host clocks cannot see when a step's kernels started)
+            self._out_events = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+            self._start_events = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            self._start_slot = 0
         self.graphs: dict[int, tuple] = {}
         if self.is_gpu and not args.enforce_eager:
             self._capture_graphs()
@@ -363,6 +367,11 @@ class ModelRunner:
         if self.graphs and not so.prefills and S <= max(self.graphs):
             gbs = min(x for x in self.graphs if x >= S)
         meta = self._prepare(so, gbs)
+        t0ev = None
+        if self.is_gpu:
+            self._start_slot = (self._start_slot + 1) % len(self._start_events)
+            t0ev = self._start_events[self._start_slot]
+            t0ev.record()
         tp = get_tp()
         if tp.tp_size > 1:
             self._steps += 1
@@ -391,7 +400,7 @@ class ModelRunner:
             pinned.copy_(ids, non_blocking=True)
             ev = self._out_events[self._out_slot]
             ev.record()
-            handle.update(pinned=pinned, ev=ev)
+            handle.update(pinned=pinned, ev=ev, ev0=t0ev)
         else:
             handle["ids"] = ids
         if lp is not None:
@@ -405,6 +414,8 @@ class ModelRunner:
             return {}
         if "ev" in handle:
             handle["ev"].synchronize()
+            if handle.get("ev0") is not None:
+                handle["gpu_s"] = handle["ev0"].elapsed_time(handle["ev"]) * 1e-3
             ids = handle["pinned"].tolist()
         elif "ids" in handle:
             ids = handle["ids"].tolist()
@@ -537,15 +548,20 @@ class ModelRunner:
         # decode projection GEMMs: hand-written MFMA kernel vs hipBLASLt, measured per bucket
         from ..ops import decode_gemm
         w = m.w
-        shapes = {"qkv": (w["l0.qkv"], 0), "o": (w["l0.o"], 0), "lm_head": (m.lm_head_weight(), 0)}
+        # qkv feeds the rope / cache-write kernel (fusable at any TP); o / down feed the residual add +
+        # next RMSNorm (fused at TP = 1, llama.py _forward_fused): the tuner times each with its epilogue
+        fuse = getattr(m, "fuse_residual", False) and m.tp_size == 1
+        norm = ("add_norm",) if fuse else None
+        shapes = {"qkv": (w["l0.qkv"], 0, ("rope", m.nh, m.nkv, m.hd) if self.cfg.head_dim in (64, 128) else None),
+                  "o": (w["l0.o"], 0, norm), "lm_head": (m.lm_head_weight(), 0)}
         if not self.cfg.is_moe:
-            shapes.update(gate_up=(w["l0.gate_up"], 1), down=(w["l0.down"], 0))
+            shapes.update(gate_up=(w["l0.gate_up"], 1), down=(w["l0.down"], 0, norm))
         with torch.inference_mode():
             t0 = time.time()
             self.decode_gemm_report = decode_gemm.tune(shapes, buckets, self.device, self.dtype)
             self.decode_gemm_tune_s = time.time() - t0
             self.prefill_gemm_report = decode_gemm.tune_prefill(
-                {k: v for k, (v, epi) in shapes.items() if epi == 0 and k != "lm_head"}, self.device, self.dtype)
+                {k: v[0] for k, v in shapes.items() if v[1] == 0 and k != "lm_head"}, self.device, self.dtype)
             if self.cfg.is_moe and "l0.w13" in w:  # expert GEMMs at decode batches (local experts)
                 from ..ops import moe as moe_ops
                 self.moe_gemm_report = moe_ops.tune(w["l0.w13"], w["l0.w2"], buckets, self.cfg.num_experts_per_tok,

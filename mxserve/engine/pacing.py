@@ -207,28 +207,36 @@ class LateAdmission:
         self.waits += 1
         self.wait_s += time.perf_counter() - t0
 
-    def launched(self, so, t_admit: float, t_launched: float) -> None:
+    def launched(self, so, t_admit: float, t_launched: float, t_begin: Optional[float] = None) -> None:
+        """t_begin: when the host started enqueueing the step.  Its GPU work starts from then (the first
+        kernels run while the host still enqueues the rest: an eager Mixtral prefill step takes tens of
+        ms to launch), so a step's GPU time is measured from there, not from the end of the launch."""
         self.host_lead = 0.9 * self.host_lead + 0.1 * (t_launched - t_admit)
         x = step_features(so)
         est = self.model.predict(x)
+        t0 = t_launched if t_begin is None else t_begin
         prev = self.inflight
-        start = t_launched
+        start = t0
         if prev is not None and prev.get("est_done") is not None:
             start = max(start, prev["est_done"])
-        self.pending_next = {"x": x, "t_launch": t_launched, "est_done": None if est is None else start + est,
+        self.pending_next = {"x": x, "t_launch": t0, "est_done": None if est is None else start + est,
                              "done": None}
 
     def rotate(self) -> None:
         """The launched step becomes the in-flight one (called once per engine step)."""
         self.inflight, self.pending_next = getattr(self, "pending_next", None), None
 
-    def observe_done(self, st: Optional[dict], t_done: Optional[float]) -> None:
-        """A step completed at t_done (None: not observed precisely).  Its GPU time ran from the
-        later of its launch and the previous step's completion."""
+    def observe_done(self, st: Optional[dict], t_done: Optional[float], gpu_s: Optional[float] = None) -> None:
+        """A step completed at t_done (None: not observed precisely).  gpu_s: its GPU time from the
+        runner's events (start marker -> end marker), which the model then fits on directly;
+        without it the GPU time is taken to run from the later of its launch and the previous
+        step's completion (host clocks: steps whose neighbours' completions were not seen drop out)."""
         if st is None:
             return
+        if gpu_s is not None:
+            self.model.update(st["x"], gpu_s)
         if t_done is not None:
-            if self.last_done is not None:
+            if self.last_done is not None and gpu_s is None:
                 begin = max(st["t_launch"], self.last_done)
                 self.model.update(st["x"], t_done - begin)
             # re-anchor the step now in flight on this observed completion (it was queued behind it)

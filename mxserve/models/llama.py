@@ -66,6 +66,9 @@ class TransformerLM:
         self.moe_dispatch = moe_dispatch
         # last layer of a prefill step: attention/o_proj/MLP only for the rows that produce logits
         self.prune_last_layer = os.environ.get("MXS_PRUNE_LAST_LAYER", "1") == "1"
+        # TP = 1 on the GPU: o_proj / down_proj end in the next RMSNorm (ops.linear_add_rms_norm: a
+        # split-K projection's slabs go straight into one sum + residual add + norm kernel)
+        self.fuse_residual = os.environ.get("MXS_FUSE_RESIDUAL", "1") == "1"
         # fp8 KV cache: stored = x / scale, per layer (1.0 until the runner calibrates them from a
         # probe prefill, mxserve/engine/model_runner.py::_calibrate_kv_scales; MXS_KV_SCALE fixes all)
         ks = float(os.environ.get("MXS_KV_SCALE", "1.0"))
@@ -172,12 +175,11 @@ class TransformerLM:
         return self.w["lm_head"]
 
     # ------------------------------------------------------------------ forward
-    def _attention(self, i: int, h: torch.Tensor, md: AttnMetadata, kv_layer: torch.Tensor):
+    def _attention(self, i: int, h: torch.Tensor, md: AttnMetadata, kv_layer: torch.Tensor, project: bool = True):
         c, w, p = self.cfg, self.w, f"l{i}."
-        qkv = ops.linear(h, w[p + "qkv"])
-        q = ops.rope_and_cache(qkv, self.nh, self.nkv, self.hd, md.positions, self.cos_sin, kv_layer,
-                               md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"), c.rms_norm_eps,
-                               **self.kv_scales[i])
+        q = ops.linear_rope_and_cache(h, w[p + "qkv"], self.nh, self.nkv, self.hd, md.positions, self.cos_sin,
+                                      kv_layer, md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"),
+                                      c.rms_norm_eps, **self.kv_scales[i])
         nd = md.num_decodes
         if not q.is_cuda:
             o = ref.paged_attention(q, kv_layer, md.block_tables, md.query_start_loc, md.seq_lens, self.scale,
@@ -195,19 +197,21 @@ class TransformerLM:
             ops.paged_attention_prefill(q[nd:], kv_layer, md.block_tables[nd:], md.prefill_query_start_loc,
                                         md.seq_lens[nd:], self.scale, md.max_query_len, out=o[nd:],
                                         **self.kv_scales[i])
+        if not project:  # the caller fuses o_proj with the residual add + next norm
+            return o.reshape(o.shape[0], -1)
         out = ops.linear(o.reshape(o.shape[0], -1), w[p + "o"])
         return tp_all_reduce(out)
 
-    def _attention_sampled(self, i: int, h: torch.Tensor, md: AttnMetadata, kv_layer: torch.Tensor):
+    def _attention_sampled(self, i: int, h: torch.Tensor, md: AttnMetadata, kv_layer: torch.Tensor,
+                           project: bool = True):
         """Last layer of a step with prefill chunks: K/V of every token still go to the cache, but
         only the rows that produce logits (the last token of each sampled sequence) need attention,
         o_proj and the MLP.  Each such row is a single query at position seq_len - 1 over its whole
         context, i.e. exactly a decode query, so it runs on the decode kernel."""
         c, w, p = self.cfg, self.w, f"l{i}."
-        qkv = ops.linear(h, w[p + "qkv"])
-        q = ops.rope_and_cache(qkv, self.nh, self.nkv, self.hd, md.positions, self.cos_sin, kv_layer,
-                               md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"), c.rms_norm_eps,
-                               **self.kv_scales[i])
+        q = ops.linear_rope_and_cache(h, w[p + "qkv"], self.nh, self.nkv, self.hd, md.positions, self.cos_sin,
+                                      kv_layer, md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"),
+                                      c.rms_norm_eps, **self.kv_scales[i])
         ns = md.logits_indices.shape[0]
         if ns == 0:  # no sequence samples this step: the layer only wrote K/V
             return h.new_empty((0, h.shape[1]))
@@ -220,6 +224,8 @@ class TransformerLM:
             o = ref.paged_attention(qs, kv_layer, bt, qsl, sl, self.scale, **self.kv_scales[i])
         else:
             o = ops.paged_attention_decode(qs, kv_layer, bt, sl, self.scale, md.max_seq_len, **self.kv_scales[i])
+        if not project:
+            return o.reshape(ns, -1)
         out = ops.linear(o.reshape(ns, -1), w[p + "o"])
         return tp_all_reduce(out)
 
@@ -271,9 +277,11 @@ class TransformerLM:
         c = self.cfg
         # K01: the embedding gather runs inside the first layer's input RMSNorm kernel
         h, residual = ops.embed_rms_norm(input_ids, self.w["embed"], self.w["l0.in_norm"], c.rms_norm_eps)
-        x = None
         # steps with prefill chunks: the last layer only computes the rows that produce logits
         prune = self.prune_last_layer and md.num_prefills > 0 and md.sample_seq is not None
+        if self.fuse_residual and self.tp_size == 1 and h.is_cuda:
+            return self._forward_fused(h, residual, md, kv_cache, prune)
+        x = None
         for i in range(c.num_layers):
             p = f"l{i}."
             if i > 0:
@@ -288,6 +296,32 @@ class TransformerLM:
             h, residual = ops.fused_add_rms_norm(x, residual, self.w[p + "post_norm"], c.rms_norm_eps)
             x = self._mlp(i, h)
         h, _ = ops.fused_add_rms_norm(x, residual, self.w["norm"], c.rms_norm_eps)
+        return h if prune else h.index_select(0, md.logits_indices)
+
+    def _forward_fused(self, h: torch.Tensor, residual: torch.Tensor, md: AttnMetadata, kv_cache: torch.Tensor,
+                       prune: bool) -> torch.Tensor:
+        """TP = 1: every projection that feeds the residual stream ends in the next RMSNorm
+        (ops.linear_add_rms_norm), so a layer is qkv -> rope/cache -> attention -> o+add+norm ->
+        gate_up+SiLU -> down+add+norm(next layer's input norm, or the final norm)."""
+        c, w = self.cfg, self.w
+        eps = c.rms_norm_eps
+        L = c.num_layers
+        for i in range(L):
+            p = f"l{i}."
+            if prune and i == L - 1:
+                o = self._attention_sampled(i, h, md, kv_cache[:, i], project=False)
+                if o.shape[0] == 0:  # no sequence samples this step: the layer only wrote K/V
+                    return o.new_empty((0, h.shape[1]))
+                residual = residual.index_select(0, md.logits_indices)
+            else:
+                o = self._attention(i, h, md, kv_cache[:, i], project=False)
+            h, residual = ops.linear_add_rms_norm(o, w[p + "o"], residual, w[p + "post_norm"], eps)
+            nxt = w[f"l{i + 1}.in_norm"] if i + 1 < L else w["norm"]
+            if c.is_moe:
+                h, residual = ops.fused_add_rms_norm(self._mlp(i, h), residual, nxt, eps)
+            else:
+                h, residual = ops.linear_add_rms_norm(ops.gate_up_silu(h, w[p + "gate_up"]), w[p + "down"], residual,
+                                                      nxt, eps)
         return h if prune else h.index_select(0, md.logits_indices)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:

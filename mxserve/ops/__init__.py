@@ -164,6 +164,25 @@ def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
     return ref.fused_add_rms_norm(x, residual, w, eps)
 
 
+def linear_add_rms_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor,
+                        eps: float):
+    """(RMSNorm(residual + x @ w.T) * norm_w, residual updated in place) for a projection that feeds
+    the residual stream (o_proj, down_proj; TP = 1).  When the decode table runs this projection
+    split-K, the fp32 slabs go straight into one epilogue kernel (sum + add + norm) instead of the
+    split-K reduce kernel, a bf16 output and the fused add + RMSNorm kernel."""
+    if _gpu(x) and x.dim() == 2 and 0 < x.shape[0] <= 256:
+        from .decode_gemm import TABLE
+        M, N = x.shape[0], w.shape[0]
+        cfg = TABLE.lookup(M, N, w.shape[1], 0)
+        if cfg is not None and TABLE.splitk(cfg) > 1:
+            dummy = residual  # [M, N] bf16: the kernel writes no output when the reduce is skipped
+            if TABLE.run(dummy, x, w, cfg, 0, reduce=False):
+                out = torch.empty_like(residual)
+                ext().splitk_add_rms_norm(out, residual, TABLE.part, TABLE.splitk(cfg), norm_w, eps)
+                return out, residual
+    return fused_add_rms_norm(linear(x, w), residual, norm_w, eps)
+
+
 def embed_rms_norm(ids: torch.Tensor, table: torch.Tensor, w: torch.Tensor, eps: float):
     """Embedding gather fused with the first layer's input RMSNorm: returns (normed, residual)
     where residual = table[ids]."""
@@ -204,6 +223,31 @@ def rope_and_cache(qkv: torch.Tensor, num_heads: int, num_kv_heads: int, head_di
     v = qkv[:, qs + ks:].reshape(T, num_kv_heads, head_dim)
     return ref.rope_and_cache(q, k, v, positions, cos_sin, kv_layer, slot_mapping, q_norm_w, k_norm_w, eps,
                               k_scale, v_scale)
+
+
+def linear_rope_and_cache(h: torch.Tensor, w: torch.Tensor, num_heads: int, num_kv_heads: int, head_dim: int,
+                          positions: torch.Tensor, cos_sin: torch.Tensor, kv_layer: torch.Tensor,
+                          slot_mapping: torch.Tensor, q_norm_w=None, k_norm_w=None, eps: float = 1e-6,
+                          k_scale: float = 1.0, v_scale: float = 1.0):
+    """qkv projection + rope_and_cache.  When the decode table runs the projection split-K, its fp32
+    slabs feed the rope / cache-write kernel directly (no reduce kernel, no bf16 qkv round trip)."""
+    if _gpu(h) and h.dim() == 2 and 0 < h.shape[0] <= 256 and head_dim in (64, 128):
+        from .decode_gemm import TABLE
+        M, N = h.shape[0], w.shape[0]
+        cfg = TABLE.lookup(M, N, w.shape[1], 0)
+        if cfg is not None and TABLE.splitk(cfg) > 1:
+            dummy = torch.empty(M, N, dtype=h.dtype, device=h.device)  # not written when the reduce is skipped
+            if TABLE.run(dummy, h, w, cfg, 0, reduce=False):
+                q = torch.empty(M, num_heads, head_dim, dtype=h.dtype, device=h.device)
+                if ext().splitk_rope_and_cache(q, TABLE.part, TABLE.splitk(cfg), M, positions, cos_sin, kv_layer,
+                                               slot_mapping, q_norm_w, k_norm_w, num_heads, num_kv_heads, head_dim,
+                                               eps, k_scale, v_scale):
+                    return q
+                TABLE.run(dummy, h, w, cfg, 0)  # kernel shape not covered: reduce and take the plain path
+                return rope_and_cache(dummy, num_heads, num_kv_heads, head_dim, positions, cos_sin, kv_layer,
+                                      slot_mapping, q_norm_w, k_norm_w, eps, k_scale, v_scale)
+    return rope_and_cache(linear(h, w), num_heads, num_kv_heads, head_dim, positions, cos_sin, kv_layer, slot_mapping,
+                          q_norm_w, k_norm_w, eps, k_scale, v_scale)
 
 
 def paged_attention_decode(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,

@@ -149,7 +149,14 @@ class DecodeGemmTable:
             return None
         return ent[i][1]
 
-    def run(self, out: torch.Tensor, x: torch.Tensor, w: torch.Tensor, cfg: tuple, epi: int) -> bool:
+    @staticmethod
+    def splitk(cfg: tuple) -> int:
+        return cfg[5] if cfg[0] == "mt" else cfg[3]
+
+    def run(self, out: torch.Tensor, x: torch.Tensor, w: torch.Tensor, cfg: tuple, epi: int,
+            reduce: bool = True) -> bool:
+        """reduce=False (split-K configurations only): leave the fp32 slabs [sk][M][N] in self.part for
+        the caller's epilogue kernel (ops.linear_add_rms_norm)."""
         from . import ext
         mt = cfg[0] == "mt"
         if mt:
@@ -171,9 +178,9 @@ class DecodeGemmTable:
                 if torch.cuda.is_current_stream_capturing():
                     return False
                 self.cnt = torch.zeros(MT_COUNTERS, dtype=torch.int32, device=x.device)
-            return bool(ext().mt_gemm(out, x, w, part, wm, wn, mr, wnf, sk, epi, self.cnt if MT_FUSED_REDUCE else None,
-                                      order))
-        return bool(ext().decode_gemm(out, x, w, part, mf, nf, wm, sk, epi, lu))
+            return bool(ext().mt_gemm(out, x, w, part, wm, wn, mr, wnf, sk, epi,
+                                      self.cnt if MT_FUSED_REDUCE and reduce else None, order, reduce))
+        return bool(ext().decode_gemm(out, x, w, part, mf, nf, wm, sk, epi, lu, reduce))
 
 
 TABLE = DecodeGemmTable()
@@ -246,10 +253,38 @@ def pick(lib_fn, cand_fns: dict) -> tuple:
     return best, best_t, t_lib
 
 
+def _epilogues(spec, M: int, N: int, device, dtype):
+    """(plain, slab) epilogue callables of a projection for timing: plain(y) runs the separate
+    epilogue kernel on the bf16 projection output, slab(sk) the fused one on sk unreduced slabs.
+    spec: ("add_norm",) -- residual add + RMSNorm (o / down at TP = 1); ("rope", Hq, Hkv, D) -- rope +
+    cache write (qkv; unmapped slots, so the timing leaves no cache bytes behind)."""
+    from . import ext
+    if spec is None:
+        return None, None
+    if spec[0] == "add_norm":
+        res = torch.randn(M, N, device=device).to(dtype)
+        nw = torch.ones(N, device=device, dtype=dtype)
+        h = torch.empty(M, N, device=device, dtype=dtype)
+        return (lambda y: ext().fused_add_rms_norm(h, y, res, nw, 1e-5),
+                lambda sk: ext().splitk_add_rms_norm(h, res, TABLE.part, sk, nw, 1e-5))
+    _, hq, hkv, hd = spec
+    pos = torch.zeros(M, dtype=torch.int64, device=device)
+    slot = torch.full((M,), -1, dtype=torch.int64, device=device)
+    cs = torch.zeros(8, hd, dtype=torch.float32, device=device)
+    kv = torch.zeros(1, 2, hkv, 16, hd, dtype=dtype, device=device)
+    q = torch.empty(M, hq, hd, dtype=dtype, device=device)
+    return (lambda y: ext().rope_and_cache(q, y, pos, cs, kv, slot, None, None, hq, hkv, hd, 1e-6, 1.0, 1.0),
+            lambda sk: ext().splitk_rope_and_cache(q, TABLE.part, sk, M, pos, cs, kv, slot, None, None, hq, hkv, hd,
+                                                   1e-6, 1.0, 1.0))
+
+
 def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
-    """shapes: {name: (weight tensor [N, K], epi)}.  Fills TABLE; returns the report rows.  Choices
-    come from the persisted table (ops/tuned.py) when it has the (shape, bucket); otherwise they are
-    measured (pick()) and added to it."""
+    """shapes: {name: (weight tensor [N, K], epi[, epilogue spec])}.  Fills TABLE; returns the report
+    rows.  Choices come from the persisted table (ops/tuned.py) when it has the (shape, bucket);
+    otherwise they are measured (pick()) and added to it.  With an epilogue spec (_epilogues) every
+    alternative is timed together with what follows it in the layer: hipBLASLt and unsplit kernels
+    plus the separate epilogue kernel, split-K kernels with their slabs summed by the fused epilogue
+    (ops.linear_add_rms_norm / ops.linear_rope_and_cache), so the choice prices the fusion."""
     if MODE != "auto":
         return []
     from . import silu_mul
@@ -260,11 +295,14 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
         return []
     store = TunedStore("decode_gemm", device_tag(device))
     # workspace for the largest split-K any candidate may pick
-    need = max(8 * max(bks) * w.shape[0] for w, _ in shapes.values())
+    need = max(8 * max(bks) * v[0].shape[0] for v in shapes.values())
     TABLE.part = torch.empty(need, dtype=torch.float32, device=device)
     TABLE.cnt = torch.zeros(MT_COUNTERS, dtype=torch.int32, device=device)
     rows = []
-    for name, (w, epi) in shapes.items():
+    for name, val in shapes.items():
+        w, epi = val[0], val[1]
+        spec = val[2] if len(val) > 2 else None
+        tag = {None: "", "add_norm": "+norm", "rope": "+rope"}[spec[0] if spec else None]
         N, K = w.shape
         ent = []
         ws = None
@@ -273,7 +311,7 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
             outN = N // 2 if epi else N
             ref_out = silu_mul(torch.nn.functional.linear(x, w)) if epi else torch.nn.functional.linear(x, w)
             out = torch.empty(M, outN, dtype=dtype, device=device)
-            key = f"{N}x{K}x{epi}@{M}"
+            key = f"{N}x{K}x{epi}{tag}@{M}"
             st = store.get(key)
             source = "table"
             if st is not None:
@@ -284,8 +322,11 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
                 source = "measured"
                 if ws is None:
                     ws = weight_copies(w)  # timed from HBM, as the decode step reads them
+                plain, slab = _epilogues(spec, M, N, device, dtype)
                 if epi:
                     lib_fn = lambda i: silu_mul(torch.nn.functional.linear(x, ws[i % len(ws)]))  # noqa: E731
+                elif plain is not None:
+                    lib_fn = lambda i: plain(torch.nn.functional.linear(x, ws[i % len(ws)]))  # noqa: E731
                 else:
                     lib_fn = lambda i: torch.nn.functional.linear(x, ws[i % len(ws)])  # noqa: E731
                 fns = {}
@@ -294,7 +335,14 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
                         continue
                     if not TABLE.run(out, x, w, cfg, epi):
                         continue
-                    fns[cfg] = (lambda c: (lambda i: TABLE.run(out, x, ws[i % len(ws)], c, epi)))(cfg)
+                    if plain is None:
+                        fns[cfg] = (lambda c: (lambda i: TABLE.run(out, x, ws[i % len(ws)], c, epi)))(cfg)
+                    elif TABLE.splitk(cfg) > 1:
+                        fns[cfg] = (lambda c: (lambda i: (TABLE.run(out, x, ws[i % len(ws)], c, epi, reduce=False),
+                                                          slab(TABLE.splitk(c)))))(cfg)
+                    else:
+                        fns[cfg] = (lambda c: (lambda i: (TABLE.run(out, x, ws[i % len(ws)], c, epi),
+                                                          plain(out))))(cfg)
                 best, best_t, t_lib = pick(lib_fn, fns) if fns else (None, None, _graph_time(lib_fn))
             if best is not None:  # correctness gate: the winner must match hipBLASLt's result
                 TABLE.run(out, x, w, best, epi)
@@ -309,7 +357,7 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
             ent.append((M, best))
             rows.append({"proj": name, "M": M, "N": N, "K": K, "epi": epi, "hipblaslt_us": t_lib and round(t_lib, 2),
                          "chosen": "hipblaslt" if best is None else "mfma", "cfg": best,
-                         "us": best_t and round(best_t, 2), "source": source})
+                         "us": best_t and round(best_t, 2), "source": source, "epilogue": tag or None})
         TABLE.entries[(N, K, epi)] = ent
         del ws
     TABLE.report = rows

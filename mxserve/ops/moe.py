@@ -239,6 +239,8 @@ def tune(w13: torch.Tensor, w2: torch.Tensor, buckets: list, top_k: int, n_exper
     rows, ent = [], []
     key = (H, I, e_local, top_k)
     TABLE.pop(key, None)
+    from .tuned import TunedStore, device_tag
+    store = TunedStore("moe_decode", device_tag(dev))
     for T in bks:
         R = T * top_k
         x = torch.randn(T, H, device=dev, generator=g).to(w13.dtype)
@@ -253,6 +255,25 @@ def tune(w13: torch.Tensor, w2: torch.Tensor, buckets: list, top_k: int, n_exper
         h = torch.empty(R, I, dtype=w13.dtype, device=dev)
         ys = torch.empty(R, H, dtype=w13.dtype, device=dev)
         part = torch.empty(8 * R * max(two_i, H), dtype=torch.float32, device=dev)
+        skey = f"{H}x{I}x{e_local}x{top_k}x{n_experts}@{T}"
+        st = store.get(skey)
+        if st is not None:  # persisted choice: only the correctness check below runs
+            cfg = st.get("cfg") or (None, None)
+            if not st.get("use") or cfg[0] is None or cfg[1] is None:
+                ent.append((T, None, None))
+                rows.append({"T": T, "chosen": "grouped_lds", "source": "table"})
+                continue
+            DECODE = False
+            ref = fused_experts(x, w13, w2, tw, ids, expert_offset)
+            DECODE = True
+            TABLE[key] = ent + [(T, cfg[0], cfg[1])]
+            out = fused_experts(x, w13, w2, tw, ids, expert_offset)
+            err = (out.float() - ref.float()).abs().max().item()
+            ok = err <= 0.03 * max(1.0, ref.float().abs().max().item())
+            ent.append((T, cfg[0], cfg[1]) if ok else (T, None, None))
+            rows.append({"T": T, "cfg_w13": cfg[0], "cfg_w2": cfg[1], "chosen": "decode" if ok else "grouped_lds",
+                         "max_abs_err": err, "source": "table"})
+            continue
         best = {}
         for name, w, epi, N, K, o, xin in (("w13", w13, 1, two_i, H, h, xs), ("w2", w2, 0, H, I, ys, h)):
             bt, bc = None, None
@@ -280,11 +301,14 @@ def tune(w13: torch.Tensor, w2: torch.Tensor, buckets: list, top_k: int, n_exper
         err = (out.float() - ref.float()).abs().max().item()
         ok = err <= 0.03 * max(1.0, ref.float().abs().max().item())
         use = ok and t_dec < t_lds * 0.98
+        store.put(skey, {"cfg": (best["w13"], best["w2"]), "use": bool(use), "layer_decode_us": round(t_dec, 1),
+                         "layer_grouped_lds_us": round(t_lds, 1)})
         ent.append((T, best["w13"], best["w2"]) if use else (T, None, None))
         rows.append({"T": T, "cfg_w13": best["w13"], "cfg_w2": best["w2"], "layer_decode_us": round(t_dec, 1),
                      "layer_grouped_lds_us": round(t_lds, 1), "chosen": "decode" if use else "grouped_lds",
                      "max_abs_err": err})
     TABLE[key] = ent
+    store.save()
     path = os.environ.get("MXS_MOE_GEMM_REPORT")
     if path:
         import json

@@ -1,0 +1,18 @@
+# fused split-K epilogues (residual add + norm, rope + cache) + epilogue-aware tuner tests; tables
+# regenerated with the epilogue keys; the 1B headline twice (second from the table); Mixtral QPS 4
+# with the 40 ms chunk budget (step time measured from the launch start)
+set -o pipefail
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out/pace gpurun_out/tuned
+cp mxserve/ops/tuned/*.json gpurun_out/tuned/
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 200 --timeout-method thread -k "splitk or rope or tuner_and_dispatch or prefill" > gpurun_out/pace/tests.log 2>&1; rc=$?; tail -5 gpurun_out/pace/tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python3 scripts/prefill_attn_probe.py > gpurun_out/pace/prefill_attn.jsonl 2>&1 || exit 1
+cat gpurun_out/pace/prefill_attn.jsonl
+timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/pace/smoke.log 2>&1; rc=$?; tail -3 gpurun_out/pace/smoke.log; [ $rc -eq 0 ] || exit $rc
+MXS_TUNED_SAVE=1 MXS_TUNED_DIR=gpurun_out/tuned timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > gpurun_out/pace/l1b.json 2> gpurun_out/pace/l1b.err || exit 1
+tail -c 1500 gpurun_out/pace/l1b.json
+MXS_TUNED_DIR=gpurun_out/tuned timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > gpurun_out/pace/l1b_2.json 2> gpurun_out/pace/l1b_2.err || exit 1
+tail -c 1500 gpurun_out/pace/l1b_2.json
+MX="--model mistralai/Mixtral-8x7B-Instruct-v0.1 --qps 4 --max-num-seqs 128 --iters-per-step 50 --steps 10 --warmup 3"
+MXS_TUNED_SAVE=1 MXS_TUNED_DIR=gpurun_out/tuned timeout -k 10 420 python3 bench.py $MX --itl-target-ms 40 > gpurun_out/pace/mixtral_t40.json 2> gpurun_out/pace/mixtral_t40.err || exit 1
+tail -c 2500 gpurun_out/pace/mixtral_t40.json

@@ -151,3 +151,34 @@ def test_nonneg_fit_on_collinear_steps():
     assert m.theta_nn is not None and (m.theta_nn >= 0).all()
     x = np.array([1.0, 8.192, 8192 * 6096 / 1e7, 2.0, 8.0])
     assert abs(float(x @ m.theta_nn) - float(x @ true)) < 0.05 * float(x @ true)
+
+
+def test_step_time_measured_from_launch_start():
+    """A long eager step starts on the GPU while the host still enqueues it: its measured time runs
+    from the start of the launch (not the end), else the model sees a 100 ms prefill step as a few ms."""
+    from types import SimpleNamespace
+    from mxserve.engine.pacing import LateAdmission
+    la = LateAdmission()
+    seen = []
+    la.model.update = lambda x, s: seen.append(s)
+    so = SimpleNamespace(prefills=[SimpleNamespace(num_new_tokens=8000, start=0)], decodes=[])
+    la.last_done = 0.0
+    la.launched(so, t_admit=0.0, t_launched=0.060, t_begin=0.001)  # 59 ms to enqueue
+    la.rotate()
+    la.observe_done(la.inflight, 0.101)
+    assert seen and abs(seen[0] - 0.100) < 1e-9
+
+
+def test_step_time_from_gpu_events_preferred():
+    """With the runner's event-measured GPU time the model fits on it, even when the host saw
+    neither this step's nor the previous step's completion."""
+    from types import SimpleNamespace
+    from mxserve.engine.pacing import LateAdmission
+    la = LateAdmission()
+    seen = []
+    la.model.update = lambda x, s: seen.append(s)
+    so = SimpleNamespace(prefills=[SimpleNamespace(num_new_tokens=8000, start=0)], decodes=[])
+    la.launched(so, t_admit=0.0, t_launched=0.02, t_begin=0.0)
+    la.rotate()
+    la.observe_done(la.inflight, None, gpu_s=0.095)
+    assert seen == [0.095]

@@ -568,14 +568,28 @@ def test_decode_gemm_tuner_and_dispatch(gpu, monkeypatch):
     from mxserve.ops import decode_gemm
     monkeypatch.setattr(decode_gemm, "MODE", "auto")
     monkeypatch.setattr(decode_gemm, "MAX_TUNE_M", 256)
+    monkeypatch.setenv("MXS_RETUNE", "1")  # measure, whatever the packaged table holds
+    monkeypatch.delenv("MXS_TUNED_SAVE", raising=False)
     w1 = (torch.randn(2048, 2048, device=gpu) * 0.02).to(torch.bfloat16)
     w2 = (torch.randn(2 * 8192, 2048, device=gpu) * 0.02).to(torch.bfloat16)
-    rows = decode_gemm.tune({"o": (w1, 0), "gate_up": (w2, 1)}, [8, 64, 256], gpu)
-    assert len(rows) == 6 and all(r["us"] <= r["hipblaslt_us"] for r in rows)
-    x = torch.randn(64, 2048, device=gpu, dtype=torch.bfloat16)
-    _close(ops.linear(x, w1), x.float() @ w1.float().t(), 2e-2, 2e-2, "tuned linear")
-    y = x.float() @ w2.float().t()
-    _close(ops.gate_up_silu(x, w2), torch.nn.functional.silu(y[:, :8192]) * y[:, 8192:], 2e-2, 2e-2, "tuned gate_up")
+    w3 = (torch.randn(3072, 2048, device=gpu) * 0.02).to(torch.bfloat16)
+    rows = decode_gemm.tune({"o": (w1, 0, ("add_norm",)), "gate_up": (w2, 1), "qkv": (w3, 0, ("rope", 32, 8, 64))},
+                            [1, 8, 64, 256], gpu)
+    assert len(rows) == 12 and all(r["us"] <= r["hipblaslt_us"] for r in rows)
+    assert {r["epilogue"] for r in rows} == {"+norm", "+rope", None}
+    for M in (1, 64):
+        x = torch.randn(M, 2048, device=gpu, dtype=torch.bfloat16)
+        _close(ops.linear(x, w1), x.float() @ w1.float().t(), 2e-2, 2e-2, "tuned linear")
+        y = x.float() @ w2.float().t()
+        _close(ops.gate_up_silu(x, w2), torch.nn.functional.silu(y[:, :8192]) * y[:, 8192:], 2e-2, 2e-2,
+               "tuned gate_up")
+        res = torch.randn(M, 2048, device=gpu, dtype=torch.bfloat16)
+        nw = torch.ones(2048, device=gpu, dtype=torch.bfloat16)
+        r2 = res.clone()
+        h, _ = ops.linear_add_rms_norm(x, w1, r2, nw, 1e-5)
+        r_want = (x.float() @ w1.float().t()).to(torch.bfloat16).float() + res.float()
+        _close(r2, r_want, 3e-2, 2e-2, "tuned o + residual")
+        _close(h, r_want * torch.rsqrt(r_want.pow(2).mean(-1, keepdim=True) + 1e-5), 3e-2, 3e-2, "tuned o + norm")
 
 
 def test_decode_gemm_rejects_untiled_shapes(gpu):
@@ -870,3 +884,69 @@ def test_sample_top_p_rate(gpu):
     ms = e0.elapsed_time(e1) / 5
     print(f"top-k 40 + top-p 0.9 sampling, 384 x 128256 bf16: {ms:.3f} ms")
     assert ms < 2.0
+
+
+@pytest.mark.parametrize("M,N,K,cfg", [(1, 2048, 2048, (1, 2, 1, 8, 0)), (24, 2048, 8192, (2, 2, 1, 4, 4)),
+                                       (256, 2048, 8192, ("mt", 4, 2, 1, 2, 8, 1)),
+                                       (200, 2048, 8192, ("mt", 4, 2, 1, 2, 8))])
+def test_linear_add_rms_norm_splitk_epilogue(gpu, M, N, K, cfg, monkeypatch):
+    """o_proj / down_proj with the split-K slabs summed by the residual-add + RMSNorm epilogue kernel
+    (norm_act.hip splitk_add_rmsnorm_kernel) vs the fp32 reference, for the register / LDS decode
+    kernels and the mt kernel in both tile orders; the residual is updated in place."""
+    from mxserve.ops import decode_gemm
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    x = torch.randn(M, K, device=gpu, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu, generator=g) * K ** -0.5).to(torch.bfloat16)
+    res = torch.randn(M, N, device=gpu, generator=g).to(torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(N, device=gpu, generator=g)).to(torch.bfloat16)
+    y = x.float() @ w.float().t()
+    r_want = y.to(torch.bfloat16).float() + res.float()
+    h_want = r_want * torch.rsqrt(r_want.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float()
+    tab = decode_gemm.DecodeGemmTable()
+    tab.part = torch.empty(8 * M * N, dtype=torch.float32, device=gpu)
+    tab.entries[(N, K, 0)] = [(256, cfg)]
+    monkeypatch.setattr(decode_gemm, "TABLE", tab)
+    monkeypatch.setattr(decode_gemm, "MODE", "auto")
+    assert decode_gemm.TABLE.lookup(M, N, K, 0) == cfg
+    r = res.clone()
+    h, r2 = ops.linear_add_rms_norm(x, w, r, nw, 1e-5)
+    assert r2 is r
+    _close(r, r_want, atol=3e-2, rtol=2e-2, name=f"residual {cfg}")
+    _close(h, h_want, atol=3e-2, rtol=3e-2, name=f"normed {cfg}")
+    # the unfused path (hipBLASLt + fused_add_rms_norm) agrees to bf16 rounding
+    r3 = res.clone()
+    h3, _ = ops.fused_add_rms_norm(torch.nn.functional.linear(x, w), r3, nw, 1e-5)
+    _close(h, h3, atol=3e-2, rtol=3e-2, name="fused vs unfused")
+
+
+@pytest.mark.parametrize("M,cfg,qknorm", [(1, (1, 2, 1, 8, 0), False), (7, (1, 2, 1, 4, 0), True),
+                                          (192, ("mt", 4, 2, 1, 2, 4), False)])
+def test_linear_rope_and_cache_splitk(gpu, M, cfg, qknorm, monkeypatch):
+    """qkv projection run split-K with its fp32 slabs summed inside the rope / cache-write kernel
+    (rope_cache.hip rope_cache_kernel<SLABS>) vs hipBLASLt + the plain rope_and_cache kernel."""
+    from mxserve.ops import decode_gemm
+    D, hq, hkv, K, nb = 64, 32, 8, 2048, 40
+    N = (hq + 2 * hkv) * D
+    g = torch.Generator(device="cuda").manual_seed(M)
+    h = torch.randn(M, K, device=gpu, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu, generator=g) * K ** -0.5).to(torch.bfloat16)
+    cos_sin = ref.build_cos_sin_cache(D, 4096, 500000.0, None, device=gpu)
+    pos = torch.randint(0, 4000, (M,), device=gpu, generator=g)
+    slots = torch.randperm(nb * 16, device=gpu, generator=g)[:M]
+    if M > 2:
+        slots[1] = -1  # a padded row: no cache write
+    qn = (1 + 0.1 * torch.randn(D, device=gpu, generator=g)).bfloat16() if qknorm else None
+    kn = (1 + 0.1 * torch.randn(D, device=gpu, generator=g)).bfloat16() if qknorm else None
+    kv = torch.zeros(nb, 2, 2, hkv, 16, D, device=gpu, dtype=torch.bfloat16)
+    kv_ref = kv.clone()
+    q_ref = ops.rope_and_cache(torch.nn.functional.linear(h, w), hq, hkv, D, pos, cos_sin, kv_ref[:, 1], slots, qn, kn,
+                               1e-6)
+    tab = decode_gemm.DecodeGemmTable()
+    tab.part = torch.empty(8 * M * N, dtype=torch.float32, device=gpu)
+    tab.entries[(N, K, 0)] = [(256, cfg)]
+    monkeypatch.setattr(decode_gemm, "TABLE", tab)
+    monkeypatch.setattr(decode_gemm, "MODE", "auto")
+    q = ops.linear_rope_and_cache(h, w, hq, hkv, D, pos, cos_sin, kv[:, 1], slots, qn, kn, 1e-6)
+    _close(q, q_ref, 0.03, 0.02, f"q {cfg}")
+    _close(kv, kv_ref, 0.03, 0.02, f"kv cache {cfg}")
+    assert kv[:, 0].abs().sum().item() == 0

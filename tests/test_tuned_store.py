@@ -11,26 +11,26 @@ from mxserve.ops import decode_gemm, tuned
 def test_store_roundtrip(tmp_path, monkeypatch):
     monkeypatch.setenv("MXS_TUNED_DIR", str(tmp_path))
     monkeypatch.setenv("MXS_TUNED_SAVE", "1")
-    st = tuned.TunedStore("decode_gemm", "gfx950_256cu")
+    st = tuned.TunedStore("decode_gemm", "gfxtest_256cu")
     assert st.get("3072x2048x0@256") is None and st.misses == 1
     st.put("3072x2048x0@256", {"cfg": ("mt", 4, 2, 1, 2, 4, 1), "us": 9.5, "hipblaslt_us": 13.0})
     st.put("2048x2048x0@256", {"cfg": None, "us": 10.1, "hipblaslt_us": 10.1})
     path = st.save()
-    assert path == str(tmp_path / "decode_gemm_gfx950_256cu.json")
+    assert path == str(tmp_path / "decode_gemm_gfxtest_256cu.json")
     d = json.loads(open(path).read())
-    assert d["device"] == "gfx950_256cu" and len(d["entries"]) == 2
-    st2 = tuned.TunedStore("decode_gemm", "gfx950_256cu")
+    assert d["device"] == "gfxtest_256cu" and len(d["entries"]) == 2
+    st2 = tuned.TunedStore("decode_gemm", "gfxtest_256cu")
     e = st2.get("3072x2048x0@256")
     assert e["cfg"] == ("mt", 4, 2, 1, 2, 4, 1)  # tuple again: hashable, comparable with candidates()
     assert st2.get("2048x2048x0@256")["cfg"] is None and st2.hits == 2
     monkeypatch.setenv("MXS_RETUNE", "1")
-    assert tuned.TunedStore("decode_gemm", "gfx950_256cu").get("3072x2048x0@256") is None
+    assert tuned.TunedStore("decode_gemm", "gfxtest_256cu").get("3072x2048x0@256") is None
 
 
 def test_save_is_opt_in(tmp_path, monkeypatch):
     monkeypatch.setenv("MXS_TUNED_DIR", str(tmp_path))
     monkeypatch.delenv("MXS_TUNED_SAVE", raising=False)
-    st = tuned.TunedStore("prefill_gemm", "gfx950_256cu")
+    st = tuned.TunedStore("prefill_gemm", "gfxtest_256cu")
     st.put("k", {"cfg": None})
     assert st.save() is None and not list(tmp_path.iterdir())
 
@@ -38,7 +38,7 @@ def test_save_is_opt_in(tmp_path, monkeypatch):
 def test_other_device_tag_does_not_match(tmp_path, monkeypatch):
     monkeypatch.setenv("MXS_TUNED_DIR", str(tmp_path))
     monkeypatch.setenv("MXS_TUNED_SAVE", "1")
-    st = tuned.TunedStore("decode_gemm", "gfx950_256cu")
+    st = tuned.TunedStore("decode_gemm", "gfxtest_256cu")
     st.put("k", {"cfg": None})
     st.save()
     assert tuned.TunedStore("decode_gemm", "gfx942_304cu").get("k") is None
