@@ -63,15 +63,11 @@ class LLMEngine:
             from .pacing import LateAdmission
             self._late = LateAdmission()
         self._inflight: Optional[tuple] = None
-        # decode-aware prefill chunk budget: priced by the late-admission step-time model, or by an
-        # own model fed with synchronous step times when late admission is off
-        self._budget_model = None
+        # decode-aware prefill chunk budget (engine/pacing.py ChunkBudget): fed with every step's GPU
+        # time (runner events; the step's wall time when synchronous on the CPU)
         if args.itl_target_ms and args.itl_target_ms > 0:
-            from .pacing import ChunkBudget, StepTimeModel
-            model = self._late.model if self._late is not None else StepTimeModel()
-            if self._late is None:
-                self._budget_model = model
-            self.scheduler.chunk_budget = ChunkBudget(model, args.itl_target_ms)
+            from .pacing import ChunkBudget
+            self.scheduler.chunk_budget = ChunkBudget(args.itl_target_ms)
         self.profiler = StepProfiler()  # MXS_TORCH_PROFILE="start:count:path"
         # MXS_STEP_TIMING=1: host seconds per phase (schedule / launch / collect wait / land)
         self.step_times: Optional[dict] = ({"schedule": 0.0, "launch": 0.0, "collect": 0.0, "land": 0.0,
@@ -208,9 +204,14 @@ class LLMEngine:
                               (time.perf_counter() if pending else None), dh.get("gpu_s"))
         else:
             sampled = self.runner.collect(dh)
-            if self._budget_model is not None and not self.async_scheduling:
-                from .pacing import step_features
-                self._budget_model.update(step_features(dso), time.perf_counter() - t_adm)
+        cb = self.scheduler.chunk_budget
+        if cb is not None:
+            from .pacing import step_features
+            g = dh.get("gpu_s")
+            if g is None and not self.async_scheduling:
+                g = time.perf_counter() - t_adm  # synchronous step: its wall time
+            if g is not None:
+                cb.observe(step_features(dso), g)
         if tm is None:
             return self._land(dso, sampled, dh.get("logprobs"))
         t3 = time.perf_counter()

@@ -53,11 +53,12 @@ def nonneg_fit(A: np.ndarray, b: np.ndarray) -> Optional[np.ndarray]:
 
 
 class StepTimeModel:
-    def __init__(self, lam: float = 0.98, warmup: int = 24):
+    def __init__(self, lam: float = 0.98, warmup: int = 24, nf: int = NF):
         self.lam = lam
         self.warmup = warmup
-        self.A = np.eye(NF) * 1e-6
-        self.b = np.zeros(NF)
+        self.nf = nf
+        self.A = np.eye(nf) * 1e-6
+        self.b = np.zeros(nf)
         self.theta: Optional[np.ndarray] = None
         # the same fit with every coefficient >= 0 (a step cannot get faster with more work): prefill
         # tokens and prefill attention work move together, so the unconstrained fit can trade one
@@ -65,20 +66,16 @@ class StepTimeModel:
         # for pricing a chunk of a given size (ChunkBudget)
         self.theta_nn: Optional[np.ndarray] = None
         self.n = 0
-        self.prefill_samples: list = []  # last few (features, seconds) of steps with prefill (stats)
 
     def update(self, x: np.ndarray, seconds: float) -> None:
         if not (0.0 < seconds < 5.0):
             return
-        if x[1] > 0:
-            self.prefill_samples = self.prefill_samples[-7:] + [[round(float(v), 4) for v in x[1:]] +
-                                                                [round(1e3 * seconds, 3)]]
         self.A = self.lam * self.A + np.outer(x, x)
         self.b = self.lam * self.b + x * seconds
         self.n += 1
         if self.n >= self.warmup and (self.n < 200 or self.n % 8 == 0):
             try:
-                self.theta = np.linalg.solve(self.A + 1e-9 * np.eye(NF), self.b)
+                self.theta = np.linalg.solve(self.A + 1e-9 * np.eye(self.nf), self.b)
             except np.linalg.LinAlgError:
                 self.theta = None
             self.theta_nn = nonneg_fit(self.A, self.b)
@@ -95,27 +92,57 @@ class ChunkBudget:
     A fixed token budget (max_num_batched_tokens) makes a step that carries a prefill chunk as long
     as the decode rows plus the whole chunk: at 250 decode rows and an 8192-token chunk that step,
     and so every running request's inter-token latency, is ~2.5x a decode-only step.  With a target
-    the scheduler prices the step's decode rows with the same online step-time model late admission
-    fits (StepTimeModel: intercept, decode rows, decode context, prefill tokens, prefill attention
-    work) and gives prefill chunks only the time left under the target.  The first chunk of a step
-    always gets at least `min_tokens`, so prefill never stalls (TTFT stays bounded when decode alone
-    exceeds the target).  The chunk is priced with the model's non-negative fit (theta_nn); until the
-    model is fitted no limit applies.
+    the scheduler prices the step's decode rows and gives prefill chunks only the time left.
+
+    Two non-negative least-squares models, fed with each step's GPU time (runner events):
+      * decode: [1, decode rows, decode context] fitted on decode-only steps;
+      * prefill: [1, prefill tokens, prefill attention work] fitted on what a mixed step took beyond
+        the decode model's price for its decode rows (the constant is the mixed step's fixed extra:
+        eager launch, MoE weights streamed again).
+    Kept apart because in a loaded closed loop nearly every step carries both, and one joint fit
+    then cannot tell decode cost from prefill cost (it settles on pricing prefill tokens at the whole
+    step's time and starves prefill).  Guards: the first chunk of a step always gets `min_tokens`;
+    when the oldest waiting request has waited `ttft_guard_s` the step is not limited at all, so an
+    overloaded worker trades ITL back for TTFT instead of queueing without bound.  Until both models
+    are fitted no limit applies.
     """
 
-    def __init__(self, model: StepTimeModel, target_ms: float, min_tokens: int = 256, align: int = 64):
-        self.model = model
+    def __init__(self, target_ms: float, min_tokens: int = 256, align: int = 64, ttft_guard_s: float = 0.5):
+        self.dec = StepTimeModel(nf=3)
+        self.pre = StepTimeModel(nf=3)
         self.target = float(target_ms) / 1e3
         self.min_tokens = int(min_tokens)
         self.align = int(align)
-        self.steps = 0  # steps that planned with a fitted model
+        self.ttft_guard_s = float(ttft_guard_s)
+        self.steps = 0  # steps that planned with fitted models
         self.limited = 0  # prefill chunks cut short by the budget
         self.cut_tokens = 0
+        self.guard_lifts = 0  # steps left unlimited because a request waited too long
 
-    def begin(self, running) -> Optional[float]:
+    @staticmethod
+    def _dec_x(nd: float, dctx: float) -> np.ndarray:
+        return np.array([1.0, nd / 1e2, dctx / 1e5])
+
+    def observe(self, x: np.ndarray, seconds: float) -> None:
+        """A step of composition x (step_features) took `seconds` of GPU time."""
+        if not (0.0 < seconds < 5.0):
+            return
+        xd = np.array([1.0, x[3], x[4]])
+        if x[1] <= 0.0:
+            self.dec.update(xd, seconds)
+            return
+        th = self.dec.theta_nn
+        if th is None:
+            return
+        self.pre.update(np.array([1.0, x[1], x[2]]), seconds - float(xd @ th))
+
+    def begin(self, running, waiting=None) -> Optional[float]:
         """Seconds left for prefill work in the next step (None = no limit)."""
-        th = self.model.theta_nn
-        if th is None or th[1] + th[2] <= 0.0:
+        td, tp = self.dec.theta_nn, self.pre.theta_nn
+        if td is None or tp is None or tp[1] + tp[2] <= 0.0:
+            return None
+        if waiting and time.monotonic() - waiting[0].arrival_time > self.ttft_guard_s:
+            self.guard_lifts += 1
             return None
         nd = 0
         dctx = 0
@@ -125,12 +152,12 @@ class ChunkBudget:
                 nd += 1
                 dctx += c
         self.steps += 1
-        return self.target - max(0.0, th[0] + th[3] * nd / 1e2 + th[4] * dctx / 1e5)
+        return self.target - float(self._dec_x(nd, dctx) @ td) - tp[0]
 
     def fit(self, left: float, start: int, want: int, first: bool) -> tuple:
         """Largest chunk <= want (tokens from position `start`) whose predicted cost fits in
         `left` seconds; returns (tokens, seconds)."""
-        th = self.model.theta_nn
+        th = self.pre.theta_nn
         c1 = th[1] / 1e3  # s per prefill token
         c2 = max(0.0, th[2] / 1e7)  # s per token x context token (attention)
         b = max(c1 + c2 * start, 1e-9)
@@ -155,14 +182,13 @@ class ChunkBudget:
         return n, n * (b + a * n)
 
     def stats(self) -> dict:
-        th = self.model.theta_nn
+        ms = lambda t: None if t is None else [round(1e3 * float(v), 4) for v in t]  # noqa: E731
         return {"target_ms": round(self.target * 1e3, 2), "planned_steps": self.steps, "limited_chunks": self.limited,
-                "cut_tokens": self.cut_tokens, "model_updates": self.model.n,
-                # fitted costs: ms per step, per 1k prefill tokens, per 1e7 token x context, per 100
-                # decode rows, per 1e5 decode context tokens
-                "theta_nn_ms": None if th is None else [round(1e3 * float(v), 4) for v in th],
-                "theta_ms": None if self.model.theta is None else [round(1e3 * float(v), 4) for v in self.model.theta],
-                "prefill_samples": self.model.prefill_samples}
+                "cut_tokens": self.cut_tokens, "guard_lifts": self.guard_lifts,
+                "decode_updates": self.dec.n, "prefill_updates": self.pre.n,
+                # fitted costs: decode ms per step / per 100 rows / per 1e5 context tokens; prefill ms
+                # per mixed step (fixed extra) / per 1k tokens / per 1e7 token x context
+                "decode_ms": ms(self.dec.theta_nn), "prefill_ms": ms(self.pre.theta_nn)}
 
 
 class LateAdmission:

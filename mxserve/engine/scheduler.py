@@ -149,7 +149,7 @@ class Scheduler:
         budget = self.max_num_batched_tokens
         scheduled: list[ScheduledReq] = []
         cb = self.chunk_budget
-        left = cb.begin(self.running) if cb is not None else None  # seconds for prefill chunks
+        left = cb.begin(self.running, self.waiting) if cb is not None else None  # seconds for prefill chunks
         first = True
         i = 0
         while i < len(self.running) and budget > 0:

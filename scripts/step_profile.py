@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--chunk", type=int, default=8192)
+    ap.add_argument("--tuned", action="store_true",
+                    help="load the decode GEMM choices the engine would use (packaged table / tuner)")
     a = ap.parse_args()
     from mxserve.models.config import get_model_config
     from mxserve.models.llama import AttnMetadata, build_model
@@ -49,6 +51,14 @@ def main():
                         block_tables=btp, seq_lens=torch.full((P,), per, **i32), query_start_loc=qsl,
                         logits_indices=(qsl[1:] - 1).long(), num_decodes=0, num_prefills=P, num_prefill_tokens=T,
                         max_query_len=per, max_seq_len=per, prefill_query_start_loc=qsl, sample_seq=torch.arange(P, **i32))
+    if a.tuned:  # the engine's decode GEMM / fused-epilogue choices for this batch bucket
+        from mxserve.ops import decode_gemm
+        w = m.w
+        norm = ("add_norm",) if m.fuse_residual else None
+        decode_gemm.tune({"qkv": (w["l0.qkv"], 0, ("rope", m.nh, m.nkv, m.hd)), "o": (w["l0.o"], 0, norm),
+                          "gate_up": (w["l0.gate_up"], 1), "down": (w["l0.down"], 0, norm),
+                          "lm_head": (m.lm_head_weight(), 0)}, [B], dev)
+        print({r["proj"]: r["cfg"] for r in decode_gemm.TABLE.report})
     ids_d = torch.randint(0, cfg.vocab_size, (B,), device=dev)
     ids_p = torch.randint(0, cfg.vocab_size, (T,), device=dev)
     with torch.inference_mode():

@@ -10,14 +10,16 @@ from mxserve.engine.request import Request, SamplingParams
 from mxserve.engine.scheduler import Scheduler
 
 
-def _model(theta):
-    m = StepTimeModel()
-    m.theta = np.asarray(theta, dtype=float)
-    m.theta_nn = m.theta
-    return m
+def _budget(target_ms, dec=(2e-3, 4e-3, 0.0), pre=(0.0, 2e-3, 0.0)):
+    """A ChunkBudget with fitted models: decode [per step, per 100 rows, per 1e5 context] and prefill
+    [fixed extra per mixed step, per 1k tokens, per 1e7 token x context] costs in seconds."""
+    cb = ChunkBudget(target_ms)
+    cb.dec.theta_nn = np.asarray(dec, dtype=float)
+    cb.pre.theta_nn = np.asarray(pre, dtype=float)
+    return cb
 
 
-# 2 ms intercept, 2 ms per 1000 prefill tokens, no attention term, 4 ms per 100 decode rows
+# 2 ms per step, 4 ms per 100 decode rows; prefill 2 ms per 1000 tokens, no attention term
 THETA = [2e-3, 2e-3, 0.0, 4e-3, 0.0]
 
 
@@ -25,11 +27,11 @@ def _req(i, n_prompt):
     return Request(f"r{i}", list(range(1, n_prompt + 1)), SamplingParams(max_tokens=64, ignore_eos=True))
 
 
-def _sched(target_ms, theta=THETA, budget=8192):
+def _sched(target_ms, pre=(0.0, 2e-3, 0.0), budget=8192):
     s = Scheduler(KVCacheManager(4096, 16, False), max_num_seqs=256, max_num_batched_tokens=budget,
                   max_model_len=8192)
     if target_ms:
-        s.chunk_budget = ChunkBudget(_model(theta), target_ms)
+        s.chunk_budget = _budget(target_ms, pre=pre)
     return s
 
 
@@ -99,8 +101,7 @@ def test_running_chunked_prefill_continues_under_budget():
 
 def test_attention_term_shrinks_late_chunks():
     # attention 1 ms per 1e7 token*context: a chunk deep into a long prompt costs more per token
-    theta = [2e-3, 2e-3, 1e-3, 0.0, 0.0]
-    cb = ChunkBudget(_model(theta), 10.0)
+    cb = _budget(10.0, pre=(0.0, 2e-3, 1e-3))
     n0, c0 = cb.fit(8e-3, 0, 8000, True)
     n1, c1 = cb.fit(8e-3, 6000, 8000, True)
     assert n1 < n0
@@ -108,11 +109,11 @@ def test_attention_term_shrinks_late_chunks():
 
 
 def test_unfitted_or_degenerate_model_means_no_limit():
-    s = _sched(10.0, theta=[2e-3, -1e-3, 0, 0, 0])
+    s = _sched(10.0, pre=(0.0, 0.0, 0.0))
     s.add(_req(0, 6000))
     assert s.schedule().prefills[0].num_new_tokens == 6000
     s = _sched(0)
-    s.chunk_budget = ChunkBudget(StepTimeModel(), 10.0)  # theta None: not fitted yet
+    s.chunk_budget = ChunkBudget(10.0)  # not fitted yet
     s.add(_req(0, 6000))
     assert s.schedule().prefills[0].num_new_tokens == 6000
 
@@ -126,7 +127,8 @@ def test_engine_wires_target_from_args():
     sp = SamplingParams(max_tokens=4, ignore_eos=True)
     outs = eng.generate([list(range(1, 40)) for _ in range(30)], sp)
     assert all(len(o) == 4 for o in outs)
-    assert eng._budget_model.n > 0
+    cb = eng.scheduler.chunk_budget
+    assert cb.dec.n + cb.pre.n > 0  # synchronous CPU steps feed their wall time
     assert eng.stats()["chunk_budget"]["target_ms"] == 50.0
 
 
@@ -182,3 +184,37 @@ def test_step_time_from_gpu_events_preferred():
     la.rotate()
     la.observe_done(la.inflight, None, gpu_s=0.095)
     assert seen == [0.095]
+
+
+def test_separate_models_survive_all_mixed_steps():
+    """Decode cost is learned from decode-only steps and kept when (under load) every later step
+    carries a chunk; prefill cost is fitted on what mixed steps take beyond it, so a chunk's price is
+    per-token prefill work, not the whole step's time (the joint-fit failure that starved prefill)."""
+    rng = np.random.default_rng(1)
+    cb = ChunkBudget(40.0)
+
+    def step(nd, p, start=0):
+        x = np.array([1.0, p / 1e3, p * (start + p / 2) / 1e7, nd / 1e2, nd * 4200 / 1e5])
+        t = 0.024 + 0.0001 * nd + ((0.004 + 0.012 * p / 1e3) if p else 0.0)  # Mixtral-like
+        return x, t * (1 + 0.01 * rng.standard_normal())
+
+    for _ in range(60):  # decode-only warmup
+        cb.observe(*step(rng.integers(60, 90), 0))
+    for _ in range(300):  # loaded: every step mixed
+        cb.observe(*step(rng.integers(60, 90), rng.integers(300, 2000), rng.integers(0, 3000)))
+    assert cb.dec.theta_nn is not None and cb.pre.theta_nn is not None
+    assert abs(cb.pre.theta_nn[1] - 0.012) < 0.003, cb.pre.theta_nn  # ~12 ms per 1k tokens
+    left = cb.begin([], [])
+    n, cost = cb.fit(left, 0, 8192, True)
+    assert 500 < n < 1200, n  # (40 - ~32 decode - ~4 extra) ms at ~12 ms / 1k tokens
+
+
+def test_ttft_guard_lifts_the_limit():
+    import time as _t
+    s = _sched(10.0)
+    old = _req(0, 6000)
+    s.add(old)
+    old.arrival_time = _t.monotonic() - 5.0  # waited far longer than the guard
+    so = s.schedule()
+    assert so.prefills[0].num_new_tokens == 6000
+    assert s.chunk_budget.guard_lifts == 1
