@@ -760,7 +760,10 @@ def phase_agg(a, ctx) -> tuple:
     drv = Driver(a2, ctx.rank, eng.model_config.vocab_size, a.qps)
     group = None
     agree = ctx.agree_fn(group, ctx.world)
+    from mxserve.utils.gcpause import PauseStats
+    gcs = PauseStats().install()  # collector passes on this rank's loop (the engine froze its start-up heap)
     st = drv.stats(run_agg(a2, eng, sp, drv, ctx.barrier, agree))
+    gcs.remove()
     info = {"kv_blocks": eng.runner.num_blocks, "graphs": sorted(eng.runner.graphs) if ctx.on_gpu else [],
             "preemptions": eng.stats()["num_preemptions"], "model": args.model,
             "kv_cache_dtype": "fp8_e4m3fn" if eng.runner.kv_fp8 else ("bf16" if ctx.on_gpu else "fp32"),
@@ -778,6 +781,7 @@ def phase_agg(a, ctx) -> tuple:
                                   "late_wakes": la.late, "margin_ms": round(1e3 * la.margin, 3)}
     if eng.scheduler.chunk_budget is not None:
         info["chunk_budget"] = eng.scheduler.chunk_budget.stats()
+    info["gc"] = gcs.summary()
     host = None
     if eng.step_times is not None and eng.step_times["steps"]:
         n = eng.step_times["steps"]
@@ -944,7 +948,7 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
     if dis is not None:
         line["disagg"] = dis
     line["engine"] = {"kv_blocks": info["kv_blocks"], "preemptions": info["preemptions"], "graphs": info["graphs"]}
-    for k in ("late_admission", "decode_gemm", "chunk_budget"):
+    for k in ("late_admission", "decode_gemm", "chunk_budget", "gc"):
         if k in info:
             line["engine"][k] = info[k]
     return line

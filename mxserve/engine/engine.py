@@ -19,6 +19,7 @@ from .kv_manager import KVCacheManager
 from .model_runner import ModelRunner
 from .request import Request, SamplingParams, Status
 from .scheduler import Scheduler
+from ..utils import gcpause
 from ..utils.tracing import ROCTX, StepProfiler
 
 log = logging.getLogger(__name__)
@@ -72,6 +73,10 @@ class LLMEngine:
         # MXS_STEP_TIMING=1: host seconds per phase (schedule / launch / collect wait / land)
         self.step_times: Optional[dict] = ({"schedule": 0.0, "launch": 0.0, "collect": 0.0, "land": 0.0,
                                             "steps": 0} if os.environ.get("MXS_STEP_TIMING") == "1" else None)
+        # the start-up heap (torch, graphs, weights' Python side) goes to the permanent generation: a
+        # full collection over it stalled the step loop ~110 ms at a time (utils/gcpause.py)
+        if self.runner.is_gpu:
+            gcpause.freeze_heap()
 
     # ------------------------------------------------------------------ requests
     def add_request(self, prompt_token_ids: list, sampling: Optional[SamplingParams] = None,
@@ -269,6 +274,7 @@ class LLMEngine:
         self._inflight = None
         self.requests.clear()
         self.runner.close()
+        gcpause.unfreeze_heap()  # this engine's cycles were frozen with it: collectable again
 
 
 class AsyncEngine:
