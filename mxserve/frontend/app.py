@@ -994,6 +994,8 @@ class Frontend:
 def serve_app(fe: Frontend, host: str = "0.0.0.0", port: int = 8000, sock=None) -> None:
     """Serve a Frontend until SIGTERM / SIGINT: our HTTP/1.1 server with the push-streaming fast
     path (httpd.py + fastpath.py; the default), or uvicorn (MXS_FRONTEND_SERVER=uvicorn)."""
+    from ..utils.gcpause import freeze_heap
+    freeze_heap()  # no full collections over the start-up heap while streaming (utils/gcpause.py)
     if os.environ.get("MXS_FRONTEND_SERVER", "httpd") == "uvicorn":
         import uvicorn
         if sock is not None:

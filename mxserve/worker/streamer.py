@@ -287,6 +287,8 @@ def main(argv=None) -> None:
     setup_logging()
     rt = _native.rt()
     cmd, out = rt.ShmRing(a.cmd, False), rt.ShmRing(a.out, False)
+    from ..utils.gcpause import freeze_heap
+    freeze_heap()  # the SSE loop of every stream runs here: keep full collections off it
     uvicorn.run(build_app(cmd, out, a.parent_pid), host=a.host, port=a.port, log_level="warning", access_log=False)
 
 
