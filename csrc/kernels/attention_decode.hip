@@ -407,7 +407,8 @@ __global__ void __launch_bounds__(256) paged_decode_mfma_kernel(
     bf16_t* __restrict__ out, float* __restrict__ tmp_out, float* __restrict__ tmp_ml,
     const bf16_t* __restrict__ q, const void* __restrict__ kv, long block_stride,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ seq_lens, int Hkv,
-    float scale, int part_len, float v_scale) {
+    float scale, int part_len, float v_scale, int q_stride, const int64_t* __restrict__ qpos_tab,
+    const float* __restrict__ cos_sin) {
   constexpr int KS = D / 32;  // k-steps of S = K Q^T
   constexpr int DT = D / 16;  // 16-dim tiles of O^T
   static_assert(G <= 16, "query heads of a kv head must fit the 16 MFMA columns");
@@ -426,26 +427,51 @@ __global__ void __launch_bounds__(256) paged_decode_mfma_kernel(
   __shared__ float red_m[kWaves][G], red_l[kWaves][G];
   __shared__ __attribute__((aligned(16))) float red_o[kWaves][G][D];
 
-  // Q^T (B operand): lane holds dims 32 ks + 8 qd .. +7 of head c, pre-scaled for exp2
+  // Q^T (B operand): lane holds dims 32 ks + 8 qd .. +7 of head c, pre-scaled for exp2.  q rows are
+  // q_stride elements apart (the fused qkv output when the caller skipped the rope kernel's q write);
+  // cos_sin != nullptr rotates them here: chunks ks and ks + KS / 2 are dims d and d + D / 2
   bf16x8d_t qf[KS];
   {
     const float qs = scale * kLog2e;
+    float x[KS][8];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       if (c < G) {
-        const uint4 v = *reinterpret_cast<const uint4*>(q + (static_cast<size_t>(seq) * Hq + kvh * G + c) * D +
+        const uint4 v = *reinterpret_cast<const uint4*>(q + static_cast<size_t>(seq) * q_stride + (kvh * G + c) * D +
                                                         32 * ks + 8 * qd);
         const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          qf[ks][2 * k] = static_cast<__bf16>(bf2f_lo(w[k]) * qs);
-          qf[ks][2 * k + 1] = static_cast<__bf16>(bf2f_hi(w[k]) * qs);
+          x[ks][2 * k] = bf2f_lo(w[k]);
+          x[ks][2 * k + 1] = bf2f_hi(w[k]);
         }
       } else {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) qf[ks][k] = static_cast<__bf16>(0.f);
+        for (int k = 0; k < 8; ++k) x[ks][k] = 0.f;
       }
     }
+    if (cos_sin != nullptr && c < G) {
+      const float* cs = cos_sin + qpos_tab[seq] * D;
+#pragma unroll
+      for (int ks = 0; ks < KS / 2; ++ks) {
+        const int d0 = 32 * ks + 8 * qd;
+        float cv[8], sv[8];
+        *reinterpret_cast<float4*>(cv) = *reinterpret_cast<const float4*>(cs + d0);
+        *reinterpret_cast<float4*>(cv + 4) = *reinterpret_cast<const float4*>(cs + d0 + 4);
+        *reinterpret_cast<float4*>(sv) = *reinterpret_cast<const float4*>(cs + D / 2 + d0);
+        *reinterpret_cast<float4*>(sv + 4) = *reinterpret_cast<const float4*>(cs + D / 2 + d0 + 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x1 = x[ks][j], x2 = x[ks + KS / 2][j];
+          x[ks][j] = bf2f(f2bf(x1 * cv[j] - x2 * sv[j]));
+          x[ks + KS / 2][j] = bf2f(f2bf(x2 * cv[j] + x1 * sv[j]));
+        }
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) qf[ks][k] = static_cast<__bf16>(x[ks][k] * qs);
   }
   const int* btp = block_tables + static_cast<size_t>(seq) * bt_stride;
   const char* kbase = reinterpret_cast<const char*>(kv) + static_cast<size_t>(kvh) * kBS * D * EB;
@@ -644,36 +670,41 @@ int decode_num_partitions(int max_seq_len) {
 // 0.323 ms = 6.5 TB/s, 8B bf16 0.371 -> 0.324 ms, 1B fp8 0.275 -> 0.202 ms, 70B-TP8 shard (G 8)
 // 0.136 -> 0.098 ms); at G <= 2 the MFMA columns are mostly padding and the VALU kernel is as fast
 // or faster (Qwen3-0.6B bf16 0.631 vs 0.636 ms, fp8 0.358 vs 0.545 ms).
-void launch_paged_decode(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, const void* kv, bool kv_fp8,
+// q_stride / qpos / cos_sin: see paged_decode_mfma_kernel (the MFMA kernel only; a strided or
+// un-rotated q forces it).  Returns false when asked for that with an unsupported shape.
+bool launch_paged_decode(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_t* q, const void* kv, bool kv_fp8,
                          long block_stride, const int* block_tables, int bt_stride, const int* seq_lens, int B,
                          int Hq, int Hkv, int D, int P, int part_len, float scale, float k_scale, float v_scale,
-                         int impl, hipStream_t s) {
-  if (B == 0) return;
+                         int impl, hipStream_t s, int q_stride, const int64_t* qpos, const float* cos_sin) {
+  if (B == 0) return true;
   const int G = Hq / Hkv;
   dim3 grid(Hkv, B, P), blk(256);
   if (kv_fp8) scale *= k_scale;
   else v_scale = 1.f;
-  const bool mfma = impl == 2 || (impl == 0 && G >= 4);
+  if (q_stride <= 0) q_stride = Hq * D;
+  const bool fused_q = cos_sin != nullptr || q_stride != Hq * D;
+  const bool mfma = fused_q || impl == 2 || (impl == 0 && G >= 4);
   if (mfma) {
 #define MXS_DECM(DD, GG)                                                                                   \
     if (D == DD && G == GG) {                                                                              \
       if (kv_fp8)                                                                                          \
         hipLaunchKernelGGL((paged_decode_mfma_kernel<DD, GG, 1>), grid, blk, 0, s, out, tmp_out, tmp_ml, q,  \
                            kv, block_stride, block_tables, bt_stride, seq_lens, Hkv, scale, part_len,      \
-                           v_scale);                                                                       \
+                           v_scale, q_stride, qpos, cos_sin);                                              \
       else                                                                                                 \
         hipLaunchKernelGGL((paged_decode_mfma_kernel<DD, GG, 2>), grid, blk, 0, s, out, tmp_out, tmp_ml, q,  \
                            kv, block_stride, block_tables, bt_stride, seq_lens, Hkv, scale, part_len,      \
-                           v_scale);                                                                       \
+                           v_scale, q_stride, qpos, cos_sin);                                              \
       if (P > 1)                                                                                           \
         hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(Hq, B), dim3(DD), 0, s, out, tmp_out,   \
                            tmp_ml, seq_lens, Hq, P, part_len);                                             \
       MXS_CHECK_LAUNCH();                                                                                  \
-      return;                                                                                              \
+      return true;                                                                                         \
     }
     MXS_DECM(64, 1) MXS_DECM(64, 2) MXS_DECM(64, 4) MXS_DECM(64, 8)
     MXS_DECM(128, 1) MXS_DECM(128, 2) MXS_DECM(128, 4) MXS_DECM(128, 8)
 #undef MXS_DECM
+    if (fused_q) return false;
   }
 #define MXS_DEC(DD, GG)                                                                                    \
   if (D == DD && G == GG) {                                                                                \
@@ -687,11 +718,12 @@ void launch_paged_decode(bf16_t* out, float* tmp_out, float* tmp_ml, const bf16_
       hipLaunchKernelGGL((paged_decode_reduce_kernel<DD>), dim3(Hq, B), dim3(DD), 0, s, out, tmp_out,     \
                          tmp_ml, seq_lens, Hq, P, part_len);                                               \
     MXS_CHECK_LAUNCH();                                                                                    \
-    return;                                                                                                \
+    return true;                                                                                           \
   }
   MXS_DEC(64, 1) MXS_DEC(64, 2) MXS_DEC(64, 4) MXS_DEC(64, 8)
   MXS_DEC(128, 1) MXS_DEC(128, 2) MXS_DEC(128, 4) MXS_DEC(128, 8)
 #undef MXS_DEC
+  return false;
 }
 
 }  // namespace mxs

@@ -58,23 +58,50 @@ __global__ void __launch_bounds__(256) paged_prefill_kernel(
   const bool rvalid = tok < ql;
   const int qpos = ctx0 + (rvalid ? tok : 0);
   const int wg_last_pos = ctx0 + min(t0 + BQ, ql) - 1;
+  const int q_stride = Hq * D;  // v2: dense q, no fused RoPE (launch_paged_prefill routes those to v3)
+  const int64_t* qpos_tab = nullptr;
+  const float* cos_sin = nullptr;
   const int nkeys = wg_last_pos + 1;
 
   // Q^T fragments (B operand): lane holds Q[row c][16 ks + 8 h + j], pre-scaled
   bf16x8_t qf[KS];
   {
-    const bf16_t* qp = q + (static_cast<size_t>(q0 + (rvalid ? tok : 0)) * Hq + head) * D + 8 * h;
+    const int qrow = q0 + (rvalid ? tok : 0);
+    const bf16_t* qp = q + static_cast<size_t>(qrow) * q_stride + head * D + 8 * h;
     const float qs = scale * kPLog2e;
+    float x[KS][8];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const uint4 v = *reinterpret_cast<const uint4*>(qp + 16 * ks);
       const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        qf[ks][2 * k] = static_cast<__bf16>(bf2f_lo(w[k]) * qs);
-        qf[ks][2 * k + 1] = static_cast<__bf16>(bf2f_hi(w[k]) * qs);
+        x[ks][2 * k] = bf2f_lo(w[k]);
+        x[ks][2 * k + 1] = bf2f_hi(w[k]);
       }
     }
+    if (cos_sin != nullptr) {
+      const float* cs = cos_sin + qpos_tab[qrow] * D;
+#pragma unroll
+      for (int ks = 0; ks < KS / 2; ++ks) {
+        const int d0 = 16 * ks + 8 * h;  // 8 consecutive dims: two 16-byte loads each of cos and sin
+        float cv[8], sv[8];
+        *reinterpret_cast<float4*>(cv) = *reinterpret_cast<const float4*>(cs + d0);
+        *reinterpret_cast<float4*>(cv + 4) = *reinterpret_cast<const float4*>(cs + d0 + 4);
+        *reinterpret_cast<float4*>(sv) = *reinterpret_cast<const float4*>(cs + D / 2 + d0);
+        *reinterpret_cast<float4*>(sv + 4) = *reinterpret_cast<const float4*>(cs + D / 2 + d0 + 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x1 = x[ks][j], x2 = x[ks + KS / 2][j];
+          x[ks][j] = bf2f(f2bf(x1 * cv[j] - x2 * sv[j]));
+          x[ks + KS / 2][j] = bf2f(f2bf(x2 * cv[j] + x1 * sv[j]));
+        }
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[ks][j] = static_cast<__bf16>(x[ks][j] * qs);
   }
 
   const int* bt = block_tables + static_cast<size_t>(seq) * bt_stride;
@@ -261,11 +288,17 @@ __device__ __forceinline__ uint4 ld8_kv(const char* p) {
     return fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(p));
 }
 
+// Q rows read straight from the fused qkv projection output (row stride q_stride elements) with the
+// rotate-half RoPE applied here when cos_sin != nullptr (the rope kernel then writes only K / V: the
+// [T, Hq, D] q tensor and its write + re-read disappear).  A lane's chunks ks and ks + KS / 2 hold
+// dims d and d + D / 2, i.e. both halves of its rotation pairs.  q is rounded to bf16 after the
+// rotation, as the standalone rope kernel stores it.
 template <int D, int G, int EB>
 __global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const void* __restrict__ kv, long block_stride,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ qsl,
-    const int* __restrict__ seq_lens, int Hkv, float scale, float v_scale) {
+    const int* __restrict__ seq_lens, int Hkv, float scale, float v_scale, int q_stride,
+    const int64_t* __restrict__ qpos_tab, const float* __restrict__ cos_sin) {
   constexpr int KS = D / 16, DT = D / 32;
   constexpr int BQ = 256 / G;        // query tokens per workgroup
   constexpr int KT = 64;             // keys per tile
@@ -302,18 +335,42 @@ __global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
 
   bf16x8_t qf[KS];
   {
-    const bf16_t* qp = q + (static_cast<size_t>(q0 + (rvalid ? tok : 0)) * Hq + head) * D + 8 * h;
+    const int qrow = q0 + (rvalid ? tok : 0);
+    const bf16_t* qp = q + static_cast<size_t>(qrow) * q_stride + head * D + 8 * h;
     const float qs = scale * kPLog2e;
+    float x[KS][8];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const uint4 v = *reinterpret_cast<const uint4*>(qp + 16 * ks);
       const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        qf[ks][2 * k] = static_cast<__bf16>(bf2f_lo(w[k]) * qs);
-        qf[ks][2 * k + 1] = static_cast<__bf16>(bf2f_hi(w[k]) * qs);
+        x[ks][2 * k] = bf2f_lo(w[k]);
+        x[ks][2 * k + 1] = bf2f_hi(w[k]);
       }
     }
+    if (cos_sin != nullptr) {
+      const float* cs = cos_sin + qpos_tab[qrow] * D;
+#pragma unroll
+      for (int ks = 0; ks < KS / 2; ++ks) {
+        const int d0 = 16 * ks + 8 * h;  // 8 consecutive dims: two 16-byte loads each of cos and sin
+        float cv[8], sv[8];
+        *reinterpret_cast<float4*>(cv) = *reinterpret_cast<const float4*>(cs + d0);
+        *reinterpret_cast<float4*>(cv + 4) = *reinterpret_cast<const float4*>(cs + d0 + 4);
+        *reinterpret_cast<float4*>(sv) = *reinterpret_cast<const float4*>(cs + D / 2 + d0);
+        *reinterpret_cast<float4*>(sv + 4) = *reinterpret_cast<const float4*>(cs + D / 2 + d0 + 4);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x1 = x[ks][j], x2 = x[ks + KS / 2][j];
+          x[ks][j] = bf2f(f2bf(x1 * cv[j] - x2 * sv[j]));
+          x[ks + KS / 2][j] = bf2f(f2bf(x2 * cv[j] + x1 * sv[j]));
+        }
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[ks][j] = static_cast<__bf16>(x[ks][j] * qs);
   }
 
   const int* bt = block_tables + static_cast<size_t>(seq) * bt_stride;
@@ -484,24 +541,30 @@ __global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
     }
 }
 
+// q_stride: elements between consecutive q rows (Hq * D for a dense q; (Hq + 2 Hkv) * D when q is
+// read from the fused qkv output); cos_sin != nullptr applies RoPE at positions qpos (v3 only).
 void launch_paged_prefill(bf16_t* out, const bf16_t* q, const void* kv_ptr, bool kv_fp8, long block_stride,
                           const int* block_tables, int bt_stride, const int* qsl, const int* seq_lens,
                           int num_seqs, int max_q_len, int Hq, int Hkv, int D, float scale, int version,
-                          float k_scale, float v_scale, hipStream_t s) {
+                          float k_scale, float v_scale, hipStream_t s, int q_stride, const int64_t* qpos,
+                          const float* cos_sin) {
   if (num_seqs == 0 || max_q_len == 0) return;
   const int G = Hq / Hkv;
   const bf16_t* kv = static_cast<const bf16_t*>(kv_ptr);
-  if (version != 2 || kv_fp8) {  // the fp8 cache has the v3 path only
+  if (q_stride <= 0) q_stride = Hq * D;
+  if (version != 2 || kv_fp8 || cos_sin != nullptr || q_stride != Hq * D) {  // fp8 / fused q: the v3 path only
     dim3 grid3((max_q_len + 256 / G - 1) / (256 / G), Hkv, num_seqs), blk3(512);
     const float sc = kv_fp8 ? scale * k_scale : scale, vs = kv_fp8 ? v_scale : 1.f;
 #define MXS_PF3(DD, GG)                                                                                    \
     if (D == DD && G == GG) {                                                                              \
       if (kv_fp8)                                                                                          \
         hipLaunchKernelGGL((paged_prefill_v3_kernel<DD, GG, 1>), grid3, blk3, 0, s, out, q, kv_ptr,        \
-                           block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs);             \
+                           block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs, q_stride,    \
+                           qpos, cos_sin);                                                                 \
       else                                                                                                 \
         hipLaunchKernelGGL((paged_prefill_v3_kernel<DD, GG, 2>), grid3, blk3, 0, s, out, q, kv_ptr,        \
-                           block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs);             \
+                           block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs, q_stride,    \
+                           qpos, cos_sin);                                                                 \
       MXS_CHECK_LAUNCH();                                                                                  \
       return;                                                                                              \
     }

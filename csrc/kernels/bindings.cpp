@@ -17,10 +17,12 @@ void launch_rope_and_cache(bf16_t*, const bf16_t*, const int64_t*, const float*,
                            const bf16_t*, const bf16_t*, int, int, int, int, int, float, float, float, hipStream_t);
 int decode_num_partitions(int);
 void decode_plan(int, int, int, int*, int*);
-void launch_paged_decode(bf16_t*, float*, float*, const bf16_t*, const void*, bool, long, const int*, int, const int*,
-                         int, int, int, int, int, int, float, float, float, int, hipStream_t);
+bool launch_paged_decode(bf16_t*, float*, float*, const bf16_t*, const void*, bool, long, const int*, int, const int*,
+                         int, int, int, int, int, int, float, float, float, int, hipStream_t, int = 0,
+                         const int64_t* = nullptr, const float* = nullptr);
 void launch_paged_prefill(bf16_t*, const bf16_t*, const void*, bool, long, const int*, int, const int*, const int*,
-                          int, int, int, int, int, float, int, float, float, hipStream_t);
+                          int, int, int, int, int, float, int, float, float, hipStream_t, int = 0,
+                          const int64_t* = nullptr, const float* = nullptr);
 void launch_sample(int64_t*, const void*, bool, int, int, long, const float*, const float*, const int*,
                    const int64_t*, const int64_t*, hipStream_t);
 void launch_logprobs(float*, int64_t*, float*, const void*, bool, int, int, long, const int64_t*, const int64_t*, int,
@@ -121,17 +123,25 @@ bool check_kv(const at::Tensor& kv, int Hkv, int D) {
   return fp8;
 }
 
-void rope_and_cache(at::Tensor q_out, at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin, at::Tensor kv,
-                    at::Tensor slot_mapping, std::optional<at::Tensor> qn, std::optional<at::Tensor> kn, int64_t Hq,
-                    int64_t Hkv, int64_t D, double eps, double k_scale, double v_scale) {
-  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_CONTIG(qkv); CHECK_CONTIG(q_out);
+// q_out None: K / V into the cache only (q stays in the qkv rows for the attention kernels' fused RoPE)
+void rope_and_cache(std::optional<at::Tensor> q_out, at::Tensor qkv, at::Tensor positions, at::Tensor cos_sin,
+                    at::Tensor kv, at::Tensor slot_mapping, std::optional<at::Tensor> qn, std::optional<at::Tensor> kn,
+                    int64_t Hq, int64_t Hkv, int64_t D, double eps, double k_scale, double v_scale) {
+  CHECK_CUDA(qkv); CHECK_BF16(qkv); CHECK_CONTIG(qkv);
+  if (q_out.has_value()) {
+    CHECK_CONTIG((*q_out));
+    TORCH_CHECK(q_out->numel() == qkv.size(0) * Hq * D, "q_out shape");
+  } else {
+    TORCH_CHECK(!qn.has_value(), "q/k norm needs the rope kernel to write q");
+  }
   TORCH_CHECK(positions.scalar_type() == at::kLong && slot_mapping.scalar_type() == at::kLong, "int64 indices");
   TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.size(1) == D, "cos_sin must be fp32 [P, D]");
   TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv width mismatch");
   const bool fp8 = check_kv(kv, Hkv, D);
   const bf16_t* qnp = qn.has_value() ? bf(*qn) : nullptr;
   const bf16_t* knp = kn.has_value() ? bf(*kn) : nullptr;
-  mxs::launch_rope_and_cache(bf(q_out), bf(qkv), positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
+  mxs::launch_rope_and_cache(q_out.has_value() ? bf(*q_out) : nullptr, bf(qkv), positions.data_ptr<int64_t>(),
+                             cos_sin.data_ptr<float>(),
                              kv.data_ptr(), fp8, kv.stride(0), slot_mapping.data_ptr<int64_t>(), qnp, knp, qkv.size(0),
                              Hq, Hkv, D, 16, static_cast<float>(eps), static_cast<float>(k_scale),
                              static_cast<float>(v_scale), stream());
@@ -158,10 +168,36 @@ bool splitk_rope_and_cache(at::Tensor q_out, at::Tensor part, int64_t S, int64_t
                                            static_cast<float>(k_scale), static_cast<float>(v_scale), stream());
 }
 
+// q [T, Hq, D]: dense, or a row-strided view of the fused qkv output (q = qkv[:, :Hq * D]); with
+// rope_pos / cos_sin the kernel applies RoPE to q itself (the rope kernel wrote only K / V).
+struct QArg {
+  int stride = 0;
+  const int64_t* pos = nullptr;
+  const float* cs = nullptr;
+};
+QArg q_arg(const at::Tensor& q, const std::optional<at::Tensor>& rope_pos, const std::optional<at::Tensor>& cos_sin) {
+  CHECK_CUDA(q); CHECK_BF16(q);
+  TORCH_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "q rows: [T, Hq, D] with dense heads");
+  TORCH_CHECK(q.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(q.data_ptr()) & 15) == 0, "q rows 16-byte aligned");
+  QArg a;
+  a.stride = static_cast<int>(q.stride(0));
+  TORCH_CHECK(rope_pos.has_value() == cos_sin.has_value(), "rope_pos and cos_sin go together");
+  if (cos_sin.has_value()) {
+    TORCH_CHECK(rope_pos->scalar_type() == at::kLong && rope_pos->is_contiguous() && rope_pos->numel() >= q.size(0),
+                "rope_pos: int64 [T]");
+    TORCH_CHECK(cos_sin->scalar_type() == at::kFloat && cos_sin->is_contiguous() && cos_sin->size(1) == q.size(2),
+                "cos_sin: fp32 [P, D]");
+    a.pos = rope_pos->data_ptr<int64_t>();
+    a.cs = cos_sin->data_ptr<float>();
+  }
+  return a;
+}
+
 void paged_attention_decode(at::Tensor out, at::Tensor q, at::Tensor kv, at::Tensor block_tables,
                             at::Tensor seq_lens, double scale, int64_t max_seq_len, double k_scale, double v_scale,
-                            int64_t impl) {
-  CHECK_CUDA(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_CONTIG(out);
+                            int64_t impl, std::optional<at::Tensor> rope_pos, std::optional<at::Tensor> cos_sin) {
+  const QArg qa = q_arg(q, rope_pos, cos_sin);
+  CHECK_CONTIG(out);
   const int B = q.size(0), Hq = q.size(1), D = q.size(2);
   const int Hkv = kv.size(2);
   const bool fp8 = check_kv(kv, Hkv, D);
@@ -175,18 +211,20 @@ void paged_attention_decode(at::Tensor out, at::Tensor q, at::Tensor kv, at::Ten
     tmp_out = at::empty({B, Hq, P, D}, q.options().dtype(at::kFloat));
     tmp_ml = at::empty({B, Hq, P, 2}, q.options().dtype(at::kFloat));
   }
-  mxs::launch_paged_decode(bf(out), P > 1 ? tmp_out.data_ptr<float>() : nullptr,
-                           P > 1 ? tmp_ml.data_ptr<float>() : nullptr, bf(q), kv.data_ptr(), fp8, kv.stride(0),
-                           block_tables.data_ptr<int>(), block_tables.stride(0), seq_lens.data_ptr<int>(), B, Hq,
-                           Hkv, D, P, /*part_len: split each sequence evenly*/ 0, static_cast<float>(scale),
-                           static_cast<float>(k_scale), static_cast<float>(v_scale), static_cast<int>(impl),
-                           stream());
+  const bool ok = mxs::launch_paged_decode(
+      bf(out), P > 1 ? tmp_out.data_ptr<float>() : nullptr, P > 1 ? tmp_ml.data_ptr<float>() : nullptr, bf(q),
+      kv.data_ptr(), fp8, kv.stride(0), block_tables.data_ptr<int>(), block_tables.stride(0), seq_lens.data_ptr<int>(),
+      B, Hq, Hkv, D, P, /*part_len: split each sequence evenly*/ 0, static_cast<float>(scale),
+      static_cast<float>(k_scale), static_cast<float>(v_scale), static_cast<int>(impl), stream(), qa.stride, qa.pos,
+      qa.cs);
+  TORCH_CHECK(ok, "paged_attention_decode: no kernel for this head shape (fused q needs the MFMA kernel)");
 }
 
 void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Tensor block_tables, at::Tensor qsl,
                              at::Tensor seq_lens, double scale, int64_t max_q_len, int64_t version, double k_scale,
-                             double v_scale) {
-  CHECK_CUDA(q); CHECK_BF16(q); CHECK_CONTIG(q); CHECK_CONTIG(out);
+                             double v_scale, std::optional<at::Tensor> rope_pos, std::optional<at::Tensor> cos_sin) {
+  const QArg qa = q_arg(q, rope_pos, cos_sin);
+  CHECK_CONTIG(out);
   const int Hq = q.size(1), D = q.size(2);
   const int Hkv = kv.size(2);
   const bool fp8 = check_kv(kv, Hkv, D);
@@ -197,7 +235,7 @@ void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Te
                             block_tables.stride(0), qsl.data_ptr<int>(), seq_lens.data_ptr<int>(), S,
                             static_cast<int>(max_q_len), Hq, Hkv, D, static_cast<float>(scale),
                             static_cast<int>(version), static_cast<float>(k_scale), static_cast<float>(v_scale),
-                            stream());
+                            stream(), qa.stride, qa.pos, qa.cs);
 }
 
 void sample(at::Tensor out, at::Tensor logits, at::Tensor temperature, at::Tensor top_p, at::Tensor top_k,
@@ -433,11 +471,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("paged_attention_decode", &paged_attention_decode, pybind11::arg("out"), pybind11::arg("q"),
         pybind11::arg("kv"), pybind11::arg("block_tables"), pybind11::arg("seq_lens"), pybind11::arg("scale"),
         pybind11::arg("max_seq_len"), pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0,
-        pybind11::arg("impl") = 0);
+        pybind11::arg("impl") = 0, pybind11::arg("rope_pos") = pybind11::none(),
+        pybind11::arg("cos_sin") = pybind11::none());
   m.def("paged_attention_prefill", &paged_attention_prefill, pybind11::arg("out"), pybind11::arg("q"),
         pybind11::arg("kv"), pybind11::arg("block_tables"), pybind11::arg("qsl"), pybind11::arg("seq_lens"),
         pybind11::arg("scale"), pybind11::arg("max_q_len"), pybind11::arg("version") = 3,
-        pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0);
+        pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0, pybind11::arg("rope_pos") = pybind11::none(),
+        pybind11::arg("cos_sin") = pybind11::none());
   m.def("sample", &sample);
   m.def("logprobs", &logprobs);
   m.def("apply_penalties", &apply_penalties);

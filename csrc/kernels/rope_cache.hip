@@ -51,12 +51,14 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
     kblk = kv + (slot / BS) * block_stride;
     off = static_cast<int>(slot % BS);
   }
-  // rotary part: (Hq + Hkv) heads x HALF pairs; a head's pairs are HALF consecutive lanes
-  const int n_items = (Hq + Hkv) * HALF;
+  // rotary part: (Hq + Hkv) heads x HALF pairs; a head's pairs are HALF consecutive lanes.  q_out ==
+  // nullptr: K / V only (the attention kernels read q from the qkv rows and rotate it themselves)
+  const int hbeg = q_out != nullptr ? 0 : Hq;
+  const int n_items = (Hq + Hkv - hbeg) * HALF;
   for (int base = 0; base < n_items; base += blockDim.x) {
     const int i = base + threadIdx.x;
     const bool active = i < n_items;
-    const int head = active ? i / HALF : 0;
+    const int head = hbeg + (active ? i / HALF : 0);
     const int p = i % HALF;
     float x1 = 0.f, x2 = 0.f;
     if (active) {
@@ -126,7 +128,8 @@ __global__ void __launch_bounds__(256) rope_cache_t16_kernel(
   __shared__ int s_fast;
   const int t0 = blockIdx.x * TPB, nt = min(TPB, T - t0);
   const int row_stride = (Hq + 2 * Hkv) * D, hkd = Hkv * D;
-  const int per_tok = (Hq + Hkv) * V4;
+  const int hbeg = q_out != nullptr ? 0 : Hq;  // nullptr: K / V only (see rope_cache_kernel)
+  const int per_tok = (Hq + Hkv - hbeg) * V4;
   if (threadIdx.x == 0) {
     const int64_t s0 = slot_mapping[t0];
     int fast = s0 >= 0 && (s0 % BS) + nt <= BS;
@@ -135,7 +138,7 @@ __global__ void __launch_bounds__(256) rope_cache_t16_kernel(
     s_fast = fast;
   }
   for (int i = threadIdx.x; i < nt * per_tok; i += blockDim.x) {
-    const int tt = i / per_tok, rem = i - tt * per_tok, head = rem / V4, p = (rem - head * V4) * 4;
+    const int tt = i / per_tok, rem = i - tt * per_tok, hh = rem / V4, p = (rem - hh * V4) * 4, head = hbeg + hh;
     const int t = t0 + tt;
     const bf16_t* src = qkv + static_cast<size_t>(t) * row_stride + head * D;
     const uint2 a = *reinterpret_cast<const uint2*>(src + p), b = *reinterpret_cast<const uint2*>(src + p + HALF);

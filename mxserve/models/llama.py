@@ -175,27 +175,44 @@ class TransformerLM:
         return self.w["lm_head"]
 
     # ------------------------------------------------------------------ forward
+    def _fused_q_rope(self, h: torch.Tensor, i: int) -> bool:
+        """Prefill / mixed steps on the GPU (hipBLASLt qkv, M > 256): the rope kernel writes only K / V
+        and both attention kernels read q from the qkv rows and rotate it while loading it (one
+        [T, Hq, D] write + read less per layer).  Needs the MFMA decode kernel (G >= 4) and no q/k
+        norm; MXS_FUSED_Q_ROPE=0 turns it off."""
+        return (_FUSED_Q_ROPE and h.is_cuda and h.shape[0] > 256 and not self.cfg.qk_norm and
+                self.hd in (64, 128) and self.nh // self.nkv >= 4 and self.nh % self.nkv == 0)
+
     def _attention(self, i: int, h: torch.Tensor, md: AttnMetadata, kv_layer: torch.Tensor, project: bool = True):
         c, w, p = self.cfg, self.w, f"l{i}."
-        q = ops.linear_rope_and_cache(h, w[p + "qkv"], self.nh, self.nkv, self.hd, md.positions, self.cos_sin,
-                                      kv_layer, md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"),
-                                      c.rms_norm_eps, **self.kv_scales[i])
+        rope = None
+        if self._fused_q_rope(h, i):
+            q = ops.rope_kv_into_cache(ops.linear(h, w[p + "qkv"]), self.nh, self.nkv, self.hd, md.positions,
+                                       self.cos_sin, kv_layer, md.slot_mapping, **self.kv_scales[i])
+            rope = (md.positions, self.cos_sin)
+        else:
+            q = ops.linear_rope_and_cache(h, w[p + "qkv"], self.nh, self.nkv, self.hd, md.positions, self.cos_sin,
+                                          kv_layer, md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"),
+                                          c.rms_norm_eps, **self.kv_scales[i])
         nd = md.num_decodes
         if not q.is_cuda:
             o = ref.paged_attention(q, kv_layer, md.block_tables, md.query_start_loc, md.seq_lens, self.scale,
                                     **self.kv_scales[i])
         elif md.num_prefills == 0:
             o = ops.paged_attention_decode(q, kv_layer, md.block_tables, md.seq_lens, self.scale,
-                                           md.max_seq_len, **self.kv_scales[i])
+                                           md.max_seq_len, rope=rope, **self.kv_scales[i])
         elif nd == 0:
             o = ops.paged_attention_prefill(q, kv_layer, md.block_tables, md.query_start_loc,
-                                            md.seq_lens, self.scale, md.max_query_len, **self.kv_scales[i])
+                                            md.seq_lens, self.scale, md.max_query_len, rope=rope, **self.kv_scales[i])
         else:
-            o = torch.empty_like(q)
+            o = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+            rd = rp = None
+            if rope is not None:
+                rd, rp = (md.positions[:nd], self.cos_sin), (md.positions[nd:], self.cos_sin)
             ops.paged_attention_decode(q[:nd], kv_layer, md.block_tables[:nd], md.seq_lens[:nd], self.scale,
-                                       md.max_seq_len, out=o[:nd], **self.kv_scales[i])
+                                       md.max_seq_len, out=o[:nd], rope=rd, **self.kv_scales[i])
             ops.paged_attention_prefill(q[nd:], kv_layer, md.block_tables[nd:], md.prefill_query_start_loc,
-                                        md.seq_lens[nd:], self.scale, md.max_query_len, out=o[nd:],
+                                        md.seq_lens[nd:], self.scale, md.max_query_len, out=o[nd:], rope=rp,
                                         **self.kv_scales[i])
         if not project:  # the caller fuses o_proj with the residual add + next norm
             return o.reshape(o.shape[0], -1)
@@ -330,6 +347,9 @@ class TransformerLM:
         if self.tp_size > 1:
             logits = tp_all_gather(logits, dim=-1)
         return logits[:, :self.cfg.vocab_size]
+
+
+_FUSED_Q_ROPE = os.environ.get("MXS_FUSED_Q_ROPE", "1") == "1"
 
 
 def _pad_rows(t: torch.Tensor, n: int) -> torch.Tensor:

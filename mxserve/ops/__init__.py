@@ -250,32 +250,51 @@ def linear_rope_and_cache(h: torch.Tensor, w: torch.Tensor, num_heads: int, num_
                           q_norm_w, k_norm_w, eps, k_scale, v_scale)
 
 
+def rope_kv_into_cache(qkv: torch.Tensor, num_heads: int, num_kv_heads: int, head_dim: int,
+                       positions: torch.Tensor, cos_sin: torch.Tensor, kv_layer: torch.Tensor,
+                       slot_mapping: torch.Tensor, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
+    """rope_and_cache without the q write (GPU): RoPE on k, K / V into the paged cache; returns the
+    un-rotated q as a row-strided view of qkv, for the attention ops' `rope=` argument."""
+    ext().rope_and_cache(None, qkv, positions, cos_sin, kv_layer, slot_mapping, None, None, num_heads, num_kv_heads,
+                         head_dim, 1e-6, k_scale, v_scale)
+    return qkv[:, :num_heads * head_dim].view(qkv.shape[0], num_heads, head_dim)
+
+
 def paged_attention_decode(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,
                            seq_lens: torch.Tensor, scale: float, max_seq_len: int,
                            out: Optional[torch.Tensor] = None, k_scale: float = 1.0,
-                           v_scale: float = 1.0, impl: Optional[int] = None) -> torch.Tensor:
+                           v_scale: float = 1.0, impl: Optional[int] = None, rope: Optional[tuple] = None) -> torch.Tensor:
     """One query token per sequence.  q [B, Hq, D] -> [B, Hq, D] (written into `out` if given).
     impl: 0 auto (MFMA kernel from G = 4 query heads per kv head), 1 VALU dot2, 2 MFMA;
-    MXS_DECODE_ATTN overrides the default."""
+    MXS_DECODE_ATTN overrides the default.  rope = (positions [B], cos_sin): q is un-rotated (a
+    strided view of the qkv rows) and the kernel applies RoPE while loading it."""
     if _gpu(q):
-        out = torch.empty_like(q) if out is None else out
+        out = torch.empty(q.shape, dtype=q.dtype, device=q.device) if out is None else out
+        rp, cs = rope if rope is not None else (None, None)
         ext().paged_attention_decode(out, q, kv_layer, block_tables, seq_lens, scale, max_seq_len, k_scale, v_scale,
-                                     _DECODE_IMPL if impl is None else impl)
+                                     _DECODE_IMPL if impl is None else impl, rp, cs)
         return out
+    if rope is not None:
+        q = ref.apply_rope(q, rope[0], rope[1])
     return ref.paged_attention_decode(q, kv_layer, block_tables, seq_lens, scale, k_scale, v_scale)
 
 
 def paged_attention_prefill(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,
                             query_start_loc: torch.Tensor, seq_lens: torch.Tensor, scale: float,
                             max_query_len: int, out: Optional[torch.Tensor] = None,
-                            version: int = 0, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
+                            version: int = 0, k_scale: float = 1.0, v_scale: float = 1.0,
+                            rope: Optional[tuple] = None) -> torch.Tensor:
     """Causal varlen attention of prefill chunks against the paged cache (prefix included).
-    version: 0 = default (v3, LDS-shared K/V tiles; MXS_PREFILL_KERNEL=2 selects v2), 2 or 3."""
+    version: 0 = default (v3, LDS-shared K/V tiles; MXS_PREFILL_KERNEL=2 selects v2), 2 or 3.
+    rope: as for paged_attention_decode (v3)."""
     if _gpu(q):
-        out = torch.empty_like(q) if out is None else out
+        out = torch.empty(q.shape, dtype=q.dtype, device=q.device) if out is None else out
+        rp, cs = rope if rope is not None else (None, None)
         ext().paged_attention_prefill(out, q, kv_layer, block_tables, query_start_loc, seq_lens,
-                                      scale, max_query_len, version or _PREFILL_VERSION, k_scale, v_scale)
+                                      scale, max_query_len, version or _PREFILL_VERSION, k_scale, v_scale, rp, cs)
         return out
+    if rope is not None:
+        q = ref.apply_rope(q, rope[0], rope[1])
     return ref.paged_attention(q, kv_layer, block_tables, query_start_loc, seq_lens, scale, k_scale, v_scale)
 
 

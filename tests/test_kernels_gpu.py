@@ -950,3 +950,78 @@ def test_linear_rope_and_cache_splitk(gpu, M, cfg, qknorm, monkeypatch):
     _close(q, q_ref, 0.03, 0.02, f"q {cfg}")
     _close(kv, kv_ref, 0.03, 0.02, f"kv cache {cfg}")
     assert kv[:, 0].abs().sum().item() == 0
+
+
+def _strided_q(T, hq, hkv, D, device):
+    """q as the attention ops see it on the fused-RoPE path: the first Hq * D columns of qkv rows."""
+    qkv = torch.randn(T, (hq + 2 * hkv) * D, device=device, dtype=torch.bfloat16)
+    return qkv, qkv[:, :hq * D].view(T, hq, D)
+
+
+@pytest.mark.parametrize("D,G", [(64, 4), (128, 4), (128, 8), (64, 8)])
+@pytest.mark.parametrize("kv_fp8", [False, True])
+def test_paged_decode_fused_rope(gpu, D, G, kv_fp8):
+    """Decode attention reading un-rotated q from the qkv rows and rotating it in the kernel == the
+    reference on the rotated q (the rope kernel's q write skipped)."""
+    hkv = 2
+    hq = hkv * G
+    lens = [513, 2000, 31, 4096, 1]
+    kv, bt = _paged_setup(lens, hkv, D, device=gpu)
+    B = len(lens)
+    _, q = _strided_q(B, hq, hkv, D, gpu)
+    pos = torch.tensor([l - 1 for l in lens], device=gpu)
+    cos_sin = ref.build_cos_sin_cache(D, 8192, 500000.0, None, device=gpu)
+    sl = torch.tensor(lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    cache = kv[:, 1]
+    sc = {}
+    if kv_fp8:
+        cache, sc = _fp8_cache(kv[:, 1].contiguous(), 0.05), {"k_scale": 0.05, "v_scale": 0.05}
+    out = ops.paged_attention_decode(q, cache, bt.to(gpu), sl.to(gpu), scale, max(lens), rope=(pos, cos_sin), **sc)
+    q_rot = ref.apply_rope(q.cpu().float(), pos.cpu(), cos_sin.cpu()).to(torch.bfloat16)
+    if kv_fp8:
+        exp = ref.paged_attention_decode(q_rot, cache.cpu(), bt, sl, scale, **sc)
+    else:
+        exp = ref.paged_attention_decode(q_rot, cache.cpu(), bt, sl, scale)
+    _close(out, exp, 0.02 * max(1.0, exp.abs().max().item()), 0.02, "decode fused rope")
+
+
+@pytest.mark.parametrize("D,G", [(64, 4), (128, 4), (128, 8)])
+def test_paged_prefill_fused_rope(gpu, D, G):
+    """Prefill v3 attention reading un-rotated q from the qkv rows (RoPE applied in the kernel)."""
+    hkv = 2
+    hq = hkv * G
+    specs = [(0, 77), (300, 45), (16, 1), (0, 130), (33, 200)]
+    seq_lens = [c + n for c, n in specs]
+    kv, bt = _paged_setup(seq_lens, hkv, D, device=gpu)
+    qsl = [0]
+    for _, n in specs:
+        qsl.append(qsl[-1] + n)
+    T = qsl[-1]
+    _, q = _strided_q(T, hq, hkv, D, gpu)
+    pos = torch.cat([torch.arange(c, c + n) for c, n in specs]).to(gpu)
+    cos_sin = ref.build_cos_sin_cache(D, 8192, 500000.0, None, device=gpu)
+    qsl_t = torch.tensor(qsl, dtype=torch.int32)
+    sl = torch.tensor(seq_lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    out = ops.paged_attention_prefill(q, kv[:, 1], bt.to(gpu), qsl_t.to(gpu), sl.to(gpu), scale,
+                                      max(n for _, n in specs), rope=(pos, cos_sin))
+    q_rot = ref.apply_rope(q.cpu().float(), pos.cpu(), cos_sin.cpu()).to(torch.bfloat16)
+    exp = ref.paged_attention(q_rot, kv[:, 1].cpu(), bt, qsl_t, sl, scale)
+    _close(out, exp, 0.03, 0.03, "prefill fused rope")
+
+
+@pytest.mark.parametrize("T", [37, 700])  # per-token kernel and the 16-token prefill kernel
+def test_rope_kv_only(gpu, T):
+    """rope_and_cache with no q output writes exactly the K / V the full kernel writes."""
+    D, hq, hkv, nb = 64, 32, 8, 64
+    cos_sin = ref.build_cos_sin_cache(D, 8192, 500000.0, None, device=gpu)
+    qkv = torch.randn(T, (hq + 2 * hkv) * D, device=gpu, dtype=torch.bfloat16)
+    pos = torch.randint(0, 8000, (T,), device=gpu)
+    slots = torch.arange(T, device=gpu) + 16
+    kv_a = torch.zeros(nb, 2, hkv, 16, D, device=gpu, dtype=torch.bfloat16)
+    kv_b = kv_a.clone()
+    ops.rope_and_cache(qkv, hq, hkv, D, pos, cos_sin, kv_a, slots)
+    q = ops.rope_kv_into_cache(qkv, hq, hkv, D, pos, cos_sin, kv_b, slots)
+    assert torch.equal(kv_a, kv_b)
+    assert q.data_ptr() == qkv.data_ptr() and q.stride(0) == qkv.shape[1]
