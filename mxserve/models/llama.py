@@ -181,7 +181,8 @@ class TransformerLM:
         [T, Hq, D] write + read less per layer).  Needs the MFMA decode kernel (G >= 4) and no q/k
         norm; MXS_FUSED_Q_ROPE=0 turns it off."""
         return (_FUSED_Q_ROPE and h.is_cuda and h.shape[0] > 256 and not self.cfg.qk_norm and
-                self.hd in (64, 128) and self.nh // self.nkv >= 4 and self.nh % self.nkv == 0)
+                self.hd in (64, 128) and self.nh // self.nkv >= 4 and self.nh % self.nkv == 0 and
+                not ops.qkv_uses_slabs(h, self.w[f"l{i}.qkv"]))
 
     def _attention(self, i: int, h: torch.Tensor, md: AttnMetadata, kv_layer: torch.Tensor, project: bool = True):
         c, w, p = self.cfg, self.w, f"l{i}."

@@ -90,19 +90,19 @@ def _gpu(t: torch.Tensor) -> bool:
 
 # ----------------------------------------------------------------------------- GEMM
 def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """y = x @ w.T.  Decode-sized GEMMs (M <= 256) run the hand-written MFMA kernel where the
+    """y = x @ w.T.  Decode-sized GEMMs (M <= decode_gemm.MAX_M) run the hand-written MFMA kernel where the
     tuning pass at graph capture measured it faster than hipBLASLt for that batch bucket and
     projection (mxserve/ops/decode_gemm.py); everything else is hipBLASLt."""
     if _gpu(x) and x.dim() == 2:
         M = x.shape[0]
-        if M <= 256:
-            from .decode_gemm import TABLE
-            cfg = TABLE.lookup(M, w.shape[0], w.shape[1], 0)
+        from . import decode_gemm
+        if M <= decode_gemm.MAX_M:
+            cfg = decode_gemm.TABLE.lookup(M, w.shape[0], w.shape[1], 0)
             if cfg is not None:
                 out = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
-                if TABLE.run(out, x, w, cfg, 0):
+                if decode_gemm.TABLE.run(out, x, w, cfg, 0):
                     return out
-        else:  # small prefill chunks: the 64/128-row tile kernel where it was measured faster
+        if M > 256:  # small prefill chunks: the 64/128-row tile kernel where it was measured faster
             from .decode_gemm import PREFILL_TABLE
             cfg = PREFILL_TABLE.lookup(M, w.shape[0], w.shape[1])
             if cfg is not None:
@@ -113,6 +113,11 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 
 _PG_PART: dict = {}
+
+
+def _decode_max_m() -> int:
+    from .decode_gemm import MAX_M
+    return MAX_M
 
 
 def prefill_gemm_configs(M: int, N: int, K: int) -> list:
@@ -136,7 +141,7 @@ def prefill_gemm(out: torch.Tensor, x: torch.Tensor, w: torch.Tensor, cfg: tuple
 def gate_up_silu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """silu(x @ gate.T) * (x @ up.T) with w = [gate; up] (K07 + K10).  Decode-sized: one MFMA kernel
     with SiLU*mul in its epilogue when tuned faster; otherwise hipBLASLt + the SiLU*mul kernel."""
-    if _gpu(x) and x.dim() == 2 and x.shape[0] <= 256:
+    if _gpu(x) and x.dim() == 2 and x.shape[0] <= _decode_max_m():
         from .decode_gemm import TABLE
         cfg = TABLE.lookup(x.shape[0], w.shape[0], w.shape[1], 1)
         if cfg is not None:
@@ -170,7 +175,7 @@ def linear_add_rms_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor
     the residual stream (o_proj, down_proj; TP = 1).  When the decode table runs this projection
     split-K, the fp32 slabs go straight into one epilogue kernel (sum + add + norm) instead of the
     split-K reduce kernel, a bf16 output and the fused add + RMSNorm kernel."""
-    if _gpu(x) and x.dim() == 2 and 0 < x.shape[0] <= 256:
+    if _gpu(x) and x.dim() == 2 and 0 < x.shape[0] <= _decode_max_m():
         from .decode_gemm import TABLE
         M, N = x.shape[0], w.shape[0]
         cfg = TABLE.lookup(M, N, w.shape[1], 0)
@@ -225,13 +230,23 @@ def rope_and_cache(qkv: torch.Tensor, num_heads: int, num_kv_heads: int, head_di
                               k_scale, v_scale)
 
 
+def qkv_uses_slabs(h: torch.Tensor, w: torch.Tensor) -> bool:
+    """Whether linear_rope_and_cache takes its split-K slab path for this qkv projection (then the rope
+    kernel reads the unreduced slabs and writes q itself)."""
+    if not (_gpu(h) and h.dim() == 2 and 0 < h.shape[0] <= _decode_max_m()):
+        return False
+    from .decode_gemm import TABLE
+    cfg = TABLE.lookup(h.shape[0], w.shape[0], w.shape[1], 0)
+    return cfg is not None and TABLE.splitk(cfg) > 1
+
+
 def linear_rope_and_cache(h: torch.Tensor, w: torch.Tensor, num_heads: int, num_kv_heads: int, head_dim: int,
                           positions: torch.Tensor, cos_sin: torch.Tensor, kv_layer: torch.Tensor,
                           slot_mapping: torch.Tensor, q_norm_w=None, k_norm_w=None, eps: float = 1e-6,
                           k_scale: float = 1.0, v_scale: float = 1.0):
     """qkv projection + rope_and_cache.  When the decode table runs the projection split-K, its fp32
     slabs feed the rope / cache-write kernel directly (no reduce kernel, no bf16 qkv round trip)."""
-    if _gpu(h) and h.dim() == 2 and 0 < h.shape[0] <= 256 and head_dim in (64, 128):
+    if _gpu(h) and h.dim() == 2 and 0 < h.shape[0] <= _decode_max_m() and head_dim in (64, 128):
         from .decode_gemm import TABLE
         M, N = h.shape[0], w.shape[0]
         cfg = TABLE.lookup(M, N, w.shape[1], 0)

@@ -59,6 +59,8 @@ def main():
                           "gate_up": (w["l0.gate_up"], 1), "down": (w["l0.down"], 0, norm),
                           "lm_head": (m.lm_head_weight(), 0)}, [B], dev)
         print({r["proj"]: r["cfg"] for r in decode_gemm.TABLE.report})
+        for r in decode_gemm.TABLE.report:  # per projection: the pick and both timings
+            print({k: r.get(k) for k in ("M", "proj", "chosen", "cfg", "us", "hipblaslt_us", "source")})
     ids_d = torch.randint(0, cfg.vocab_size, (B,), device=dev)
     ids_p = torch.randint(0, cfg.vocab_size, (T,), device=dev)
     with torch.inference_mode():
