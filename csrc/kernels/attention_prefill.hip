@@ -294,7 +294,8 @@ __device__ __forceinline__ uint4 ld8_kv(const char* p) {
 // dims d and d + D / 2, i.e. both halves of its rotation pairs.  q is rounded to bf16 after the
 // rotation, as the standalone rope kernel stores it.
 template <int D, int G, int EB>
-__global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(D == 64 ? 4 : 1, D == 64 ? 4 : 8)))
+paged_prefill_v3_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const void* __restrict__ kv, long block_stride,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ qsl,
     const int* __restrict__ seq_lens, int Hkv, float scale, float v_scale, int q_stride,
@@ -444,16 +445,29 @@ __global__ void __launch_bounds__(512) paged_prefill_v3_kernel(
     const float off = first ? 0.f : -m;
     float16_ sacc[2];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) sacc[kt][i] = off;
-      const int key = kt * 32 + c;
+    // K fragments two reads ahead of their MFMAs (sched_group_barrier pins the order: left alone,
+    // hipcc serialises read -> wait -> MFMA eight times per tile; 210.6 -> 205.5 us per layer at an
+    // 8192-token chunk).  The softmax below stays in scalar f32: packed v_pk_add_f32 beside MFMAs
+    // costs more than it saves (MI355X_MICROARCH: an anti-lever; measured 205.5 -> 223.9 us).
+    uint4 ka[2 * KS];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const uint4 a = *reinterpret_cast<const uint4*>(kl + key * KROW + (((2 * ks + h) ^ (key & 7)) << 4));
-        sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), qf[ks], sacc[kt], 0, 0, 0);
-      }
+    for (int idx = 0; idx < 2 * KS; ++idx) {
+      const int key = (idx / KS) * 32 + c, ks = idx % KS;
+      ka[idx] = *reinterpret_cast<const uint4*>(kl + key * KROW + (((2 * ks + h) ^ (key & 7)) << 4));
     }
+#pragma unroll
+    for (int idx = 0; idx < 2 * KS; ++idx)
+      sacc[idx / KS] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ka[idx]), qf[idx % KS], sacc[idx / KS], 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+    for (int idx = 0; idx < 2 * KS - 2; ++idx) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
     if (k0 + KT - 1 > wave_min_pos) {  // tile crosses the diagonal (or the end) of some row of this wave
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
