@@ -17,7 +17,10 @@ Phases (--mode auto: agg for N = 1, agg then disagg for N >= 2, both in the one 
           from the two roles' capacities for this workload (a decode GPU is KV-bandwidth bound at
           ~76 req/s, a prefill GPU computes ~118 req/s: 1P+1D at N = 2, 2P+2D at 4, 3P+5D at 8)
           and offers the node the rate that loads the tighter role to 85 % (32 req/s per GPU at
-          N = 2 and 4, 37.6 at 8; the agg rate of 42 would overload a 1:1 split's decode GPU).
+          N = 2 and 4, 37.6 at 8; the agg rate of 44 would overload a 1:1 split's decode GPU and
+          load 3P+5D's prefill GPUs to 99 %).  Default rate 44 req/s per GPU: sustained over 60-step
+          windows at TTFT p50 34 ms / ITL p90 21 ms (profiles/r3/s3/long_q44.json; QPS 46 holds
+          TTFT but puts ITL p90 at 23-26 ms, QPS 48 queues).
           Requests arrive at the decode ranks; a decode rank reserves KV blocks and hands each
           prompt to the prefill rank with the fewest prompts in flight, which computes it, pushes
           the blocks into the decode rank's staging arena with the IPC copy kernel (xGMI between
@@ -86,7 +89,7 @@ def parse(argv=None):
     ap.add_argument("--model", default="meta-llama/Llama-3.2-1B-Instruct")
     ap.add_argument("--isl", type=int, default=4000)
     ap.add_argument("--osl", type=int, default=500)
-    ap.add_argument("--qps", type=float, default=float(os.environ.get("MXS_BENCH_QPS", "42")),
+    ap.add_argument("--qps", type=float, default=float(os.environ.get("MXS_BENCH_QPS", "44")),
                     help="Poisson arrival rate per GPU (requests/s)")
     ap.add_argument("--max-num-seqs", type=int, default=384)
     ap.add_argument("--disagg-max-num-seqs", type=int, default=512,
