@@ -383,19 +383,33 @@ paged_prefill_v3_kernel(
 
   // ---- staging: global -> registers (tile k0), registers -> LDS buffer
   uint4 sk[NK], sv[NV];
-  auto gload = [&](int k0) {
-    int bid[4];
+  // A staging chunk's cache block is wave-uniform: chunk ci = tid + 512 n covers keys of block
+  // ci / (2 D) (2 D >= 128 chunks per block, waves are 64 consecutive threads), so each wave reads its
+  // block id with one scalar load and adds a per-lane offset fixed for the whole loop (no per-lane
+  // select among the tile's four block ids, no 64-bit multiply per chunk).
+  size_t koff[NK], voff[NV];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bid[j] = bt[min(k0 / kPBS + j, last_blk)];  // wave-uniform: scalar loads
+  for (int n = 0; n < NK; ++n) {
+    const int ci = tid + 512 * n, key = ci / KCH, ch = ci % KCH;
+    koff[n] = k_head_off + static_cast<size_t>((key & 15) * (D * EB) + ch * 8 * EB);
+  }
+#pragma unroll
+  for (int n = 0; n < NV; ++n) {
+    const int rem = (tid + 512 * n) % (2 * D), dim = rem >> 1, half = rem & 1;
+    voff[n] = v_head_off + static_cast<size_t>(dim * 16 * EB + half * 8 * EB);
+  }
+  auto gload = [&](int k0) {
 #pragma unroll
     for (int n = 0; n < NK; ++n) {
-      const int ci = tid + 512 * n, key = ci / KCH, ch = ci % KCH;
-      sk[n] = ld8_kv<EB>(kvb + bid[key >> 4] * bstride + k_head_off + (key & 15) * (D * EB) + ch * 8 * EB);
+      const int blk = __builtin_amdgcn_readfirstlane((tid + 512 * n) / (2 * D));
+      const long b = bt[min(k0 / kPBS + blk, last_blk)];
+      sk[n] = ld8_kv<EB>(kvb + b * bstride + koff[n]);
     }
 #pragma unroll
     for (int n = 0; n < NV; ++n) {
-      const int ci = tid + 512 * n, blk = ci / (2 * D), rem = ci % (2 * D), dim = rem >> 1, half = rem & 1;
-      uint4 v = ld8_kv<EB>(kvb + bid[blk] * bstride + v_head_off + dim * 16 * EB + half * 8 * EB);
+      const int ci = tid + 512 * n, blk = __builtin_amdgcn_readfirstlane(ci / (2 * D)), half = (ci % (2 * D)) & 1;
+      const long b = bt[min(k0 / kPBS + blk, last_blk)];
+      uint4 v = ld8_kv<EB>(kvb + b * bstride + voff[n]);
       const int kb = k0 + blk * 16 + half * 8;  // keys >= L: zero (unwritten cache bytes may be NaN)
       if (kb + 8 > L) {
         uint32_t* w = reinterpret_cast<uint32_t*>(&v);
