@@ -309,6 +309,14 @@ paged_prefill_v3_kernel(
   constexpr int VBYTES = D * KT * 2; // [D][64 keys]
   constexpr int NK = KT * KCH / 512; // K chunks staged per thread per tile
   constexpr int NV = D * 8 / 512;    // V chunks (8 keys of one dim) staged per thread per tile
+  // LDS chunk swizzles: a ds_read_b128 serves 16 lanes = 16 consecutive rows per pass.  128-byte rows
+  // (K at D = 64, V always) put rows r and r + 2 on the same banks: XOR the 16-byte chunk with
+  // (row >> 1) & 7 so the 16 rows hit 16 distinct slots (rows 2j, 2j + 1 share a swizzle but sit
+  // 32 banks apart); 256-byte K rows (D = 128) put every row on the same banks: XOR with row & 15
+  // over their 16 chunks.  (row & 7 was 2-way: SQ_LDS_BANK_CONFLICT ~2x the LDS-active cycles,
+  // profiles/r3/s3/prefill_attn_counters.json.)
+  auto kswz = [](int key) { return D == 64 ? ((key >> 1) & 7) : (key & 15); };
+  auto vswz = [](int dim) { return (dim >> 1) & 7; };
   __shared__ __attribute__((aligned(16))) char lds[2][KBYTES + VBYTES];
 
   const int NTL = gridDim.x, total = NTL * gridDim.y * gridDim.z;
@@ -426,7 +434,7 @@ paged_prefill_v3_kernel(
 #pragma unroll
     for (int n = 0; n < NK; ++n) {
       const int ci = tid + 512 * n, key = ci / KCH, ch = ci % KCH;
-      *reinterpret_cast<uint4*>(kl + key * KROW + ((ch ^ (key & 7)) << 4)) = sk[n];
+      *reinterpret_cast<uint4*>(kl + key * KROW + ((ch ^ kswz(key)) << 4)) = sk[n];
     }
 #pragma unroll
     for (int n = 0; n < NV; ++n) {
@@ -435,8 +443,8 @@ paged_prefill_v3_kernel(
       char* row = vl + dim * (KT * 2);
       const int c0 = blk * 2 + 0, c1 = blk * 2 + 1;  // 16-byte chunks of this block's 16 keys
       uint2 lo = make_uint2(sv[n].x, sv[n].y), hi = make_uint2(sv[n].z, sv[n].w);
-      *reinterpret_cast<uint2*>(row + ((c0 ^ (dim & 7)) << 4) + half * 8) = lo;
-      *reinterpret_cast<uint2*>(row + ((c1 ^ (dim & 7)) << 4) + half * 8) = hi;
+      *reinterpret_cast<uint2*>(row + ((c0 ^ vswz(dim)) << 4) + half * 8) = lo;
+      *reinterpret_cast<uint2*>(row + ((c1 ^ vswz(dim)) << 4) + half * 8) = hi;
     }
   };
 
@@ -470,7 +478,7 @@ paged_prefill_v3_kernel(
 #pragma unroll
     for (int idx = 0; idx < 2 * KS; ++idx) {
       const int key = (idx / KS) * 32 + c, ks = idx % KS;
-      ka[idx] = *reinterpret_cast<const uint4*>(kl + key * KROW + (((2 * ks + h) ^ (key & 7)) << 4));
+      ka[idx] = *reinterpret_cast<const uint4*>(kl + key * KROW + (((2 * ks + h) ^ kswz(key)) << 4));
     }
 #pragma unroll
     for (int idx = 0; idx < 2 * KS; ++idx)
@@ -536,7 +544,7 @@ paged_prefill_v3_kernel(
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
           const int dim = 32 * dt + c;
-          const uint4 a = *reinterpret_cast<const uint4*>(vl + dim * (KT * 2) + (((4 * kt + 2 * s2 + h) ^ (dim & 7)) << 4));
+          const uint4 a = *reinterpret_cast<const uint4*>(vl + dim * (KT * 2) + (((4 * kt + 2 * s2 + h) ^ vswz(dim)) << 4));
           o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), pf[kt][s2], o[dt], 0, 0, 0);
         }
   };
