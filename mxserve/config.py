@@ -36,7 +36,9 @@ class EngineArgs:
     gpu_memory_utilization: float = 0.90
     num_gpu_blocks: Optional[int] = None  # override the memory-derived count
     enforce_eager: bool = False  # disable hipGraph capture of decode steps
-    cuda_graph_max_bs: int = 256
+    # largest decode batch captured as a hipGraph; 0 = follow max_num_seqs (up to the 512 bucket), so a
+    # larger --max-num-seqs never leaves its big decode batches to eager launches
+    cuda_graph_max_bs: int = 0
     # schedule + launch step N+1 before waiting for step N's sampled tokens (host work overlaps
     # the GPU; decode inputs are read on the device from the last sampled token of each row)
     async_scheduling: bool = True

@@ -536,7 +536,7 @@ class ModelRunner:
         return ids, logits
 
     def _capture_graphs(self) -> None:
-        maxb = min(self.args.cuda_graph_max_bs, self.args.max_num_seqs)
+        maxb = min(self.args.cuda_graph_max_bs or min(self.args.max_num_seqs, 512), self.args.max_num_seqs)
         m = self.model
         # largest collective message of a decode step at batch b: the all-reduces of [b, H] and the
         # logits all-gather ([b, vocab/tp] per rank)
