@@ -109,7 +109,71 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
                 out = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
                 if prefill_gemm(out, x, w, cfg):
                     return out
+            plan = _mplan(M, w.shape[0], w.shape[1], x.device)
+            if plan is not None:
+                return _run_mplan(x, w, plan)
     return torch.nn.functional.linear(x, w)
+
+
+# ----------------------------------------------------------------------------- prefill M plans
+# hipBLASLt's kernel choice is not monotone in the row count: Llama-3.2-1B gate_up takes 189 us at
+# 4096 rows and 247 us at 4224-4352 (a mixed step with one 4000-token prompt and ~270 decode rows),
+# down 171 us at 8192 and 396 us at 8320; F.linear and mm(out=) sometimes pick different kernels too
+# (profiles/r3/s3/hipblaslt_m_sweep.jsonl, 128-row grid).  A persisted per-device plan
+# (ops/tuned/prefill_mplan_<arch>_<cus>cu.json, built from that sweep) splits such a GEMM into a
+# sweet-spot block plus the remainder, or takes the faster call form, wherever that measured >= 4 %
+# faster than one F.linear.  MXS_MPLAN=0 disables.
+_MPLAN: dict = {}
+
+
+def _mplan(M: int, N: int, K: int, device) -> Optional[list]:
+    if os.environ.get("MXS_MPLAN", "1") != "1":
+        return None
+    tab = _MPLAN.get(device)
+    if tab is None:
+        tab = _MPLAN[device] = _load_mplan(device)
+    ent = tab.get(f"{N}x{K}")
+    if not ent:
+        return None
+    bucket = -(-M // 128) * 128
+    e = ent.get(str(bucket))
+    if e is None:
+        return None
+    plan = [list(seg) for seg in e["plan"]]
+    short = bucket - M
+    if short:  # the actual rows are up to 127 fewer than the bucket: take them off the smaller segment
+        i = min(range(len(plan)), key=lambda j: plan[j][0])
+        if plan[i][0] <= short:
+            return None
+        plan[i][0] -= short
+    return plan
+
+
+def _load_mplan(device) -> dict:
+    import json
+    from .tuned import PKG_DIR, device_tag
+    try:
+        with open(os.path.join(PKG_DIR, f"prefill_mplan_{device_tag(device)}.json")) as f:
+            return json.load(f).get("entries", {})
+    except (OSError, ValueError):
+        return {}
+
+
+def _run_mplan(x: torch.Tensor, w: torch.Tensor, plan: list) -> torch.Tensor:
+    M = x.shape[0]
+    if len(plan) == 1 and plan[0][1] == "lin":
+        return torch.nn.functional.linear(x, w)
+    y = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
+    r = 0
+    for rows, form in plan:
+        xs, ys = x[r:r + rows], y[r:r + rows]
+        if form == "mm":
+            torch.mm(xs, w.t(), out=ys)
+        else:
+            ys.copy_(torch.nn.functional.linear(xs, w))
+        r += rows
+    assert r == M, (r, M, plan)
+    return y
 
 
 _PG_PART: dict = {}

@@ -427,6 +427,9 @@ def test_installer_reports_grove_kai_and_waits_for_gpu_operator_pods(tmp_path):
     state = tmp_path / "polls"
     (bindir / "kubectl").write_text(f"""#!/usr/bin/env bash
 echo "kubectl $*" >> {tmp_path}/calls
+# like the real kubectl, consume a piped manifest (an early exit would SIGPIPE the writer: exit 141
+# under the installer's pipefail)
+case "$*" in *"-f -"*) cat > /dev/null ;; esac
 case "$*" in
   *"get pods -n kube-amd-gpu --no-headers"*)
     n=$(cat {state} 2>/dev/null || echo 0); echo $((n + 1)) > {state}
