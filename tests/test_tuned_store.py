@@ -50,6 +50,8 @@ def test_packaged_tables_parse():
     for p in glob.glob(os.path.join(tuned.PKG_DIR, "*.json")):
         d = json.loads(open(p).read())
         assert d["entries"], p
+        if d.get("kind") == "prefill_mplan":  # {shape: {M bucket: plan}} (ops._mplan; tests/test_mplan.py)
+            continue
         for k, v in d["entries"].items():
             assert "@" in k and "cfg" in v, (p, k)
 
