@@ -562,6 +562,10 @@ class ModelRunner:
             self.decode_gemm_tune_s = time.time() - t0
             self.prefill_gemm_report = decode_gemm.tune_prefill(
                 {k: v[0] for k, v in shapes.items() if v[1] == 0 and k != "lm_head"}, self.device, self.dtype)
+            # prefill / mixed-step GEMMs: row-count plans around hipBLASLt's kernel-choice cliffs
+            from ..ops import mplan
+            self.mplan_report = mplan.tune({k: v[0] for k, v in shapes.items() if k != "lm_head"},
+                                           self.args.max_num_batched_tokens + self.args.max_num_seqs, self.device)
             if self.cfg.is_moe and "l0.w13" in w:  # expert GEMMs at decode batches (local experts)
                 from ..ops import moe as moe_ops
                 self.moe_gemm_report = moe_ops.tune(w["l0.w13"], w["l0.w2"], buckets, self.cfg.num_experts_per_tok,

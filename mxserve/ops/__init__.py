@@ -135,8 +135,13 @@ def _mplan(M: int, N: int, K: int, device) -> Optional[list]:
     ent = tab.get(f"{N}x{K}")
     if not ent:
         return None
-    bucket = -(-M // 128) * 128
-    e = ent.get(str(bucket))
+    # the packaged table is on a 128-row grid, tables tuned at start-up on a 256-row one
+    e = None
+    for g in (128, 256):
+        bucket = -(-M // g) * g
+        e = ent.get(str(bucket))
+        if e is not None:
+            break
     if e is None:
         return None
     plan = [list(seg) for seg in e["plan"]]
@@ -150,13 +155,8 @@ def _mplan(M: int, N: int, K: int, device) -> Optional[list]:
 
 
 def _load_mplan(device) -> dict:
-    import json
-    from .tuned import PKG_DIR, device_tag
-    try:
-        with open(os.path.join(PKG_DIR, f"prefill_mplan_{device_tag(device)}.json")) as f:
-            return json.load(f).get("entries", {})
-    except (OSError, ValueError):
-        return {}
+    from .mplan import load
+    return load(device)
 
 
 def _run_mplan(x: torch.Tensor, w: torch.Tensor, plan: list) -> torch.Tensor:

@@ -27,9 +27,11 @@ def timed(fn, iters=20):
 def main():
     dev = torch.device("cuda:0")
     shapes = {"qkv": (3072, 2048), "o": (2048, 2048), "gate_up": (16384, 2048), "down": (2048, 8192)}
+    if os.environ.get("SWEEP_SHAPES") == "lm_head":  # the LM head of a decode / mixed step (M = sampled rows)
+        shapes = {"lm_head": (128256, 2048)}
     Ms = [int(a) for a in sys.argv[1:]] or list(range(128, 8705, 128)) + [4300, 4270, 4200, 3300, 3170]
     ws = {k: (torch.randn(n, kk, device=dev) * kk ** -0.5).to(torch.bfloat16) for k, (n, kk) in shapes.items()}
-    xmax = {k: torch.randn(8960, kk, device=dev).to(torch.bfloat16) for k, (n, kk) in shapes.items()}
+    xmax = {k: torch.randn(max(8960, max(Ms) + 256), kk, device=dev).to(torch.bfloat16) for k, (n, kk) in shapes.items()}
     out = []
     for M in sorted(set(Ms)):
         Mp = -(-M // 256) * 256
@@ -44,7 +46,7 @@ def main():
             out.append(r)
             print(json.dumps(r), flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
-    with open("gpurun_out/hipblaslt_m_sweep.jsonl", "w") as f:
+    with open(os.environ.get("SWEEP_OUT", "gpurun_out/hipblaslt_m_sweep.jsonl"), "w") as f:
         for r in out:
             f.write(json.dumps(r) + "\n")
 

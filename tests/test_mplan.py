@@ -20,7 +20,8 @@ def test_mplan_lookup_and_shrink(monkeypatch):
     try:
         assert ops._mplan(4352, 16384, 2048, dev) == [[256, "mm"], [4096, "lin"]]
         assert ops._mplan(4270, 16384, 2048, dev) == [[174, "mm"], [4096, "lin"]]
-        assert ops._mplan(4100, 16384, 2048, dev) is None  # bucket 4224: no plan stored
+        assert ops._mplan(4100, 16384, 2048, dev) == [[4, "mm"], [4096, "lin"]]  # 128-row bucket 4224 absent: 256-row 4352
+        assert ops._mplan(3900, 16384, 2048, dev) is None  # no bucket within reach
         assert ops._mplan(4352, 3072, 2048, dev) is None
         monkeypatch.setenv("MXS_MPLAN", "0")
         assert ops._mplan(4352, 16384, 2048, dev) is None
@@ -37,3 +38,25 @@ def test_packaged_plan_table_parses():
         for m, e in ent.items():
             assert sum(r for r, _ in e["plan"]) == int(m)
             assert all(f in ("lin", "mm") for _, f in e["plan"])
+
+
+def test_plans_from_times_prefers_split_around_a_cliff():
+    from mxserve.ops import mplan
+    # F.linear: smooth except a cliff at 512 rows; mm(out=) as F.linear
+    t = {128: (10.0, 10.0), 256: (12.0, 12.0), 384: (14.0, 14.0), 512: (40.0, 40.0)}
+    p = mplan.plans_from_times(t, N=1024)
+    assert "512" in p and sorted(r for r, _ in p["512"]["plan"]) in ([128, 384], [256, 256])
+    assert "256" not in p  # no cliff: one F.linear
+    # a faster call form alone
+    p2 = mplan.plans_from_times({128: (10.0, 5.0), 256: (12.0, 12.0)}, N=64)
+    assert p2["128"]["plan"] == [[128, "mm"]]
+
+
+def test_mplan_coarse_grid_lookup():
+    dev = torch.device("cpu")
+    ops._MPLAN[dev] = {"4096x14336": {"4352": {"plan": [[256, "mm"], [4096, "mm"]]}}}
+    try:
+        assert ops._mplan(4200, 4096, 14336, dev) == [[104, "mm"], [4096, "mm"]]  # 256-row bucket 4352
+        assert ops._mplan(4100, 4096, 14336, dev) == [[4, "mm"], [4096, "mm"]]
+    finally:
+        ops._MPLAN.pop(dev, None)
