@@ -210,21 +210,24 @@ class Guard:
 
 
 # Capacity of one MI355X in the disagg roles for the headline workload (Llama-3.2-1B, ISL 4000 / OSL
-# 500, bf16): a prefill GPU computes ~476k prompt tok/s in 8192-token chunks (17.2 ms each,
-# profiles/r2_decode_step_microbench/mb_1b_256.jsonl) = ~118 req/s; a decode GPU streams every running
-# request's KV each step (~136 MB at a 4.25k context, ~22 us at 6.1 TB/s) and sustains ~38k tok/s at
-# 512 running = ~76 req/s.
-_CAP_PREFILL, _CAP_DECODE, _DISAGG_UTIL = 118.0, 76.0, 0.85
+# 500, bf16): a prefill GPU running 16384-token steps sustains 127.6 req/s (510k prompt tok/s,
+# steady-state rounds of scripts/prefill_capacity_probe.py, profiles/r3/s3/prefill_capacity); a decode
+# GPU streams every running request's KV each step (~136 MB at a 4.25k context, ~22 us at 6.1 TB/s)
+# and sustains ~38k tok/s at 512 running = ~76 req/s.
+_CAP_PREFILL, _CAP_DECODE, _DISAGG_UTIL = 127.0, 76.0, 0.85
+_PREFILL_STEP_TOKENS = 16384
 
 
 def disagg_plan(a, world: int) -> tuple:
-    """(prefill ranks, decode ranks, arrival rate per GPU) of the disagg phase.  The split follows the
-    two roles' capacities (~3 prefill : 5 decode GPUs for this workload; 1:1 below 4 GPUs), and the
+    """(prefill ranks, decode ranks, arrival rate per GPU) of the disagg phase.  The split maximises
+    the capacity of the tighter role (3 prefill : 5 decode GPUs on 8 for this workload), and the
     node rate loads the tighter role to 85 %.  Other models: a 1:1 split at --qps x 0.76."""
     p = a.disagg_prefill_ranks
     headline = a.model == "meta-llama/Llama-3.2-1B-Instruct" and a.isl == 4000 and a.osl == 500
     if p <= 0:
-        p = max(1, round(world * _CAP_DECODE / (_CAP_PREFILL + _CAP_DECODE))) if headline else world // 2
+        # the split whose tighter role carries the most (3P+5D on 8 GPUs, 2P+2D on 4, 1P+1D on 2)
+        p = max(range(1, max(2, world)), key=lambda k: min(k * _CAP_PREFILL, (world - k) * _CAP_DECODE)) \
+            if headline else world // 2
     p = min(max(1, p), world - 1)
     d = world - p
     qps = a.disagg_qps
@@ -801,8 +804,10 @@ def phase_disagg(a, ctx) -> tuple:
     is_prefill = rank < p
     isl, osl = (a.isl, a.osl) if ctx.on_gpu else (min(a.isl, 200), min(a.osl, 20))
     a2 = argparse.Namespace(**{**vars(a), "isl": isl, "osl": osl})
-    if is_prefill:  # prefill-only steps never replay decode graphs
-        args = engine_args(a, ctx, disagg_mode="prefill", enforce_eager=True)
+    if is_prefill:  # prefill-only steps never replay decode graphs; no decode rows to pace, so the
+        # largest steps (16384 tokens: ~128 req/s against ~120 at 8192, profiles/r3/s3/prefill_capacity)
+        args = engine_args(a, ctx, disagg_mode="prefill", enforce_eager=True, itl_target_ms=0.0,
+                           max_num_batched_tokens=max(a.max_num_batched_tokens, _PREFILL_STEP_TOKENS))
     else:
         mns = a.disagg_max_num_seqs
         args = engine_args(a, ctx, disagg_mode="decode", max_num_seqs=mns, cuda_graph_max_bs=mns)

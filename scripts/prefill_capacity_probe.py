@@ -22,19 +22,29 @@ def main():
                                enforce_eager=True))
     rng = np.random.default_rng(0)
     sp = SamplingParams(max_tokens=1, temperature=0, ignore_eos=True)
-    for n in (32, 256):  # warm-up round, then the measured one
+    for n in (32,) + (256,) * int(os.environ.get("ROUNDS", "1")):  # warm-up round, then measured ones
         for i in range(n):
             eng.add_request(rng.integers(100, 120000, size=4000).tolist(), sp)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        slow = []
         while eng.has_unfinished():
+            before = dict(eng.step_times) if eng.step_times is not None else None
+            ts = time.perf_counter()
             eng.step()
+            w = time.perf_counter() - ts
+            if w > 0.08 and n == 256:  # a stalled step: which host phase took the time
+                slow.append({"step": eng.num_steps, "wall_ms": round(w * 1e3, 1),
+                             **({k: round((eng.step_times[k] - before[k]) * 1e3, 1) for k in before
+                                 if k != "steps"} if before else {})})
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        if n == 256:
+            print(json.dumps({"round_s": round(dt, 3), "slow_steps": slow}), flush=True)
         if n == 32 and eng.step_times is not None:
             eng.step_times.update({k: 0.0 for k in eng.step_times})
     print(json.dumps({"max_num_batched_tokens": mnbt, "prompts": 256, "isl": 4000, "seconds": round(dt, 3), "req_per_s": round(256 / dt, 1),
-                      "prefill_tok_per_s": round(256 * 4000 / dt),
+                      "prefill_tok_per_s": round(256 * 4000 / dt), "slow_steps": slow,
                       "host_ms_per_step": ({k: round(v / max(1, eng.step_times["steps"]) * 1e3, 3)
                                             for k, v in eng.step_times.items() if k != "steps"}
                                            if eng.step_times else None)}), flush=True)

@@ -135,6 +135,10 @@ def test_disagg_plan_like_for_like():
     assert (p, d) == (1, 1) and q < 42.0
     assert bench.disagg_plan(_ns(disagg_qps=-1), 8)[2] < 42.0
     assert bench.disagg_plan(_ns(disagg_qps=30.0), 8)[2] == 30.0
+    # the default arrival rate (QPS 44) is carried like-for-like by 3P+5D; 4 GPUs split 2P+2D
+    assert bench.disagg_plan(_ns(qps=44.0), 8) == (3, 5, 44.0)
+    assert bench.disagg_plan(_ns(qps=44.0), 4)[:2] == (2, 2)
+    assert bench.disagg_plan(_ns(qps=44.0), 3)[:2] == (1, 2)
 
 
 def test_compare_modes_marks_winners():
