@@ -504,7 +504,10 @@ paged_prefill_v3_kernel(
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[kt][i]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    {  // the row's other half lives 32 lanes away: one permlane32 swap, not an LDS bpermute round trip
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
     // first tile: m := its max; later: lazy rescale when the tile raises the max by more than 2^8.
     // Both halves of a row see the same mx, hence the same decision.
     const bool bump = first || mx > 8.f;
