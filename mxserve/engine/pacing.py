@@ -24,6 +24,13 @@ from typing import Optional
 
 import numpy as np
 
+try:  # imported with the engine: a first import inside the step loop (the 24th observed step, when the
+    # model is first fitted) held the host ~300-400 ms while the GPU queue drained (scripts/
+    # prefill_capacity_probe.py: one 330-400 ms step at engine step 25 whatever the step size)
+    from scipy.optimize import nnls as _nnls
+except Exception:  # noqa: BLE001 - no scipy: no constrained fit
+    _nnls = None
+
 NF = 5
 
 
@@ -43,10 +50,11 @@ def step_features(so) -> np.ndarray:
 def nonneg_fit(A: np.ndarray, b: np.ndarray) -> Optional[np.ndarray]:
     """argmin_{theta >= 0} theta' A theta - 2 b' theta for the normal equations (A = X'X, b = X'y):
     with A = L L' that is the non-negative least squares problem ||L' theta - L^-1 b||."""
+    if _nnls is None:
+        return None
     try:
-        from scipy.optimize import nnls
         L = np.linalg.cholesky(A + 1e-9 * np.eye(A.shape[0]))
-        theta, _ = nnls(L.T, np.linalg.solve(L, b))
+        theta, _ = _nnls(L.T, np.linalg.solve(L, b))
         return theta
     except Exception:  # noqa: BLE001 - no scipy / not positive definite: no constrained fit
         return None
