@@ -19,9 +19,9 @@ def main():
     mnbt = int(os.environ.get("MNBT", "8192"))
     eng = LLMEngine(EngineArgs(model="meta-llama/Llama-3.2-1B-Instruct", device="cuda", max_num_seqs=64,
                                max_num_batched_tokens=mnbt, max_model_len=max(8192, mnbt), load_format="random",
-                               enforce_eager=True))
+                               enforce_eager=os.environ.get("EAGER", "1") == "1"))
     rng = np.random.default_rng(0)
-    sp = SamplingParams(max_tokens=1, temperature=0, ignore_eos=True)
+    sp = SamplingParams(max_tokens=int(os.environ.get("OSL", "1")), temperature=0, ignore_eos=True)
     for n in (32,) + (256,) * int(os.environ.get("ROUNDS", "1")):  # warm-up round, then measured ones
         for i in range(n):
             eng.add_request(rng.integers(100, 120000, size=4000).tolist(), sp)
@@ -33,14 +33,14 @@ def main():
             ts = time.perf_counter()
             eng.step()
             w = time.perf_counter() - ts
-            if w > 0.08 and n == 256:  # a stalled step: which host phase took the time
+            if w > float(os.environ.get("SLOW_S", "0.08")):  # a stalled step: which host phase took the time
                 slow.append({"step": eng.num_steps, "wall_ms": round(w * 1e3, 1),
                              **({k: round((eng.step_times[k] - before[k]) * 1e3, 1) for k in before
                                  if k != "steps"} if before else {})})
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        if n == 256:
-            print(json.dumps({"round_s": round(dt, 3), "slow_steps": slow}), flush=True)
+        if True:
+            print(json.dumps({"n": n, "round_s": round(dt, 3), "slow_steps": slow}), flush=True)
         if n == 32 and eng.step_times is not None:
             eng.step_times.update({k: 0.0 for k in eng.step_times})
     print(json.dumps({"max_num_batched_tokens": mnbt, "prompts": 256, "isl": 4000, "seconds": round(dt, 3), "req_per_s": round(256 / dt, 1),
