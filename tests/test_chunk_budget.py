@@ -218,3 +218,22 @@ def test_ttft_guard_lifts_the_limit():
     so = s.schedule()
     assert so.prefills[0].num_new_tokens == 6000
     assert s.chunk_budget.guard_lifts == 1
+
+
+def test_nnls_imported_with_the_module():
+    """The first constrained fit must not import scipy inside the step loop (a 330-400 ms host stall at
+    engine step 25 that drained the GPU queue): the solver is bound when pacing is imported."""
+    import importlib.util
+
+    from mxserve.engine import pacing
+    if importlib.util.find_spec("scipy") is None:
+        assert pacing._nnls is None
+        return
+    assert pacing._nnls is not None
+    import sys
+    mods = set(sys.modules)
+    m = pacing.StepTimeModel(nf=3, warmup=2)
+    for k in range(4):
+        m.update(np.array([1.0, k, k * k]), 0.01 + 0.002 * k)
+    assert m.theta_nn is not None
+    assert not {x for x in set(sys.modules) - mods if x.startswith("scipy")}
