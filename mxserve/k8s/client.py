@@ -5,9 +5,11 @@ certificate), or an explicit server URL (tests use the in-process fake apiserver
 from __future__ import annotations
 
 import base64
+import hashlib
+import json
 import os
 import tempfile
-from typing import Optional
+from typing import Iterator, Optional
 
 import httpx
 import yaml
@@ -22,7 +24,20 @@ PLURALS = {
     "DynamoGraphDeployment": ("nvidia.com/v1alpha1", "dynamographdeployments"),
     "DynamoGraphDeploymentRequest": ("nvidia.com/v1alpha1", "dynamographdeploymentrequests"),
     "DynamoComponentDeployment": ("nvidia.com/v1alpha1", "dynamocomponentdeployments"),
+    "Event": ("v1", "events"),
 }
+# annotation carrying the hash of the spec the operator last applied (apply() skips unchanged objects)
+HASH_ANNOTATION = "mxserve.io/spec-hash"
+
+
+def spec_hash(obj: dict) -> str:
+    """Hash of everything apply() would write (the object minus status and the hash itself)."""
+    body = {k: v for k, v in obj.items() if k != "status"}
+    meta = dict(body.get("metadata") or {})
+    ann = {k: v for k, v in (meta.get("annotations") or {}).items() if k != HASH_ANNOTATION}
+    meta["annotations"] = ann
+    body["metadata"] = meta
+    return hashlib.sha256(json.dumps(body, sort_keys=True, default=str).encode()).hexdigest()[:20]
 CLUSTER_SCOPED = {"Namespace", "Node"}
 
 
@@ -108,13 +123,64 @@ class KubeClient:
                          headers={"Content-Type": "application/merge-patch+json"})
 
     def apply(self, obj: dict) -> dict:
-        """Create, or merge-patch the spec/labels/owners of an existing object."""
+        """Create, or merge-patch the spec/labels/owners of an existing object.  The object is stamped
+        with a hash of what is written; an existing object carrying the same hash is left alone (no
+        write), so a reconcile of an unchanged graph costs reads only.  A patch the apiserver refuses
+        as invalid (422: e.g. a Deployment's immutable selector changed) deletes and recreates."""
         meta = obj["metadata"]
+        h = spec_hash(obj)
+        obj = dict(obj, metadata=dict(meta, annotations={**(meta.get("annotations") or {}), HASH_ANNOTATION: h}))
         cur = self.get(obj["kind"], meta["name"], meta.get("namespace"))
         if cur is None:
             return self.create(obj)
+        if ((cur.get("metadata") or {}).get("annotations") or {}).get(HASH_ANNOTATION) == h:
+            return cur
         patch = {k: v for k, v in obj.items() if k not in ("apiVersion", "kind", "status")}
-        return self.merge_patch(obj["kind"], meta["name"], meta.get("namespace"), patch)
+        try:
+            return self.merge_patch(obj["kind"], meta["name"], meta.get("namespace"), patch)
+        except ApiError as e:
+            if e.status != 422:
+                raise
+            self.delete(obj["kind"], meta["name"], meta.get("namespace"))
+            return self.create(obj)
+
+    def list_rv(self, kind: str, namespace: Optional[str] = None, label_selector: Optional[str] = None) -> tuple:
+        """(items, the list's resourceVersion) -- the starting point of a watch."""
+        params = {"labelSelector": label_selector} if label_selector else None
+        out = self._req("GET", _path(kind, namespace), params=params)
+        return out.get("items", []), str((out.get("metadata") or {}).get("resourceVersion") or "")
+
+    def watch(self, kind: str, namespace: Optional[str] = None, resource_version: str = "",
+              timeout_s: int = 60, label_selector: Optional[str] = None) -> Iterator[dict]:
+        """Stream watch events ({"type": ADDED|MODIFIED|DELETED|BOOKMARK|ERROR, "object": ...}) from
+        resource_version on, for at most timeout_s seconds (the apiserver closes the stream then)."""
+        params = {"watch": "true", "timeoutSeconds": str(int(timeout_s)), "allowWatchBookmarks": "true"}
+        if resource_version:
+            params["resourceVersion"] = resource_version
+        if label_selector:
+            params["labelSelector"] = label_selector
+        with self.http.stream("GET", _path(kind, namespace), params=params, timeout=timeout_s + 10) as r:
+            if r.status_code >= 400:
+                r.read()
+                raise ApiError(r.status_code, r.text[:300])
+            for line in r.iter_lines():
+                if line.strip():
+                    yield json.loads(line)
+
+    def event(self, involved: dict, reason: str, message: str, kind: str = "Normal") -> None:
+        """Record a core/v1 Event on `involved` (best effort: an Event failing never fails a reconcile)."""
+        meta = involved.get("metadata") or {}
+        ns = meta.get("namespace") or "default"
+        try:
+            self.create({"apiVersion": "v1", "kind": "Event",
+                         "metadata": {"generateName": f"{meta.get('name', 'obj')}.", "namespace": ns,
+                                      "name": f"{meta.get('name', 'obj')}.{os.urandom(6).hex()}"},
+                         "involvedObject": {"apiVersion": involved.get("apiVersion"), "kind": involved.get("kind"),
+                                            "name": meta.get("name"), "namespace": ns, "uid": meta.get("uid")},
+                         "reason": reason, "message": message, "type": kind,
+                         "source": {"component": "mxserve-operator"}})
+        except (ApiError, OSError, httpx.HTTPError):
+            pass
 
     def delete(self, kind: str, name: str, namespace: Optional[str] = None) -> None:
         try:

@@ -1,19 +1,22 @@
 """In-process fake Kubernetes apiserver: the REST subset the operator and deploy scripts use
-(CRUD, merge-patch, /status, labelSelector lists, ownerReference-free storage).  Used by the
+(CRUD, merge-patch, /status, labelSelector lists, list + watch from a resourceVersion,
+ownerReference-free storage).  Used by the
 operator tests and the script tests; `python -m mxserve.k8s.fake_apiserver
 --port P` runs it standalone.  Optionally marks Deployments ready (simulated kubelet)."""
 from __future__ import annotations
 
 import argparse
+import asyncio
 import copy
 import itertools
+import json
 import os
 import threading
 import time
 import uuid
 
 from fastapi import FastAPI, Request
-from fastapi.responses import JSONResponse
+from fastapi.responses import JSONResponse, StreamingResponse
 
 
 def _merge(dst: dict, patch: dict) -> dict:
@@ -59,6 +62,7 @@ class FakeApiServer:
         self.job_runner = self._run_profiler_job
         self.jobs_run: list = []
         self.log: list = []
+        self.events: list = []  # (resourceVersion, type, gv, plural, ns, obj) for watches
         self._rv = itertools.count(1)
         for i in range(nodes):
             self._put("v1", "nodes", None, {
@@ -83,7 +87,9 @@ class FakeApiServer:
                 if not p.get("nodePort"):
                     p["nodePort"] = next(n for n in range(30000, 32768) if n not in used)
                     used.add(p["nodePort"])
+        kind = "MODIFIED" if (gv, plural, ns, meta["name"]) in self.store else "ADDED"
         self.store[(gv, plural, ns, meta["name"])] = obj
+        self.events.append((int(meta["resourceVersion"]), kind, gv, plural, ns, copy.deepcopy(obj)))
         if plural == "services" and self.auto_ready and obj.get("spec", {}).get("selector"):
             # the endpoints controller: a ready address per selected pod (one, here)
             ports = [{"name": p.get("name"), "port": p.get("targetPort", p.get("port"))}
@@ -125,6 +131,10 @@ class FakeApiServer:
                 cur["status"] = {"succeeded": 1} if ok else {"failed": 2}
         threading.Thread(target=run, daemon=True).start()
 
+    def writes(self) -> list:
+        """Mutating requests received (method, gv, plural, ns, name, sub)."""
+        return [e for e in self.log if e[0] in ("POST", "PUT", "PATCH", "DELETE")]
+
     def objects(self, plural: str, ns: str | None = None) -> list:
         return [o for (gv, p, n, _), o in self.store.items() if p == plural and (ns is None or n == ns)]
 
@@ -140,7 +150,9 @@ class FakeApiServer:
                     items = [copy.deepcopy(o) for (g, p, n, _), o in srv.store.items()
                              if g == gv and p == plural and (ns is None or n == ns)
                              and _match(o["metadata"].get("labels") or {}, params.get("labelSelector"))]
-                    return 200, {"kind": "List", "apiVersion": gv, "items": items}
+                    last = srv.events[-1][0] if srv.events else 0
+                    return 200, {"kind": "List", "apiVersion": gv, "metadata": {"resourceVersion": str(last)},
+                                 "items": items}
                 if method == "POST":
                     nm = body["metadata"]["name"]
                     if (gv, plural, ns, nm) in srv.store:
@@ -159,16 +171,19 @@ class FakeApiServer:
                 return 200, copy.deepcopy(cur)
             if method == "DELETE":
                 del srv.store[key]
+                srv.events.append((next(srv._rv), "DELETED", gv, plural, ns, copy.deepcopy(cur)))
                 return 200, {"kind": "Status", "status": "Success"}
             if method == "PATCH":
                 if sub == "status":
                     cur.setdefault("status", {})
                     _merge(cur["status"], body.get("status", {}))
+                    cur["metadata"]["resourceVersion"] = str(next(srv._rv))
+                    srv.events.append((int(cur["metadata"]["resourceVersion"]), "MODIFIED", gv, plural, ns,
+                                       copy.deepcopy(cur)))
                 else:
                     body = {k: v for k, v in body.items() if k != "status"}
                     _merge(cur, body)
-                    if plural in ("deployments", "services"):
-                        srv._put(gv, plural, ns, cur)
+                    srv._put(gv, plural, ns, cur)
                 return 200, copy.deepcopy(cur)
             if method == "PUT":
                 return 200, copy.deepcopy(srv._put(gv, plural, ns, copy.deepcopy(body)))
@@ -190,8 +205,26 @@ class FakeApiServer:
             body = None
             if request.method in ("POST", "PUT", "PATCH"):
                 body = await request.json()
+            q = dict(request.query_params)
+            if request.method == "GET" and name is None and q.get("watch") in ("true", "1"):
+                return StreamingResponse(watch(gv, plural, ns, q), media_type="application/json")
             code, out = handle(request.method, gv, plural, ns, name, sub, body, dict(request.query_params))
             return JSONResponse(out, status_code=code)
+
+        async def watch(gv, plural, ns, q):
+            """Newline-delimited watch events after resourceVersion, until timeoutSeconds."""
+            srv.log.append(("WATCH", gv, plural, ns, None, None))
+            rv = int(q.get("resourceVersion") or 0)
+            deadline = time.monotonic() + float(q.get("timeoutSeconds") or 30)
+            sel = q.get("labelSelector")
+            while time.monotonic() < deadline:
+                for ev_rv, kind, g, p, n, obj in list(srv.events):
+                    if ev_rv <= rv or g != gv or p != plural or (ns is not None and n != ns):
+                        continue
+                    rv = ev_rv
+                    if _match(obj["metadata"].get("labels") or {}, sel):
+                        yield json.dumps({"type": kind, "object": obj}) + "\n"
+                await asyncio.sleep(0.05)
 
         app.add_api_route("/{path:path}", core, methods=["GET", "POST", "PUT", "PATCH", "DELETE"])
         return app

@@ -1,14 +1,18 @@
 """The mxserve operator: reconciles DynamoGraphDeployment(Request)s (replaces the Dynamo operator
 controller-manager).
 
-Level-triggered polling reconcile (robust to missed events, no watch-resume bookkeeping):
+Level-triggered reconcile, woken by watches and re-run as a periodic resync (robust to missed
+events: a watch only shortens the wait, the full pass always reads the current state):
   DGDR -> profiling Job from `profilerImage` running mxserve.profiler.sla (live timings on one GPU
           when useAiConfigurator is false, else the MI355X roofline), results published in a
           ConfigMap (state Profiling until the Job ends) -> DGD rendered from the request's ConfigMap
           template (+ workersImage override) -> applied if autoApply; results in status.
           MXS_PROFILER_MODE=inline (or no profilerImage) runs the roofline in the operator instead.
   DGD  -> DCD per service -> Deployment + Service + PodMonitor; DGD status.state = successful once
-          every Deployment has its replicas ready
+          every Deployment has its replicas ready (P/D group pods: every shape Deployment's pods)
+Writes are skipped when nothing changed (a spec hash on every child, status compared before it is
+patched), so an idle operator only reads; state transitions and image rewrites are recorded as
+Events.
 Orphans (children whose DGD is gone) are deleted, as the Kubernetes garbage collector would via
 ownerReferences.  `python -m mxserve.k8s.operator [--namespace NS] [--interval S] [--server URL]`.
 """
@@ -18,6 +22,7 @@ import argparse
 import json
 import logging
 import os
+import threading
 import time
 from typing import Optional
 
@@ -26,8 +31,8 @@ import yaml
 from ..profiler import sla
 from .client import ApiError, KubeClient
 from .resources import (API_VERSION, DCD_KIND, DGD_KIND, DGDR_KIND, NS_LABEL, ValidationError,
-                        apply_plan_to_template, parse_dgd, parse_dgdr, render_children, render_dcds,
-                        render_profiler_job)
+                        apply_plan_to_template, group_deployment_name, group_shapes, image_rewrites, parse_dgd,
+                        parse_dgdr, pd_groups, pd_pairs, render_children, render_dcds, render_profiler_job)
 
 log = logging.getLogger("mxserve.operator")
 
@@ -38,21 +43,60 @@ class Operator:
         self.ns = namespace
         self.podmonitors = podmonitors
         self._pm_disabled = False
+        self._wake = threading.Event()
+        self.watch_errors = 0
+
+    def _set_status(self, kind: str, obj: Optional[dict], name: str, ns: str, st: dict) -> None:
+        """Patch status only when it differs from what the object already carries."""
+        cur = (obj or {}).get("status") or {}
+        if all(cur.get(k) == v for k, v in st.items()):
+            return
+        self.k.patch_status(kind, name, ns, st)
+        if obj is not None and cur.get("state") != st.get("state") and st.get("state"):
+            self.k.event(obj, f"State{str(st['state']).capitalize()}",
+                         f"{kind} {name}: state {cur.get('state') or 'none'} -> {st['state']}",
+                         "Warning" if str(st["state"]).lower() == "failed" else "Normal")
+
+    def _service_ready(self, g, ns: str) -> dict:
+        """{service key: (ready workers/replicas, wanted)}.  A P/D-grouped decode service runs its
+        workers AND the prefill service's in group pods, one Deployment per pod shape: ready decode
+        (prefill) workers = sum over shapes of ready pods x decode (prefill) workers per pod."""
+        out = {}
+        pair = pd_pairs(g)
+        if pair is not None:
+            dec, pre = pair
+            name = f"{g.name}-{dec.dns_name}"
+            rd = rp = 0
+            for k, (n_pre, n_dec, count) in enumerate(group_shapes(pd_groups(dec, pre))):
+                d = self.k.get("Deployment", group_deployment_name(name, k), ns) or {}
+                ready = min(count, int((d.get("status") or {}).get("readyReplicas", 0) or 0))
+                rd += ready * n_dec
+                rp += ready * n_pre
+            out[dec.key] = (rd, dec.replicas)
+            out[pre.key] = (rp, pre.replicas)
+        for s in g.services:
+            if s.key in out:
+                continue
+            d = self.k.get("Deployment", f"{g.name}-{s.dns_name}", ns) or {}
+            out[s.key] = (int((d.get("status") or {}).get("readyReplicas", 0) or 0), s.replicas)
+        return out
 
     # ------------------------------------------------------------------ DGD
     def reconcile_dgd(self, obj: dict) -> dict:
         ns = obj["metadata"].get("namespace") or self.ns or "default"
         try:
             g = parse_dgd(obj, ns)
+            render_children(g)  # layout errors (e.g. a P/D group that cannot fit) surface as InvalidSpec
         except ValidationError as e:
             st = {"state": "failed", "conditions": [{"type": "Ready", "status": "False", "reason": "InvalidSpec",
                                                       "message": str(e)}]}
-            self.k.patch_status(DGD_KIND, obj["metadata"]["name"], ns, st)
+            self._set_status(DGD_KIND, obj, obj["metadata"]["name"], ns, st)
             return st
-        uids = {}
+        uids, dcd_objs = {}, {}
         for dcd in render_dcds(g):
             cur = self.k.apply(dcd)
             uids[dcd["metadata"]["name"]] = (cur.get("metadata") or {}).get("uid")
+            dcd_objs[dcd["metadata"]["name"]] = cur
         want = set()
         for child in render_children(g, uids):
             if child["kind"] == "PodMonitor" and (not self.podmonitors or self._pm_disabled):
@@ -78,18 +122,26 @@ class Operator:
                     self.k.delete(kind, n, ns)
         # status
         services, ready_all = {}, True
+        ready = self._service_ready(g, ns)
         for s in g.services:
-            name = f"{g.name}-{s.dns_name}"
-            d = self.k.get("Deployment", name, ns) or {}
-            ready = int((d.get("status") or {}).get("readyReplicas", 0) or 0)
-            services[s.key] = {"componentType": s.component_type, "replicas": s.replicas, "readyReplicas": ready}
-            ready_all &= ready >= s.replicas
+            r, want = ready[s.key]
+            services[s.key] = {"componentType": s.component_type, "replicas": s.replicas, "readyReplicas": r}
+            ready_all &= r >= want
         st = {"state": "successful" if ready_all else "pending", "services": services,
               "conditions": [{"type": "Ready", "status": "True" if ready_all else "False",
                               "reason": "AllServicesReady" if ready_all else "WaitingForReplicas"}]}
-        self.k.patch_status(DGD_KIND, g.name, ns, st)
-        for dname, uid in uids.items():
-            self.k.patch_status(DCD_KIND, dname, ns, {"state": st["state"]})
+        self._set_status(DGD_KIND, obj, g.name, ns, st)
+        rewrites = image_rewrites(g)
+        for s in g.services:
+            dname = f"{g.name}-{s.dns_name}"
+            dst = {"state": st["state"]}
+            if s.key in rewrites:  # an image the node cannot run, replaced (resources.map_image)
+                dst["imageRewrite"] = rewrites[s.key]
+            cur = dcd_objs.get(dname)
+            if cur is not None and "imageRewrite" in dst and ((cur.get("status") or {}).get("imageRewrite")
+                                                               != dst["imageRewrite"]):
+                self.k.event(cur, "ImageRewritten", f"{dst['imageRewrite']['from']} -> {dst['imageRewrite']['to']}")
+            self._set_status(DCD_KIND, cur, dname, ns, dst)
         return st
 
     # ------------------------------------------------------------------ DGDR
@@ -101,18 +153,18 @@ class Operator:
             r = parse_dgdr(obj, ns)
         except ValidationError as e:
             st = {"state": "Failed", "message": str(e)}
-            self.k.patch_status(DGDR_KIND, obj["metadata"]["name"], ns, st)
+            self._set_status(DGDR_KIND, obj, obj["metadata"]["name"], ns, st)
             return st
         if r.profiler_image and os.environ.get("MXS_PROFILER_MODE", "job") == "job":
             p = self._profiling_job(r, ns)
             if isinstance(p, dict) and "state" in p:  # still profiling, or the Job failed
-                self.k.patch_status(DGDR_KIND, r.name, ns, p)
+                self._set_status(DGDR_KIND, obj, r.name, ns, p)
                 return p
         else:
             p = sla.plan(r.model, r.isl, r.osl, r.ttft_ms, r.itl_ms, system="mi355x")
         if not p["feasible"]:
             st = {"state": "Failed", "message": "SLA not reachable on one node", "profilingResults": p}
-            self.k.patch_status(DGDR_KIND, r.name, ns, st)
+            self._set_status(DGDR_KIND, obj, r.name, ns, st)
             return st
         roles = {}
         if p["disagg"]:
@@ -124,7 +176,7 @@ class Operator:
             cm = self.k.get("ConfigMap", r.config_map, ns)
             if cm is None:
                 st = {"state": "Pending", "message": f"ConfigMap {r.config_map} not found"}
-                self.k.patch_status(DGDR_KIND, r.name, ns, st)
+                self._set_status(DGDR_KIND, obj, r.name, ns, st)
                 return st
             template = yaml.safe_load((cm.get("data") or {}).get(r.config_key or "disagg.yaml", ""))
         if template is None:
@@ -137,7 +189,7 @@ class Operator:
               "deployment": {"name": dgd["metadata"]["name"], "applied": r.auto_apply}}
         if r.auto_apply:
             self.k.apply(dgd)
-        self.k.patch_status(DGDR_KIND, r.name, ns, st)
+        self._set_status(DGDR_KIND, obj, r.name, ns, st)
         return st
 
     def _profiling_job(self, r, ns: str) -> dict:
@@ -189,13 +241,55 @@ class Operator:
                 log.exception("DGD %s", obj["metadata"].get("name"))
         self.gc_orphans()
 
-    def run(self, interval: float = 5.0) -> None:
-        while True:
+    def _watch_loop(self, kind: str, stop: threading.Event) -> None:
+        """List + watch `kind` from the list's resourceVersion; every event wakes the reconcile loop.
+        Re-lists on expiry (410) and backs off on errors; an apiserver without watch support leaves
+        the operator on its resync interval."""
+        rv, backoff = "", 1.0
+        while not stop.is_set():
             try:
-                self.reconcile_all()
-            except Exception:  # noqa: BLE001 - apiserver hiccup
-                log.exception("reconcile pass failed")
-            time.sleep(interval)
+                if not rv:
+                    _, rv = self.k.list_rv(kind, self.ns)
+                for ev in self.k.watch(kind, self.ns, rv, timeout_s=60):
+                    if ev.get("type") == "ERROR":
+                        rv = ""  # expired resourceVersion: re-list
+                        break
+                    rv = str(((ev.get("object") or {}).get("metadata") or {}).get("resourceVersion") or rv)
+                    if ev.get("type") != "BOOKMARK":
+                        self._wake.set()
+                    if stop.is_set():
+                        return
+                backoff = 1.0
+            except Exception as e:  # noqa: BLE001 - apiserver hiccup / no watch support
+                self.watch_errors += 1
+                rv = ""
+                log.debug("watch %s: %s", kind, e)
+                if stop.wait(backoff):
+                    return
+                backoff = min(60.0, backoff * 2)
+
+    def start_watches(self, kinds=(DGD_KIND, DGDR_KIND, "Deployment", "Job")) -> threading.Event:
+        stop = threading.Event()
+        for kind in kinds:
+            threading.Thread(target=self._watch_loop, args=(kind, stop), name=f"watch-{kind}", daemon=True).start()
+        return stop
+
+    def run(self, interval: float = 30.0, watch: bool = True, stop: Optional[threading.Event] = None) -> None:
+        """Reconcile on every watch event (coalesced) and at least every `interval` seconds."""
+        stop = stop or threading.Event()
+        wstop = self.start_watches() if watch else None
+        try:
+            while not stop.is_set():
+                self._wake.clear()
+                try:
+                    self.reconcile_all()
+                except Exception:  # noqa: BLE001 - apiserver hiccup
+                    log.exception("reconcile pass failed")
+                self._wake.wait(interval)
+                time.sleep(0.2)  # coalesce a burst of events into one pass
+        finally:
+            if wstop is not None:
+                wstop.set()
 
 
 def default_template(model: str) -> dict:
@@ -213,14 +307,15 @@ def default_template(model: str) -> dict:
 def main(argv=None) -> None:
     ap = argparse.ArgumentParser(prog="python -m mxserve.k8s.operator")
     ap.add_argument("--namespace", default=None, help="watch one namespace (default: all)")
-    ap.add_argument("--interval", type=float, default=5.0)
+    ap.add_argument("--interval", type=float, default=30.0, help="resync period (watch events reconcile at once)")
+    ap.add_argument("--no-watch", action="store_true", help="poll every --interval instead of watching")
     ap.add_argument("--server", default=None, help="apiserver URL (default: in-cluster / kubeconfig)")
     ap.add_argument("--no-podmonitors", action="store_true")
     a = ap.parse_args(argv)
     from ..utils.logs import setup_logging
     setup_logging()
     op = Operator(KubeClient(a.server) if a.server else KubeClient(), a.namespace, not a.no_podmonitors)
-    op.run(a.interval)
+    op.run(a.interval, watch=not a.no_watch)
 
 
 if __name__ == "__main__":

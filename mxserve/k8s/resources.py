@@ -13,6 +13,7 @@ lists the fields honoured here.  Rendering (pure functions, unit-tested without 
 from __future__ import annotations
 
 import copy
+import fnmatch
 import json
 import os
 import re
@@ -30,11 +31,18 @@ COMPONENT_LABEL = "nvidia.com/dynamo-component"
 TYPE_LABEL = "nvidia.com/dynamo-component-type"
 SUBTYPE_LABEL = "nvidia.com/dynamo-sub-component-type"
 GPU_RESOURCE = os.environ.get("MXS_GPU_RESOURCE", "amd.com/gpu")
-DEFAULT_IMAGE = os.environ.get("MXS_DEFAULT_IMAGE", "ghcr.io/mxserve/mxserve-rocm:0.1.0")
+DEFAULT_IMAGE = os.environ.get("MXS_DEFAULT_IMAGE", "mxserve/mxserve-rocm:0.1.0")
 # set on the operator Deployment by install-dynamo-1node.sh; passed to every component it renders
 PROMETHEUS_ENDPOINT = os.environ.get("PROMETHEUS_ENDPOINT", "")
 FRONTEND_PORT = 8000
 WORKER_PORT = 8081
+# The reference pins NVIDIA's CUDA runtime images on every service
+# (/root/reference/examples/deploy/vllm/agg.yaml:17,27; examples/dgdr/trtllm/disagg.yaml:17,28,53);
+# scheduled unchanged on an MI355X node they cannot run.  Such images are rewritten to the mxserve
+# image (which also provides the reference's /workspace layout, docker/Dockerfile), and the rewrite is
+# recorded in the DCD status.  MXS_IMAGE_MAP="<glob>=<image>;..." adds mappings (checked first);
+# MXS_IMAGE_MAP=off keeps every image as written.
+BUILTIN_IMAGE_MAP = [("nvcr.io/nvidia/ai-dynamo/*-runtime:*", None), ("nvcr.io/nvidia/ai-dynamo/*", None)]
 
 _DNS = re.compile(r"^[a-z0-9]([-a-z0-9]*[a-z0-9])?$")
 
@@ -130,6 +138,41 @@ def parse_dgd(obj: dict, namespace: Optional[str] = None) -> GraphSpec:
                      pvcs=pvcs, uid=meta.get("uid"))
 
 
+def image_map() -> list:
+    """[(glob, image or None = the default image)] in match order."""
+    env = os.environ.get("MXS_IMAGE_MAP", "")
+    if env.strip().lower() == "off":
+        return []
+    out = []
+    for part in env.split(";"):
+        if "=" in part:
+            pat, img = part.split("=", 1)
+            if pat.strip() and img.strip():
+                out.append((pat.strip(), img.strip()))
+    return out + BUILTIN_IMAGE_MAP
+
+
+def map_image(image: Optional[str]) -> tuple:
+    """(image to run, the image it replaced or None)."""
+    if not image:
+        return DEFAULT_IMAGE, None
+    for pat, repl in image_map():
+        if fnmatch.fnmatchcase(image, pat):
+            new = repl or DEFAULT_IMAGE
+            return new, (image if new != image else None)
+    return image, None
+
+
+def image_rewrites(g: "GraphSpec") -> dict:
+    """{service key: {"from": original, "to": image}} for every service whose image was mapped."""
+    out = {}
+    for s in g.services:
+        new, old = map_image(s.image)
+        if old:
+            out[s.key] = {"from": old, "to": new}
+    return out
+
+
 def _owner(kind: str, name: str, uid: Optional[str]) -> list:
     if not uid:
         return []
@@ -153,7 +196,7 @@ def render_dcds(g: GraphSpec) -> list[dict]:
                          "ownerReferences": _owner(DGD_KIND, g.name, g.uid)},
             "spec": {"dynamoNamespace": f"{g.namespace}-{g.name}", "serviceName": s.key,
                      "componentType": s.component_type, "subComponentType": s.sub_component_type,
-                     "replicas": s.replicas, "gpus": s.gpus, "image": s.image or DEFAULT_IMAGE}})
+                     "replicas": s.replicas, "gpus": s.gpus, "image": map_image(s.image)[0]}})
     return out
 
 
@@ -211,7 +254,7 @@ def _container(g: GraphSpec, s: ServiceSpec) -> dict:
         env += [{"name": "MXS_FRONTEND_URL", "value": frontend_url(g)},
                 {"name": "DYN_SYSTEM_PORT", "value": str(WORKER_PORT)}]
     env += [dict(e) for e in s.envs]
-    c = {"name": "main", "image": s.image or DEFAULT_IMAGE, "command": list(cmd), "env": env,
+    c = {"name": "main", "image": map_image(s.image)[0], "command": list(cmd), "env": env,
          "ports": [{"name": "http" if is_fe else "system", "containerPort": port}],
          "readinessProbe": {"httpGet": {"path": "/health", "port": port}, "periodSeconds": 5,
                             "failureThreshold": 720},
@@ -270,8 +313,23 @@ def pd_groups(d: ServiceSpec, p: ServiceSpec, node_gpus: int = 0) -> list:
     while True:
         groups = [(P // n + (i < P % n), D // n + (i < D % n)) for i in range(n)]
         if all(pi * gp + di * gd <= node for pi, di in groups):
-            return [gr for gr in groups if gr != (0, 0)]
+            break
         n += 1
+    if D > 0 and n > D:
+        # a pod without a decode worker would have a prefill worker on its readiness/system port and
+        # no decode worker to hand its KV to inside the pod
+        raise ValidationError(f"{P} prefill + {D} decode workers need {n} group pods of at most {node} GPUs, "
+                              f"more pods than decode workers; use MXS_PD_POD_MODE=split for this layout")
+    return [gr for gr in groups if gr != (0, 0)]
+
+
+def group_shapes(groups: list) -> list:
+    """[(prefill workers, decode workers, pod count)] per distinct group-pod shape, most pods first
+    (the order of the shape Deployments: group_deployment_name)."""
+    shapes: dict = {}
+    for gr in groups:
+        shapes[gr] = shapes.get(gr, 0) + 1
+    return [(a, b, c) for (a, b), c in sorted(shapes.items(), key=lambda x: (-x[1], x[0]))]
 
 
 def _full_command(g: GraphSpec, s: ServiceSpec) -> list:
@@ -304,11 +362,16 @@ def _group_container(g: GraphSpec, d: ServiceSpec, p: ServiceSpec, n_pre: int, n
     return c
 
 
+def group_deployment_name(name: str, k: int) -> str:
+    """Deployment of the k-th (0-based) group-pod shape of a grouped decode service."""
+    return name if k == 0 else f"{name}-g{k + 1}"
+
+
 def _deployment(g: GraphSpec, name: str, labels: dict, owner: list, replicas: int, pod_spec: dict,
-                extra_selector: Optional[dict] = None) -> dict:
+                extra_selector: Optional[dict] = None, dep_name: Optional[str] = None) -> dict:
     sel = {"app.kubernetes.io/name": name, **(extra_selector or {})}
     return {"apiVersion": "apps/v1", "kind": "Deployment",
-            "metadata": {"name": name if not extra_selector else f"{name}-{extra_selector[SHAPE_LABEL]}",
+            "metadata": {"name": dep_name or name,
                          "namespace": g.namespace, "labels": dict(labels, **(extra_selector or {})),
                          "ownerReferences": owner},
             "spec": {"replicas": replicas, "selector": {"matchLabels": sel},
@@ -361,13 +424,12 @@ def render_children(g: GraphSpec, dcd_uids: Optional[dict] = None) -> list[dict]
 
         if grouped:
             labels[PAIR_LABEL] = f"{pair[0].key}+{pair[1].key}"
-            shapes: dict = {}
-            for gr in groups:
-                shapes[gr] = shapes.get(gr, 0) + 1
-            for k, ((n_pre, n_dec), count) in enumerate(sorted(shapes.items(), key=lambda x: (-x[1], x[0]))):
+            for k, (n_pre, n_dec, count) in enumerate(group_shapes(groups)):
+                # every shape Deployment selects on its own shape label (the first one too), so no
+                # two Deployments' selectors overlap; the Service and PodMonitor select on the name
                 c = _group_container(g, pair[0], pair[1], n_pre, n_dec)
-                objs.append(_deployment(g, name, labels, owner, count, pod(c),
-                                        None if k == 0 else {SHAPE_LABEL: f"g{k + 1}"}))
+                objs.append(_deployment(g, name, labels, owner, count, pod(c), {SHAPE_LABEL: f"g{k + 1}"},
+                                        group_deployment_name(name, k)))
         else:
             replicas = 0 if (pair is not None and s is pair[1]) else s.replicas
             objs.append(_deployment(g, name, labels, owner, replicas, pod(_container(g, s))))
@@ -465,7 +527,7 @@ def render_profiler_job(r: RequestSpec, job: str, results_cm: str) -> list[dict]
            "--output-configmap", results_cm, "--namespace", ns]
     if r.measure:
         cmd.append("--measure")
-    c = {"name": "profiler", "image": r.profiler_image or DEFAULT_IMAGE, "command": cmd,
+    c = {"name": "profiler", "image": map_image(r.profiler_image)[0], "command": cmd,
          "env": [{"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}]}
     if r.measure:
         c["resources"] = {"limits": {GPU_RESOURCE: "1"}, "requests": {GPU_RESOURCE: "1"}}

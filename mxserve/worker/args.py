@@ -12,8 +12,9 @@ Precedence: CLI > --extra-engine-args YAML > MXS_* env > defaults.
 from __future__ import annotations
 
 import argparse
+import logging
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Optional
 
 import yaml
@@ -30,6 +31,16 @@ class WorkerArgs:
     advertise_host: Optional[str] = None
     dialect: str = "vllm"
     worker_id: Optional[str] = None
+    # configuration problems the worker started with anyway (reported by /health "config_warnings")
+    warnings: list = field(default_factory=list)
+
+
+log = logging.getLogger("mxserve.worker.args")
+# the checkout / image root: the reference runs its workers from /workspace (examples/deploy/vllm/
+# agg.yaml:28) and points --extra-engine-args at ./examples/backends/... inside the NVIDIA image
+# (examples/dgdr/trtllm/disagg.yaml:29,39-40); the same relative paths exist under this root
+PACKAGE_ROOT = os.environ.get("MXS_EXAMPLES_ROOT") or os.path.dirname(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__))))
 
 
 def _parser(dialect: str) -> argparse.ArgumentParser:
@@ -101,12 +112,40 @@ _YAML_MAP = {
 }
 
 
-def load_extra_engine_args(path: str) -> dict:
-    """Parse a TRT-LLM/vLLM engine YAML into EngineArgs overrides.  A missing file is tolerated (the
-    reference points at paths inside the NVIDIA image, dgdr/trtllm/disagg.yaml:39-40)."""
-    if not path or not os.path.exists(path):
+def resolve_engine_args_path(path: str) -> Optional[str]:
+    """The file an --extra-engine-args path names: as given (relative to the working directory), else
+    the same path under PACKAGE_ROOT (a reference path like ./examples/backends/trtllm/engine_configs/
+    qwen3/prefill.yaml or /workspace/examples/... resolves to this image's copy).  None if neither."""
+    if not path:
+        return None
+    if os.path.exists(path):
+        return path
+    rel = os.path.normpath(path)
+    for prefix in ("/workspace/", "workspace/"):
+        if rel.startswith(prefix):
+            rel = rel[len(prefix):]
+    rel = rel.lstrip("/")
+    cand = os.path.join(PACKAGE_ROOT, rel)
+    return cand if os.path.exists(cand) else None
+
+
+def load_extra_engine_args(path: str, warnings: Optional[list] = None) -> dict:
+    """Parse a TRT-LLM/vLLM engine YAML into EngineArgs overrides.  The path is resolved against the
+    image layout (resolve_engine_args_path); a file that is still missing is NOT silently dropped: it
+    is logged and appended to `warnings` (the worker reports them in /health), and the worker starts
+    with its other settings."""
+    found = resolve_engine_args_path(path)
+    if found is None:
+        if path:
+            msg = (f"--extra-engine-args {path!r} not found (cwd {os.getcwd()!r}, image root {PACKAGE_ROOT!r}); "
+                   "starting without it")
+            log.warning(msg)
+            if warnings is not None:
+                warnings.append(msg)
         return {}
-    with open(path) as f:
+    if found != path:
+        log.info("--extra-engine-args %s resolved to %s", path, found)
+    with open(found) as f:
         d = yaml.safe_load(f) or {}
     out = {}
     for k, v in d.items():
@@ -127,8 +166,9 @@ def load_extra_engine_args(path: str) -> dict:
 def parse_worker_args(argv: list[str], dialect: str = "vllm") -> WorkerArgs:
     a = _parser(dialect).parse_args(argv)
     kw = env_overrides()
+    warnings: list = []
     if a.extra_engine_args:
-        kw.update(load_extra_engine_args(a.extra_engine_args))
+        kw.update(load_extra_engine_args(a.extra_engine_args, warnings))
     cli = {
         "model": a.model, "served_model_name": a.served_model_name, "dtype": a.dtype, "load_format": a.load_format,
         "seed": a.seed, "tensor_parallel_size": a.tp, "block_size": a.block_size, "max_model_len": a.max_model_len,
@@ -156,4 +196,4 @@ def parse_worker_args(argv: list[str], dialect: str = "vllm") -> WorkerArgs:
     if eng.model is None:
         raise SystemExit("--model / --model-path is required")
     return WorkerArgs(engine=eng, host=a.host, port=a.port, frontend_url=a.frontend_url,
-                      advertise_host=a.advertise_host, dialect=dialect, worker_id=a.worker_id)
+                      advertise_host=a.advertise_host, dialect=dialect, worker_id=a.worker_id, warnings=warnings)

@@ -163,6 +163,7 @@ class Worker:
     def __init__(self, wargs: WorkerArgs, engine: Optional[LLMEngine] = None):
         self.wargs = wargs
         self.args = wargs.engine
+        self.config_warnings = list(getattr(wargs, "warnings", []) or [])
         self.engine = engine or LLMEngine(self.args)
         self.aeng = AsyncEngine(self.engine)
         self.role = self.args.disagg_mode
@@ -548,7 +549,10 @@ class Worker:
             rp = getattr(w, "_ring_plane", None)
             if rp is not None and (rp.dead or rp.streamer_exited()):  # its token plane is gone
                 return JSONResponse({"status": "streamer down"}, status_code=503)
-            return {"status": "ready", "model": w.model, "role": w.role, "worker_id": w.worker_id}
+            out = {"status": "ready", "model": w.model, "role": w.role, "worker_id": w.worker_id}
+            if w.config_warnings:
+                out["config_warnings"] = list(w.config_warnings)
+            return out
 
         @app.get("/live")
         async def live():
