@@ -11,6 +11,10 @@ find Deployments by `nvidia.com/dynamo-namespace=<ns>-<dgd>` and Services by `<d
 NodePort for every non-headless Service (fixed port for the frontend if given) -> wait for every
 Deployment ready (all replicas, not just the first pod) -> wait for the frontend's Endpoints ->
 print the quick test.  With a token, every DGD service gets envFromSecret: hf-token-secret.
+While it waits it prints, every MXS_PROGRESS_SECONDS (15), each Deployment's ready count, each pod's
+phase and container waiting reasons (ImagePullBackOff, CrashLoopBackOff, ...) and the namespace's
+recent Warning events (e.g. FailedScheduling: Insufficient amd.com/gpu), as the reference's wait loop
+does (deploy-incluster.sh:511-605); a timeout error carries the same report.
 Fixes the reference quirks listed in SURVEY.md Appendix B items 2, 3 and 5.
 """
 from __future__ import annotations
@@ -56,18 +60,74 @@ def parse_args(argv=None) -> argparse.Namespace:
     a.services_timeout = int(e.get("SERVICES_TIMEOUT", "180"))
     a.deployments_timeout = int(e.get("DEPLOYMENTS_TIMEOUT", "180"))
     a.poll = float(e.get("MXS_POLL_SECONDS", "3"))
+    a.progress = float(e.get("MXS_PROGRESS_SECONDS", "15"))
     return a
 
 
-def _poll(fn, timeout: float, interval: float, what: str):
-    t0 = time.time()
+def _poll(fn, timeout: float, interval: float, what: str, report=None, every: float = 15.0):
+    """Call fn until it returns something truthy.  `report()` (a list of lines) is printed every
+    `every` seconds while waiting and appended to the timeout error."""
+    t0 = last = time.time()
     while True:
         v = fn()
         if v:
             return v
-        if time.time() - t0 > timeout:
-            raise DeployError(f"timed out after {timeout:.0f}s waiting for {what}")
+        now = time.time()
+        if now - t0 > timeout:
+            lines = report() if report else []
+            raise DeployError(f"timed out after {timeout:.0f}s waiting for {what}" +
+                              ("".join("\n  " + ln for ln in lines) if lines else ""))
+        if report and now - last >= every:
+            last = now
+            print(f"... waiting for {what} ({now - t0:.0f}s / {timeout:.0f}s)", flush=True)
+            for ln in report():
+                print("    " + ln, flush=True)
         time.sleep(interval)
+
+
+def _ts(ev: dict) -> str:
+    return str(ev.get("lastTimestamp") or ev.get("eventTime") or (ev.get("metadata") or {}).get("creationTimestamp")
+               or "")
+
+
+def status_report(k: KubeClient, ns: str, sel: str, max_events: int = 6) -> list:
+    """Human-readable state of a graph's Deployments, pods and recent Warning events."""
+    out = []
+    try:
+        names = set()
+        for d in k.list("Deployment", ns, sel):
+            st = d.get("status") or {}
+            names.add(d["metadata"]["name"])
+            out.append(f"deployment {d['metadata']['name']}: ready {int(st.get('readyReplicas', 0) or 0)}/"
+                       f"{int(d['spec'].get('replicas', 1))}")
+        for p in k.list("Pod", ns, sel):
+            names.add(p["metadata"]["name"])
+            st = p.get("status") or {}
+            cs = st.get("containerStatuses") or []
+            ready = sum(1 for c in cs if c.get("ready"))
+            why = []
+            for c in cs:
+                for state in ("waiting", "terminated"):
+                    w = (c.get("state") or {}).get(state)
+                    if w and w.get("reason"):
+                        why.append(f"{c.get('name')}: {w['reason']}" + (f" ({w['message'][:120]})" if w.get("message")
+                                                                       else ""))
+                if c.get("restartCount"):
+                    why.append(f"{c.get('name')}: {c['restartCount']} restarts")
+            for cond in st.get("conditions") or []:
+                if cond.get("type") == "PodScheduled" and cond.get("status") == "False":
+                    why.append(f"unschedulable: {cond.get('message', cond.get('reason', ''))[:160]}")
+            out.append(f"pod {p['metadata']['name']}: {st.get('phase', '?')} {ready}/{len(cs) or 1}"
+                       + (" -- " + "; ".join(why) if why else ""))
+        evs = [e for e in k.list("Event", ns) if e.get("type") == "Warning"
+               and any(((e.get("involvedObject") or {}).get("name") or "").startswith(n) for n in names)]
+        for e in sorted(evs, key=_ts)[-max_events:]:
+            io = e.get("involvedObject") or {}
+            out.append(f"event {io.get('kind', '')}/{io.get('name', '')}: {e.get('reason', '')}: "
+                       f"{(e.get('message') or '')[:160]}")
+    except (ApiError, OSError) as e:  # a report never turns into the error itself
+        out.append(f"(status unavailable: {e})")
+    return out
 
 
 def run(a: argparse.Namespace, k: Optional[KubeClient] = None) -> dict:
@@ -134,14 +194,18 @@ def run(a: argparse.Namespace, k: Optional[KubeClient] = None) -> dict:
                 ds = k.list("Deployment", ns, sel)
                 return all(int((d.get("status") or {}).get("readyReplicas", 0) or 0) >= int(d["spec"].get("replicas", 1))
                            for d in ds) and ds
-            _poll(ready, a.pods_timeout, a.poll, f"all pods of {g} ready")
+            _poll(ready, a.pods_timeout, a.poll, f"all pods of {g} ready",
+                  report=lambda: status_report(k, ns, sel), every=a.progress)
+            for ln in status_report(k, ns, sel):
+                print("    " + ln, flush=True)
             # reference wait_endpoints (:94-108, :573): the frontend Service routes to a ready pod
             fe_name = fe[0]["metadata"]["name"]
 
             def has_endpoints():
                 ep = k.get("Endpoints", fe_name, ns) or {}
                 return any(ss.get("addresses") for ss in ep.get("subsets") or [])
-            _poll(has_endpoints, a.endpoints_timeout, a.poll, f"endpoints of {fe_name}")
+            _poll(has_endpoints, a.endpoints_timeout, a.poll, f"endpoints of {fe_name}",
+                  report=lambda: status_report(k, ns, sel), every=a.progress)
         result["graphs"][g] = {"deployments": sorted(d["metadata"]["name"] for d in deps),
                                "services": sorted(s["metadata"]["name"] for s in svcs),
                                "frontend": fe[0]["metadata"]["name"], "nodeports": ports}
