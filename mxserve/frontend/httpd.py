@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
 import signal
 import socket
 from typing import Awaitable, Callable, Optional
@@ -25,6 +26,10 @@ log = logging.getLogger("mxserve.frontend.httpd")
 
 MAX_HEAD = 64 << 10
 MAX_BODY = 256 << 20
+# a request's head and body must arrive within HEADER_TIMEOUT_S of its first byte (slowloris); an idle
+# keep-alive connection is closed after IDLE_TIMEOUT_S
+HEADER_TIMEOUT_S = float(os.environ.get("MXS_HTTP_HEADER_TIMEOUT_S", "30"))
+IDLE_TIMEOUT_S = float(os.environ.get("MXS_HTTP_IDLE_TIMEOUT_S", "75"))
 _REASONS = {200: "OK", 204: "No Content", 400: "Bad Request", 404: "Not Found", 405: "Method Not Allowed",
             408: "Request Timeout", 411: "Length Required", 413: "Payload Too Large", 422: "Unprocessable Entity",
             429: "Too Many Requests", 500: "Internal Server Error", 503: "Service Unavailable"}
@@ -56,6 +61,9 @@ class Connection(asyncio.Protocol):
         self.transport: Optional[asyncio.Transport] = None
         self.buf = bytearray()
         self.busy = False  # a request is being answered; later bytes wait in buf
+        self._timer: Optional[asyncio.TimerHandle] = None
+        self._timer_kind = ""  # "idle" | "head" | ""
+        self._continued = False  # 100 Continue already sent for the request being received
         self.closed = False
         self.on_close: list = []  # callbacks run once the client is gone (abort its request)
         self.keep_alive = True
@@ -72,9 +80,38 @@ class Connection(asyncio.Protocol):
             except OSError:
                 pass
         self.server.conns.add(self)
+        self._arm()
+
+    # ------------------------------------------------------------------ timeouts
+    def _arm(self) -> None:
+        """Idle connection: IDLE_TIMEOUT_S; a request partly received: HEADER_TIMEOUT_S from its first
+        byte; a request being answered: no timer."""
+        want = "" if (self.busy or self.closed) else ("head" if self.buf else "idle")
+        if want == self._timer_kind:
+            return
+        if self._timer is not None:
+            self._timer.cancel()
+            self._timer = None
+        self._timer_kind = want
+        if want:
+            loop = asyncio.get_event_loop()
+            self._timer = loop.call_later(HEADER_TIMEOUT_S if want == "head" else IDLE_TIMEOUT_S, self._expire, want)
+
+    def _expire(self, kind: str) -> None:
+        self._timer = None
+        self._timer_kind = ""
+        if self.closed or self.busy:
+            return
+        if kind == "head":
+            self._fail(408, "request not received in time")
+        elif self.transport is not None:
+            self.transport.close()
 
     def connection_lost(self, exc) -> None:
         self.closed = True
+        if self._timer is not None:
+            self._timer.cancel()
+            self._timer = None
         self.server.conns.discard(self)
         if self._drain is not None and not self._drain.done():
             self._drain.set_result(None)
@@ -102,6 +139,7 @@ class Connection(asyncio.Protocol):
         self.buf += data
         if not self.busy:
             self._next()
+        self._arm()
 
     # ------------------------------------------------------------------ parsing
     def _next(self) -> None:
@@ -110,6 +148,8 @@ class Connection(asyncio.Protocol):
             if req is None:
                 return
             self.busy = True
+            self._continued = False
+            self._arm()
             asyncio.ensure_future(self._handle(req))
 
     def _parse(self) -> Optional[Request]:
@@ -125,17 +165,23 @@ class Connection(asyncio.Protocol):
             self._fail(400, "bad request line")
             return None
         headers = []
-        clen = 0
+        clen = None
+        expect_continue = False
         for line in head[1:]:
             k, _, v = line.partition(":")
             k, v = k.strip().lower(), v.strip()
             headers.append((k.encode("latin-1"), v.encode("latin-1")))
             if k == "content-length":
-                try:
-                    clen = int(v)
-                except ValueError:
+                # digits only (int() would take "-5", "+5", "1_0"); a repeated header must agree
+                if not v or not v.isascii() or not v.isdigit():
                     self._fail(400, "bad content-length")
                     return None
+                if clen is not None and int(v) != clen:
+                    self._fail(400, "conflicting content-length headers")
+                    return None
+                clen = int(v)
+            elif k == "expect" and v.lower() == "100-continue":
+                expect_continue = True
             elif k == "transfer-encoding" and v.lower() != "identity":
                 self._fail(411, "chunked request bodies are not supported; send Content-Length")
                 return None
@@ -143,10 +189,14 @@ class Connection(asyncio.Protocol):
                 self.keep_alive = v.lower() != "close"
         if version == "HTTP/1.0":
             self.keep_alive = any(k == b"connection" and v.lower() == b"keep-alive" for k, v in headers)
+        clen = clen or 0
         if clen > MAX_BODY:
             self._fail(413, "request body too large")
             return None
         if len(self.buf) < end + 4 + clen:
+            if expect_continue and not self._continued and version != "HTTP/1.0":
+                self._continued = True
+                self.write(b"HTTP/1.1 100 Continue\r\n\r\n")
             return None
         body = bytes(self.buf[end + 4:end + 4 + clen])
         del self.buf[:end + 4 + clen]
@@ -198,6 +248,7 @@ class Connection(asyncio.Protocol):
         self.busy = False
         if self.buf:
             self._next()
+        self._arm()
 
     async def _handle(self, req: Request) -> None:
         try:

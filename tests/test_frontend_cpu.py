@@ -759,3 +759,93 @@ def test_httpd_keep_alive_errors_and_bridge(agg_stack):
         assert lines[-1] == "data: [DONE]" and len(lines) >= 2
         assert c.get("/health").status_code == 200
         assert "dynamo_frontend_requests_total" in c.get("/metrics").text
+
+
+def test_httpd_rejects_bad_lengths_times_out_slow_heads_and_continues(monkeypatch):
+    """Content-Length is digits only and repeated values must agree (400 otherwise); a
+    request head that does not complete within the header timeout gets 408 and a close; an idle
+    keep-alive connection is closed; Expect: 100-continue gets an interim 100 before the body."""
+    import asyncio
+    import socket as _socket
+    import threading
+    import time
+
+    from mxserve.frontend import httpd
+
+    monkeypatch.setattr(httpd, "HEADER_TIMEOUT_S", 0.5)
+    monkeypatch.setattr(httpd, "IDLE_TIMEOUT_S", 0.8)
+
+    async def app(scope, receive, send):
+        if scope["type"] == "lifespan":
+            while True:
+                m = await receive()
+                await send({"type": m["type"] + ".complete"})
+                if m["type"] == "lifespan.shutdown":
+                    return
+        msg = await receive()
+        body = b"got %d" % len(msg["body"])
+        await send({"type": "http.response.start", "status": 200, "headers": [(b"content-type", b"text/plain")]})
+        await send({"type": "http.response.body", "body": body})
+
+    sock = httpd.listen("127.0.0.1", 0)
+    port = sock.getsockname()[1]
+    loop = asyncio.new_event_loop()
+    stop = asyncio.Event()
+    srv = httpd.Server(app)
+    th = threading.Thread(target=lambda: loop.run_until_complete(srv.serve(sock, stop)), daemon=True)
+    th.start()
+
+    def talk(data: bytes, wait: float = 0.3, read_until_close: bool = False) -> bytes:
+        c = _socket.create_connection(("127.0.0.1", port), timeout=5)
+        c.sendall(data)
+        time.sleep(wait)
+        out = b""
+        c.settimeout(3)
+        try:
+            while True:
+                b = c.recv(65536)
+                if not b:
+                    break
+                out += b
+                if not read_until_close and b"\r\n\r\n" in out and out.count(b"HTTP/1.1") >= 1 and b"got" in out:
+                    break
+        except _socket.timeout:
+            pass
+        c.close()
+        return out
+
+    try:
+        time.sleep(0.3)
+        ok = talk(b"POST / HTTP/1.1\r\nhost: x\r\ncontent-length: 3\r\n\r\nabc")
+        assert ok.startswith(b"HTTP/1.1 200") and b"got 3" in ok
+        for bad in (b"-5", b"+3", b"1_0", b"3 3", b""):
+            r = talk(b"POST / HTTP/1.1\r\nhost: x\r\ncontent-length: " + bad + b"\r\n\r\nabc", read_until_close=True)
+            assert r.startswith(b"HTTP/1.1 400"), (bad, r)
+        r = talk(b"POST / HTTP/1.1\r\ncontent-length: 3\r\ncontent-length: 4\r\n\r\nabcd", read_until_close=True)
+        assert r.startswith(b"HTTP/1.1 400") and b"conflicting" in r
+        r = talk(b"POST / HTTP/1.1\r\ncontent-length: 3\r\ncontent-length: 3\r\n\r\nabc")
+        assert r.startswith(b"HTTP/1.1 200")
+        # slowloris: half a head, then nothing -> 408 and the connection is closed
+        r = talk(b"POST / HTTP/1.1\r\nhost: x\r\n", wait=1.0, read_until_close=True)
+        assert r.startswith(b"HTTP/1.1 408"), r
+        # idle keep-alive connection: closed by the server
+        c = _socket.create_connection(("127.0.0.1", port), timeout=5)
+        t0 = time.time()
+        c.settimeout(5)
+        assert c.recv(10) == b""  # EOF from the idle timeout
+        assert time.time() - t0 < 4
+        c.close()
+        # Expect: 100-continue -> interim response, then the real one after the body
+        c = _socket.create_connection(("127.0.0.1", port), timeout=5)
+        c.sendall(b"POST / HTTP/1.1\r\nhost: x\r\nexpect: 100-continue\r\ncontent-length: 5\r\n\r\n")
+        c.settimeout(3)
+        assert c.recv(100).startswith(b"HTTP/1.1 100 Continue")
+        c.sendall(b"hello")
+        out = b""
+        while b"got 5" not in out:
+            out += c.recv(1000)
+        assert b"HTTP/1.1 200" in out
+        c.close()
+    finally:
+        loop.call_soon_threadsafe(stop.set)
+        th.join(timeout=10)
