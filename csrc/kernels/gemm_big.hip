@@ -316,6 +316,210 @@ __global__ void __launch_bounds__(512) gemm_big_ring_kernel(bf16_t* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Ping-pong variant (variant 6): the same 256 x 256 x 64 tile, but the 8 waves run as two groups of 4
+// that are one barrier apart (waves w and w + 4 share a SIMD), so on every SIMD one wave's 16-MFMA
+// segment runs beside its partner's LDS-read / DMA-issue segment (cdna_hip_programming.md §5 "256²
+// 8-phase template", MI355X_MICROARCH.md "Two waves per SIMD").
+//
+//   * a wave owns 128 tokens x 64 weight rows (acc[4 w-frags][8 token-frags]); a k-tile is 4 phases,
+//     one output quadrant (2 w-frags x 4 token-frags x 2 k-steps = 16 MFMAs) each, visited in the
+//     order (w0,t0) (w1,t0) (w1,t1) (w0,t1): fragment reads per phase 12 / 4 / 8 / 0 ds_read_b128,
+//     each operand read once per k-tile;
+//   * LDS = 2 k-tile buffers x 4 half-tiles (X rows 0-127, X rows 128-255, W rows 0-127, W rows
+//     128-255) of 16 KB; half-tiles of k-tile u + 1 are DMA'd at phases 3 (of u - 1), 0 and 1 (of u),
+//     each thread issuing 2 global_load_lds_dwordx4 per half-tile, and the only vmcnt wait is at phase
+//     3 (vmcnt(0), before that phase's DMA issue) -- the youngest half-tile then has had two phases to
+//     land.  Buffer u & 1 is last read at phase 2 of u, and refilled from phase 3 of u on;
+//   * every load segment ends with lgkmcnt(0) before its barrier, so a barrier retires all reads
+//     issued before it (the DMA that reuses a buffer is issued behind such a barrier).
+template <int EPI>
+__global__ void __launch_bounds__(512, 1) gemm_pp_kernel(bf16_t* __restrict__ Y, const bf16_t* __restrict__ X,
+                                                         const bf16_t* __restrict__ W, int M, int K, int ldx, int ldy,
+                                                         int inter, int ntm, int ntn) {
+  constexpr int HT = 16384, KT = 4 * HT;
+  __shared__ __attribute__((aligned(16))) char smem[2 * KT];
+
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  constexpr int GM = 8;
+  const int per_group = GM * ntn, grp = wg / per_group, first_m = grp * GM;
+  const int gsz = min(ntm - first_m, GM), in_grp = wg - grp * per_group;
+  const int tm = first_m + in_grp % gsz, tn = in_grp / gsz;
+  const int m0 = tm * 256;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;  // token half, 64-row weight block
+
+  // DMA sources: half-tile h, instruction j (0, 1) of this wave fills half-tile rows 8 (2 wid + j) .. +7
+  const bf16_t* src[4][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * (2 * wid + j) + (lane >> 3);  // row inside the half-tile
+    const int gch = (lane & 7) ^ ((row >> 1) & 7);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      src[h][j] = X + static_cast<size_t>(min(m0 + 128 * h + row, M - 1)) * ldx + 8 * gch;
+      const int r = 128 * h + row;  // weight image row
+      int wrow;
+      if constexpr (EPI == GB_EPI_SWIGLU) {
+        const int fr = (r >> 4) & 3, feat = tn * 128 + 32 * (r >> 6) + 16 * (fr & 1) + (r & 15);
+        wrow = fr < 2 ? feat : inter + feat;
+      } else {
+        wrow = tn * 256 + r;
+      }
+      src[2 + h][j] = W + static_cast<size_t>(wrow) * K + 8 * gch;
+    }
+  }
+  auto stage = [&](int h, int u) {  // half-tile h of k-tile u
+    char* dst = smem + (u & 1) * KT + h * HT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(src[h][j] + 64 * u),
+                                       (__attribute__((address_space(3))) void*)(dst + (2 * wid + j) * 1024), 16, 0,
+                                       0);
+  };
+
+  float4_ acc[4][8];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[f][t] = float4_{0.f, 0.f, 0.f, 0.f};
+
+  const int r16 = lane & 15, kq = lane >> 4;
+  // byte offsets (inside a k-tile buffer) of this lane's fragment rows, k-chunk 0
+  int woff[4], xoff[8];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const int row = 64 * (wc & 1) + 16 * f + r16;
+    woff[f] = (2 + (wc >> 1)) * HT + row * 128;
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) xoff[t] = wr * HT + (16 * t + r16) * 128;
+  // chunk c of row r sits at slot c ^ ((r >> 1) & 7); r16 fixes (r >> 1) & 7 for every fragment row
+  const int swz = (r16 >> 1) & 7;
+  const int sl0 = ((kq) ^ swz) << 4, sl1 = ((4 + kq) ^ swz) << 4;
+
+  gb_u32x4 wa[2][2][2], xb[4][2];  // [w half][frag][k-step], [token frag][k-step]
+  auto rd_w = [&](const char* b, int a) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      wa[a][f][0] = *reinterpret_cast<const gb_u32x4*>(b + woff[2 * a + f] + sl0);
+      wa[a][f][1] = *reinterpret_cast<const gb_u32x4*>(b + woff[2 * a + f] + sl1);
+    }
+  };
+  auto rd_x = [&](const char* b, int hb) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      xb[t][0] = *reinterpret_cast<const gb_u32x4*>(b + xoff[4 * hb + t] + sl0);
+      xb[t][1] = *reinterpret_cast<const gb_u32x4*>(b + xoff[4 * hb + t] + sl1);
+    }
+  };
+  auto quad = [&](int a, int hb) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[2 * a + f][4 * hb + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              gb_frag(wa[a][f][kk]), gb_frag(xb[t][kk]), acc[2 * a + f][4 * hb + t], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+#define PP_BAR()                           \
+  do {                                     \
+    __builtin_amdgcn_sched_barrier(0);     \
+    __builtin_amdgcn_s_barrier();          \
+    __builtin_amdgcn_sched_barrier(0);     \
+  } while (0)
+#define PP_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+  const int nk = K / 64;
+  // prologue: all of k-tile 0, half-tiles 0 and 1 of k-tile 1
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(h, 0);
+  if (nk > 1) {
+    stage(0, 1);
+    stage(1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  PP_BAR();
+  if (wr == 1) PP_BAR();  // the stagger: waves 4-7 run one barrier behind waves 0-3
+
+  for (int u = 0; u < nk; ++u) {
+    const char* b = smem + (u & 1) * KT;
+    const bool nxt = u + 1 < nk;
+    // phase 0: quadrant (w0, t0)
+    if (nxt) stage(2, u + 1);
+    rd_w(b, 0);
+    rd_x(b, 0);
+    PP_LGKM0();
+    PP_BAR();
+    quad(0, 0);
+    PP_BAR();
+    // phase 1: (w1, t0)
+    if (nxt) stage(3, u + 1);
+    rd_w(b, 1);
+    PP_LGKM0();
+    PP_BAR();
+    quad(1, 0);
+    PP_BAR();
+    // phase 2: (w1, t1) -- the last reads of buffer u & 1
+    rd_x(b, 1);
+    PP_LGKM0();
+    PP_BAR();
+    quad(1, 1);
+    PP_BAR();
+    // phase 3: (w0, t1); k-tile u + 1 complete; start k-tile u + 2 in buffer u & 1
+    if (nxt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (u + 2 < nk) {
+        stage(0, u + 2);
+        stage(1, u + 2);
+      }
+    }
+    PP_BAR();
+    quad(0, 1);
+    PP_BAR();
+  }
+  if (wr == 0) PP_BAR();  // balance the stagger barrier
+#undef PP_BAR
+#undef PP_LGKM0
+
+  // epilogue: lane (r16, kq), acc[f][t]: token m0 + 128 wr + 16 t + r16, image rows 64 wc + 16 f + 4 kq + e
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int m = m0 + 128 * wr + 16 * t + r16;
+    if (m >= M) continue;
+    bf16_t* yr = Y + static_cast<size_t>(m) * ldy;
+    if constexpr (EPI == GB_EPI_SWIGLU) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const float4_& g = acc[p][t];
+        const float4_& v = acc[p + 2][t];
+        const int n = tn * 128 + 32 * wc + 16 * p + 4 * kq;
+        uint2 o;
+        o.x = pack2(gb_silu(g[0]) * v[0], gb_silu(g[1]) * v[1]);
+        o.y = pack2(gb_silu(g[2]) * v[2], gb_silu(g[3]) * v[3]);
+        *reinterpret_cast<uint2*>(yr + n) = o;
+      }
+    } else {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const float4_& a = acc[f][t];
+        const int n = tn * 256 + 64 * wc + 16 * f + 4 * kq;
+        uint2 o;
+        o.x = pack2(a[0], a[1]);
+        o.y = pack2(a[2], a[3]);
+        *reinterpret_cast<uint2*>(yr + n) = o;
+      }
+    }
+  }
+}
+
 // epi 0: Y [M, N] = X W^T (N % 256 == 0).  epi 1 (SwiGLU): W = [gate; up] rows [2 I, K], Y [M, I] =
 // SiLU(X gate^T) * (X up^T) (I % 128 == 0).  K % 64 == 0, 16-byte aligned rows.  False when the
 // shape is not supported (the caller keeps its other path).
@@ -323,7 +527,7 @@ __global__ void __launch_bounds__(512) gemm_big_ring_kernel(bf16_t* __restrict__
 // the MFMA clusters
 bool launch_gemm_big(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx, int ldy, int epi,
                      int variant, hipStream_t s) {
-  if (M <= 0 || K % 64 != 0 || ldx % 8 != 0 || ldy % 4 != 0 || variant < 0 || variant > 5) return false;
+  if (M <= 0 || K % 64 != 0 || ldx % 8 != 0 || ldy % 4 != 0 || variant < 0 || variant > 6) return false;
   if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W)) & 15) return false;
   if (reinterpret_cast<uintptr_t>(Y) & 7) return false;
   if (N % 256 != 0 || (epi != GB_EPI_NONE && epi != GB_EPI_SWIGLU)) return false;  // SwiGLU: N = 2 I, I % 128 == 0
@@ -337,14 +541,16 @@ bool launch_gemm_big(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, 
     else if (variant == 2) MXS_GB((gemm_big_ring_kernel<GB_EPI_SWIGLU, true>));
     else if (variant == 3) MXS_GB((gemm_big_kernel<GB_EPI_SWIGLU, 1>));
     else if (variant == 4) MXS_GB((gemm_big_kernel<GB_EPI_SWIGLU, 2>));
-    else MXS_GB((gemm_big_kernel<GB_EPI_SWIGLU, 3>));
+    else if (variant == 5) MXS_GB((gemm_big_kernel<GB_EPI_SWIGLU, 3>));
+    else MXS_GB(gemm_pp_kernel<GB_EPI_SWIGLU>);
   } else {
     if (variant == 0) MXS_GB(gemm_big_kernel<GB_EPI_NONE>);
     else if (variant == 1) MXS_GB((gemm_big_ring_kernel<GB_EPI_NONE, false>));
     else if (variant == 2) MXS_GB((gemm_big_ring_kernel<GB_EPI_NONE, true>));
     else if (variant == 3) MXS_GB((gemm_big_kernel<GB_EPI_NONE, 1>));
     else if (variant == 4) MXS_GB((gemm_big_kernel<GB_EPI_NONE, 2>));
-    else MXS_GB((gemm_big_kernel<GB_EPI_NONE, 3>));
+    else if (variant == 5) MXS_GB((gemm_big_kernel<GB_EPI_NONE, 3>));
+    else MXS_GB(gemm_pp_kernel<GB_EPI_NONE>);
   }
 #undef MXS_GB
   MXS_CHECK_LAUNCH();

@@ -14,6 +14,7 @@ from __future__ import annotations
 import asyncio
 import bisect
 import json
+import logging
 import time
 import uuid
 from typing import Optional
@@ -24,6 +25,9 @@ from .tokenizer import IncrementalDetokenizer
 
 # a client that reads slower than this much buffered output is dropped (its request is aborted)
 MAX_BUFFERED = 16 << 20
+
+
+log = logging.getLogger("mxserve.frontend.fastpath")
 
 
 class ClientGone(ConnectionError):
@@ -298,21 +302,25 @@ async def handle(fe, req, conn) -> bool:
     endpoint = "chat_completions" if chat else "completions"
     task = asyncio.current_task()
     conn.on_close.append(task.cancel)  # the client left: stop routing / waiting, abort on the worker
-    status = "success"
+    status, reason, err = "success", "ok", None
     ps.head()
     try:
         await fe.run_push(model, ids, sampling, ps.rid, ps)
         ps.finish_ok()
     except asyncio.CancelledError:
-        status = "error"
+        status, reason = "error", "client_gone"
     except APIError as e:
-        status = "error"
+        status, reason, err = "error", f"api_error_{e.status}", e
         ps.finish_error(e.message, e.etype, e.status)
     except Exception as e:  # noqa: BLE001 - reported in the stream, like the FastAPI path
-        status = "error"
+        status, reason, err = "error", f"error_{type(e).__name__}", e
         ps.finish_error(str(e))
     finally:
         ps.record(status, endpoint)
+        fe.metrics.stream_close.labels(model, reason).inc()
+        if reason != "ok":
+            log.warning("stream %s closed early: %s after %d tokens%s", ps.rid, reason, ps.n,
+                        f" ({err!r})" if err is not None else "")
         conn.end_chunked()
         conn.finish()
     return True

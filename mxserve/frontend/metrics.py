@@ -48,6 +48,9 @@ class FrontendMetrics:
                               ["model"], registry=r)
         self.migrations = Counter("dynamo_frontend_request_migrations", "Streams moved to another worker mid-request",
                                   ["model"], registry=r)
+        # why each streamed response ended: ok | client_gone | api_error_<status> | error_<exception type>
+        self.stream_close = Counter("dynamo_frontend_stream_close", "Streamed responses by close reason",
+                                    ["model", "reason"], registry=r)
 
     def render(self) -> bytes:
         if _multiproc():

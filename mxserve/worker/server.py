@@ -135,6 +135,7 @@ class MuxChannel:
         self.closed = False
 
     async def lines(self, aeng: AsyncEngine):
+        why = "frontend closed the channel"
         try:
             yield (json.dumps({"hello": self.sid}) + "\n").encode()
             while True:
@@ -151,7 +152,13 @@ class MuxChannel:
                         self.rids.discard(rid)
                 if batch:
                     yield (json.dumps({"b": batch}) + "\n").encode()
+        except BaseException as e:  # noqa: BLE001 - logged, then re-raised
+            why = "frontend disconnected" if isinstance(e, (GeneratorExit, asyncio.CancelledError)) else repr(e)
+            raise
         finally:  # the frontend went away: its requests have nobody to stream to
+            if self.rids:
+                log.warning("mux channel %s closed (%s): aborting %d in-flight requests", self.sid,
+                            "replaced by a new channel" if self.closed else why, len(self.rids))
             self.closed = True
             for rid in list(self.rids):
                 if aeng._queues.pop(rid, None) is not None:

@@ -221,6 +221,7 @@ def build_app(cmd_ring, out_ring, parent_pid: Optional[int] = None):
         ch = chans[sid] = _Chan(sid)
 
         async def lines():
+            why = "frontend closed the channel"
             try:
                 yield (json.dumps({"hello": sid}) + "\n").encode()
                 while True:
@@ -231,7 +232,13 @@ def build_app(cmd_ring, out_ring, parent_pid: Optional[int] = None):
                     for t in outs:
                         by_rid.setdefault(t[0], []).append(t)
                     yield (json.dumps({"b": [[rid, _batch_dict(os_)] for rid, os_ in by_rid.items()]}) + "\n").encode()
+            except BaseException as e:  # noqa: BLE001 - logged, then re-raised
+                why = "frontend disconnected" if isinstance(e, (GeneratorExit, asyncio.CancelledError)) else repr(e)
+                raise
             finally:  # the frontend went away: abort its requests
+                if ch.rids:
+                    log.warning("mux channel %s closed (%s): aborting %d in-flight requests", sid,
+                                "replaced by a new channel" if chans.get(sid) is not ch else why, len(ch.rids))
                 ch.closed = True
                 for rid in list(ch.rids):
                     owner.pop(rid, None)

@@ -128,17 +128,24 @@ def fake_worker(port: int, frontend: str, wid: str, step_ms: float) -> None:
 def client(port: int, rate: float, duration: float, osl: int, seed: int, out: str) -> None:
     rng = random.Random(seed)
     res = {"ttft": [], "gaps": [], "done": 0, "dropped": 0, "tokens": 0, "t0": time.perf_counter(), "t1": 0.0,
-           "per_s": {}}
+           "per_s": {}, "drop_reasons": {}}
+
+    def drop(reason: str) -> None:
+        res["dropped"] += 1
+        res["drop_reasons"][reason] = res["drop_reasons"].get(reason, 0) + 1
 
     class Stream(asyncio.Protocol):
         """One streaming request on its own connection; data_received counts SSE chunks (no
         StreamReader / task wakeup per read: the client must be cheaper than what it measures)."""
-        __slots__ = ("t_sched", "n", "first", "last", "tail", "done", "fut", "tr")
+        __slots__ = ("t_sched", "n", "first", "last", "tail", "done", "fut", "tr", "status", "err", "lost")
 
         def __init__(self, t_sched: float, body: bytes, fut):
             self.t_sched, self.n, self.first, self.last, self.tail, self.done = t_sched, 0, None, None, b"", False
             self.fut = fut
             self.tr = body
+            self.status = None  # HTTP status of the response
+            self.err = None  # the stream's SSE error message, if it sent one
+            self.lost = None  # repr of the connection_lost exception
 
         def connection_made(self, tr):
             body, self.tr = self.tr, tr
@@ -147,6 +154,11 @@ def client(port: int, rate: float, duration: float, osl: int, seed: int, out: st
 
         def data_received(self, data):
             now = time.perf_counter()
+            if self.status is None and data.startswith(b"HTTP/1.1 "):
+                self.status = int(data[9:12])
+            if self.err is None and b'data: {"error"' in data:
+                i = data.find(b'data: {"error"')
+                self.err = data[i + 6:data.find(b"\n", i)].decode(errors="replace")[:200]
             buf = self.tail + data  # the tail (11 bytes) cannot hold a whole `data: {`: nothing counts twice
             k = buf.count(b"data: {")
             if k:
@@ -165,6 +177,8 @@ def client(port: int, rate: float, duration: float, osl: int, seed: int, out: st
             self.tail = buf[-11:]
 
         def connection_lost(self, exc):
+            if exc is not None:
+                self.lost = repr(exc)[:120]
             if not self.fut.done():
                 self.fut.set_result(None)
 
@@ -178,14 +192,21 @@ def client(port: int, rate: float, duration: float, osl: int, seed: int, out: st
         fut = loop.create_future()
         try:
             _, st = await loop.create_connection(lambda: Stream(t_sched, body, fut), "127.0.0.1", port)
-        except OSError:
-            res["dropped"] += 1
+        except OSError as e:
+            drop(f"connect: {type(e).__name__} {getattr(e, 'errno', '')}")
             return
         await fut
         if st.done and st.n >= osl:
             res["done"] += 1
+        elif st.status is not None and st.status != 200:
+            drop(f"http {st.status}")
+        elif st.err is not None:
+            drop(f"stream error: {st.err}")
+        elif st.done:
+            drop(f"[DONE] after {st.n} < {osl} tokens")
         else:
-            res["dropped"] += 1
+            drop(f"closed before [DONE] ({'no response' if st.status is None else 'mid-stream'})"
+                 + (f": {st.lost}" if st.lost else ""))
         res["tokens"] += st.n
 
     async def main():
@@ -265,16 +286,22 @@ def main():
                                            "--frontend", furl, "--wid", f"fake-{i}", "--step-ms", str(a.step_ms)],
                                           env=env))
         import urllib.request
-        t_end = time.time() + 60
-        while time.time() < t_end:
+
+        def known() -> int:
+            with urllib.request.urlopen(furl + "/internal/workers", timeout=2) as r:
+                return len(json.loads(r.read())["workers"])
+        # every frontend process must have heard of every worker (the discovery bus forwards a
+        # registration from the process that took it): fresh connections land on the processes at
+        # random (SO_REUSEPORT), so require 8 * procs answers in a row to know them all; a request
+        # reaching a process that does not know the model yet would be answered 404
+        t_end, streak = time.time() + 60, 0
+        while time.time() < t_end and streak < 8 * a.procs:
             try:
-                with urllib.request.urlopen(furl + "/internal/workers", timeout=2) as r:
-                    if len(json.loads(r.read())["workers"]) >= a.workers:
-                        break
+                streak = streak + 1 if known() >= a.workers else 0
             except Exception:  # noqa: BLE001
-                pass
-            time.sleep(0.3)
-        time.sleep(1.5)  # every frontend process has heard of every worker (discovery bus)
+                streak = 0
+            if streak == 0:
+                time.sleep(0.3)
         rate = a.rate or a.tok_per_s / a.osl
         c0 = cpu_seconds(fe.pid)
         t0 = time.time()
@@ -287,7 +314,7 @@ def main():
         wall = time.time() - t0
         c1 = cpu_seconds(fe.pid)
         w_cpu = sum(cpu_seconds(p.pid) for p in procs[1:])
-        ttft, gaps, done, dropped, toks, spans, per_s = [], [], 0, 0, 0, [], {}
+        ttft, gaps, done, dropped, toks, spans, per_s, reasons = [], [], 0, 0, 0, [], {}, {}
         c_cpu = 0.0
         for i in range(a.clients):
             r = json.load(open(os.path.join(tmp, f"c{i}.json")))
@@ -298,6 +325,8 @@ def main():
             toks += r["tokens"]
             spans.append(r["t1"] - r["t0"])
             c_cpu += r.get("cpu_s", 0.0)
+            for why, k in r.get("drop_reasons", {}).items():
+                reasons[why] = reasons.get(why, 0) + k
             for sec, k in r["per_s"].items():
                 per_s[int(sec)] = per_s.get(int(sec), 0) + k
         # steady state: after one request lifetime (osl x step) of ramp-up, until arrivals stop
@@ -306,7 +335,8 @@ def main():
         res = {"target_tok_per_s": a.tok_per_s,
                "delivered_tok_per_s": round(sum(steady) / max(1, len(steady)), 1),
                "steady_window_s": [lo, hi],
-               "requests_done": done, "requests_dropped": dropped, "frontend_procs": a.procs, "workers": a.workers,
+               "requests_done": done, "requests_dropped": dropped, "drop_reasons": reasons,
+               "frontend_procs": a.procs, "workers": a.workers,
                "client_procs": a.clients, "osl": a.osl, "step_ms": a.step_ms,
                "ttft_ms_p50": round(1e3 * _pct(ttft, 0.5), 2), "ttft_ms_p90": round(1e3 * _pct(ttft, 0.9), 2),
                "chunk_gap_ms_p50": round(1e3 * _pct(gaps, 0.5), 2), "chunk_gap_ms_p90": round(1e3 * _pct(gaps, 0.9), 2),

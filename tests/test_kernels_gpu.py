@@ -814,7 +814,7 @@ def test_gemm_big(gpu, M, N, K):
     x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
     w = ((torch.rand(N, K, device=gpu) * 2 - 1) * K ** -0.5).to(torch.bfloat16)
     w[:, 0] += torch.arange(N, device=gpu, dtype=torch.bfloat16) * 1e-3
-    for variant in (0, 1, 2):
+    for variant in (0, 1, 2, 6):
         out = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
         assert ops.ext().gemm_big(out, x, w, 0, variant)
         _close(out, x.float() @ w.float().t(), atol=2e-2, rtol=2e-2, name=f"gemm_big v{variant} {M}x{N}x{K}")
@@ -828,7 +828,7 @@ def test_gemm_big_swiglu(gpu, M, I, K):
     w = ((torch.rand(2 * I, K, device=gpu) * 2 - 1) * 2 * K ** -0.5).to(torch.bfloat16)
     gu = x.float() @ w.float().t()
     want = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
-    for variant in (0, 1, 2):
+    for variant in (0, 1, 2, 6):
         out = torch.full((M, I), float("nan"), device=gpu, dtype=torch.bfloat16)
         assert ops.ext().gemm_big(out, x, w, 1, variant)
         _close(out, want, atol=2e-2, rtol=2e-2, name=f"gemm_big v{variant} swiglu {M}x{I}x{K}")
