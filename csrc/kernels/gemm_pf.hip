@@ -1,0 +1,485 @@
+// K05-K08 at prefill chunks (M = 1k-16k tokens): Y[M, N] = X[M, K] . W[N, K]^T on MFMA, with the
+// projection's elementwise tail fused into the epilogue.  Replaces hipBLASLt (+ the separate SiLU*mul
+// pass) on the prefill path.
+//
+// Tile: 256 weight rows (n) x 256 tokens (m) x 64 (k) per 512-thread workgroup, one workgroup per CU.
+//   * 8 waves as 2 (token halves) x 4 (64-row weight blocks); a wave owns acc[4 w-frags][8 token
+//     frags] of v_mfma_f32_16x16x32_bf16 with A = W (output columns on the accumulator rows) and
+//     B = X^T, so a lane holds Y[token][4 consecutive columns];
+//   * ping-pong: waves 4-7 run one barrier behind waves 0-3 (waves w and w + 4 share a SIMD), so on
+//     every SIMD one wave's 32-MFMA segment runs beside its partner's LDS-read / DMA-issue segment
+//     (cdna_hip_programming.md §5 "256² 8-phase template", MI355X_MICROARCH.md "Two waves per
+//     SIMD").  A k-tile is two phases (token half 0, token half 1) of 32 MFMAs; fragment reads per
+//     phase: 8 W + 8 X / 8 X ds_read_b128;
+//   * operands go HBM/L2 -> LDS by global_load_lds_dwordx4 (lane-linear 1 KB pieces, no VGPRs):
+//     2 k-tile buffers of W half-tiles (128 rows, 16 KB) and X quarter-tiles (64 tokens, 8 KB); the
+//     16-byte chunks of a 128-byte row are XOR-swizzled by (row >> 1) & 7 on the SOURCE address and
+//     un-swizzled on the read, conflict-free for the ds_read_b128 lane groups (T2, rule 21);
+//     k-tile s + 1's W and X(., 0) are issued at phase 1 of s - 1 (their regions were last read at
+//     phase 0 of s - 1), its X(., 1) at phase 0 of s; the one vmcnt wait is at the end of phase 1's
+//     load segment (counted: the pieces issued for s + 2 stay in flight);
+//   * persistent stream-K (hybrid data-parallel + stream-K): the grid is at most one workgroup per
+//     CU; full rounds of tiles run data-parallel, the last one-to-two rounds' k-iterations are split
+//     evenly over the workgroups.  Every workgroup runs ONE continuous k-tile pipeline over its
+//     positions (a new tile's first k-tiles are already in LDS when the previous tile's epilogue
+//     runs).  A tile split over workgroups is finished by the one that arrives last: every segment
+//     publishes an fp32 slab (write-through sc1 stores, then a ticket), the last arriver reads the
+//     slabs with sc1 loads, sums them in segment order (deterministic) and runs the epilogue (§5
+//     "Projection GEMM at M = 256" item 2, sc1 form);
+//   * tiles are visited XCD-aware: the 32 workgroups of an XCD take 32 consecutive tiles of a round
+//     in the host-built tile map's order (8 token tiles per weight-column sweep), so they share W and
+//     X panels in their L2.
+//
+// EPI_NONE: Y = acc.  EPI_SWIGLU: W = [gate; up] [2 I, K]; a tile's image interleaves 16 gate and the
+// 16 matching up rows per fragment pair (the DMA addresses gather them), Y [M, I] = SiLU(g) * u.
+#include <algorithm>
+#include <type_traits>
+
+#include "common.h"
+
+namespace mxs {
+
+typedef __bf16 pf_bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int pf_u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int PF_SC1 = 16;  // buffer cache-policy bits: sc1 (CPol::SC1 = SCC): write-through / L2-coherent
+constexpr int PF_EPI_NONE = 0;
+constexpr int PF_EPI_SWIGLU = 1;
+
+__device__ __forceinline__ pf_bf16x8 pf_frag(const pf_u32x4& v) { return __builtin_bit_cast(pf_bf16x8, v); }
+__device__ __forceinline__ float pf_silu(float g) { return g / (1.f + __expf(-g)); }
+
+struct PfArgs {
+  bf16_t* Y;
+  const bf16_t* X;
+  const bf16_t* W;
+  float* slab;  // stream-K partials: [2 * grid][8 * 4 * 8 (frag pairs)][512 threads][4] fp32
+  int* cnt;     // per stream-K tile arrival counters (zero between launches)
+  const int* tile_map;  // logical tile -> token tile | weight tile << 16 (pf_tile_map)
+  int M, K, ldx, ldy, inter, ntm, ntn, nk;
+  int nrows_w;  // rows of W
+  int dp_rounds;  // full data-parallel rounds of tiles
+  int sk_tiles;   // tiles after them, split over the grid by k-iterations
+};
+
+// a segment of a workgroup's k-tile stream: k-tiles [k0, k1) of logical tile L (token tile tm,
+// weight tile tn), starting at stream position c
+struct PfSeg {
+  int c, L, k0, k1, tm, tn;
+};
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
+  constexpr int HT = 16384, QT = 8192, KT = 4 * HT, XB = 2 * HT;  // W halves at 0 / HT, X halves at XB
+  __shared__ __attribute__((aligned(16))) char smem[2 * KT + 16];
+  int* flag = reinterpret_cast<int*>(smem + 2 * KT);
+
+  const int G = gridDim.x, nk = a.nk;
+  // order of this workgroup: blocks b and b + 8 share an XCD; give each XCD a contiguous range
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+  const int o = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int I = a.sk_tiles * nk;  // stream-K iterations (< 2 * grid * nk: fits 32 bits with o * I)
+  const int sk_lo = o * I / G, sk_hi = (o + 1) * I / G;
+  const int dp_end = a.dp_rounds * nk;
+  const int ns = dp_end + sk_hi - sk_lo;  // positions of this workgroup's stream
+
+  // the segment starting at stream position c (c < ns): a data-parallel round's whole tile, or a
+  // stream-K piece; its tile coordinates come from the host-built map (one scalar load per segment)
+  auto make_seg = [&](int c) -> PfSeg {
+    PfSeg g;
+    g.c = c;
+    if (c < dp_end) {
+      g.L = (c / nk) * G + o;
+      g.k0 = 0;
+      g.k1 = nk;
+    } else {
+      const int i = sk_lo + c - dp_end;
+      g.L = a.dp_rounds * G + i / nk;
+      g.k0 = i % nk;
+      g.k1 = min(nk, g.k0 + sk_hi - i);
+    }
+    const int v = __builtin_amdgcn_readfirstlane(a.tile_map[g.L]);
+    g.tm = v & 0xFFFF;
+    g.tn = v >> 16;
+    return g;
+  };
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+
+  // DMA sources: buffer descriptors per tile (scalar), per-lane byte offsets (VGPR, fixed), the
+  // k-tile in the scalar offset: no address arithmetic on the VALU in the loop.  X rows past M fall
+  // outside the tile's descriptor and load as zeros (never stored).
+  int wvo[2][2];  // W half h, instruction j
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * (2 * wid + j) + (lane >> 3);
+    const int ch = 8 * ((lane & 7) ^ ((row >> 1) & 7));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = 128 * h + row;
+      int wr_l;
+      if constexpr (EPI == PF_EPI_SWIGLU) {
+        const int fr = (r >> 4) & 3;
+        wr_l = (fr < 2 ? 0 : a.inter) + 32 * (r >> 6) + 16 * (fr & 1) + (r & 15);
+      } else {
+        wr_l = r;
+      }
+      wvo[h][j] = (wr_l * a.K + ch) * 2;
+    }
+  }
+  int xvo[2][2];  // X quarter (h, t)
+  {
+    const int rq = 8 * wid + (lane >> 3);
+    const int ch = 8 * ((lane & 7) ^ ((rq >> 1) & 7));
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) xvo[h][t] = ((128 * h + 64 * t + rq) * a.ldx + ch) * 2;
+  }
+  constexpr int WSTEP = EPI == PF_EPI_SWIGLU ? 128 : 256;  // weight rows per tile step
+  const long w_bytes = 2L * a.K * a.nrows_w;
+
+  typedef __attribute__((address_space(3))) void lds_t;
+  auto rsrc_w = [&](int tn) -> __amdgpu_buffer_rsrc_t {  // W rows of weight tile tn
+    const long off = 2L * tn * WSTEP * a.K;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.W) + off / 2, static_cast<short>(0),
+                                             static_cast<int>(min(w_bytes - off, 0x7FFFFFFFL)), 0x00020000);
+  };
+  auto rsrc_x = [&](int tm) -> __amdgpu_buffer_rsrc_t {  // X rows of token tile tm (rows past M: out of range)
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.X) + static_cast<size_t>(tm) * 256 * a.ldx,
+                                             static_cast<short>(0), (a.M - tm * 256) * a.ldx * 2, 0x00020000);
+  };
+  auto dma_w = [&](int pos, __amdgpu_buffer_rsrc_t rs, int k) {  // both W half-tiles of position pos
+    char* dst = smem + (pos & 1) * KT;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(dst + h * HT + (2 * wid + j) * 1024), 16, wvo[h][j],
+                                                 128 * k, 0, 0);
+  };
+  auto dma_x = [&](int pos, __amdgpu_buffer_rsrc_t rs, int k, int t) {  // X quarters (0, t), (1, t) of pos
+    char* dst = smem + (pos & 1) * KT + XB + t * QT;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(dst + h * HT + wid * 1024), 16, xvo[h][t], 128 * k, 0,
+                                               0);
+  };
+
+  float4_ acc[4][8];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[f][t] = float4_{0.f, 0.f, 0.f, 0.f};
+
+  const int r16 = lane & 15, kq = lane >> 4;
+  int woff[4], xoff[8];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) woff[f] = (wc >> 1) * HT + (64 * (wc & 1) + 16 * f + r16) * 128;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) xoff[t] = XB + wr * HT + (16 * t + r16) * 128;
+  const int swz = (r16 >> 1) & 7;
+  const int sl0 = (kq ^ swz) << 4, sl1 = ((4 + kq) ^ swz) << 4;
+
+  pf_u32x4 wa[4][2], xb[4][2];  // [w frag][k-step], [token frag][k-step]
+  auto rd_w = [&](const char* b) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      wa[f][0] = *reinterpret_cast<const pf_u32x4*>(b + woff[f] + sl0);
+      wa[f][1] = *reinterpret_cast<const pf_u32x4*>(b + woff[f] + sl1);
+    }
+  };
+  auto rd_x = [&](const char* b, int hb) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      xb[t][0] = *reinterpret_cast<const pf_u32x4*>(b + xoff[4 * hb + t] + sl0);
+      xb[t][1] = *reinterpret_cast<const pf_u32x4*>(b + xoff[4 * hb + t] + sl1);
+    }
+  };
+  auto mma = [&](int hb) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[f][4 * hb + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf_frag(wa[f][kk]), pf_frag(xb[t][kk]),
+                                                                        acc[f][4 * hb + t], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // epilogue of a finished tile from acc: lane (r16, kq), acc[f][t] = Y[token m0 + 128 wr + 16 t +
+  // r16][image column 64 wc + 16 f + 4 kq + e]
+  auto epilogue = [&](int tm, int tn) {
+    const int m0 = tm * 256;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int m = m0 + 128 * wr + 16 * t + r16;
+      if (m >= a.M) continue;
+      bf16_t* yr = a.Y + static_cast<size_t>(m) * a.ldy;
+      if constexpr (EPI == PF_EPI_SWIGLU) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const float4_& g = acc[p][t];
+          const float4_& v = acc[p + 2][t];
+          const int n = tn * 128 + 32 * wc + 16 * p + 4 * kq;
+          uint2 ov;
+          ov.x = pack2(pf_silu(g[0]) * v[0], pf_silu(g[1]) * v[1]);
+          ov.y = pack2(pf_silu(g[2]) * v[2], pf_silu(g[3]) * v[3]);
+          *reinterpret_cast<uint2*>(yr + n) = ov;
+        }
+      } else {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const float4_& v = acc[f][t];
+          const int n = tn * 256 + 64 * wc + 16 * f + 4 * kq;
+          uint2 ov;
+          ov.x = pack2(v[0], v[1]);
+          ov.y = pack2(v[2], v[3]);
+          *reinterpret_cast<uint2*>(yr + n) = ov;
+        }
+      }
+    }
+  };
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[f][t] = float4_{0.f, 0.f, 0.f, 0.f};
+  };
+  // stream-K bookkeeping: first SK iteration of order q, owner of SK iteration i
+  auto sk_start = [&](int q) -> int { return q * I / G; };
+  auto sk_owner = [&](int i) -> int { return ((i + 1) * G + I - 1) / I - 1; };
+  constexpr int SLAB = 32 * 512 * 4;  // floats per segment slab
+
+#define PF_BAR()                           \
+  do {                                     \
+    __builtin_amdgcn_sched_barrier(0);     \
+    __builtin_amdgcn_s_barrier();          \
+    __builtin_amdgcn_sched_barrier(0);     \
+  } while (0)
+#define PF_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+  if (ns <= 0) return;  // every wave of the workgroup leaves together: no barrier is pending
+
+  PfSeg seg = make_seg(0);
+  PfSeg nseg = seg.k1 - seg.k0 < ns ? make_seg(seg.k1 - seg.k0) : seg;  // valid iff nseg.c > seg.c
+  // k-tile of the position d ahead of k when it lies past the current segment: (tm, tn, k)
+  auto ahead = [&](int k, int d, int& tm, int& tn, int& kk) {
+    const int e = k + d - seg.k1, nl = nseg.k1 - nseg.k0;
+    if (e < nl) {
+      tm = nseg.tm;
+      tn = nseg.tn;
+      kk = nseg.k0 + e;
+      return;
+    }
+    const PfSeg n2 = make_seg(nseg.c + nl);  // rare: a one-k-tile segment in between
+    tm = n2.tm;
+    tn = n2.tn;
+    kk = n2.k0 + e - nl;
+  };
+  __amdgpu_buffer_rsrc_t rw = rsrc_w(seg.tn), rx = rsrc_x(seg.tm);  // the current segment's operands
+
+  dma_w(0, rw, seg.k0);
+  dma_x(0, rx, seg.k0, 0);
+  dma_x(0, rx, seg.k0, 1);
+  if (ns > 1) {
+    if (seg.k0 + 1 < seg.k1) {
+      dma_w(1, rw, seg.k0 + 1);
+      dma_x(1, rx, seg.k0 + 1, 0);
+    } else {
+      int tm1, tn1, k1;
+      ahead(seg.k0, 1, tm1, tn1, k1);
+      dma_w(1, rsrc_w(tn1), k1);
+      dma_x(1, rsrc_x(tm1), k1, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  PF_BAR();
+  if (wr == 1) PF_BAR();  // the stagger
+
+  // one stream position: the k-tile in buffer s & 1 (two phases), and the DMA of positions s + 1 and
+  // s + 2.  FAST: both lie in the current segment (the common case: no segment arithmetic)
+  auto position = [&](auto fast, int s, int k) {
+    constexpr bool FAST = decltype(fast)::value;
+    const char* b = smem + (s & 1) * KT;
+    // phase 0: token half 0; X(., 1) of position s + 1 (its region was last read at phase 1 of s - 1)
+    if (FAST) {
+      dma_x(s + 1, rx, k + 1, 1);
+    } else if (s + 1 < ns) {
+      if (k + 1 < seg.k1) {
+        dma_x(s + 1, rx, k + 1, 1);
+      } else {
+        int tm1, tn1, k1;
+        ahead(k, 1, tm1, tn1, k1);
+        dma_x(s + 1, rsrc_x(tm1), k1, 1);
+      }
+    }
+    rd_w(b);
+    rd_x(b, 0);
+    PF_LGKM0();
+    PF_BAR();
+    mma(0);
+    PF_BAR();
+    // phase 1: token half 1; W and X(., 0) of position s + 2 into buffer s & 1 (last read at phase 0,
+    // retired by the lgkmcnt + barrier above); position s + 1 complete
+    rd_x(b, 1);
+    if (FAST || s + 2 < ns) {
+      if (FAST || k + 2 < seg.k1) {
+        dma_w(s, rw, k + 2);
+        dma_x(s, rx, k + 2, 0);
+      } else {
+        int tm2, tn2, k2;
+        ahead(k, 2, tm2, tn2, k2);
+        dma_w(s, rsrc_w(tn2), k2);
+        dma_x(s, rsrc_x(tm2), k2, 0);
+      }
+      // the 6 pieces just issued for s + 2 stay in flight: waiting here, after this segment's issue
+      // work, gives the youngest piece of s + 1 (issued at phase 0) the whole segment to land
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    PF_LGKM0();
+    PF_BAR();
+    mma(1);
+    PF_BAR();
+  };
+
+  int s = 0;  // stream position (k-tile buffer parity)
+  for (;;) {
+    int k = seg.k0;
+    for (; k + 2 < seg.k1; ++k, ++s) position(std::integral_constant<bool, true>(), s, k);
+    for (; k < seg.k1; ++k, ++s) position(std::integral_constant<bool, false>(), s, k);
+
+    // end of a segment
+    bool write = seg.k0 == 0 && seg.k1 == nk;  // the whole tile
+    if (!write) {  // a stream-K segment: publish, and finish the tile if this workgroup arrives last
+      if (wr == 0) PF_BAR();  // un-stagger: both halves meet here
+      const int l = seg.L - a.dp_rounds * G;  // stream-K tile
+      const int t0 = l * nk;
+      const int o_lo = sk_owner(t0), o_hi = sk_owner(t0 + nk - 1);
+      const int my_slot = 2 * o + (sk_start(o) >= t0 ? 0 : 1);
+      // slab stores / loads through a buffer descriptor: one VGPR offset (tid * 16), the fragment
+      // offset in the scalar field (64-bit addresses per store would not fit the VGPR budget)
+      const __amdgpu_buffer_rsrc_t ms = __builtin_amdgcn_make_buffer_rsrc(
+          a.slab + static_cast<size_t>(my_slot) * SLAB, static_cast<short>(0), SLAB * 4, 0x00020000);
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pf_u32x4, acc[f][t]), ms, tid * 16,
+                                                 (f * 8 + t) * 8192, PF_SC1);
+      // hand-off without agent-scope fences (MI355X_MICROARCH.md "Valid forms", first table row):
+      // write-through (sc1) 16-byte slab stores, every storing wave drained before the barrier, one
+      // lane's agent-scope ticket; the last arriver reads every slab with sc1 loads.  A release fence
+      // here would write back the XCD L2's dirty lines (the other tiles' outputs) on every segment.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      PF_BAR();  // every wave's slab stores are complete
+      if (tid == 0) {
+        const int ticket = __hip_atomic_fetch_add(a.cnt + l, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = ticket == o_hi - o_lo;
+        if (last) a.cnt[l] = 0;  // re-armed for the next launch
+        flag[0] = last;
+      }
+      PF_LGKM0();
+      PF_BAR();
+      write = flag[0] != 0;
+      PF_BAR();  // flag read by every wave before it is written again
+      if (write) {
+        zero_acc();
+        for (int q = o_lo; q <= o_hi; ++q) {  // segment order: the sum does not depend on arrival
+          const int slot = 2 * q + (sk_start(q) >= t0 ? 0 : 1);
+          const __amdgpu_buffer_rsrc_t ss = __builtin_amdgcn_make_buffer_rsrc(
+              a.slab + static_cast<size_t>(slot) * SLAB, static_cast<short>(0), SLAB * 4, 0x00020000);
+#pragma unroll
+          for (int f = 0; f < 4; ++f) {  // 8 loads in flight at a time (VGPR budget)
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+              acc[f][t] += __builtin_bit_cast(float4_, __builtin_amdgcn_raw_buffer_load_b128(
+                                                           ss, tid * 16, (f * 8 + t) * 8192, PF_SC1));
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      if (wr == 1) PF_BAR();  // re-stagger
+    }
+    if (write) epilogue(seg.tm, seg.tn);
+    zero_acc();
+    if (nseg.c <= seg.c) break;  // the stream ends
+    seg = nseg;
+    rw = rsrc_w(seg.tn);
+    rx = rsrc_x(seg.tm);
+    const int nc = seg.c + seg.k1 - seg.k0;
+    if (nc < ns) nseg = make_seg(nc);
+    else nseg.c = -1;  // no further segment
+  }
+  if (wr == 0) PF_BAR();  // balance the stagger barrier
+#undef PF_BAR
+#undef PF_LGKM0
+}
+
+// Launch geometry: grid = min(CUs, work / min_iters) workgroups; full rounds of tiles data-parallel,
+// the rest stream-K.  Returns the grid (0 = not launched: shape unsupported).
+int pf_plan(int M, int N, int K, int epi, int num_cu, int min_iters, int* dp_rounds, int* sk_tiles, int* grid) {
+  if (M <= 0 || K % 64 != 0 || N % 256 != 0) return 0;
+  const int ntm = (M + 255) / 256, ntn = epi == PF_EPI_SWIGLU ? N / 256 : N / 256;
+  const int T = ntm * ntn, nk = K / 64;
+  const long work = static_cast<long>(T) * nk;
+  int G = static_cast<int>(std::min<long>(num_cu, std::max<long>(1, work / std::max(1, min_iters))));
+  if (T % G == 0) {  // whole rounds: no stream-K
+    *dp_rounds = T / G;
+    *sk_tiles = 0;
+  } else {
+    const int R = T / G;
+    *dp_rounds = R > 0 ? R - 1 : 0;
+    *sk_tiles = T - *dp_rounds * G;
+  }
+  *grid = G;
+  return G;
+}
+
+// epi 0: Y [M, N] = X W^T (N % 256 == 0).  epi 1 (SwiGLU): W = [gate; up] rows [2 I, K], Y [M, I]
+// (I % 128 == 0).  K % 64 == 0, 16-byte aligned rows.  slab: >= 2 * grid * 32 * 512 * 4 floats; cnt:
+// >= sk_tiles ints, zero (left zero by every launch).  False when the shape is not supported.
+bool launch_gemm_pf(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx, int ldy, int epi,
+                    float* slab, long slab_floats, int* cnt, int cnt_len, const int* tile_map, int map_len,
+                    int num_cu, int min_iters, hipStream_t s) {
+  if (M <= 0 || K % 64 != 0 || ldx % 8 != 0 || ldy % 4 != 0 || (epi != PF_EPI_NONE && epi != PF_EPI_SWIGLU)) return false;
+  if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W)) & 15) return false;
+  if (reinterpret_cast<uintptr_t>(Y) & 7) return false;
+  if (N % 256 != 0) return false;  // SwiGLU: N = 2 I with I % 128 == 0
+  int dp, sk, G;
+  if (!pf_plan(M, N, K, epi, num_cu, min_iters, &dp, &sk, &G)) return false;
+  if (sk > 0 && (slab == nullptr || cnt == nullptr || cnt_len < sk || slab_floats < 2L * G * 32 * 512 * 4)) return false;
+  if (tile_map == nullptr || map_len < ((M + 255) / 256) * (N / 256)) return false;
+  if (static_cast<long>(M) * ldx * 2 > 0x7FFFFFFFL) return false;  // X rows addressed by 32-bit buffer offsets
+  PfArgs a;
+  a.Y = Y;
+  a.X = X;
+  a.W = W;
+  a.slab = slab;
+  a.cnt = cnt;
+  a.tile_map = tile_map;
+  a.nrows_w = N;
+  a.M = M;
+  a.K = K;
+  a.ldx = ldx;
+  a.ldy = ldy;
+  a.inter = epi == PF_EPI_SWIGLU ? N / 2 : 0;
+  a.ntm = (M + 255) / 256;
+  a.ntn = N / 256;
+  a.nk = K / 64;
+  a.dp_rounds = dp;
+  a.sk_tiles = sk;
+  if (epi == PF_EPI_SWIGLU) hipLaunchKernelGGL(gemm_pf_kernel<PF_EPI_SWIGLU>, dim3(G), dim3(512), 0, s, a);
+  else hipLaunchKernelGGL(gemm_pf_kernel<PF_EPI_NONE>, dim3(G), dim3(512), 0, s, a);
+  MXS_CHECK_LAUNCH();
+  return true;
+}
+
+}  // namespace mxs

@@ -566,6 +566,11 @@ class ModelRunner:
             from ..ops import mplan
             self.mplan_report = mplan.tune({k: v[0] for k, v in shapes.items() if k != "lm_head"},
                                            self.args.max_num_batched_tokens + self.args.max_num_seqs, self.device)
+            # prefill projections: the stream-K MFMA kernel (SwiGLU fused for gate_up) vs that path
+            from ..ops import prefill_pf
+            pf_w = {k: (v[0], v[1]) for k, v in shapes.items() if k != "lm_head"}
+            self.prefill_pf_report = prefill_pf.tune(pf_w, self.args.max_num_batched_tokens + self.args.max_num_seqs,
+                                                     self.device, self.dtype)
             if self.cfg.is_moe and "l0.w13" in w:  # expert GEMMs at decode batches (local experts)
                 from ..ops import moe as moe_ops
                 self.moe_gemm_report = moe_ops.tune(w["l0.w13"], w["l0.w2"], buckets, self.cfg.num_experts_per_tok,

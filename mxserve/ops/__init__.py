@@ -102,7 +102,16 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
                 out = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
                 if decode_gemm.TABLE.run(out, x, w, cfg, 0):
                     return out
-        if M > 256:  # small prefill chunks: the 64/128-row tile kernel where it was measured faster
+        if M > 256:
+            # prefill chunks: the persistent stream-K MFMA kernel where the start-up tuner measured it
+            # faster (ops/prefill_pf.py)
+            from .prefill_pf import TABLE as PF_TABLE
+            mi = PF_TABLE.lookup(M, w.shape[0], w.shape[1], 0)
+            if mi is not None:
+                out = gemm_pf(x, w, 0, None, mi)
+                if out is not None:
+                    return out
+            # small prefill chunks: the 64/128-row tile kernel where it was measured faster
             from .decode_gemm import PREFILL_TABLE
             cfg = PREFILL_TABLE.lookup(M, w.shape[0], w.shape[1])
             if cfg is not None:
@@ -202,9 +211,69 @@ def prefill_gemm(out: torch.Tensor, x: torch.Tensor, w: torch.Tensor, cfg: tuple
     return bool(ext().prefill_gemm(out, x, w, part, bm, sk))
 
 
+# ----------------------------------------------------------------------------- prefill GEMM (gemm_pf.hip)
+_PF_WS: dict = {}
+
+
+def _pf_workspace(device) -> tuple:
+    """(fp32 stream-K slabs, int32 tile counters, CU count) of a device; the counters start zero and
+    every launch leaves them zero."""
+    ws = _PF_WS.get(device)
+    if ws is None:
+        ncu = torch.cuda.get_device_properties(device).multi_processor_count
+        slab = torch.empty(2 * ncu * 32 * 512 * 4, dtype=torch.float32, device=device)
+        cnt = torch.zeros(1 << 16, dtype=torch.int32, device=device)
+        ws = _PF_WS[device] = (slab, cnt, ncu)
+    return ws
+
+
+_PF_MAPS: dict = {}
+
+
+def pf_tile_map(ntm: int, ntn: int, device, gm: int = 8) -> torch.Tensor:
+    """Logical tile -> token tile | weight tile << 16 for gemm_pf: GM token tiles per weight-column
+    sweep, so the 32 consecutive tiles an XCD runs together share W and X panels (cached)."""
+    key = (ntm, ntn, gm, str(device))
+    t = _PF_MAPS.get(key)
+    if t is None:
+        L = torch.arange(ntm * ntn, dtype=torch.int64)
+        per = gm * ntn
+        grp = L // per
+        first = grp * gm
+        gsz = torch.clamp(ntm - first, max=gm)
+        ing = L - grp * per
+        tm, tn = first + ing % gsz, ing // gsz
+        t = _PF_MAPS[key] = (tm | (tn << 16)).to(torch.int32).to(device)
+    return t
+
+
+def gemm_pf(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None,
+            min_iters: int = 16) -> Optional[torch.Tensor]:
+    """Prefill GEMM on the hand-written persistent stream-K kernel: epi 0 x @ w.T, epi 1 SiLU(x @
+    gate.T) * (x @ up.T) with w = [gate; up].  None when the shape is not supported."""
+    M, N = x.shape[0], w.shape[0]
+    if N % 256:
+        return None
+    if out is None:
+        out = torch.empty(M, N // 2 if epi == 1 else N, dtype=x.dtype, device=x.device)
+    slab, cnt, ncu = _pf_workspace(x.device)
+    tmap = pf_tile_map(-(-M // 256), N // 256, x.device)
+    if not ext().gemm_pf(out, x, w, epi, slab, cnt, tmap, ncu, min_iters):
+        return None
+    return out
+
+
 def gate_up_silu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """silu(x @ gate.T) * (x @ up.T) with w = [gate; up] (K07 + K10).  Decode-sized: one MFMA kernel
-    with SiLU*mul in its epilogue when tuned faster; otherwise hipBLASLt + the SiLU*mul kernel."""
+    with SiLU*mul in its epilogue when tuned faster; prefill-sized: the stream-K kernel with the same
+    epilogue (ops/prefill_pf.py); otherwise hipBLASLt + the SiLU*mul kernel."""
+    if _gpu(x) and x.dim() == 2 and x.shape[0] > _decode_max_m():
+        from .prefill_pf import TABLE as PF_TABLE
+        mi = PF_TABLE.lookup(x.shape[0], w.shape[0], w.shape[1], 1)
+        if mi is not None:
+            out = gemm_pf(x, w, 1, None, mi)
+            if out is not None:
+                return out
     if _gpu(x) and x.dim() == 2 and x.shape[0] <= _decode_max_m():
         from .decode_gemm import TABLE
         cfg = TABLE.lookup(x.shape[0], w.shape[0], w.shape[1], 1)

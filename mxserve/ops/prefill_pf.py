@@ -1,0 +1,131 @@
+"""Routing of prefill-sized projection GEMMs (M > 256 rows) to the hand-written persistent stream-K
+kernel (csrc/kernels/gemm_pf.hip, ops.gemm_pf) instead of hipBLASLt (+ the separate SiLU*mul pass
+after gate_up).
+
+A start-up tuner (run with the decode-GEMM tuning at graph capture, model_runner._capture_graphs)
+times, per projection and row bucket, gemm_pf at a few minimum stream-K segment lengths against the
+path it replaces (ops.linear's hipBLASLt / M-plan route; for gate_up the GEMM plus ops.silu_mul) and
+keeps gemm_pf where it is faster.  Choices persist in mxserve/ops/tuned/prefill_pf_<arch>_<cus>cu.json
+like the other tables (ops/tuned.py), so every start-up on the same hardware runs the same kernels.
+
+MXS_GEMM_PF=auto (default: the tuned table) | on (gemm_pf for every supported shape, min_iters 16;
+tests, probes) | off (never).
+"""
+from __future__ import annotations
+
+import bisect
+import os
+from typing import Optional
+
+import torch
+
+MODE = os.environ.get("MXS_GEMM_PF", "auto")
+MIN_ITERS = (8, 16, 32)
+WIN_MARGIN = 0.98  # gemm_pf must be this much faster than the path it replaces
+ROUNDS = 3
+
+
+def buckets_for(max_rows: int) -> list:
+    """Row buckets up to max_rows (a step's largest token count): 512-row steps to 4 k, then 1 k."""
+    out, m = [], 512
+    while m < max_rows:
+        out.append(m)
+        m += 512 if m < 4096 else 1024
+    out.append(max(max_rows, 512))
+    return sorted(set(out))
+
+
+class PfTable:
+    """(N, K, epi) -> sorted [(M bucket, min_iters | None)]; a row count takes its bucket (the
+    smallest bucket >= M; past the last, the last)."""
+
+    def __init__(self):
+        self.entries: dict = {}
+        self.report: list = []
+
+    def lookup(self, M: int, N: int, K: int, epi: int) -> Optional[int]:
+        if MODE == "off" or M <= 256 or N % 256 or K % 64:
+            return None
+        if MODE == "on":
+            return 16
+        ent = self.entries.get((N, K, epi))
+        if not ent:
+            return None
+        i = bisect.bisect_left(ent, (M,))
+        return ent[min(i, len(ent) - 1)][1]
+
+
+TABLE = PfTable()
+
+
+def _time(fn, iters: int = 8) -> float:
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
+def tune(weights: dict, max_rows: int, device, dtype=torch.bfloat16) -> list:
+    """weights: {name: (w [N, K], epi)} (epi 1: gate_up with SiLU*mul).  Fills TABLE; returns report
+    rows.  Stored choices are re-checked for correctness, not re-timed."""
+    if MODE != "auto":
+        return []
+    from .. import ops
+    from .tuned import TunedStore, device_tag, median
+    store = TunedStore("prefill_pf", device_tag(device))
+    rows = []
+    saved_mode = globals()["MODE"]
+    for name, (w, epi) in weights.items():
+        N, K = w.shape
+        if N % 256 or K % 64:
+            continue
+        ent = []
+        for M in buckets_for(max_rows):
+            key = f"{N}x{K}:{epi}@{M}"
+            x = (torch.randn(M, K, device=device) * 0.5).to(dtype)
+
+            def base():
+                globals()["MODE"] = "off"
+                try:
+                    y = ops.linear(x, w)
+                    return ops.silu_mul(y) if epi == 1 else y
+                finally:
+                    globals()["MODE"] = saved_mode
+            ref = base()
+            out = torch.empty(M, N // 2 if epi == 1 else N, dtype=dtype, device=device)
+            st = store.get(key)
+            if st is not None:
+                best, best_t, t_base, source = st.get("cfg"), st.get("us"), st.get("base_us"), "table"
+            else:
+                source = "measured"
+                tb, tc = [], {mi: [] for mi in MIN_ITERS}
+                for _ in range(ROUNDS):
+                    tb.append(_time(base))
+                    for mi in MIN_ITERS:
+                        tc[mi].append(_time(lambda: ops.gemm_pf(x, w, epi, out, mi)))
+                t_base = median(tb)
+                best, best_t = None, t_base
+                for mi in MIN_ITERS:
+                    t = median(tc[mi])
+                    if t < t_base * WIN_MARGIN and t < best_t:
+                        best, best_t = mi, t
+            if best is not None:
+                ops.gemm_pf(x, w, epi, out, best)
+                err = (out.float() - ref.float()).abs().max().item()
+                if not err <= 0.02 * max(1.0, ref.float().abs().max().item()):
+                    best, best_t = None, t_base
+            if source == "measured":
+                store.put(key, {"cfg": best, "us": best_t and round(best_t, 2), "base_us": round(t_base, 2)})
+            ent.append((M, best))
+            rows.append({"proj": name, "M": M, "N": N, "K": K, "epi": epi, "base_us": t_base and round(t_base, 2),
+                         "chosen": "hipblaslt" if best is None else f"gemm_pf/{best}",
+                         "us": best_t and round(best_t, 2), "source": source})
+        TABLE.entries[(N, K, epi)] = ent
+    TABLE.report = rows
+    store.save()
+    return rows

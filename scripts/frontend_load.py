@@ -304,6 +304,8 @@ def main():
                 time.sleep(0.3)
         rate = a.rate or a.tok_per_s / a.osl
         c0 = cpu_seconds(fe.pid)
+        import psutil
+        sys0 = psutil.cpu_times()
         t0 = time.time()
         cl = [subprocess.Popen([sys.executable, me, "--role", "client", "--port", str(fe_port), "--rate",
                                 str(rate / a.clients), "--duration", str(a.duration), "--osl", str(a.osl),
@@ -312,6 +314,9 @@ def main():
         for p in cl:
             p.wait(timeout=a.duration + 300)
         wall = time.time() - t0
+        sys1 = psutil.cpu_times()
+        busy = sum(getattr(sys1, f) - getattr(sys0, f) for f in ("user", "nice", "system", "irq", "softirq"))
+        idle = sum(getattr(sys1, f) - getattr(sys0, f) for f in ("idle", "iowait"))
         c1 = cpu_seconds(fe.pid)
         w_cpu = sum(cpu_seconds(p.pid) for p in procs[1:])
         ttft, gaps, done, dropped, toks, spans, per_s, reasons = [], [], 0, 0, 0, [], {}, {}
@@ -343,6 +348,8 @@ def main():
                "frontend_cpu_ms_per_1k_tokens": round(1e6 * (c1 - c0) / max(1, toks), 2),
                "cpu_s": {"frontend": round(c1 - c0, 1), "fake_workers": round(w_cpu, 1), "clients": round(c_cpu, 1)},
                "wall_s": round(wall, 1),
+               # the whole box's CPU use during the run (this test's processes and everything else)
+               "system_cpu_busy": round(busy / max(1e-9, busy + idle), 3),
                "cpus": os.cpu_count()}
         line = json.dumps(res)
         print(line, flush=True)

@@ -43,8 +43,12 @@ def main():
             ref = lib()
             fl = 2 * M * N * K
             row = {"proj": name, "M": M, "N": N, "K": K, "fused_swiglu": swiglu}
-            variants = [int(v) for v in os.environ.get("GB_VARIANTS", "0,1,2").split(",")]
+            variants = [int(v) for v in os.environ.get("GB_VARIANTS", "0,1,2").split(",") if v]
             fns = {"hipblaslt": lib}
+            for mi in [int(v) for v in os.environ.get("GB_PF", "").split(",") if v]:
+                fns[f"pf{mi}"] = (lambda mi=mi: ops.gemm_pf(x, w, 1 if swiglu else 0, y, mi))
+                assert fns[f"pf{mi}"]() is not None
+                row[f"pf{mi}_rel_err"] = round(float((y.float() - ref.float()).abs().max() / ref.float().abs().max()), 5)
             for v in variants:
                 fns[f"v{v}"] = (lambda v=v: ext.gemm_big(y, x, w, 1 if swiglu else 0, v))
                 assert fns[f"v{v}"]()
