@@ -209,36 +209,31 @@ class Guard:
         os._exit(0 if (self.rank != 0 or self.pending is not None) else 3)
 
 
-# Capacity of one MI355X in the disagg roles for the headline workload (Llama-3.2-1B, ISL 4000 / OSL
-# 500, bf16): a prefill GPU running 16384-token steps sustains 127.6 req/s (510k prompt tok/s,
-# steady-state rounds of scripts/prefill_capacity_probe.py, profiles/r3/s3/prefill_capacity); a decode
-# GPU streams every running request's KV each step (~136 MB at a 4.25k context, ~22 us at 6.1 TB/s)
-# and sustains ~38k tok/s at 512 running = ~76 req/s.
-_CAP_PREFILL, _CAP_DECODE, _DISAGG_UTIL = 127.0, 76.0, 0.85
 _PREFILL_STEP_TOKENS = 16384
 
 
 def disagg_plan(a, world: int) -> tuple:
-    """(prefill ranks, decode ranks, arrival rate per GPU) of the disagg phase.  The split maximises
-    the capacity of the tighter role (3 prefill : 5 decode GPUs on 8 for this workload), and the
-    node rate loads the tighter role to 85 %.  Other models: a 1:1 split at --qps x 0.76."""
+    """(prefill ranks, decode ranks, arrival rate per GPU) of the disagg phase.  The role capacities
+    come from the same model the DGDR profiler plans with (mxserve/profiler/capacity.py: the measured
+    MI355X table for this workload, else its roofline); the split maximises the tighter role's
+    capacity (3 prefill : 5 decode GPUs on 8 for the headline workload) and the capacity-derived rate
+    loads that role to 85 %."""
+    from mxserve.profiler import capacity as capm
+    cap = capm.capacity(a.model, a.isl, a.osl)
+    cp, cd = cap["prefill_rps"], cap["decode_rps"]
     p = a.disagg_prefill_ranks
-    headline = a.model == "meta-llama/Llama-3.2-1B-Instruct" and a.isl == 4000 and a.osl == 500
     if p <= 0:
-        # the split whose tighter role carries the most (3P+5D on 8 GPUs, 2P+2D on 4, 1P+1D on 2)
-        p = max(range(1, max(2, world)), key=lambda k: min(k * _CAP_PREFILL, (world - k) * _CAP_DECODE)) \
-            if headline else world // 2
+        p = capm.pd_split(world, cp, cd)[0]
     p = min(max(1, p), world - 1)
     d = world - p
+    full = min(p * cp, d * cd) / world  # per GPU
     qps = a.disagg_qps
-    cap = (_DISAGG_UTIL * min(p * _CAP_PREFILL, d * _CAP_DECODE) / world) if headline else 0.76 * a.qps
     if qps == 0:
         # like-for-like with the agg phase (the same arrival rate per GPU) unless this split cannot
-        # carry it (1P+1D on 2 GPUs has one decode GPU for twice its share): then the capacity rate
-        full = min(p * _CAP_PREFILL, d * _CAP_DECODE) / world if headline else a.qps
-        qps = a.qps if a.qps <= 0.95 * full + 1e-9 else cap
+        # carry it (1P+1D on 2 GPUs has one decode GPU for twice its share): then the planned rate
+        qps = a.qps if a.qps <= 0.95 * full + 1e-9 else capm.PLAN_UTIL * full
     elif qps < 0:  # capacity-derived: the tighter role loaded to 85 %
-        qps = cap
+        qps = capm.PLAN_UTIL * full
     return p, d, qps
 
 
@@ -780,6 +775,12 @@ def phase_agg(a, ctx) -> tuple:
                                "mt_kernel": sum(bool(r["cfg"]) and r["cfg"][0] == "mt" for r in rep),
                                "tune_s": round(getattr(eng.runner, "decode_gemm_tune_s", 0.0), 1),
                                "from_table": sum(r.get("source") == "table" for r in rep)}
+    rep = getattr(eng.runner, "prefill_pf_report", None)
+    if rep:  # start-up choice per (projection, row bucket): stream-K MFMA GEMM vs hipBLASLt
+        info["prefill_gemm"] = {"buckets": len(rep), "gemm_pf": sum(r["chosen"] != "hipblaslt" for r in rep),
+                                "by_proj": {p: sum(r["chosen"] != "hipblaslt" for r in rep if r["proj"] == p)
+                                            for p in sorted({r["proj"] for r in rep})},
+                                "from_table": sum(r.get("source") == "table" for r in rep)}
     la = getattr(eng, "_late", None)
     if la is not None:  # engine/pacing.py: how often the host waited for a late admission, and how long
         info["late_admission"] = {"waits": la.waits, "mean_wait_ms": round(1e3 * la.wait_s / max(1, la.waits), 3),
@@ -956,7 +957,7 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
     if dis is not None:
         line["disagg"] = dis
     line["engine"] = {"kv_blocks": info["kv_blocks"], "preemptions": info["preemptions"], "graphs": info["graphs"]}
-    for k in ("late_admission", "decode_gemm", "chunk_budget", "gc"):
+    for k in ("late_admission", "decode_gemm", "prefill_gemm", "chunk_budget", "gc"):
         if k in info:
             line["engine"][k] = info[k]
     return line

@@ -520,6 +520,200 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(bf16_t* __restrict__ Y,
   }
 }
 
+// Two-phase ping-pong (variant 7): as variant 6, but a k-tile is 2 phases of 32 MFMAs (all 4 weight
+// fragments x one token half), so each load segment (16 / 8 ds_read_b128 + DMA issue) is shorter
+// than the partner's MFMA segment.  DMA granules: W half-tiles (16 KB) and X quarter-tiles (64
+// tokens, 8 KB); k-tile u + 1's W and X(., 0) are issued at phase 1 of u - 1 (their regions were last
+// read at phase 0 of u - 1), its X(., 1) at phase 0 of u; the only vmcnt wait is at phase 1 of u.
+template <int EPI>
+__global__ void __launch_bounds__(512, 1) gemm_pp2_kernel(bf16_t* __restrict__ Y, const bf16_t* __restrict__ X,
+                                                          const bf16_t* __restrict__ W, int M, int K, int ldx,
+                                                          int ldy, int inter, int ntm, int ntn) {
+  constexpr int HT = 16384, QT = 8192, KT = 4 * HT, XB = 2 * HT;  // X region starts at XB
+  __shared__ __attribute__((aligned(16))) char smem[2 * KT];
+
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  constexpr int GM = 8;
+  const int per_group = GM * ntn, grp = wg / per_group, first_m = grp * GM;
+  const int gsz = min(ntm - first_m, GM), in_grp = wg - grp * per_group;
+  const int tm = first_m + in_grp % gsz, tn = in_grp / gsz;
+  const int m0 = tm * 256;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+
+  // DMA sources: W half h, instruction j: half-tile rows 8 (2 wid + j) .. +7; X quarter (h, t):
+  // quarter rows 8 wid .. +7
+  const bf16_t* wsrc[2][2];
+  const bf16_t* xsrc[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 8 * (2 * wid + j) + (lane >> 3);
+    const int gch = (lane & 7) ^ ((row >> 1) & 7);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = 128 * h + row;
+      int wrow;
+      if constexpr (EPI == GB_EPI_SWIGLU) {
+        const int fr = (r >> 4) & 3, feat = tn * 128 + 32 * (r >> 6) + 16 * (fr & 1) + (r & 15);
+        wrow = fr < 2 ? feat : inter + feat;
+      } else {
+        wrow = tn * 256 + r;
+      }
+      wsrc[h][j] = W + static_cast<size_t>(wrow) * K + 8 * gch;
+    }
+  }
+  {
+    const int rq = 8 * wid + (lane >> 3);
+    const int gch = (lane & 7) ^ ((rq >> 1) & 7);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        xsrc[h][t] = X + static_cast<size_t>(min(m0 + 128 * h + 64 * t + rq, M - 1)) * ldx + 8 * gch;
+  }
+  typedef __attribute__((address_space(3))) void lds_t;
+  auto dma_w = [&](int u) {  // both W half-tiles of k-tile u
+    char* dst = smem + (u & 1) * KT;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_global_load_lds(static_cast<const void*>(wsrc[h][j] + 64 * u),
+                                         (lds_t*)(dst + h * HT + (2 * wid + j) * 1024), 16, 0, 0);
+  };
+  auto dma_x = [&](int u, int t) {  // X quarters (0, t) and (1, t) of k-tile u
+    char* dst = smem + (u & 1) * KT + XB + t * QT;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      __builtin_amdgcn_global_load_lds(static_cast<const void*>(xsrc[h][t] + 64 * u),
+                                       (lds_t*)(dst + h * HT + wid * 1024), 16, 0, 0);
+  };
+
+  float4_ acc[4][8];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[f][t] = float4_{0.f, 0.f, 0.f, 0.f};
+
+  const int r16 = lane & 15, kq = lane >> 4;
+  int woff[4], xoff[8];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) woff[f] = (wc >> 1) * HT + (64 * (wc & 1) + 16 * f + r16) * 128;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) xoff[t] = XB + wr * HT + (16 * t + r16) * 128;
+  const int swz = (r16 >> 1) & 7;
+  const int sl0 = (kq ^ swz) << 4, sl1 = ((4 + kq) ^ swz) << 4;
+
+  gb_u32x4 wa[4][2], xb[4][2];  // [w frag][k-step], [token frag][k-step]
+  auto rd_w = [&](const char* b) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      wa[f][0] = *reinterpret_cast<const gb_u32x4*>(b + woff[f] + sl0);
+      wa[f][1] = *reinterpret_cast<const gb_u32x4*>(b + woff[f] + sl1);
+    }
+  };
+  auto rd_x = [&](const char* b, int hb) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      xb[t][0] = *reinterpret_cast<const gb_u32x4*>(b + xoff[4 * hb + t] + sl0);
+      xb[t][1] = *reinterpret_cast<const gb_u32x4*>(b + xoff[4 * hb + t] + sl1);
+    }
+  };
+  auto mma = [&](int hb) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[f][4 * hb + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gb_frag(wa[f][kk]), gb_frag(xb[t][kk]),
+                                                                        acc[f][4 * hb + t], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+#define PP_BAR()                           \
+  do {                                     \
+    __builtin_amdgcn_sched_barrier(0);     \
+    __builtin_amdgcn_s_barrier();          \
+    __builtin_amdgcn_sched_barrier(0);     \
+  } while (0)
+#define PP_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+  const int nk = K / 64;
+  dma_w(0);
+  dma_x(0, 0);
+  dma_x(0, 1);
+  if (nk > 1) {
+    dma_w(1);
+    dma_x(1, 0);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  PP_BAR();
+  if (wr == 1) PP_BAR();
+
+  for (int u = 0; u < nk; ++u) {
+    const char* b = smem + (u & 1) * KT;
+    // phase 0: token half 0; X(., 1) of k-tile u + 1 (its region was last read at phase 1 of u - 1)
+    if (u + 1 < nk) dma_x(u + 1, 1);
+    rd_w(b);
+    rd_x(b, 0);
+    PP_LGKM0();
+    PP_BAR();
+    mma(0);
+    PP_BAR();
+    // phase 1: token half 1; k-tile u + 1 complete; W and X(., 0) of k-tile u + 2 into buffer u & 1
+    // (last read at phase 0, retired by the lgkmcnt + barrier above)
+    if (u + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (u + 2 < nk) {
+        dma_w(u + 2);
+        dma_x(u + 2, 0);
+      }
+    }
+    rd_x(b, 1);
+    PP_LGKM0();
+    PP_BAR();
+    mma(1);
+    PP_BAR();
+  }
+  if (wr == 0) PP_BAR();
+#undef PP_BAR
+#undef PP_LGKM0
+
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int m = m0 + 128 * wr + 16 * t + r16;
+    if (m >= M) continue;
+    bf16_t* yr = Y + static_cast<size_t>(m) * ldy;
+    if constexpr (EPI == GB_EPI_SWIGLU) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const float4_& g = acc[p][t];
+        const float4_& v = acc[p + 2][t];
+        const int n = tn * 128 + 32 * wc + 16 * p + 4 * kq;
+        uint2 o;
+        o.x = pack2(gb_silu(g[0]) * v[0], gb_silu(g[1]) * v[1]);
+        o.y = pack2(gb_silu(g[2]) * v[2], gb_silu(g[3]) * v[3]);
+        *reinterpret_cast<uint2*>(yr + n) = o;
+      }
+    } else {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const float4_& a = acc[f][t];
+        const int n = tn * 256 + 64 * wc + 16 * f + 4 * kq;
+        uint2 o;
+        o.x = pack2(a[0], a[1]);
+        o.y = pack2(a[2], a[3]);
+        *reinterpret_cast<uint2*>(yr + n) = o;
+      }
+    }
+  }
+}
+
 // epi 0: Y [M, N] = X W^T (N % 256 == 0).  epi 1 (SwiGLU): W = [gate; up] rows [2 I, K], Y [M, I] =
 // SiLU(X gate^T) * (X up^T) (I % 128 == 0).  K % 64 == 0, 16-byte aligned rows.  False when the
 // shape is not supported (the caller keeps its other path).
@@ -527,7 +721,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(bf16_t* __restrict__ Y,
 // the MFMA clusters
 bool launch_gemm_big(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx, int ldy, int epi,
                      int variant, hipStream_t s) {
-  if (M <= 0 || K % 64 != 0 || ldx % 8 != 0 || ldy % 4 != 0 || variant < 0 || variant > 6) return false;
+  if (M <= 0 || K % 64 != 0 || ldx % 8 != 0 || ldy % 4 != 0 || variant < 0 || variant > 7) return false;
   if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W)) & 15) return false;
   if (reinterpret_cast<uintptr_t>(Y) & 7) return false;
   if (N % 256 != 0 || (epi != GB_EPI_NONE && epi != GB_EPI_SWIGLU)) return false;  // SwiGLU: N = 2 I, I % 128 == 0
@@ -542,7 +736,8 @@ bool launch_gemm_big(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, 
     else if (variant == 3) MXS_GB((gemm_big_kernel<GB_EPI_SWIGLU, 1>));
     else if (variant == 4) MXS_GB((gemm_big_kernel<GB_EPI_SWIGLU, 2>));
     else if (variant == 5) MXS_GB((gemm_big_kernel<GB_EPI_SWIGLU, 3>));
-    else MXS_GB(gemm_pp_kernel<GB_EPI_SWIGLU>);
+    else if (variant == 6) MXS_GB(gemm_pp_kernel<GB_EPI_SWIGLU>);
+    else MXS_GB(gemm_pp2_kernel<GB_EPI_SWIGLU>);
   } else {
     if (variant == 0) MXS_GB(gemm_big_kernel<GB_EPI_NONE>);
     else if (variant == 1) MXS_GB((gemm_big_ring_kernel<GB_EPI_NONE, false>));
@@ -550,7 +745,8 @@ bool launch_gemm_big(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, 
     else if (variant == 3) MXS_GB((gemm_big_kernel<GB_EPI_NONE, 1>));
     else if (variant == 4) MXS_GB((gemm_big_kernel<GB_EPI_NONE, 2>));
     else if (variant == 5) MXS_GB((gemm_big_kernel<GB_EPI_NONE, 3>));
-    else MXS_GB(gemm_pp_kernel<GB_EPI_NONE>);
+    else if (variant == 6) MXS_GB(gemm_pp_kernel<GB_EPI_NONE>);
+    else MXS_GB(gemm_pp2_kernel<GB_EPI_NONE>);
   }
 #undef MXS_GB
   MXS_CHECK_LAUNCH();

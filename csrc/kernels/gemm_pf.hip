@@ -80,7 +80,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
   const int o = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int I = a.sk_tiles * nk;  // stream-K iterations (< 2 * grid * nk: fits 32 bits with o * I)
   const int sk_lo = o * I / G, sk_hi = (o + 1) * I / G;
-  const int dp_end = a.dp_rounds * nk;
+  // data-parallel rounds of this workgroup (the last round may be partial: min_iters 0 = no stream-K)
+  const int my_rounds = o < a.ntm * a.ntn ? min(a.dp_rounds, (a.ntm * a.ntn - 1 - o) / G + 1) : 0;
+  const int dp_end = my_rounds * nk;
   const int ns = dp_end + sk_hi - sk_lo;  // positions of this workgroup's stream
 
   // the segment starting at stream position c (c < ns): a data-parallel round's whole tile, or a
@@ -106,6 +108,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
+  // the wave index as a scalar: LDS-DMA destinations (M0) then need no VALU + readfirstlane per issue
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
 
   // DMA sources: buffer descriptors per tile (scalar), per-lane byte offsets (VGPR, fixed), the
   // k-tile in the scalar offset: no address arithmetic on the VALU in the loop.  X rows past M fall
@@ -156,15 +160,15 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(dst + h * HT + (2 * wid + j) * 1024), 16, wvo[h][j],
-                                                 128 * k, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(dst + h * HT + (2 * wid_s + j) * 1024), 16,
+                                                 wvo[h][j], 128 * k, 0, 0);
   };
   auto dma_x = [&](int pos, __amdgpu_buffer_rsrc_t rs, int k, int t) {  // X quarters (0, t), (1, t) of pos
     char* dst = smem + (pos & 1) * KT + XB + t * QT;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(dst + h * HT + wid * 1024), 16, xvo[h][t], 128 * k, 0,
-                                               0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(dst + h * HT + wid_s * 1024), 16, xvo[h][t], 128 * k,
+                                               0, 0);
   };
 
   float4_ acc[4][8];
@@ -174,27 +178,30 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
     for (int t = 0; t < 8; ++t) acc[f][t] = float4_{0.f, 0.f, 0.f, 0.f};
 
   const int r16 = lane & 15, kq = lane >> 4;
-  int woff[4], xoff[8];
-#pragma unroll
-  for (int f = 0; f < 4; ++f) woff[f] = (wc >> 1) * HT + (64 * (wc & 1) + 16 * f + r16) * 128;
-#pragma unroll
-  for (int t = 0; t < 8; ++t) xoff[t] = XB + wr * HT + (16 * t + r16) * 128;
+  // fragment addresses: one VGPR base per (operand, k-step); fragments f / t of a wave sit 2048 bytes
+  // apart (16 rows), folded into the ds_read immediate offsets
   const int swz = (r16 >> 1) & 7;
   const int sl0 = (kq ^ swz) << 4, sl1 = ((4 + kq) ^ swz) << 4;
+  const int wbase = (wc >> 1) * HT + (64 * (wc & 1) + r16) * 128, xbase = XB + wr * HT + r16 * 128;
+  const int wb0 = wbase + sl0, wb1 = wbase + sl1, xb0 = xbase + sl0, xb1 = xbase + sl1;
 
   pf_u32x4 wa[4][2], xb[4][2];  // [w frag][k-step], [token frag][k-step]
   auto rd_w = [&](const char* b) {
+    const char* p0 = b + wb0;
+    const char* p1 = b + wb1;
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-      wa[f][0] = *reinterpret_cast<const pf_u32x4*>(b + woff[f] + sl0);
-      wa[f][1] = *reinterpret_cast<const pf_u32x4*>(b + woff[f] + sl1);
+      wa[f][0] = *reinterpret_cast<const pf_u32x4*>(p0 + f * 2048);
+      wa[f][1] = *reinterpret_cast<const pf_u32x4*>(p1 + f * 2048);
     }
   };
   auto rd_x = [&](const char* b, int hb) {
+    const char* p0 = b + xb0 + hb * 8192;
+    const char* p1 = b + xb1 + hb * 8192;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      xb[t][0] = *reinterpret_cast<const pf_u32x4*>(b + xoff[4 * hb + t] + sl0);
-      xb[t][1] = *reinterpret_cast<const pf_u32x4*>(b + xoff[4 * hb + t] + sl1);
+      xb[t][0] = *reinterpret_cast<const pf_u32x4*>(p0 + t * 2048);
+      xb[t][1] = *reinterpret_cast<const pf_u32x4*>(p1 + t * 2048);
     }
   };
   auto mma = [&](int hb) {
@@ -430,6 +437,12 @@ int pf_plan(int M, int N, int K, int epi, int num_cu, int min_iters, int* dp_rou
   const int ntm = (M + 255) / 256, ntn = epi == PF_EPI_SWIGLU ? N / 256 : N / 256;
   const int T = ntm * ntn, nk = K / 64;
   const long work = static_cast<long>(T) * nk;
+  if (min_iters <= 0) {  // data-parallel only: one workgroup per tile, the last round may be partial
+    *grid = std::min(num_cu, T);
+    *dp_rounds = (T + *grid - 1) / *grid;
+    *sk_tiles = 0;
+    return *grid;
+  }
   int G = static_cast<int>(std::min<long>(num_cu, std::max<long>(1, work / std::max(1, min_iters))));
   if (T % G == 0) {  // whole rounds: no stream-K
     *dp_rounds = T / G;

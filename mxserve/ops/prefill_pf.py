@@ -20,7 +20,7 @@ from typing import Optional
 import torch
 
 MODE = os.environ.get("MXS_GEMM_PF", "auto")
-MIN_ITERS = (8, 16, 32)
+MIN_ITERS = (0, 8, 16, 32)  # 0: data-parallel tiles only (no stream-K)
 WIN_MARGIN = 0.98  # gemm_pf must be this much faster than the path it replaces
 ROUNDS = 3
 

@@ -134,18 +134,27 @@ class Planner:
         return out
 
     def capacity(self, kind: str, tp: int, isl: float, osl: float) -> float:
-        """Requests/s one replica sustains at the SLA (roofline, calibrated on our measurements)."""
+        """Requests/s one replica sustains at the SLA: the per-GPU role capacities the DGDR profiler
+        and bench.py plan with (profiler/capacity.py: measured MI355X table, else roofline), scaled
+        to the replica's TP degree by the roofline's own ratio."""
+        from ..profiler import capacity as capm
         c, s = self.model, self.sys
         isl, osl = max(1, int(isl)), max(1, int(osl))
-        ttft = sla.prefill_latency(c, s, isl, tp)
-        b = sla.max_decode_batch(c, s, isl + osl // 2, tp, self.cfg.itl_ms / 1e3)
-        itl = sla.decode_itl(c, s, max(1, b), isl + osl // 2, tp)
-        dec = b / (osl * itl) if b else 0.0
+        cap = capm.capacity(c.name, isl, osl, self.cfg.itl_ms, s.name)
+        ctx = isl + osl // 2
+
+        def dec_model(t):
+            b = sla.max_decode_batch(c, s, ctx, t, self.cfg.itl_ms / 1e3)
+            return b / (osl * sla.decode_itl(c, s, max(1, b), ctx, t)) if b else 0.0
+        pre = cap["prefill_rps"] * sla.prefill_latency(c, s, isl, 1) / sla.prefill_latency(c, s, isl, tp)
+        d1 = dec_model(1)
+        dec = cap["decode_rps"] * dec_model(tp) / d1 if d1 > 0 else dec_model(tp)
         if kind == "prefill":
-            return 1.0 / ttft
+            return pre
         if kind == "decode":
             return dec
-        return 1.0 / (1.0 / dec + ttft) if dec > 0 else 1.0 / ttft / 10  # agg: both on one replica
+        # agg: one replica does both halves of every request
+        return 1.0 / (1.0 / dec + 1.0 / pre) if dec > 0 else pre / 10
 
     def decide(self, w: Window, roles: list[Role]) -> dict[str, int]:
         cfg = self.cfg

@@ -38,8 +38,10 @@ class System:
 
 
 SYSTEMS = {
-    # MI355X: 2.5 PF bf16 dense, 8 TB/s spec (6.3 measured), 288 GB, 7 xGMI links x ~153 GB/s
-    "mi355x": System("mi355x", 2.5e15, 6.3e12, 288e9, 8, 153e9, 0.27, 0.80, 0.6e-3),
+    # MI355X: 2.5 PF bf16 dense, 8 TB/s spec (6.3 measured), 288 GB, 7 xGMI links x ~153 GB/s.
+    # Efficiencies this engine measures (round 3-4): batched prefill ~1.1 PF/s (0.44 of dense peak,
+    # profiles/r3/s3/prefill_capacity), decode KV streaming 6.1-6.4 TB/s (0.97 of achievable)
+    "mi355x": System("mi355x", 2.5e15, 6.3e12, 288e9, 8, 153e9, 0.44, 0.97, 0.6e-3),
     "mi300x": System("mi300x", 1.3e15, 4.3e12, 192e9, 8, 64e9, 0.30, 0.75, 0.7e-3),
     "a100_sxm": System("a100_sxm", 312e12, 1.6e12, 80e9, 8, 240e9, 0.55, 0.80, 0.6e-3),
     "h100_sxm": System("h100_sxm", 989e12, 2.8e12, 80e9, 8, 360e9, 0.45, 0.80, 0.5e-3),
@@ -184,6 +186,13 @@ def measure(model: str, isl: int, osl: int, batches=(1, 8, 32, 64, 128, 256), se
             "ttft_ms": round(ttft * 1e3, 3), "decode_itl_ms": itl}
 
 
+def b1_rps(max_batch, dec_itl, osl: int) -> float:
+    """Decode requests/s of one TP-1 replica under the ITL model in use (the scale that maps the
+    capacity model's per-GPU decode rate onto other TP degrees)."""
+    b = max_batch(1)
+    return b / (osl * dec_itl(b, 1)) if b else 0.0
+
+
 def plan(model: str, isl: int, osl: int, ttft_ms: float, itl_ms: float, system: str = "mi355x",
          gpus: int | None = None, measured: dict | None = None) -> dict:
     """Choose prefill/decode TP and replica counts meeting the SLA on one node.  With `measured`
@@ -226,19 +235,35 @@ def plan(model: str, isl: int, osl: int, ttft_ms: float, itl_ms: float, system: 
                 hi = mid - 1
         return lo
     fits = [t for t in tps if _weights_bytes(cfg) / t < sys.hbm_bytes * 0.8]
+    # per-GPU role capacities at TP 1: the one capacity model bench.py's split uses too
+    # (profiler/capacity.py: this engine's measured MI355X table, else the roofline); a --measure run
+    # replaces them with its own live throughputs
+    from . import capacity as capm
+    cap = capm.capacity(model, isl, osl, itl_ms, system)
+    if measured is not None and measured.get("prefill_rps"):
+        cap = dict(cap, prefill_rps=measured["prefill_rps"], source="measured")
+    if measured is not None:
+        b1 = max_batch(1)
+        if b1:
+            cap = dict(cap, decode_rps=b1 / (osl * dec_itl(b1, 1)), source="measured")
+    d1 = b1_rps(max_batch, dec_itl, osl)
     cands = []
     for tp_p in fits:
         ttft = pre_lat(tp_p)
         if ttft * 1e3 > ttft_ms:
             continue
-        pre_rps = 1.0 / ttft  # requests/s one prefill replica sustains
+        # requests/s one prefill replica sustains: batched prompts, not one prompt at a time; TP
+        # splits the compute and adds the all-reduces (the latency ratio prices them)
+        pre_rps = cap["prefill_rps"] * pre_lat(1) / pre_lat(tp_p)
         for tp_d in fits:
             b = max_batch(tp_d)
             if b == 0:
                 continue
             itl = dec_itl(b, tp_d)
-            dec_rps = b / (osl * itl)
-            # split the node: prefill replicas r_p, decode replicas r_d, r_p*tp_p + r_d*tp_d <= gpus
+            # the per-GPU capacity at TP 1, scaled to this TP degree by the ITL model's own ratio
+            dec_rps = cap["decode_rps"] * (b / (osl * itl)) / d1 if d1 > 0 else b / (osl * itl)
+            # split the node: prefill replicas r_p, decode replicas r_d, r_p*tp_p + r_d*tp_d <= gpus;
+            # ties go to fewer prefill replicas (capm.pd_split's rule)
             best = None
             for r_p in range(1, gpus // tp_p + 1):
                 r_d = (gpus - r_p * tp_p) // tp_d
@@ -269,8 +294,8 @@ def plan(model: str, isl: int, osl: int, ttft_ms: float, itl_ms: float, system: 
                 "itl_ms": round(itl * 1e3, 3)}
         if agg is None or cand["requests_per_s"] > agg["requests_per_s"]:
             agg = cand
-    best = max(cands, key=lambda c: c["requests_per_s"]) if cands else None
-    return {"model": cfg.name, "system": sys.name, "gpus": gpus, "sla": {"isl": isl, "osl": osl, "ttft_ms": ttft_ms,
+    best = max(cands, key=lambda c: (c["requests_per_s"], -c["gpus_used"])) if cands else None
+    return {"model": cfg.name, "capacity": {k: cap[k] for k in ("prefill_rps", "decode_rps", "source") if k in cap}, "system": sys.name, "gpus": gpus, "sla": {"isl": isl, "osl": osl, "ttft_ms": ttft_ms,
                                                                            "itl_ms": itl_ms},
             "disagg": best, "agg": agg, "feasible": best is not None or agg is not None,
             "source": "measured" if measured is not None else "roofline", "measurements": measured,

@@ -84,7 +84,7 @@ def test_planner_agg_graph_and_dry_run(api):
     cfg = PlannerConfig(namespace="ns", dgd="g", model="meta-llama/Llama-3.2-1B-Instruct", dry_run=True)
     p = Planner(cfg, api, lambda: dict(feed.c), clock=lambda: feed.t)
     p.step()
-    feed.advance(30, rps=200)
+    feed.advance(30, rps=1000)
     rec = p.step()
     assert rec["changes"]["W"] == 8  # capped by the node's GPUs
     assert api.get("DynamoGraphDeployment", "g", "ns")["spec"]["services"]["W"]["replicas"] == 1  # dry run
@@ -105,3 +105,35 @@ def test_sla_plan_from_measurements():
     assert m.itl(64) == 8.0 / 1e3 and abs(m.itl(160) - 19e-3) < 1e-9 and m.itl(512) > m.itl(256)
     # a TTFT target below the measured prefill split over 8 GPUs is infeasible
     assert not sla.plan("Qwen/Qwen3-0.6B", 4000, 500, 5, 25, measured=fast)["feasible"]
+
+
+def test_one_capacity_model_for_bench_profiler_and_planner():
+    """bench.py's disagg split, the DGDR profiler and the SLA planner read one
+    capacity model (profiler/capacity.py): the headline workload splits 3P+5D on 8 GPUs in both
+    planners, neither role is planned above 85 %, and the reference DGDR example fits one node."""
+    import argparse
+
+    import bench
+    from mxserve.profiler import capacity, sla
+    model = "meta-llama/Llama-3.2-1B-Instruct"
+    cap = capacity.capacity(model, 4000, 500)
+    assert cap["prefill_rps"] > 0 and cap["decode_rps"] > 0
+    p, d, rate = capacity.pd_split(8, cap["prefill_rps"], cap["decode_rps"])
+    ns = argparse.Namespace(model=model, isl=4000, osl=500, qps=-1.0, disagg_qps=-1.0, disagg_prefill_ranks=0)
+    bp, bd, bq = bench.disagg_plan(ns, 8)
+    plan = sla.plan(model, 4000, 500, 600, 25)
+    assert (bp, bd) == (p, d) == (plan["disagg"]["prefill"]["replicas"], plan["disagg"]["decode"]["replicas"])
+    assert plan["disagg"]["prefill"]["tp"] == plan["disagg"]["decode"]["tp"] == 1
+    # the planned node rate loads the tighter role to 85 %, in both
+    assert abs(bq * 8 - rate) < 1e-6
+    assert bq * 8 <= 0.85 * min(bp * cap["prefill_rps"], bd * cap["decode_rps"]) + 1e-6
+    # the SLA planner prices a TP-1 replica with the same per-GPU capacities
+    from mxserve.planner.planner import Planner, PlannerConfig
+    pl = Planner.__new__(Planner)
+    pl.cfg = PlannerConfig(namespace="n", dgd="g", model=model)
+    pl.model, pl.sys = sla.get_model_config(model), sla.SYSTEMS["mi355x"]
+    assert abs(pl.capacity("prefill", 1, 4000, 500) - cap["prefill_rps"]) < 1e-6
+    assert abs(pl.capacity("decode", 1, 4000, 500) - cap["decode_rps"]) < 1e-6
+    # the reference DGDR example (Qwen3-0.6B, 8 GPUs) plans within the node
+    q = sla.plan("Qwen/Qwen3-0.6B", 4000, 500, 600, 25)
+    assert q["feasible"] and q["disagg"]["gpus_used"] <= 8
