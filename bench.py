@@ -11,17 +11,24 @@ Phases (--mode auto: agg for N = 1, agg then disagg for N >= 2, both in the one 
   agg     each rank runs an independent engine replica -- the reference scales Llama-3.2-1B by
           `replicas:` of single-GPU workers behind the frontend router (examples/deploy/vllm/agg.yaml:14,21;
           SURVEY.md §2.4 P01) -- under an open-loop Poisson arrival process of --qps requests/s
-          per GPU (weak scaling).  `value` is this phase.
+          per GPU (weak scaling).  `value` is this phase.  N >= 2 (--arrivals router, default):
+          ONE stream at N x --qps, each request placed by the frontend's KV-aware router
+          (mxserve.router.Router, native KvIndexer) from the ranks' scheduler load reports, as
+          the reference's frontend places requests over its replicas (mxserve/tools/arrival_hub.py;
+          the line's `arrivals` / `per_rank` show the split and each rank's TTFT and token rate).
   disagg  ranks [0, P) prefill, [P, N) decode (examples/deploy/vllm/disagg.yaml:18-57: separate
           prefill and decode workers, each scaled by its own `replicas`).  disagg_plan() sizes P:D
-          from the two roles' capacities for this workload (a decode GPU is KV-bandwidth bound at
-          ~76 req/s, a prefill GPU computes ~118 req/s: 1P+1D at N = 2, 2P+2D at 4, 3P+5D at 8)
-          and offers the node the rate that loads the tighter role to 85 % (32 req/s per GPU at
-          N = 2 and 4, 37.6 at 8; the agg rate of 44 would overload a 1:1 split's decode GPU and
-          load 3P+5D's prefill GPUs to 99 %).  Default rate 44 req/s per GPU: sustained over 60-step
-          windows at TTFT p50 34 ms / ITL p90 21 ms (profiles/r3/s3/long_q44.json; QPS 46 holds
-          TTFT but puts ITL p90 at 23-26 ms, QPS 48 queues).
-          Requests arrive at the decode ranks; a decode rank reserves KV blocks and hands each
+          from the two roles' capacities for this workload (mxserve/profiler/capacity_mi355x.json,
+          measured: a decode GPU is KV-bandwidth bound at 76.7 req/s, a prefill GPU computes 127.6
+          req/s: 1P+1D at N = 2, 2P+2D at 4, 3P+5D at 8)
+          and offers the node the rate that loads the tighter role to 85 %; when the split carries
+          the agg rate, the disagg phase runs at it (like-for-like).  Default rate 48 req/s per GPU:
+          sustained on one MI355X over 40-step windows at TTFT p50 41 ms / ITL p90 24.0 ms, 22.5k
+          tok/s (profiles/r4/bench_q48_steps40.json; QPS 46: 21.6k at TTFT p50 34 ms / ITL p90
+          22.3 ms).  The realised Poisson rate of the fixed-seed arrival stream over those windows
+          is 97-98 % of nominal, which with the request tail bounds value at ~94 % of QPS x OSL.
+          Requests arrive at the decode ranks (routed over them like the agg phase's when D >= 2);
+          a decode rank reserves KV blocks and hands each
           prompt to the prefill rank with the fewest prompts in flight, which computes it, pushes
           the blocks into the decode rank's staging arena with the IPC copy kernel (xGMI between
           GPUs; mxserve/disagg/kv_transfer.py) and returns the first token.  TTFT includes the
@@ -89,8 +96,13 @@ def parse(argv=None):
     ap.add_argument("--model", default="meta-llama/Llama-3.2-1B-Instruct")
     ap.add_argument("--isl", type=int, default=4000)
     ap.add_argument("--osl", type=int, default=500)
-    ap.add_argument("--qps", type=float, default=float(os.environ.get("MXS_BENCH_QPS", "44")),
+    ap.add_argument("--qps", type=float, default=float(os.environ.get("MXS_BENCH_QPS", "48")),
                     help="Poisson arrival rate per GPU (requests/s)")
+    ap.add_argument("--arrivals", choices=["router", "local"], default=os.environ.get("MXS_BENCH_ARRIVALS", "router"),
+                    help="N >= 2: router = one Poisson stream at the node's rate, each request routed to a rank "
+                         "by the frontend's KV-aware router from the ranks' load reports "
+                         "(mxserve/tools/arrival_hub.py); local = an independent stream per rank")
+    ap.add_argument("--router-mode", choices=["kv", "round_robin", "random"], default="kv")
     ap.add_argument("--max-num-seqs", type=int, default=384)
     ap.add_argument("--disagg-max-num-seqs", type=int, default=512,
                     help="decode ranks of the disagg phase carry 2x the per-GPU request rate")
@@ -336,6 +348,24 @@ class Driver:
         self.c = {"ttft": [], "tokens": 0}
         # per-step samples for the steady-state test: (time, running set, arrivals, finished)
         self.hist: list = []
+        self.source = None  # ArrivalClient: requests routed here by the node's router (--arrivals router)
+        self.load_fn = None
+
+    def attach(self, source, load_fn) -> None:
+        self.source, self.load_fn = source, load_fn
+
+    def report(self, force: bool = False) -> None:
+        if self.source is not None:
+            self.source.report(self.load_fn, force)
+
+    def on_phase(self, phase: str) -> None:
+        if self.source is None:
+            return
+        if phase == "warmup":  # arrivals start once every request-owning rank is here
+            self.report(force=True)
+            self.source.start()
+        elif phase == "stop":
+            self.source.stop()
 
     def prompt(self) -> list:
         return self.rng.integers(100, self.vocab - 100, size=self.isl, dtype=np.int64).tolist()
@@ -343,6 +373,12 @@ class Driver:
     def due(self) -> list:
         """(request_id, prompt) for every arrival whose time has come."""
         out = []
+        if self.source is not None:
+            for rid, t_arr, prompt in self.source.poll():
+                self.arrival_of[rid] = t_arr  # the hub's schedule, CLOCK_MONOTONIC = perf_counter's clock
+                out.append((rid, prompt.tolist()))
+            self.nxt += len(out)
+            return out
         now_rel = time.perf_counter() - self.t_start
         while self.nxt < self.horizon and self.arrivals[self.nxt] <= now_rel:
             rid = f"r{self.rank}-{self.nxt}"
@@ -352,7 +388,9 @@ class Driver:
         return out
 
     def wait_next(self) -> None:
-        if self.nxt < self.horizon:
+        if self.source is not None:
+            self.source.wait(0.05)
+        elif self.nxt < self.horizon:
             time.sleep(max(0.0, min(0.05, self.t_start + self.arrivals[self.nxt] - time.perf_counter())))
 
     def token(self, rid: str, now: float, finished: bool = False) -> None:
@@ -406,6 +444,11 @@ _STAT_NAN = [0.0, 0.0, float("nan"), float("nan"), 0.0, float("nan"), float("nan
 def timed_phases(a, step, barrier, agree, drv, running, on_phase=lambda phase: None) -> float:
     """Warm up to steady state (agreed by every request-owning rank), soak for TTFT samples, then
     exactly K steps between barrier + device sync; returns the timed window."""
+    phase_hook = on_phase
+
+    def on_phase(ph):
+        phase_hook(ph)
+        drv.on_phase(ph)
     on_phase("warmup")
     barrier()
     vlog("warmup")
@@ -471,6 +514,7 @@ def run_agg(a, eng, sp, drv, barrier, agree) -> float:
         now = time.perf_counter()
         for o in outs:
             drv.token(o.request_id, now, o.finished)
+        drv.report()
         if eng.step_times is not None:
             eng.step_times["engine_step"] = eng.step_times.get("engine_step", 0.0) + now - t0
             eng.step_times["loop"] = eng.step_times.get("loop", 0.0) + time.perf_counter() - t_loop[0]
@@ -571,6 +615,7 @@ def run_disagg_decode(a, eng, sp, drv, barrier, agree, conns: list) -> float:
                 conns[0].poll(0.02)
             else:
                 time.sleep(0.0005)
+        drv.report()
 
     def on_phase(ph):
         for conn in conns:
@@ -718,6 +763,33 @@ def engine_args(a, ctx, **kw):
     return args
 
 
+def start_arrivals(a, ctx, owners: list, rate: float, isl: int, vocab: int, eng=None, drv=None):
+    """--arrivals router with >= 2 request-owning ranks: rank 0 starts the arrival hub (its own
+    process: one Poisson stream at the node's rate, each request routed by mxserve.router.Router from
+    the ranks' load reports), every rank learns its port, and each owner's Driver takes its requests
+    from the hub.  Collective over all ranks of ctx.  Returns rank 0's hub process (else None)."""
+    if a.arrivals != "router" or len(owners) < 2:
+        return None
+    from mxserve.tools import arrival_hub
+    hub, port = None, 0
+    if ctx.rank == 0:
+        hub, port = arrival_hub.spawn(owners, rate, isl, vocab, seed=4321 + a.seed, mode=a.router_mode)
+    port = int(ctx.gather([float(port)])[0, 0])
+    if ctx.rank in owners:
+        cl = arrival_hub.ArrivalClient(("127.0.0.1", port), ctx.rank, eng.runner.num_blocks, eng.args.block_size)
+        drv.attach(cl, eng.scheduler.stats)
+    return hub
+
+
+def finish_arrivals(hub, drv) -> dict | None:
+    if drv is not None and drv.source is not None:
+        drv.source.close()
+    if hub is None:
+        return None
+    from mxserve.tools import arrival_hub
+    return arrival_hub.collect(hub)
+
+
 def free_engine(eng, ctx) -> None:
     eng.close()
     del eng
@@ -739,7 +811,14 @@ def summarize(col: np.ndarray, steps: int, owners: list) -> dict:
 
     r = lambda x, n=2: None if x is None else round(x, n)  # noqa: E731
     ttft, itl = med(2), med(3)
-    return {"value": round(value, 2), "ms_per_step": round(t_max / steps * 1e3, 4),
+    per_rank = None
+    if len(owners) > 1:  # how evenly the node's load landed (routed arrivals) and what each rank saw
+        rr = lambda v, n: [None if np.isnan(x) else round(float(x), n) for x in v]  # noqa: E731
+        per_rank = {"rank": list(owners), "tok_s": rr(col[:, 1] / np.maximum(col[:, 0], 1e-9), 1),
+                    "first_tokens": [int(x) for x in col[:, 4]], "ttft_p50_ms": rr(col[:, 2] * 1e3, 2),
+                    "ttft_p90_ms": rr(col[:, 9] * 1e3, 2), "itl_p90_ms": rr(col[:, 10] * 1e3, 3),
+                    "running_mean": rr(col[:, 8], 1)}
+    return {"value": round(value, 2), "ms_per_step": round(t_max / steps * 1e3, 4), "per_rank": per_rank,
             "ttft_p50_ms": r(ttft), "ttft_p90_ms": r(med(9)), "itl_p50_ms": r(itl, 3), "itl_p90_ms": r(med(10), 3),
             "requests_with_first_token": int(col[:, 4].sum()),
             "warmup_steps_executed": int(np.nanmax(col[:, 5])), "warmup_s": round(float(np.nanmax(col[:, 6])), 1),
@@ -759,16 +838,21 @@ def phase_agg(a, ctx) -> tuple:
     vlog(f"agg: engine ready ({eng.runner.num_blocks} KV blocks)")
     sp = SamplingParams(max_tokens=osl, temperature=a.temperature, ignore_eos=True)
     drv = Driver(a2, ctx.rank, eng.model_config.vocab_size, a.qps)
+    hub = start_arrivals(a, ctx, list(range(ctx.world)), a.qps * ctx.world, isl, eng.model_config.vocab_size,
+                         eng, drv)
     group = None
     agree = ctx.agree_fn(group, ctx.world)
     from mxserve.utils.gcpause import PauseStats
     gcs = PauseStats().install()  # collector passes on this rank's loop (the engine froze its start-up heap)
     st = drv.stats(run_agg(a2, eng, sp, drv, ctx.barrier, agree))
     gcs.remove()
+    arrivals = finish_arrivals(hub, drv)
     info = {"kv_blocks": eng.runner.num_blocks, "graphs": sorted(eng.runner.graphs) if ctx.on_gpu else [],
             "preemptions": eng.stats()["num_preemptions"], "model": args.model,
             "kv_cache_dtype": "fp8_e4m3fn" if eng.runner.kv_fp8 else ("bf16" if ctx.on_gpu else "fp32"),
-            "isl": isl, "osl": osl}
+            "isl": isl, "osl": osl,
+            "arrivals": arrivals or {"mode": "local" if ctx.world > 1 else "single rank",
+                                     "per_rank_rate": a.qps}}
     rep = getattr(eng.runner, "decode_gemm_report", None)
     if rep:  # capture-time choice per (bucket, projection): hand-written MFMA kernels vs hipBLASLt
         info["decode_gemm"] = {"pairs": len(rep), "hand_written": sum(r["chosen"] == "mfma" for r in rep),
@@ -816,17 +900,21 @@ def phase_disagg(a, ctx) -> tuple:
     eng = LLMEngine(args)
     vlog(f"disagg: engine ready ({eng.runner.num_blocks} KV blocks)")
     conns = _disagg_conns(rank, p, world, ctx.gather)
+    drv = None
+    if not is_prefill:
+        drv = Driver(a2, rank, eng.model_config.vocab_size, qps * world / d)  # the node's rate over D ranks
+    hub = start_arrivals(a, ctx, list(range(p, world)), qps * world, isl, eng.model_config.vocab_size, eng, drv)
     if is_prefill:
         run_disagg_prefill(eng, a.temperature, ctx.barrier, conns)
         st = list(_STAT_NAN)
     else:
         sp = SamplingParams(max_tokens=osl, temperature=a.temperature, ignore_eos=True)
-        drv = Driver(a2, rank, eng.model_config.vocab_size, qps * world / d)  # the node's rate over D ranks
         agree = ctx.agree_fn(ctx.pg_decode, d)
         st = drv.stats(run_disagg_decode(a2, eng, sp, drv, ctx.barrier, agree, conns))
+    arrivals = finish_arrivals(hub, drv)
     for c in conns:
         c.close()
-    info = {"decode_max_num_seqs": a.disagg_max_num_seqs, "prefill_ranks": p, "decode_ranks": d,
+    info = {"arrivals": arrivals or {"mode": "local" if d > 1 else "single decode rank"},"decode_max_num_seqs": a.disagg_max_num_seqs, "prefill_ranks": p, "decode_ranks": d,
             "qps_per_gpu": round(qps, 2), "qps_node": round(qps * world, 2),
             "qps_per_decode_rank": round(qps * world / d, 2)}
     free_engine(eng, ctx)
@@ -956,6 +1044,9 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
         line["agg_vs_disagg"] = compare_modes(agg, dis, a.qps)
     if dis is not None:
         line["disagg"] = dis
+    line["per_rank"] = head.get("per_rank")
+    if "arrivals" in info:
+        line["arrivals"] = info["arrivals"]
     line["engine"] = {"kv_blocks": info["kv_blocks"], "preemptions": info["preemptions"], "graphs": info["graphs"]}
     for k in ("late_admission", "decode_gemm", "prefill_gemm", "chunk_budget", "gc"):
         if k in info:

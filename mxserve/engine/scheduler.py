@@ -58,6 +58,9 @@ class Scheduler:
         self.running: list[Request] = []
         self.finished_ids: list[str] = []
         self.num_preemptions = 0
+        # requests ever queued here (add / reserve_remote): routers match it against what they sent
+        # to tell which of their routed requests this worker's load already reflects
+        self.num_added = 0
         # disaggregated decode: requests whose prompt KV is being written by a prefill worker
         self.remote: dict[str, Request] = {}
         # decode-aware prefill budget (engine/pacing.py ChunkBudget), set by the engine when an
@@ -71,6 +74,7 @@ class Scheduler:
                              f"{self.max_model_len}")
         req.status = Status.WAITING
         self.waiting.append(req)
+        self.num_added += 1
 
     def abort(self, request_id: str) -> Optional[Request]:
         if request_id in self.remote:
@@ -106,6 +110,7 @@ class Scheduler:
             return False
         req.status = Status.WAITING
         self.remote[req.request_id] = req
+        self.num_added += 1
         return True
 
     def complete_remote(self, request_id: str, first_token: int) -> Request:
@@ -274,8 +279,14 @@ class Scheduler:
     def release_blocks(self, req: Request) -> None:
         self.kv.free(req)
 
+    def waiting_blocks(self) -> int:
+        """KV blocks the waiting queue will take on admission (prompt + first token, uncached)."""
+        bs = self.kv.block_size
+        return sum(-(-(r.num_prompt_tokens + 1) // bs) for r in self.waiting)
+
     def stats(self) -> dict:
         return {"num_running": len(self.running), "num_waiting": len(self.waiting),
                 "kv_usage": self.kv.usage(), "kv_free_blocks": self.kv.num_free(),
                 "kv_total_blocks": self.kv.num_blocks, "prefix_hit_rate": self.kv.hit_rate(),
-                "num_preemptions": self.num_preemptions}
+                "num_preemptions": self.num_preemptions, "num_added": self.num_added,
+                "kv_waiting_blocks": self.waiting_blocks()}

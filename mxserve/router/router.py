@@ -8,6 +8,10 @@ its lease (ttl) is dropped.  Routing modes:
   already caches (native KvIndexer, csrc/runtime/block_pool.cpp).  Cost per worker:
       cost = overlap_weight * (prompt blocks still to prefill) + (active KV blocks after admission)
   normalised by the worker's pool size; lowest cost wins (ties -> fewest running requests).
+  Active blocks are the worker's last report (held + its waiting queue's demand) plus the blocks of
+  the requests routed to it since that report: a burst of arrivals between two heartbeats spreads
+  over the workers instead of landing on the one that looked emptiest.  Workers report how many
+  requests they have queued in total (num_added), which retires routed requests from that count.
 """
 from __future__ import annotations
 
@@ -15,6 +19,7 @@ import itertools
 import random
 import threading
 import time
+from collections import deque
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -39,6 +44,12 @@ class WorkerInfo:
     num_waiting: int = 0
     kv_active_blocks: int = 0
     inflight: int = 0  # requests routed by this frontend and not finished
+    kv_waiting_blocks: int = 0  # demand of the worker's waiting queue (its last report)
+    num_added: int = -1  # requests the worker had queued at its last report (-1: not reported)
+    unseen: deque = field(default_factory=deque)  # blocks of routed requests its report does not hold yet
+
+    def load_blocks(self) -> int:
+        return self.kv_active_blocks + self.kv_waiting_blocks + sum(self.unseen)
 
     def public(self) -> dict:
         return {"worker_id": self.worker_id, "url": self.url, "model": self.model, "role": self.role,
@@ -80,6 +91,14 @@ class Registry:
             tot = int(load.get("kv_total_blocks", w.kv_total_blocks) or 1)
             w.kv_total_blocks = tot
             w.kv_active_blocks = tot - int(load.get("kv_free_blocks", tot))
+            w.kv_waiting_blocks = int(load.get("kv_waiting_blocks", 0))
+            if "num_added" in load:
+                n = int(load["num_added"])
+                for _ in range(min(len(w.unseen), max(0, n - w.num_added) if w.num_added >= 0 else len(w.unseen))):
+                    w.unseen.popleft()
+                w.num_added = n
+            else:  # a worker without the counter: its report is all the router knows
+                w.unseen.clear()
             if stored:
                 self.indexer.apply_stored(w.index, list(stored))
             if removed:
@@ -124,8 +143,18 @@ class Router:
     def block_hashes(self, token_ids: list, block_size: int = 16) -> list:
         return self._hash(token_ids, block_size, 0, 0)
 
-    def pick(self, candidates: list[WorkerInfo], token_ids: Optional[list] = None) -> tuple[WorkerInfo, int]:
-        """Returns (worker, overlap_blocks)."""
+    def pick(self, candidates: list[WorkerInfo], token_ids: Optional[list] = None,
+             commit: bool = True) -> tuple[WorkerInfo, int]:
+        """Returns (worker, overlap_blocks).  commit: count the request's blocks against the chosen
+        worker until its load report includes them."""
+        w, ov = self._pick(candidates, token_ids)
+        if commit and token_ids:
+            bs = w.block_size
+            with self.reg._lock:
+                w.unseen.append(max(0, -(-(len(token_ids) + 1) // bs) - ov))
+        return w, ov
+
+    def _pick(self, candidates: list[WorkerInfo], token_ids: Optional[list] = None) -> tuple[WorkerInfo, int]:
         if not candidates:
             raise LookupError("no workers available")
         if self.mode == "round_robin" or len(candidates) == 1:
@@ -142,7 +171,7 @@ class Router:
         for w in candidates:
             ov = overlaps[w.index]
             prefill_blocks = max(0, nblocks - ov)
-            active = w.kv_active_blocks + nblocks
+            active = w.load_blocks() + nblocks
             cost = (self.overlap_weight * prefill_blocks + active) / max(1, w.kv_total_blocks)
             key = (cost, w.num_running + w.num_waiting + w.inflight, self._rng.random())
             if best_key is None or key < best_key:

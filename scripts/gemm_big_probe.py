@@ -29,7 +29,10 @@ def main():
     dev = torch.device("cuda:0")
     ext = ops.ext()
     out = []
-    shapes = {"qkv": (3072, 2048), "o": (2048, 2048), "gate_up": (16384, 2048), "down": (2048, 8192)}
+    shapes = {"qkv": (3072, 2048), "o": (2048, 2048), "gate_up": (16384, 2048), "down": (2048, 8192),
+              "lm_head": (128256, 2048)}
+    only = [s for s in os.environ.get("GB_SHAPES", "qkv,o,gate_up,down").split(",") if s]
+    shapes = {k: v for k, v in shapes.items() if k in only}
     for M in (int(a) for a in (sys.argv[1:] or ["8192", "4096", "2048"])):
         for name, (N, K) in shapes.items():
             x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
