@@ -29,6 +29,9 @@ void launch_custom_allreduce_2shot(unsigned short*, const unsigned short*, long,
                                    unsigned*, unsigned*, hipStream_t);
 void launch_ipc_all_to_all(void*, const void*, long, const ArPeers&, int, int, long, unsigned*, unsigned*,
                            hipStream_t, const int*, long);
+void launch_car_add_rmsnorm(unsigned short*, unsigned short*, const unsigned short*, const float*, int, int, int,
+                            const unsigned short*, float, const ArPeers&, int, int, long, unsigned*, unsigned*, bool,
+                            hipStream_t);
 void launch_ep_route(int*, int*, int*, const int*, int, int, int, int, int, int, hipStream_t);
 void launch_ep_gather_rows(unsigned short*, const unsigned short*, const int*, int, int, int, int, hipStream_t);
 void launch_ep_segment_rows(int*, const int*, int, int, hipStream_t);
@@ -158,6 +161,47 @@ void custom_allreduce(at::Tensor out, at::Tensor x, std::vector<int64_t> recv_pt
          reinterpret_cast<unsigned*>(err_ptr), c10::hip::getCurrentHIPStream().stream());
 }
 
+// Fused TP epilogue: h = RMSNorm(residual += AllReduce(partial)) * w.  The partial is x (bf16 [M, H])
+// or part (fp32 split-K slabs [S][M][H]); residual [M, H] is updated in place.
+void car_add_rms_norm(at::Tensor h, at::Tensor residual, c10::optional<at::Tensor> x, c10::optional<at::Tensor> part,
+                      at::Tensor w, double eps, std::vector<int64_t> recv_ptrs, std::vector<int64_t> flag_ptrs,
+                      int64_t rank, int64_t slot_elems, int64_t epochs_ptr, int64_t err_ptr, bool two_shot) {
+  TORCH_CHECK(residual.is_cuda() && residual.scalar_type() == at::kBFloat16 && residual.is_contiguous() &&
+                  residual.dim() == 2, "residual: contiguous bf16 [M, H] GPU tensor");
+  const int M = residual.size(0), H = residual.size(1);
+  TORCH_CHECK(h.is_contiguous() && h.scalar_type() == at::kBFloat16 && h.numel() == residual.numel(), "h shape");
+  TORCH_CHECK(w.is_contiguous() && w.scalar_type() == at::kBFloat16 && w.numel() == H, "w: bf16 [H]");
+  TORCH_CHECK(H % 8 == 0 && H <= 16384, "H must be a multiple of 8, at most 16384");
+  TORCH_CHECK(static_cast<int64_t>(M) * H <= slot_elems, "M * H must fit a slot");
+  TORCH_CHECK(x.has_value() != part.has_value(), "exactly one of x (bf16 partial) / part (fp32 slabs)");
+  const unsigned short* xp = nullptr;
+  const float* pp = nullptr;
+  int S = 1;
+  if (x.has_value()) {
+    TORCH_CHECK(x->is_contiguous() && x->scalar_type() == at::kBFloat16 && x->numel() == residual.numel(), "x shape");
+    xp = reinterpret_cast<const unsigned short*>(x->data_ptr());
+  } else {
+    TORCH_CHECK(part->is_contiguous() && part->scalar_type() == at::kFloat && part->numel() % residual.numel() == 0,
+                "part: fp32 [S, M, H]");
+    S = static_cast<int>(part->numel() / residual.numel());
+    TORCH_CHECK(S >= 1, "at least one slab");
+    pp = part->data_ptr<float>();
+  }
+  const int n = static_cast<int>(recv_ptrs.size());
+  TORCH_CHECK(n >= 1 && n <= mxs::kArMaxRanks && static_cast<int>(flag_ptrs.size()) == n, "1..8 ranks");
+  mxs::ArPeers peers{};
+  for (int r = 0; r < n; ++r) {
+    peers.recv[r] = reinterpret_cast<char*>(recv_ptrs[r]);
+    peers.flags[r] = reinterpret_cast<unsigned*>(flag_ptrs[r]);
+  }
+  if (M == 0) return;
+  mxs::launch_car_add_rmsnorm(reinterpret_cast<unsigned short*>(h.data_ptr()),
+                              reinterpret_cast<unsigned short*>(residual.data_ptr()), xp, pp, S, M, H,
+                              reinterpret_cast<const unsigned short*>(w.data_ptr()), static_cast<float>(eps), peers,
+                              static_cast<int>(rank), n, slot_elems, reinterpret_cast<unsigned*>(epochs_ptr),
+                              reinterpret_cast<unsigned*>(err_ptr), two_shot, c10::hip::getCurrentHIPStream().stream());
+}
+
 // equal splits: out/in hold N segments of seg_bytes each; segment d of `in` goes to rank d
 void ipc_all_to_all(at::Tensor out, at::Tensor in, std::vector<int64_t> recv_ptrs, std::vector<int64_t> flag_ptrs,
                     int64_t rank, int64_t slot_bytes, int64_t epochs_ptr, int64_t err_ptr,
@@ -232,6 +276,10 @@ void register_comm(pybind11::module_& m) {
   m.def("host_register", &host_register);
   m.def("host_unregister", &host_unregister);
   m.def("custom_allreduce", &custom_allreduce, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("recv_ptrs"),
+        pybind11::arg("flag_ptrs"), pybind11::arg("rank"), pybind11::arg("slot_elems"), pybind11::arg("epochs_ptr"),
+        pybind11::arg("err_ptr"), pybind11::arg("two_shot") = false);
+  m.def("car_add_rms_norm", &car_add_rms_norm, pybind11::arg("h"), pybind11::arg("residual"), pybind11::arg("x"),
+        pybind11::arg("part"), pybind11::arg("w"), pybind11::arg("eps"), pybind11::arg("recv_ptrs"),
         pybind11::arg("flag_ptrs"), pybind11::arg("rank"), pybind11::arg("slot_elems"), pybind11::arg("epochs_ptr"),
         pybind11::arg("err_ptr"), pybind11::arg("two_shot") = false);
   m.def("ipc_all_to_all", &ipc_all_to_all, pybind11::arg("out"), pybind11::arg("in"), pybind11::arg("recv_ptrs"),

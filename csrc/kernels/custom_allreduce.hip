@@ -214,6 +214,189 @@ void launch_custom_allreduce_2shot(bf16_t* out, const bf16_t* x, long n, const A
   MXS_CHECK_LAUNCH();
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused TP epilogue of a projection that feeds the residual stream (o_proj / down_proj at TP > 1):
+//   y = AllReduce(x) rounded to bf16, residual += y (in place), h = RMSNorm(residual) * w
+// -- one launch instead of the all-reduce plus the fused add + RMSNorm kernel, and the reduced
+// projection output never makes a bf16 round trip through memory.  The input is this rank's partial
+// projection, either bf16 [M, H] or S fp32 split-K slabs [S][M][H] left by the decode GEMM with its
+// reduce skipped (summed and rounded to bf16 here, as the GEMM's own output would be), so the split-K
+// reduce kernel disappears too.  Rounding follows the unfused path: bf16 partials, an fp32 sum in
+// rank order rounded to bf16, bf16 residual add (the residual matches bit for bit), the norm over
+// the rounded residual (its sum of squares reduced over this kernel's thread layout).
+//
+// The pushes spread over all blocks (a decode batch of a few rows still uses every block's links);
+// the norm needs whole rows, so after the exchange a block waits for EVERY (block, rank) flag of the
+// call (64 x N flags, one per thread) and then owns rows blockIdx.x, + gridDim.x, ...  Epochs, parity
+// and the one-call-ahead argument are the one-shot kernel's (a peer's call k + 2 needs this rank's
+// flags of call k + 1, raised only by this rank's next launch, which the stream starts after every
+// block of this one has finished reading).  TWO: the two-shot exchange (reduce-scatter by push, owner
+// sums, all-gather by push) for large messages; its row phase reads each slice from its owner's slot.
+template <int NV, bool TWO>
+__global__ void __launch_bounds__(512) car_add_rmsnorm_kernel(
+    bf16_t* __restrict__ h, bf16_t* __restrict__ residual, const bf16_t* __restrict__ x,
+    const float* __restrict__ part, int S, int M, int H, const bf16_t* __restrict__ w, float eps, ArPeers peers,
+    int rank, int nranks, long slot_elems, unsigned* epochs, unsigned* err) {
+  __shared__ float scratch[16];
+  __shared__ unsigned s_epoch;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const long nv = static_cast<long>(M) * H / 8;
+  const long sl = TWO ? (nv + nranks - 1) / nranks : nv;  // vectors per owner slice
+  const long per = (sl + gridDim.x - 1) / gridDim.x;
+  const long o0 = b * per, o1 = min(sl, o0 + per);
+  if (tid == 0) s_epoch = epochs[b] + 1;
+  __syncthreads();
+  const unsigned e = s_epoch;
+  const int par = e & 1;
+  const long my_slot = (static_cast<long>(par) * nranks + rank) * slot_elems * 2;  // bytes
+  const size_t slab = static_cast<size_t>(M) * H;
+  // this rank's partial of vector v, rounded to bf16
+  auto partial = [&](long v) -> uint4 {
+    if (part == nullptr) return reinterpret_cast<const uint4*>(x)[v];
+    const float* p = part + v * 8;
+    float4 a = *reinterpret_cast<const float4*>(p), c = *reinterpret_cast<const float4*>(p + 4);
+    for (int s2 = 1; s2 < S; ++s2) {
+      const float4 a2 = *reinterpret_cast<const float4*>(p + s2 * slab);
+      const float4 c2 = *reinterpret_cast<const float4*>(p + s2 * slab + 4);
+      a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
+      c.x += c2.x; c.y += c2.y; c.z += c2.z; c.w += c2.w;
+    }
+    return make_uint4(pack2(a.x, a.y), pack2(a.z, a.w), pack2(c.x, c.y), pack2(c.z, c.w));
+  };
+  auto sum_slots = [&](const char* base, long v) -> uint4 {  // fp32 sum over ranks, rank order
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < nranks; ++r) {
+      const uint4 q = reinterpret_cast<const uint4*>(base + r * slot_elems * 2)[v];
+      const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[2 * k] += bf2f_lo(u[k]);
+        acc[2 * k + 1] += bf2f_hi(u[k]);
+      }
+    }
+    return make_uint4(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]), pack2(acc[4], acc[5]), pack2(acc[6], acc[7]));
+  };
+  auto wait_all = [&](int flag_base) {  // every (block, rank) flag of this epoch: one per thread
+    if (tid < static_cast<int>(gridDim.x) * nranks) {
+      const int bb = tid / nranks, r = tid - bb * nranks;
+      ar_wait(peers.flags[rank] + flag_base + bb * kArMaxRanks + r, e, err);
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  };
+  const char* mine = peers.recv[rank] + (static_cast<long>(par) * nranks * slot_elems) * 2;
+  if constexpr (!TWO) {
+    // 1. push this block's vectors into slot [par][rank] of every rank (self included)
+    for (long v = o0 + tid; v < o1; v += blockDim.x) {
+      const uint4 val = partial(v);
+      for (int r = 0; r < nranks; ++r) reinterpret_cast<uint4*>(peers.recv[r] + my_slot)[v] = val;
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (tid < nranks) st_flag(peers.flags[tid] + b * kArMaxRanks + rank, e);
+    wait_all(0);
+  } else {
+    // 1. reduce-scatter push: slice r of the partial -> rank r
+    for (int r = 0; r < nranks; ++r) {
+      uint4* dst = reinterpret_cast<uint4*>(peers.recv[r] + my_slot);
+      for (long o = o0 + tid; o < o1; o += blockDim.x) {
+        const long v = r * sl + o;
+        if (v < nv) dst[v] = partial(v);
+      }
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (tid < nranks) st_flag(peers.flags[tid] + b * kArMaxRanks + rank, e);
+    if (tid < nranks) ar_wait(peers.flags[rank] + b * kArMaxRanks + tid, e, err);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    // 2. sum the owned slice and push it to every rank's slot [par][rank]
+    for (long o = o0 + tid; o < o1; o += blockDim.x) {
+      const long v = rank * sl + o;
+      if (v >= nv) break;
+      const uint4 rr = sum_slots(mine, v);
+      for (int r = 0; r < nranks; ++r) reinterpret_cast<uint4*>(peers.recv[r] + my_slot)[v] = rr;
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (tid < nranks) st_flag(peers.flags[tid] + kArFlags2 + b * kArMaxRanks + rank, e);
+    wait_all(kArFlags2);
+  }
+  // 3. rows: reduced y (+ residual) -> residual, RMSNorm -> h
+  const int hv = H / 8;
+  for (int row = b; row < M; row += gridDim.x) {
+    bf16_t* rr = residual + static_cast<size_t>(row) * H;
+    uint4 vals[NV];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = tid + i * blockDim.x;
+      if (c < hv) {
+        const long v = static_cast<long>(row) * hv + c;
+        uint4 y;
+        if constexpr (TWO) {
+          const int q = static_cast<int>(v / sl);
+          y = reinterpret_cast<const uint4*>(mine + q * slot_elems * 2)[v];
+        } else {
+          y = sum_slots(mine, v);
+        }
+        const uint4 rv = *reinterpret_cast<const uint4*>(rr + c * 8);
+        const uint32_t py[4] = {y.x, y.y, y.z, y.w}, pr[4] = {rv.x, rv.y, rv.z, rv.w};
+        uint32_t po[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          po[k] = pack2(bf2f_lo(py[k]) + bf2f_lo(pr[k]), bf2f_hi(py[k]) + bf2f_hi(pr[k]));
+          const float lo = bf2f_lo(po[k]), hi = bf2f_hi(po[k]);
+          ss += lo * lo + hi * hi;
+        }
+        vals[i] = make_uint4(po[0], po[1], po[2], po[3]);
+        *reinterpret_cast<uint4*>(rr + c * 8) = vals[i];
+      }
+    }
+    const float inv = rsqrtf(block_sum(ss, scratch) / static_cast<float>(H) + eps);
+    bf16_t* hr = h + static_cast<size_t>(row) * H;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = tid + i * blockDim.x;
+      if (c < hv) {
+        const uint4 wv = *reinterpret_cast<const uint4*>(w + c * 8);
+        const uint32_t p[4] = {vals[i].x, vals[i].y, vals[i].z, vals[i].w}, pw[4] = {wv.x, wv.y, wv.z, wv.w};
+        uint32_t po[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          po[k] = pack2(bf2f_lo(p[k]) * inv * bf2f_lo(pw[k]), bf2f_hi(p[k]) * inv * bf2f_hi(pw[k]));
+        *reinterpret_cast<uint4*>(hr + c * 8) = make_uint4(po[0], po[1], po[2], po[3]);
+      }
+    }
+    __syncthreads();  // scratch reuse by the next row's block_sum
+  }
+  if (tid == 0) epochs[b] = e;
+}
+
+void launch_car_add_rmsnorm(bf16_t* h, bf16_t* residual, const bf16_t* x, const float* part, int S, int M, int H,
+                            const bf16_t* w, float eps, const ArPeers& peers, int rank, int nranks, long slot_elems,
+                            unsigned* epochs, unsigned* err, bool two_shot, hipStream_t s) {
+  const int nv = (H / 8 + 511) / 512;
+#define MXS_CARN(NVV, TW)                                                                                     \
+  hipLaunchKernelGGL((car_add_rmsnorm_kernel<NVV, TW>), dim3(kArMaxBlocks), dim3(512), 0, s, h, residual, x, \
+                     part, S, M, H, w, eps, peers, rank, nranks, slot_elems, epochs, err)
+  if (two_shot) {
+    switch (nv) {
+      case 1: MXS_CARN(1, true); break;
+      case 2: MXS_CARN(2, true); break;
+      default: MXS_CARN(4, true); break;
+    }
+  } else {
+    switch (nv) {
+      case 1: MXS_CARN(1, false); break;
+      case 2: MXS_CARN(2, false); break;
+      default: MXS_CARN(4, false); break;
+    }
+  }
+#undef MXS_CARN
+  MXS_CHECK_LAUNCH();
+}
+
 // Equal-split all-to-all over the same IPC slots (EP dispatch / combine of fixed-capacity MoE
 // layouts, SURVEY.md §5.8 "direct peer writes into pre-registered IPC receive buffers"): segment d
 // of the input is pushed into rank d's slot [par][rank], one flag per (block, peer), then segment r

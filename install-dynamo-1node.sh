@@ -5,6 +5,11 @@
 #   3) the mxserve operator (replaces the Dynamo operator + etcd + NATS: workers register with the
 #      frontend directly, no external state store)
 #   4) AMD GPU Operator (or the ROCm k8s-device-plugin DaemonSet) and wait for amd.com/gpu allocatable
+# 2) and 3) are two Helm releases when helm is on PATH (deploy/helm/mxserve-crds, mxserve-platform;
+# the reference's CRD + platform releases): upgrade = re-run with a new RELEASE_VERSION, rollback =
+# `helm rollback mxserve-platform -n $NAMESPACE`, removal = `UNINSTALL=true ./install-dynamo-1node.sh`
+# (the CRDs, and with them every DGD, only with PURGE_CRDS=true).  Without helm (MXS_USE_HELM=false
+# or no binary) the same objects are applied with kubectl.
 set -euo pipefail
 HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
 
@@ -30,14 +35,46 @@ GPU_OPERATOR_POD_WAIT_INTERVAL="${GPU_OPERATOR_POD_WAIT_INTERVAL:-5}"
 # reference's flags; a single node needs neither, so they are reported and otherwise no-ops
 ENABLE_GROVE="${ENABLE_GROVE:-false}"
 ENABLE_KAI_SCHEDULER="${ENABLE_KAI_SCHEDULER:-false}"
+MXS_USE_HELM="${MXS_USE_HELM:-auto}"                               # auto | true | false
+CRD_RELEASE="${CRD_RELEASE:-mxserve-crds}"
+PLATFORM_RELEASE="${PLATFORM_RELEASE:-mxserve-platform}"
+HELM_TIMEOUT="${HELM_TIMEOUT:-10m}"
+UNINSTALL="${UNINSTALL:-false}"
+PURGE_CRDS="${PURGE_CRDS:-false}"
 
 say() { printf '\n[install] %s\n' "$*"; }
 die() { printf 'ERROR: %s\n' "$*" >&2; exit 1; }
 for c in kubectl; do command -v "$c" >/dev/null || die "missing $c"; done
 kubectl version >/dev/null 2>&1 || die "cannot reach the cluster (KUBECONFIG?)"
 
+use_helm=false
+if [[ "$MXS_USE_HELM" == "true" ]] || { [[ "$MXS_USE_HELM" == "auto" ]] && command -v helm >/dev/null; }; then
+  command -v helm >/dev/null || die "MXS_USE_HELM=true but helm is not on PATH"
+  use_helm=true
+fi
+
+if [[ "$UNINSTALL" == "true" ]]; then
+  say "uninstall: operator release / objects in ${NAMESPACE}"
+  if $use_helm && helm status "$PLATFORM_RELEASE" -n "$NAMESPACE" >/dev/null 2>&1; then
+    helm uninstall "$PLATFORM_RELEASE" -n "$NAMESPACE" --wait
+  else
+    kubectl delete -n "$NAMESPACE" -f "$HERE/deploy/operator/operator.yaml" --ignore-not-found
+  fi
+  if [[ "$PURGE_CRDS" == "true" ]]; then
+    say "uninstall: CRDs (deletes every DGD / DGDR / DCD)"
+    if $use_helm && helm status "$CRD_RELEASE" -n default >/dev/null 2>&1; then
+      helm uninstall "$CRD_RELEASE" -n default --wait
+    else
+      kubectl delete -f "$HERE/deploy/crds/" --ignore-not-found
+    fi
+  else
+    say "CRDs kept (PURGE_CRDS=true removes them and every custom resource)"
+  fi
+  exit 0
+fi
+
 say "configuration"
-for v in NAMESPACE RELEASE_VERSION MXS_IMAGE NAMESPACE_RESTRICTED_OPERATOR ENABLE_GROVE ENABLE_KAI_SCHEDULER \
+for v in NAMESPACE RELEASE_VERSION MXS_IMAGE MXS_USE_HELM NAMESPACE_RESTRICTED_OPERATOR ENABLE_GROVE ENABLE_KAI_SCHEDULER \
          PROMETHEUS_ENDPOINT GPU_RESOURCE GPU_OPERATOR_MODE GPU_OPERATOR_NS GPU_OPERATOR_RELEASE GPU_OPERATOR_HELM_TIMEOUT; do
   echo "  ${v}=${!v}"
 done
@@ -54,17 +91,28 @@ if ! kubectl get storageclass -o jsonpath='{range .items[*]}{.metadata.annotatio
   kubectl patch storageclass local-path -p '{"metadata":{"annotations":{"storageclass.kubernetes.io/is-default-class":"true"}}}'
 fi
 
-say "CRDs"
-kubectl apply -f "$HERE/deploy/crds/"
-
-say "operator ${MXS_IMAGE} in ${NAMESPACE}"
-kubectl create namespace "$NAMESPACE" --dry-run=client -o yaml | kubectl apply -f -
-watch_args='[]'
-[[ "$NAMESPACE_RESTRICTED_OPERATOR" == "true" ]] && watch_args="[\"--namespace\", \"${NAMESPACE}\"]"
-sed -e "s#IMAGE_PLACEHOLDER#${MXS_IMAGE}#g" -e "s#NAMESPACE_PLACEHOLDER#${NAMESPACE}#g" \
-    -e "s#WATCH_ARGS_PLACEHOLDER#${watch_args}#" -e "s#GPU_RESOURCE_PLACEHOLDER#${GPU_RESOURCE}#" \
-    -e "s#PROMETHEUS_ENDPOINT_PLACEHOLDER#${PROMETHEUS_ENDPOINT}#" \
-    "$HERE/deploy/operator/operator.yaml" | kubectl apply -n "$NAMESPACE" -f -
+if $use_helm; then
+  say "CRDs: helm release ${CRD_RELEASE} (chart deploy/helm/mxserve-crds, version ${RELEASE_VERSION})"
+  helm upgrade --install "$CRD_RELEASE" "$HERE/deploy/helm/mxserve-crds" -n default \
+    --version "$RELEASE_VERSION" --wait --timeout "$HELM_TIMEOUT"
+  say "operator: helm release ${PLATFORM_RELEASE} in ${NAMESPACE} (${MXS_IMAGE})"
+  helm upgrade --install "$PLATFORM_RELEASE" "$HERE/deploy/helm/mxserve-platform" -n "$NAMESPACE" --create-namespace \
+    --set image.repository="${MXS_IMAGE%:*}" --set image.tag="${MXS_IMAGE##*:}" \
+    --set namespaceRestricted="$NAMESPACE_RESTRICTED_OPERATOR" --set gpuResource="$GPU_RESOURCE" \
+    --set prometheusEndpoint="$PROMETHEUS_ENDPOINT" --wait --timeout "$HELM_TIMEOUT"
+  helm history "$PLATFORM_RELEASE" -n "$NAMESPACE" --max 3 || true
+else
+  say "CRDs (kubectl)"
+  kubectl apply -f "$HERE/deploy/crds/"
+  say "operator ${MXS_IMAGE} in ${NAMESPACE} (kubectl)"
+  kubectl create namespace "$NAMESPACE" --dry-run=client -o yaml | kubectl apply -f -
+  watch_args='["--interval", "30"]'
+  [[ "$NAMESPACE_RESTRICTED_OPERATOR" == "true" ]] && watch_args="[\"--interval\", \"30\", \"--namespace\", \"${NAMESPACE}\"]"
+  sed -e "s#IMAGE_PLACEHOLDER#${MXS_IMAGE}#g" -e "s#NAMESPACE_PLACEHOLDER#${NAMESPACE}#g" \
+      -e "s#WATCH_ARGS_PLACEHOLDER#${watch_args}#" -e "s#GPU_RESOURCE_PLACEHOLDER#${GPU_RESOURCE}#" \
+      -e "s#PROMETHEUS_ENDPOINT_PLACEHOLDER#${PROMETHEUS_ENDPOINT}#" \
+      "$HERE/deploy/operator/operator.yaml" | kubectl apply -n "$NAMESPACE" -f -
+fi
 kubectl -n "$NAMESPACE" rollout status deploy/mxserve-operator --timeout=600s
 # the operator hands PROMETHEUS_ENDPOINT to the SLA planners it runs (reference: prometheusEndpoint
 # Helm value of the platform chart); workers and frontends are scraped through PodMonitors

@@ -19,7 +19,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops import reference as ref
-from ..parallel.comm import get_tp, tp_all_gather, tp_all_reduce
+from ..parallel.comm import get_tp, tp_add_rms_norm, tp_all_gather, tp_all_reduce, tp_linear_add_rms_norm
 from .config import ModelConfig
 
 
@@ -247,12 +247,14 @@ class TransformerLM:
         out = ops.linear(o.reshape(ns, -1), w[p + "o"])
         return tp_all_reduce(out)
 
-    def _mlp(self, i: int, h: torch.Tensor) -> torch.Tensor:
+    def _mlp(self, i: int, h: torch.Tensor, reduce: bool = True) -> tuple:
+        """(output, partial): partial = the output is this rank's share, still to be all-reduced
+        (always False when reduce=True: the all-reduce ran here)."""
         w, p = self.w, f"l{i}."
         if self.cfg.is_moe and self.moe_dispatch == "a2a" and self.tp_size > 1:
             from ..parallel.expert import moe_a2a
             return moe_a2a(h, w[p + "gate"], w[p + "w13"], w[p + "w2"], self.cfg.num_experts_per_tok,
-                           self.tp_rank, self.tp_size, get_tp().group)
+                           self.tp_rank, self.tp_size, get_tp().group), False
         if self.cfg.is_moe:
             router = F.linear(h, w[p + "gate"])
             tw, tid = ops.moe_topk_softmax(router, self.cfg.num_experts_per_tok)
@@ -260,7 +262,9 @@ class TransformerLM:
         else:
             a = ops.gate_up_silu(h, w[p + "gate_up"])
             out = ops.linear(a, w[p + "down"])
-        return tp_all_reduce(out)
+        if not reduce:
+            return out, self.tp_size > 1
+        return tp_all_reduce(out), False
 
     @torch.inference_mode()
     def calibrate_kv_scales(self, block_size: int = 16, n: int = 256, headroom: float = 2.0) -> None:
@@ -297,7 +301,7 @@ class TransformerLM:
         h, residual = ops.embed_rms_norm(input_ids, self.w["embed"], self.w["l0.in_norm"], c.rms_norm_eps)
         # steps with prefill chunks: the last layer only computes the rows that produce logits
         prune = self.prune_last_layer and md.num_prefills > 0 and md.sample_seq is not None
-        if self.fuse_residual and self.tp_size == 1 and h.is_cuda:
+        if self.fuse_residual and h.is_cuda:
             return self._forward_fused(h, residual, md, kv_cache, prune)
         x = None
         for i in range(c.num_layers):
@@ -312,15 +316,18 @@ class TransformerLM:
             else:
                 x = self._attention(i, h, md, kv_cache[:, i])
             h, residual = ops.fused_add_rms_norm(x, residual, self.w[p + "post_norm"], c.rms_norm_eps)
-            x = self._mlp(i, h)
+            x = self._mlp(i, h)[0]
         h, _ = ops.fused_add_rms_norm(x, residual, self.w["norm"], c.rms_norm_eps)
         return h if prune else h.index_select(0, md.logits_indices)
 
     def _forward_fused(self, h: torch.Tensor, residual: torch.Tensor, md: AttnMetadata, kv_cache: torch.Tensor,
                        prune: bool) -> torch.Tensor:
-        """TP = 1: every projection that feeds the residual stream ends in the next RMSNorm
-        (ops.linear_add_rms_norm), so a layer is qkv -> rope/cache -> attention -> o+add+norm ->
-        gate_up+SiLU -> down+add+norm(next layer's input norm, or the final norm)."""
+        """Every projection that feeds the residual stream ends in the next RMSNorm, so a layer is
+        qkv -> rope/cache -> attention -> o+add+norm -> gate_up+SiLU -> down+add+norm(next layer's
+        input norm, or the final norm).  TP = 1: ops.linear_add_rms_norm (split-K slabs summed in the
+        norm kernel).  TP > 1: comm.tp_linear_add_rms_norm -- the row-parallel partial (or its split-K
+        slabs) goes through ONE kernel that all-reduces over the IPC mesh, adds the residual and
+        normalises (custom_allreduce.hip car_add_rmsnorm_kernel)."""
         c, w = self.cfg, self.w
         eps = c.rms_norm_eps
         L = c.num_layers
@@ -333,13 +340,15 @@ class TransformerLM:
                 residual = residual.index_select(0, md.logits_indices)
             else:
                 o = self._attention(i, h, md, kv_cache[:, i], project=False)
-            h, residual = ops.linear_add_rms_norm(o, w[p + "o"], residual, w[p + "post_norm"], eps)
+            h, residual = tp_linear_add_rms_norm(o, w[p + "o"], residual, w[p + "post_norm"], eps)
             nxt = w[f"l{i + 1}.in_norm"] if i + 1 < L else w["norm"]
             if c.is_moe:
-                h, residual = ops.fused_add_rms_norm(self._mlp(i, h), residual, nxt, eps)
+                y, partial = self._mlp(i, h, reduce=False)
+                h, residual = tp_add_rms_norm(y, residual, nxt, eps) if partial else \
+                    ops.fused_add_rms_norm(y, residual, nxt, eps)
             else:
-                h, residual = ops.linear_add_rms_norm(ops.gate_up_silu(h, w[p + "gate_up"]), w[p + "down"], residual,
-                                                      nxt, eps)
+                h, residual = tp_linear_add_rms_norm(ops.gate_up_silu(h, w[p + "gate_up"]), w[p + "down"], residual,
+                                                     nxt, eps)
         return h if prune else h.index_select(0, md.logits_indices)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:

@@ -63,6 +63,7 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
 
 
 MT_MIN_M = 64
+SPLITS = (1, 2, 4, 8, 16, 32)  # split-K factors the tuner tries (16 / 32: narrow shards over a long K)
 MT_SMALL_M_MIN_BYTES = int(os.environ.get("MXS_MT_SMALL_M_MIN_BYTES", str(192 << 20)))
 MT_COUNTERS = 1 << 16  # tile counters of the in-launch split-K reduction (every launch leaves them zero)
 # in-launch split-K reduction (last arriver sums the slabs): measured slower than the separate reduce
@@ -88,7 +89,7 @@ def mt_candidates(M: int, N: int, K: int, epi: int, max_blocks: int = 1024) -> l
             continue
         ntm = -(-M // bm)
         tiles = ntm * (outN // outb)
-        for sk in (1, 2, 4, 8):
+        for sk in SPLITS[:5]:
             if K % (64 * sk) or K // sk < 128 or tiles * sk > max_blocks:
                 continue
             out.append(("mt", wm, wn, mr, wnf, sk))
@@ -121,8 +122,13 @@ def _candidates_mf(M: int, N: int, K: int, epi: int, mf: int) -> list[tuple]:
             outN = N // 2 if epi else N
             if outN % (wn * nh * 16):
                 continue
-            for sk in (1, 2, 4, 8):
+            ntiles = outN // (wn * nh * 16)
+            for sk in SPLITS:
                 if K % (32 * unroll(mf, nf) * sk):
+                    continue
+                # deep splits only where the column tiles alone leave the chip idle (TP-sharded
+                # projections: Llama-3-70B qkv at TP 8 is 1280 columns over K = 8192)
+                if sk > 8 and (ntiles * sk > 1024 or K // sk < 256):
                     continue
                 out.append((mf, nf, wm, sk, 0))
     return out
@@ -296,7 +302,7 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
         return []
     store = TunedStore("decode_gemm", device_tag(device))
     # workspace for the largest split-K any candidate may pick
-    need = max(8 * max(bks) * v[0].shape[0] for v in shapes.values())
+    need = max(max(SPLITS) * max(bks) * v[0].shape[0] for v in shapes.values())
     TABLE.part = torch.empty(need, dtype=torch.float32, device=device)
     TABLE.cnt = torch.zeros(MT_COUNTERS, dtype=torch.int32, device=device)
     rows = []

@@ -96,6 +96,43 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def tp_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float) -> tuple:
+    """(RMSNorm(residual + AllReduce(x)) * w, new residual) for a TP-partial projection output x that
+    feeds the residual stream.  With the custom all-reduce: one kernel (exchange + add + norm); else
+    the all-reduce and then the fused add + RMSNorm kernel.  TP = 1: just the add + norm."""
+    from .. import ops
+    st = _STATE
+    if st.tp_size > 1:
+        car = st.custom_ar
+        if car is not None and x.is_contiguous() and x.dtype == residual.dtype and car.can_add_rms_norm(residual):
+            return car.add_rms_norm(residual, w, eps, x=x)
+        x = tp_all_reduce(x)
+    return ops.fused_add_rms_norm(x, residual, w, eps)
+
+
+def tp_linear_add_rms_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, norm_w: torch.Tensor,
+                           eps: float) -> tuple:
+    """The projection x @ w.T (o_proj / down_proj, row-parallel: a TP-partial sum) + all-reduce +
+    residual add + RMSNorm.  TP = 1: ops.linear_add_rms_norm.  TP > 1 with the custom all-reduce:
+    when the decode table runs the shard split-K, its fp32 slabs go straight into the fused
+    all-reduce kernel (no split-K reduce kernel, no bf16 partial); otherwise the bf16 partial does."""
+    from .. import ops
+    st = _STATE
+    if st.tp_size == 1:
+        return ops.linear_add_rms_norm(x, w, residual, norm_w, eps)
+    car = st.custom_ar
+    if car is not None and car.can_add_rms_norm(residual) and x.is_cuda and x.dim() == 2 \
+            and 0 < x.shape[0] <= ops._decode_max_m():
+        from ..ops.decode_gemm import TABLE
+        M, N = x.shape[0], w.shape[0]
+        cfg = TABLE.lookup(M, N, w.shape[1], 0)
+        if cfg is not None and TABLE.splitk(cfg) > 1:
+            S = TABLE.splitk(cfg)
+            if TABLE.run(residual, x, w, cfg, 0, reduce=False):  # no output written: reduce skipped
+                return car.add_rms_norm(residual, norm_w, eps, part=TABLE.part[:S * M * N])
+    return tp_add_rms_norm(ops.linear(x, w), residual, norm_w, eps)
+
+
 def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
     st = _STATE
     if st.tp_size == 1:

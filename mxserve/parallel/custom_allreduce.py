@@ -103,6 +103,23 @@ class CustomAllReduce:
                                    self.epochs_ptr, self.err_ptr, two_shot)
         return out
 
+    def can_add_rms_norm(self, residual: torch.Tensor) -> bool:
+        return (not self.disabled and residual.is_cuda and residual.dtype == torch.bfloat16 and residual.dim() == 2
+                and residual.shape[1] % 8 == 0 and residual.shape[1] <= 16384
+                and residual.numel() * 2 <= self.max_bytes)
+
+    def add_rms_norm(self, residual: torch.Tensor, w: torch.Tensor, eps: float, x: Optional[torch.Tensor] = None,
+                     part: Optional[torch.Tensor] = None) -> tuple:
+        """(RMSNorm(residual + AllReduce(partial)) * w, residual updated in place) in one kernel
+        (custom_allreduce.hip car_add_rmsnorm_kernel).  The partial is x (bf16, residual's shape) or
+        part (fp32 split-K slabs [S, M, H] of the projection, summed and rounded here)."""
+        from .. import ops
+        h = torch.empty_like(residual)
+        two_shot = self.world > 2 and residual.numel() * 2 >= self.two_shot_min_bytes
+        ops.ext().car_add_rms_norm(h, residual, x, part, w, eps, self.recv_ptrs, self.flag_ptrs, self.rank,
+                                   self.slot_elems, self.epochs_ptr, self.err_ptr, two_shot)
+        return h, residual
+
     def can_all_to_all(self, x: torch.Tensor) -> bool:
         nbytes = x.numel() * x.element_size()
         return (not self.disabled and x.is_cuda and x.is_contiguous() and nbytes % self.world == 0

@@ -372,6 +372,18 @@ class Probe:
         res.update(info, model=model, parallelism=f"disagg {p}P+{n - p}D")
         return res
 
+    def tp_layer(self) -> dict:
+        """Llama-3-70B decode layer of one TP shard at this world size (mxserve/tools/tp_layer_bench.py):
+        tuned shard GEMMs + the fused all-reduce / residual-add / RMSNorm epilogues, the chain captured
+        in a hipGraph on every rank against the weight-streaming floor.  A real node only: ranks that
+        share a GPU are time-sliced by the command processor, so their collectives measure nothing."""
+        if not self.on_gpu:
+            return {"skipped": "no GPU"}
+        if self.shared:
+            return {"skipped": "ranks share a GPU (time-sliced collectives); see profiles/r4/tp"}
+        from . import tp_layer_bench
+        return tp_layer_bench.run((1, 8, 64), shared=False, barrier=self.barrier, log=lambda s: None) or {}
+
     def p2p(self) -> dict:
         torch = self.torch
         if not self.on_gpu or self.ndev < 2 or self.rank != 0:
@@ -439,6 +451,7 @@ class Probe:
                     ("tp", lambda: self.sharded_vs_full(tp_model, "allreduce")),
                     ("ep", lambda: self.sharded_vs_full(ep_model, "a2a")),
                     ("p2p", self.p2p),
+                    ("tp_layer", self.tp_layer),
                     ("tp_engine", lambda: self.tp_engine(MODEL_TP_ENGINE if self.on_gpu else "tiny-llama")),
                     ("ep_engine", lambda: self.tp_engine(MODEL_EP_ENGINE if self.on_gpu else "tiny-mixtral", "a2a")),
                     ("disagg_8b", lambda: self.disagg(MODEL_DISAGG if self.on_gpu else "tiny-llama", 2.0))]

@@ -1,0 +1,154 @@
+"""Fused TP epilogue: one kernel all-reduces a row-parallel projection's partial
+over the IPC mesh, adds the residual and applies RMSNorm (custom_allreduce.hip
+car_add_rmsnorm_kernel).  2 / 4 / 8 ranks are processes sharing GPU 0, each with its own exported and
+peer-mapped buffers exactly as across xGMI.  Checked against a plain fp32 PyTorch reference of the
+same op (rank-order fp32 sum of the bf16 partials, bf16 rounding where the unfused path rounds),
+against the unfused all-reduce + fused add/RMSNorm kernels (residual bit for bit), with fp32 split-K slabs as the
+input, one-shot and two-shot, and inside a captured hipGraph."""
+import multiprocessing as mp
+import os
+import traceback
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EPS = 1e-5
+SHAPES = [(1, 8192), (7, 2048), (64, 8192), (200, 8192), (3, 16384), (256, 1024)]
+
+
+def _ref(parts, residual, w):
+    """fp32 reference: y = bf16(sum_r bf16 partial_r, rank order), res = bf16(y + residual),
+    h = bf16(res * rsqrt(mean(res^2) + eps) * w)."""
+    import torch
+    acc = torch.zeros_like(parts[0], dtype=torch.float32)
+    for p in parts:
+        acc = acc + p.float()
+    y = acc.to(torch.bfloat16).float()
+    res = (y + residual.float()).to(torch.bfloat16)
+    r = res.float()
+    inv = torch.rsqrt(r.pow(2).mean(dim=-1, keepdim=True) + EPS)
+    return (r * inv * w.float()).to(torch.bfloat16), res
+
+
+def _rank(rank, world, port, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        from mxserve import ops
+        from mxserve.parallel.custom_allreduce import CustomAllReduce
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda:0")
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        car = CustomAllReduce.create(dist.group.WORLD, dev, max_bytes=8 << 20)
+        errs = []
+
+        def data(M, H, seed, slabs=0):
+            g = torch.Generator().manual_seed(seed)
+            res = (torch.randn(M, H, generator=g) * 2).to(torch.bfloat16)
+            w = (1 + 0.1 * torch.randn(H, generator=g)).to(torch.bfloat16)
+            parts, slab = [], None
+            for r in range(world):
+                if slabs:
+                    s = torch.randn(slabs, M, H, generator=g) * 0.3
+                    acc = torch.zeros(M, H)
+                    for k in range(slabs):
+                        acc = acc + s[k]
+                    parts.append(acc.to(torch.bfloat16))
+                    if r == rank:
+                        slab = s.to(dev)
+                else:
+                    parts.append((torch.randn(M, H, generator=g) * 0.5).to(torch.bfloat16))
+            return parts, res, w, slab
+
+        call = 0
+        for two_shot in ([False, True] if world > 2 else [False]):
+            car.two_shot_min_bytes = 0 if two_shot else 1 << 40
+            for M, H in SHAPES:
+                for slabs in (0, 3):
+                    call += 1
+                    parts, res, w, slab = data(M, H, 1000 * call, slabs)
+                    hr, rr = _ref(parts, res, w)
+                    residual = res.to(dev)
+                    wd = w.to(dev)
+                    if slabs:
+                        h, residual = car.add_rms_norm(residual, wd, EPS, part=slab)
+                    else:
+                        h, residual = car.add_rms_norm(residual, wd, EPS, x=parts[rank].to(dev))
+                    torch.cuda.synchronize()
+                    tag = f"world {world} two_shot {two_shot} M {M} H {H} slabs {slabs}"
+                    if not torch.equal(residual.cpu(), rr):
+                        errs.append(f"{tag}: residual max err {(residual.cpu().float() - rr.float()).abs().max()}")
+                    err = (h.cpu().float() - hr.float()).abs().max().item()
+                    if err > 0.02 * max(1.0, hr.float().abs().max().item()):
+                        errs.append(f"{tag}: h max err {err}")
+                    if slabs == 0:  # the unfused all-reduce + add/RMSNorm kernels: the same residual
+                        # bit for bit; h within one bf16 rounding (the row's sum of squares is
+                        # reduced over a different thread layout)
+                        res2 = res.to(dev)
+                        y = car.all_reduce(parts[rank].to(dev))
+                        h2, res2 = ops.fused_add_rms_norm(y, res2, wd, EPS)
+                        torch.cuda.synchronize()
+                        if not torch.equal(res2, residual):
+                            errs.append(f"{tag}: residual differs from the unfused path")
+                        d = (h2.float() - h.float()).abs() / h2.float().abs().clamp_min(1e-3)
+                        if d.max().item() > 1.0 / 128:
+                            errs.append(f"{tag}: h differs from the unfused path by {d.max().item()}")
+        # hipGraph: two fused calls captured, replayed twice (device-side epochs)
+        car.two_shot_min_bytes = 512 << 10
+        specs = [(16, 8192, 0), (128, 8192, 2)]
+        bufs = []
+        for k, (M, H, slabs) in enumerate(specs):
+            parts, res, w, slab = data(M, H, 777 + k, slabs)
+            bufs.append((res, w.to(dev), parts[rank].to(dev), slab, _ref(parts, res, w), res.to(dev)))
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        outs = []
+        with torch.cuda.stream(s):
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=s):
+                for res, wd, xd, slab, _, rd in bufs:
+                    outs.append(car.add_rms_norm(rd, wd, EPS, part=slab) if slab is not None
+                                else car.add_rms_norm(rd, wd, EPS, x=xd))
+        for rep in range(2):
+            for res, _, _, _, _, rd in bufs:
+                rd.copy_(res.to(dev))
+            torch.cuda.synchronize()
+            dist.barrier()
+            g.replay()
+            torch.cuda.synchronize()
+            for k, ((h, r2), b) in enumerate(zip(outs, bufs)):
+                hr, rr = b[4]
+                if not torch.equal(r2.cpu(), rr) or (h.cpu().float() - hr.float()).abs().max().item() > 0.05:
+                    errs.append(f"graph rep {rep} call {k}")
+        dist.barrier()
+        assert car.check(), "error word raised"
+        q.put((rank, errs))
+    except BaseException:  # noqa: BLE001
+        q.put((rank, [traceback.format_exc()]))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_fused_allreduce_add_rmsnorm(world):
+    import socket
+    import torch
+    if torch.cuda.device_count() < 1:
+        pytest.skip("no GPU")
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's HIP state is inherited
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        res = dict(q.get(timeout=240) for _ in range(world))
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert res[r] == [], res[r]

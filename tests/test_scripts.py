@@ -206,6 +206,7 @@ def test_bench_contract_cpu(mode, nproc, launcher, tmp_path):
     want = {"auto": "agg" if nproc == 1 else "both"}.get(mode, mode)
     assert d["config"]["mode"] == want
     if want == "both":
+        assert "value" in d["disagg"], d["disagg"]
         assert d["agg"]["value"] == d["value"] and d["disagg"]["value"] > 0
         assert d["disagg"]["parallelism"] == f"disagg {nproc // 2}P+{nproc // 2}D"
     if want in ("both", "disagg"):  # hosted by the crash-isolated probe processes

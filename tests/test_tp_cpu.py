@@ -65,3 +65,43 @@ def test_tp2_matches_tp1(model, moe_dispatch):
     assert out == ref
     # every step's inputs went to the follower through the /dev/shm ring, none over gloo
     assert ring_steps > 6 and fallbacks == 0
+
+
+def _ar_norm_rank(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    from mxserve.ops import reference as ref
+    from mxserve.parallel.comm import init_distributed, tp_add_rms_norm, tp_linear_add_rms_norm
+    init_distributed(world, backend="gloo")
+    g = torch.Generator().manual_seed(7)
+    x_all = torch.randn(world, 5, 64, generator=g)
+    w_all = torch.randn(world, 64, 32, generator=g) * 0.2
+    a_all = torch.randn(world, 5, 32, generator=g)
+    res0 = torch.randn(5, 64, generator=g)
+    nw = 1 + 0.1 * torch.randn(64, generator=g)
+    h, res = tp_add_rms_norm(x_all[rank].clone(), res0.clone(), nw, 1e-5)
+    want_h, want_res = ref.fused_add_rms_norm(x_all.sum(0), res0.clone(), nw, 1e-5)
+    h2, res2 = tp_linear_add_rms_norm(a_all[rank].clone(), w_all[rank], res0.clone(), nw, 1e-5)
+    y = sum(a_all[r] @ w_all[r].T for r in range(world))
+    want_h2, want_res2 = ref.fused_add_rms_norm(y, res0.clone(), nw, 1e-5)
+    ok = all(torch.allclose(u, v, atol=1e-4, rtol=1e-4) for u, v in
+             ((h, want_h), (res, want_res), (h2, want_h2), (res2, want_res2)))
+    q.put((rank, ok))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_tp_add_rms_norm_gloo():
+    """comm.tp_add_rms_norm / tp_linear_add_rms_norm (the TP > 1 residual epilogues: one fused
+    all-reduce + add + RMSNorm kernel on the GPU) reduce the row-parallel partials over the group and
+    match the unsharded add + RMSNorm (CPU, gloo, 2 ranks)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_ar_norm_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=30)
+    assert res == {0: True, 1: True}
