@@ -161,6 +161,26 @@ void custom_allreduce(at::Tensor out, at::Tensor x, std::vector<int64_t> recv_pt
          reinterpret_cast<unsigned*>(err_ptr), c10::hip::getCurrentHIPStream().stream());
 }
 
+// A HIP stream restricted to a subset of the CUs (hipExtStreamCreateWithCUMask): bit i of the mask
+// words enables CU i.  Used to run bandwidth-bound and compute-bound kernels side by side on disjoint
+// CU sets (mxserve/engine/cu_partition.py); torch wraps the handle with torch.cuda.ExternalStream.
+int64_t cu_mask_stream(std::vector<int64_t> mask_words) {
+  std::vector<uint32_t> m(mask_words.begin(), mask_words.end());
+  hipStream_t s = nullptr;
+  hip_check(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(m.size()), m.data()),
+            "hipExtStreamCreateWithCUMask");
+  return reinterpret_cast<int64_t>(s);
+}
+
+std::vector<int64_t> stream_cu_mask(int64_t stream, int64_t words) {
+  std::vector<uint32_t> m(static_cast<size_t>(words), 0u);
+  hip_check(hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(stream), static_cast<uint32_t>(words), m.data()),
+            "hipExtStreamGetCUMask");
+  return std::vector<int64_t>(m.begin(), m.end());
+}
+
+void stream_destroy(int64_t stream) { (void)hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)); }
+
 // Fused TP epilogue: h = RMSNorm(residual += AllReduce(partial)) * w.  The partial is x (bf16 [M, H])
 // or part (fp32 split-K slabs [S][M][H]); residual [M, H] is updated in place.
 void car_add_rms_norm(at::Tensor h, at::Tensor residual, c10::optional<at::Tensor> x, c10::optional<at::Tensor> part,
@@ -278,6 +298,9 @@ void register_comm(pybind11::module_& m) {
   m.def("custom_allreduce", &custom_allreduce, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("recv_ptrs"),
         pybind11::arg("flag_ptrs"), pybind11::arg("rank"), pybind11::arg("slot_elems"), pybind11::arg("epochs_ptr"),
         pybind11::arg("err_ptr"), pybind11::arg("two_shot") = false);
+  m.def("cu_mask_stream", &cu_mask_stream);
+  m.def("stream_cu_mask", &stream_cu_mask);
+  m.def("stream_destroy", &stream_destroy);
   m.def("car_add_rms_norm", &car_add_rms_norm, pybind11::arg("h"), pybind11::arg("residual"), pybind11::arg("x"),
         pybind11::arg("part"), pybind11::arg("w"), pybind11::arg("eps"), pybind11::arg("recv_ptrs"),
         pybind11::arg("flag_ptrs"), pybind11::arg("rank"), pybind11::arg("slot_elems"), pybind11::arg("epochs_ptr"),

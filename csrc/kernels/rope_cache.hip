@@ -130,12 +130,16 @@ __global__ void __launch_bounds__(256) rope_cache_t16_kernel(
   const int row_stride = (Hq + 2 * Hkv) * D, hkd = Hkv * D;
   const int hbeg = q_out != nullptr ? 0 : Hq;  // nullptr: K / V only (see rope_cache_kernel)
   const int per_tok = (Hq + Hkv - hbeg) * V4;
-  if (threadIdx.x == 0) {
-    const int64_t s0 = slot_mapping[t0];
-    int fast = s0 >= 0 && (s0 % BS) + nt <= BS;
-    for (int k = 1; k < nt && fast; ++k) fast = slot_mapping[t0 + k] == s0 + k;
-    s_slot0 = s0;
-    s_fast = fast;
+  if (threadIdx.x < 64) {  // wave 0: the nt slots in parallel (one load per lane, not a serial chain)
+    const int k = threadIdx.x;
+    const int64_t sk = k < nt ? slot_mapping[t0 + k] : 0;
+    const int64_t s0 = __shfl(sk, 0, 64);
+    const bool ok = k >= nt || sk == s0 + k;
+    const bool all_ok = __all(ok);
+    if (k == 0) {
+      s_slot0 = s0;
+      s_fast = all_ok && s0 >= 0 && (s0 % BS) + nt <= BS;
+    }
   }
   for (int i = threadIdx.x; i < nt * per_tok; i += blockDim.x) {
     const int tt = i / per_tok, rem = i - tt * per_tok, hh = rem / V4, p = (rem - hh * V4) * 4, head = hbeg + hh;

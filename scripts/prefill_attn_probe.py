@@ -15,7 +15,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     from mxserve import ops
     dev = torch.device("cuda:0")
-    for D, hq, hkv, nseq, per in ((64, 32, 8, 2, 4096), (64, 32, 8, 1, 8192), (128, 32, 8, 2, 4096)):
+    cases = ((64, 32, 8, 2, 4096), (64, 32, 8, 1, 8192), (128, 32, 8, 2, 4096))
+    if os.environ.get("PA_CASE"):  # one case (counter passes): index into cases
+        cases = (cases[int(os.environ["PA_CASE"])],)
+    for D, hq, hkv, nseq, per in cases:
         T = nseq * per
         pb = math.ceil(per / 16)
         bt = torch.arange(nseq * pb, device=dev, dtype=torch.int32).view(nseq, pb)
