@@ -59,7 +59,16 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
     # profiles/r2_mt_gemm_probe_70b_cold_weights.jsonl)
     if mt and (M >= MT_MIN_M or (M >= 8 and N * K * 2 >= MT_SMALL_M_MIN_BYTES)):
         out += mt_candidates(M, N, K, epi)
+    # the persistent 256 x 256-tile prefill kernel (gemm_pf.hip, data-parallel tiles) on the widest
+    # projections only -- lm_head: 501 column tiles keep every CU busy at any batch; 154 vs 183 us at
+    # M = 256 (profiles/r4/gemm_pf_at_decode_batches.jsonl), while narrow ones leave it a dozen tiles
+    if M >= PF_MIN_M and N % 256 == 0 and K % 64 == 0 and N >= PF_MIN_N:
+        out.append(("pf", 0))
     return out
+
+
+PF_MIN_M = 128
+PF_MIN_N = 32768
 
 
 MT_MIN_M = 64
@@ -146,7 +155,7 @@ class DecodeGemmTable:
         if MODE == "off" or M > MAX_M:
             return None
         if MODE == "force":
-            c = [x for x in candidates(M, N, K, epi) if x[0] != "mt"]
+            c = [x for x in candidates(M, N, K, epi) if x[0] not in ("mt", "pf")]
             return next((x for x in c if x[3] == 1), c[0] if c else None)
         ent = self.entries.get((N, K, epi))
         if not ent:
@@ -158,6 +167,8 @@ class DecodeGemmTable:
 
     @staticmethod
     def splitk(cfg: tuple) -> int:
+        if cfg[0] == "pf":
+            return 1
         return cfg[5] if cfg[0] == "mt" else cfg[3]
 
     def run(self, out: torch.Tensor, x: torch.Tensor, w: torch.Tensor, cfg: tuple, epi: int,
@@ -165,6 +176,9 @@ class DecodeGemmTable:
         """reduce=False (split-K configurations only): leave the fp32 slabs [sk][M][N] in self.part for
         the caller's epilogue kernel (ops.linear_add_rms_norm)."""
         from . import ext
+        if cfg[0] == "pf":
+            from . import gemm_pf
+            return gemm_pf(x, w, epi, out, int(cfg[1])) is not None
         mt = cfg[0] == "mt"
         if mt:
             wm, wn, mr, wnf, sk = cfg[1:6]
@@ -338,7 +352,7 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
                     lib_fn = lambda i: torch.nn.functional.linear(x, ws[i % len(ws)])  # noqa: E731
                 fns = {}
                 for cfg in candidates(M, N, K, epi):
-                    if cfg[0] != "mt" and M > OLD_FORMS_MAX_M:
+                    if cfg[0] not in ("mt", "pf") and M > OLD_FORMS_MAX_M:
                         continue
                     if not TABLE.run(out, x, w, cfg, epi):
                         continue
