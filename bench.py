@@ -23,9 +23,9 @@ Phases (--mode auto: agg for N = 1, agg then disagg for N >= 2, both in the one 
           req/s: 1P+1D at N = 2, 2P+2D at 4, 3P+5D at 8)
           and offers the node the rate that loads the tighter role to 85 %; when the split carries
           the agg rate, the disagg phase runs at it (like-for-like).  Default rate 48 req/s per GPU:
-          sustained on one MI355X over 40-step windows at TTFT p50 41 ms / ITL p90 24.0 ms, 22.5k
-          tok/s (profiles/r4/bench_q48_steps40.json; QPS 46: 21.6k at TTFT p50 34 ms / ITL p90
-          22.3 ms).  The realised Poisson rate of the fixed-seed arrival stream over those windows
+          sustained on one MI355X over 40-step windows at 22.5k tok/s, TTFT p50 54 ms / ITL p90
+          21.3 ms with 6144-token steps (8192: 22.5k, 42 ms / 24.2 ms; QPS 50 queues: TTFT ~1 s;
+          profiles/r4/sched_q*.json).  The realised Poisson rate of the fixed-seed arrival stream over those windows
           is 97-98 % of nominal, which with the request tail bounds value at ~94 % of QPS x OSL.
           Requests arrive at the decode ranks (routed over them like the agg phase's when D >= 2);
           a decode rank reserves KV blocks and hands each
@@ -111,7 +111,9 @@ def parse(argv=None):
                          "can carry it, else the capacity rate; < 0 = the capacity rate of disagg_plan()")
     ap.add_argument("--disagg-prefill-ranks", type=int, default=int(os.environ.get("MXS_BENCH_DISAGG_P", "0")),
                     help="prefill ranks of the disagg phase (the rest decode); 0 = disagg_plan()")
-    ap.add_argument("--max-num-batched-tokens", type=int, default=8192)
+    ap.add_argument("--max-num-batched-tokens", type=int, default=int(os.environ.get("MXS_BENCH_MNBT", "6144")),
+                    help="token budget of a step (prefill chunk + decode rows): 6144 holds ITL p90 at 21 ms at QPS 48 "
+                         "where 8192 sits at 24-25 ms, at the same output rate (profiles/r4/sched_q48_*.json)")
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--itl-target-ms", type=float, default=float(os.environ.get("MXS_BENCH_ITL_TARGET_MS", "0")),
                     help="decode-aware prefill chunk budget (0 = fixed --max-num-batched-tokens chunks)")

@@ -78,6 +78,11 @@ class ArrivalHub:
             self.error = repr(e)[:300]
         finally:
             self._done.set()
+            for c in self.conns.values():  # every rank stopped: its reader sees EOF and ends
+                try:
+                    c.close()
+                except OSError:
+                    pass
 
     def _reader(self, r: int, c) -> None:
         try:
@@ -154,7 +159,8 @@ class ArrivalClient:
         self.received = 0
         self._lock = threading.Lock()
         self._ev = threading.Event()
-        threading.Thread(target=self._reader, daemon=True).start()
+        self._thread = threading.Thread(target=self._reader, daemon=True)
+        self._thread.start()
 
     def _reader(self) -> None:
         try:
@@ -163,8 +169,8 @@ class ArrivalClient:
                 if msg[0] == "req":
                     self.q.put((msg[1], float(msg[2]), msg[3]))
                     self._ev.set()
-        except (EOFError, OSError):
-            pass
+        except (EOFError, OSError, TypeError, ValueError):
+            pass  # the hub closed its end (every rank stopped) or this end was closed
 
     def wait(self, timeout: float) -> None:
         """Block until a request is queued here (or timeout)."""
@@ -205,7 +211,12 @@ class ArrivalClient:
         self.received += len(out)
         return out
 
-    def close(self) -> None:
+    def close(self, timeout: float = 10.0) -> None:
+        """The hub closes its end once every rank has stopped; the reader then sees EOF.  Close this
+        end only after that: closing a socket under a reader blocked in it frees the descriptor
+        number while the reader may still read from it, and a socket opened next (the next phase's
+        control channels) could take that number."""
+        self._thread.join(timeout)
         try:
             self.conn.close()
         except OSError:

@@ -491,7 +491,12 @@ class Probe:
                 res[name] = {"status": "failed", "error": repr(e)[:300]}
             if isinstance(res[name], dict):
                 res[name]["wall_s"] = round(time.perf_counter() - t0, 1)
-            self.barrier()
+            try:
+                self.barrier()
+            except Exception as e:  # noqa: BLE001 - a rank lost in that section: keep what was measured
+                traceback.print_exc()
+                res["aborted_after"] = {"section": name, "error": repr(e)[:200]}
+                break
             if name == "disagg_headline":  # the optional sections' cap starts after it
                 t_start = time.perf_counter()
         self.current = "done"
