@@ -144,13 +144,14 @@ def _mplan(M: int, N: int, K: int, device) -> Optional[list]:
     ent = tab.get(f"{N}x{K}")
     if not ent:
         return None
-    # the packaged table is on a 128-row grid, tables tuned at start-up on a 256-row one
-    e = None
-    for g in (128, 256):
-        bucket = -(-M // g) * g
-        e = ent.get(str(bucket))
-        if e is not None:
-            break
+    # each shape's entry lives on the row grid it was swept on (the packaged table: 128 rows; start-up
+    # tuning: 256): the grid is its smallest bucket.  Only that grid's bucket is looked up -- a plan
+    # measured for the next coarser bucket must not be stretched over up to 255 shaved rows
+    g = ent.get("_grid")
+    if g is None:
+        g = ent["_grid"] = min(int(k) for k in ent if k.isdigit())
+    bucket = -(-M // g) * g
+    e = ent.get(str(bucket))
     if e is None:
         return None
     plan = [list(seg) for seg in e["plan"]]

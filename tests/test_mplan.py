@@ -60,3 +60,20 @@ def test_mplan_coarse_grid_lookup():
         assert ops._mplan(4100, 4096, 14336, dev) == [[4, "mm"], [4096, "mm"]]
     finally:
         ops._MPLAN.pop(dev, None)
+
+
+def test_mplan_lookup_stays_on_the_entry_grid():
+    """a shape swept on the 128-row grid is looked up on that grid only -- a missing
+    128-row bucket means 'no plan' (F.linear was best there), not the next 256-row bucket's plan
+    stretched over up to 255 shaved rows; a start-up table swept every 256 rows uses its own grid."""
+    dev = torch.device("cpu")
+    ops._MPLAN[dev] = {
+        "16384x2048": {"128": {"plan": [[128, "lin"]]}, "384": {"plan": [[128, "mm"], [256, "lin"]]},
+                       "512": {"plan": [[256, "mm"], [256, "lin"]]}},
+        "2048x8192": {"256": {"plan": [[256, "lin"]]}, "512": {"plan": [[256, "mm"], [256, "lin"]]}}}
+    try:
+        assert ops._mplan(300, 16384, 2048, dev) == [[44, "mm"], [256, "lin"]]  # 128-grid bucket 384
+        assert ops._mplan(200, 16384, 2048, dev) is None  # 128-grid bucket 256 absent: no plan
+        assert ops._mplan(300, 2048, 8192, dev) == [[44, "mm"], [256, "lin"]]  # 256-grid bucket 512
+    finally:
+        ops._MPLAN.pop(dev, None)
