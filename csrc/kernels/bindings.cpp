@@ -32,6 +32,7 @@ void launch_penalties(void*, bool, int, int, long, const int*, long, const int64
 void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStream_t);
 void launch_moe_align(int*, int*, const int*, int, int, int, int*, hipStream_t);
 void launch_moe_combine(bf16_t*, const bf16_t*, const float*, const int*, int, int, int, hipStream_t);
+bool launch_skinny_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, bool, hipStream_t);
 bool launch_decode_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int,
                         int, hipStream_t, const int* = nullptr, int = 0, int = 0, int = 0, int = 1);
 bool launch_mt_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int, int,
@@ -318,6 +319,25 @@ bool decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::T
                                  epi, stream(), nullptr, 0, 0, lu, reduce ? 1 : 0);
 }
 
+// Skinny form (gemm_decode.hip skinny_gemm_kernel): M <= 16 rows, 16-column W slices x 4 k-ranges of
+// kr per workgroup; K / (4 kr) > 1 groups leave fp32 slabs [groups][M][N] in `part` (summed here when
+// reduce, else by the caller's epilogue).
+bool skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> part, int64_t kr, bool reduce) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == N, "shape mismatch");
+  if (x.stride(1) != 1 || out.stride(1) != 1 || kr <= 0 || K % (4 * kr) != 0) return false;
+  const int64_t groups = K / (4 * kr);
+  float* p = nullptr;
+  if (groups > 1) {
+    TORCH_CHECK(part.has_value() && part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->numel() >= groups * M * N, "split-K needs an fp32 workspace of groups * M * N");
+    p = part->data_ptr<float>();
+  }
+  return mxs::launch_skinny_gemm(bf(out), p, bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), kr, reduce, stream());
+}
+
 // Medium-M form of the decode projection (gemm_decode.hip mt_gemm_kernel, M = 64-256 and short
 // prefill chunks): WM x WN waves of 32 MR rows x 32 WNF weight rows, same epilogues and workspace rule
 // as decode_gemm; with `cnt` (int32 tile counters, zeroed once, left zero by every launch) the split-K
@@ -506,6 +526,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("moe_align", &moe_align, pybind11::arg("expert_offsets"), pybind11::arg("perm"), pybind11::arg("topk_ids"),
         pybind11::arg("e_lo"), pybind11::arg("e_local"), pybind11::arg("inv") = pybind11::none());
   m.def("moe_combine", &moe_combine);
+  m.def("skinny_gemm", &skinny_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
+        pybind11::arg("part") = pybind11::none(), pybind11::arg("kr") = 256, pybind11::arg("reduce") = true);
   m.def("decode_gemm", &decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("part"), pybind11::arg("mf"), pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"),
         pybind11::arg("epi"), pybind11::arg("lu") = 0, pybind11::arg("reduce") = true);

@@ -321,6 +321,87 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Skinny form ("sk"): M <= 16 rows (small-batch decode) against a weight whose columns alone cannot
+// fill 256 CUs with long enough streams -- the tensor-parallel shards of a large model (Llama-3-70B
+// at TP 8: qkv 1280 x 8192, o 8192 x 1024, down 8192 x 3584).  Pure weight streaming: every W byte is
+// read once, so the whole game is bytes in flight per CU.
+//   * a workgroup = 4 waves on ONE 16-row slice of W and 4 consecutive k-ranges of KR; a wave issues
+//     all its KR / 32 W fragment loads (16 B per lane, non-temporal) and the matching X loads up front,
+//     then runs v_mfma_f32_16x16x32_bf16 (A = W slice, B = X^T, padded rows of X read as zeros):
+//     at KR = 256 a wave keeps 8 KiB of W in flight, ~10 waves per CU on the TP-8 qkv shard;
+//   * the 4 partial 16 x 16 tiles meet in LDS; blockIdx.y is a k-group of 4 KR: one group writes
+//     bf16 Y, several write fp32 slabs [group][M][N] that the consumer sums (the split-K reduce, the
+//     fused rope / all-reduce + RMSNorm epilogues read slabs directly).
+template <int KR>
+__global__ void __launch_bounds__(256) skinny_gemm_kernel(bf16_t* __restrict__ Y, float* __restrict__ part,
+                                                          const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                          int M, int N, int K, int ldx, int ldy) {
+  constexpr int STEPS = KR / 32;
+  __shared__ float red[4][16][17];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int k0 = (blockIdx.y * 4 + wid) * KR + 8 * q;
+  const bf16_t* wp = W + static_cast<size_t>(n0 + r) * K + k0;
+  const bool xrow = r < M;
+  const bf16_t* xp = X + static_cast<size_t>(xrow ? r : 0) * ldx + k0;
+  u32x4 wf[STEPS], xf[STEPS];
+#pragma unroll
+  for (int s = 0; s < STEPS; ++s) wf[s] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wp + 32 * s));
+#pragma unroll
+  for (int s = 0; s < STEPS; ++s) {
+    xf[s] = *reinterpret_cast<const u32x4*>(xp + 32 * s);
+    if (!xrow) xf[s] = u32x4{0u, 0u, 0u, 0u};
+  }
+  float4_ acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < STEPS; ++s)
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wf[s]), as_bf16x8(xf[s]), acc, 0, 0, 0);
+  // acc[i] = C[n = 4 q + i][m = r]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wid][4 * q + i][r] = acc[i];
+  __syncthreads();
+  if (wid != 0) return;
+  // wave 0: 16 x 16 outputs, 4 per lane: n = 4 q + i, m = r
+  if (r >= M) return;
+  float v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = 4 * q + i;
+    v[i] = red[0][n][r] + red[1][n][r] + red[2][n][r] + red[3][n][r];
+  }
+  if (part != nullptr) {
+    float* pr = part + (static_cast<size_t>(blockIdx.y) * M + r) * N + n0 + 4 * q;
+    *reinterpret_cast<float4_*>(pr) = float4_{v[0], v[1], v[2], v[3]};
+  } else {
+    bf16_t* yr = Y + static_cast<size_t>(r) * ldy + n0 + 4 * q;
+    *reinterpret_cast<uint2*>(yr) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+  }
+}
+
+bool launch_skinny_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx,
+                        int ldy, int KR, bool reduce, hipStream_t s) {
+  if (M <= 0 || M > 16 || N % 16 != 0 || ldx % 8 != 0 || ldy % 4 != 0 || (KR != 128 && KR != 256)) return false;
+  if (K % (4 * KR) != 0) return false;
+  const int groups = K / (4 * KR);
+  if (groups > 1 && part == nullptr) return false;
+  dim3 grid(N / 16, groups), blk(256);
+  float* p = groups > 1 ? part : nullptr;
+  if (KR == 128)
+    hipLaunchKernelGGL(skinny_gemm_kernel<128>, grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
+  else
+    hipLaunchKernelGGL(skinny_gemm_kernel<256>, grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
+  MXS_CHECK_LAUNCH();
+  if (groups > 1 && reduce) {
+    const long total4 = static_cast<long>(M) * N / 4;
+    const int blocks = static_cast<int>(std::min<long>((total4 + 255) / 256, 1024));
+    hipLaunchKernelGGL(splitk_reduce_kernel<EPI_NONE>, dim3(blocks), dim3(256), 0, s, Y, part, M, N, groups, ldy, 0);
+    MXS_CHECK_LAUNCH();
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------------
 // Medium-M form ("mt"): decode batches of 64-256 rows (and short prefill chunks), where the weight
 // bytes no longer dominate the on-chip traffic: at M = 256 every weight element feeds 512 FLOP, so
 // the MFMA pipe, the LDS read port and the L2 re-reads of X all matter (cdna_hip_programming.md §5,

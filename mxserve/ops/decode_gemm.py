@@ -64,6 +64,9 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
     # M = 256 (profiles/r4/gemm_pf_at_decode_batches.jsonl), while narrow ones leave it a dozen tiles
     if M >= PF_MIN_M and N % 256 == 0 and K % 64 == 0 and N >= PF_MIN_N:
         out.append(("pf", 0))
+    # small batches: 16-column weight slices streamed with every load in flight (skinny_gemm_kernel)
+    if M <= 16 and not epi and N % 16 == 0:
+        out += [("sk", kr, K // (4 * kr)) for kr in (128, 256) if K % (4 * kr) == 0]
     return out
 
 
@@ -155,7 +158,7 @@ class DecodeGemmTable:
         if MODE == "off" or M > MAX_M:
             return None
         if MODE == "force":
-            c = [x for x in candidates(M, N, K, epi) if x[0] not in ("mt", "pf")]
+            c = [x for x in candidates(M, N, K, epi) if x[0] not in ("mt", "pf", "sk")]
             return next((x for x in c if x[3] == 1), c[0] if c else None)
         ent = self.entries.get((N, K, epi))
         if not ent:
@@ -169,6 +172,8 @@ class DecodeGemmTable:
     def splitk(cfg: tuple) -> int:
         if cfg[0] == "pf":
             return 1
+        if cfg[0] == "sk":  # ("sk", kr, k-groups of 4 x kr)
+            return cfg[2]
         return cfg[5] if cfg[0] == "mt" else cfg[3]
 
     def run(self, out: torch.Tensor, x: torch.Tensor, w: torch.Tensor, cfg: tuple, epi: int,
@@ -179,6 +184,19 @@ class DecodeGemmTable:
         if cfg[0] == "pf":
             from . import gemm_pf
             return gemm_pf(x, w, epi, out, int(cfg[1])) is not None
+        if cfg[0] == "sk":
+            groups = w.shape[1] // (4 * int(cfg[1]))
+            if groups != cfg[2]:
+                return False
+            part = None
+            if groups > 1:
+                need = groups * x.shape[0] * w.shape[0]
+                if self.part is None or self.part.numel() < need:
+                    if torch.cuda.is_current_stream_capturing():
+                        return False
+                    self.part = torch.empty(need, dtype=torch.float32, device=x.device)
+                part = self.part
+            return bool(ext().skinny_gemm(out, x, w, part, int(cfg[1]), reduce))
         mt = cfg[0] == "mt"
         if mt:
             wm, wn, mr, wnf, sk = cfg[1:6]
@@ -352,7 +370,7 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
                     lib_fn = lambda i: torch.nn.functional.linear(x, ws[i % len(ws)])  # noqa: E731
                 fns = {}
                 for cfg in candidates(M, N, K, epi):
-                    if cfg[0] not in ("mt", "pf") and M > OLD_FORMS_MAX_M:
+                    if cfg[0] not in ("mt", "pf", "sk") and M > OLD_FORMS_MAX_M:
                         continue
                     if not TABLE.run(out, x, w, cfg, epi):
                         continue

@@ -518,14 +518,19 @@ def test_decode_gemm_all_configs(gpu, M, N, K, epi):
     want = torch.nn.functional.silu(y[:, :N // 2]) * y[:, N // 2:] if epi else y
     cands = decode_gemm.candidates(M, N, K, epi)
     assert cands
-    part = torch.empty(8 * M * N, dtype=torch.float32, device=gpu)
-    assert any(c[0] != "mt" and c[4] for c in cands) or M <= 16, "LDS-form configurations are among the candidates"
+    part = torch.empty(max(decode_gemm.SPLITS) * M * N, dtype=torch.float32, device=gpu)
+    reg = [c for c in cands if isinstance(c[0], int)]
+    assert any(c[4] for c in reg) or M <= 16, "LDS-form configurations are among the candidates"
     big = N * K * 2 >= decode_gemm.MT_SMALL_M_MIN_BYTES
     assert any(c[0] == "mt" for c in cands) == (M >= decode_gemm.MT_MIN_M or (M >= 8 and big))
+    assert any(c[0] == "sk" for c in cands) == (M <= 16 and not epi and N % 16 == 0 and K % 512 == 0)
+    decode_gemm.TABLE.part = part
     for c in cands:
         out = torch.full((M, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
         if c[0] == "mt":
             assert ops.ext().mt_gemm(out, x, w, part, *c[1:6], epi, None, c[6] if len(c) > 6 else 0)
+        elif c[0] in ("sk", "pf"):
+            assert decode_gemm.TABLE.run(out, x, w, c, epi)
         else:
             assert ops.ext().decode_gemm(out, x, w, part, *c[:4], epi, c[4])
         _close(out, want, atol=2e-2, rtol=2e-2, name=f"decode gemm {M}x{N}x{K} epi{epi} cfg {c}")
@@ -1048,3 +1053,30 @@ def test_gemm_pf(gpu, M, N, K, epi):
         assert torch.equal(again, out), "stream-K sum must not depend on arrival order"
     slab, cnt, _ = ops._pf_workspace(x.device)
     assert int(cnt.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("N,K", [(1280, 8192), (8192, 1024), (8192, 3584), (3072, 2048)])
+def test_skinny_gemm(gpu, M, N, K):
+    """skinny_gemm_kernel (M <= 16, 16-column W slices x 4 k-ranges per workgroup) vs an fp32
+    reference: bf16 output (one k-group or slabs summed by the reduce kernel) and the raw fp32 slabs
+    [groups][M][N] a fused epilogue would read; Llama-3-70B TP-8 shard shapes and the 1B qkv."""
+    g = torch.Generator(device="cuda").manual_seed(M * 131 + N + K)
+    x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16, generator=g)
+    w = (torch.randn(N, K, device=gpu, generator=g) * K ** -0.5).to(torch.bfloat16)
+    w[: N // 2] *= 1.5  # asymmetric: a transposed store shows
+    want = x.float() @ w.float().t()
+    for kr in (128, 256):
+        if K % (4 * kr):
+            continue
+        groups = K // (4 * kr)
+        part = torch.full((groups * M * N,), float("nan"), dtype=torch.float32, device=gpu)
+        out = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+        assert ops.ext().skinny_gemm(out, x, w, part, kr, True)
+        _close(out, want, atol=2e-2, rtol=2e-2, name=f"skinny {M}x{N}x{K} kr{kr}")
+        if groups > 1:
+            out2 = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+            assert ops.ext().skinny_gemm(out2, x, w, part, kr, False)
+            slabs = part.view(groups, M, N).sum(0)
+            _close(slabs, want, atol=2e-2, rtol=2e-2, name=f"skinny slabs {M}x{N}x{K} kr{kr}")
+            assert torch.isnan(out2.float()).all(), "reduce=False must leave the output untouched"
