@@ -549,8 +549,10 @@ class ModelRunner:
         from ..ops import decode_gemm
         w = m.w
         # qkv feeds the rope / cache-write kernel (fusable at any TP); o / down feed the residual add +
-        # next RMSNorm (fused at TP = 1, llama.py _forward_fused): the tuner times each with its epilogue
-        fuse = getattr(m, "fuse_residual", False) and m.tp_size == 1
+        # next RMSNorm (llama.py _forward_fused: at TP = 1 the split-K slabs go into the norm kernel, at
+        # TP > 1 into the fused all-reduce + add + norm kernel): the tuner times each with its epilogue
+        from ..parallel.comm import get_tp
+        fuse = getattr(m, "fuse_residual", False) and (m.tp_size == 1 or get_tp().custom_ar is not None)
         norm = ("add_norm",) if fuse else None
         shapes = {"qkv": (w["l0.qkv"], 0, ("rope", m.nh, m.nkv, m.hd) if self.cfg.head_dim in (64, 128) else None),
                   "o": (w["l0.o"], 0, norm), "lm_head": (m.lm_head_weight(), 0)}

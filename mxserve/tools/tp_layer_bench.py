@@ -85,11 +85,17 @@ def run(buckets=(1, 8, 32, 64, 128), shared: bool = False, barrier=None, log=pri
     floor_us = bytes_layer / (HBM_TBPS * 1e12) * 1e6
     # the decode-GEMM table for these shard shapes (persisted per device like every tuned table)
     t0 = time.time()
+    # each projection priced with its epilogue, as the engine's capture-time tuning does: qkv with the
+    # rope / cache write, o / down with the residual add + norm (slab-consuming forms win there)
+    hq, hkv = LLAMA3_70B["heads"] // tp, max(1, LLAMA3_70B["kv_heads"] // tp)
+    specs = {"qkv": ("rope", hq, hkv, LLAMA3_70B["head_dim"]), "o": ("add_norm",), "gate_up": None,
+             "down": ("add_norm",)}
+    tshapes = {k: (ws[k], shapes[k][2]) + ((specs[k],) if specs[k] else ()) for k in shapes}
     if rank == 0 or not shared:
-        decode_gemm.tune({k: (ws[k], shapes[k][2]) for k in shapes}, list(buckets), dev)
+        decode_gemm.tune(tshapes, list(buckets), dev)
     barrier()
     if shared and rank != 0:  # same table on every rank (the fused epilogue's split-K choice)
-        decode_gemm.tune({k: (ws[k], shapes[k][2]) for k in shapes}, list(buckets), dev)
+        decode_gemm.tune(tshapes, list(buckets), dev)
     tune_s = time.time() - t0
     rows = []
     car = st.custom_ar
