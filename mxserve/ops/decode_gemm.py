@@ -47,8 +47,10 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
     """(mf, nf, wm, splitk, lu) configurations that tile the shape (wave row tile MF x 16 sized to M
     unless all_mf: then every MF, i.e. more row tiles re-reading the weights from L2).  lu = 0: the
     register kernel (wm waves over M); lu = 2 / 4: the LDS form (X tile shared by the workgroup's 4
-    waves through LDS, lu k-steps per group).  With mt, from M = MT_MIN_M on, also the medium-M
-    kernel's ("mt", wm, wn, wnf, splitk) configurations."""
+    waves through LDS, lu k-steps per group).  With mt (dense weights; the grouped MoE form passes
+    mt=False), from M = MT_MIN_M on, also the medium-M kernel's ("mt", wm, wn, wnf, splitk)
+    configurations, plus the persistent prefill kernel ("pf", 0) on the widest projections and the
+    skinny split-K form ("sk", kr, groups) at M <= 16."""
     out = []
     for mf in ((1, 2, 4) if all_mf else (_mf(M),)):
         out += _candidates_mf(M, N, K, epi, mf)
@@ -62,6 +64,8 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
     # the persistent 256 x 256-tile prefill kernel (gemm_pf.hip, data-parallel tiles) on the widest
     # projections only -- lm_head: 501 column tiles keep every CU busy at any batch; 154 vs 183 us at
     # M = 256 (profiles/r4/gemm_pf_at_decode_batches.jsonl), while narrow ones leave it a dozen tiles
+    if not mt:  # the grouped (MoE) form: register / LDS configurations only
+        return out
     if M >= PF_MIN_M and N % 256 == 0 and K % 64 == 0 and N >= PF_MIN_N:
         out.append(("pf", 0))
     # small batches: 16-column weight slices streamed with every load in flight (skinny_gemm_kernel)
