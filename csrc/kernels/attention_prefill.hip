@@ -293,7 +293,7 @@ __device__ __forceinline__ uint4 ld8_kv(const char* p) {
 // [T, Hq, D] q tensor and its write + re-read disappear).  A lane's chunks ks and ks + KS / 2 hold
 // dims d and d + D / 2, i.e. both halves of its rotation pairs.  q is rounded to bf16 after the
 // rotation, as the standalone rope kernel stores it.
-template <int D, int G, int EB, bool PRIO = false>
+template <int D, int G, int EB>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(D == 64 ? 4 : 1, D == 64 ? 4 : 8)))
 paged_prefill_v3_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const void* __restrict__ kv, long block_stride,
@@ -480,7 +480,6 @@ paged_prefill_v3_kernel(
       const int key = (idx / KS) * 32 + c, ks = idx % KS;
       ka[idx] = *reinterpret_cast<const uint4*>(kl + key * KROW + (((2 * ks + h) ^ kswz(key)) << 4));
     }
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);  // MFMA issue first: the co-resident wave's softmax fills the gaps
 #pragma unroll
     for (int idx = 0; idx < 2 * KS; ++idx)
       sacc[idx / KS] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ka[idx]), qf[idx % KS], sacc[idx / KS], 0, 0, 0);
@@ -491,7 +490,6 @@ paged_prefill_v3_kernel(
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if (k0 + KT - 1 > wave_min_pos) {  // tile crosses the diagonal (or the end) of some row of this wave
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -542,7 +540,6 @@ paged_prefill_v3_kernel(
         pf[kt][i >> 3][i & 7] = static_cast<__bf16>(p);
       }
     l += ps;
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -553,7 +550,6 @@ paged_prefill_v3_kernel(
           const uint4 a = *reinterpret_cast<const uint4*>(vl + dim * (KT * 2) + (((4 * kt + 2 * s2 + h) ^ vswz(dim)) << 4));
           o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), pf[kt][s2], o[dt], 0, 0, 0);
         }
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   gload(0);
@@ -597,19 +593,11 @@ void launch_paged_prefill(bf16_t* out, const bf16_t* q, const void* kv_ptr, bool
   if (q_stride <= 0) q_stride = Hq * D;
   if (version != 2 || kv_fp8 || cos_sin != nullptr || q_stride != Hq * D) {  // fp8 / fused q: the v3 path only
     dim3 grid3((max_q_len + 256 / G - 1) / (256 / G), Hkv, num_seqs), blk3(512);
-    static const bool prio = [] {
-      const char* e = getenv("MXS_PREFILL_PRIO");
-      return e != nullptr && e[0] == '1';
-    }();
     const float sc = kv_fp8 ? scale * k_scale : scale, vs = kv_fp8 ? v_scale : 1.f;
 #define MXS_PF3(DD, GG)                                                                                    \
     if (D == DD && G == GG) {                                                                              \
       if (kv_fp8)                                                                                          \
         hipLaunchKernelGGL((paged_prefill_v3_kernel<DD, GG, 1>), grid3, blk3, 0, s, out, q, kv_ptr,        \
-                           block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs, q_stride,    \
-                           qpos, cos_sin);                                                                 \
-      else if (prio && DD == 64)                                                                           \
-        hipLaunchKernelGGL((paged_prefill_v3_kernel<DD, GG, 2, true>), grid3, blk3, 0, s, out, q, kv_ptr,  \
                            block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs, q_stride,    \
                            qpos, cos_sin);                                                                 \
       else                                                                                                 \
