@@ -43,7 +43,6 @@ bool launch_splitk_rope_and_cache(bf16_t*, const float*, int, const int64_t*, co
                                   float, hipStream_t);
 bool launch_prefill_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int,
                          hipStream_t);
-bool launch_gemm_big(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, hipStream_t);
 bool launch_gemm_pf(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, float*, long, int*, int,
                     const int*, int, int, int, hipStream_t);
 int pf_plan(int, int, int, int, int, int, int*, int*, int*);
@@ -387,17 +386,6 @@ bool prefill_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::
                                   stream());
 }
 
-// K05-K08 at full prefill chunks (csrc/kernels/gemm_big.hip): epi 0 out [M, N] = x w^T; epi 1 (SwiGLU)
-// w = [gate; up] [2 I, K], out [M, I] = SiLU(x gate^T) * (x up^T).  False if the shape is unsupported.
-bool gemm_big(at::Tensor out, at::Tensor x, at::Tensor w, int64_t epi, int64_t variant) {
-  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
-  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
-  TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == (epi == 1 ? N / 2 : N), "shape mismatch");
-  if (x.stride(1) != 1 || out.stride(1) != 1 || M > (1 << 30)) return false;
-  return mxs::launch_gemm_big(bf(out), bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), epi, variant, stream());
-}
-
 // K05-K08 at prefill chunks (csrc/kernels/gemm_pf.hip, persistent stream-K): epi 0 out [M, N] =
 // x w^T; epi 1 (SwiGLU) w = [gate; up] [2 I, K], out [M, I].  slab: fp32 stream-K workspace, cnt:
 // int32 tile counters (zero; every launch leaves them zero).  False if the shape is unsupported.
@@ -545,8 +533,6 @@ PYBIND11_MODULE(_C, m) {
     mxs::pf_plan(M, N, K, epi, num_cu, min_iters, &dp, &sk, &g);
     return std::make_tuple(g, dp, sk);
   });
-  m.def("gemm_big", &gemm_big, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("epi"),
-        pybind11::arg("variant") = 1);
   m.def("moe_decode_gemm", &moe_decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("offs"), pybind11::arg("part"), pybind11::arg("rows_max"), pybind11::arg("mf"),
         pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"), pybind11::arg("epi"),

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""gemm_big (csrc/kernels/gemm_big.hip) vs hipBLASLt (torch F.linear) at the Llama-3.2-1B prefill
-projections, random operands, interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).
-gate_up compares the fused SwiGLU kernel with hipBLASLt + the SiLU*mul kernel.  JSON lines."""
+"""gemm_pf (csrc/kernels/gemm_pf.hip) at several stream-K segment lengths (GB_PF) vs hipBLASLt (torch
+F.linear) at the Llama-3.2-1B projections (GB_SHAPES), random operands, interleaved rounds in one
+process (cdna_hip_programming.md §5.4 rule 24).  gate_up compares the fused SwiGLU epilogue with
+hipBLASLt + the SiLU*mul kernel.  JSON lines.  (The earlier gemm_big kernel and its ping-pong variants
+that led to gemm_pf were removed in round 4; profiles/r4/gemm_pingpong_v6_vs_hipblaslt.jsonl.)"""
 import json
 import os
 import sys
@@ -27,7 +29,6 @@ def timed(fn, iters=20):
 def main():
     from mxserve import ops
     dev = torch.device("cuda:0")
-    ext = ops.ext()
     out = []
     shapes = {"qkv": (3072, 2048), "o": (2048, 2048), "gate_up": (16384, 2048), "down": (2048, 8192),
               "lm_head": (128256, 2048)}
@@ -46,16 +47,11 @@ def main():
             ref = lib()
             fl = 2 * M * N * K
             row = {"proj": name, "M": M, "N": N, "K": K, "fused_swiglu": swiglu}
-            variants = [int(v) for v in os.environ.get("GB_VARIANTS", "0,1,2").split(",") if v]
             fns = {"hipblaslt": lib}
-            for mi in [int(v) for v in os.environ.get("GB_PF", "").split(",") if v]:
+            for mi in [int(v) for v in os.environ.get("GB_PF", "0,16").split(",") if v]:
                 fns[f"pf{mi}"] = (lambda mi=mi: ops.gemm_pf(x, w, 1 if swiglu else 0, y, mi))
                 assert fns[f"pf{mi}"]() is not None
                 row[f"pf{mi}_rel_err"] = round(float((y.float() - ref.float()).abs().max() / ref.float().abs().max()), 5)
-            for v in variants:
-                fns[f"v{v}"] = (lambda v=v: ext.gemm_big(y, x, w, 1 if swiglu else 0, v))
-                assert fns[f"v{v}"]()
-                row[f"v{v}_rel_err"] = round(float((y.float() - ref.float()).abs().max() / ref.float().abs().max()), 5)
             ts = {k: [] for k in fns}
             for _ in range(3):
                 for k, fn in fns.items():
@@ -66,7 +62,7 @@ def main():
             out.append(row)
             print(json.dumps(row), flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
-    with open("gpurun_out/gemm_big_probe.jsonl", "w") as f:
+    with open("gpurun_out/gemm_probe.jsonl", "w") as f:
         for r in out:
             f.write(json.dumps(r) + "\n")
 

@@ -811,43 +811,6 @@ def test_prefill_gemm_all_configs(gpu, M, N, K):
         _close(out, want, atol=2e-2, rtol=2e-2, name=f"prefill gemm {M}x{N}x{K} cfg {cfg}")
 
 
-@pytest.mark.parametrize("M,N,K", [(1, 256, 64), (300, 3072, 2048), (4133, 2048, 2048), (8192, 2048, 8192),
-                                   (257, 512, 192)])
-def test_gemm_big(gpu, M, N, K):
-    """Full-chunk prefill GEMM (csrc/kernels/gemm_big.hip) vs an fp32 reference, row counts that are
-    not tile multiples included, with an asymmetric W so a transposed store cannot pass."""
-    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
-    w = ((torch.rand(N, K, device=gpu) * 2 - 1) * K ** -0.5).to(torch.bfloat16)
-    w[:, 0] += torch.arange(N, device=gpu, dtype=torch.bfloat16) * 1e-3
-    for variant in (0, 6, 7):
-        out = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
-        assert ops.ext().gemm_big(out, x, w, 0, variant)
-        _close(out, x.float() @ w.float().t(), atol=2e-2, rtol=2e-2, name=f"gemm_big v{variant} {M}x{N}x{K}")
-
-
-@pytest.mark.parametrize("M,I,K", [(1, 128, 64), (777, 1024, 2048), (4096, 8192, 2048)])
-def test_gemm_big_swiglu(gpu, M, I, K):
-    """gate_up with SiLU(gate) * up in the epilogue (W rows [gate; up], gathered per tile by the DMA
-    addresses) vs fp32 SiLU(x gate^T) * (x up^T)."""
-    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
-    w = ((torch.rand(2 * I, K, device=gpu) * 2 - 1) * 2 * K ** -0.5).to(torch.bfloat16)
-    gu = x.float() @ w.float().t()
-    want = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
-    for variant in (0, 6, 7):
-        out = torch.full((M, I), float("nan"), device=gpu, dtype=torch.bfloat16)
-        assert ops.ext().gemm_big(out, x, w, 1, variant)
-        _close(out, want, atol=2e-2, rtol=2e-2, name=f"gemm_big v{variant} swiglu {M}x{I}x{K}")
-
-
-def test_gemm_big_rejects_unsupported(gpu):
-    x = torch.randn(64, 2048, device=gpu, dtype=torch.bfloat16)
-    w = torch.randn(3000, 2048, device=gpu, dtype=torch.bfloat16)  # N not a multiple of 256
-    assert not ops.ext().gemm_big(torch.empty(64, 3000, device=gpu, dtype=torch.bfloat16), x, w, 0)
-    w = torch.randn(256, 2000, device=gpu, dtype=torch.bfloat16)  # K not a multiple of 64
-    assert not ops.ext().gemm_big(torch.empty(64, 256, device=gpu, dtype=torch.bfloat16),
-                                  torch.randn(64, 2000, device=gpu, dtype=torch.bfloat16), w, 0)
-
-
 def test_prefill_gemm_tuner_and_dispatch(gpu, monkeypatch):
     """Startup tuner for small prefill chunks: hipBLASLt vs the tile kernel per M bucket, and
     ops.linear follows the table (the kernel runs when it was chosen) with correct results."""
