@@ -863,9 +863,13 @@ def phase_agg(a, ctx) -> tuple:
                                "from_table": sum(r.get("source") == "table" for r in rep)}
     rep = getattr(eng.runner, "prefill_pf_report", None)
     if rep:  # start-up choice per (projection, row bucket): stream-K MFMA GEMM vs hipBLASLt
-        info["prefill_gemm"] = {"buckets": len(rep), "gemm_pf": sum(r["chosen"] != "hipblaslt" for r in rep),
-                                "by_proj": {p: sum(r["chosen"] != "hipblaslt" for r in rep if r["proj"] == p)
-                                            for p in sorted({r["proj"] for r in rep})},
+        pf = [r for r in rep if "code" not in r]
+        fu = [r for r in rep if "code" in r]  # fused chain (llama.py _forward_pf): gemm_pf forms kept
+        info["prefill_gemm"] = {"buckets": len(pf), "gemm_pf": sum(r["chosen"] != "hipblaslt" for r in pf),
+                                "by_proj": {p: sum(r["chosen"] != "hipblaslt" for r in pf if r["proj"] == p)
+                                            for p in sorted({r["proj"] for r in pf})},
+                                "fused": {p: sum(r["chosen"].startswith("gemm_pf") for r in fu if r["proj"] == p)
+                                          for p in sorted({r["proj"] for r in fu})},
                                 "from_table": sum(r.get("source") == "table" for r in rep)}
     la = getattr(eng, "_late", None)
     if la is not None:  # engine/pacing.py: how often the host waited for a late admission, and how long

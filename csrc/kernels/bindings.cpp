@@ -44,7 +44,7 @@ bool launch_splitk_rope_and_cache(bf16_t*, const float*, int, const int64_t*, co
 bool launch_prefill_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int,
                          hipStream_t);
 bool launch_gemm_pf(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, float*, long, int*, int,
-                    const int*, int, int, int, hipStream_t);
+                    const int*, int, int, int, hipStream_t, const bf16_t*, int, bool, float);
 int pf_plan(int, int, int, int, int, int, int*, int*, int*);
 bool launch_moe_grouped_gemm(bf16_t*, const bf16_t*, const bf16_t*, const int*, int, int, int, int, int, bool,
                              int, float*, hipStream_t);
@@ -387,10 +387,13 @@ bool prefill_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::
 }
 
 // K05-K08 at prefill chunks (csrc/kernels/gemm_pf.hip, persistent stream-K): epi 0 out [M, N] =
-// x w^T; epi 1 (SwiGLU) w = [gate; up] [2 I, K], out [M, I].  slab: fp32 stream-K workspace, cnt:
-// int32 tile counters (zero; every launch leaves them zero).  False if the shape is unsupported.
+// x w^T; epi 1 (SwiGLU) w = [gate; up] [2 I, K], out [M, I]; epi 2 out = resid + x w^T (resid may be
+// out).  row_scale (epi 0 / 1): rows scaled by rsqrt(mean(x^2) + eps) (fused RMSNorm, the norm weight
+// folded into w).  slab: fp32 stream-K workspace, cnt: int32 tile counters (zero; every launch leaves
+// them zero).  False if the shape is unsupported.
 bool gemm_pf(at::Tensor out, at::Tensor x, at::Tensor w, int64_t epi, at::Tensor slab, at::Tensor cnt,
-             at::Tensor tile_map, int64_t num_cu, int64_t min_iters) {
+             at::Tensor tile_map, int64_t num_cu, int64_t min_iters, c10::optional<at::Tensor> resid,
+             bool row_scale, double eps) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
   const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
@@ -399,9 +402,20 @@ bool gemm_pf(at::Tensor out, at::Tensor x, at::Tensor w, int64_t epi, at::Tensor
   TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && cnt.is_contiguous(), "cnt: int32 CUDA");
   TORCH_CHECK(tile_map.is_cuda() && tile_map.scalar_type() == at::kInt && tile_map.is_contiguous(), "tile_map");
   if (x.stride(1) != 1 || out.stride(1) != 1 || M > (1 << 24)) return false;
+  const bf16_t* R = nullptr;
+  int ldr = 0;
+  if (epi == 2) {
+    TORCH_CHECK(resid.has_value(), "epi 2 needs resid");
+    CHECK_BF16((*resid));
+    TORCH_CHECK(resid->dim() == 2 && resid->size(0) == M && resid->size(1) == N && resid->stride(1) == 1,
+                "resid shape");
+    R = bf(*resid);
+    ldr = static_cast<int>(resid->stride(0));
+  }
   return mxs::launch_gemm_pf(bf(out), bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), epi, slab.data_ptr<float>(),
                              slab.numel(), cnt.data_ptr<int>(), cnt.numel(), tile_map.data_ptr<int>(),
-                             tile_map.numel(), num_cu, min_iters, stream());
+                             tile_map.numel(), num_cu, min_iters, stream(), R, ldr, row_scale,
+                             static_cast<float>(eps));
 }
 
 // Grouped decode form of decode_gemm (K16 at decode batches): w [E, N, K], x = routed rows sorted by
@@ -527,7 +541,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("part"), pybind11::arg("bm"), pybind11::arg("splitk"));
   m.def("gemm_pf", &gemm_pf, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("epi"),
         pybind11::arg("slab"), pybind11::arg("cnt"), pybind11::arg("tile_map"), pybind11::arg("num_cu"),
-        pybind11::arg("min_iters") = 16);
+        pybind11::arg("min_iters") = 16, pybind11::arg("resid") = pybind11::none(),
+        pybind11::arg("row_scale") = false, pybind11::arg("eps") = 1e-5);
   m.def("gemm_pf_plan", [](int M, int N, int K, int epi, int num_cu, int min_iters) {
     int dp = 0, sk = 0, g = 0;
     mxs::pf_plan(M, N, K, epi, num_cu, min_iters, &dp, &sk, &g);

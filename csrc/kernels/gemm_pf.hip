@@ -32,6 +32,16 @@
 //
 // EPI_NONE: Y = acc.  EPI_SWIGLU: W = [gate; up] [2 I, K]; a tile's image interleaves 16 gate and the
 // 16 matching up rows per fragment pair (the DMA addresses gather them), Y [M, I] = SiLU(g) * u.
+// EPI_RESID: Y = R + acc (R may be Y: the residual stream updated in place by o_proj / down_proj).
+//
+// RS (row scale, the consumer half of a fused RMSNorm): X is the un-normalised residual stream and
+// W's columns carry the norm weight (W' = W diag(g), folded at load), so RMSNorm(x) W^T = rstd(x) *
+// (x W'^T) with rstd(x) = rsqrt(mean(x^2) + eps) over the K = hidden columns the tile streams
+// anyway.  Every wave sums x^2 of its X fragments as they pass through its registers (v_dot2 of a
+// bf16 pair with itself: 16 VALU per phase beside 32 MFMAs), the 4 k-quarter lanes of a row are
+// combined in the epilogue and the accumulators scaled before the SwiGLU / store.  The separate
+// normalisation pass over [M, hidden] (read + write) disappears; partial sums of stream-K segments
+// travel in the slab with the accumulators.
 #include <algorithm>
 #include <type_traits>
 
@@ -41,10 +51,13 @@ namespace mxs {
 
 typedef __bf16 pf_bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int pf_u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 pf_bf16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int PF_SC1 = 16;  // buffer cache-policy bits: sc1 (CPol::SC1 = SCC): write-through / L2-coherent
 constexpr int PF_EPI_NONE = 0;
 constexpr int PF_EPI_SWIGLU = 1;
+constexpr int PF_EPI_RESID = 2;
+constexpr int PF_SLAB_FRAGS = 34;  // 32 accumulator fragments + 2 float4 of RS row sums per thread
 
 __device__ __forceinline__ pf_bf16x8 pf_frag(const pf_u32x4& v) { return __builtin_bit_cast(pf_bf16x8, v); }
 __device__ __forceinline__ float pf_silu(float g) { return g / (1.f + __expf(-g)); }
@@ -58,6 +71,9 @@ struct PfArgs {
   const int* tile_map;  // logical tile -> token tile | weight tile << 16 (pf_tile_map)
   int M, K, ldx, ldy, inter, ntm, ntn, nk;
   int nrows_w;  // rows of W
+  const bf16_t* R;  // EPI_RESID: residual rows (ldr), may equal Y
+  int ldr;
+  float inv_k, eps;  // RS: 1 / K, RMSNorm epsilon
   int dp_rounds;  // full data-parallel rounds of tiles
   int sk_tiles;   // tiles after them, split over the grid by k-iterations
 };
@@ -68,7 +84,7 @@ struct PfSeg {
   int c, L, k0, k1, tm, tn;
 };
 
-template <int EPI>
+template <int EPI, bool RS>
 __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
   constexpr int HT = 16384, QT = 8192, KT = 4 * HT, XB = 2 * HT;  // W halves at 0 / HT, X halves at XB
   __shared__ __attribute__((aligned(16))) char smem[2 * KT + 16];
@@ -176,6 +192,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
   for (int f = 0; f < 4; ++f)
 #pragma unroll
     for (int t = 0; t < 8; ++t) acc[f][t] = float4_{0.f, 0.f, 0.f, 0.f};
+  float ssq[8];  // RS: sum of x^2 over this lane's k-quarter of token rows 128 wr + 16 t + r16
+#pragma unroll
+  for (int t = 0; t < 8; ++t) ssq[t] = 0.f;
 
   const int r16 = lane & 15, kq = lane >> 4;
   // fragment addresses: one VGPR base per (operand, k-step); fragments f / t of a wave sit 2048 bytes
@@ -214,6 +233,17 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
         for (int t = 0; t < 4; ++t)
           acc[f][4 * hb + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf_frag(wa[f][kk]), pf_frag(xb[t][kk]),
                                                                         acc[f][4 * hb + t], 0, 0, 0);
+    if constexpr (RS) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const pf_bf16x2 v = __builtin_bit_cast(pf_bf16x2, xb[t][kk][d]);
+            ssq[4 * hb + t] = __builtin_amdgcn_fdot2_f32_bf16(v, v, ssq[4 * hb + t], false);
+          }
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -221,11 +251,38 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
   // r16][image column 64 wc + 16 f + 4 kq + e]
   auto epilogue = [&](int tm, int tn) {
     const int m0 = tm * 256;
+    if constexpr (RS) {  // the 4 k-quarter lanes of each row: full-row sums -> rstd, applied to acc
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        float v = ssq[t];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        const float r = rsqrtf(v * a.inv_k + a.eps);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) acc[f][t] *= r;
+      }
+    }
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const int m = m0 + 128 * wr + 16 * t + r16;
       if (m >= a.M) continue;
       bf16_t* yr = a.Y + static_cast<size_t>(m) * a.ldy;
+      if constexpr (EPI == PF_EPI_RESID) {
+        const bf16_t* rr = a.R + static_cast<size_t>(m) * a.ldr;
+        uint2 rv[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) rv[f] = *reinterpret_cast<const uint2*>(rr + tn * 256 + 64 * wc + 16 * f + 4 * kq);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const float4_& v = acc[f][t];
+          const int n = tn * 256 + 64 * wc + 16 * f + 4 * kq;
+          uint2 ov;
+          ov.x = pack2(v[0] + bf2f_lo(rv[f].x), v[1] + bf2f_hi(rv[f].x));
+          ov.y = pack2(v[2] + bf2f_lo(rv[f].y), v[3] + bf2f_hi(rv[f].y));
+          *reinterpret_cast<uint2*>(yr + n) = ov;
+        }
+        continue;
+      }
       if constexpr (EPI == PF_EPI_SWIGLU) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
@@ -255,11 +312,15 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
     for (int f = 0; f < 4; ++f)
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[f][t] = float4_{0.f, 0.f, 0.f, 0.f};
+    if constexpr (RS) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) ssq[t] = 0.f;
+    }
   };
   // stream-K bookkeeping: first SK iteration of order q, owner of SK iteration i
   auto sk_start = [&](int q) -> int { return q * I / G; };
   auto sk_owner = [&](int i) -> int { return ((i + 1) * G + I - 1) / I - 1; };
-  constexpr int SLAB = 32 * 512 * 4;  // floats per segment slab
+  constexpr int SLAB = PF_SLAB_FRAGS * 512 * 4;  // floats per segment slab
 
 #define PF_BAR()                           \
   do {                                     \
@@ -381,6 +442,13 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
         for (int t = 0; t < 8; ++t)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pf_u32x4, acc[f][t]), ms, tid * 16,
                                                  (f * 8 + t) * 8192, PF_SC1);
+      if constexpr (RS) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(pf_u32x4, float4_{ssq[4 * h], ssq[4 * h + 1], ssq[4 * h + 2], ssq[4 * h + 3]}), ms,
+              tid * 16, (32 + h) * 8192, PF_SC1);
+      }
       // hand-off without agent-scope fences (MI355X_MICROARCH.md "Valid forms", first table row):
       // write-through (sc1) 16-byte slab stores, every storing wave drained before the barrier, one
       // lane's agent-scope ticket; the last arriver reads every slab with sc1 loads.  A release fence
@@ -410,6 +478,15 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
               acc[f][t] += __builtin_bit_cast(float4_, __builtin_amdgcn_raw_buffer_load_b128(
                                                            ss, tid * 16, (f * 8 + t) * 8192, PF_SC1));
             __builtin_amdgcn_sched_barrier(0);
+          }
+          if constexpr (RS) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const float4_ v = __builtin_bit_cast(
+                  float4_, __builtin_amdgcn_raw_buffer_load_b128(ss, tid * 16, (32 + h) * 8192, PF_SC1));
+#pragma unroll
+              for (int e = 0; e < 4; ++e) ssq[4 * h + e] += v[e];
+            }
           }
         }
       }
@@ -457,18 +534,23 @@ int pf_plan(int M, int N, int K, int epi, int num_cu, int min_iters, int* dp_rou
 }
 
 // epi 0: Y [M, N] = X W^T (N % 256 == 0).  epi 1 (SwiGLU): W = [gate; up] rows [2 I, K], Y [M, I]
-// (I % 128 == 0).  K % 64 == 0, 16-byte aligned rows.  slab: >= 2 * grid * 32 * 512 * 4 floats; cnt:
+// (I % 128 == 0).  epi 2: Y = R + X W^T.  row_scale (epi 0 / 1): rows scaled by rsqrt(mean(x^2) + eps).  K % 64 == 0, 16-byte aligned rows.  slab: >= 2 * grid * 32 * 512 * 4 floats; cnt:
 // >= sk_tiles ints, zero (left zero by every launch).  False when the shape is not supported.
 bool launch_gemm_pf(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx, int ldy, int epi,
                     float* slab, long slab_floats, int* cnt, int cnt_len, const int* tile_map, int map_len,
-                    int num_cu, int min_iters, hipStream_t s) {
-  if (M <= 0 || K % 64 != 0 || ldx % 8 != 0 || ldy % 4 != 0 || (epi != PF_EPI_NONE && epi != PF_EPI_SWIGLU)) return false;
+                    int num_cu, int min_iters, hipStream_t s, const bf16_t* R, int ldr, bool row_scale,
+                    float eps) {
+  if (M <= 0 || K % 64 != 0 || ldx % 8 != 0 || ldy % 4 != 0) return false;
+  if (epi != PF_EPI_NONE && epi != PF_EPI_SWIGLU && epi != PF_EPI_RESID) return false;
+  if (epi == PF_EPI_RESID && (R == nullptr || ldr % 4 != 0 || (reinterpret_cast<uintptr_t>(R) & 7) || row_scale))
+    return false;
   if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W)) & 15) return false;
   if (reinterpret_cast<uintptr_t>(Y) & 7) return false;
   if (N % 256 != 0) return false;  // SwiGLU: N = 2 I with I % 128 == 0
   int dp, sk, G;
   if (!pf_plan(M, N, K, epi, num_cu, min_iters, &dp, &sk, &G)) return false;
-  if (sk > 0 && (slab == nullptr || cnt == nullptr || cnt_len < sk || slab_floats < 2L * G * 32 * 512 * 4)) return false;
+  if (sk > 0 && (slab == nullptr || cnt == nullptr || cnt_len < sk || slab_floats < 2L * G * PF_SLAB_FRAGS * 512 * 4))
+    return false;
   if (tile_map == nullptr || map_len < ((M + 255) / 256) * (N / 256)) return false;
   if (static_cast<long>(M) * ldx * 2 > 0x7FFFFFFFL) return false;  // X rows addressed by 32-bit buffer offsets
   PfArgs a;
@@ -489,8 +571,20 @@ bool launch_gemm_pf(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, i
   a.nk = K / 64;
   a.dp_rounds = dp;
   a.sk_tiles = sk;
-  if (epi == PF_EPI_SWIGLU) hipLaunchKernelGGL(gemm_pf_kernel<PF_EPI_SWIGLU>, dim3(G), dim3(512), 0, s, a);
-  else hipLaunchKernelGGL(gemm_pf_kernel<PF_EPI_NONE>, dim3(G), dim3(512), 0, s, a);
+  a.R = R;
+  a.ldr = ldr;
+  a.inv_k = 1.f / static_cast<float>(K);
+  a.eps = eps;
+  const dim3 g(G), b(512);
+  if (epi == PF_EPI_SWIGLU) {
+    if (row_scale) hipLaunchKernelGGL((gemm_pf_kernel<PF_EPI_SWIGLU, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((gemm_pf_kernel<PF_EPI_SWIGLU, false>), g, b, 0, s, a);
+  } else if (epi == PF_EPI_RESID) {
+    hipLaunchKernelGGL((gemm_pf_kernel<PF_EPI_RESID, false>), g, b, 0, s, a);
+  } else {
+    if (row_scale) hipLaunchKernelGGL((gemm_pf_kernel<PF_EPI_NONE, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((gemm_pf_kernel<PF_EPI_NONE, false>), g, b, 0, s, a);
+  }
   MXS_CHECK_LAUNCH();
   return true;
 }

@@ -215,12 +215,159 @@ __global__ void __launch_bounds__(256) rope_cache_t16_kernel(
   }
 }
 
+// Prefill K / V-only form (q is rotated inside the attention kernels, llama.py _fused_q_rope): 16
+// tokens per workgroup, and every global load of the tile is in flight before the first is used.
+// rope_cache_t16_kernel walks 8-byte items in a loop whose every trip chains a positions load, a
+// cos/sin load and the stores (37.6 us per 6144-token call in the headline run, ~10x its HBM time:
+// profiles/r4/bench_q48_kernel_stats.csv).  Here a thread owns NI 8-pair chunks of K (16-byte
+// loads of both halves, 2 x 32-byte cos/sin) and NV 16-byte pieces of the V rows, all issued up
+// front; the slot / position loads are the only dependent round trip.  Loads index with clamped
+// (always valid) addresses instead of predicates, so no load is branched around
+// (cdna_hip_programming.md §5 trap (c)); only the stores are predicated.
+__device__ __forceinline__ void kv_store8(bf16_t* p, const float* x, float) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(pack2(x[0], x[1]), pack2(x[2], x[3]), pack2(x[4], x[5]), pack2(x[6], x[7]));
+}
+__device__ __forceinline__ void kv_store8(fp8_t* p, const float* x, float inv) {
+  uint32_t w[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v |= static_cast<uint32_t>(static_cast<uint8_t>(f2fp8(x[4 * h + e] * inv))) << (8 * e);
+    w[h] = v;
+  }
+  *reinterpret_cast<uint2*>(p) = make_uint2(w[0], w[1]);
+}
+
+// MXS_KV_T16_LEGACY=1: the older rope_cache_t16_kernel for this case (A/B probes)
+static bool kv_t16_legacy() {
+  static const bool v = [] {
+    const char* e = getenv("MXS_KV_T16_LEGACY");
+    return e != nullptr && e[0] == '1';
+  }();
+  return v;
+}
+
+template <int D, typename KT, int NI, int NV>
+__global__ void __launch_bounds__(256) kv_rope_t16_kernel(
+    const bf16_t* __restrict__ qkv, const int64_t* __restrict__ positions, const float* __restrict__ cos_sin,
+    KT* __restrict__ kv, long block_stride, const int64_t* __restrict__ slot_mapping, int Hq, int Hkv, int BS, int T,
+    float k_inv_scale, float v_inv_scale) {
+  constexpr int HALF = D / 2, CH = HALF / 8, TPB = 16;
+  extern __shared__ __attribute__((aligned(16))) bf16_t vstage[];  // [TPB][Hkv * D]
+  __shared__ int s_fast;
+  const int t0 = blockIdx.x * TPB, nt = min(TPB, T - t0), tid = threadIdx.x;
+  const int row_stride = (Hq + 2 * Hkv) * D, hkd = Hkv * D;
+  const int n_k = nt * Hkv * CH, n_v = nt * (hkd / 8);
+  const bf16_t* tile = qkv + static_cast<size_t>(t0) * row_stride;
+  // V rows into registers (independent of everything else)
+  uint4 vr[NV];
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int i = min(tid + 256 * u, n_v - 1), tt = i / (hkd / 8), j = (i - tt * (hkd / 8)) * 8;
+    vr[u] = *reinterpret_cast<const uint4*>(tile + static_cast<size_t>(tt) * row_stride + (Hq + Hkv) * D + j);
+  }
+  // K chunks: both halves of 8 pairs, and the token's position / slot
+  uint4 ka[NI], kb[NI];
+  int64_t pos[NI], slot[NI];
+#pragma unroll
+  for (int u = 0; u < NI; ++u) {
+    const int i = min(tid + 256 * u, n_k - 1), tt = i / (Hkv * CH), r = i - tt * (Hkv * CH), h = r / CH,
+              c = r - h * CH;
+    const bf16_t* src = tile + static_cast<size_t>(tt) * row_stride + (Hq + h) * D + 8 * c;
+    ka[u] = *reinterpret_cast<const uint4*>(src);
+    kb[u] = *reinterpret_cast<const uint4*>(src + HALF);
+    pos[u] = positions[t0 + tt];
+    slot[u] = slot_mapping[t0 + tt];
+  }
+  if (tid < 64) {  // wave 0: does the tile fill one run of a block's slots?
+    const int64_t sk = tid < nt ? slot_mapping[t0 + tid] : 0;
+    const int64_t s0 = __shfl(sk, 0, 64);
+    const bool all_ok = __all(tid >= nt || sk == s0 + tid);
+    if (tid == 0) s_fast = all_ok && s0 >= 0 && (s0 % BS) + nt <= BS;
+  }
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int i = tid + 256 * u;
+    if (i < n_v) {
+      const int tt = i / (hkd / 8), j = (i - tt * (hkd / 8)) * 8;
+      *reinterpret_cast<uint4*>(vstage + tt * hkd + j) = vr[u];
+    }
+  }
+  // rotate and store K
+#pragma unroll
+  for (int u = 0; u < NI; ++u) {
+    const int i = tid + 256 * u, r = i % (Hkv * CH), h = r / CH, c = r - h * CH;
+    const float* cs = cos_sin + pos[u] * D + 8 * c;
+    const float4 c0 = *reinterpret_cast<const float4*>(cs), c1 = *reinterpret_cast<const float4*>(cs + 4);
+    const float4 s0 = *reinterpret_cast<const float4*>(cs + HALF), s1 = *reinterpret_cast<const float4*>(cs + HALF + 4);
+    const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const uint32_t xa[4] = {ka[u].x, ka[u].y, ka[u].z, ka[u].w}, xb[4] = {kb[u].x, kb[u].y, kb[u].z, kb[u].w};
+    float o1[8], o2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x1 = (e & 1) ? bf2f_hi(xa[e >> 1]) : bf2f_lo(xa[e >> 1]);
+      const float x2 = (e & 1) ? bf2f_hi(xb[e >> 1]) : bf2f_lo(xb[e >> 1]);
+      o1[e] = x1 * cc[e] - x2 * sn[e];
+      o2[e] = x2 * cc[e] + x1 * sn[e];
+    }
+    if (i < n_k && slot[u] >= 0) {
+      KT* kd = kv + (slot[u] / BS) * block_stride + (static_cast<size_t>(h) * BS + slot[u] % BS) * D + 8 * c;
+      kv_store8(kd, o1, k_inv_scale);
+      kv_store8(kd + HALF, o2, k_inv_scale);
+    }
+  }
+  __syncthreads();
+  if (!s_fast) {  // tokens of different blocks (or unmapped): one store per (token, dim)
+    for (int i = tid; i < nt * hkd; i += blockDim.x) {
+      const int tt = i / hkd, j = i - tt * hkd;
+      const int64_t sl = slot_mapping[t0 + tt];
+      if (sl < 0) continue;
+      KT* dst = kv + (sl / BS) * block_stride + static_cast<size_t>(Hkv) * BS * D + static_cast<size_t>(j) * BS + sl % BS;
+      kv_store(dst, bf2f(vstage[tt * hkd + j]), v_inv_scale);
+    }
+    return;
+  }
+  const int64_t sl0 = slot_mapping[t0];
+  const int off0 = static_cast<int>(sl0 % BS);
+  KT* vblk = kv + (sl0 / BS) * block_stride + static_cast<size_t>(Hkv) * BS * D;
+  for (int j = tid; j < hkd; j += blockDim.x) {
+    KT* dst = vblk + static_cast<size_t>(j) * BS + off0;
+    if (nt == TPB && off0 == 0 && BS == TPB) {  // a whole row of the block: 16 tokens
+      float x[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) x[k] = bf2f(vstage[k * hkd + j]);
+      kv_store8(dst, x, v_inv_scale);
+      kv_store8(dst + 8, x + 8, v_inv_scale);
+      continue;
+    }
+    for (int tt = 0; tt < nt; ++tt) kv_store(dst + tt, bf2f(vstage[tt * hkd + j]), v_inv_scale);
+  }
+}
+
 template <typename KT>
 static void launch_rope_typed(bf16_t* q_out, const bf16_t* qkv, const int64_t* positions, const float* cos_sin,
                               KT* kv, long block_stride, const int64_t* slot_mapping, const bf16_t* qn,
                               const bf16_t* kn, int T, int Hq, int Hkv, int D, int BS, float eps, float kis, float vis,
                               hipStream_t s) {
   const bool norm = qn != nullptr;
+  if (!norm && q_out == nullptr && T >= 512 && (D == 64 || D == 128) && Hkv * D <= 1024 && !kv_t16_legacy()) {
+    const dim3 g16((T + 15) / 16), b16(256);
+    const size_t lds = static_cast<size_t>(16) * Hkv * D * sizeof(bf16_t);
+    const bool small = Hkv * D <= 512;
+#define MXS_KV16(DD, NI, NV)                                                                                    \
+  hipLaunchKernelGGL((kv_rope_t16_kernel<DD, KT, NI, NV>), g16, b16, lds, s, qkv, positions, cos_sin, kv,       \
+                     block_stride, slot_mapping, Hq, Hkv, BS, T, kis, vis)
+    if (D == 64) {
+      if (small) MXS_KV16(64, 2, 4); else MXS_KV16(64, 4, 8);
+    } else {
+      if (small) MXS_KV16(128, 2, 4); else MXS_KV16(128, 4, 8);
+    }
+#undef MXS_KV16
+    MXS_CHECK_LAUNCH();
+    return;
+  }
   if (!norm && T >= 512 && D % 8 == 0 && (D == 64 || D == 128) && Hkv * D * 16 * 2 <= 64 * 1024) {
     const dim3 g16((T + 15) / 16), b16(256);
     const size_t lds = static_cast<size_t>(16) * Hkv * D * sizeof(bf16_t);

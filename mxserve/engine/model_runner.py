@@ -120,6 +120,8 @@ class ModelRunner:
         self.kv_dtype = torch.uint8 if self.kv_fp8 else self.dtype
         if self.kv_fp8 and "MXS_KV_SCALE" not in os.environ:
             self.model.calibrate_kv_scales(self.bs)
+        # norm-folded weights of the fused prefill chain: allocated before the KV pool is sized
+        self.model.prepare_fused_prefill()
         self.num_blocks = self._determine_num_blocks()
         m = self.model
         self.kv_cache = torch.zeros(self.num_blocks, cfg.num_layers, 2, m.nkv, self.bs, cfg.head_dim,
@@ -573,6 +575,13 @@ class ModelRunner:
             pf_w = {k: (v[0], v[1]) for k, v in shapes.items() if k != "lm_head"}
             self.prefill_pf_report = prefill_pf.tune(pf_w, self.args.max_num_batched_tokens + self.args.max_num_seqs,
                                                      self.device, self.dtype)
+            if m.wf:  # the fused prefill chain (llama.py _forward_pf): each fused form vs its unfused one
+                fw = {"qkv": (w["l0.qkv"], m.wf["l0.qkv"], prefill_pf.CODE_RS),
+                      "gate_up": (w["l0.gate_up"], m.wf["l0.gate_up"], prefill_pf.CODE_RS_SWIGLU),
+                      "o": (w["l0.o"], None, prefill_pf.CODE_RESID), "down": (w["l0.down"], None, prefill_pf.CODE_RESID)}
+                self.prefill_pf_report = self.prefill_pf_report + prefill_pf.tune_fused(
+                    fw, self.args.max_num_batched_tokens + self.args.max_num_seqs, self.device, self.dtype,
+                    self.cfg.rms_norm_eps)
             if self.cfg.is_moe and "l0.w13" in w:  # expert GEMMs at decode batches (local experts)
                 from ..ops import moe as moe_ops
                 self.moe_gemm_report = moe_ops.tune(w["l0.w13"], w["l0.w2"], buckets, self.cfg.num_experts_per_tok,

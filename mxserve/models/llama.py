@@ -69,6 +69,10 @@ class TransformerLM:
         # TP = 1 on the GPU: o_proj / down_proj end in the next RMSNorm (ops.linear_add_rms_norm: a
         # split-K projection's slabs go straight into one sum + residual add + norm kernel)
         self.fuse_residual = os.environ.get("MXS_FUSE_RESIDUAL", "1") == "1"
+        # TP = 1 dense models on the GPU, prefill / mixed steps: RMSNorms inside the consumer GEMMs and
+        # residual adds inside the producers (_forward_pf); self.wf holds the norm-folded weights
+        self.fuse_prefill = os.environ.get("MXS_PF_FUSED", "1") == "1"
+        self.wf: dict[str, torch.Tensor] = {}
         # fp8 KV cache: stored = x / scale, per layer (1.0 until the runner calibrates them from a
         # probe prefill, mxserve/engine/model_runner.py::_calibrate_kv_scales; MXS_KV_SCALE fixes all)
         ks = float(os.environ.get("MXS_KV_SCALE", "1.0"))
@@ -164,6 +168,22 @@ class TransformerLM:
             out.pop("lm_head", None)
         self.w = out
 
+    def prepare_fused_prefill(self) -> bool:
+        """Norm-folded copies of the qkv / gate_up weights (W diag(g), ops.fold_norm_weight) for the
+        prefill forward whose RMSNorms run inside the consumer GEMMs (_forward_pf).  TP = 1 dense
+        models on the GPU.  Call after the weights are final and before the KV pool is sized: the
+        copies take the qkv + gate_up bytes of every layer once more (1.3 GB for Llama-3.2-1B)."""
+        c = self.cfg
+        self.wf = {}
+        if not (self.fuse_prefill and self.fuse_residual and self.device.type == "cuda" and self.tp_size == 1
+                and not c.is_moe and c.hidden_size % 64 == 0):
+            return False
+        for i in range(c.num_layers):
+            p = f"l{i}."
+            self.wf[p + "qkv"] = ops.fold_norm_weight(self.w[p + "qkv"], self.w[p + "in_norm"])
+            self.wf[p + "gate_up"] = ops.fold_norm_weight(self.w[p + "gate_up"], self.w[p + "post_norm"])
+        return True
+
     def lm_head_weight(self) -> torch.Tensor:
         if self.cfg.tie_word_embeddings:
             if self.tp_size == 1:
@@ -175,22 +195,30 @@ class TransformerLM:
         return self.w["lm_head"]
 
     # ------------------------------------------------------------------ forward
-    def _fused_q_rope(self, h: torch.Tensor, i: int) -> bool:
+    def _fused_q_rope(self, h: torch.Tensor, i: int, qkv_given: bool = False) -> bool:
         """Prefill / mixed steps on the GPU (hipBLASLt qkv, M > 256): the rope kernel writes only K / V
         and both attention kernels read q from the qkv rows and rotate it while loading it (one
         [T, Hq, D] write + read less per layer).  Needs the MFMA decode kernel (G >= 4) and no q/k
         norm; MXS_FUSED_Q_ROPE=0 turns it off."""
         return (_FUSED_Q_ROPE and h.is_cuda and h.shape[0] > 256 and not self.cfg.qk_norm and
                 self.hd in (64, 128) and self.nh // self.nkv >= 4 and self.nh % self.nkv == 0 and
-                not ops.qkv_uses_slabs(h, self.w[f"l{i}.qkv"]))
+                (qkv_given or not ops.qkv_uses_slabs(h, self.w[f"l{i}.qkv"])))
 
-    def _attention(self, i: int, h: torch.Tensor, md: AttnMetadata, kv_layer: torch.Tensor, project: bool = True):
+    def _attention(self, i: int, h: Optional[torch.Tensor], md: AttnMetadata, kv_layer: torch.Tensor,
+                   project: bool = True, qkv: Optional[torch.Tensor] = None):
+        """qkv: the projection already computed (_forward_pf); h is then unused."""
         c, w, p = self.cfg, self.w, f"l{i}."
         rope = None
-        if self._fused_q_rope(h, i):
-            q = ops.rope_kv_into_cache(ops.linear(h, w[p + "qkv"]), self.nh, self.nkv, self.hd, md.positions,
+        if self._fused_q_rope(h if qkv is None else qkv, i, qkv is not None):
+            if qkv is None:
+                qkv = ops.linear(h, w[p + "qkv"])
+            q = ops.rope_kv_into_cache(qkv, self.nh, self.nkv, self.hd, md.positions,
                                        self.cos_sin, kv_layer, md.slot_mapping, **self.kv_scales[i])
             rope = (md.positions, self.cos_sin)
+        elif qkv is not None:
+            q = ops.rope_and_cache(qkv, self.nh, self.nkv, self.hd, md.positions, self.cos_sin, kv_layer,
+                                   md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"), c.rms_norm_eps,
+                                   **self.kv_scales[i])
         else:
             q = ops.linear_rope_and_cache(h, w[p + "qkv"], self.nh, self.nkv, self.hd, md.positions, self.cos_sin,
                                           kv_layer, md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"),
@@ -220,16 +248,21 @@ class TransformerLM:
         out = ops.linear(o.reshape(o.shape[0], -1), w[p + "o"])
         return tp_all_reduce(out)
 
-    def _attention_sampled(self, i: int, h: torch.Tensor, md: AttnMetadata, kv_layer: torch.Tensor,
-                           project: bool = True):
+    def _attention_sampled(self, i: int, h: Optional[torch.Tensor], md: AttnMetadata, kv_layer: torch.Tensor,
+                           project: bool = True, qkv: Optional[torch.Tensor] = None):
         """Last layer of a step with prefill chunks: K/V of every token still go to the cache, but
         only the rows that produce logits (the last token of each sampled sequence) need attention,
         o_proj and the MLP.  Each such row is a single query at position seq_len - 1 over its whole
         context, i.e. exactly a decode query, so it runs on the decode kernel."""
         c, w, p = self.cfg, self.w, f"l{i}."
-        q = ops.linear_rope_and_cache(h, w[p + "qkv"], self.nh, self.nkv, self.hd, md.positions, self.cos_sin,
-                                      kv_layer, md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"),
-                                      c.rms_norm_eps, **self.kv_scales[i])
+        if qkv is not None:
+            q = ops.rope_and_cache(qkv, self.nh, self.nkv, self.hd, md.positions, self.cos_sin, kv_layer,
+                                   md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"), c.rms_norm_eps,
+                                   **self.kv_scales[i])
+        else:
+            q = ops.linear_rope_and_cache(h, w[p + "qkv"], self.nh, self.nkv, self.hd, md.positions, self.cos_sin,
+                                          kv_layer, md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"),
+                                          c.rms_norm_eps, **self.kv_scales[i])
         ns = md.logits_indices.shape[0]
         if ns == 0:  # no sequence samples this step: the layer only wrote K/V
             return h.new_empty((0, h.shape[1]))
@@ -297,10 +330,12 @@ class TransformerLM:
     def forward(self, input_ids: torch.Tensor, md: AttnMetadata, kv_cache: torch.Tensor) -> torch.Tensor:
         """Returns final hidden states (normed) of the rows selected by md.logits_indices."""
         c = self.cfg
-        # K01: the embedding gather runs inside the first layer's input RMSNorm kernel
-        h, residual = ops.embed_rms_norm(input_ids, self.w["embed"], self.w["l0.in_norm"], c.rms_norm_eps)
         # steps with prefill chunks: the last layer only computes the rows that produce logits
         prune = self.prune_last_layer and md.num_prefills > 0 and md.sample_seq is not None
+        if self.wf and input_ids.shape[0] > 256 and input_ids.is_cuda:
+            return self._forward_pf(input_ids, md, kv_cache, prune)
+        # K01: the embedding gather runs inside the first layer's input RMSNorm kernel
+        h, residual = ops.embed_rms_norm(input_ids, self.w["embed"], self.w["l0.in_norm"], c.rms_norm_eps)
         if self.fuse_residual and h.is_cuda:
             return self._forward_fused(h, residual, md, kv_cache, prune)
         x = None
@@ -350,6 +385,39 @@ class TransformerLM:
                 h, residual = tp_linear_add_rms_norm(ops.gate_up_silu(h, w[p + "gate_up"]), w[p + "down"], residual,
                                                      nxt, eps)
         return h if prune else h.index_select(0, md.logits_indices)
+
+    def _forward_pf(self, input_ids: torch.Tensor, md: AttnMetadata, kv_cache: torch.Tensor,
+                    prune: bool) -> torch.Tensor:
+        """Prefill / mixed steps (M > 256 rows, TP = 1, dense, GPU).  The residual stream r is the only
+        activation between the projections: every RMSNorm runs inside its consumer GEMM (gemm_pf row
+        scale over the norm-folded weight, the x^2 row sums taken from the X fragments the tile streams
+        anyway) and every residual add inside its producer (gemm_pf epi 2, r updated in place).  A layer
+        is qkv(rs) -> rope/cache -> attention -> o(+r) -> gate_up(rs, SwiGLU) -> down(+r): four GEMMs
+        and no normalisation pass over [M, hidden].  Per projection and row bucket the start-up tuner
+        (ops/prefill_pf.tune_fused) keeps a norm pass + the unfused GEMM, or hipBLASLt addmm_, where
+        those measured faster.  The last layer of a pruned step finishes on the sampled rows through
+        the unfused decode-size path."""
+        from ..ops.prefill_pf import norm_linear, resid_linear
+        c, w, wf = self.cfg, self.w, self.wf
+        eps = c.rms_norm_eps
+        L = c.num_layers
+        r = F.embedding(input_ids, w["embed"])
+        for i in range(L):
+            p = f"l{i}."
+            qkv = norm_linear(r, w[p + "qkv"], wf.get(p + "qkv"), w[p + "in_norm"], eps, 0)
+            if prune and i == L - 1:
+                o = self._attention_sampled(i, None, md, kv_cache[:, i], project=False, qkv=qkv)
+                if o.shape[0] == 0:  # no sequence samples this step: the layer only wrote K/V
+                    return o.new_empty((0, c.hidden_size))
+                rs = r.index_select(0, md.logits_indices)
+                h, rs = tp_linear_add_rms_norm(o, w[p + "o"], rs, w[p + "post_norm"], eps)
+                return tp_linear_add_rms_norm(ops.gate_up_silu(h, w[p + "gate_up"]), w[p + "down"], rs, w["norm"],
+                                              eps)[0]
+            o = self._attention(i, None, md, kv_cache[:, i], project=False, qkv=qkv)
+            resid_linear(o, w[p + "o"], r)
+            m = norm_linear(r, w[p + "gate_up"], wf.get(p + "gate_up"), w[p + "post_norm"], eps, 1)
+            resid_linear(m, w[p + "down"], r)
+        return ops.rms_norm(r.index_select(0, md.logits_indices), w["norm"], eps)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         # bf16 on the GPU: the sampling kernel reads bf16 rows directly (no fp32 copy of [B, V])

@@ -222,7 +222,7 @@ def _pf_workspace(device) -> tuple:
     ws = _PF_WS.get(device)
     if ws is None:
         ncu = torch.cuda.get_device_properties(device).multi_processor_count
-        slab = torch.empty(2 * ncu * 32 * 512 * 4, dtype=torch.float32, device=device)
+        slab = torch.empty(2 * ncu * 34 * 512 * 4, dtype=torch.float32, device=device)  # PF_SLAB_FRAGS = 34
         cnt = torch.zeros(1 << 16, dtype=torch.int32, device=device)
         ws = _PF_WS[device] = (slab, cnt, ncu)
     return ws
@@ -249,9 +249,13 @@ def pf_tile_map(ntm: int, ntn: int, device, gm: int = 8) -> torch.Tensor:
 
 
 def gemm_pf(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None,
-            min_iters: int = 16) -> Optional[torch.Tensor]:
+            min_iters: int = 16, resid: Optional[torch.Tensor] = None, row_scale: bool = False,
+            eps: float = 1e-5) -> Optional[torch.Tensor]:
     """Prefill GEMM on the hand-written persistent stream-K kernel: epi 0 x @ w.T, epi 1 SiLU(x @
-    gate.T) * (x @ up.T) with w = [gate; up].  None when the shape is not supported."""
+    gate.T) * (x @ up.T) with w = [gate; up], epi 2 resid + x @ w.T (out may be resid: in place).
+    row_scale (epi 0 / 1): every row of the product is scaled by rsqrt(mean(x_row^2) + eps), i.e.
+    RMSNorm(x) @ w'.T with the norm weight folded into w' (fold_norm_weight).  None when the shape is
+    not supported."""
     M, N = x.shape[0], w.shape[0]
     if N % 256:
         return None
@@ -259,9 +263,15 @@ def gemm_pf(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.
         out = torch.empty(M, N // 2 if epi == 1 else N, dtype=x.dtype, device=x.device)
     slab, cnt, ncu = _pf_workspace(x.device)
     tmap = pf_tile_map(-(-M // 256), N // 256, x.device)
-    if not ext().gemm_pf(out, x, w, epi, slab, cnt, tmap, ncu, min_iters):
+    if not ext().gemm_pf(out, x, w, epi, slab, cnt, tmap, ncu, min_iters, resid, row_scale, eps):
         return None
     return out
+
+
+def fold_norm_weight(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
+    """w diag(norm_w): the weight a row-scaled GEMM (gemm_pf row_scale) multiplies by, so that
+    rstd(x) * (x @ fold.T) == RMSNorm(x, norm_w) @ w.T."""
+    return (w.float() * norm_w.float()[None, :]).to(w.dtype).contiguous()
 
 
 def gate_up_silu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:

@@ -10,6 +10,13 @@ like the other tables (ops/tuned.py), so every start-up on the same hardware run
 
 MXS_GEMM_PF=auto (default: the tuned table) | on (gemm_pf for every supported shape, min_iters 16;
 tests, probes) | off (never).
+
+Fused prefill chain (models/llama.py _forward_pf, TP = 1 dense models): the RMSNorms run inside
+their consumer GEMMs (gemm_pf row scale over the norm-folded qkv / gate_up weights: table codes
+3 = plain, 4 = SwiGLU) and the residual adds inside their producers (code 2: gemm_pf epi 2, r += x
+W^T in place).  tune_fused() times each against the unfused alternative at the same row buckets
+(codes 3 / 4: RMSNorm pass + the routed GEMM; code 2: hipBLASLt addmm_ with beta = 1, or GEMM + add)
+and keeps the faster; norm_linear() / resid_linear() run the choice.
 """
 from __future__ import annotations
 
@@ -43,7 +50,9 @@ class PfTable:
         self.entries: dict = {}
         self.report: list = []
 
-    def lookup(self, M: int, N: int, K: int, epi: int) -> Optional[int]:
+    def lookup(self, M: int, N: int, K: int, epi: int):
+        """min_iters of gemm_pf for this (shape, code) at M rows, None for the unfused path; code 2
+        may also hold "addmm" (hipBLASLt with beta = 1)."""
         if MODE == "off" or M <= 256 or N % 256 or K % 64:
             return None
         if MODE == "on":
@@ -127,5 +136,109 @@ def tune(weights: dict, max_rows: int, device, dtype=torch.bfloat16) -> list:
                          "us": best_t and round(best_t, 2), "source": source})
         TABLE.entries[(N, K, epi)] = ent
     TABLE.report = rows
+    store.save()
+    return rows
+
+
+# ----------------------------------------------------------------------------- fused prefill chain
+CODE_RESID, CODE_RS, CODE_RS_SWIGLU = 2, 3, 4
+
+
+def norm_linear(r: torch.Tensor, w: torch.Tensor, wf: Optional[torch.Tensor], norm_w: torch.Tensor, eps: float,
+                epi: int) -> torch.Tensor:
+    """RMSNorm(r, norm_w) @ w.T (epi 0) or SiLU(. @ gate.T) * (. @ up.T) (epi 1).  gemm_pf with the
+    row scale over wf = fold_norm_weight(w, norm_w) where tuned faster, else a norm pass + the
+    routed unfused GEMM."""
+    from .. import ops
+    mi = TABLE.lookup(r.shape[0], w.shape[0], w.shape[1], CODE_RS + epi) if wf is not None else None
+    if isinstance(mi, int):
+        out = ops.gemm_pf(r, wf, epi, None, mi, row_scale=True, eps=eps)
+        if out is not None:
+            return out
+    x = ops.rms_norm(r, norm_w, eps)
+    return ops.linear(x, w) if epi == 0 else ops.gate_up_silu(x, w)
+
+
+def resid_linear(x: torch.Tensor, w: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
+    """r += x @ w.T in place (o_proj / down_proj into the residual stream)."""
+    from .. import ops
+    mi = TABLE.lookup(x.shape[0], w.shape[0], w.shape[1], CODE_RESID)
+    if isinstance(mi, int) and ops.gemm_pf(x, w, 2, r, mi, resid=r) is not None:
+        return r
+    if mi == "addmm":
+        return r.addmm_(x, w.t())
+    return r.add_(ops.linear(x, w))
+
+
+def tune_fused(weights: dict, max_rows: int, device, dtype=torch.bfloat16, eps: float = 1e-5) -> list:
+    """weights: {name: (w, wf | None, code)} with code 3 / 4 (row-scaled consumer, wf the folded
+    weight) or 2 (residual producer).  Adds the codes' entries to TABLE (run after tune(): the
+    unfused alternatives route through its choices); returns report rows."""
+    if MODE != "auto":
+        return []
+    from .. import ops
+    from .tuned import TunedStore, device_tag, median
+    store = TunedStore("prefill_pf", device_tag(device))
+    rows = []
+    for name, (w, wf, code) in weights.items():
+        N, K = w.shape
+        if N % 256 or K % 64:
+            continue
+        epi = code - CODE_RS if code != CODE_RESID else 2
+        ent = []
+        for M in buckets_for(max_rows):
+            key = f"{N}x{K}:{code}@{M}"
+            st = store.get(key)
+            x = (torch.randn(M, K, device=device) * (2.0 if code != CODE_RESID else 0.5)).to(dtype)
+            if st is not None:
+                best, best_t, t_base, source = st.get("cfg"), st.get("us"), st.get("base_us"), "table"
+            else:
+                source = "measured"
+                nw = torch.ones(K, device=device, dtype=dtype)
+                if code == CODE_RESID:
+                    r = torch.randn(M, N, device=device).to(dtype)
+                    bases = {None: lambda: r.add_(ops.linear(x, w)), "addmm": lambda: r.addmm_(x, w.t())}
+                    cand = {mi: (lambda mi=mi: ops.gemm_pf(x, w, 2, r, mi, resid=r)) for mi in MIN_ITERS}
+                else:
+                    bases = {None: (lambda: ops.linear(ops.rms_norm(x, nw, eps), w)) if epi == 0 else
+                             (lambda: ops.gate_up_silu(ops.rms_norm(x, nw, eps), w))}
+                    cand = {mi: (lambda mi=mi: ops.gemm_pf(x, wf, epi, None, mi, row_scale=True, eps=eps))
+                            for mi in MIN_ITERS}
+                tb = {k: [] for k in bases}
+                tc = {k: [] for k in cand}
+                for _ in range(ROUNDS):
+                    for k, fn in bases.items():
+                        tb[k].append(_time(fn))
+                    for k, fn in cand.items():
+                        tc[k].append(_time(fn))
+                bk = min(tb, key=lambda k: median(tb[k]))
+                t_base = median(tb[bk])
+                best, best_t = bk, t_base
+                for mi in MIN_ITERS:
+                    t = median(tc[mi])
+                    if t < t_base * WIN_MARGIN and t < best_t:
+                        best, best_t = mi, t
+            if isinstance(best, int):  # correctness of the kept kernel against the unfused path
+                if code == CODE_RESID:
+                    r0 = torch.randn(M, N, device=device).to(dtype)
+                    want = r0.float() + ops.linear(x, w).float()
+                    got = ops.gemm_pf(x, w, 2, None, best, resid=r0)
+                else:
+                    want = ops.linear(ops.rms_norm(x, torch.ones(K, device=device, dtype=dtype), eps), w)
+                    if epi == 1:
+                        want = ops.silu_mul(want)
+                    want = want.float()
+                    got = ops.gemm_pf(x, w, epi, None, best, row_scale=True, eps=eps)
+                err = (got.float() - want).abs().max().item()
+                if not err <= 0.03 * max(1.0, want.abs().max().item()):
+                    best, best_t = None, t_base
+            if source == "measured":
+                store.put(key, {"cfg": best, "us": best_t and round(best_t, 2), "base_us": round(t_base, 2)})
+            ent.append((M, best))
+            rows.append({"proj": name, "M": M, "N": N, "K": K, "code": code, "base_us": t_base and round(t_base, 2),
+                         "chosen": f"gemm_pf/{best}" if isinstance(best, int) else (best or "unfused"),
+                         "us": best_t and round(best_t, 2), "source": source})
+        TABLE.entries[(N, K, code)] = ent
+    TABLE.report = TABLE.report + rows
     store.save()
     return rows

@@ -228,3 +228,36 @@ def test_llama_1b_smoke_throughput(gpu):
     eng = LLMEngine(args)
     outs = eng.generate([list(range(1000, 1000 + 512))] * 32, SamplingParams(max_tokens=32, ignore_eos=True))
     assert all(len(o) == 32 for o in outs)
+
+
+@pytest.mark.parametrize("mode", ["on", "off"])
+@pytest.mark.parametrize("prune", [False, True])
+def test_fused_prefill_chain_matches_unfused(gpu, mode, prune, monkeypatch):
+    """llama.py _forward_pf (RMSNorms inside the consumer GEMMs over norm-folded weights, residual
+    adds inside the producers) vs the unfused forward on the same weights: logits and the K/V written.
+    mode "on" forces every fused gemm_pf form (row scale, residual epilogue); "off" takes the
+    fallbacks (norm pass + routed GEMM, residual add after the GEMM) of the same chain."""
+    from mxserve.ops import prefill_pf
+    cfg = get_model_config("small-llama")
+    sd = random_full_state(cfg, seed=3, std=0.05)
+    n = 600
+    ids = torch.randint(3, cfg.vocab_size, (n,), generator=torch.Generator().manual_seed(2)).to(gpu)
+    m = TransformerLM(cfg, gpu, torch.bfloat16)
+    m.load_full_state(sd)
+    m.prune_last_layer = prune
+    md = _prefill_md(n, gpu)
+    if prune:
+        md.logits_indices = torch.tensor([n - 1], device=gpu)
+        md.sample_seq = torch.tensor([0], dtype=torch.int32, device=gpu)
+    nb = (n + 15) // 16
+    kv_a = torch.zeros(nb, cfg.num_layers, 2, cfg.num_kv_heads, 16, cfg.head_dim, dtype=torch.bfloat16, device=gpu)
+    kv_b = kv_a.clone()
+    want = m.compute_logits(m.forward(ids, md, kv_a)).float()
+    assert m.prepare_fused_prefill()
+    monkeypatch.setattr(prefill_pf, "MODE", mode)
+    got = m.compute_logits(m.forward(ids, md, kv_b)).float()
+    assert got.shape == want.shape
+    scale = want.abs().max().item()
+    assert (got - want).abs().max().item() < 0.05 * scale
+    kd = (kv_a.float() - kv_b.float()).abs().max().item()
+    assert kd < 0.05 * kv_a.float().abs().max().item(), kd

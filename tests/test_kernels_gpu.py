@@ -979,19 +979,31 @@ def test_paged_prefill_fused_rope(gpu, D, G):
     _close(out, exp, 0.03, 0.03, "prefill fused rope")
 
 
-@pytest.mark.parametrize("T", [37, 700])  # per-token kernel and the 16-token prefill kernel
-def test_rope_kv_only(gpu, T):
-    """rope_and_cache with no q output writes exactly the K / V the full kernel writes."""
-    D, hq, hkv, nb = 64, 32, 8, 64
+@pytest.mark.parametrize("T,D,hkv,slot_kind,kv_fp8", [
+    (37, 64, 8, "run", False), (700, 64, 8, "run", False), (4099, 64, 8, "run", False),
+    (700, 64, 8, "scrambled", False), (700, 64, 8, "run", True), (1030, 128, 8, "run", False),
+    (1030, 128, 1, "scrambled", True), (520, 128, 4, "run", False)])
+def test_rope_kv_only(gpu, T, D, hkv, slot_kind, kv_fp8):
+    """rope_and_cache with no q output (the per-token kernel below 512 tokens, kv_rope_t16_kernel at
+    and above) writes exactly the K / V the full kernel writes: runs of whole blocks, runs starting
+    mid-block, scrambled slots with unmapped (-1) tokens, fp8 caches."""
+    hq = 4 * hkv
+    nb = (T + 15) // 16 + 8
     cos_sin = ref.build_cos_sin_cache(D, 8192, 500000.0, None, device=gpu)
     qkv = torch.randn(T, (hq + 2 * hkv) * D, device=gpu, dtype=torch.bfloat16)
     pos = torch.randint(0, 8000, (T,), device=gpu)
-    slots = torch.arange(T, device=gpu) + 16
-    kv_a = torch.zeros(nb, 2, hkv, 16, D, device=gpu, dtype=torch.bfloat16)
+    if slot_kind == "run":
+        slots = torch.arange(T, device=gpu) + 16 + (7 if T % 2 else 0)
+    else:
+        slots = torch.randperm(nb * 16, device=gpu)[:T]
+        slots[::13] = -1
+    dt = torch.float8_e4m3fn if kv_fp8 else torch.bfloat16
+    kv_a = torch.zeros(nb, 2, hkv, 16, D, device=gpu, dtype=torch.bfloat16).to(dt)
     kv_b = kv_a.clone()
-    ops.rope_and_cache(qkv, hq, hkv, D, pos, cos_sin, kv_a, slots)
-    q = ops.rope_kv_into_cache(qkv, hq, hkv, D, pos, cos_sin, kv_b, slots)
-    assert torch.equal(kv_a, kv_b)
+    sc = dict(k_scale=0.05, v_scale=0.07) if kv_fp8 else {}
+    ops.rope_and_cache(qkv, hq, hkv, D, pos, cos_sin, kv_a, slots, **sc)
+    q = ops.rope_kv_into_cache(qkv, hq, hkv, D, pos, cos_sin, kv_b, slots, **sc)
+    assert torch.equal(kv_a.view(torch.uint8), kv_b.view(torch.uint8))
     assert q.data_ptr() == qkv.data_ptr() and q.stride(0) == qkv.shape[1]
 
 
@@ -1016,6 +1028,49 @@ def test_gemm_pf(gpu, M, N, K, epi):
         assert torch.equal(again, out), "stream-K sum must not depend on arrival order"
     slab, cnt, _ = ops._pf_workspace(x.device)
     assert int(cnt.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(4240, 3072, 2048, 0), (4240, 16384, 2048, 1), (777, 768, 4096, 0),
+                                       (300, 512, 192, 1), (6400, 3072, 2048, 0)])
+def test_gemm_pf_row_scale(gpu, M, N, K, epi):
+    """gemm_pf with the fused-RMSNorm row scale vs fp32 RMSNorm(x, g) @ w.T (SwiGLU after it for epi 1):
+    the x^2 sums travel through stream-K slabs, rows past M stay unwritten; the norm weight folded
+    into w by ops.fold_norm_weight."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    x = (torch.randn(M, K, device=gpu, generator=g) * 3).to(torch.bfloat16)
+    x[::7] *= 0.01  # rows of very different scale
+    nw = (1 + 0.3 * torch.randn(K, device=gpu, generator=g)).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu, generator=g) * K ** -0.5).to(torch.bfloat16)
+    eps = 1e-5
+    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + eps) * nw.float()
+    ref = xn @ w.float().t()
+    if epi == 1:
+        ref = torch.nn.functional.silu(ref[:, :N // 2]) * ref[:, N // 2:]
+    wf = ops.fold_norm_weight(w, nw)
+    for mi in (0, 4, 16):
+        out = torch.full((M + 3, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
+        assert ops.gemm_pf(x, wf, epi, out[:M], mi, row_scale=True, eps=eps) is not None
+        assert torch.isnan(out[M:].float()).all()
+        _close(out[:M], ref, atol=3e-2, rtol=3e-2, name=f"gemm_pf rs {M}x{N}x{K} epi{epi} min_iters {mi}")
+        again = ops.gemm_pf(x, wf, epi, None, mi, row_scale=True, eps=eps)
+        assert torch.equal(again, out[:M])
+    assert int(ops._pf_workspace(x.device)[1].abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M,N,K", [(4240, 2048, 2048), (4240, 2048, 8192), (777, 768, 4096), (6400, 2048, 8192)])
+def test_gemm_pf_residual(gpu, M, N, K):
+    """gemm_pf epi 2: out = resid + x @ w.T, in place on the residual stream and out of place."""
+    g = torch.Generator(device="cuda").manual_seed(7 * M + N + K)
+    x = torch.randn(M, K, device=gpu, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu, generator=g) * K ** -0.5).to(torch.bfloat16)
+    r = (torch.randn(M, N, device=gpu, generator=g) * 4).to(torch.bfloat16)
+    ref = r.float() + x.float() @ w.float().t()
+    for mi in (0, 16):
+        out = ops.gemm_pf(x, w, 2, None, mi, resid=r)
+        _close(out, ref, atol=3e-2, rtol=2e-2, name=f"gemm_pf resid {M}x{N}x{K} mi {mi}")
+        rr = r.clone()
+        assert ops.gemm_pf(x, w, 2, rr, mi, resid=rr) is not None
+        assert torch.equal(rr, out), "in place == out of place"
 
 
 @pytest.mark.parametrize("M", [1, 5, 16])
