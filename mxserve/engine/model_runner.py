@@ -579,9 +579,12 @@ class ModelRunner:
                 fw = {"qkv": (w["l0.qkv"], m.wf["l0.qkv"], prefill_pf.CODE_RS),
                       "gate_up": (w["l0.gate_up"], m.wf["l0.gate_up"], prefill_pf.CODE_RS_SWIGLU),
                       "o": (w["l0.o"], None, prefill_pf.CODE_RESID), "down": (w["l0.down"], None, prefill_pf.CODE_RESID)}
-                self.prefill_pf_report = self.prefill_pf_report + prefill_pf.tune_fused(
-                    fw, self.args.max_num_batched_tokens + self.args.max_num_seqs, self.device, self.dtype,
-                    self.cfg.rms_norm_eps)
+                rep = prefill_pf.tune_fused(fw, self.args.max_num_batched_tokens + self.args.max_num_seqs,
+                                            self.device, self.dtype, self.cfg.rms_norm_eps)
+                self.prefill_pf_report = self.prefill_pf_report + rep
+                m.drop_folded([p for p in ("qkv", "gate_up")
+                               if not any(r["proj"] == p and r["chosen"].startswith("gemm_pf") for r in rep)])
+                torch.cuda.empty_cache()
             if self.cfg.is_moe and "l0.w13" in w:  # expert GEMMs at decode batches (local experts)
                 from ..ops import moe as moe_ops
                 self.moe_gemm_report = moe_ops.tune(w["l0.w13"], w["l0.w2"], buckets, self.cfg.num_experts_per_tok,

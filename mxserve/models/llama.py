@@ -72,6 +72,7 @@ class TransformerLM:
         # TP = 1 dense models on the GPU, prefill / mixed steps: RMSNorms inside the consumer GEMMs and
         # residual adds inside the producers (_forward_pf); self.wf holds the norm-folded weights
         self.fuse_prefill = os.environ.get("MXS_PF_FUSED", "1") == "1"
+        self.pf_chain = False
         self.wf: dict[str, torch.Tensor] = {}
         # fp8 KV cache: stored = x / scale, per layer (1.0 until the runner calibrates them from a
         # probe prefill, mxserve/engine/model_runner.py::_calibrate_kv_scales; MXS_KV_SCALE fixes all)
@@ -175,14 +176,21 @@ class TransformerLM:
         copies take the qkv + gate_up bytes of every layer once more (1.3 GB for Llama-3.2-1B)."""
         c = self.cfg
         self.wf = {}
-        if not (self.fuse_prefill and self.fuse_residual and self.device.type == "cuda" and self.tp_size == 1
-                and not c.is_moe and c.hidden_size % 64 == 0):
+        self.pf_chain = (self.fuse_prefill and self.fuse_residual and self.device.type == "cuda" and
+                         self.tp_size == 1 and not c.is_moe and c.hidden_size % 64 == 0)
+        if not self.pf_chain:
             return False
         for i in range(c.num_layers):
             p = f"l{i}."
             self.wf[p + "qkv"] = ops.fold_norm_weight(self.w[p + "qkv"], self.w[p + "in_norm"])
             self.wf[p + "gate_up"] = ops.fold_norm_weight(self.w[p + "gate_up"], self.w[p + "post_norm"])
         return True
+
+    def drop_folded(self, names) -> None:
+        """Free the folded copies of projections (e.g. "qkv", "gate_up") whose row-scaled form the
+        start-up tuner rejected at every row bucket: norm_linear then always takes the norm pass."""
+        for k in [k for k in self.wf if k.split(".", 1)[1] in set(names)]:
+            del self.wf[k]
 
     def lm_head_weight(self) -> torch.Tensor:
         if self.cfg.tie_word_embeddings:
@@ -332,7 +340,7 @@ class TransformerLM:
         c = self.cfg
         # steps with prefill chunks: the last layer only computes the rows that produce logits
         prune = self.prune_last_layer and md.num_prefills > 0 and md.sample_seq is not None
-        if self.wf and input_ids.shape[0] > 256 and input_ids.is_cuda:
+        if self.pf_chain and input_ids.shape[0] > 256 and input_ids.is_cuda:
             return self._forward_pf(input_ids, md, kv_cache, prune)
         # K01: the embedding gather runs inside the first layer's input RMSNorm kernel
         h, residual = ops.embed_rms_norm(input_ids, self.w["embed"], self.w["l0.in_norm"], c.rms_norm_eps)

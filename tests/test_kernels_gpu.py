@@ -1003,7 +1003,13 @@ def test_rope_kv_only(gpu, T, D, hkv, slot_kind, kv_fp8):
     sc = dict(k_scale=0.05, v_scale=0.07) if kv_fp8 else {}
     ops.rope_and_cache(qkv, hq, hkv, D, pos, cos_sin, kv_a, slots, **sc)
     q = ops.rope_kv_into_cache(qkv, hq, hkv, D, pos, cos_sin, kv_b, slots, **sc)
-    assert torch.equal(kv_a.view(torch.uint8), kv_b.view(torch.uint8))
+    # V is a copy (bit-exact); K's rotation may contract into FMAs differently per kernel (one rounding
+    # step of the stored value at most)
+    assert torch.equal(kv_a[:, 1].view(torch.uint8), kv_b[:, 1].view(torch.uint8))
+    ka, kb = kv_a[:, 0].float(), kv_b[:, 0].float()
+    assert torch.equal(ka == 0, kb == 0), "the same slots written"
+    assert (ka - kb).abs().max().item() <= (0.07 if kv_fp8 else 0.02) * ka.abs().max().item()
+    assert (ka != kb).float().mean().item() < 0.01
     assert q.data_ptr() == qkv.data_ptr() and q.stride(0) == qkv.shape[1]
 
 

@@ -237,33 +237,42 @@ def test_bench_rejects_world_mismatch(tmp_path):
 
 def test_probe_wall_budget_skips_sections_on_every_rank():
     """bench.py caps the multi-GPU probe's wall time (MXS_PROBE_BUDGET_S): once rank 0's clock is
-    past the budget no further section starts on ANY rank, and the probe still reports."""
+    past the budget no further section starts on ANY rank, and the probe still reports.  The
+    rendezvous port is picked free and released before rank 0 binds it, so under a parallel test run
+    another process can take it first: such a start-up failure is retried on a new port."""
     import json
     import socket
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
-    procs = []
-    for r in range(2):
-        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
-                   WORLD_SIZE="2", PYTHONPATH=ROOT, MXS_PROBE_DEVICE="cpu", MXS_PROBE_BUDGET_S="1e-9",
-                   MXS_PROBE_SECTIONS="collectives,tp")
-        procs.append(subprocess.Popen([sys.executable, "-m", "mxserve.tools.mgpu_probe"], stdin=subprocess.PIPE,
-                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, cwd=ROOT))
-    outs = []
-    try:
-        for p in procs:
-            p.stdin.write(b"go\n")
-            p.stdin.close()
-            p.stdin = None
-        for p in procs:
-            outs.append(p.communicate(timeout=120))
-    finally:
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
-    for p, (_, err) in zip(procs, outs):
-        assert p.returncode == 0, err.decode()[-3000:]
+    for attempt in range(3):
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        procs = []
+        for r in range(2):
+            env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
+                       WORLD_SIZE="2", PYTHONPATH=ROOT, MXS_PROBE_DEVICE="cpu", MXS_PROBE_BUDGET_S="1e-9",
+                       MXS_PROBE_SECTIONS="collectives,tp")
+            procs.append(subprocess.Popen([sys.executable, "-m", "mxserve.tools.mgpu_probe"], stdin=subprocess.PIPE,
+                                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, cwd=ROOT))
+        outs = []
+        try:
+            for p in procs:
+                p.stdin.write(b"go\n")
+                p.stdin.close()
+                p.stdin = None
+            for p in procs:
+                outs.append(p.communicate(timeout=120))
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        errs = [e.decode() for _, e in outs]
+        if any(p.returncode != 0 for p in procs) and attempt < 2 and any(
+                k in e for e in errs for k in ("Address already in use", "EADDRINUSE", "Connection refused",
+                                                "connect()", "DistNetworkError", "Connection reset")):
+            continue
+        break
+    for p, err in zip(procs, errs):
+        assert p.returncode == 0, err[-3000:]
     line = [ln for ln in outs[0][0].decode().splitlines() if ln.startswith("PROBE ")][-1]
     d = json.loads(line[len("PROBE "):])
     assert d["status"] == "ok", d
