@@ -96,7 +96,7 @@ def parse(argv=None):
     ap.add_argument("--model", default="meta-llama/Llama-3.2-1B-Instruct")
     ap.add_argument("--isl", type=int, default=4000)
     ap.add_argument("--osl", type=int, default=500)
-    ap.add_argument("--qps", type=float, default=float(os.environ.get("MXS_BENCH_QPS", "48")),
+    ap.add_argument("--qps", type=float, default=float(os.environ.get("MXS_BENCH_QPS", "49")),
                     help="Poisson arrival rate per GPU (requests/s)")
     ap.add_argument("--arrivals", choices=["router", "local"], default=os.environ.get("MXS_BENCH_ARRIVALS", "router"),
                     help="N >= 2: router = one Poisson stream at the node's rate, each request routed to a rank "
