@@ -273,7 +273,7 @@ class TransformerLM:
                                           c.rms_norm_eps, **self.kv_scales[i])
         ns = md.logits_indices.shape[0]
         if ns == 0:  # no sequence samples this step: the layer only wrote K/V
-            return h.new_empty((0, h.shape[1]))
+            return q.new_empty((0, self.cfg.hidden_size))
         qs = q.index_select(0, md.logits_indices)
         seq = md.sample_seq.long()
         bt = md.block_tables.index_select(0, seq)

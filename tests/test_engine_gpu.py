@@ -231,7 +231,7 @@ def test_llama_1b_smoke_throughput(gpu):
 
 
 @pytest.mark.parametrize("mode", ["on", "off"])
-@pytest.mark.parametrize("prune", [False, True])
+@pytest.mark.parametrize("prune", [False, True, "nosample"])
 def test_fused_prefill_chain_matches_unfused(gpu, mode, prune, monkeypatch):
     """llama.py _forward_pf (RMSNorms inside the consumer GEMMs over norm-folded weights, residual
     adds inside the producers) vs the unfused forward on the same weights: logits and the K/V written.
@@ -244,14 +244,25 @@ def test_fused_prefill_chain_matches_unfused(gpu, mode, prune, monkeypatch):
     ids = torch.randint(3, cfg.vocab_size, (n,), generator=torch.Generator().manual_seed(2)).to(gpu)
     m = TransformerLM(cfg, gpu, torch.bfloat16)
     m.load_full_state(sd)
-    m.prune_last_layer = prune
+    m.prune_last_layer = bool(prune)
     md = _prefill_md(n, gpu)
-    if prune:
+    if prune == "nosample":  # a mid-prompt chunk: K/V written, no row samples
+        md.logits_indices = torch.zeros(0, dtype=torch.long, device=gpu)
+        md.sample_seq = torch.zeros(0, dtype=torch.int32, device=gpu)
+    elif prune:
         md.logits_indices = torch.tensor([n - 1], device=gpu)
         md.sample_seq = torch.tensor([0], dtype=torch.int32, device=gpu)
     nb = (n + 15) // 16
     kv_a = torch.zeros(nb, cfg.num_layers, 2, cfg.num_kv_heads, 16, cfg.head_dim, dtype=torch.bfloat16, device=gpu)
     kv_b = kv_a.clone()
+    if prune == "nosample":
+        assert m.forward(ids, md, kv_a).shape == (0, cfg.hidden_size)
+        assert m.prepare_fused_prefill()
+        monkeypatch.setattr(prefill_pf, "MODE", mode)
+        assert m.forward(ids, md, kv_b).shape == (0, cfg.hidden_size)
+        kd = (kv_a.float() - kv_b.float()).abs().max().item()
+        assert kd < 0.05 * kv_a.float().abs().max().item(), kd
+        return
     want = m.compute_logits(m.forward(ids, md, kv_a)).float()
     assert m.prepare_fused_prefill()
     monkeypatch.setattr(prefill_pf, "MODE", mode)
