@@ -22,10 +22,10 @@ Phases (--mode auto: agg for N = 1, agg then disagg for N >= 2, both in the one 
           measured: a decode GPU is KV-bandwidth bound at 76.7 req/s, a prefill GPU computes 127.6
           req/s: 1P+1D at N = 2, 2P+2D at 4, 3P+5D at 8)
           and offers the node the rate that loads the tighter role to 85 %; when the split carries
-          the agg rate, the disagg phase runs at it (like-for-like).  Default rate 48 req/s per GPU:
-          sustained on one MI355X over 40-step windows at 22.5k tok/s, TTFT p50 54 ms / ITL p90
-          21.3 ms with 6144-token steps (8192: 22.5k, 42 ms / 24.2 ms; QPS 50 queues: TTFT ~1 s;
-          profiles/r4/sched_q*.json).  The realised Poisson rate of the fixed-seed arrival stream over those windows
+          the agg rate, the disagg phase runs at it (like-for-like).  Default rate 49 req/s per GPU:
+          sustained on one MI355X at 22.6k tok/s, TTFT p50 52 ms / ITL p90 21.2 ms with 6144-token
+          steps (profiles/r4/s2/bench_q49_kvrope.json; QPS 50 queues at every step budget from 3072
+          to 6144: TTFT p50 0.5-1.1 s, profiles/r4/s2/step_budget/).  The realised Poisson rate of the fixed-seed arrival stream over those windows
           is 97-98 % of nominal, which with the request tail bounds value at ~94 % of QPS x OSL.
           Requests arrive at the decode ranks (routed over them like the agg phase's when D >= 2);
           a decode rank reserves KV blocks and hands each
