@@ -120,6 +120,10 @@ def decode_cfg(T: int, N: int, K: int, epi: int, e_local: int, top_k: int = 2) -
     return best
 
 
+# split-K slices the fused epilogues (silu_mul_partials, moe_combine_partials) sum at most
+MAX_SLABS = 8
+
+
 def _mdg(out, x, w, offs, part, rows_max: int, cfg: tuple, epi: int) -> bool:
     from . import ext
     mf, nf, wm, sk = cfg[:4]
@@ -141,7 +145,7 @@ def _fused_experts_decode(x, w13, w2, topk_w, offs, inv, xs, expert_offset) -> t
         return None
     else:
         c13, c2 = tuned
-    if c13 is None or c2 is None:
+    if c13 is None or c2 is None or c13[3] > MAX_SLABS or c2[3] > MAX_SLABS:
         return None
     dev = x.device
     h = torch.empty(R, two_i // 2, dtype=x.dtype, device=dev)
@@ -279,7 +283,7 @@ def tune(w13: torch.Tensor, w2: torch.Tensor, buckets: list, top_k: int, n_exper
             bt, bc = None, None
             for cfg in candidates(T, N, K, epi, all_mf=True, mt=False):
                 sk = cfg[3]
-                if cfg[2] > 2:
+                if cfg[2] > 2 or sk > MAX_SLABS:  # the slab-summing epilogues take at most 8 slices
                     continue
                 pp = part[: sk * R * N].view(sk, R, N) if sk > 1 else None
                 if not _mdg(o, xin, w, offs, pp, T, cfg, epi):
