@@ -61,6 +61,9 @@ constexpr int PF_SLAB_FRAGS = 34;  // 32 accumulator fragments + 2 float4 of RS 
 
 __device__ __forceinline__ pf_bf16x8 pf_frag(const pf_u32x4& v) { return __builtin_bit_cast(pf_bf16x8, v); }
 __device__ __forceinline__ float pf_silu(float g) { return g / (1.f + __expf(-g)); }
+// a dword as two bf16, by value: __builtin_bit_cast of a vector ELEMENT (q.y, q[d]) reads dword 0 of
+// the vector (hipcc / ROCm 7.2: the element's "address" is the vector's), so copy it out first
+__device__ __forceinline__ pf_bf16x2 pf_pair(unsigned v) { return __builtin_bit_cast(pf_bf16x2, v); }
 
 struct PfArgs {
   bf16_t* Y;
@@ -223,6 +226,21 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
       xb[t][1] = *reinterpret_cast<const pf_u32x4*>(p1 + t * 2048);
     }
   };
+  // RS: x^2 of this phase's X fragments, in the wave's LDS-read segment (after its reads landed, before
+  // the barrier into its MFMA segment) while the partner wave on the SIMD runs its MFMAs
+  auto rs_sum = [&](int hb) {
+    if constexpr (RS) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const pf_bf16x2 v = pf_pair(xb[t][kk][d]);
+            ssq[4 * hb + t] = __builtin_amdgcn_fdot2_f32_bf16(v, v, ssq[4 * hb + t], false);
+          }
+    }
+  };
   auto mma = [&](int hb) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -233,17 +251,6 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
         for (int t = 0; t < 4; ++t)
           acc[f][4 * hb + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf_frag(wa[f][kk]), pf_frag(xb[t][kk]),
                                                                         acc[f][4 * hb + t], 0, 0, 0);
-    if constexpr (RS) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const pf_bf16x2 v = __builtin_bit_cast(pf_bf16x2, xb[t][kk][d]);
-            ssq[4 * hb + t] = __builtin_amdgcn_fdot2_f32_bf16(v, v, ssq[4 * hb + t], false);
-          }
-    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -390,6 +397,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
     rd_w(b);
     rd_x(b, 0);
     PF_LGKM0();
+    rs_sum(0);
     PF_BAR();
     mma(0);
     PF_BAR();
@@ -413,6 +421,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     PF_LGKM0();
+    rs_sum(1);
     PF_BAR();
     mma(1);
     PF_BAR();

@@ -248,6 +248,54 @@ static bool kv_t16_legacy() {
   return v;
 }
 
+// V rows of the dim-major cache block ([Hkv][D][BS]) take a tile's tokens as RUNS: consecutive
+// tokens with consecutive slots inside one block (a prefill chunk: one run, or two when the chunk
+// starts mid-block -- every continuation chunk does; a decode row: a run of one).  A run of n values
+// at element offset o of a row is written in aligned pieces of 8 / 4 / 2 / 1 elements (a whole
+// 16-token row: two 16-byte stores for bf16), not one 2-byte store per element.
+// src: the run's first value in the LDS stage, consecutive tokens `stride` elements apart (values are
+// read per piece from LDS: a dynamically indexed register array would live in scratch)
+template <typename KT>
+__device__ __forceinline__ void kv_put(KT* row, int o, int n, const bf16_t* src, int stride, float inv) {
+  int i = 0;
+  while (i < n) {
+    const int a = o + i, left = n - i;
+    const bf16_t* p = src + i * stride;
+    if ((a & 7) == 0 && left >= 8) {
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = bf2f(p[e * stride]);
+      kv_store8(row + a, x, inv);
+      i += 8;
+    } else if ((a & 3) == 0 && left >= 4) {
+      float x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = bf2f(p[e * stride]);
+      if constexpr (sizeof(KT) == 2) {
+        *reinterpret_cast<uint2*>(row + a) = make_uint2(pack2(x[0], x[1]), pack2(x[2], x[3]));
+      } else {
+        uint32_t v = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v |= static_cast<uint32_t>(static_cast<uint8_t>(f2fp8(x[e] * inv))) << (8 * e);
+        *reinterpret_cast<uint32_t*>(row + a) = v;
+      }
+      i += 4;
+    } else if ((a & 1) == 0 && left >= 2) {
+      const float x0 = bf2f(p[0]), x1 = bf2f(p[stride]);
+      if constexpr (sizeof(KT) == 2) {
+        *reinterpret_cast<uint32_t*>(row + a) = pack2(x0, x1);
+      } else {
+        const uint32_t lo = static_cast<uint8_t>(f2fp8(x0 * inv)), hi = static_cast<uint8_t>(f2fp8(x1 * inv));
+        *reinterpret_cast<unsigned short*>(row + a) = static_cast<unsigned short>(lo | (hi << 8));
+      }
+      i += 2;
+    } else {
+      kv_store(row + a, bf2f(p[0]), inv);
+      i += 1;
+    }
+  }
+}
+
 template <int D, typename KT, int NI, int NV>
 __global__ void __launch_bounds__(256) kv_rope_t16_kernel(
     const bf16_t* __restrict__ qkv, const int64_t* __restrict__ positions, const float* __restrict__ cos_sin,
@@ -255,7 +303,8 @@ __global__ void __launch_bounds__(256) kv_rope_t16_kernel(
     float k_inv_scale, float v_inv_scale) {
   constexpr int HALF = D / 2, CH = HALF / 8, TPB = 16;
   extern __shared__ __attribute__((aligned(16))) bf16_t vstage[];  // [TPB][Hkv * D]
-  __shared__ int s_fast;
+  __shared__ unsigned s_runs;       // bit k: token k starts a run
+  __shared__ int64_t s_slot[TPB];
   const int t0 = blockIdx.x * TPB, nt = min(TPB, T - t0), tid = threadIdx.x;
   const int row_stride = (Hq + 2 * Hkv) * D, hkd = Hkv * D;
   const int n_k = nt * Hkv * CH, n_v = nt * (hkd / 8);
@@ -280,11 +329,13 @@ __global__ void __launch_bounds__(256) kv_rope_t16_kernel(
     pos[u] = positions[t0 + tt];
     slot[u] = slot_mapping[t0 + tt];
   }
-  if (tid < 64) {  // wave 0: does the tile fill one run of a block's slots?
-    const int64_t sk = tid < nt ? slot_mapping[t0 + tid] : 0;
-    const int64_t s0 = __shfl(sk, 0, 64);
-    const bool all_ok = __all(tid >= nt || sk == s0 + tid);
-    if (tid == 0) s_fast = all_ok && s0 >= 0 && (s0 % BS) + nt <= BS;
+  if (tid < 64) {  // wave 0: the tile's runs (unmapped tokens, slot -1, start a run and are skipped)
+    const int64_t sk = tid < nt ? slot_mapping[t0 + tid] : -1;
+    const int64_t sp = __shfl_up(sk, 1, 64);
+    const bool start = tid < nt && (tid == 0 || sk < 0 || sp < 0 || sk != sp + 1 || sk % BS == 0);
+    const unsigned long long m = __ballot(start);
+    if (tid < nt) s_slot[tid] = sk;
+    if (tid == 0) s_runs = static_cast<unsigned>(m & 0xFFFFu);
   }
 #pragma unroll
   for (int u = 0; u < NV; ++u) {
@@ -319,30 +370,20 @@ __global__ void __launch_bounds__(256) kv_rope_t16_kernel(
     }
   }
   __syncthreads();
-  if (!s_fast) {  // tokens of different blocks (or unmapped): one store per (token, dim)
-    for (int i = tid; i < nt * hkd; i += blockDim.x) {
-      const int tt = i / hkd, j = i - tt * hkd;
-      const int64_t sl = slot_mapping[t0 + tt];
-      if (sl < 0) continue;
-      KT* dst = kv + (sl / BS) * block_stride + static_cast<size_t>(Hkv) * BS * D + static_cast<size_t>(j) * BS + sl % BS;
-      kv_store(dst, bf2f(vstage[tt * hkd + j]), v_inv_scale);
-    }
-    return;
-  }
-  const int64_t sl0 = slot_mapping[t0];
-  const int off0 = static_cast<int>(sl0 % BS);
-  KT* vblk = kv + (sl0 / BS) * block_stride + static_cast<size_t>(Hkv) * BS * D;
+  // V: each thread owns rows j (one (head, dim) of the block's dim-major image); the run loop is
+  // wave-uniform (the runs belong to the tile)
+  const unsigned runs = s_runs;
   for (int j = tid; j < hkd; j += blockDim.x) {
-    KT* dst = vblk + static_cast<size_t>(j) * BS + off0;
-    if (nt == TPB && off0 == 0 && BS == TPB) {  // a whole row of the block: 16 tokens
-      float x[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) x[k] = bf2f(vstage[k * hkd + j]);
-      kv_store8(dst, x, v_inv_scale);
-      kv_store8(dst + 8, x + 8, v_inv_scale);
-      continue;
+    unsigned rest = runs;
+    while (rest) {
+      const int a = __builtin_ctz(rest);
+      rest &= rest - 1;
+      const int b = rest ? __builtin_ctz(rest) : nt;  // run = tokens [a, b)
+      const int64_t sl = s_slot[a];
+      if (sl < 0) continue;
+      KT* row = kv + (sl / BS) * block_stride + static_cast<size_t>(Hkv) * BS * D + static_cast<size_t>(j) * BS;
+      kv_put(row, static_cast<int>(sl % BS), b - a, vstage + a * hkd + j, hkd, v_inv_scale);
     }
-    for (int tt = 0; tt < nt; ++tt) kv_store(dst + tt, bf2f(vstage[tt * hkd + j]), v_inv_scale);
   }
 }
 

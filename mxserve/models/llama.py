@@ -221,7 +221,8 @@ class TransformerLM:
             if qkv is None:
                 qkv = ops.linear(h, w[p + "qkv"])
             q = ops.rope_kv_into_cache(qkv, self.nh, self.nkv, self.hd, md.positions,
-                                       self.cos_sin, kv_layer, md.slot_mapping, **self.kv_scales[i])
+                                       self.cos_sin, kv_layer, md.slot_mapping, **self.kv_scales[i],
+                                       num_decodes=md.num_decodes)
             rope = (md.positions, self.cos_sin)
         elif qkv is not None:
             q = ops.rope_and_cache(qkv, self.nh, self.nkv, self.hd, md.positions, self.cos_sin, kv_layer,
@@ -263,6 +264,26 @@ class TransformerLM:
         o_proj and the MLP.  Each such row is a single query at position seq_len - 1 over its whole
         context, i.e. exactly a decode query, so it runs on the decode kernel."""
         c, w, p = self.cfg, self.w, f"l{i}."
+        x = h if qkv is None else qkv
+        if self._fused_q_rope(x, i, qkv is not None):
+            # K / V of every token into the cache; q stays un-rotated in the qkv rows and only the
+            # sampled rows' q is gathered and rotated inside the decode kernel (no [T, Hq, D] q write)
+            if qkv is None:
+                qkv = ops.linear(h, w[p + "qkv"])
+            q = ops.rope_kv_into_cache(qkv, self.nh, self.nkv, self.hd, md.positions, self.cos_sin, kv_layer,
+                                       md.slot_mapping, **self.kv_scales[i], num_decodes=md.num_decodes)
+            ns = md.logits_indices.shape[0]
+            if ns == 0:
+                return q.new_empty((0, self.cfg.hidden_size))
+            qs = q.index_select(0, md.logits_indices)
+            seq = md.sample_seq.long()
+            o = ops.paged_attention_decode(qs, kv_layer, md.block_tables.index_select(0, seq),
+                                           md.seq_lens.index_select(0, seq), self.scale, md.max_seq_len,
+                                           rope=(md.positions.index_select(0, md.logits_indices), self.cos_sin),
+                                           **self.kv_scales[i])
+            if not project:
+                return o.reshape(ns, -1)
+            return tp_all_reduce(ops.linear(o.reshape(ns, -1), w[p + "o"]))
         if qkv is not None:
             q = ops.rope_and_cache(qkv, self.nh, self.nkv, self.hd, md.positions, self.cos_sin, kv_layer,
                                    md.slot_mapping, w.get(p + "q_norm"), w.get(p + "k_norm"), c.rms_norm_eps,

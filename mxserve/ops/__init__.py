@@ -411,12 +411,22 @@ def linear_rope_and_cache(h: torch.Tensor, w: torch.Tensor, num_heads: int, num_
 
 def rope_kv_into_cache(qkv: torch.Tensor, num_heads: int, num_kv_heads: int, head_dim: int,
                        positions: torch.Tensor, cos_sin: torch.Tensor, kv_layer: torch.Tensor,
-                       slot_mapping: torch.Tensor, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
+                       slot_mapping: torch.Tensor, k_scale: float = 1.0, v_scale: float = 1.0,
+                       num_decodes: int = 0) -> torch.Tensor:
     """rope_and_cache without the q write (GPU): RoPE on k, K / V into the paged cache; returns the
-    un-rotated q as a row-strided view of qkv, for the attention ops' `rope=` argument."""
-    ext().rope_and_cache(None, qkv, positions, cos_sin, kv_layer, slot_mapping, None, None, num_heads, num_kv_heads,
-                         head_dim, 1e-6, k_scale, v_scale)
-    return qkv[:, :num_heads * head_dim].view(qkv.shape[0], num_heads, head_dim)
+    un-rotated q as a row-strided view of qkv, for the attention ops' `rope=` argument.
+    num_decodes: a mixed step's leading decode rows (one token per sequence, scattered slots) go to
+    the one-token-per-workgroup kernel, the prefill rows to the 16-token tile kernel: a tile of 16
+    decode rows is 16 runs of one token, i.e. 8k two-byte V stores on one workgroup, the slowest
+    tile of the launch."""
+    T = qkv.shape[0]
+    parts = [(0, T)]
+    if 0 < num_decodes < T and T - num_decodes >= 512:
+        parts = [(0, num_decodes), (num_decodes, T)]
+    for a, b in parts:
+        ext().rope_and_cache(None, qkv[a:b], positions[a:b], cos_sin, kv_layer, slot_mapping[a:b], None, None,
+                             num_heads, num_kv_heads, head_dim, 1e-6, k_scale, v_scale)
+    return qkv[:, :num_heads * head_dim].view(T, num_heads, head_dim)
 
 
 def paged_attention_decode(q: torch.Tensor, kv_layer: torch.Tensor, block_tables: torch.Tensor,

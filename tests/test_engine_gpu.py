@@ -52,31 +52,35 @@ def test_forward_matches_cpu_reference(gpu, name):
     assert hit > 0.95
 
 
+@pytest.mark.parametrize("lens", [[40, 30, 77], [300, 200, 77]])  # the second: > 256 rows, fused q RoPE
 @pytest.mark.parametrize("name", ["small-llama", "tiny-qwen3-gpu"])
-def test_pruned_last_layer_matches_full(gpu, name):
+def test_pruned_last_layer_matches_full(gpu, name, lens):
     """Prefill steps compute the last layer only for the rows that sample (on the decode kernel);
     the logits must match the full last layer, and the K/V written must be identical."""
     cfg = get_model_config(name)
     sd = random_full_state(cfg, seed=2, std=0.05)
-    lens = [40, 30, 77]
     n = sum(lens)
     ids = torch.randint(3, cfg.vocab_size, (n,), generator=torch.Generator().manual_seed(1)).to(gpu)
     pos, slots, bts, blk = [], [], [], 0
+    width = max((L + 15) // 16 for L in lens)
     for L in lens:
         nb = (L + 15) // 16
         pos += list(range(L))
         slots += [(blk + p // 16) * 16 + p % 16 for p in range(L)]
-        bts.append(list(range(blk, blk + nb)) + [0] * (8 - nb))
+        bts.append(list(range(blk, blk + nb)) + [0] * (width - nb))
         blk += nb
-    qsl = torch.tensor([0, 40, 70, 147], dtype=torch.int32, device=gpu)
+    starts = [0]
+    for L in lens:
+        starts.append(starts[-1] + L)
+    qsl = torch.tensor(starts, dtype=torch.int32, device=gpu)
     # sequence 1 is a mid-prompt chunk: it writes K/V but does not sample
     sample_seq = torch.tensor([0, 2], dtype=torch.int32, device=gpu)
     md = AttnMetadata(positions=torch.tensor(pos, device=gpu), slot_mapping=torch.tensor(slots, device=gpu),
                       block_tables=torch.tensor(bts, dtype=torch.int32, device=gpu),
                       seq_lens=torch.tensor(lens, dtype=torch.int32, device=gpu), query_start_loc=qsl,
-                      logits_indices=torch.tensor([39, 146], device=gpu), num_decodes=0, num_prefills=3,
-                      num_prefill_tokens=n, max_query_len=77, max_seq_len=77, prefill_query_start_loc=qsl,
-                      sample_seq=sample_seq)
+                      logits_indices=torch.tensor([starts[1] - 1, starts[3] - 1], device=gpu), num_decodes=0,
+                      num_prefills=3, num_prefill_tokens=n, max_query_len=max(lens), max_seq_len=max(lens),
+                      prefill_query_start_loc=qsl, sample_seq=sample_seq)
     m = TransformerLM(cfg, gpu, torch.bfloat16)
     m.load_full_state(sd)
     out = {}

@@ -982,18 +982,38 @@ def test_paged_prefill_fused_rope(gpu, D, G):
 @pytest.mark.parametrize("T,D,hkv,slot_kind,kv_fp8", [
     (37, 64, 8, "run", False), (700, 64, 8, "run", False), (4099, 64, 8, "run", False),
     (700, 64, 8, "scrambled", False), (700, 64, 8, "run", True), (1030, 128, 8, "run", False),
-    (1030, 128, 1, "scrambled", True), (520, 128, 4, "run", False)])
+    (1030, 128, 1, "scrambled", True), (520, 128, 4, "run", False), (900, 64, 8, "mixed", False),
+    (1200, 64, 8, "mixed", True), (2000, 64, 8, "chunks", False)])
 def test_rope_kv_only(gpu, T, D, hkv, slot_kind, kv_fp8):
     """rope_and_cache with no q output (the per-token kernel below 512 tokens, kv_rope_t16_kernel at
     and above) writes exactly the K / V the full kernel writes: runs of whole blocks, runs starting
-    mid-block, scrambled slots with unmapped (-1) tokens, fp8 caches."""
+    mid-block, scrambled slots with unmapped (-1) tokens, fp8 caches; "mixed": a mixed step's
+    scattered decode rows first (num_decodes: the per-token kernel), then a mid-block prefill run;
+    "chunks": several prompts' chunks, each a run through its own non-adjacent blocks."""
     hq = 4 * hkv
     nb = (T + 15) // 16 + 8
     cos_sin = ref.build_cos_sin_cache(D, 8192, 500000.0, None, device=gpu)
     qkv = torch.randn(T, (hq + 2 * hkv) * D, device=gpu, dtype=torch.bfloat16)
     pos = torch.randint(0, 8000, (T,), device=gpu)
+    nd = 0
     if slot_kind == "run":
         slots = torch.arange(T, device=gpu) + 16 + (7 if T % 2 else 0)
+    elif slot_kind == "mixed":
+        nd = 300
+        base = (T // 16 + 4) * 16  # decode slots past the prefill run, scattered
+        slots = torch.cat([base + torch.randperm(4 * nd, device=gpu)[:nd], torch.arange(T - nd, device=gpu) + 5])
+        nb = (base + 4 * nd) // 16 + 1
+    elif slot_kind == "chunks":  # 3 prompts: blocks of each drawn from a shuffled pool
+        pool = torch.randperm(nb, device=gpu)
+        lens, out, bi = [700, 613, T - 1313], [], 0
+        for i, L in enumerate(lens):
+            start = 9 if i == 1 else 0  # a continuation chunk starting mid-block
+            nblk = (start + L + 15) // 16
+            blocks = pool[bi:bi + nblk]
+            bi += nblk
+            pos_in = torch.arange(start, start + L, device=gpu)
+            out.append(blocks[pos_in // 16] * 16 + pos_in % 16)
+        slots = torch.cat(out)
     else:
         slots = torch.randperm(nb * 16, device=gpu)[:T]
         slots[::13] = -1
@@ -1002,7 +1022,7 @@ def test_rope_kv_only(gpu, T, D, hkv, slot_kind, kv_fp8):
     kv_b = kv_a.clone()
     sc = dict(k_scale=0.05, v_scale=0.07) if kv_fp8 else {}
     ops.rope_and_cache(qkv, hq, hkv, D, pos, cos_sin, kv_a, slots, **sc)
-    q = ops.rope_kv_into_cache(qkv, hq, hkv, D, pos, cos_sin, kv_b, slots, **sc)
+    q = ops.rope_kv_into_cache(qkv, hq, hkv, D, pos, cos_sin, kv_b, slots, **sc, num_decodes=nd)
     # V is a copy (bit-exact); K's rotation may contract into FMAs differently per kernel (one rounding
     # step of the stored value at most)
     assert torch.equal(kv_a[:, 1].view(torch.uint8), kv_b[:, 1].view(torch.uint8))
