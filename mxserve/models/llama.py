@@ -265,7 +265,7 @@ class TransformerLM:
         context, i.e. exactly a decode query, so it runs on the decode kernel."""
         c, w, p = self.cfg, self.w, f"l{i}."
         x = h if qkv is None else qkv
-        if self._fused_q_rope(x, i, qkv is not None):
+        if _SAMPLED_QROPE and self._fused_q_rope(x, i, qkv is not None):
             # K / V of every token into the cache; q stays un-rotated in the qkv rows and only the
             # sampled rows' q is gathered and rotated inside the decode kernel (no [T, Hq, D] q write)
             if qkv is None:
@@ -457,6 +457,7 @@ class TransformerLM:
 
 
 _FUSED_Q_ROPE = os.environ.get("MXS_FUSED_Q_ROPE", "1") == "1"
+_SAMPLED_QROPE = os.environ.get("MXS_SAMPLED_QROPE", "1") == "1"  # pruned last layer: q rotated in-kernel
 
 
 def _pad_rows(t: torch.Tensor, n: int) -> torch.Tensor:

@@ -409,6 +409,9 @@ def linear_rope_and_cache(h: torch.Tensor, w: torch.Tensor, num_heads: int, num_
                           q_norm_w, k_norm_w, eps, k_scale, v_scale)
 
 
+_ROPE_SPLIT = os.environ.get("MXS_ROPE_SPLIT", "1") == "1"  # 0: one launch for mixed steps (A/B)
+
+
 def rope_kv_into_cache(qkv: torch.Tensor, num_heads: int, num_kv_heads: int, head_dim: int,
                        positions: torch.Tensor, cos_sin: torch.Tensor, kv_layer: torch.Tensor,
                        slot_mapping: torch.Tensor, k_scale: float = 1.0, v_scale: float = 1.0,
@@ -421,7 +424,7 @@ def rope_kv_into_cache(qkv: torch.Tensor, num_heads: int, num_kv_heads: int, hea
     tile of the launch."""
     T = qkv.shape[0]
     parts = [(0, T)]
-    if 0 < num_decodes < T and T - num_decodes >= 512:
+    if 0 < num_decodes < T and T - num_decodes >= 512 and _ROPE_SPLIT:
         parts = [(0, num_decodes), (num_decodes, T)]
     for a, b in parts:
         ext().rope_and_cache(None, qkv[a:b], positions[a:b], cos_sin, kv_layer, slot_mapping[a:b], None, None,
