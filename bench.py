@@ -103,7 +103,8 @@ def parse(argv=None):
                          "by the frontend's KV-aware router from the ranks' load reports "
                          "(mxserve/tools/arrival_hub.py); local = an independent stream per rank")
     ap.add_argument("--router-mode", choices=["kv", "round_robin", "random"], default="kv")
-    ap.add_argument("--max-num-seqs", type=int, default=384)
+    ap.add_argument("--max-num-seqs", type=int, default=int(os.environ.get("MXS_BENCH_MAX_SEQS", "448")),
+                    help="running-sequence cap (448: at QPS 49 the 384 cap made arrivals wait for a slot, TTFT p90 194 vs 82 ms, profiles/r4/s2/max_num_seqs/)")
     ap.add_argument("--disagg-max-num-seqs", type=int, default=512,
                     help="decode ranks of the disagg phase carry 2x the per-GPU request rate")
     ap.add_argument("--disagg-qps", type=float, default=float(os.environ.get("MXS_BENCH_DISAGG_QPS", "0")),
