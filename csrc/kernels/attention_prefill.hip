@@ -293,9 +293,7 @@ __device__ __forceinline__ uint4 ld8_kv(const char* p) {
 // [T, Hq, D] q tensor and its write + re-read disappear).  A lane's chunks ks and ks + KS / 2 hold
 // dims d and d + D / 2, i.e. both halves of its rotation pairs.  q is rounded to bf16 after the
 // rotation, as the standalone rope kernel stores it.
-// STAGE = false (experiment, MXS_PF_ATTN_NOSTAGE=1): tiles after the first are not staged (the loop
-// computes on the first tile's LDS image): the compute-only time of the loop, to price the staging
-template <int D, int G, int EB, bool STAGE = true>
+template <int D, int G, int EB>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(D == 64 ? 4 : 1, D == 64 ? 4 : 8)))
 paged_prefill_v3_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const void* __restrict__ kv, long block_stride,
@@ -558,11 +556,11 @@ paged_prefill_v3_kernel(
   sstore(0);
   __syncthreads();
   for (int it = 0, k0 = 0; k0 < nkeys; ++it, k0 += KT) {
-    const int buf = STAGE ? (it & 1) : 0;
+    const int buf = it & 1;
     const bool more = k0 + KT < nkeys;
-    if (STAGE && more) gload(k0 + KT);  // in flight under this tile's MFMAs
+    if (more) gload(k0 + KT);           // in flight under this tile's MFMAs
     if (k0 <= wave_max_pos) compute(buf, k0);  // waves whose rows all precede the tile skip it
-    if (STAGE && more) sstore(buf ^ 1);
+    if (more) sstore(buf ^ 1);
     __syncthreads();
   }
 
@@ -580,14 +578,6 @@ paged_prefill_v3_kernel(
       v.y = pack2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
       *reinterpret_cast<uint2*>(op + d0) = v;
     }
-}
-
-static bool pf_attn_nostage() {
-  static const bool v = [] {
-    const char* e = getenv("MXS_PF_ATTN_NOSTAGE");
-    return e != nullptr && e[0] == '1';
-  }();
-  return v;
 }
 
 // q_stride: elements between consecutive q rows (Hq * D for a dense q; (Hq + 2 Hkv) * D when q is
@@ -608,10 +598,6 @@ void launch_paged_prefill(bf16_t* out, const bf16_t* q, const void* kv_ptr, bool
     if (D == DD && G == GG) {                                                                              \
       if (kv_fp8)                                                                                          \
         hipLaunchKernelGGL((paged_prefill_v3_kernel<DD, GG, 1>), grid3, blk3, 0, s, out, q, kv_ptr,        \
-                           block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs, q_stride,    \
-                           qpos, cos_sin);                                                                 \
-      else if (pf_attn_nostage())                                                                          \
-        hipLaunchKernelGGL((paged_prefill_v3_kernel<DD, GG, 2, false>), grid3, blk3, 0, s, out, q, kv_ptr, \
                            block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs, q_stride,    \
                            qpos, cos_sin);                                                                 \
       else                                                                                                 \
