@@ -332,65 +332,92 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
 //   * the 4 partial 16 x 16 tiles meet in LDS; blockIdx.y is a k-group of 4 KR: one group writes
 //     bf16 Y, several write fp32 slabs [group][M][N] that the consumer sums (the split-K reduce, the
 //     fused rope / all-reduce + RMSNorm epilogues read slabs directly).
-template <int KR>
+// MF token fragments of 16 (M <= 16 MF): every W fragment feeds MF MFMAs against the matching X
+// fragments (tokens 16 f + r), so the weight is still read once while M grows to 64 (the TP-8 shard
+// shapes at decode batches 17-64, where hipBLASLt streams the narrow qkv at 0.6-0.8 TB/s); the KR
+// choices shrink with MF to hold the X fragments in registers.
+template <int KR, int MF>
 __global__ void __launch_bounds__(256) skinny_gemm_kernel(bf16_t* __restrict__ Y, float* __restrict__ part,
                                                           const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
                                                           int M, int N, int K, int ldx, int ldy) {
   constexpr int STEPS = KR / 32;
-  __shared__ float red[4][16][17];
+  __shared__ float red[4][16][16 * MF + 1];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r = lane & 15, q = lane >> 4;
   const int n0 = blockIdx.x * 16;
   const int k0 = (blockIdx.y * 4 + wid) * KR + 8 * q;
   const bf16_t* wp = W + static_cast<size_t>(n0 + r) * K + k0;
-  const bool xrow = r < M;
-  const bf16_t* xp = X + static_cast<size_t>(xrow ? r : 0) * ldx + k0;
-  u32x4 wf[STEPS], xf[STEPS];
+  u32x4 wf[STEPS], xf[MF][STEPS];
 #pragma unroll
   for (int s = 0; s < STEPS; ++s) wf[s] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wp + 32 * s));
 #pragma unroll
-  for (int s = 0; s < STEPS; ++s) {
-    xf[s] = *reinterpret_cast<const u32x4*>(xp + 32 * s);
-    if (!xrow) xf[s] = u32x4{0u, 0u, 0u, 0u};
+  for (int f = 0; f < MF; ++f) {
+    const int m = 16 * f + r;
+    const bool xrow = m < M;
+    const bf16_t* xp = X + static_cast<size_t>(xrow ? m : 0) * ldx + k0;
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      xf[f][s] = *reinterpret_cast<const u32x4*>(xp + 32 * s);
+      if (!xrow) xf[f][s] = u32x4{0u, 0u, 0u, 0u};
+    }
   }
-  float4_ acc = {0.f, 0.f, 0.f, 0.f};
+  float4_ acc[MF];
+#pragma unroll
+  for (int f = 0; f < MF; ++f) acc[f] = float4_{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < STEPS; ++s)
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wf[s]), as_bf16x8(xf[s]), acc, 0, 0, 0);
-  // acc[i] = C[n = 4 q + i][m = r]
 #pragma unroll
-  for (int i = 0; i < 4; ++i) red[wid][4 * q + i][r] = acc[i];
+    for (int f = 0; f < MF; ++f)
+      acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wf[s]), as_bf16x8(xf[f][s]), acc[f], 0, 0, 0);
+  // acc[f][i] = C[n = 4 q + i][m = 16 f + r]
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wid][4 * q + i][16 * f + r] = acc[f][i];
   __syncthreads();
   if (wid != 0) return;
-  // wave 0: 16 x 16 outputs, 4 per lane: n = 4 q + i, m = r
-  if (r >= M) return;
-  float v[4];
+  // wave 0: 16 x 16 MF outputs, 4 per lane and fragment: n = 4 q + i, m = 16 f + r
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int n = 4 * q + i;
-    v[i] = red[0][n][r] + red[1][n][r] + red[2][n][r] + red[3][n][r];
-  }
-  if (part != nullptr) {
-    float* pr = part + (static_cast<size_t>(blockIdx.y) * M + r) * N + n0 + 4 * q;
-    *reinterpret_cast<float4_*>(pr) = float4_{v[0], v[1], v[2], v[3]};
-  } else {
-    bf16_t* yr = Y + static_cast<size_t>(r) * ldy + n0 + 4 * q;
-    *reinterpret_cast<uint2*>(yr) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+  for (int f = 0; f < MF; ++f) {
+    const int m = 16 * f + r;
+    if (m >= M) continue;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = 4 * q + i;
+      v[i] = red[0][n][m] + red[1][n][m] + red[2][n][m] + red[3][n][m];
+    }
+    if (part != nullptr) {
+      float* pr = part + (static_cast<size_t>(blockIdx.y) * M + m) * N + n0 + 4 * q;
+      *reinterpret_cast<float4_*>(pr) = float4_{v[0], v[1], v[2], v[3]};
+    } else {
+      bf16_t* yr = Y + static_cast<size_t>(m) * ldy + n0 + 4 * q;
+      *reinterpret_cast<uint2*>(yr) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
   }
 }
 
 bool launch_skinny_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx,
                         int ldy, int KR, bool reduce, hipStream_t s) {
-  if (M <= 0 || M > 16 || N % 16 != 0 || ldx % 8 != 0 || ldy % 4 != 0 || (KR != 128 && KR != 256)) return false;
+  // M <= 16: KR 128 / 256; M <= 32 (two token fragments): 64 / 128; M <= 64 (four): 64 / 128
+  if (M <= 0 || M > 64 || N % 16 != 0 || ldx % 8 != 0 || ldy % 4 != 0) return false;
+  const int MF = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  if (MF == 1 ? (KR != 128 && KR != 256) : (KR != 64 && KR != 128)) return false;
   if (K % (4 * KR) != 0) return false;
   const int groups = K / (4 * KR);
   if (groups > 1 && part == nullptr) return false;
   dim3 grid(N / 16, groups), blk(256);
   float* p = groups > 1 ? part : nullptr;
-  if (KR == 128)
-    hipLaunchKernelGGL(skinny_gemm_kernel<128>, grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
-  else
-    hipLaunchKernelGGL(skinny_gemm_kernel<256>, grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
+  if (MF == 1) {
+    if (KR == 128) hipLaunchKernelGGL((skinny_gemm_kernel<128, 1>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
+    else hipLaunchKernelGGL((skinny_gemm_kernel<256, 1>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
+  } else if (MF == 2) {
+    if (KR == 64) hipLaunchKernelGGL((skinny_gemm_kernel<64, 2>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
+    else hipLaunchKernelGGL((skinny_gemm_kernel<128, 2>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
+  } else {
+    if (KR == 64) hipLaunchKernelGGL((skinny_gemm_kernel<64, 4>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
+    else hipLaunchKernelGGL((skinny_gemm_kernel<128, 4>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
+  }
   MXS_CHECK_LAUNCH();
   if (groups > 1 && reduce) {
     const long total4 = static_cast<long>(M) * N / 4;

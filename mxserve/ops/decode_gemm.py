@@ -50,7 +50,7 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
     waves through LDS, lu k-steps per group).  With mt (dense weights; the grouped MoE form passes
     mt=False), from M = MT_MIN_M on, also the medium-M kernel's ("mt", wm, wn, wnf, splitk)
     configurations, plus the persistent prefill kernel ("pf", 0) on the widest projections and the
-    skinny split-K form ("sk", kr, groups) at M <= 16."""
+    skinny split-K form ("sk", kr, groups) at M <= 64."""
     out = []
     for mf in ((1, 2, 4) if all_mf else (_mf(M),)):
         out += _candidates_mf(M, N, K, epi, mf)
@@ -69,8 +69,9 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
     if M >= PF_MIN_M and N % 256 == 0 and K % 64 == 0 and N >= PF_MIN_N:
         out.append(("pf", 0))
     # small batches: 16-column weight slices streamed with every load in flight (skinny_gemm_kernel)
-    if M <= 16 and not epi and N % 16 == 0:
-        out += [("sk", kr, K // (4 * kr)) for kr in (128, 256) if K % (4 * kr) == 0]
+    if M <= 64 and not epi and N % 16 == 0:
+        krs = (128, 256) if M <= 16 else (64, 128)  # 2 / 4 token fragments above 16 rows
+        out += [("sk", kr, K // (4 * kr)) for kr in krs if K % (4 * kr) == 0]
     return out
 
 

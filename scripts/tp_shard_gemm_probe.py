@@ -19,7 +19,7 @@ def main():
         w = (torch.randn(N, K, device=dev) * K ** -0.5).to(torch.bfloat16)
         ws = dg.weight_copies(w)
         dg.TABLE.part = torch.empty(32 * 64 * N, dtype=torch.float32, device=dev)
-        for M in (1, 8, 32):
+        for M in (1, 8, 32, 64):
             x = (torch.randn(M, K, device=dev) * 0.5).to(torch.bfloat16)
             out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             t_lib = dg._graph_time(lambda i: torch.nn.functional.linear(x, ws[i % len(ws)]))

@@ -523,7 +523,8 @@ def test_decode_gemm_all_configs(gpu, M, N, K, epi):
     assert any(c[4] for c in reg) or M <= 16, "LDS-form configurations are among the candidates"
     big = N * K * 2 >= decode_gemm.MT_SMALL_M_MIN_BYTES
     assert any(c[0] == "mt" for c in cands) == (M >= decode_gemm.MT_MIN_M or (M >= 8 and big))
-    assert any(c[0] == "sk" for c in cands) == (M <= 16 and not epi and N % 16 == 0 and K % 512 == 0)
+    assert any(c[0] == "sk" for c in cands) == (M <= 64 and not epi and N % 16 == 0 and
+                                                 K % (512 if M <= 16 else 256) == 0)
     decode_gemm.TABLE.part = part
     for c in cands:
         out = torch.full((M, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
@@ -1099,10 +1100,10 @@ def test_gemm_pf_residual(gpu, M, N, K):
         assert torch.equal(rr, out), "in place == out of place"
 
 
-@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("M", [1, 5, 16, 17, 32, 40, 64])
 @pytest.mark.parametrize("N,K", [(1280, 8192), (8192, 1024), (8192, 3584), (3072, 2048)])
 def test_skinny_gemm(gpu, M, N, K):
-    """skinny_gemm_kernel (M <= 16, 16-column W slices x 4 k-ranges per workgroup) vs an fp32
+    """skinny_gemm_kernel (M <= 64 in 1 / 2 / 4 token fragments, 16-column W slices x 4 k-ranges per workgroup) vs an fp32
     reference: bf16 output (one k-group or slabs summed by the reduce kernel) and the raw fp32 slabs
     [groups][M][N] a fused epilogue would read; Llama-3-70B TP-8 shard shapes and the 1B qkv."""
     g = torch.Generator(device="cuda").manual_seed(M * 131 + N + K)
@@ -1110,7 +1111,7 @@ def test_skinny_gemm(gpu, M, N, K):
     w = (torch.randn(N, K, device=gpu, generator=g) * K ** -0.5).to(torch.bfloat16)
     w[: N // 2] *= 1.5  # asymmetric: a transposed store shows
     want = x.float() @ w.float().t()
-    for kr in (128, 256):
+    for kr in ((128, 256) if M <= 16 else (64, 128)):
         if K % (4 * kr):
             continue
         groups = K // (4 * kr)
