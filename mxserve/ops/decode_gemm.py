@@ -24,7 +24,7 @@ import torch
 log = logging.getLogger(__name__)
 
 # largest decode batch the table serves (MXS_DECODE_GEMM_MAX_M; the graph buckets run to 384)
-MAX_M = int(os.environ.get("MXS_DECODE_GEMM_MAX_M", "384"))
+MAX_M = int(os.environ.get("MXS_DECODE_GEMM_MAX_M", "448"))  # the bench's 448-sequence cap
 # buckets the capture-time tuner measures (the whole decode-graph range): up to OLD_FORMS_MAX_M the
 # register / LDS forms compete, above it only the medium-M (mt) kernel, since the register-staged forms
 # measured 1.3-2.5x behind hipBLASLt there (profiles/r2_decode_gemm_probe_vs_hipblaslt.jsonl)
