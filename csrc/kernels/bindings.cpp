@@ -32,7 +32,8 @@ void launch_penalties(void*, bool, int, int, long, const int*, long, const int64
 void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStream_t);
 void launch_moe_align(int*, int*, const int*, int, int, int, int*, hipStream_t);
 void launch_moe_combine(bf16_t*, const bf16_t*, const float*, const int*, int, int, int, hipStream_t);
-bool launch_skinny_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, bool, hipStream_t);
+bool launch_skinny_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, bool, int,
+                        hipStream_t);
 bool launch_decode_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int,
                         int, hipStream_t, const int* = nullptr, int = 0, int = 0, int = 0, int = 1);
 bool launch_mt_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int, int,
@@ -320,21 +321,26 @@ bool decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::T
 
 // Skinny form (gemm_decode.hip skinny_gemm_kernel): M <= 16 rows, 16-column W slices x 4 k-ranges of
 // kr per workgroup; K / (4 kr) > 1 groups leave fp32 slabs [groups][M][N] in `part` (summed here when
-// reduce, else by the caller's epilogue).
-bool skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> part, int64_t kr, bool reduce) {
+// reduce, else by the caller's epilogue).  epi 1: w = [gate; up], out [M, N / 2] = SiLU(gate) * up (slabs
+// always written, reduce required).
+bool skinny_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> part, int64_t kr, bool reduce,
+                 int64_t epi) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
+  TORCH_CHECK(epi == 0 || epi == 1, "epi 0 (none) or 1 (SiLU*mul)");
   const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
-  TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == N, "shape mismatch");
+  TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == (epi ? N / 2 : N), "shape mismatch");
   if (x.stride(1) != 1 || out.stride(1) != 1 || kr <= 0 || K % (4 * kr) != 0) return false;
+  if (epi && (!reduce || N % 32 != 0)) return false;
   const int64_t groups = K / (4 * kr);
   float* p = nullptr;
-  if (groups > 1) {
+  if (groups > 1 || epi) {
     TORCH_CHECK(part.has_value() && part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
                     part->numel() >= groups * M * N, "split-K needs an fp32 workspace of groups * M * N");
     p = part->data_ptr<float>();
   }
-  return mxs::launch_skinny_gemm(bf(out), p, bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), kr, reduce, stream());
+  return mxs::launch_skinny_gemm(bf(out), p, bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), kr, reduce,
+                                 static_cast<int>(epi), stream());
 }
 
 // Medium-M form of the decode projection (gemm_decode.hip mt_gemm_kernel, M = 64-256 and short
@@ -529,7 +535,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("e_lo"), pybind11::arg("e_local"), pybind11::arg("inv") = pybind11::none());
   m.def("moe_combine", &moe_combine);
   m.def("skinny_gemm", &skinny_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
-        pybind11::arg("part") = pybind11::none(), pybind11::arg("kr") = 256, pybind11::arg("reduce") = true);
+        pybind11::arg("part") = pybind11::none(), pybind11::arg("kr") = 256, pybind11::arg("reduce") = true,
+        pybind11::arg("epi") = 0);
   m.def("decode_gemm", &decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("part"), pybind11::arg("mf"), pybind11::arg("nf"), pybind11::arg("wm"), pybind11::arg("splitk"),
         pybind11::arg("epi"), pybind11::arg("lu") = 0, pybind11::arg("reduce") = true);

@@ -353,12 +353,14 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(bf16_t* __restrict__ Y
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
     const int m = 16 * f + r;
-    const bool xrow = m < M;
-    const bf16_t* xp = X + static_cast<size_t>(xrow ? m : 0) * ldx + k0;
+    const bf16_t* xp = X + static_cast<size_t>(m) * ldx + k0;
+    // lanes of padded rows issue no X loads (at M = 1, 60 of 64 lanes): only W occupies the memory pipe
+    if (m < M) {
 #pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-      xf[f][s] = *reinterpret_cast<const u32x4*>(xp + 32 * s);
-      if (!xrow) xf[f][s] = u32x4{0u, 0u, 0u, 0u};
+      for (int s = 0; s < STEPS; ++s) xf[f][s] = *reinterpret_cast<const u32x4*>(xp + 32 * s);
+    } else {
+#pragma unroll
+      for (int s = 0; s < STEPS; ++s) xf[f][s] = u32x4{0u, 0u, 0u, 0u};
     }
   }
   float4_ acc[MF];
@@ -397,17 +399,21 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(bf16_t* __restrict__ Y
   }
 }
 
+// epi = EPI_SILU: W = [gate; up] (N = 2 inter rows), Y [M, inter] = SiLU(gate) * up -- the two halves
+// of an output column live in different workgroups, so every group writes its slab (even a single
+// one) and the reduce kernel applies SiLU*mul as it sums them.
 bool launch_skinny_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx,
-                        int ldy, int KR, bool reduce, hipStream_t s) {
+                        int ldy, int KR, bool reduce, int epi, hipStream_t s) {
   // M <= 16: KR 128 / 256; M <= 32 (two token fragments): 64 / 128; M <= 64 (four): 64 / 128
   if (M <= 0 || M > 64 || N % 16 != 0 || ldx % 8 != 0 || ldy % 4 != 0) return false;
+  if (epi != EPI_NONE && (epi != EPI_SILU || N % 32 != 0 || !reduce || part == nullptr)) return false;
   const int MF = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
   if (MF == 1 ? (KR != 128 && KR != 256) : (KR != 64 && KR != 128)) return false;
   if (K % (4 * KR) != 0) return false;
   const int groups = K / (4 * KR);
   if (groups > 1 && part == nullptr) return false;
   dim3 grid(N / 16, groups), blk(256);
-  float* p = groups > 1 ? part : nullptr;
+  float* p = groups > 1 || epi == EPI_SILU ? part : nullptr;
   if (MF == 1) {
     if (KR == 128) hipLaunchKernelGGL((skinny_gemm_kernel<128, 1>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
     else hipLaunchKernelGGL((skinny_gemm_kernel<256, 1>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
@@ -419,7 +425,13 @@ bool launch_skinny_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W
     else hipLaunchKernelGGL((skinny_gemm_kernel<128, 4>), grid, blk, 0, s, Y, p, X, W, M, N, K, ldx, ldy);
   }
   MXS_CHECK_LAUNCH();
-  if (groups > 1 && reduce) {
+  if (epi == EPI_SILU) {
+    const long total4 = static_cast<long>(M) * (N / 2) / 4;
+    const int blocks = static_cast<int>(std::min<long>((total4 + 255) / 256, 1024));
+    hipLaunchKernelGGL(splitk_reduce_kernel<EPI_SILU>, dim3(blocks), dim3(256), 0, s, Y, part, M, N, groups, ldy,
+                       N / 2);
+    MXS_CHECK_LAUNCH();
+  } else if (groups > 1 && reduce) {
     const long total4 = static_cast<long>(M) * N / 4;
     const int blocks = static_cast<int>(std::min<long>((total4 + 255) / 256, 1024));
     hipLaunchKernelGGL(splitk_reduce_kernel<EPI_NONE>, dim3(blocks), dim3(256), 0, s, Y, part, M, N, groups, ldy, 0);

@@ -57,9 +57,9 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
         if lds and mf > 1:  # one 16-row tile: the X fragment is as small as one W fragment
             out += _candidates_lds(N, K, epi, mf)
     # dense only (the grouped MoE form has no mt kernel); below MT_MIN_M only for large matrices,
-    # where it streams W at 5.3-5.6 TB/s (Llama-3-70B gate_up / down at M = 8-32,
-    # profiles/r2_mt_gemm_probe_70b_cold_weights.jsonl)
-    if mt and (M >= MT_MIN_M or (M >= 8 and N * K * 2 >= MT_SMALL_M_MIN_BYTES)):
+    # where its coalesced LDS-staged weight stream reaches 5.3-5.6 TB/s (Llama-3-70B gate_up / down at
+    # M = 8-32, profiles/r2_mt_gemm_probe_70b_cold_weights.jsonl) -- TP-8 shards of those included
+    if mt and (M >= MT_MIN_M or N * K * 2 >= MT_SMALL_M_MIN_BYTES):
         out += mt_candidates(M, N, K, epi)
     # the persistent 256 x 256-tile prefill kernel (gemm_pf.hip, data-parallel tiles) on the widest
     # projections only -- lm_head: 501 column tiles keep every CU busy at any batch; 154 vs 183 us at
@@ -68,8 +68,9 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
         return out
     if M >= PF_MIN_M and N % 256 == 0 and K % 64 == 0 and N >= PF_MIN_N:
         out.append(("pf", 0))
-    # small batches: 16-column weight slices streamed with every load in flight (skinny_gemm_kernel)
-    if M <= 64 and not epi and N % 16 == 0:
+    # small batches: 16-column weight slices streamed with every load in flight (skinny_gemm_kernel;
+    # SwiGLU: slabs + the SiLU*mul reduce)
+    if M <= 64 and N % (32 if epi else 16) == 0:
         krs = (128, 256) if M <= 16 else (64, 128)  # 2 / 4 token fragments above 16 rows
         out += [("sk", kr, K // (4 * kr)) for kr in krs if K % (4 * kr) == 0]
     return out
@@ -81,7 +82,7 @@ PF_MIN_N = 32768
 
 MT_MIN_M = 64
 SPLITS = (1, 2, 4, 8, 16, 32)  # split-K factors the tuner tries (16 / 32: narrow shards over a long K)
-MT_SMALL_M_MIN_BYTES = int(os.environ.get("MXS_MT_SMALL_M_MIN_BYTES", str(192 << 20)))
+MT_SMALL_M_MIN_BYTES = int(os.environ.get("MXS_MT_SMALL_M_MIN_BYTES", str(48 << 20)))
 MT_COUNTERS = 1 << 16  # tile counters of the in-launch split-K reduction (every launch leaves them zero)
 # in-launch split-K reduction (last arriver sums the slabs): measured slower than the separate reduce
 # kernel at every decode shape (agent-scope release per workgroup + a serial slab read), so opt-in
@@ -191,17 +192,17 @@ class DecodeGemmTable:
             return gemm_pf(x, w, epi, out, int(cfg[1])) is not None
         if cfg[0] == "sk":
             groups = w.shape[1] // (4 * int(cfg[1]))
-            if groups != cfg[2]:
+            if groups != cfg[2] or (epi and not reduce):
                 return False
             part = None
-            if groups > 1:
+            if groups > 1 or epi:
                 need = groups * x.shape[0] * w.shape[0]
                 if self.part is None or self.part.numel() < need:
                     if torch.cuda.is_current_stream_capturing():
                         return False
                     self.part = torch.empty(need, dtype=torch.float32, device=x.device)
                 part = self.part
-            return bool(ext().skinny_gemm(out, x, w, part, int(cfg[1]), reduce))
+            return bool(ext().skinny_gemm(out, x, w, part, int(cfg[1]), reduce, int(epi)))
         mt = cfg[0] == "mt"
         if mt:
             wm, wn, mr, wnf, sk = cfg[1:6]

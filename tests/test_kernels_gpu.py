@@ -522,8 +522,8 @@ def test_decode_gemm_all_configs(gpu, M, N, K, epi):
     reg = [c for c in cands if isinstance(c[0], int)]
     assert any(c[4] for c in reg) or M <= 16, "LDS-form configurations are among the candidates"
     big = N * K * 2 >= decode_gemm.MT_SMALL_M_MIN_BYTES
-    assert any(c[0] == "mt" for c in cands) == (M >= decode_gemm.MT_MIN_M or (M >= 8 and big))
-    assert any(c[0] == "sk" for c in cands) == (M <= 64 and not epi and N % 16 == 0 and
+    assert any(c[0] == "mt" for c in cands) == (M >= decode_gemm.MT_MIN_M or big)
+    assert any(c[0] == "sk" for c in cands) == (M <= 64 and N % (32 if epi else 16) == 0 and
                                                  K % (512 if M <= 16 else 256) == 0)
     decode_gemm.TABLE.part = part
     for c in cands:
@@ -1125,3 +1125,34 @@ def test_skinny_gemm(gpu, M, N, K):
             slabs = part.view(groups, M, N).sum(0)
             _close(slabs, want, atol=2e-2, rtol=2e-2, name=f"skinny slabs {M}x{N}x{K} kr{kr}")
             assert torch.isnan(out2.float()).all(), "reduce=False must leave the output untouched"
+
+
+@pytest.mark.parametrize("M", [1, 8, 16, 32, 64])
+@pytest.mark.parametrize("N,K", [(7168, 8192), (16384, 2048), (2 * 1792, 1024)])
+def test_skinny_gemm_swiglu(gpu, M, N, K):
+    """skinny_gemm_kernel with the SiLU*mul reduce (epi 1: w = [gate; up], out = SiLU(x gate^T) * (x up^T))
+    vs an fp32 reference: Llama-3-70B TP-8 gate_up shard, the 1B gate_up, and a one-k-group shape (the
+    single slab still goes through the reduce)."""
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
+    x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16, generator=g)
+    w = (torch.randn(N, K, device=gpu, generator=g) * K ** -0.5).to(torch.bfloat16)
+    w[N // 2:] *= 1.5  # gate / up halves differ: a swapped pair shows
+    y = x.float() @ w.float().t()
+    I = N // 2
+    want = torch.nn.functional.silu(y[:, :I]) * y[:, I:]
+    for kr in ((128, 256) if M <= 16 else (64, 128)):
+        if K % (4 * kr):
+            continue
+        groups = K // (4 * kr)
+        part = torch.full((groups * M * N,), float("nan"), dtype=torch.float32, device=gpu)
+        out = torch.full((M, I), float("nan"), device=gpu, dtype=torch.bfloat16)
+        assert ops.ext().skinny_gemm(out, x, w, part, kr, True, 1)
+        _close(out, want, atol=2e-2, rtol=2e-2, name=f"skinny swiglu {M}x{N}x{K} kr{kr}")
+        assert not ops.ext().skinny_gemm(out, x, w, part, kr, False, 1), "SwiGLU needs the reduce"
+    from mxserve.ops import decode_gemm
+    for cfg in decode_gemm.candidates(M, N, K, 1):
+        if cfg[0] == "sk":
+            out = torch.full((M, I), float("nan"), device=gpu, dtype=torch.bfloat16)
+            decode_gemm.TABLE.part = None
+            assert decode_gemm.TABLE.run(out, x, w, cfg, 1), cfg
+            _close(out, want, atol=2e-2, rtol=2e-2, name=f"TABLE.run {cfg}")
