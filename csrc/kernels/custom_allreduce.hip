@@ -255,19 +255,34 @@ __global__ void __launch_bounds__(512) car_add_rmsnorm_kernel(
     if (part == nullptr) return reinterpret_cast<const uint4*>(x)[v];
     const float* p = part + v * 8;
     float4 a = *reinterpret_cast<const float4*>(p), c = *reinterpret_cast<const float4*>(p + 4);
-    for (int s2 = 1; s2 < S; ++s2) {
-      const float4 a2 = *reinterpret_cast<const float4*>(p + s2 * slab);
-      const float4 c2 = *reinterpret_cast<const float4*>(p + s2 * slab + 4);
-      a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
-      c.x += c2.x; c.y += c2.y; c.z += c2.z; c.w += c2.w;
+    // 4 slabs' loads in flight at a time, summed in slab order (no load -> add round trip per slab)
+    for (int s0 = 1; s0 < S; s0 += 4) {
+      float4 a2[4], c2[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t o = static_cast<size_t>(s0 + j < S ? s0 + j : 0) * slab;
+        a2[j] = *reinterpret_cast<const float4*>(p + o);
+        c2[j] = *reinterpret_cast<const float4*>(p + o + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (s0 + j < S) {
+          a.x += a2[j].x; a.y += a2[j].y; a.z += a2[j].z; a.w += a2[j].w;
+          c.x += c2[j].x; c.y += c2[j].y; c.z += c2[j].z; c.w += c2[j].w;
+        }
     }
     return make_uint4(pack2(a.x, a.y), pack2(a.z, a.w), pack2(c.x, c.y), pack2(c.z, c.w));
   };
   auto sum_slots = [&](const char* base, long v) -> uint4 {  // fp32 sum over ranks, rank order
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int r = 0; r < nranks; ++r) {
-      const uint4 q = reinterpret_cast<const uint4*>(base + r * slot_elems * 2)[v];
-      const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+    uint4 q[kArMaxRanks];  // every rank's slot loaded before the first add (one round trip, not nranks)
+#pragma unroll
+    for (int r = 0; r < kArMaxRanks; ++r)
+      if (r < nranks) q[r] = reinterpret_cast<const uint4*>(base + r * slot_elems * 2)[v];
+#pragma unroll
+    for (int r = 0; r < kArMaxRanks; ++r) {
+      if (r >= nranks) break;
+      const uint32_t u[4] = {q[r].x, q[r].y, q[r].z, q[r].w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         acc[2 * k] += bf2f_lo(u[k]);

@@ -305,10 +305,24 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(bf16_t* __restrict__
        q += static_cast<long>(gridDim.x) * blockDim.x) {
     const int m = static_cast<int>((q * 4) / ncols), n = static_cast<int>((q * 4) % ncols);
     float4_ g = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < S; ++s) {
-      const float* row = part + (static_cast<size_t>(s) * M + m) * static_cast<size_t>(N);
-      g += *reinterpret_cast<const float4_*>(row + n);
-      if (EPI == EPI_SILU) u += *reinterpret_cast<const float4_*>(row + inter + n);
+    const size_t sstride = static_cast<size_t>(M) * N;
+    const float* row0 = part + static_cast<size_t>(m) * N + n;
+    // 4 slabs' loads in flight at a time, summed in slab order (a load -> add chain pays one L2 round
+    // trip per slab)
+    for (int s0 = 0; s0 < S; s0 += 4) {
+      float4_ bg[4], bu[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float* row = row0 + (s0 + j < S ? s0 + j : 0) * sstride;
+        bg[j] = *reinterpret_cast<const float4_*>(row);
+        if (EPI == EPI_SILU) bu[j] = *reinterpret_cast<const float4_*>(row + inter);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (s0 + j < S) {
+          g += bg[j];
+          if (EPI == EPI_SILU) u += bu[j];
+        }
     }
     float v[4];
 #pragma unroll

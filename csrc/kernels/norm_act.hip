@@ -126,11 +126,22 @@ __global__ void __launch_bounds__(1024) splitk_add_rmsnorm_kernel(bf16_t* __rest
     if (c < nvec) {
       const float* p = part + static_cast<size_t>(row) * H + c * 8;
       float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-      for (int s = 1; s < S; ++s) {
-        const float4 a2 = *reinterpret_cast<const float4*>(p + s * slab);
-        const float4 b2 = *reinterpret_cast<const float4*>(p + s * slab + 4);
-        a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
-        b.x += b2.x; b.y += b2.y; b.z += b2.z; b.w += b2.w;
+      // 4 slabs' loads in flight at a time, summed in slab order (a load -> add chain costs one L2
+      // round trip per slab, the whole latency of a batch-1 row)
+      for (int s0 = 1; s0 < S; s0 += 4) {
+        float4 a2[4], b2[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const size_t o = static_cast<size_t>(s0 + j < S ? s0 + j : 0) * slab;
+          a2[j] = *reinterpret_cast<const float4*>(p + o);
+          b2[j] = *reinterpret_cast<const float4*>(p + o + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (s0 + j < S) {
+            a.x += a2[j].x; a.y += a2[j].y; a.z += a2[j].z; a.w += a2[j].w;
+            b.x += b2[j].x; b.y += b2[j].y; b.z += b2[j].z; b.w += b2[j].w;
+          }
       }
       const float y[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
       const uint4 rv = *reinterpret_cast<const uint4*>(rr + c * 8);

@@ -5,6 +5,8 @@
 //   contiguous 16-byte load per lane).
 // cos/sin come from a host-precomputed fp32 table (cdna_hip_programming.md App. B: no device trig).
 // KT = bf16_t, or fp8_t for an fp8 (e4m3fn) cache: K and V stored as x / k_scale, x / v_scale.
+#include <algorithm>
+
 #include "common.h"
 
 namespace mxs {
@@ -20,8 +22,17 @@ struct QkvRow {
   size_t slab;
   __device__ __forceinline__ float operator[](int j) const {
     if constexpr (SLABS) {
+      // the slabs' loads issued 8 at a time, summed in slab order (a serial load -> add chain costs
+      // one L2 round trip per slab: ~8 us for a TP-8 qkv shard's 8 slabs at batch 1)
       float a = prow[j];
-      for (int s = 1; s < S; ++s) a += prow[s * slab + j];
+      for (int s0 = 1; s0 < S; s0 += 8) {
+        float b[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) b[u] = s0 + u < S ? prow[(s0 + u) * slab + j] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (s0 + u < S) a += b[u];
+      }
       return bf2f(f2bf(a));
     } else {
       return bf2f(row[j]);
@@ -55,7 +66,11 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
   // nullptr: K / V only (the attention kernels read q from the qkv rows and rotate it themselves)
   const int hbeg = q_out != nullptr ? 0 : Hq;
   const int n_items = (Hq + Hkv - hbeg) * HALF;
-  for (int base = 0; base < n_items; base += blockDim.x) {
+  // blockIdx.y splits a token's items over gridDim.y workgroups (small decode batches: a token per
+  // workgroup alone leaves the chip idle); bases stay multiples of blockDim.x, so a head's pairs
+  // stay in one wave for the q/k-norm shuffles
+  const int ystep = gridDim.y * blockDim.x;
+  for (int base = blockIdx.y * blockDim.x; base < n_items; base += ystep) {
     const int i = base + threadIdx.x;
     const bool active = i < n_items;
     const int head = hbeg + (active ? i / HALF : 0);
@@ -94,7 +109,7 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
   // V: copy into the dim-major half of the block
   const int v0 = (Hq + Hkv) * D;
   KT* vblk = kblk + static_cast<size_t>(Hkv) * BS * D;
-  for (int j = threadIdx.x; j < Hkv * D; j += blockDim.x) {
+  for (int j = blockIdx.y * blockDim.x + threadIdx.x; j < Hkv * D; j += ystep) {
     const int h = j / D, d = j % D;
     KT* dst = vblk + (static_cast<size_t>(h) * D + d) * BS + off;
     if constexpr (sizeof(KT) == 2 && !SLABS)
@@ -387,6 +402,13 @@ __global__ void __launch_bounds__(256) kv_rope_t16_kernel(
   }
 }
 
+// workgroups per token of rope_cache_kernel: up to one per 256 items at small decode batches
+static int rope_grid_y(int T, int Hq, int Hkv, int D) {
+  if (T > 64) return 1;
+  const int items = std::max((Hq + Hkv) * (D / 2), Hkv * D);
+  return std::min(8, (items + 255) / 256);
+}
+
 template <typename KT>
 static void launch_rope_typed(bf16_t* q_out, const bf16_t* qkv, const int64_t* positions, const float* cos_sin,
                               KT* kv, long block_stride, const int64_t* slot_mapping, const bf16_t* qn,
@@ -421,7 +443,7 @@ static void launch_rope_typed(bf16_t* q_out, const bf16_t* qkv, const int64_t* p
     MXS_CHECK_LAUNCH();
     return;
   }
-  dim3 g(T), b(256);
+  dim3 g(T, rope_grid_y(T, Hq, Hkv, D)), b(256);
 #define MXS_ROPE_CASE(DD)                                                                                   \
   if (D == DD) {                                                                                            \
     if (norm)                                                                                               \
@@ -444,7 +466,7 @@ static void launch_rope_slabs_typed(bf16_t* q_out, const float* part, int S, con
                                     const float* cos_sin, KT* kv, long block_stride, const int64_t* slot_mapping,
                                     const bf16_t* qn, const bf16_t* kn, int T, int Hq, int Hkv, int D, int BS, float eps,
                                     float kis, float vis, hipStream_t s) {
-  dim3 g(T), b(256);
+  dim3 g(T, rope_grid_y(T, Hq, Hkv, D)), b(256);
 #define MXS_ROPE_SLAB(DD)                                                                                      \
   if (D == DD) {                                                                                               \
     if (qn != nullptr)                                                                                         \

@@ -889,7 +889,8 @@ def test_linear_add_rms_norm_splitk_epilogue(gpu, M, N, K, cfg, monkeypatch):
 
 
 @pytest.mark.parametrize("M,cfg,qknorm", [(1, (1, 2, 1, 8, 0), False), (7, (1, 2, 1, 4, 0), True),
-                                          (192, ("mt", 4, 2, 1, 2, 4), False)])
+                                          (192, ("mt", 4, 2, 1, 2, 4), False), (1, ("sk", 128, 4), False),
+                                          (5, ("sk", 128, 4), True), (40, ("sk", 64, 8), False)])
 def test_linear_rope_and_cache_splitk(gpu, M, cfg, qknorm, monkeypatch):
     """qkv projection run split-K with its fp32 slabs summed inside the rope / cache-write kernel
     (rope_cache.hip rope_cache_kernel<SLABS>) vs hipBLASLt + the plain rope_and_cache kernel."""
