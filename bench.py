@@ -47,7 +47,8 @@ tok/s and windows of 200 iterations (2 s) 16.9-19.8k, against ~20.3k over 1,500 
 steps of 50 iterations is a ~9 s window, a couple of request lifetimes.  The
 warmup runs at least W steps and
 until the open-loop system is in steady state on every rank: over the last two windows the mean
-running set is flat and completions match arrivals (or --max-warmup-s passes; reported).  Then a
+running set is flat, completions match arrivals and two request lifetimes have passed (or
+--max-warmup-s passes; reported).  Then a
 short soak collects TTFT samples in steady state, and exactly K steps are timed between a
 barrier + device sync on both sides.  value = output tokens produced in the timed window summed
 over ranks / the slowest rank's window.  TTFT is measured from each request's scheduled Poisson
@@ -333,6 +334,7 @@ class Driver:
         self.horizon = 65536
         self.arrivals = np.cumsum(rng.exponential(1.0 / qps, size=self.horizon))
         self.isl = a.isl
+        self.osl = a.osl
         self.vocab = vocab
         self.rng = rng
         self.rank = rank
@@ -345,6 +347,7 @@ class Driver:
         self.record_ttft = False  # steady state reached: TTFT samples count from here
         self.record = False  # timed window: tokens + ITL
         self.finished = 0
+        self.lifetimes: list = []  # arrival -> last token of finished requests (steady-state test)
         self.warmup_steps = 0
         self.warmup_s = 0.0
         self.steady = False
@@ -398,6 +401,8 @@ class Driver:
 
     def token(self, rid: str, now: float, finished: bool = False) -> None:
         self.finished += finished
+        if finished and rid in self.arrival_of:
+            self.lifetimes.append(now - self.arrival_of[rid])
         if rid not in self.first_tok:
             self.first_tok[rid] = now
             if self.record_ttft:
@@ -412,13 +417,25 @@ class Driver:
         self.hist.append((time.perf_counter(), running, self.nxt, self.finished))
 
     def is_steady(self, window: float) -> bool:
-        """Running set flat over two consecutive windows and completions ~= arrivals in the last."""
+        """Running set flat over two consecutive windows, completions ~= arrivals in the last, and two
+        request lifetimes since the load started (OSL x the current iteration time, or the median
+        lifetime of the last 20 finished requests if longer -- not the ramp's short small-batch ones):
+        one lifetime in, the running set still holds the ramp's requests, served at the small-batch
+        ITL, so it reads flat a few seconds before the system settles (warmups of ~12 s here timed a
+        window at ~93 % of the offered rate, ~19 s ones at ~98 %)."""
         if not self.hist or self.finished == 0:
             return False
         t_now = self.hist[-1][0]
         if t_now - self.t_start < 2 * window:
             return False
         h = np.asarray(self.hist, dtype=np.float64)
+        # the lifetime a request admitted now will have: OSL iterations at the current iteration time
+        # (each engine iteration gives every running request one token), not the ramp's shorter ones
+        recent = h[h[:, 0] >= t_now - window]
+        if len(recent) >= 2:
+            life_now = self.osl * (recent[-1, 0] - recent[0, 0]) / (len(recent) - 1)
+            if t_now - self.t_start < 2.0 * max(life_now, float(np.median(self.lifetimes[-20:])) if self.lifetimes else 0.0):
+                return False
         a_mask = (h[:, 0] >= t_now - 2 * window) & (h[:, 0] < t_now - window)
         b_mask = h[:, 0] >= t_now - window
         if a_mask.sum() < 5 or b_mask.sum() < 5:
