@@ -19,19 +19,21 @@
 namespace mxs {
 void launch_copy_blocks(char*, const char*, const int*, const int*, int, long, hipStream_t);
 constexpr int kArMaxRanks = 8;
-struct ArPeers {
+struct ArPeers {  // custom_allreduce.hip
   char* recv[kArMaxRanks];
   unsigned* flags[kArMaxRanks];
+  long long timeout_ticks;
 };
 void launch_custom_allreduce(unsigned short*, const unsigned short*, long, const ArPeers&, int, int, long, unsigned*,
-                             unsigned*, hipStream_t);
+                             hipStream_t);
 void launch_custom_allreduce_2shot(unsigned short*, const unsigned short*, long, const ArPeers&, int, int, long,
-                                   unsigned*, unsigned*, hipStream_t);
-void launch_ipc_all_to_all(void*, const void*, long, const ArPeers&, int, int, long, unsigned*, unsigned*,
-                           hipStream_t, const int*, long);
+                                   unsigned*, hipStream_t);
+void launch_ipc_all_to_all(void*, const void*, long, const ArPeers&, int, int, long, unsigned*, hipStream_t,
+                           const int*, long);
 void launch_car_add_rmsnorm(unsigned short*, unsigned short*, const unsigned short*, const float*, int, int, int,
-                            const unsigned short*, float, const ArPeers&, int, int, long, unsigned*, unsigned*, bool,
+                            const unsigned short*, float, const ArPeers&, int, int, long, unsigned*, bool,
                             hipStream_t);
+void launch_car_poll_err(unsigned*, const ArPeers&, int, hipStream_t);
 void launch_ep_route(int*, int*, int*, const int*, int, int, int, int, int, int, hipStream_t);
 void launch_ep_gather_rows(unsigned short*, const unsigned short*, const int*, int, int, int, int, hipStream_t);
 void launch_ep_segment_rows(int*, const int*, int, int, hipStream_t);
@@ -137,28 +139,68 @@ void host_register(int64_t ptr, int64_t bytes) {
 }
 void host_unregister(int64_t ptr) { (void)hipHostUnregister(reinterpret_cast<void*>(ptr)); }
 
-int64_t car_read_u32(int64_t ptr) {  // synchronous 4-byte device -> host read (error word)
-  unsigned v = 0;
-  hip_check(hipMemcpy(&v, reinterpret_cast<void*>(ptr), sizeof(v), hipMemcpyDeviceToHost), "hipMemcpy");
-  return v;
-}
-
-void custom_allreduce(at::Tensor out, at::Tensor x, std::vector<int64_t> recv_ptrs, std::vector<int64_t> flag_ptrs,
-                      int64_t rank, int64_t slot_elems, int64_t epochs_ptr, int64_t err_ptr, bool two_shot) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "x: contiguous bf16 GPU tensor");
-  TORCH_CHECK(out.is_contiguous() && out.numel() == x.numel(), "out shape");
+mxs::ArPeers make_peers(const std::vector<int64_t>& recv_ptrs, const std::vector<int64_t>& flag_ptrs,
+                        int64_t timeout_ticks) {
   const int n = static_cast<int>(recv_ptrs.size());
   TORCH_CHECK(n >= 1 && n <= mxs::kArMaxRanks && static_cast<int>(flag_ptrs.size()) == n, "1..8 ranks");
-  TORCH_CHECK(x.numel() % 8 == 0 && x.numel() <= slot_elems, "numel must be a multiple of 8 and fit a slot");
+  TORCH_CHECK(timeout_ticks > 0, "timeout_ticks must be positive");
   mxs::ArPeers peers{};
   for (int r = 0; r < n; ++r) {
     peers.recv[r] = reinterpret_cast<char*>(recv_ptrs[r]);
     peers.flags[r] = reinterpret_cast<unsigned*>(flag_ptrs[r]);
   }
+  peers.timeout_ticks = timeout_ticks;
+  return peers;
+}
+
+void custom_allreduce(at::Tensor out, at::Tensor x, std::vector<int64_t> recv_ptrs, std::vector<int64_t> flag_ptrs,
+                      int64_t rank, int64_t slot_elems, int64_t epochs_ptr, int64_t timeout_ticks, bool two_shot) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "x: contiguous bf16 GPU tensor");
+  TORCH_CHECK(out.is_contiguous() && out.numel() == x.numel(), "out shape");
+  const mxs::ArPeers peers = make_peers(recv_ptrs, flag_ptrs, timeout_ticks);
+  const int n = static_cast<int>(recv_ptrs.size());
+  TORCH_CHECK(rank >= 0 && rank < n, "rank out of range");
+  TORCH_CHECK(x.numel() % 8 == 0 && x.numel() <= slot_elems, "numel must be a multiple of 8 and fit a slot");
   auto launch = two_shot ? mxs::launch_custom_allreduce_2shot : mxs::launch_custom_allreduce;
   launch(reinterpret_cast<unsigned short*>(out.data_ptr()), reinterpret_cast<const unsigned short*>(x.data_ptr()),
          x.numel(), peers, static_cast<int>(rank), n, slot_elems, reinterpret_cast<unsigned*>(epochs_ptr),
-         reinterpret_cast<unsigned*>(err_ptr), c10::hip::getCurrentHIPStream().stream());
+         c10::hip::getCurrentHIPStream().stream());
+}
+
+// Every rank's error word -> out (uint32 [>= n], host-pinned), ordered on the current stream.
+void car_poll_err(at::Tensor out, std::vector<int64_t> recv_ptrs, std::vector<int64_t> flag_ptrs) {
+  TORCH_CHECK(out.is_pinned() && out.scalar_type() == at::kInt && out.numel() >= static_cast<int64_t>(flag_ptrs.size()),
+              "out: pinned int32 [>= ranks]");
+  const mxs::ArPeers peers = make_peers(recv_ptrs, flag_ptrs, 1);
+  void* dev = nullptr;
+  hip_check(hipHostGetDevicePointer(&dev, out.data_ptr(), 0), "hipHostGetDevicePointer");
+  mxs::launch_car_poll_err(static_cast<unsigned*>(dev), peers, static_cast<int>(flag_ptrs.size()),
+                           c10::hip::getCurrentHIPStream().stream());
+}
+
+// n consecutive uint32 words of device memory (a signal page's error word / give-up record), read
+// synchronously: fault diagnosis and tests only, never on the step loop.
+std::vector<int64_t> car_read_words(int64_t ptr, int64_t n) {
+  TORCH_CHECK(n > 0 && n <= 4096, "1..4096 words");
+  std::vector<unsigned> v(static_cast<size_t>(n), 0u);
+  hip_check(hipMemcpy(v.data(), reinterpret_cast<void*>(ptr), sizeof(unsigned) * n, hipMemcpyDeviceToHost),
+            "hipMemcpy");
+  return std::vector<int64_t>(v.begin(), v.end());
+}
+
+// Zero n bytes of this rank's signal page (epochs, flags, error word, records) after every rank
+// has quiesced: the collective restarts from epoch 1 everywhere.
+void car_clear(int64_t ptr, int64_t bytes) {
+  hip_check(hipMemset(reinterpret_cast<void*>(ptr), 0, static_cast<size_t>(bytes)), "hipMemset");
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+}
+
+// Wall-clock counter rate of the device (kHz): converts the wait budget to device ticks.
+int64_t car_wall_clock_khz() {
+  int dev = 0, khz = 0;
+  hip_check(hipGetDevice(&dev), "hipGetDevice");
+  hip_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev), "hipDeviceGetAttribute");
+  return khz > 0 ? khz : 100000;
 }
 
 // A HIP stream restricted to a subset of the CUs (hipExtStreamCreateWithCUMask): bit i of the mask
@@ -185,7 +227,7 @@ void stream_destroy(int64_t stream) { (void)hipStreamDestroy(reinterpret_cast<hi
 // or part (fp32 split-K slabs [S][M][H]); residual [M, H] is updated in place.
 void car_add_rms_norm(at::Tensor h, at::Tensor residual, c10::optional<at::Tensor> x, c10::optional<at::Tensor> part,
                       at::Tensor w, double eps, std::vector<int64_t> recv_ptrs, std::vector<int64_t> flag_ptrs,
-                      int64_t rank, int64_t slot_elems, int64_t epochs_ptr, int64_t err_ptr, bool two_shot) {
+                      int64_t rank, int64_t slot_elems, int64_t epochs_ptr, int64_t timeout_ticks, bool two_shot) {
   TORCH_CHECK(residual.is_cuda() && residual.scalar_type() == at::kBFloat16 && residual.is_contiguous() &&
                   residual.dim() == 2, "residual: contiguous bf16 [M, H] GPU tensor");
   const int M = residual.size(0), H = residual.size(1);
@@ -207,38 +249,30 @@ void car_add_rms_norm(at::Tensor h, at::Tensor residual, c10::optional<at::Tenso
     TORCH_CHECK(S >= 1, "at least one slab");
     pp = part->data_ptr<float>();
   }
+  const mxs::ArPeers peers = make_peers(recv_ptrs, flag_ptrs, timeout_ticks);
   const int n = static_cast<int>(recv_ptrs.size());
-  TORCH_CHECK(n >= 1 && n <= mxs::kArMaxRanks && static_cast<int>(flag_ptrs.size()) == n, "1..8 ranks");
-  mxs::ArPeers peers{};
-  for (int r = 0; r < n; ++r) {
-    peers.recv[r] = reinterpret_cast<char*>(recv_ptrs[r]);
-    peers.flags[r] = reinterpret_cast<unsigned*>(flag_ptrs[r]);
-  }
+  TORCH_CHECK(rank >= 0 && rank < n, "rank out of range");
   if (M == 0) return;
   mxs::launch_car_add_rmsnorm(reinterpret_cast<unsigned short*>(h.data_ptr()),
                               reinterpret_cast<unsigned short*>(residual.data_ptr()), xp, pp, S, M, H,
                               reinterpret_cast<const unsigned short*>(w.data_ptr()), static_cast<float>(eps), peers,
-                              static_cast<int>(rank), n, slot_elems, reinterpret_cast<unsigned*>(epochs_ptr),
-                              reinterpret_cast<unsigned*>(err_ptr), two_shot, c10::hip::getCurrentHIPStream().stream());
+                              static_cast<int>(rank), n, slot_elems, reinterpret_cast<unsigned*>(epochs_ptr), two_shot,
+                              c10::hip::getCurrentHIPStream().stream());
 }
 
 // equal splits: out/in hold N segments of seg_bytes each; segment d of `in` goes to rank d
 void ipc_all_to_all(at::Tensor out, at::Tensor in, std::vector<int64_t> recv_ptrs, std::vector<int64_t> flag_ptrs,
-                    int64_t rank, int64_t slot_bytes, int64_t epochs_ptr, int64_t err_ptr,
+                    int64_t rank, int64_t slot_bytes, int64_t epochs_ptr, int64_t timeout_ticks,
                     c10::optional<at::Tensor> push_rows, int64_t row_bytes) {
   TORCH_CHECK(in.is_cuda() && in.is_contiguous() && out.is_contiguous(), "contiguous GPU tensors");
   TORCH_CHECK(in.scalar_type() == out.scalar_type() && in.numel() == out.numel(), "in/out shape");
+  const mxs::ArPeers peers = make_peers(recv_ptrs, flag_ptrs, timeout_ticks);
   const int n = static_cast<int>(recv_ptrs.size());
-  TORCH_CHECK(n >= 1 && n <= mxs::kArMaxRanks && static_cast<int>(flag_ptrs.size()) == n, "1..8 ranks");
+  TORCH_CHECK(rank >= 0 && rank < n, "rank out of range");
   const long bytes = in.numel() * in.element_size();
   TORCH_CHECK(bytes % n == 0, "equal splits");
   const long seg = bytes / n;
   TORCH_CHECK(seg % 4 == 0 && seg <= slot_bytes, "segment must be a multiple of 4 bytes and fit a slot");
-  mxs::ArPeers peers{};
-  for (int r = 0; r < n; ++r) {
-    peers.recv[r] = reinterpret_cast<char*>(recv_ptrs[r]);
-    peers.flags[r] = reinterpret_cast<unsigned*>(flag_ptrs[r]);
-  }
   const int* pr = nullptr;
   if (push_rows.has_value()) {
     const at::Tensor& t = *push_rows;
@@ -248,8 +282,8 @@ void ipc_all_to_all(at::Tensor out, at::Tensor in, std::vector<int64_t> recv_ptr
     pr = t.data_ptr<int>();
   }
   mxs::launch_ipc_all_to_all(out.data_ptr(), in.data_ptr(), seg, peers, static_cast<int>(rank), n, slot_bytes,
-                             reinterpret_cast<unsigned*>(epochs_ptr), reinterpret_cast<unsigned*>(err_ptr),
-                             c10::hip::getCurrentHIPStream().stream(), pr, row_bytes);
+                             reinterpret_cast<unsigned*>(epochs_ptr), c10::hip::getCurrentHIPStream().stream(), pr,
+                             row_bytes);
 }
 
 // ---- EP dispatch (csrc/kernels/ep.hip)
@@ -292,22 +326,25 @@ void ep_segment_rows(at::Tensor counts, at::Tensor ids, int64_t C) {
 void register_comm(pybind11::module_& m) {
   m.def("car_alloc", &car_alloc);
   m.def("car_free", &car_free);
-  m.def("car_read_u32", &car_read_u32);
+  m.def("car_read_words", &car_read_words);
+  m.def("car_clear", &car_clear);
+  m.def("car_wall_clock_khz", &car_wall_clock_khz);
+  m.def("car_poll_err", &car_poll_err);
   m.def("host_register", &host_register);
   m.def("host_unregister", &host_unregister);
   m.def("custom_allreduce", &custom_allreduce, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("recv_ptrs"),
         pybind11::arg("flag_ptrs"), pybind11::arg("rank"), pybind11::arg("slot_elems"), pybind11::arg("epochs_ptr"),
-        pybind11::arg("err_ptr"), pybind11::arg("two_shot") = false);
+        pybind11::arg("timeout_ticks"), pybind11::arg("two_shot") = false);
   m.def("cu_mask_stream", &cu_mask_stream);
   m.def("stream_cu_mask", &stream_cu_mask);
   m.def("stream_destroy", &stream_destroy);
   m.def("car_add_rms_norm", &car_add_rms_norm, pybind11::arg("h"), pybind11::arg("residual"), pybind11::arg("x"),
         pybind11::arg("part"), pybind11::arg("w"), pybind11::arg("eps"), pybind11::arg("recv_ptrs"),
         pybind11::arg("flag_ptrs"), pybind11::arg("rank"), pybind11::arg("slot_elems"), pybind11::arg("epochs_ptr"),
-        pybind11::arg("err_ptr"), pybind11::arg("two_shot") = false);
+        pybind11::arg("timeout_ticks"), pybind11::arg("two_shot") = false);
   m.def("ipc_all_to_all", &ipc_all_to_all, pybind11::arg("out"), pybind11::arg("in"), pybind11::arg("recv_ptrs"),
         pybind11::arg("flag_ptrs"), pybind11::arg("rank"), pybind11::arg("slot_bytes"), pybind11::arg("epochs_ptr"),
-        pybind11::arg("err_ptr"), pybind11::arg("push_rows") = pybind11::none(), pybind11::arg("row_bytes") = 0);
+        pybind11::arg("timeout_ticks"), pybind11::arg("push_rows") = pybind11::none(), pybind11::arg("row_bytes") = 0);
   m.def("ep_route", &ep_route);
   m.def("ep_gather_rows", &ep_gather_rows);
   m.def("ep_segment_rows", &ep_segment_rows);

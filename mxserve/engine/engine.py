@@ -17,6 +17,7 @@ from ..config import EngineArgs
 from ..models.config import get_model_config
 from .kv_manager import KVCacheManager
 from .model_runner import ModelRunner
+from ..parallel.custom_allreduce import CollectiveFault
 from .request import Request, SamplingParams, Status
 from .scheduler import Scheduler
 from ..utils import gcpause
@@ -52,6 +53,7 @@ class LLMEngine:
         self.num_steps = 0
         self.num_generated = 0
         self.num_prompt_computed = 0
+        self.num_collective_faults = 0  # TP steps discarded and recomputed after a custom all-reduce fault
         self.check_invariants = False
         # async scheduling: the launched-but-not-collected step (scheduler output, runner handle)
         self.async_scheduling = bool(args.async_scheduling)
@@ -200,15 +202,18 @@ class LLMEngine:
         if done is None:
             return []
         dso, dh = done
-        if late is not None:
-            ev = dh.get("ev")
-            pending = ev is not None and not ev.query()
-            sampled = self.runner.collect(dh)
-            t_done = done_state.get("done") if done_state else None
-            late.observe_done(done_state, t_done if t_done is not None else
-                              (time.perf_counter() if pending else None), dh.get("gpu_s"))
-        else:
-            sampled = self.runner.collect(dh)
+        try:
+            if late is not None:
+                ev = dh.get("ev")
+                pending = ev is not None and not ev.query()
+                sampled = self.runner.collect(dh)
+                t_done = done_state.get("done") if done_state else None
+                late.observe_done(done_state, t_done if t_done is not None else
+                                  (time.perf_counter() if pending else None), dh.get("gpu_s"))
+            else:
+                sampled = self.runner.collect(dh)
+        except CollectiveFault as fault:
+            return self._recover_collective_fault(dso, fault)
         cb = self.scheduler.chunk_budget
         if cb is not None:
             from .pacing import step_features
@@ -225,6 +230,28 @@ class LLMEngine:
         tm["land"] += time.perf_counter() - t3
         tm["steps"] += 1
         return out
+
+    def _recover_collective_fault(self, so, fault: CollectiveFault) -> list[StepOutput]:
+        """A TP collective gave up during step `so` (runner.collect raised before anything of it
+        landed).  Nothing of that step, nor of the step already in flight behind it (its inputs may
+        be the faulted step's tokens), reaches a client: both are drained and discarded, their
+        requests rewound to the positions those steps were computing (the scheduler recomputes the
+        same positions with the same sampling counters, so seeded and greedy outputs are unchanged),
+        and the collective path is re-armed -- or, after repeated faults, turned off -- on every
+        rank before the next step."""
+        inflight, self._inflight = self._inflight, None
+        steps = [so]
+        if inflight is not None:
+            self.runner.drain(inflight[1])
+            steps.append(inflight[0])
+        n = self.scheduler.rewind(steps)
+        self.runner.recover_collectives(fault)
+        self.num_collective_faults += 1
+        if self._late is not None:
+            self._late.inflight = self._late.pending_next = None
+            self._late.last_done = None
+        log.error("collective fault: discarded %d step(s), rewound %d request(s)", len(steps), n)
+        return []
 
     def _land(self, so, sampled: dict, logprobs: Optional[dict] = None) -> list[StepOutput]:
         emitted = self.scheduler.update(so, sampled)
@@ -256,6 +283,7 @@ class LLMEngine:
     def stats(self) -> dict:
         s = self.scheduler.stats()
         s.update(num_steps=self.num_steps, num_generated=self.num_generated, **self.runner.kv_stats())
+        s["custom_ar_timeouts"] = self.num_collective_faults
         la = self._late
         if la is not None:
             s["late_admission"] = {"waits": la.waits, "late_wakes": la.late, "margin_ms": round(1e3 * la.margin, 3),

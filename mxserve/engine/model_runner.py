@@ -27,7 +27,8 @@ from ..config import EngineArgs
 from ..models.config import ModelConfig
 from ..models.llama import AttnMetadata, build_model
 from ..models.weights import load_weights
-from ..parallel.comm import collectives_capturable, get_tp, setup_meta_ring, tp_broadcast_object
+from ..parallel.comm import collectives_capturable, get_tp, setup_meta_ring, tp_barrier, tp_broadcast_object
+from ..parallel.custom_allreduce import CollectiveFault
 from .scheduler import SchedulerOutput
 
 log = logging.getLogger(__name__)
@@ -171,7 +172,16 @@ class ModelRunner:
             self._out_events = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
             self._start_events = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             self._start_slot = 0
+        # custom all-reduce health: every TP step's end polls each rank's error word into one of two
+        # pinned arrays (engine.py discards and recomputes a step whose poll is non-zero)
+        self.collective_faults = 0
+        self._err_slot = 0
+        if self.is_gpu and get_tp().tp_size > 1 and get_tp().custom_ar is not None:
+            self._err_pinned = [torch.zeros(8, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+            self._err_events = [torch.cuda.Event(), torch.cuda.Event()]
         self.graphs: dict[int, tuple] = {}
+        if get_tp().tp_size > 1:  # every rank's start-up work is done before the first collective
+            tp_barrier()
         if self.is_gpu and not args.enforce_eager:
             self._capture_graphs()
 
@@ -375,16 +385,24 @@ class ModelRunner:
             t0ev = self._start_events[self._start_slot]
             t0ev.record()
         tp = get_tp()
+        car = tp.custom_ar if tp.tp_size > 1 and self.is_gpu else None
+        if car is not None and car.disabled:
+            car = None
         if tp.tp_size > 1:
             self._steps += 1
-            # error words are host-mapped uncached memory: a few 4-byte reads, so check every step
-            # (a peer timeout surfaces within the steps still in flight, not 512 steps later)
-            if tp.custom_ar is not None and not tp.custom_ar.disabled and not tp.custom_ar.check():
-                meta["car_disable"] = True
-                self._disable_custom_ar()
             tp_broadcast_object(("step", self.buf.host_bytes(), meta))
+            _fault_injection(self._steps, tp.tp_rank)
         ids = self.execute_host(meta)
         handle = {"so": so, "rows": meta["sample_rows"]}
+        if car is not None:
+            # every TP step, sampling or not: a fault is caught at the step that contains it
+            self._err_slot ^= 1
+            handle["err"] = self._err_pinned[self._err_slot]
+            car.poll_into(handle["err"])
+            if ids is None:
+                ev = self._err_events[self._err_slot]
+                ev.record()
+                handle["ev"] = ev
         if ids is None:
             return handle
         lp = None
@@ -416,6 +434,11 @@ class ModelRunner:
             return {}
         if "ev" in handle:
             handle["ev"].synchronize()
+            err = handle.get("err")
+            if err is not None and any(err.tolist()):
+                raise CollectiveFault([int(v) for v in err.tolist()])
+            if "pinned" not in handle:
+                return {}
             if handle.get("ev0") is not None:
                 handle["gpu_s"] = handle["ev0"].elapsed_time(handle["ev"]) * 1e-3
             ids = handle["pinned"].tolist()
@@ -434,6 +457,11 @@ class ModelRunner:
     def execute(self, so: SchedulerOutput) -> dict[str, int]:
         return self.collect(self.launch(so))
 
+    def drain(self, handle: Optional[dict]) -> None:
+        """Wait for a launched step without reading its results (it is being discarded)."""
+        if handle is not None and "ev" in handle:
+            handle["ev"].synchronize()
+
     @torch.inference_mode()
     def execute_host(self, meta: dict):
         """Run one step on this rank; returns the device tensor of sampled ids (or None)."""
@@ -451,21 +479,54 @@ class ModelRunner:
             msg = tp_broadcast_object(None)
             if msg is None or msg[0] == "shutdown":
                 return
-            _, host_bytes, meta = msg
-            if meta.get("car_disable"):
-                self._disable_custom_ar()
+            kind, host_bytes, meta = msg
+            if kind == "car_reset":
+                self._reset_collectives(meta)
+                continue
+            self._steps += 1
+            _fault_injection(self._steps, get_tp().tp_rank)
             # the previous step's non_blocking H2D copy may still be reading the pinned buffer
             self.buf.wait_free()
             self.buf.load_host_bytes(host_bytes)
             self.execute_host(meta)
 
-    def _disable_custom_ar(self) -> None:
-        """Every rank at the same step: RCCL from now on; the captured graphs still hold the custom
-        all-reduce kernels, so decode runs eagerly."""
+    def recover_collectives(self, fault: CollectiveFault) -> None:
+        """Driver rank, after a custom all-reduce fault (its steps already discarded by the engine):
+        log the diagnosis, then re-arm the path on every rank -- or, after MXS_CAR_MAX_FAULTS faults,
+        turn it off and re-capture the decode graphs over RCCL."""
         tp = get_tp()
-        if tp.custom_ar is not None:
-            tp.custom_ar.disabled = True
-        self.graphs.clear()
+        car = tp.custom_ar
+        diag = car.diagnose() if car is not None else []
+        self.collective_faults += 1
+        self.last_collective_fault = {"error_words": fault.words, "ranks": diag}
+        limit = int(os.environ.get("MXS_CAR_MAX_FAULTS", "3"))
+        meta = {"disable": self.collective_faults >= limit}
+        log.error("custom all-reduce fault %d (%s): %s", self.collective_faults,
+                  "turning it off" if meta["disable"] else "re-arming", self.last_collective_fault)
+        tp_broadcast_object(("car_reset", None, meta))
+        self._reset_collectives(meta)
+
+    def _reset_collectives(self, meta: dict) -> None:
+        """Every rank, in step order: quiesce, barrier, clear this rank's signal page, barrier.  With
+        meta["disable"]: all-reduces go to RCCL from now on and the decode graphs (which hold the custom
+        kernels) are re-captured over it when the group's backend can be captured (RCCL), else decode
+        runs eagerly (gloo functional runs)."""
+        tp = get_tp()
+        car = tp.custom_ar
+        if self.is_gpu:
+            torch.cuda.synchronize()
+        tp_barrier()
+        if car is not None:
+            car.faults += 1
+            if meta.get("disable"):
+                car.disabled = True
+            else:
+                car.reset()
+        tp_barrier()
+        if meta.get("disable"):
+            self.graphs.clear()
+            if self.is_gpu and not self.args.enforce_eager:
+                self._capture_graphs(tune=False)
 
     def shutdown_followers(self) -> None:
         if get_tp().tp_size > 1 and get_tp().tp_rank == 0:
@@ -537,7 +598,7 @@ class ModelRunner:
         self.last_tok.index_copy_(0, v["srows"], ids)
         return ids, logits
 
-    def _capture_graphs(self) -> None:
+    def _capture_graphs(self, tune: bool = True) -> None:
         maxb = min(self.args.cuda_graph_max_bs or min(self.args.max_num_seqs, 512), self.args.max_num_seqs)
         m = self.model
         # largest collective message of a decode step at batch b: the all-reduces of [b, H] and the
@@ -547,6 +608,12 @@ class ModelRunner:
         if not buckets:
             log.warning("no decode bucket has graph-capturable collectives; decode runs eagerly")
             return
+        if tune:
+            self._tune_gemms(buckets)
+        self._capture(buckets)
+
+    def _tune_gemms(self, buckets: list) -> None:
+        m = self.model
         # decode projection GEMMs: hand-written MFMA kernel vs hipBLASLt, measured per bucket
         from ..ops import decode_gemm
         w = m.w
@@ -589,6 +656,8 @@ class ModelRunner:
                 from ..ops import moe as moe_ops
                 self.moe_gemm_report = moe_ops.tune(w["l0.w13"], w["l0.w2"], buckets, self.cfg.num_experts_per_tok,
                                                     self.cfg.num_experts, m.e_offset, self.device)
+
+    def _capture(self, buckets: list) -> None:
         self._arange = torch.arange(max(buckets), dtype=torch.int64, device=self.device)
         # benign contents for capture: every row is a 1-token sequence that writes nowhere
         h = self.buf.hn
@@ -637,3 +706,15 @@ class ModelRunner:
         return {"num_blocks": self.num_blocks, "block_bytes": self.block_bytes,
                 "kv_bytes": self.num_blocks * self.block_bytes}
 
+
+
+def _fault_injection(step: int, rank: int) -> None:
+    """MXS_FAULT="car_delay:rank=R:step=K:ms=T" (tests): TP rank R sleeps T ms before launching its
+    K-th step, so its peers' custom all-reduce waits run out (with MXS_CAR_TIMEOUT_MS < T)."""
+    from ..utils.tracing import FAULTS
+    kv = FAULTS.args.get("car_delay")
+    if kv is None:
+        return
+    if int(kv.get("rank", 1)) == rank and int(kv.get("step", 5)) == step:
+        log.warning("MXS_FAULT: rank %d sleeping %s ms before step %d", rank, kv.get("ms", "1000"), step)
+        time.sleep(float(kv.get("ms", "1000")) / 1e3)

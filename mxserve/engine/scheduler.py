@@ -276,6 +276,24 @@ class Scheduler:
             emitted.append(req)
         return emitted
 
+    def rewind(self, outs: list) -> int:
+        """Undo launched-but-never-landed steps (their results were discarded: a collective fault).
+        Each request goes back to the first position those steps computed and forgets their pending
+        samples; its blocks stay allocated (the recomputation writes the same slots) and no block
+        those steps wrote was registered in the prefix cache (registration happens at update).
+        Returns the number of requests rewound."""
+        seen = set()
+        for out in outs:
+            for s in out.all():
+                req = s.req
+                if s.sample:
+                    req.num_pending = max(0, req.num_pending - 1)
+                if req.is_finished:
+                    continue
+                req.num_computed_tokens = min(req.num_computed_tokens, s.start)
+                seen.add(req.request_id)
+        return len(seen)
+
     def release_blocks(self, req: Request) -> None:
         self.kv.free(req)
 

@@ -77,6 +77,11 @@ class WorkerMetrics:
                                      registry=r)
         self.kv_xfer_lat = Histogram("dynamo_component_kv_transfer_seconds", "KV transfer latency", ["model"],
                                      buckets=_LAT, registry=r)
+        # TP steps discarded and recomputed because a custom all-reduce wait ran out (engine.py
+        # _recover_collective_fault); any increase is worth an alert
+        self.car_timeouts = Counter("dynamo_component_custom_ar_timeouts", "Custom all-reduce faults recovered",
+                                    ["model"], registry=r)
+        self._car_seen: dict = {}
 
     def update(self, model: str, stats: dict) -> None:
         tot = stats.get("kv_total_blocks", 0)
@@ -87,6 +92,9 @@ class WorkerMetrics:
         self.hit_rate.labels(model).set(stats.get("prefix_hit_rate", 0.0))
         self.running.labels(model).set(stats.get("num_running", 0))
         self.waiting.labels(model).set(stats.get("num_waiting", 0))
+        n = int(stats.get("custom_ar_timeouts", 0))
+        self.car_timeouts.labels(model).inc(max(0, n - self._car_seen.get(model, 0)))
+        self._car_seen[model] = max(n, self._car_seen.get(model, 0))
 
     def render(self) -> bytes:
         return generate_latest(self.registry)

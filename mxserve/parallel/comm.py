@@ -86,6 +86,13 @@ def init_distributed(tp_size: int, backend: Optional[str] = None, device: Option
     return st
 
 
+def tp_barrier() -> None:
+    """CPU-group barrier of the TP group (no-op at TP 1)."""
+    st = _STATE
+    if st.tp_size > 1:
+        dist.barrier(group=st.cpu_group or st.group)
+
+
 def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     st = _STATE
     if st.tp_size == 1:

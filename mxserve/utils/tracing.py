@@ -139,14 +139,18 @@ class Faults:
     def __init__(self, spec: Optional[str] = None):
         spec = os.environ.get("MXS_FAULT", "") if spec is None else spec
         self.p: dict = {}
+        self.args: dict = {}  # structured faults, e.g. "car_delay:rank=2:step=6:ms=1500" -> {rank: "2", ...}
         for item in filter(None, (x.strip() for x in spec.split(","))):
             k, _, v = item.partition(":")
+            if "=" in v:
+                self.args[k] = dict(kv.split("=", 1) for kv in v.split(":") if "=" in kv)
+                continue
             self.p[k] = float(v or 1)
         self._rng = random.Random(int(os.environ.get("MXS_FAULT_SEED", "0")))
         self.tokens = 0
 
     def active(self) -> bool:
-        return bool(self.p)
+        return bool(self.p or self.args)
 
     def hit(self, name: str) -> bool:
         p = self.p.get(name, 0.0)

@@ -50,7 +50,7 @@ def _rank(rank, world, port, name, moe_dispatch, custom_ar, q):
         assert (st.custom_ar is not None) == custom_ar
         got = _logits(name, moe_dispatch)
         if custom_ar:
-            assert st.custom_ar.check(), "custom collective timed out"
+            assert st.custom_ar.check(), ("custom collective timed out", st.custom_ar.diagnose())
         ref = None
         if rank == 0:
             comm.set_tp(comm.ParallelState())  # the same model unsharded, in this process

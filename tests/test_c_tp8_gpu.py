@@ -65,7 +65,7 @@ def _rank(rank, world, port, q, model=MODEL_70B_2L, moe_dispatch="allreduce"):
         cfg = get_model_config(model)
         full = random_full_state(cfg, seed=4, std=0.02, dtype=torch.bfloat16, device="cuda:0")
         got = _logits(full, model=model, moe_dispatch=moe_dispatch)
-        assert st.custom_ar.check(), "custom all-reduce timed out"
+        assert st.custom_ar.check(), ("custom all-reduce timed out", st.custom_ar.diagnose())
         ref = None
         if rank == 0:
             comm.set_tp(comm.ParallelState())  # the same weights unsharded, in this process
@@ -152,7 +152,7 @@ def _ep_rank(rank, world, port, q, T):
             got = moe_a2a(x, gate, w13.unsqueeze(0).contiguous(), w2.unsqueeze(0).contiguous(), K, rank, world,
                           st.group)
         torch.cuda.synchronize()
-        assert st.custom_ar.check(), "custom all-reduce timed out"
+        assert st.custom_ar.check(), ("custom all-reduce timed out", st.custom_ar.diagnose())
         ref = None
         if rank == 0:
             S = (T + world - 1) // world

@@ -122,7 +122,7 @@ def _rank(rank, world, port, q):
                 if not torch.equal(r2.cpu(), rr) or (h.cpu().float() - hr.float()).abs().max().item() > 0.05:
                     errs.append(f"graph rep {rep} call {k}")
         dist.barrier()
-        assert car.check(), "error word raised"
+        assert car.check(), ("error word raised", car.diagnose())
         q.put((rank, errs))
     except BaseException:  # noqa: BLE001
         q.put((rank, [traceback.format_exc()]))

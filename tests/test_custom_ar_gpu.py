@@ -108,7 +108,7 @@ def _rank(rank, world, port, q):
         if not torch.equal(out.float(), want(4096, 40)):
             errs.append("all-reduce after an agent's ipc_close")
         dist.barrier()
-        assert car.check(), "error word raised"
+        assert car.check(), ("error word raised", car.diagnose())
         dist.barrier()
         q.put((rank, errs))
     except BaseException:  # noqa: BLE001

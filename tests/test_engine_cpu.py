@@ -214,3 +214,38 @@ def test_step_timing(monkeypatch):
     ref = _engine(True)
     assert ref.step_times is None
     assert ref.generate([list(range(5, 30)), list(range(40, 52))], sp) == out
+
+
+@pytest.mark.parametrize("async_sched,blocks,budget", [(True, 256, 64), (True, 14, 48), (False, 256, 64)])
+def test_collective_fault_discards_and_recomputes(async_sched, blocks, budget):
+    """A custom all-reduce fault surfaces at collect (runner raises CollectiveFault): the faulted step
+    and the one in flight behind it must never reach a client -- the requests are rewound and the
+    same positions recomputed, so every stream equals the fault-free run token for token (greedy and
+    seeded sampling, chunked prefill, prefix hits, preemption), and the fault is counted."""
+    from mxserve.parallel.custom_allreduce import CollectiveFault
+    reqs = _workload(1)
+    ref_out, ref_tok = _run(_engine(async_sched, blocks, budget), reqs)
+    eng = _engine(async_sched, blocks, budget)
+    real_collect = eng.runner.collect
+    calls = {"n": 0, "recovered": 0}
+    fault_at = {3, 9, 10, 17, 30}
+
+    def collect(handle):
+        calls["n"] += 1
+        if calls["n"] in fault_at:
+            eng.runner.drain(handle)
+            raise CollectiveFault([0, 2])
+        return real_collect(handle)
+
+    def recover(fault):
+        assert fault.words == [0, 2]
+        calls["recovered"] += 1
+
+    eng.runner.collect = collect
+    eng.runner.recover_collectives = recover
+    out, tok = _run(eng, reqs)
+    assert out == ref_out
+    assert tok == ref_tok
+    assert calls["recovered"] == len(fault_at) == eng.stats()["custom_ar_timeouts"]
+    assert eng.kv.num_free() == blocks and eng.kv.check_invariants()
+    assert not eng.requests and eng._inflight is None
