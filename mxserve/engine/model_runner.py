@@ -27,7 +27,8 @@ from ..config import EngineArgs
 from ..models.config import ModelConfig
 from ..models.llama import AttnMetadata, build_model
 from ..models.weights import load_weights
-from ..parallel.comm import collectives_capturable, get_tp, setup_meta_ring, tp_barrier, tp_broadcast_object
+from ..parallel.comm import (collectives_capturable, collectives_local, get_tp, setup_meta_ring, tp_barrier,
+                             tp_broadcast_object)
 from ..parallel.custom_allreduce import CollectiveFault
 from .scheduler import SchedulerOutput
 
@@ -121,8 +122,10 @@ class ModelRunner:
         self.kv_dtype = torch.uint8 if self.kv_fp8 else self.dtype
         if self.kv_fp8 and "MXS_KV_SCALE" not in os.environ:
             self.model.calibrate_kv_scales(self.bs)
-        # norm-folded weights of the fused prefill chain: allocated before the KV pool is sized
-        self.model.prepare_fused_prefill()
+        # norm-folded weights of the fused prefill chain: allocated before the KV pool is sized, and
+        # only those the start-up tuner (not run under enforce_eager) may still choose
+        self.model.prepare_fused_prefill(tuning=self.is_gpu and not args.enforce_eager,
+                                         max_rows=args.max_num_batched_tokens + args.max_num_seqs)
         self.num_blocks = self._determine_num_blocks()
         m = self.model
         self.kv_cache = torch.zeros(self.num_blocks, cfg.num_layers, 2, m.nkv, self.bs, cfg.head_dim,
@@ -642,10 +645,11 @@ class ModelRunner:
             pf_w = {k: (v[0], v[1]) for k, v in shapes.items() if k != "lm_head"}
             self.prefill_pf_report = prefill_pf.tune(pf_w, self.args.max_num_batched_tokens + self.args.max_num_seqs,
                                                      self.device, self.dtype)
-            if m.wf:  # the fused prefill chain (llama.py _forward_pf): each fused form vs its unfused one
-                fw = {"qkv": (w["l0.qkv"], m.wf["l0.qkv"], prefill_pf.CODE_RS),
-                      "gate_up": (w["l0.gate_up"], m.wf["l0.gate_up"], prefill_pf.CODE_RS_SWIGLU),
-                      "o": (w["l0.o"], None, prefill_pf.CODE_RESID), "down": (w["l0.down"], None, prefill_pf.CODE_RESID)}
+            if getattr(m, "pf_chain", False):  # the fused prefill chain (llama.py _forward_pf): fused vs unfused
+                fw = {"o": (w["l0.o"], None, prefill_pf.CODE_RESID), "down": (w["l0.down"], None, prefill_pf.CODE_RESID)}
+                for p, code in (("qkv", prefill_pf.CODE_RS), ("gate_up", prefill_pf.CODE_RS_SWIGLU)):
+                    if "l0." + p in m.wf:  # folded only where the stored table does not reject it
+                        fw[p] = (w["l0." + p], m.wf["l0." + p], code)
                 rep = prefill_pf.tune_fused(fw, self.args.max_num_batched_tokens + self.args.max_num_seqs,
                                             self.device, self.dtype, self.cfg.rms_norm_eps)
                 self.prefill_pf_report = self.prefill_pf_report + rep
@@ -677,8 +681,19 @@ class ModelRunner:
         t0 = time.time()
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
+        tp_rank = get_tp().tp_rank
         with torch.inference_mode():
             for b in sorted(buckets, reverse=True):
+                # the warm-up runs collectives: every rank starts it together.  Host work per rank
+                # differs in length (the previous bucket's capture + hipGraph instantiation, first-call
+                # library loads), and at TP on one shared GPU it spread ranks by over the all-reduce
+                # wait budget (profiles/r5/car_timeout/README.md)
+                tb = time.time()
+                if get_tp().tp_size > 1 and not self.cfg.is_moe:
+                    with collectives_local():  # first-call loads at this rank's own pace (comm.py)
+                        self._graph_body(b)
+                torch.cuda.synchronize()
+                tp_barrier()
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
@@ -687,9 +702,12 @@ class ModelRunner:
                 torch.cuda.current_stream().wait_stream(s)
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
+                tc = time.time()
                 with torch.cuda.graph(g, pool=pool):
                     out, logits = self._graph_body(b)
                 self.graphs[b] = (g, out, logits)
+                log.info("rank %d bucket %d: barrier+warm-up %.2fs, capture %.2fs", tp_rank, b, tc - tb,
+                          time.time() - tc)
         torch.cuda.synchronize()
         log.info("captured %d decode graphs (%s) in %.1fs", len(buckets), buckets, time.time() - t0)
 

@@ -444,7 +444,7 @@ class Frontend:
         tried: set = set()
         generated: list = []
         for attempt in range(4):
-            pick = self._choose(model, token_ids, sampling, generated, tried, attempt)
+            pick = self._choose(model, token_ids, sampling, generated, tried, attempt, rid)
             if pick is None:
                 break
             w, ids, sp, purl = pick
@@ -457,6 +457,7 @@ class Frontend:
                         return
                 raise ConnectionError(f"worker {w.worker_id} ended the stream early")
             except _STREAM_ERRORS as e:
+                self.router.forget(w, rid)
                 self._attempt_failed(model, w, e, generated, tried)
             finally:
                 w.inflight -= 1
@@ -469,7 +470,7 @@ class Frontend:
         tried: set = set()
         generated = ps.generated
         for attempt in range(4):
-            pick = self._choose(model, token_ids, sampling, generated, tried, attempt)
+            pick = self._choose(model, token_ids, sampling, generated, tried, attempt, rid)
             if pick is None:
                 break
             w, ids, sp, purl = pick
@@ -481,6 +482,7 @@ class Frontend:
                 from .fastpath import ClientGone
                 if isinstance(e, ClientGone):  # nobody to stream to: no retry
                     raise
+                self.router.forget(w, rid)
                 self._attempt_failed(model, w, e, generated, tried)
             finally:
                 w.inflight -= 1
@@ -530,7 +532,8 @@ class Frontend:
                 self._bg.add(t)
                 t.add_done_callback(self._bg.discard)
 
-    def _choose(self, model: str, token_ids: list, sampling: dict, generated: list, tried: set, attempt: int):
+    def _choose(self, model: str, token_ids: list, sampling: dict, generated: list, tried: set, attempt: int,
+                rid: Optional[str] = None):
         """(decode / agg worker, token ids, sampling, prefill URL) of the next attempt, or None: the
         router's pick among the workers not tried yet; after a failure mid-stream the ids are prompt +
         generated and the budget what is left (migration).  A decode worker gets a prefill worker of
@@ -544,7 +547,7 @@ class Frontend:
         if generated:
             sp = dict(sampling, max_tokens=int(sampling.get("max_tokens", 16)) - len(generated),
                       min_tokens=max(0, int(sampling.get("min_tokens") or 0) - len(generated)))
-        w, overlap = self.router.pick(decode, ids)
+        w, overlap = self.router.pick(decode, ids, request_id=rid)
         tr = _TRACE.get()
         if tr is not None and attempt == 0:
             tr.mark("routed")

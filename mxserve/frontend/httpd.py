@@ -83,11 +83,18 @@ class Connection(asyncio.Protocol):
         self._arm()
 
     # ------------------------------------------------------------------ timeouts
-    def _arm(self) -> None:
-        """Idle connection: IDLE_TIMEOUT_S; a request partly received: HEADER_TIMEOUT_S from its first
-        byte; a request being answered: no timer."""
-        want = "" if (self.busy or self.closed) else ("head" if self.buf else "idle")
-        if want == self._timer_kind:
+    def _arm(self, progress: bool = False) -> None:
+        """Idle connection: IDLE_TIMEOUT_S; a request head partly received: HEADER_TIMEOUT_S from its
+        first byte; a head received and its body still arriving: HEADER_TIMEOUT_S from the LAST
+        chunk (`progress` re-arms it), so a large upload that keeps moving is never cut off; a
+        request being answered: no timer."""
+        if self.busy or self.closed:
+            want = ""
+        elif not self.buf:
+            want = "idle"
+        else:  # find() stops at the first match: cheap even with a large body buffered
+            want = "body" if self.buf.find(b"\r\n\r\n") >= 0 else "head"
+        if want == self._timer_kind and not (progress and want == "body"):
             return
         if self._timer is not None:
             self._timer.cancel()
@@ -95,14 +102,14 @@ class Connection(asyncio.Protocol):
         self._timer_kind = want
         if want:
             loop = asyncio.get_event_loop()
-            self._timer = loop.call_later(HEADER_TIMEOUT_S if want == "head" else IDLE_TIMEOUT_S, self._expire, want)
+            self._timer = loop.call_later(IDLE_TIMEOUT_S if want == "idle" else HEADER_TIMEOUT_S, self._expire, want)
 
     def _expire(self, kind: str) -> None:
         self._timer = None
         self._timer_kind = ""
         if self.closed or self.busy:
             return
-        if kind == "head":
+        if kind in ("head", "body"):
             self._fail(408, "request not received in time")
         elif self.transport is not None:
             self.transport.close()
@@ -139,7 +146,7 @@ class Connection(asyncio.Protocol):
         self.buf += data
         if not self.busy:
             self._next()
-        self._arm()
+        self._arm(progress=True)
 
     # ------------------------------------------------------------------ parsing
     def _next(self) -> None:

@@ -169,22 +169,30 @@ class TransformerLM:
             out.pop("lm_head", None)
         self.w = out
 
-    def prepare_fused_prefill(self) -> bool:
+    def prepare_fused_prefill(self, tuning: bool = True, max_rows: int = 8192) -> bool:
         """Norm-folded copies of the qkv / gate_up weights (W diag(g), ops.fold_norm_weight) for the
         prefill forward whose RMSNorms run inside the consumer GEMMs (_forward_pf).  TP = 1 dense
         models on the GPU.  Call after the weights are final and before the KV pool is sized: the
-        copies take the qkv + gate_up bytes of every layer once more (1.3 GB for Llama-3.2-1B)."""
+        copies take the qkv + gate_up bytes of every layer once more (1.3 GB for Llama-3.2-1B), so a
+        copy is only made when its row-scaled form can run at all: the start-up tuner will run
+        (`tuning`: not enforce_eager) and the stored table does not already reject it at every row
+        bucket (ops/prefill_pf.py folded_weight_needed)."""
+        from ..ops import prefill_pf
         c = self.cfg
         self.wf = {}
         self.pf_chain = (self.fuse_prefill and self.fuse_residual and self.device.type == "cuda" and
                          self.tp_size == 1 and not c.is_moe and c.hidden_size % 64 == 0)
-        if not self.pf_chain:
+        if not self.pf_chain or not tuning:
             return False
+        want = {name: prefill_pf.folded_weight_needed(*self.w["l0." + name].shape, code, max_rows, self.device)
+                for name, code in (("qkv", prefill_pf.CODE_RS), ("gate_up", prefill_pf.CODE_RS_SWIGLU))}
+        norms = {"qkv": "in_norm", "gate_up": "post_norm"}
         for i in range(c.num_layers):
             p = f"l{i}."
-            self.wf[p + "qkv"] = ops.fold_norm_weight(self.w[p + "qkv"], self.w[p + "in_norm"])
-            self.wf[p + "gate_up"] = ops.fold_norm_weight(self.w[p + "gate_up"], self.w[p + "post_norm"])
-        return True
+            for name, keep in want.items():
+                if keep:
+                    self.wf[p + name] = ops.fold_norm_weight(self.w[p + name], self.w[p + norms[name]])
+        return bool(self.wf)
 
     def drop_folded(self, names) -> None:
         """Free the folded copies of projections (e.g. "qkv", "gate_up") whose row-scaled form the

@@ -170,6 +170,23 @@ def resid_linear(x: torch.Tensor, w: torch.Tensor, r: torch.Tensor) -> torch.Ten
     return r.add_(ops.linear(x, w))
 
 
+def folded_weight_needed(N: int, K: int, code: int, max_rows: int, device) -> bool:
+    """Before the KV pool is sized: will the row-scaled form (codes 3 / 4) over a norm-folded copy of
+    an [N, K] weight possibly run?  Off -> never; on -> always; auto -> unless the stored table already
+    rejects it at every row bucket (then no folded copy is made, and its bytes go to the KV pool)."""
+    if MODE == "off" or N % 256 or K % 64:
+        return False
+    if MODE == "on":
+        return True
+    from .tuned import TunedStore, device_tag
+    store = TunedStore("prefill_pf", device_tag(device))
+    for M in buckets_for(max_rows):
+        st = store.get(f"{N}x{K}:{code}@{M}")
+        if st is None or isinstance(st.get("cfg"), int):
+            return True  # not measured here yet, or gemm_pf kept at this bucket
+    return False
+
+
 def tune_fused(weights: dict, max_rows: int, device, dtype=torch.bfloat16, eps: float = 1e-5) -> list:
     """weights: {name: (w, wf | None, code)} with code 3 / 4 (row-scaled consumer, wf the folded
     weight) or 2 (residual producer).  Adds the codes' entries to TABLE (run after tune(): the

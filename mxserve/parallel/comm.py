@@ -86,6 +86,26 @@ def init_distributed(tp_size: int, backend: Optional[str] = None, device: Option
     return st
 
 
+_LOCAL = [False]
+
+
+class collectives_local:
+    """Context manager: every TP collective of this process becomes a local stand-in (all-reduce ->
+    this rank's partial, all-gather -> its shard tiled).  A dense model's forward then runs every
+    kernel and library GEMM of the real one without waiting for a peer: a local warm-up pays the
+    first-call costs (hipBLASLt solution and code-object loads from a cold page cache took one rank
+    seconds longer than its peers, profiles/r5/car_timeout/README.md) at each rank's own pace, before
+    the collective warm-up.  Numbers computed inside are meaningless."""
+
+    def __enter__(self):
+        _LOCAL[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _LOCAL[0] = False
+        return False
+
+
 def tp_barrier() -> None:
     """CPU-group barrier of the TP group (no-op at TP 1)."""
     st = _STATE
@@ -95,7 +115,7 @@ def tp_barrier() -> None:
 
 def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     st = _STATE
-    if st.tp_size == 1:
+    if st.tp_size == 1 or _LOCAL[0]:
         return x
     if st.custom_ar is not None and st.custom_ar.should_use(x):
         return st.custom_ar.all_reduce(x)
@@ -109,7 +129,7 @@ def tp_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, ep
     the all-reduce and then the fused add + RMSNorm kernel.  TP = 1: just the add + norm."""
     from .. import ops
     st = _STATE
-    if st.tp_size > 1:
+    if st.tp_size > 1 and not _LOCAL[0]:
         car = st.custom_ar
         if car is not None and x.is_contiguous() and x.dtype == residual.dtype and car.can_add_rms_norm(residual):
             return car.add_rms_norm(residual, w, eps, x=x)
@@ -127,6 +147,8 @@ def tp_linear_add_rms_norm(x: torch.Tensor, w: torch.Tensor, residual: torch.Ten
     st = _STATE
     if st.tp_size == 1:
         return ops.linear_add_rms_norm(x, w, residual, norm_w, eps)
+    if _LOCAL[0]:
+        return ops.fused_add_rms_norm(ops.linear(x, w), residual, norm_w, eps)
     car = st.custom_ar
     if car is not None and car.can_add_rms_norm(residual) and x.is_cuda and x.dim() == 2 \
             and 0 < x.shape[0] <= ops._decode_max_m():
@@ -144,6 +166,8 @@ def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
     st = _STATE
     if st.tp_size == 1:
         return x
+    if _LOCAL[0]:
+        return torch.cat([x] * st.tp_size, dim=dim)
     car = st.custom_ar
     if car is not None and x.is_cuda and dim in (0, -1, x.dim() - 1):
         # every rank pushes its shard to every peer through the IPC all-to-all (one xGMI hop per

@@ -58,11 +58,21 @@ def roofline(model: str, isl: int, osl: int, itl_ms: float = 25.0, system: str =
 
 def capacity(model: str, isl: int, osl: int, itl_ms: float = 25.0, system: str = "mi355x") -> dict:
     """{"prefill_rps", "decode_rps", "source", ...}: the measured entry on MI355X when the table
-    has the workload, else the roofline."""
+    has the workload, else the roofline.  The measured decode capacity holds for ITL targets at least
+    as loose as the one it was measured at (decode_itl_target_ms): a tighter target caps the decode
+    batch lower, so the decode side then scales the measurement by the roofline's ratio between the
+    two targets (the prefill side does not depend on the ITL)."""
     if system.lower() == "mi355x":
         e = lookup(model, isl, osl)
         if e is not None and e.get("prefill_rps") and e.get("decode_rps"):
-            return dict(e, source=e.get("source", "measured"))
+            out = dict(e, source=e.get("source", "measured"))
+            at = float(e.get("decode_itl_target_ms") or itl_ms)
+            if itl_ms < at:
+                tight, loose = roofline(model, isl, osl, itl_ms), roofline(model, isl, osl, at)
+                ratio = tight["decode_rps"] / loose["decode_rps"] if loose["decode_rps"] else 0.0
+                out["decode_rps"] = e["decode_rps"] * ratio
+                out["decode_source"] = f"measured at ITL {at:g} ms x roofline ratio for ITL {itl_ms:g} ms"
+            return out
     return roofline(model, isl, osl, itl_ms, system)
 
 

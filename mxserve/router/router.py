@@ -12,6 +12,9 @@ its lease (ttl) is dropped.  Routing modes:
   the requests routed to it since that report: a burst of arrivals between two heartbeats spreads
   over the workers instead of landing on the one that looked emptiest.  Workers report how many
   requests they have queued in total (num_added), which retires routed requests from that count.
+  A routed request that never reaches the worker's queue (failed dispatch, rejected prompt, abort
+  before admission) is retired by `forget(worker, request_id)` or, failing that, after `unseen_ttl`
+  seconds; a worker whose num_added goes backwards restarted, and its unseen entries are dropped.
 """
 from __future__ import annotations
 
@@ -46,10 +49,14 @@ class WorkerInfo:
     inflight: int = 0  # requests routed by this frontend and not finished
     kv_waiting_blocks: int = 0  # demand of the worker's waiting queue (its last report)
     num_added: int = -1  # requests the worker had queued at its last report (-1: not reported)
-    unseen: deque = field(default_factory=deque)  # blocks of routed requests its report does not hold yet
+    # routed requests its report does not hold yet: [expiry (monotonic), blocks, request id]
+    unseen: deque = field(default_factory=deque)
 
-    def load_blocks(self) -> int:
-        return self.kv_active_blocks + self.kv_waiting_blocks + sum(self.unseen)
+    def load_blocks(self, now: Optional[float] = None) -> int:
+        now = time.monotonic() if now is None else now
+        while self.unseen and self.unseen[0][0] <= now:  # entries are appended in expiry order
+            self.unseen.popleft()
+        return self.kv_active_blocks + self.kv_waiting_blocks + sum(e[1] for e in self.unseen)
 
     def public(self) -> dict:
         return {"worker_id": self.worker_id, "url": self.url, "model": self.model, "role": self.role,
@@ -59,8 +66,9 @@ class WorkerInfo:
 
 
 class Registry:
-    def __init__(self, ttl: float = 10.0):
+    def __init__(self, ttl: float = 10.0, unseen_ttl: Optional[float] = None):
         self.ttl = ttl
+        self.unseen_ttl = ttl if unseen_ttl is None else unseen_ttl
         self._lock = threading.Lock()
         self.workers: dict[str, WorkerInfo] = {}
         self._free_idx = list(range(63, -1, -1))
@@ -94,8 +102,11 @@ class Registry:
             w.kv_waiting_blocks = int(load.get("kv_waiting_blocks", 0))
             if "num_added" in load:
                 n = int(load["num_added"])
-                for _ in range(min(len(w.unseen), max(0, n - w.num_added) if w.num_added >= 0 else len(w.unseen))):
-                    w.unseen.popleft()
+                if 0 <= n < w.num_added:  # the worker restarted: nothing routed before is queued there
+                    w.unseen.clear()
+                else:
+                    for _ in range(min(len(w.unseen), max(0, n - w.num_added) if w.num_added >= 0 else len(w.unseen))):
+                        w.unseen.popleft()
                 w.num_added = n
             else:  # a worker without the counter: its report is all the router knows
                 w.unseen.clear()
@@ -144,15 +155,29 @@ class Router:
         return self._hash(token_ids, block_size, 0, 0)
 
     def pick(self, candidates: list[WorkerInfo], token_ids: Optional[list] = None,
-             commit: bool = True) -> tuple[WorkerInfo, int]:
+             commit: bool = True, request_id: Optional[str] = None) -> tuple[WorkerInfo, int]:
         """Returns (worker, overlap_blocks).  commit: count the request's blocks against the chosen
-        worker until its load report includes them."""
+        worker until its load report includes them (or forget(), or the registry's unseen_ttl)."""
         w, ov = self._pick(candidates, token_ids)
         if commit and token_ids:
             bs = w.block_size
             with self.reg._lock:
-                w.unseen.append(max(0, -(-(len(token_ids) + 1) // bs) - ov))
+                w.unseen.append([time.monotonic() + self.reg.unseen_ttl,
+                                 max(0, -(-(len(token_ids) + 1) // bs) - ov), request_id])
         return w, ov
+
+    def forget(self, w: WorkerInfo, request_id: Optional[str]) -> bool:
+        """A routed request that will not be queued on w (its dispatch failed): stop counting its
+        blocks against w.  The entry goes away entirely: the worker's num_added never counts it, so
+        the next increments retire the requests routed after it."""
+        if request_id is None:
+            return False
+        with self.reg._lock:
+            for e in w.unseen:
+                if e[2] == request_id:
+                    w.unseen.remove(e)
+                    return True
+        return False
 
     def _pick(self, candidates: list[WorkerInfo], token_ids: Optional[list] = None) -> tuple[WorkerInfo, int]:
         if not candidates:

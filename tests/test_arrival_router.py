@@ -41,6 +41,33 @@ def test_router_spreads_a_burst_between_heartbeats():
     assert not reg.workers["w1"].unseen
 
 
+def test_router_unseen_load_does_not_leak():
+    """Phantom load: a failed dispatch is forgotten at once, an entry the worker never
+    reports expires after unseen_ttl, and a worker restart (num_added going backwards) drops every
+    entry routed before it."""
+    from mxserve.router.router import Registry, Router, WorkerInfo
+    reg = Registry(unseen_ttl=0.2)
+    reg.register(WorkerInfo(worker_id="w0", url="", model="m", kv_total_blocks=1000))
+    reg.heartbeat("w0", _load(added=5))
+    r = Router(reg, mode="kv")
+    w0 = reg.workers["w0"]
+    prompt = list(range(100, 100 + 400))  # 26 blocks with the first token
+    r.pick([w0], prompt, request_id="a")
+    r.pick([w0], prompt, request_id="b")
+    assert w0.load_blocks() == 2 * 26
+    assert r.forget(w0, "a") and not r.forget(w0, "a") and not r.forget(w0, "zz")
+    assert w0.load_blocks() == 26 and len(w0.unseen) == 1
+    reg.heartbeat("w0", _load(waiting=26, added=6))  # "b" reached the queue: its report holds it now
+    assert not w0.unseen and w0.load_blocks() == 26
+    r.pick([w0], prompt, request_id="c")  # never reported (e.g. rejected by the worker): expires
+    assert w0.load_blocks() == 2 * 26
+    time.sleep(0.25)
+    assert w0.load_blocks() == 26 and not w0.unseen
+    r.pick([w0], prompt, request_id="d")
+    reg.heartbeat("w0", _load(added=0))  # restarted: its counter starts over
+    assert not w0.unseen and w0.load_blocks() == 0
+
+
 def test_scheduler_reports_admission_counter_and_waiting_demand():
     from mxserve.config import EngineArgs
     from mxserve.engine.engine import LLMEngine

@@ -45,6 +45,10 @@ def _logits(full, n=40, model=MODEL_70B_2L, moe_dispatch="allreduce"):
     m.load_full_state(full)
     ids = torch.randint(3, cfg.vocab_size, (n,), generator=torch.Generator().manual_seed(2)).to("cuda:0")
     kv = torch.zeros(4, cfg.num_layers, 2, m.nkv, 16, cfg.head_dim, dtype=torch.bfloat16, device="cuda:0")
+    from mxserve.parallel import comm
+    if comm.get_tp().tp_size > 1 and not cfg.is_moe:  # first-call loads before any peer waits (comm.py)
+        with torch.inference_mode(), comm.collectives_local():
+            m.compute_logits(m.forward(ids, _md(n, "cuda:0"), kv))
     with torch.inference_mode():
         out = m.compute_logits(m.forward(ids, _md(n, "cuda:0"), kv)).float().cpu()
     del m

@@ -846,6 +846,24 @@ def test_httpd_rejects_bad_lengths_times_out_slow_heads_and_continues(monkeypatc
             out += c.recv(1000)
         assert b"HTTP/1.1 200" in out
         c.close()
+        # a body that keeps arriving is never cut off by the header timeout (0.5 s here:
+        # the upload takes ~1.2 s in 0.2 s chunks) ...
+        c = _socket.create_connection(("127.0.0.1", port), timeout=5)
+        c.sendall(b"POST / HTTP/1.1\r\nhost: x\r\ncontent-length: 60\r\n\r\n")
+        for _ in range(6):
+            time.sleep(0.2)
+            c.sendall(b"x" * 10)
+        c.settimeout(3)
+        out = b""
+        while b"got 60" not in out:
+            b = c.recv(1000)
+            assert b, out
+            out += b
+        assert out.startswith(b"HTTP/1.1 200"), out
+        c.close()
+        # ... but a body that stops arriving gets 408
+        r = talk(b"POST / HTTP/1.1\r\nhost: x\r\ncontent-length: 60\r\n\r\nxxxx", wait=1.0, read_until_close=True)
+        assert r.startswith(b"HTTP/1.1 408"), r
     finally:
         loop.call_soon_threadsafe(stop.set)
         th.join(timeout=10)

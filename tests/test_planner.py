@@ -137,3 +137,18 @@ def test_one_capacity_model_for_bench_profiler_and_planner():
     # the reference DGDR example (Qwen3-0.6B, 8 GPUs) plans within the node
     q = sla.plan("Qwen/Qwen3-0.6B", 4000, 500, 600, 25)
     assert q["feasible"] and q["disagg"]["gpus_used"] <= 8
+
+
+def test_measured_decode_capacity_respects_a_tighter_itl():
+    """the measured decode capacity was taken at a 25 ms ITL target; a tighter target must
+    not be planned with it (fewer rows fit per step), a looser one keeps the measurement."""
+    from mxserve.profiler import capacity
+    model = "meta-llama/Llama-3.2-1B-Instruct"
+    e = capacity.lookup(model, 4000, 500)
+    assert e is not None and e["decode_itl_target_ms"] == 25.0
+    base = capacity.capacity(model, 4000, 500, 25.0)
+    assert base["decode_rps"] == e["decode_rps"]
+    assert capacity.capacity(model, 4000, 500, 40.0)["decode_rps"] == e["decode_rps"]
+    tight = capacity.capacity(model, 4000, 500, 8.0)
+    assert tight["decode_rps"] < e["decode_rps"] and "roofline ratio" in tight["decode_source"]
+    assert tight["prefill_rps"] == e["prefill_rps"]

@@ -86,6 +86,28 @@ def _ar_norm_rank(rank, world, port, q):
     want_h2, want_res2 = ref.fused_add_rms_norm(y, res0.clone(), nw, 1e-5)
     ok = all(torch.allclose(u, v, atol=1e-4, rtol=1e-4) for u, v in
              ((h, want_h), (res, want_res), (h2, want_h2), (res2, want_res2)))
+    # collectives_local (the per-rank warm-up before collective warm-ups): no peer is involved
+    # (every collective call raises here) and each epilogue uses this rank's partial alone
+    import torch.distributed as dist
+    from mxserve.parallel import comm
+    real = (dist.all_reduce, dist.all_gather)
+
+    def boom(*a, **k):
+        raise AssertionError("collective called in local mode")
+    dist.all_reduce = dist.all_gather = boom
+    try:
+        with comm.collectives_local():
+            hl, resl = tp_add_rms_norm(x_all[rank].clone(), res0.clone(), nw, 1e-5)
+            hl2, _ = tp_linear_add_rms_norm(a_all[rank].clone(), w_all[rank], res0.clone(), nw, 1e-5)
+            ar = comm.tp_all_reduce(x_all[rank].clone())
+            ag = comm.tp_all_gather(a_all[rank], dim=-1)
+    finally:
+        dist.all_reduce, dist.all_gather = real
+    wl, wresl = ref.fused_add_rms_norm(x_all[rank], res0.clone(), nw, 1e-5)
+    wl2, _ = ref.fused_add_rms_norm(a_all[rank] @ w_all[rank].T, res0.clone(), nw, 1e-5)
+    ok = ok and all(torch.allclose(u, v, atol=1e-4, rtol=1e-4) for u, v in
+                    ((hl, wl), (resl, wresl), (hl2, wl2), (ar, x_all[rank])))
+    ok = ok and ag.shape == (5, 32 * world) and torch.equal(ag[:, :32], a_all[rank])
     q.put((rank, ok))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
