@@ -92,11 +92,20 @@ if ! kubectl get storageclass -o jsonpath='{range .items[*]}{.metadata.annotatio
 fi
 
 if $use_helm; then
-  say "CRDs: helm release ${CRD_RELEASE} (chart deploy/helm/mxserve-crds, version ${RELEASE_VERSION})"
-  helm upgrade --install "$CRD_RELEASE" "$HERE/deploy/helm/mxserve-crds" -n default \
-    --version "$RELEASE_VERSION" --wait --timeout "$HELM_TIMEOUT"
+  # `--version` does not select a version of a chart DIRECTORY: package both charts at
+  # RELEASE_VERSION (chart version and appVersion) and install the packages, so `helm history` /
+  # `helm rollback` track the release version
+  charts="$(mktemp -d)"
+  trap 'rm -rf "$charts"' EXIT
+  for c in mxserve-crds mxserve-platform; do
+    helm package "$HERE/deploy/helm/$c" --version "$RELEASE_VERSION" --app-version "$RELEASE_VERSION" \
+      -d "$charts" >/dev/null
+  done
+  say "CRDs: helm release ${CRD_RELEASE} (chart mxserve-crds ${RELEASE_VERSION})"
+  helm upgrade --install "$CRD_RELEASE" "$charts/mxserve-crds-${RELEASE_VERSION}.tgz" -n default \
+    --wait --timeout "$HELM_TIMEOUT"
   say "operator: helm release ${PLATFORM_RELEASE} in ${NAMESPACE} (${MXS_IMAGE})"
-  helm upgrade --install "$PLATFORM_RELEASE" "$HERE/deploy/helm/mxserve-platform" -n "$NAMESPACE" --create-namespace \
+  helm upgrade --install "$PLATFORM_RELEASE" "$charts/mxserve-platform-${RELEASE_VERSION}.tgz" -n "$NAMESPACE" --create-namespace \
     --set image.repository="${MXS_IMAGE%:*}" --set image.tag="${MXS_IMAGE##*:}" \
     --set namespaceRestricted="$NAMESPACE_RESTRICTED_OPERATOR" --set gpuResource="$GPU_RESOURCE" \
     --set prometheusEndpoint="$PROMETHEUS_ENDPOINT" --wait --timeout "$HELM_TIMEOUT"
@@ -106,8 +115,8 @@ else
   kubectl apply -f "$HERE/deploy/crds/"
   say "operator ${MXS_IMAGE} in ${NAMESPACE} (kubectl)"
   kubectl create namespace "$NAMESPACE" --dry-run=client -o yaml | kubectl apply -f -
-  watch_args='["--interval", "30"]'
-  [[ "$NAMESPACE_RESTRICTED_OPERATOR" == "true" ]] && watch_args="[\"--interval\", \"30\", \"--namespace\", \"${NAMESPACE}\"]"
+  watch_args='["--interval", "30", "--health-port", "8081"]'
+  [[ "$NAMESPACE_RESTRICTED_OPERATOR" == "true" ]] && watch_args="[\"--interval\", \"30\", \"--health-port\", \"8081\", \"--namespace\", \"${NAMESPACE}\"]"
   sed -e "s#IMAGE_PLACEHOLDER#${MXS_IMAGE}#g" -e "s#NAMESPACE_PLACEHOLDER#${NAMESPACE}#g" \
       -e "s#WATCH_ARGS_PLACEHOLDER#${watch_args}#" -e "s#GPU_RESOURCE_PLACEHOLDER#${GPU_RESOURCE}#" \
       -e "s#PROMETHEUS_ENDPOINT_PLACEHOLDER#${PROMETHEUS_ENDPOINT}#" \

@@ -67,17 +67,31 @@ if [[ "$INSTALL_HELM" == "true" ]] && ! command -v helm >/dev/null; then
   rm -rf "$tmp"
 fi
 
-say "kubeadm init (${CLUSTER_NAME}, pods ${POD_CIDR})"
-kubeadm init --pod-network-cidr="$POD_CIDR" --skip-phases=addon/kube-proxy
+NODE_NAME="${NODE_NAME:-$(hostname -s | tr '[:upper:]' '[:lower:]')}"
+say "kubeadm init (${CLUSTER_NAME}, node ${NODE_NAME}, pods ${POD_CIDR})"
+kubeadm init --pod-network-cidr="$POD_CIDR" --node-name="$NODE_NAME" --skip-phases=addon/kube-proxy
 install -d -o "$OWNER" "$OWNER_HOME/.kube"
 install -m 0600 -o "$OWNER" /etc/kubernetes/admin.conf "$OWNER_HOME/.kube/config"
 export KUBECONFIG=/etc/kubernetes/admin.conf
-grep -q 'alias k=kubectl' "$OWNER_HOME/.bashrc" 2>/dev/null || echo 'alias k=kubectl' >> "$OWNER_HOME/.bashrc"
+# the sudo user's shell: `k` alias with kubectl's bash completion on both names
+bashrc="$OWNER_HOME/.bashrc"
+grep -q 'alias k=kubectl' "$bashrc" 2>/dev/null || echo 'alias k=kubectl' >> "$bashrc"
+grep -q 'kubectl completion bash' "$bashrc" 2>/dev/null || cat >> "$bashrc" <<'RC'
+source <(kubectl completion bash)
+complete -o default -F __start_kubectl k
+RC
+chown "$OWNER" "$bashrc" 2>/dev/null || true
 
 say "Cilium (kube-proxy replacement, hubble=${ENABLE_HUBBLE})"
 CILIUM_CLI_VERSION="$(curl -fsSL https://raw.githubusercontent.com/cilium/cilium-cli/main/stable.txt)"
-curl -fsSL "https://github.com/cilium/cilium-cli/releases/download/${CILIUM_CLI_VERSION}/cilium-linux-${ARCH}.tar.gz" \
-  | tar -xz -C /usr/local/bin cilium
+tmp="$(mktemp -d)"
+cilium_url="https://github.com/cilium/cilium-cli/releases/download/${CILIUM_CLI_VERSION}/cilium-linux-${ARCH}.tar.gz"
+curl -fsSL -o "$tmp/cilium-linux-${ARCH}.tar.gz" "$cilium_url"
+curl -fsSL -o "$tmp/cilium-linux-${ARCH}.tar.gz.sha256sum" "${cilium_url}.sha256sum"
+# nothing is unpacked as root before its published checksum matches
+(cd "$tmp" && sha256sum --check "cilium-linux-${ARCH}.tar.gz.sha256sum")
+tar -xzf "$tmp/cilium-linux-${ARCH}.tar.gz" -C /usr/local/bin cilium
+rm -rf "$tmp"
 cilium install --set kubeProxyReplacement=true --set cluster.name="$CLUSTER_NAME"
 if [[ "$ENABLE_HUBBLE" == "true" ]]; then cilium hubble enable --ui; fi
 kubectl taint nodes --all node-role.kubernetes.io/control-plane- 2>/dev/null || true

@@ -25,6 +25,7 @@ PLURALS = {
     "DynamoGraphDeploymentRequest": ("nvidia.com/v1alpha1", "dynamographdeploymentrequests"),
     "DynamoComponentDeployment": ("nvidia.com/v1alpha1", "dynamocomponentdeployments"),
     "Event": ("v1", "events"),
+    "Lease": ("coordination.k8s.io/v1", "leases"),
 }
 # annotation carrying the hash of the spec the operator last applied (apply() skips unchanged objects)
 HASH_ANNOTATION = "mxserve.io/spec-hash"

@@ -37,6 +37,61 @@ from .resources import (API_VERSION, DCD_KIND, DGD_KIND, DGDR_KIND, NS_LABEL, Va
 log = logging.getLogger("mxserve.operator")
 
 
+class LeaderElector:
+    """Lease-based leader election (coordination.k8s.io/v1 Lease, the client-go protocol's fields):
+    the holder renews spec.renewTime well inside leaseDurationSeconds; another replica takes the
+    lease over only once it has expired.  Writes carry the lease's resourceVersion, so two replicas
+    racing for an expired lease cannot both win (the apiserver answers the loser 409)."""
+
+    def __init__(self, client: KubeClient, namespace: str, name: str = "mxserve-operator",
+                 identity: Optional[str] = None, lease_s: float = 30.0):
+        import socket
+        self.k, self.ns, self.name = client, namespace, name
+        self.id = identity or f"{socket.gethostname()}-{os.getpid()}"
+        self.lease_s = lease_s
+        self.leader = False
+
+    @staticmethod
+    def _now() -> str:
+        return time.strftime("%Y-%m-%dT%H:%M:%S.000000Z", time.gmtime())
+
+    @staticmethod
+    def _parse(ts: Optional[str]) -> float:
+        if not ts:
+            return 0.0
+        import calendar
+        return calendar.timegm(time.strptime(ts.split(".")[0].rstrip("Z"), "%Y-%m-%dT%H:%M:%S"))
+
+    def step(self) -> bool:
+        """Acquire or renew; returns whether this replica leads now."""
+        try:
+            lease = self.k.get("Lease", self.name, self.ns)
+            spec = {"holderIdentity": self.id, "leaseDurationSeconds": int(self.lease_s), "renewTime": self._now()}
+            if lease is None:
+                self.k.create({"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
+                               "metadata": {"name": self.name, "namespace": self.ns},
+                               "spec": dict(spec, acquireTime=spec["renewTime"], leaseTransitions=0)})
+                self.leader = True
+                return True
+            cur = lease.get("spec") or {}
+            holder = cur.get("holderIdentity")
+            expired = time.time() > self._parse(cur.get("renewTime")) + float(cur.get("leaseDurationSeconds") or
+                                                                               self.lease_s)
+            if holder != self.id and not expired:
+                self.leader = False
+                return False
+            if holder != self.id:
+                spec.update(acquireTime=spec["renewTime"], leaseTransitions=int(cur.get("leaseTransitions") or 0) + 1)
+            self.k.merge_patch("Lease", self.name, self.ns,
+                               {"metadata": {"resourceVersion": lease["metadata"].get("resourceVersion")},
+                                "spec": spec})
+            self.leader = True
+        except ApiError as e:
+            log.info("leader election: %s", e)
+            self.leader = False
+        return self.leader
+
+
 class Operator:
     def __init__(self, client: KubeClient, namespace: Optional[str] = None, podmonitors: bool = True):
         self.k = client
@@ -45,6 +100,13 @@ class Operator:
         self._pm_disabled = False
         self._wake = threading.Event()
         self.watch_errors = 0
+        # liveness: each watch thread and the reconcile loop stamp a beat every cycle; /healthz fails
+        # when one has not cycled within twice its period (a hung watch thread is otherwise invisible)
+        self.watch_timeout_s = 60.0
+        self.interval = 30.0
+        self.beats: dict = {}
+        self.last_pass: Optional[float] = None
+        self.elector: Optional[LeaderElector] = None
 
     def _set_status(self, kind: str, obj: Optional[dict], name: str, ns: str, st: dict) -> None:
         """Patch status only when it differs from what the object already carries."""
@@ -247,10 +309,12 @@ class Operator:
         the operator on its resync interval."""
         rv, backoff = "", 1.0
         while not stop.is_set():
+            self.beats[kind] = time.monotonic()
             try:
                 if not rv:
                     _, rv = self.k.list_rv(kind, self.ns)
-                for ev in self.k.watch(kind, self.ns, rv, timeout_s=60):
+                for ev in self.k.watch(kind, self.ns, rv, timeout_s=self.watch_timeout_s):
+                    self.beats[kind] = time.monotonic()
                     if ev.get("type") == "ERROR":
                         rv = ""  # expired resourceVersion: re-list
                         break
@@ -266,30 +330,87 @@ class Operator:
                 log.debug("watch %s: %s", kind, e)
                 if stop.wait(backoff):
                     return
-                backoff = min(60.0, backoff * 2)
+                backoff = min(self.watch_timeout_s, backoff * 2)
 
     def start_watches(self, kinds=(DGD_KIND, DGDR_KIND, "Deployment", "Job")) -> threading.Event:
         stop = threading.Event()
+        now = time.monotonic()
         for kind in kinds:
+            self.beats[kind] = now
             threading.Thread(target=self._watch_loop, args=(kind, stop), name=f"watch-{kind}", daemon=True).start()
         return stop
 
     def run(self, interval: float = 30.0, watch: bool = True, stop: Optional[threading.Event] = None) -> None:
         """Reconcile on every watch event (coalesced) and at least every `interval` seconds."""
         stop = stop or threading.Event()
+        self.interval = interval
         wstop = self.start_watches() if watch else None
         try:
             while not stop.is_set():
                 self._wake.clear()
+                self.beats["reconcile"] = time.monotonic()
+                if self.elector is not None and not self.elector.step():
+                    stop.wait(min(interval, self.elector.lease_s / 3))  # standby: retry for the lease
+                    continue
                 try:
                     self.reconcile_all()
+                    self.last_pass = time.monotonic()
                 except Exception:  # noqa: BLE001 - apiserver hiccup
                     log.exception("reconcile pass failed")
-                self._wake.wait(interval)
+                wait = interval if self.elector is None else min(interval, self.elector.lease_s / 3)
+                self._wake.wait(wait)  # a leader wakes at least every third of its lease to renew it
                 time.sleep(0.2)  # coalesce a burst of events into one pass
         finally:
             if wstop is not None:
                 wstop.set()
+
+
+    # ------------------------------------------------------------------ probes
+    def health(self) -> tuple:
+        """(alive, detail): every watch thread and the reconcile loop cycled within twice its period."""
+        now = time.monotonic()
+        detail, ok = {}, True
+        for name, t in sorted(self.beats.items()):
+            limit = 2 * (self.interval + 5 if name == "reconcile" else self.watch_timeout_s)
+            age = now - t
+            detail[name] = round(age, 1)
+            if age > limit:
+                ok = False
+                detail.setdefault("stalled", []).append(name)
+        return ok, detail
+
+    def ready(self) -> bool:
+        """Ready once a reconcile pass has completed (a standby replica of a leader-elected
+        deployment stays unready: it does not reconcile)."""
+        return self.last_pass is not None and (self.elector is None or self.elector.leader)
+
+    def serve_probes(self, port: int, host: str = "0.0.0.0"):
+        """/healthz (liveness) and /readyz (readiness) on a daemon thread; returns the server."""
+        import http.server
+        import json as _json
+        op = self
+
+        class H(http.server.BaseHTTPRequestHandler):
+            def do_GET(self):  # noqa: N802
+                if self.path.startswith("/healthz"):
+                    ok, detail = op.health()
+                elif self.path.startswith("/readyz"):
+                    ok, detail = op.ready(), {"last_pass": op.last_pass is not None}
+                else:
+                    ok, detail = False, {"error": "not found"}
+                body = _json.dumps({"ok": ok, **detail}).encode()
+                self.send_response(200 if ok else (404 if "error" in detail else 503))
+                self.send_header("content-type", "application/json")
+                self.send_header("content-length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+            def log_message(self, *a):
+                pass
+
+        srv = http.server.ThreadingHTTPServer((host, port), H)
+        threading.Thread(target=srv.serve_forever, name="operator-probes", daemon=True).start()
+        return srv
 
 
 def default_template(model: str) -> dict:
@@ -311,10 +432,19 @@ def main(argv=None) -> None:
     ap.add_argument("--no-watch", action="store_true", help="poll every --interval instead of watching")
     ap.add_argument("--server", default=None, help="apiserver URL (default: in-cluster / kubeconfig)")
     ap.add_argument("--no-podmonitors", action="store_true")
+    ap.add_argument("--health-port", type=int, default=int(os.environ.get("MXS_OPERATOR_HEALTH_PORT", "8081")),
+                    help="/healthz and /readyz (0: off)")
+    ap.add_argument("--leader-elect", action="store_true", help="Lease-based leader election (replicas > 1)")
+    ap.add_argument("--lease-namespace", default=os.environ.get("POD_NAMESPACE", "default"))
     a = ap.parse_args(argv)
     from ..utils.logs import setup_logging
     setup_logging()
-    op = Operator(KubeClient(a.server) if a.server else KubeClient(), a.namespace, not a.no_podmonitors)
+    client = KubeClient(a.server) if a.server else KubeClient()
+    op = Operator(client, a.namespace, not a.no_podmonitors)
+    if a.leader_elect:
+        op.elector = LeaderElector(client, a.lease_namespace)
+    if a.health_port:
+        op.serve_probes(a.health_port)
     op.run(a.interval, watch=not a.no_watch)
 
 

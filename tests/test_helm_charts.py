@@ -90,8 +90,18 @@ def test_platform_chart_renders_the_operator():
     chart = yaml.safe_load(open(os.path.join(HELM, "mxserve-platform", "Chart.yaml")))
     assert c["image"] == f"mxserve/mxserve-rocm:{chart['appVersion']}"  # tag defaults to appVersion
     assert c["command"] == ["python3", "-m", "mxserve.k8s.operator"] and "--namespace" not in c["args"]
-    env = {e["name"]: e["value"] for e in c["env"]}
+    env = {e["name"]: e.get("value") for e in c["env"]}
     assert env["MXS_DEFAULT_IMAGE"] == c["image"] and env["MXS_GPU_RESOURCE"] == "amd.com/gpu"
+    # liveness / readiness probes on the operator's health port; no leader
+    # election at one replica
+    assert c["livenessProbe"]["httpGet"]["path"] == "/healthz" and c["readinessProbe"]["httpGet"]["path"] == "/readyz"
+    assert c["ports"][0]["containerPort"] == 8081 and "--health-port" in c["args"] and "--leader-elect" not in c["args"]
+    assert dep["spec"]["replicas"] == 1
+    rules = next(o for o in objs if o["kind"] == "ClusterRole")["rules"]
+    assert any("leases" in r["resources"] for r in rules)
+    ha = _chart("mxserve-platform", {"replicas": 2, "leaderElection": True})
+    dha = next(o for o in ha if o["kind"] == "Deployment")
+    assert dha["spec"]["replicas"] == 2 and "--leader-elect" in dha["spec"]["template"]["spec"]["containers"][0]["args"]
     crb = next(o for o in objs if o["kind"] == "ClusterRoleBinding")
     assert crb["subjects"][0]["namespace"] == "dynamo-system"
     # the kubectl path applies the same rules
@@ -108,8 +118,11 @@ def test_platform_chart_renders_the_operator():
 
 def test_installer_uses_helm_releases_and_can_uninstall():
     sh = open(os.path.join(ROOT, "install-dynamo-1node.sh")).read()
-    assert 'helm upgrade --install "$CRD_RELEASE" "$HERE/deploy/helm/mxserve-crds"' in sh
-    assert 'helm upgrade --install "$PLATFORM_RELEASE" "$HERE/deploy/helm/mxserve-platform"' in sh
+    # `--version` does not pick a version of a chart directory; the installer
+    # packages both charts at RELEASE_VERSION and installs the packages
+    assert 'helm package "$HERE/deploy/helm/$c" --version "$RELEASE_VERSION" --app-version "$RELEASE_VERSION"' in sh
+    assert 'helm upgrade --install "$CRD_RELEASE" "$charts/mxserve-crds-${RELEASE_VERSION}.tgz"' in sh
+    assert 'helm upgrade --install "$PLATFORM_RELEASE" "$charts/mxserve-platform-${RELEASE_VERSION}.tgz"' in sh
     assert 'helm uninstall "$PLATFORM_RELEASE"' in sh and "PURGE_CRDS" in sh
     assert subprocess.run(["bash", "-n", os.path.join(ROOT, "install-dynamo-1node.sh")]).returncode == 0
     # the chart version tracks the release version the installer passes

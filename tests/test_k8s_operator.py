@@ -638,3 +638,82 @@ def test_watch_wakes_the_operator(cluster):
         stop.set()
         op._wake.set()
         t.join(timeout=10)
+
+
+def test_operator_health_fails_after_a_stalled_watch(cluster):
+    """/healthz (the liveness probe) fails once a watch thread has not cycled
+    within twice its timeout -- here a watch that hangs inside its HTTP read; /readyz turns ready
+    after the first reconcile pass."""
+    import json as _json
+    import threading
+    import urllib.error
+    import urllib.request
+    fake, k = cluster
+    op = Operator(k)
+    op.watch_timeout_s = 0.5
+    hang = threading.Event()
+    real_watch = k.watch
+
+    def watch(kind, *a, **kw):
+        if kind == "Job" and hang.is_set():  # the Job watch stops returning (a wedged connection)
+            threading.Event().wait(60)
+        return real_watch(kind, *a, **kw)
+
+    k.watch = watch
+    srv = op.serve_probes(0, host="127.0.0.1")
+    port = srv.server_address[1]
+
+    def get(path):
+        try:
+            with urllib.request.urlopen(f"http://127.0.0.1:{port}{path}", timeout=5) as r:
+                return r.status, _json.loads(r.read())
+        except urllib.error.HTTPError as e:
+            return e.code, _json.loads(e.read())
+
+    stop = threading.Event()
+    t = threading.Thread(target=op.run, kwargs={"interval": 0.5, "stop": stop}, daemon=True)
+    try:
+        assert get("/readyz")[0] == 503  # no reconcile pass yet
+        t.start()
+        deadline = time.time() + 10
+        while time.time() < deadline and get("/readyz")[0] != 200:
+            time.sleep(0.1)
+        assert get("/readyz")[0] == 200
+        time.sleep(1.5)
+        code, body = get("/healthz")
+        assert code == 200 and body["ok"], body
+        hang.set()
+        deadline = time.time() + 10
+        while time.time() < deadline and get("/healthz")[0] == 200:
+            time.sleep(0.2)
+        code, body = get("/healthz")
+        assert code == 503 and body["stalled"] == ["Job"], body
+        assert get("/nope")[0] == 404
+    finally:
+        stop.set()
+        op._wake.set()
+        t.join(timeout=10)
+        srv.shutdown()
+
+
+def test_lease_leader_election(cluster):
+    """Two operator replicas: one holds the Lease and reconciles; the other stays on standby (not
+    ready) until the holder stops renewing and the lease expires, then takes over."""
+    from mxserve.k8s.operator import LeaderElector
+    fake, k = cluster
+    a = LeaderElector(k, "dynamo-system", identity="a", lease_s=1.0)
+    b = LeaderElector(k, "dynamo-system", identity="b", lease_s=1.0)
+    assert a.step() and not b.step()
+    lease = k.get("Lease", "mxserve-operator", "dynamo-system")
+    assert lease["spec"]["holderIdentity"] == "a"
+    assert a.step() and not b.step()  # renewal keeps it
+    time.sleep(2.2)  # a stops renewing: expired (second-granularity renewTime)
+    assert b.step() and not a.step()
+    lease = k.get("Lease", "mxserve-operator", "dynamo-system")
+    assert lease["spec"]["holderIdentity"] == "b" and lease["spec"]["leaseTransitions"] == 1
+    op = Operator(k)
+    op.elector = b
+    op.last_pass = time.monotonic()
+    assert op.ready()
+    op.elector = a
+    assert not op.ready()  # standby
