@@ -137,6 +137,10 @@ def parse(argv=None):
                     help="KV pool size per rank (default: what the GPU's free memory allows)")
     ap.add_argument("--probe-timeout-s", type=float, default=float(os.environ.get("MXS_BENCH_PROBE_TIMEOUT", "300")),
                     help="N >= 2: budget of the multi-GPU probe run after the serving phases (0: no probe)")
+    ap.add_argument("--served", type=int, default=int(os.environ.get("MXS_BENCH_SERVED", "1")),
+                    help="N = 1: after the engine-direct phase, drive the same Poisson stream through the served "
+                         "stack (frontend HTTP/SSE -> worker streamer -> engine) and report it as the line's "
+                         "`served` block (mxserve/tools/served_phase.py); 0 = skip")
     ap.add_argument("--time-budget-s", type=float, default=float(os.environ.get("MXS_BENCH_BUDGET_S", "450")),
                     help="wall budget of the whole run, from process start: the probe and the disagg phase get "
                          "what the agg phase leaves; at the deadline rank 0 prints the line it has and every "
@@ -905,6 +909,51 @@ def phase_agg(a, ctx) -> tuple:
     return ctx.gather(st), info, host
 
 
+def phase_served(a, ctx, agg: dict, info: dict, guard) -> dict:
+    """The engine-direct phase's workload through the served stack (mxserve/tools/served_phase.py),
+    same QPS / ISL / OSL / engine limits, warm-up and window lengths; with the delta against the
+    engine-direct numbers."""
+    from mxserve.models.config import get_model_config
+    from mxserve.tools import served_phase
+    model = info["model"]
+    isl, osl = info["isl"], info["osl"]
+    flags = ["--max-num-seqs", str(a.max_num_seqs), "--max-num-batched-tokens", str(a.max_num_batched_tokens),
+             "--max-model-len", str(a.max_model_len), "--seed", str(a.seed)]
+    if a.itl_target_ms:
+        flags += ["--itl-target-ms", str(a.itl_target_ms)]
+    if a.kv_cache_dtype != "auto":
+        flags += ["--kv-cache-dtype", a.kv_cache_dtype]
+    if a.enforce_eager:
+        flags.append("--enforce-eager")
+    if a.num_gpu_blocks:
+        flags += ["--num-gpu-blocks-override", str(a.num_gpu_blocks)]
+    if not ctx.on_gpu:
+        flags += ["--device", "cpu", "--num-gpu-blocks-override", "4096"]
+    os.environ["MXS_CUDA_GRAPH_MAX_BS"] = str(a.max_num_seqs)  # the engine-direct phase's capture range
+    window_s = agg["ms_per_step"] * a.steps / 1e3
+    warmup_s = float(agg.get("warmup_s") or 10.0)
+    vlog(f"served: warmup {warmup_s:.1f}s, window {window_s:.1f}s")
+    log_dir = os.environ.get("MXS_BENCH_LOG_DIR", "")
+    try:
+        res = served_phase.run(model, a.qps, isl, osl, warmup_s, window_s, flags,
+                               get_model_config(model).vocab_size, a.seed, ctx.on_gpu, guard.deadline - 20, log_dir,
+                               guard.children)
+    except Exception as e:  # noqa: BLE001 - the engine-direct line stands
+        import traceback
+        traceback.print_exc()
+        return {"status": "failed", "error": repr(e)[:300]}
+    if res.get("status") == "ok" and res.get("value"):
+        res["vs_engine_direct"] = {"value_ratio": round(res["value"] / agg["value"], 4) if agg["value"] else None,
+                                   "ttft_p50_delta_ms": round(res["ttft_p50_ms"] - agg["ttft_p50_ms"], 2)
+                                   if res.get("ttft_p50_ms") is not None and agg.get("ttft_p50_ms") is not None
+                                   else None,
+                                   "itl_p50_delta_ms": round(res["itl_p50_ms"] - agg["itl_p50_ms"], 3)
+                                   if res.get("itl_p50_ms") is not None and agg.get("itl_p50_ms") is not None
+                                   else None}
+    vlog(f"served: {res}")
+    return res
+
+
 def phase_disagg(a, ctx) -> tuple:
     from mxserve.engine.engine import LLMEngine
     from mxserve.engine.request import SamplingParams
@@ -977,6 +1026,10 @@ def main():
                 line["multi_gpu_probe"] = {"status": "pending"}
             guard.pending = line
             vlog(f"agg done: {agg['value']} tok/s; {guard.remaining():.0f}s of the budget left")
+    if agg is not None and world == 1 and a.served:
+        served = phase_served(a, ctx, agg, info, guard)
+        if ctx.rank == 0:
+            guard.pending = dict(guard.pending or {}, served=served)
     if mode in ("disagg", "both") and not host_disagg:
         dis = run_guarded(lambda: phase_disagg(a, ctx), min(a.phase_timeout_s, max(1.0, guard.remaining() - 15)),
                           ctx, agg_info=info, agg=agg, a=a, mode=mode, guard=guard)
@@ -997,6 +1050,8 @@ def main():
                 "kv_cache_dtype": "bf16", "isl": a.isl, "osl": a.osl}
     if ctx.rank == 0:
         line = build_line(a, ctx, mode, agg, dis, info)
+        if isinstance(guard.pending, dict) and "served" in guard.pending:
+            line["served"] = guard.pending["served"]
         if probe_res is not None:
             line["multi_gpu_probe"] = probe_res
         line["wall_s"] = round(time.time() - _WALL0, 1)

@@ -66,7 +66,7 @@ async def one_request(sess, url: str, model: str, prompt, osl: int, t_sched: flo
     if err or first is None:
         return {"ok": False, "error": err or "no tokens"}
     out_tokens = usage["completion_tokens"] if usage else n_chunks
-    return {"ok": True, "ttft": first - t_sched, "e2e": last - t_sched, "itl": gaps, "out": out_tokens,
+    return {"ok": True, "ttft": first - t_sched, "e2e": last - t_sched, "itl": gaps, "out": out_tokens, "chunks": n_chunks,
             "in": usage["prompt_tokens"] if usage else None, "start": t0, "sched": t_sched, "first": first,
             "last": last}
 
@@ -78,7 +78,14 @@ def steady_window(results: list, t_a: float, t_b: float) -> dict:
     ok = [r for r in results if r["ok"]]
     toks = 0.0
     for r in ok:
-        lo, hi = max(r["first"], t_a), min(r["last"], t_b)
+        if r.get("chunks") == r["out"]:  # one token per streamed chunk: count the chunks that landed inside
+            t = r["first"]
+            toks += t_a <= t <= t_b
+            for g in r["itl"]:
+                t += g
+                toks += t_a <= t <= t_b
+            continue
+        lo, hi = max(r["first"], t_a), min(r["last"], t_b)  # chunks carrying several tokens: spread them
         if hi <= lo:
             continue
         span = max(r["last"] - r["first"], 1e-9)
@@ -88,7 +95,7 @@ def steady_window(results: list, t_a: float, t_b: float) -> dict:
     pct = lambda xs, q: float(np.percentile(xs, q)) * 1e3 if xs else None  # noqa: E731
     return {"steady_window_s": t_b - t_a, "steady_output_tok_per_s": toks / max(t_b - t_a, 1e-9),
             "steady_requests": len(ttft), "steady_ttft_ms_p50": pct(ttft, 50), "steady_ttft_ms_p90": pct(ttft, 90),
-            "steady_itl_ms_p50": pct(itl, 50)}
+            "steady_itl_ms_p50": pct(itl, 50), "steady_itl_ms_p90": pct(itl, 90)}
 
 
 def summarize(results: list, wall: float, label: dict) -> dict:
@@ -123,10 +130,15 @@ async def run_concurrency(url, model, conc, n, isl, osl, token_ids, vocab, seed)
     return summarize(results, wall, {"mode": "concurrency", "concurrency": conc, "isl": isl, "osl": osl})
 
 
-async def run_rate(url, model, rate, n, isl, osl, token_ids, vocab, seed, warmup_s: float = 0.0):
-    rng = random.Random(seed)
-    prompts = [synth_prompt(rng, isl, token_ids, vocab) for _ in range(n)]
-    gaps = np.random.default_rng(seed).exponential(1.0 / rate, size=n)
+async def run_rate(url, model, rate, n, isl, osl, token_ids, vocab, seed, warmup_s: float = 0.0, gaps=None,
+                   prompts=None):
+    """Open-loop Poisson arrivals.  gaps / prompts: an explicit arrival stream (bench.py's served
+    phase replays the engine-direct phase's exact stream) instead of one drawn from `seed`."""
+    if prompts is None:
+        rng = random.Random(seed)
+        prompts = [synth_prompt(rng, isl, token_ids, vocab) for _ in range(n)]
+    if gaps is None:
+        gaps = np.random.default_rng(seed).exponential(1.0 / rate, size=n)
     conn = aiohttp.TCPConnector(limit=0)
     async with aiohttp.ClientSession(connector=conn, timeout=aiohttp.ClientTimeout(total=None)) as sess:
         t0 = time.perf_counter()

@@ -609,6 +609,12 @@ class Worker:
                 continue
             try:
                 sess = await self.http()
+                if not registered and self.stream_url:
+                    # advertise the streamer's request plane only once it accepts connections: a
+                    # request routed to it earlier is refused and the frontend drops this worker
+                    async with sess.get(self.stream_url + "/health") as r:
+                        if r.status != 200:
+                            raise ConnectionError(f"streamer not ready ({r.status})")
                 if not registered:
                     async with sess.post(base + "/internal/register", json=self.registration()) as r:
                         registered = r.status == 200
