@@ -45,8 +45,8 @@ bool launch_splitk_rope_and_cache(bf16_t*, const float*, int, const int64_t*, co
 bool launch_prefill_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int,
                          hipStream_t);
 bool launch_gemm_pf(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, float*, long, int*, int,
-                    const int*, int, int, int, hipStream_t, const bf16_t*, int, bool, float);
-int pf_plan(int, int, int, int, int, int, int*, int*, int*);
+                    const int*, int, int, int, hipStream_t, const bf16_t*, int, bool, float, int);
+int pf_plan(int, int, int, int, int, int, int*, int*, int*, int);
 bool launch_moe_grouped_gemm(bf16_t*, const bf16_t*, const bf16_t*, const int*, int, int, int, int, int, bool,
                              int, float*, hipStream_t);
 void launch_moe_combine_partials(bf16_t*, const float*, const float*, const int*, int, int, int, int, long,
@@ -399,7 +399,7 @@ bool prefill_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::
 // them zero).  False if the shape is unsupported.
 bool gemm_pf(at::Tensor out, at::Tensor x, at::Tensor w, int64_t epi, at::Tensor slab, at::Tensor cnt,
              at::Tensor tile_map, int64_t num_cu, int64_t min_iters, c10::optional<at::Tensor> resid,
-             bool row_scale, double eps) {
+             bool row_scale, double eps, int64_t trows) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
   const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
@@ -421,7 +421,7 @@ bool gemm_pf(at::Tensor out, at::Tensor x, at::Tensor w, int64_t epi, at::Tensor
   return mxs::launch_gemm_pf(bf(out), bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), epi, slab.data_ptr<float>(),
                              slab.numel(), cnt.data_ptr<int>(), cnt.numel(), tile_map.data_ptr<int>(),
                              tile_map.numel(), num_cu, min_iters, stream(), R, ldr, row_scale,
-                             static_cast<float>(eps));
+                             static_cast<float>(eps), static_cast<int>(trows));
 }
 
 // Grouped decode form of decode_gemm (K16 at decode batches): w [E, N, K], x = routed rows sorted by
@@ -549,10 +549,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_pf", &gemm_pf, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("epi"),
         pybind11::arg("slab"), pybind11::arg("cnt"), pybind11::arg("tile_map"), pybind11::arg("num_cu"),
         pybind11::arg("min_iters") = 16, pybind11::arg("resid") = pybind11::none(),
-        pybind11::arg("row_scale") = false, pybind11::arg("eps") = 1e-5);
-  m.def("gemm_pf_plan", [](int M, int N, int K, int epi, int num_cu, int min_iters) {
+        pybind11::arg("row_scale") = false, pybind11::arg("eps") = 1e-5, pybind11::arg("trows") = 256);
+  m.def("gemm_pf_plan", [](int M, int N, int K, int epi, int num_cu, int min_iters, int trows) {
     int dp = 0, sk = 0, g = 0;
-    mxs::pf_plan(M, N, K, epi, num_cu, min_iters, &dp, &sk, &g);
+    mxs::pf_plan(M, N, K, epi, num_cu, min_iters, &dp, &sk, &g, trows);
     return std::make_tuple(g, dp, sk);
   });
   m.def("moe_decode_gemm", &moe_decode_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),

@@ -22,10 +22,11 @@
 //     CU; full rounds of tiles run data-parallel, the last one-to-two rounds' k-iterations are split
 //     evenly over the workgroups.  Every workgroup runs ONE continuous k-tile pipeline over its
 //     positions (a new tile's first k-tiles are already in LDS when the previous tile's epilogue
-//     runs).  A tile split over workgroups is finished by the one that arrives last: every segment
-//     publishes an fp32 slab (write-through sc1 stores, then a ticket), the last arriver reads the
-//     slabs with sc1 loads, sums them in segment order (deterministic) and runs the epilogue (§5
-//     "Projection GEMM at M = 256" item 2, sc1 form);
+//     runs).  A tile split over workgroups is finished by its HEAD (the owner of its first k-tiles,
+//     whose segment ends that owner's range while the others open theirs): the other segments
+//     publish fp32 slabs (write-through sc1 stores, then a count), the head adds them to the
+//     accumulators it holds in segment order (deterministic: fp32 addition commutes) and runs the
+//     epilogue (§5 "Projection GEMM at M = 256" item 2, sc1 form);
 //   * tiles are visited XCD-aware: the 32 workgroups of an XCD take 32 consecutive tiles of a round
 //     in the host-built tile map's order (8 token tiles per weight-column sweep), so they share W and
 //     X panels in their L2.
@@ -69,7 +70,7 @@ struct PfArgs {
   bf16_t* Y;
   const bf16_t* X;
   const bf16_t* W;
-  float* slab;  // stream-K partials: [2 * grid][8 * 4 * 8 (frag pairs)][512 threads][4] fp32
+  float* slab;  // stream-K partials: [grid][34 fragments][512 threads][4] fp32 (one per workgroup)
   int* cnt;     // per stream-K tile arrival counters (zero between launches)
   const int* tile_map;  // logical tile -> token tile | weight tile << 16 (pf_tile_map)
   int M, K, ldx, ldy, inter, ntm, ntn, nk;
@@ -87,11 +88,18 @@ struct PfSeg {
   int c, L, k0, k1, tm, tn;
 };
 
-template <int EPI, bool RS>
+template <int EPI, bool RS, int TMF>
 __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
   constexpr int HT = 16384, QT = 8192, KT = 4 * HT, XB = 2 * HT;  // W halves at 0 / HT, X halves at XB
-  __shared__ __attribute__((aligned(16))) char smem[2 * KT + 16];
-  int* flag = reinterpret_cast<int*>(smem + 2 * KT);
+  // token tile: TMF 16-row fragments per wave row-half, 32 TMF rows (256, 192, 160, 128); a wave's
+  // fragments split over the two phases of a k-tile as P0 + P1.  The X image keeps its four 64-row
+  // quarters (h, t): quarter (wr, hb) holds the P_hb fragments wave row-half wr multiplies in phase
+  // hb -- tile rows 16 TMF h + 16 P0 t + [0, 16 P_t) -- so a phase reads only its own quarters and the
+  // phase-1 DMA of k-tile s + 2 into the (., 0) quarters never races a read (the 256-row layout's
+  // invariant for any height).  Rows of a quarter past 16 P_t are not loaded (wave-uniform skip).
+  constexpr int TROWS = 32 * TMF, P0 = (TMF + 1) / 2, P1 = TMF - P0;
+  static_assert(TMF >= 4 && TMF <= 8, "token tile of 128..256 rows");
+  __shared__ __attribute__((aligned(16))) char smem[2 * KT];
 
   const int G = gridDim.x, nk = a.nk;
   // order of this workgroup: blocks b and b + 8 share an XCD; give each XCD a contiguous range
@@ -158,7 +166,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) xvo[h][t] = ((128 * h + 64 * t + rq) * a.ldx + ch) * 2;
+      for (int t = 0; t < 2; ++t) xvo[h][t] = ((16 * TMF * h + 16 * P0 * t + rq) * a.ldx + ch) * 2;
   }
   constexpr int WSTEP = EPI == PF_EPI_SWIGLU ? 128 : 256;  // weight rows per tile step
   const long w_bytes = 2L * a.K * a.nrows_w;
@@ -170,8 +178,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
                                              static_cast<int>(min(w_bytes - off, 0x7FFFFFFFL)), 0x00020000);
   };
   auto rsrc_x = [&](int tm) -> __amdgpu_buffer_rsrc_t {  // X rows of token tile tm (rows past M: out of range)
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.X) + static_cast<size_t>(tm) * 256 * a.ldx,
-                                             static_cast<short>(0), (a.M - tm * 256) * a.ldx * 2, 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.X) + static_cast<size_t>(tm) * TROWS * a.ldx,
+                                             static_cast<short>(0), (a.M - tm * TROWS) * a.ldx * 2, 0x00020000);
   };
   auto dma_w = [&](int pos, __amdgpu_buffer_rsrc_t rs, int k) {  // both W half-tiles of position pos
     char* dst = smem + (pos & 1) * KT;
@@ -184,20 +192,22 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
   };
   auto dma_x = [&](int pos, __amdgpu_buffer_rsrc_t rs, int k, int t) {  // X quarters (0, t), (1, t) of pos
     char* dst = smem + (pos & 1) * KT + XB + t * QT;
+    if (8 * wid_s < 16 * (t ? P1 : P0)) {  // this wave's 8 rows of the quarter are used
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(dst + h * HT + wid_s * 1024), 16, xvo[h][t], 128 * k,
-                                               0, 0);
+      for (int h = 0; h < 2; ++h)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(dst + h * HT + wid_s * 1024), 16, xvo[h][t], 128 * k,
+                                                 0, 0);
+    }
   };
 
-  float4_ acc[4][8];
+  float4_ acc[4][TMF];
 #pragma unroll
   for (int f = 0; f < 4; ++f)
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc[f][t] = float4_{0.f, 0.f, 0.f, 0.f};
-  float ssq[8];  // RS: sum of x^2 over this lane's k-quarter of token rows 128 wr + 16 t + r16
+    for (int t = 0; t < TMF; ++t) acc[f][t] = float4_{0.f, 0.f, 0.f, 0.f};
+  float ssq[TMF];  // RS: sum of x^2 over this lane's k-quarter of token rows 16 TMF wr + 16 t + r16
 #pragma unroll
-  for (int t = 0; t < 8; ++t) ssq[t] = 0.f;
+  for (int t = 0; t < TMF; ++t) ssq[t] = 0.f;
 
   const int r16 = lane & 15, kq = lane >> 4;
   // fragment addresses: one VGPR base per (operand, k-step); fragments f / t of a wave sit 2048 bytes
@@ -217,11 +227,12 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
       wa[f][1] = *reinterpret_cast<const pf_u32x4*>(p1 + f * 2048);
     }
   };
-  auto rd_x = [&](const char* b, int hb) {
-    const char* p0 = b + xb0 + hb * 8192;
-    const char* p1 = b + xb1 + hb * 8192;
+  auto rd_x = [&](const char* b, int hb) {  // phase hb's fragments, from quarter (wr, hb)
+    const char* p0 = b + xb0 + hb * QT;
+    const char* p1 = b + xb1 + hb * QT;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < P0; ++t) {
+      if (hb && t >= P1) break;
       xb[t][0] = *reinterpret_cast<const pf_u32x4*>(p0 + t * 2048);
       xb[t][1] = *reinterpret_cast<const pf_u32x4*>(p1 + t * 2048);
     }
@@ -231,14 +242,16 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
   auto rs_sum = [&](int hb) {
     if constexpr (RS) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < P0; ++t) {
+        if (hb && t >= P1) break;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
           for (int d = 0; d < 4; ++d) {
             const pf_bf16x2 v = pf_pair(xb[t][kk][d]);
-            ssq[4 * hb + t] = __builtin_amdgcn_fdot2_f32_bf16(v, v, ssq[4 * hb + t], false);
+            ssq[hb * P0 + t] = __builtin_amdgcn_fdot2_f32_bf16(v, v, ssq[hb * P0 + t], false);
           }
+      }
     }
   };
   auto mma = [&](int hb) {
@@ -248,19 +261,21 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
 #pragma unroll
       for (int f = 0; f < 4; ++f)
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-          acc[f][4 * hb + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf_frag(wa[f][kk]), pf_frag(xb[t][kk]),
-                                                                        acc[f][4 * hb + t], 0, 0, 0);
+        for (int t = 0; t < P0; ++t) {
+          if (hb && t >= P1) break;
+          acc[f][hb * P0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf_frag(wa[f][kk]), pf_frag(xb[t][kk]),
+                                                                         acc[f][hb * P0 + t], 0, 0, 0);
+        }
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // epilogue of a finished tile from acc: lane (r16, kq), acc[f][t] = Y[token m0 + 128 wr + 16 t +
+  // epilogue of a finished tile from acc: lane (r16, kq), acc[f][t] = Y[token m0 + 16 TMF wr + 16 t +
   // r16][image column 64 wc + 16 f + 4 kq + e]
   auto epilogue = [&](int tm, int tn) {
-    const int m0 = tm * 256;
+    const int m0 = tm * TROWS;
     if constexpr (RS) {  // the 4 k-quarter lanes of each row: full-row sums -> rstd, applied to acc
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
+      for (int t = 0; t < TMF; ++t) {
         float v = ssq[t];
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
@@ -270,8 +285,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
       }
     }
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int m = m0 + 128 * wr + 16 * t + r16;
+    for (int t = 0; t < TMF; ++t) {
+      const int m = m0 + 16 * TMF * wr + 16 * t + r16;
       if (m >= a.M) continue;
       bf16_t* yr = a.Y + static_cast<size_t>(m) * a.ldy;
       if constexpr (EPI == PF_EPI_RESID) {
@@ -318,14 +333,13 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
 #pragma unroll
     for (int f = 0; f < 4; ++f)
 #pragma unroll
-      for (int t = 0; t < 8; ++t) acc[f][t] = float4_{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < TMF; ++t) acc[f][t] = float4_{0.f, 0.f, 0.f, 0.f};
     if constexpr (RS) {
 #pragma unroll
-      for (int t = 0; t < 8; ++t) ssq[t] = 0.f;
+      for (int t = 0; t < TMF; ++t) ssq[t] = 0.f;
     }
   };
-  // stream-K bookkeeping: first SK iteration of order q, owner of SK iteration i
-  auto sk_start = [&](int q) -> int { return q * I / G; };
+  // stream-K bookkeeping: owner of SK iteration i (order q owns [q I / G, (q + 1) I / G))
   auto sk_owner = [&](int i) -> int { return ((i + 1) * G + I - 1) / I - 1; };
   constexpr int SLAB = PF_SLAB_FRAGS * 512 * 4;  // floats per segment slab
 
@@ -356,6 +370,7 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
     kk = n2.k0 + e - nl;
   };
   __amdgpu_buffer_rsrc_t rw = rsrc_w(seg.tn), rx = rsrc_x(seg.tm);  // the current segment's operands
+  const bool x0_loads = 8 * wid_s < 16 * P0;  // wave-uniform: this wave issues dma_x(., t = 0) pieces
 
   dma_w(0, rw, seg.k0);
   dma_x(0, rx, seg.k0, 0);
@@ -370,7 +385,8 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
       dma_w(1, rsrc_w(tn1), k1);
       dma_x(1, rsrc_x(tm1), k1, 0);
     }
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (x0_loads) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // position 1's 4 W + 2 X pieces
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -414,9 +430,11 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
         dma_w(s, rsrc_w(tn2), k2);
         dma_x(s, rsrc_x(tm2), k2, 0);
       }
-      // the 6 pieces just issued for s + 2 stay in flight: waiting here, after this segment's issue
-      // work, gives the youngest piece of s + 1 (issued at phase 0) the whole segment to land
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      // the pieces just issued for s + 2 (4 W, and 2 X if this wave loads (., 0) rows) stay in flight:
+      // waiting here, after this segment's issue work, gives the youngest piece of s + 1 (issued at
+      // phase 0) the whole segment to land
+      if (x0_loads) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -435,57 +453,71 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
 
     // end of a segment
     bool write = seg.k0 == 0 && seg.k1 == nk;  // the whole tile
-    if (!write) {  // a stream-K segment: publish, and finish the tile if this workgroup arrives last
+#ifdef PF_PROBE_NO_FIXUP  // scripts/probes/gemm_pf_sk_probe.hip: the schedule without the hand-off (wrong sums)
+    write = seg.k0 == 0;
+    if (false) {
+#else
+    if (!write) {  // a stream-K segment of tile l
+#endif
       if (wr == 0) PF_BAR();  // un-stagger: both halves meet here
       const int l = seg.L - a.dp_rounds * G;  // stream-K tile
       const int t0 = l * nk;
       const int o_lo = sk_owner(t0), o_hi = sk_owner(t0 + nk - 1);
-      const int my_slot = 2 * o + (sk_start(o) >= t0 ? 0 : 1);
-      // slab stores / loads through a buffer descriptor: one VGPR offset (tid * 16), the fragment
-      // offset in the scalar field (64-bit addresses per store would not fit the VGPR budget)
-      const __amdgpu_buffer_rsrc_t ms = __builtin_amdgcn_make_buffer_rsrc(
-          a.slab + static_cast<size_t>(my_slot) * SLAB, static_cast<short>(0), SLAB * 4, 0x00020000);
+      if (seg.k0 != 0) {
+        // not the tile's head: publish the partial in this workgroup's slab (a workgroup has at most
+        // one such segment: the first of its range) and count it in.  Hand-off without agent-scope
+        // fences (MI355X_MICROARCH.md "Valid forms", first table row): write-through (sc1) 16-byte
+        // slab stores, every storing wave drained before the barrier, one lane's agent-scope count.
+        const __amdgpu_buffer_rsrc_t ms = __builtin_amdgcn_make_buffer_rsrc(
+            a.slab + static_cast<size_t>(o) * SLAB, static_cast<short>(0), SLAB * 4, 0x00020000);
 #pragma unroll
-      for (int f = 0; f < 4; ++f)
+        for (int f = 0; f < 4; ++f)
 #pragma unroll
-        for (int t = 0; t < 8; ++t)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pf_u32x4, acc[f][t]), ms, tid * 16,
-                                                 (f * 8 + t) * 8192, PF_SC1);
-      if constexpr (RS) {
+          for (int t = 0; t < TMF; ++t)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(pf_u32x4, acc[f][t]), ms, tid * 16,
+                                                   (f * 8 + t) * 8192, PF_SC1);
+        if constexpr (RS) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(pf_u32x4, float4_{ssq[4 * h], ssq[4 * h + 1], ssq[4 * h + 2], ssq[4 * h + 3]}), ms,
-              tid * 16, (32 + h) * 8192, PF_SC1);
-      }
-      // hand-off without agent-scope fences (MI355X_MICROARCH.md "Valid forms", first table row):
-      // write-through (sc1) 16-byte slab stores, every storing wave drained before the barrier, one
-      // lane's agent-scope ticket; the last arriver reads every slab with sc1 loads.  A release fence
-      // here would write back the XCD L2's dirty lines (the other tiles' outputs) on every segment.
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      PF_BAR();  // every wave's slab stores are complete
-      if (tid == 0) {
-        const int ticket = __hip_atomic_fetch_add(a.cnt + l, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = ticket == o_hi - o_lo;
-        if (last) a.cnt[l] = 0;  // re-armed for the next launch
-        flag[0] = last;
-      }
-      PF_LGKM0();
-      PF_BAR();
-      write = flag[0] != 0;
-      PF_BAR();  // flag read by every wave before it is written again
-      if (write) {
-        zero_acc();
-        for (int q = o_lo; q <= o_hi; ++q) {  // segment order: the sum does not depend on arrival
-          const int slot = 2 * q + (sk_start(q) >= t0 ? 0 : 1);
+          for (int h = 0; h < 2; ++h)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(pf_u32x4, float4_{ssq[(4 * h) % TMF], ssq[(4 * h + 1) % TMF],
+                                                     ssq[(4 * h + 2) % TMF], ssq[(4 * h + 3) % TMF]}),
+                ms, tid * 16, (32 + h) * 8192, PF_SC1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PF_BAR();  // every wave's slab stores are complete
+        if (tid == 0) __hip_atomic_fetch_add(a.cnt + l, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        // the tile's head (k-tiles from 0): its segment is the LAST of its range, while the tile's other
+        // segments open their owners' ranges, so they are published by the time it gets here.  It waits
+        // for their count, then adds their slabs to the accumulators it holds, in segment order:
+        // ((s0 + s1) + s2) ... with s0 in registers -- fp32 addition commutes, so the bits do not depend
+        // on which workgroup finishes when.  No own slab round trip, no arrival ticket.
+        if (tid == 0) {
+          const int want = o_hi - o_lo;
+          for (long spin = 0; __hip_atomic_load(a.cnt + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want;
+               ++spin) {
+            if (spin > (1L << 30)) break;  // every owner is a running workgroup of this grid: never taken
+            __builtin_amdgcn_s_sleep(2);
+          }
+          a.cnt[l] = 0;  // re-armed for the next launch
+        }
+        PF_BAR();
+        for (int q = o_lo + 1; q <= o_hi; ++q) {
           const __amdgpu_buffer_rsrc_t ss = __builtin_amdgcn_make_buffer_rsrc(
-              a.slab + static_cast<size_t>(slot) * SLAB, static_cast<short>(0), SLAB * 4, 0x00020000);
+              a.slab + static_cast<size_t>(q) * SLAB, static_cast<short>(0), SLAB * 4, 0x00020000);
 #pragma unroll
-          for (int f = 0; f < 4; ++f) {  // 8 loads in flight at a time (VGPR budget)
+          for (int f = 0; f < 4; f += 2) {  // 16 loads in flight (the k-loop's fragment registers are free)
+            pf_u32x4 v[2][TMF];
 #pragma unroll
-            for (int t = 0; t < 8; ++t)
-              acc[f][t] += __builtin_bit_cast(float4_, __builtin_amdgcn_raw_buffer_load_b128(
-                                                           ss, tid * 16, (f * 8 + t) * 8192, PF_SC1));
+            for (int ff = 0; ff < 2; ++ff)
+#pragma unroll
+              for (int t = 0; t < TMF; ++t)
+                v[ff][t] = __builtin_amdgcn_raw_buffer_load_b128(ss, tid * 16, ((f + ff) * 8 + t) * 8192, PF_SC1);
+#pragma unroll
+            for (int ff = 0; ff < 2; ++ff)
+#pragma unroll
+              for (int t = 0; t < TMF; ++t) acc[f + ff][t] += __builtin_bit_cast(float4_, v[ff][t]);
             __builtin_amdgcn_sched_barrier(0);
           }
           if constexpr (RS) {
@@ -494,10 +526,12 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
               const float4_ v = __builtin_bit_cast(
                   float4_, __builtin_amdgcn_raw_buffer_load_b128(ss, tid * 16, (32 + h) * 8192, PF_SC1));
 #pragma unroll
-              for (int e = 0; e < 4; ++e) ssq[4 * h + e] += v[e];
+              for (int e = 0; e < 4; ++e)
+                if (4 * h + e < TMF) ssq[4 * h + e] += v[e];
             }
           }
         }
+        write = true;
       }
       if (wr == 1) PF_BAR();  // re-stagger
     }
@@ -517,10 +551,13 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
 }
 
 // Launch geometry: grid = min(CUs, work / min_iters) workgroups; full rounds of tiles data-parallel,
-// the rest stream-K.  Returns the grid (0 = not launched: shape unsupported).
-int pf_plan(int M, int N, int K, int epi, int num_cu, int min_iters, int* dp_rounds, int* sk_tiles, int* grid) {
+// the rest stream-K.  trows: token-tile height (256, 192, 160 or 128 rows).  Returns the grid (0 = not
+// launched: shape unsupported).
+int pf_plan(int M, int N, int K, int epi, int num_cu, int min_iters, int* dp_rounds, int* sk_tiles, int* grid,
+            int trows) {
   if (M <= 0 || K % 64 != 0 || N % 256 != 0) return 0;
-  const int ntm = (M + 255) / 256, ntn = epi == PF_EPI_SWIGLU ? N / 256 : N / 256;
+  if (trows != 256 && trows != 192 && trows != 160 && trows != 128) return 0;
+  const int ntm = (M + trows - 1) / trows, ntn = N / 256;
   const int T = ntm * ntn, nk = K / 64;
   const long work = static_cast<long>(T) * nk;
   if (min_iters <= 0) {  // data-parallel only: one workgroup per tile, the last round may be partial
@@ -548,7 +585,7 @@ int pf_plan(int M, int N, int K, int epi, int num_cu, int min_iters, int* dp_rou
 bool launch_gemm_pf(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx, int ldy, int epi,
                     float* slab, long slab_floats, int* cnt, int cnt_len, const int* tile_map, int map_len,
                     int num_cu, int min_iters, hipStream_t s, const bf16_t* R, int ldr, bool row_scale,
-                    float eps) {
+                    float eps, int trows) {
   if (M <= 0 || K % 64 != 0 || ldx % 8 != 0 || ldy % 4 != 0) return false;
   if (epi != PF_EPI_NONE && epi != PF_EPI_SWIGLU && epi != PF_EPI_RESID) return false;
   if (epi == PF_EPI_RESID && (R == nullptr || ldr % 4 != 0 || (reinterpret_cast<uintptr_t>(R) & 7) || row_scale))
@@ -557,10 +594,11 @@ bool launch_gemm_pf(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, i
   if (reinterpret_cast<uintptr_t>(Y) & 7) return false;
   if (N % 256 != 0) return false;  // SwiGLU: N = 2 I with I % 128 == 0
   int dp, sk, G;
-  if (!pf_plan(M, N, K, epi, num_cu, min_iters, &dp, &sk, &G)) return false;
+  if (!pf_plan(M, N, K, epi, num_cu, min_iters, &dp, &sk, &G, trows)) return false;
+  if (row_scale && trows != 256) return false;  // the fused-RMSNorm forms exist at 256 rows
   if (sk > 0 && (slab == nullptr || cnt == nullptr || cnt_len < sk || slab_floats < 2L * G * PF_SLAB_FRAGS * 512 * 4))
     return false;
-  if (tile_map == nullptr || map_len < ((M + 255) / 256) * (N / 256)) return false;
+  if (tile_map == nullptr || map_len < ((M + trows - 1) / trows) * (N / 256)) return false;
   if (static_cast<long>(M) * ldx * 2 > 0x7FFFFFFFL) return false;  // X rows addressed by 32-bit buffer offsets
   PfArgs a;
   a.Y = Y;
@@ -575,7 +613,7 @@ bool launch_gemm_pf(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, i
   a.ldx = ldx;
   a.ldy = ldy;
   a.inter = epi == PF_EPI_SWIGLU ? N / 2 : 0;
-  a.ntm = (M + 255) / 256;
+  a.ntm = (M + trows - 1) / trows;
   a.ntn = N / 256;
   a.nk = K / 64;
   a.dp_rounds = dp;
@@ -585,15 +623,25 @@ bool launch_gemm_pf(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, i
   a.inv_k = 1.f / static_cast<float>(K);
   a.eps = eps;
   const dim3 g(G), b(512);
-  if (epi == PF_EPI_SWIGLU) {
-    if (row_scale) hipLaunchKernelGGL((gemm_pf_kernel<PF_EPI_SWIGLU, true>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((gemm_pf_kernel<PF_EPI_SWIGLU, false>), g, b, 0, s, a);
-  } else if (epi == PF_EPI_RESID) {
-    hipLaunchKernelGGL((gemm_pf_kernel<PF_EPI_RESID, false>), g, b, 0, s, a);
-  } else {
-    if (row_scale) hipLaunchKernelGGL((gemm_pf_kernel<PF_EPI_NONE, true>), g, b, 0, s, a);
-    else hipLaunchKernelGGL((gemm_pf_kernel<PF_EPI_NONE, false>), g, b, 0, s, a);
+#define MXS_PF(E, RSV, T) hipLaunchKernelGGL((gemm_pf_kernel<E, RSV, T>), g, b, 0, s, a)
+#define MXS_PF_ROWS(E)              \
+  switch (trows) {                  \
+    case 192: MXS_PF(E, false, 6); break; \
+    case 160: MXS_PF(E, false, 5); break; \
+    case 128: MXS_PF(E, false, 4); break; \
+    default: MXS_PF(E, false, 8); break;  \
   }
+  if (epi == PF_EPI_SWIGLU) {
+    if (row_scale) MXS_PF(PF_EPI_SWIGLU, true, 8);
+    else MXS_PF_ROWS(PF_EPI_SWIGLU);
+  } else if (epi == PF_EPI_RESID) {
+    MXS_PF_ROWS(PF_EPI_RESID);
+  } else {
+    if (row_scale) MXS_PF(PF_EPI_NONE, true, 8);
+    else MXS_PF_ROWS(PF_EPI_NONE);
+  }
+#undef MXS_PF_ROWS
+#undef MXS_PF
   MXS_CHECK_LAUNCH();
   return true;
 }

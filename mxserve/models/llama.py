@@ -72,6 +72,10 @@ class TransformerLM:
         # TP = 1 dense models on the GPU, prefill / mixed steps: RMSNorms inside the consumer GEMMs and
         # residual adds inside the producers (_forward_pf); self.wf holds the norm-folded weights
         self.fuse_prefill = os.environ.get("MXS_PF_FUSED", "1") == "1"
+        # pure-decode steps of more than 256 rows: the prefill chain (_forward_pf: gemm_pf / the
+        # prefill-bucket tables) or the decode chain (_forward_fused: the decode table's tuned forms
+        # with their rope / add+norm epilogues).  MXS_PF_DECODE=1 keeps the prefill chain.
+        self.pf_decode = os.environ.get("MXS_PF_DECODE", "1") == "1"
         self.pf_chain = False
         self.wf: dict[str, torch.Tensor] = {}
         # fp8 KV cache: stored = x / scale, per layer (1.0 until the runner calibrates them from a
@@ -369,7 +373,7 @@ class TransformerLM:
         c = self.cfg
         # steps with prefill chunks: the last layer only computes the rows that produce logits
         prune = self.prune_last_layer and md.num_prefills > 0 and md.sample_seq is not None
-        if self.pf_chain and input_ids.shape[0] > 256 and input_ids.is_cuda:
+        if self.pf_chain and input_ids.shape[0] > 256 and input_ids.is_cuda and (md.num_prefills > 0 or self.pf_decode):
             return self._forward_pf(input_ids, md, kv_cache, prune)
         # K01: the embedding gather runs inside the first layer's input RMSNorm kernel
         h, residual = ops.embed_rms_norm(input_ids, self.w["embed"], self.w["l0.in_norm"], c.rms_norm_eps)

@@ -105,10 +105,11 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         if M > 256:
             # prefill chunks: the persistent stream-K MFMA kernel where the start-up tuner measured it
             # faster (ops/prefill_pf.py)
-            from .prefill_pf import TABLE as PF_TABLE
+            from .prefill_pf import TABLE as PF_TABLE, pf_cfg
             mi = PF_TABLE.lookup(M, w.shape[0], w.shape[1], 0)
             if mi is not None:
-                out = gemm_pf(x, w, 0, None, mi)
+                it, tr = pf_cfg(mi)
+                out = gemm_pf(x, w, 0, None, it, trows=tr)
                 if out is not None:
                     return out
             # small prefill chunks: the 64/128-row tile kernel where it was measured faster
@@ -250,20 +251,23 @@ def pf_tile_map(ntm: int, ntn: int, device, gm: int = 8) -> torch.Tensor:
 
 def gemm_pf(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None,
             min_iters: int = 16, resid: Optional[torch.Tensor] = None, row_scale: bool = False,
-            eps: float = 1e-5) -> Optional[torch.Tensor]:
+            eps: float = 1e-5, trows: int = 256) -> Optional[torch.Tensor]:
     """Prefill GEMM on the hand-written persistent stream-K kernel: epi 0 x @ w.T, epi 1 SiLU(x @
     gate.T) * (x @ up.T) with w = [gate; up], epi 2 resid + x @ w.T (out may be resid: in place).
     row_scale (epi 0 / 1): every row of the product is scaled by rsqrt(mean(x_row^2) + eps), i.e.
     RMSNorm(x) @ w'.T with the norm weight folded into w' (fold_norm_weight).  None when the shape is
-    not supported."""
+    not supported.  trows: token-tile height (256, 192, 160, 128): fewer rows per tile fill the CUs
+    better when a 256-row tiling leaves a partial last round (e.g. 6,656 rows x 2,048 columns: 208
+    tiles of 256 rows on 256 CUs, 240 of 224... 256 of 128 would be one full round at half the work
+    per tile)."""
     M, N = x.shape[0], w.shape[0]
     if N % 256:
         return None
     if out is None:
         out = torch.empty(M, N // 2 if epi == 1 else N, dtype=x.dtype, device=x.device)
     slab, cnt, ncu = _pf_workspace(x.device)
-    tmap = pf_tile_map(-(-M // 256), N // 256, x.device)
-    if not ext().gemm_pf(out, x, w, epi, slab, cnt, tmap, ncu, min_iters, resid, row_scale, eps):
+    tmap = pf_tile_map(-(-M // trows), N // 256, x.device)
+    if not ext().gemm_pf(out, x, w, epi, slab, cnt, tmap, ncu, min_iters, resid, row_scale, eps, trows):
         return None
     return out
 
@@ -279,10 +283,11 @@ def gate_up_silu(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     with SiLU*mul in its epilogue when tuned faster; prefill-sized: the stream-K kernel with the same
     epilogue (ops/prefill_pf.py); otherwise hipBLASLt + the SiLU*mul kernel."""
     if _gpu(x) and x.dim() == 2 and x.shape[0] > _decode_max_m():
-        from .prefill_pf import TABLE as PF_TABLE
+        from .prefill_pf import TABLE as PF_TABLE, pf_cfg
         mi = PF_TABLE.lookup(x.shape[0], w.shape[0], w.shape[1], 1)
         if mi is not None:
-            out = gemm_pf(x, w, 1, None, mi)
+            it, tr = pf_cfg(mi)
+            out = gemm_pf(x, w, 1, None, it, trows=tr)
             if out is not None:
                 return out
     if _gpu(x) and x.dim() == 2 and x.shape[0] <= _decode_max_m():

@@ -28,8 +28,24 @@ import torch
 
 MODE = os.environ.get("MXS_GEMM_PF", "auto")
 MIN_ITERS = (0, 8, 16, 32)  # 0: data-parallel tiles only (no stream-K)
+# (token-tile rows, min_iters) candidates of the plain / SwiGLU / residual forms: the 256-row tile is the
+# most efficient per CU, the shorter ones fill the CUs when 256-row tiles leave a partial last round
+# (qkv at 6,144 rows: 192-row tiles 1.16x hipBLASLt where 256 reach 0.92x, profiles/r5/prefill_gemm)
+CANDIDATES = tuple((256, mi) for mi in MIN_ITERS) + ((192, 0), (192, 32), (160, 0), (160, 32), (128, 0), (128, 8))
 WIN_MARGIN = 0.98  # gemm_pf must be this much faster than the path it replaces
 ROUNDS = 3
+
+
+def pf_cfg(cfg) -> tuple:
+    """(min_iters, token-tile rows) of a stored gemm_pf choice: an int is min_iters at 256 rows (tables
+    of earlier rounds), a pair is [rows, min_iters]."""
+    if isinstance(cfg, (list, tuple)):
+        return int(cfg[1]), int(cfg[0])
+    return int(cfg), 256
+
+
+def is_pf(cfg) -> bool:
+    return isinstance(cfg, int) or (isinstance(cfg, (list, tuple)) and len(cfg) == 2)
 
 
 def buckets_for(max_rows: int) -> list:
@@ -51,8 +67,8 @@ class PfTable:
         self.report: list = []
 
     def lookup(self, M: int, N: int, K: int, epi: int):
-        """min_iters of gemm_pf for this (shape, code) at M rows, None for the unfused path; code 2
-        may also hold "addmm" (hipBLASLt with beta = 1)."""
+        """The gemm_pf choice for this (shape, code) at M rows (pf_cfg() unpacks it), None for the
+        unfused path; code 2 may also hold "addmm" (hipBLASLt with beta = 1)."""
         if MODE == "off" or M <= 256 or N % 256 or K % 64:
             return None
         if MODE == "on":
@@ -112,19 +128,20 @@ def tune(weights: dict, max_rows: int, device, dtype=torch.bfloat16) -> list:
                 best, best_t, t_base, source = st.get("cfg"), st.get("us"), st.get("base_us"), "table"
             else:
                 source = "measured"
-                tb, tc = [], {mi: [] for mi in MIN_ITERS}
+                tb, tc = [], {c: [] for c in CANDIDATES}
                 for _ in range(ROUNDS):
                     tb.append(_time(base))
-                    for mi in MIN_ITERS:
-                        tc[mi].append(_time(lambda: ops.gemm_pf(x, w, epi, out, mi)))
+                    for c in CANDIDATES:
+                        tc[c].append(_time(lambda: ops.gemm_pf(x, w, epi, out, c[1], trows=c[0])))
                 t_base = median(tb)
                 best, best_t = None, t_base
-                for mi in MIN_ITERS:
-                    t = median(tc[mi])
+                for c in CANDIDATES:
+                    t = median(tc[c])
                     if t < t_base * WIN_MARGIN and t < best_t:
-                        best, best_t = mi, t
+                        best, best_t = list(c), t
             if best is not None:
-                ops.gemm_pf(x, w, epi, out, best)
+                mi, tr = pf_cfg(best)
+                ops.gemm_pf(x, w, epi, out, mi, trows=tr)
                 err = (out.float() - ref.float()).abs().max().item()
                 if not err <= 0.02 * max(1.0, ref.float().abs().max().item()):
                     best, best_t = None, t_base
@@ -132,7 +149,7 @@ def tune(weights: dict, max_rows: int, device, dtype=torch.bfloat16) -> list:
                 store.put(key, {"cfg": best, "us": best_t and round(best_t, 2), "base_us": round(t_base, 2)})
             ent.append((M, best))
             rows.append({"proj": name, "M": M, "N": N, "K": K, "epi": epi, "base_us": t_base and round(t_base, 2),
-                         "chosen": "hipblaslt" if best is None else f"gemm_pf/{best}",
+                         "chosen": "hipblaslt" if best is None else "gemm_pf/%d/%d" % pf_cfg(best)[::-1],
                          "us": best_t and round(best_t, 2), "source": source})
         TABLE.entries[(N, K, epi)] = ent
     TABLE.report = rows
@@ -151,8 +168,8 @@ def norm_linear(r: torch.Tensor, w: torch.Tensor, wf: Optional[torch.Tensor], no
     routed unfused GEMM."""
     from .. import ops
     mi = TABLE.lookup(r.shape[0], w.shape[0], w.shape[1], CODE_RS + epi) if wf is not None else None
-    if isinstance(mi, int):
-        out = ops.gemm_pf(r, wf, epi, None, mi, row_scale=True, eps=eps)
+    if is_pf(mi):
+        out = ops.gemm_pf(r, wf, epi, None, pf_cfg(mi)[0], row_scale=True, eps=eps)
         if out is not None:
             return out
     x = ops.rms_norm(r, norm_w, eps)
@@ -163,7 +180,7 @@ def resid_linear(x: torch.Tensor, w: torch.Tensor, r: torch.Tensor) -> torch.Ten
     """r += x @ w.T in place (o_proj / down_proj into the residual stream)."""
     from .. import ops
     mi = TABLE.lookup(x.shape[0], w.shape[0], w.shape[1], CODE_RESID)
-    if isinstance(mi, int) and ops.gemm_pf(x, w, 2, r, mi, resid=r) is not None:
+    if is_pf(mi) and ops.gemm_pf(x, w, 2, r, pf_cfg(mi)[0], resid=r, trows=pf_cfg(mi)[1]) is not None:
         return r
     if mi == "addmm":
         return r.addmm_(x, w.t())
@@ -215,11 +232,11 @@ def tune_fused(weights: dict, max_rows: int, device, dtype=torch.bfloat16, eps: 
                 if code == CODE_RESID:
                     r = torch.randn(M, N, device=device).to(dtype)
                     bases = {None: lambda: r.add_(ops.linear(x, w)), "addmm": lambda: r.addmm_(x, w.t())}
-                    cand = {mi: (lambda mi=mi: ops.gemm_pf(x, w, 2, r, mi, resid=r)) for mi in MIN_ITERS}
+                    cand = {c: (lambda c=c: ops.gemm_pf(x, w, 2, r, c[1], resid=r, trows=c[0])) for c in CANDIDATES}
                 else:
                     bases = {None: (lambda: ops.linear(ops.rms_norm(x, nw, eps), w)) if epi == 0 else
                              (lambda: ops.gate_up_silu(ops.rms_norm(x, nw, eps), w))}
-                    cand = {mi: (lambda mi=mi: ops.gemm_pf(x, wf, epi, None, mi, row_scale=True, eps=eps))
+                    cand = {(256, mi): (lambda mi=mi: ops.gemm_pf(x, wf, epi, None, mi, row_scale=True, eps=eps))
                             for mi in MIN_ITERS}
                 tb = {k: [] for k in bases}
                 tc = {k: [] for k in cand}
@@ -231,21 +248,22 @@ def tune_fused(weights: dict, max_rows: int, device, dtype=torch.bfloat16, eps: 
                 bk = min(tb, key=lambda k: median(tb[k]))
                 t_base = median(tb[bk])
                 best, best_t = bk, t_base
-                for mi in MIN_ITERS:
-                    t = median(tc[mi])
+                for c in cand:
+                    t = median(tc[c])
                     if t < t_base * WIN_MARGIN and t < best_t:
-                        best, best_t = mi, t
-            if isinstance(best, int):  # correctness of the kept kernel against the unfused path
+                        best, best_t = list(c), t
+            if is_pf(best):  # correctness of the kept kernel against the unfused path
+                bmi, btr = pf_cfg(best)
                 if code == CODE_RESID:
                     r0 = torch.randn(M, N, device=device).to(dtype)
                     want = r0.float() + ops.linear(x, w).float()
-                    got = ops.gemm_pf(x, w, 2, None, best, resid=r0)
+                    got = ops.gemm_pf(x, w, 2, None, bmi, resid=r0, trows=btr)
                 else:
                     want = ops.linear(ops.rms_norm(x, torch.ones(K, device=device, dtype=dtype), eps), w)
                     if epi == 1:
                         want = ops.silu_mul(want)
                     want = want.float()
-                    got = ops.gemm_pf(x, w, epi, None, best, row_scale=True, eps=eps)
+                    got = ops.gemm_pf(x, w, epi, None, bmi, row_scale=True, eps=eps)
                 err = (got.float() - want).abs().max().item()
                 if not err <= 0.03 * max(1.0, want.abs().max().item()):
                     best, best_t = None, t_base
@@ -253,7 +271,7 @@ def tune_fused(weights: dict, max_rows: int, device, dtype=torch.bfloat16, eps: 
                 store.put(key, {"cfg": best, "us": best_t and round(best_t, 2), "base_us": round(t_base, 2)})
             ent.append((M, best))
             rows.append({"proj": name, "M": M, "N": N, "K": K, "code": code, "base_us": t_base and round(t_base, 2),
-                         "chosen": f"gemm_pf/{best}" if isinstance(best, int) else (best or "unfused"),
+                         "chosen": ("gemm_pf/%d/%d" % pf_cfg(best)[::-1]) if is_pf(best) else (best or "unfused"),
                          "us": best_t and round(best_t, 2), "source": source})
         TABLE.entries[(N, K, code)] = ent
     TABLE.report = TABLE.report + rows

@@ -10,7 +10,7 @@ in a JSON file keyed by GPU architecture and CU count:
     same hardware runs the same kernels;
   * shapes not in the table are timed (median of repeated hipGraph timings, ops/decode_gemm.py) and
     added; MXS_TUNED_SAVE=1 writes the grown table back (to MXS_TUNED_DIR when set, else the package
-    directory), MXS_RETUNE=1 ignores the stored choices.
+    directory), MXS_RETUNE=1 ignores the stored choices (MXS_RETUNE=prefill_pf: only that table's).
 """
 from __future__ import annotations
 
@@ -47,7 +47,8 @@ class TunedStore:
     def __init__(self, kind: str, tag: str):
         self.kind = kind
         self.tag = tag
-        self.retune = os.environ.get("MXS_RETUNE") == "1"
+        rt = os.environ.get("MXS_RETUNE", "")
+        self.retune = rt == "1" or kind in rt.split(",")  # "1": every table; "prefill_pf,...": those kinds
         self.save_enabled = os.environ.get("MXS_TUNED_SAVE") == "1"
         d = os.environ.get("MXS_TUNED_DIR")
         self.read_paths = ([os.path.join(d, self.filename)] if d else []) + [os.path.join(PKG_DIR, self.filename)]

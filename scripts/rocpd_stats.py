@@ -14,8 +14,48 @@ def main():
     ap.add_argument("--per", type=float, default=1.0)
     ap.add_argument("--csv", default="")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--by-grid", default="", help="also break kernels whose name contains this down by grid size")
+    ap.add_argument("--busy", type=float, default=0.0,
+                    help="print the GPU-busy fraction (union of kernel intervals) per bin of this many seconds")
     a = ap.parse_args()
     db = sqlite3.connect(a.db)
+    if a.busy:
+        iv = db.execute("select start, end from kernels order by start").fetchall()
+        t0, t1 = iv[0][0], max(e for _, e in iv)
+        binw = int(a.busy * 1e9)
+        nb = (t1 - t0) // binw + 1
+        busy = [0] * nb
+        cs, ce = iv[0]
+        def add(s_, e_):
+            while s_ < e_:
+                b = (s_ - t0) // binw
+                be = t0 + (b + 1) * binw
+                busy[b] += min(e_, be) - s_
+                s_ = min(e_, be)
+        for s_, e_ in iv[1:]:
+            if s_ > ce:
+                add(cs, ce)
+                cs, ce = s_, e_
+            else:
+                ce = max(ce, e_)
+        add(cs, ce)
+        print("-- GPU busy per bin (union of kernel intervals)")
+        for i, b in enumerate(busy):
+            print(f"{i * a.busy:7.1f}s  {100.0 * b / binw:6.2f}%")
+    cols = [r[1] for r in db.execute("pragma table_info(kernels)").fetchall()]
+    if a.by_grid:
+        gx = next((c for c in cols if c.lower() in ("grid_size_x", "grid_x", "grid_size")), None)
+        gy = next((c for c in cols if c.lower() in ("grid_size_y", "grid_y")), None)
+        wx = next((c for c in cols if c.lower() in ("workgroup_size_x", "workgroup_x", "workgroup_size")), None)
+        if gx is None:
+            print("columns:", cols)
+        else:
+            q = (f"select name, {gx}, {gy or 0}, {wx or 0}, count(*), sum(end - start) from kernels where name like ? "
+                 f"group by name, {gx}, {gy or 0} order by 6 desc")
+            tot = db.execute("select sum(end - start) from kernels").fetchone()[0]
+            print(f"-- by grid ({a.by_grid})")
+            for n, x, y, w, c, t in db.execute(q, (f"%{a.by_grid}%",)).fetchall()[:a.top]:
+                print(f"{100.0 * t / tot:6.2f}%  {c:7d} calls  {t / 1e3 / c:9.2f} us  grid {x}x{y} wg {w}  {n[:90]}")
     rows = db.execute("select name, count(*), sum(end - start) from kernels group by name order by 3 desc").fetchall()
     tot = sum(r[2] for r in rows)
     out = [(n, c, t / 1e3, t / 1e3 / c, 100.0 * t / tot) for n, c, t in rows]

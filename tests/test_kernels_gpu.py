@@ -1040,7 +1040,7 @@ def test_rope_kv_only(gpu, T, D, hkv, slot_kind, kv_fp8):
                                        (300, 512, 192, 1), (2048, 4096, 1024, 1), (777, 768, 4096, 0)])
 def test_gemm_pf(gpu, M, N, K, epi):
     """Persistent stream-K prefill GEMM (csrc/kernels/gemm_pf.hip) vs fp32: data-parallel rounds,
-    stream-K tails (tiles split over workgroups, finished by the last arriver), row counts that are not
+    stream-K tails (tiles split over workgroups, finished by the head segment), row counts that are not
     tile multiples, SwiGLU epilogue; bitwise repeatable, tile counters left zero."""
     x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
     w = ((torch.rand(N, K, device=gpu) * 2 - 1) * 2 * K ** -0.5).to(torch.bfloat16)
@@ -1048,11 +1048,11 @@ def test_gemm_pf(gpu, M, N, K, epi):
     ref = x.float() @ w.float().t()
     if epi == 1:
         ref = torch.nn.functional.silu(ref[:, :N // 2]) * ref[:, N // 2:]
-    for mi in (4, 16, 64):
+    for tr, mi in [(256, 4), (256, 16), (256, 64), (192, 0), (192, 8), (160, 0), (160, 16), (128, 0), (128, 8)]:
         out = torch.full((M, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
-        assert ops.gemm_pf(x, w, epi, out, mi) is not None
-        _close(out, ref, atol=2e-2, rtol=2e-2, name=f"gemm_pf {M}x{N}x{K} epi{epi} min_iters {mi}")
-        again = ops.gemm_pf(x, w, epi, None, mi)
+        assert ops.gemm_pf(x, w, epi, out, mi, trows=tr) is not None
+        _close(out, ref, atol=2e-2, rtol=2e-2, name=f"gemm_pf {M}x{N}x{K} epi{epi} rows {tr} min_iters {mi}")
+        again = ops.gemm_pf(x, w, epi, None, mi, trows=tr)
         assert torch.equal(again, out), "stream-K sum must not depend on arrival order"
     slab, cnt, _ = ops._pf_workspace(x.device)
     assert int(cnt.abs().sum()) == 0
@@ -1093,11 +1093,11 @@ def test_gemm_pf_residual(gpu, M, N, K):
     w = (torch.randn(N, K, device=gpu, generator=g) * K ** -0.5).to(torch.bfloat16)
     r = (torch.randn(M, N, device=gpu, generator=g) * 4).to(torch.bfloat16)
     ref = r.float() + x.float() @ w.float().t()
-    for mi in (0, 16):
-        out = ops.gemm_pf(x, w, 2, None, mi, resid=r)
-        _close(out, ref, atol=3e-2, rtol=2e-2, name=f"gemm_pf resid {M}x{N}x{K} mi {mi}")
+    for mi, tr in ((0, 256), (16, 256), (8, 160), (0, 128)):
+        out = ops.gemm_pf(x, w, 2, None, mi, resid=r, trows=tr)
+        _close(out, ref, atol=3e-2, rtol=2e-2, name=f"gemm_pf resid {M}x{N}x{K} mi {mi} rows {tr}")
         rr = r.clone()
-        assert ops.gemm_pf(x, w, 2, rr, mi, resid=rr) is not None
+        assert ops.gemm_pf(x, w, 2, rr, mi, resid=rr, trows=tr) is not None
         assert torch.equal(rr, out), "in place == out of place"
 
 
