@@ -24,6 +24,16 @@ constexpr int kPBS = 16;
 constexpr float kPLog2e = 1.4426950408889634f;
 
 __device__ __forceinline__ bf16x8_t as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 
 template <int D, int G>
 __global__ void __launch_bounds__(256) paged_prefill_kernel(
@@ -293,22 +303,46 @@ __device__ __forceinline__ uint4 ld8_kv(const char* p) {
 // [T, Hq, D] q tensor and its write + re-read disappear).  A lane's chunks ks and ks + KS / 2 hold
 // dims d and d + D / 2, i.e. both halves of its rotation pairs.  q is rounded to bf16 after the
 // rotation, as the standalone rope kernel stores it.
-template <int D, int G, int EB>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(D == 64 ? 4 : 1, D == 64 ? 4 : 8)))
+//
+// VAR: softmax variant bits (VALU issue is what bounds a tile at D = 64: per 16 MFMAs of a 64-key
+// tile one wave issues 32 v_exp (8 cycles each), 32 row-sum adds, a 32-element max chain, 16 cvt_pk
+// and 16 accumulator moves, ~840 issue cycles against 512 matrix-pipe cycles):
+//   1  biased reference, overflow check instead of a max: after a row's first tile the reference m
+//      sits kBias = 64 above its running max, so every later p = exp2(s - m) <= 2^-64 unless s passes
+//      the running max by 65.  That is caught after the exponentials by OR-ing the packed bf16 P words
+//      and testing the top exponent bit of each half (p >= 2); the rare tile that trips it is redone
+//      with a real max (one more QK^T from the same LDS tile) and a rescale.  f32 / bf16 keep the
+//      2^-64-scaled values at full relative precision (normals reach 2^-126), and O / l cancel it.
+//   2  row sum on the matrix pipe: lsum = ones^T . P^T (4 MFMAs per tile) instead of 32 VALU adds.
+//   4  the QK^T chain starts from a persistent -m register block (C operand) instead of 16 moves.
+//   8  256-thread workgroups (4 waves x 32 rows, 128 rows): three per CU at D = 64, so 168 registers
+//      a wave instead of 128 (4 waves per SIMD) or 256 (2 per SIMD) -- room for bits 2 / 4 without
+//      halving the waves that hide each other's softmax latency.
+// Bits 2 / 4 need more than the 128 registers of 4 waves per SIMD: with 512 threads they run 2 per SIMD.
+constexpr int kPf3DefaultVar = 0;
+constexpr int pf3_threads(int VAR) { return (VAR & 8) ? 256 : 512; }
+constexpr int pf3_wpe(int D, int VAR) {
+  return (VAR & 8) ? (D == 64 ? 3 : 2) : (D == 64 ? ((VAR & 6) ? 2 : 4) : 0);
+}
+
+template <int D, int G, int EB, int VAR>
+__global__ void __launch_bounds__(pf3_threads(VAR))
+__attribute__((amdgpu_waves_per_eu(pf3_wpe(D, VAR) ? pf3_wpe(D, VAR) : 1, pf3_wpe(D, VAR) ? pf3_wpe(D, VAR) : 8)))
 paged_prefill_v3_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const void* __restrict__ kv, long block_stride,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ qsl,
     const int* __restrict__ seq_lens, int Hkv, float scale, float v_scale, int q_stride,
     const int64_t* __restrict__ qpos_tab, const float* __restrict__ cos_sin) {
   constexpr int KS = D / 16, DT = D / 32;
-  constexpr int BQ = 256 / G;        // query tokens per workgroup
+  constexpr int NT = pf3_threads(VAR);
+  constexpr int BQ = NT / 2 / G;     // query tokens per workgroup (32 rows per wave)
   constexpr int KT = 64;             // keys per tile
   constexpr int KROW = D * 2;        // bytes of one K row in LDS
   constexpr int KCH = D / 8;         // 16-byte chunks per K row
   constexpr int KBYTES = KT * KROW;
   constexpr int VBYTES = D * KT * 2; // [D][64 keys]
-  constexpr int NK = KT * KCH / 512; // K chunks staged per thread per tile
-  constexpr int NV = D * 8 / 512;    // V chunks (8 keys of one dim) staged per thread per tile
+  constexpr int NK = KT * KCH / NT;  // K chunks staged per thread per tile
+  constexpr int NV = D * 8 / NT;     // V chunks (8 keys of one dim) staged per thread per tile
   // LDS chunk swizzles: a ds_read_b128 serves 16 lanes = 16 consecutive rows per pass.  128-byte rows
   // (K at D = 64, V always) put rows r and r + 2 on the same banks: XOR the 16-byte chunk with
   // (row >> 1) & 7 so the 16 rows hit 16 distinct slots (rows 2j, 2j + 1 share a swizzle but sit
@@ -391,31 +425,31 @@ paged_prefill_v3_kernel(
 
   // ---- staging: global -> registers (tile k0), registers -> LDS buffer
   uint4 sk[NK], sv[NV];
-  // A staging chunk's cache block is wave-uniform: chunk ci = tid + 512 n covers keys of block
+  // A staging chunk's cache block is wave-uniform: chunk ci = tid + NT n covers keys of block
   // ci / (2 D) (2 D >= 128 chunks per block, waves are 64 consecutive threads), so each wave reads its
   // block id with one scalar load and adds a per-lane offset fixed for the whole loop (no per-lane
   // select among the tile's four block ids, no 64-bit multiply per chunk).
   size_t koff[NK], voff[NV];
 #pragma unroll
   for (int n = 0; n < NK; ++n) {
-    const int ci = tid + 512 * n, key = ci / KCH, ch = ci % KCH;
+    const int ci = tid + NT * n, key = ci / KCH, ch = ci % KCH;
     koff[n] = k_head_off + static_cast<size_t>((key & 15) * (D * EB) + ch * 8 * EB);
   }
 #pragma unroll
   for (int n = 0; n < NV; ++n) {
-    const int rem = (tid + 512 * n) % (2 * D), dim = rem >> 1, half = rem & 1;
+    const int rem = (tid + NT * n) % (2 * D), dim = rem >> 1, half = rem & 1;
     voff[n] = v_head_off + static_cast<size_t>(dim * 16 * EB + half * 8 * EB);
   }
   auto gload = [&](int k0) {
 #pragma unroll
     for (int n = 0; n < NK; ++n) {
-      const int blk = __builtin_amdgcn_readfirstlane((tid + 512 * n) / (2 * D));
+      const int blk = __builtin_amdgcn_readfirstlane((tid + NT * n) / (2 * D));
       const long b = bt[min(k0 / kPBS + blk, last_blk)];
       sk[n] = ld8_kv<EB>(kvb + b * bstride + koff[n]);
     }
 #pragma unroll
     for (int n = 0; n < NV; ++n) {
-      const int ci = tid + 512 * n, blk = __builtin_amdgcn_readfirstlane(ci / (2 * D)), half = (ci % (2 * D)) & 1;
+      const int ci = tid + NT * n, blk = __builtin_amdgcn_readfirstlane(ci / (2 * D)), half = (ci % (2 * D)) & 1;
       const long b = bt[min(k0 / kPBS + blk, last_blk)];
       uint4 v = ld8_kv<EB>(kvb + b * bstride + voff[n]);
       const int kb = k0 + blk * 16 + half * 8;  // keys >= L: zero (unwritten cache bytes may be NaN)
@@ -433,12 +467,12 @@ paged_prefill_v3_kernel(
     char* vl = lds[buf] + KBYTES;
 #pragma unroll
     for (int n = 0; n < NK; ++n) {
-      const int ci = tid + 512 * n, key = ci / KCH, ch = ci % KCH;
+      const int ci = tid + NT * n, key = ci / KCH, ch = ci % KCH;
       *reinterpret_cast<uint4*>(kl + key * KROW + ((ch ^ kswz(key)) << 4)) = sk[n];
     }
 #pragma unroll
     for (int n = 0; n < NV; ++n) {
-      const int ci = tid + 512 * n, blk = ci / (2 * D), rem = ci % (2 * D), dim = rem >> 1, half = rem & 1;
+      const int ci = tid + NT * n, blk = ci / (2 * D), rem = ci % (2 * D), dim = rem >> 1, half = rem & 1;
       // keys blk*16 + 8 half + j: j < 4 -> group position 4 half + j, j >= 4 -> 8 + 4 half + j - 4
       char* row = vl + dim * (KT * 2);
       const int c0 = blk * 2 + 0, c1 = blk * 2 + 1;  // 16-byte chunks of this block's 16 keys
@@ -454,26 +488,31 @@ paged_prefill_v3_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
   float m = -INFINITY, l = 0.f;
+  constexpr bool ORCHK = VAR & 1, MSUM = VAR & 2, CBLK = VAR & 4;
+  constexpr float kBias = 64.f;
+  float16_ negm, lsum;  // CBLK: -m in every element; MSUM: the row sum (every element holds it)
+  bf16x8_t ones;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) negm[i] = lsum[i] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = static_cast<__bf16>(1.f);
 
-  // Scores are accumulated relative to the running max: the QK^T accumulator starts at -m (the
-  // row's max so far), so exp2 reads the MFMA output directly and the per-element subtraction is
-  // gone from the VALU stream (at D = 64 the softmax VALU, not the MFMA pipe, bounds a tile).  The
-  // first tile of a row starts at 0 and sets m from its own max; later tiles only move m (lazy
-  // rescale) when their max exceeds it by more than 2^8.
-  auto compute = [&](int buf, int k0) {
-    const char* kl = lds[buf];
-    const char* vl = lds[buf] + KBYTES;
-    const bool first = k0 == 0;
-    const float off = first ? 0.f : -m;
-    float16_ sacc[2];
+  // Scores are accumulated relative to the reference m: the QK^T accumulator starts at -m, so exp2
+  // reads the MFMA output directly and the per-element subtraction is gone from the VALU stream (at
+  // D = 64 the softmax VALU, not the MFMA pipe, bounds a tile).  The first tile of a row starts at 0
+  // and sets m from its own max; later tiles move m (lazy rescale) when their max exceeds it by more
+  // than 2^8 (VAR 0) or trips the overflow check (VAR & 1, see above).
+  // K fragments two reads ahead of their MFMAs (sched_group_barrier pins the order: left alone,
+  // hipcc serialises read -> wait -> MFMA eight times per tile; 210.6 -> 205.5 us per layer at an
+  // 8192-token chunk).  The softmax stays in scalar f32: packed v_pk_add_f32 beside MFMAs costs more
+  // than it saves (MI355X_MICROARCH: an anti-lever; measured 205.5 -> 223.9 us).
+  auto qk = [&](const char* kl, float16_ (&sacc)[2], float off) {
+    if constexpr (!CBLK) {
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[kt][i] = off;
-    // K fragments two reads ahead of their MFMAs (sched_group_barrier pins the order: left alone,
-    // hipcc serialises read -> wait -> MFMA eight times per tile; 210.6 -> 205.5 us per layer at an
-    // 8192-token chunk).  The softmax below stays in scalar f32: packed v_pk_add_f32 beside MFMAs
-    // costs more than it saves (MI355X_MICROARCH: an anti-lever; measured 205.5 -> 223.9 us).
+        for (int i = 0; i < 16; ++i) sacc[kt][i] = off;
+    }
     uint4 ka[2 * KS];
 #pragma unroll
     for (int idx = 0; idx < 2 * KS; ++idx) {
@@ -482,7 +521,8 @@ paged_prefill_v3_kernel(
     }
 #pragma unroll
     for (int idx = 0; idx < 2 * KS; ++idx)
-      sacc[idx / KS] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ka[idx]), qf[idx % KS], sacc[idx / KS], 0, 0, 0);
+      sacc[idx / KS] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ka[idx]), qf[idx % KS],
+                                                               (CBLK && idx % KS == 0) ? negm : sacc[idx / KS], 0, 0, 0);
     __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
     for (int idx = 0; idx < 2 * KS - 2; ++idx) {
@@ -490,56 +530,135 @@ paged_prefill_v3_kernel(
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-    if (k0 + KT - 1 > wave_min_pos) {  // tile crosses the diagonal (or the end) of some row of this wave
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int kk = k0 + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (kk > qpos) sacc[kt][i] = -INFINITY;
-        }
-    }
-    float mx = sacc[0][0];  // relative to m (absolute on the first tile)
+  };
+  auto mask = [&](float16_ (&sacc)[2], int k0) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sacc[kt][i]);
-    {  // the row's other half lives 32 lanes away: one permlane32 swap, not an LDS bpermute round trip
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      for (int i = 0; i < 16; ++i) {
+        const int kk = k0 + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (kk > qpos) sacc[kt][i] = -INFINITY;
+      }
+  };
+  auto rowmax = [&](const float16_ (&sacc)[2]) {
+    // a balanced max3 tree (depth 4; the 17-deep max chain it replaces was on the critical path from
+    // the QK^T MFMAs to the exponentials: 855 -> 954 TF/s at 1 x 8192 with four chains).  Inline asm:
+    // fmaxf on MFMA results makes hipcc canonicalise its operands first (an extra v_max each).
+    float mx;
+    if constexpr (VAR & 16) {  // four fmaxf chains (hipcc's max3 + canonicalising moves)
+      float mq[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mq[j] = fmaxf(sacc[j >> 1][(j & 1) * 8], sacc[j >> 1][(j & 1) * 8 + 1]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 2; i < 8; ++i) mq[j] = fmaxf(mq[j], sacc[j >> 1][(j & 1) * 8 + i]);
+      mx = fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3]));
+    } else {
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int kt = j >> 2, i0 = (j & 3) * 4;
+        t[j] = vmax(vmax3(sacc[kt][i0], sacc[kt][i0 + 1], sacc[kt][i0 + 2]), sacc[kt][i0 + 3]);
+      }
+      mx = vmax3(vmax3(t[0], t[1], t[2]), vmax3(t[3], t[4], t[5]), vmax(t[6], t[7]));
     }
-    // first tile: m := its max; later: lazy rescale when the tile raises the max by more than 2^8.
-    // Both halves of a row see the same mx, hence the same decision.
-    const bool bump = first || mx > 8.f;
-    if (__ballot(bump)) {
-      const float d = bump ? mx : 0.f;  // how far m moves (relative)
-      if (!first) {
-        const float alpha = __builtin_amdgcn_exp2f(-d);
-        l *= alpha;
+    // the row's other half lives 32 lanes away: one permlane32 swap, not an LDS bpermute round trip
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    return vmax(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+  };
+  // move the reference by d (per row; both halves of a row hold the same d): rescale what is already
+  // accumulated at the old reference, shift this tile's scores.
+  auto move_ref = [&](float16_ (&sacc)[2], float d, bool rescale) {
+    if (rescale) {
+      const float alpha = __builtin_amdgcn_exp2f(-d);
+      if constexpr (MSUM) {
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
-        m += d;
+        for (int i = 0; i < 16; ++i) lsum[i] *= alpha;
       } else {
-        m = d;
+        l *= alpha;
       }
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[kt][i] -= d;
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
     }
+    m = rescale ? m + d : d;  // the first tile sets m (m starts at -inf)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[kt][i] -= d;
+    if constexpr (CBLK) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) negm[i] = -m;
+    }
+  };
+  auto expcvt = [&](const float16_ (&sacc)[2], bf16x8_t (&pf)[2][2]) {
+    // one add chain: split sums keep more exponentials live and spill at 4 waves per SIMD
     float ps = 0.f;
-    bf16x8_t pf[2][2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float p = __builtin_amdgcn_exp2f(sacc[kt][i]);
-        ps += p;
+        if constexpr (!MSUM) ps += p;
         pf[kt][i >> 3][i & 7] = static_cast<__bf16>(p);
       }
-    l += ps;
+    return ps;
+  };
+  auto overflow = [&](const bf16x8_t (&pf)[2][2]) {  // some p >= 2: the top exponent bit of a half
+    uint32_t x = 0;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const uint4 w = __builtin_bit_cast(uint4, pf[kt][s2]);
+        x |= w.x | w.y | w.z | w.w;
+      }
+    return (x & 0x40004000u) != 0u;
+  };
+
+  auto compute = [&](int buf, int k0) {
+    const char* kl = lds[buf];
+    const char* vl = lds[buf] + KBYTES;
+    const bool first = k0 == 0;
+    const bool diag = k0 + KT - 1 > wave_min_pos;  // tile crosses the diagonal (or the end) of some row
+    float16_ sacc[2];
+    bf16x8_t pf[2][2];
+    float ps;
+    qk(kl, sacc, first ? 0.f : -m);
+    if (diag) mask(sacc, k0);
+    if constexpr (ORCHK) {
+      if (first) {
+        move_ref(sacc, rowmax(sacc) + kBias, false);
+        ps = expcvt(sacc, pf);
+      } else {
+        ps = expcvt(sacc, pf);
+        if (__ballot(overflow(pf))) {  // a score passed its row's running max by 65: redo with a real max
+          asm volatile("" ::: "memory");  // re-read K from LDS: keeping the first pass's fragments live costs 32 registers
+          qk(kl, sacc, -m);
+          if (diag) mask(sacc, k0);
+          const float mx = rowmax(sacc);
+          move_ref(sacc, mx > 0.f ? mx + kBias : 0.f, true);
+          ps = expcvt(sacc, pf);
+        }
+      }
+    } else {
+      const float mx = rowmax(sacc);  // relative to m (absolute on the first tile)
+      // first tile: m := its max; later: lazy rescale when the tile raises the max by more than 2^8.
+      // Both halves of a row see the same mx, hence the same decision.
+      const bool bump = first || mx > 8.f;
+      if (__ballot(bump)) move_ref(sacc, bump ? mx : 0.f, !first);
+      ps = expcvt(sacc, pf);
+    }
+    if constexpr (MSUM) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) lsum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[kt][s2], lsum, 0, 0, 0);
+    } else {
+      l += ps;
+    }
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -564,7 +683,10 @@ paged_prefill_v3_kernel(
     __syncthreads();
   }
 
-  l += __shfl_xor(l, 32, 64);
+  if constexpr (MSUM)
+    l = lsum[0];  // ones^T . P^T summed both half-waves' keys already
+  else
+    l += __shfl_xor(l, 32, 64);
   if (!rvalid) return;
   const float inv = v_scale / l;
   bf16_t* op = out + (static_cast<size_t>(q0 + tok) * Hq + head) * D;
@@ -580,8 +702,46 @@ paged_prefill_v3_kernel(
     }
 }
 
+template <int D, int G, int EB, int VAR>
+static void pf3_launch(bf16_t* out, const bf16_t* q, const void* kv, long block_stride, const int* block_tables,
+                       int bt_stride, const int* qsl, const int* seq_lens, int num_seqs, int max_q_len, int Hkv,
+                       float sc, float vs, int q_stride, const int64_t* qpos, const float* cos_sin, hipStream_t s) {
+  constexpr int NT = pf3_threads(VAR), BQ = NT / 2 / G;
+  const dim3 grid((max_q_len + BQ - 1) / BQ, Hkv, num_seqs);
+  hipLaunchKernelGGL((paged_prefill_v3_kernel<D, G, EB, VAR>), grid, dim3(NT), 0, s, out, q, kv, block_stride,
+                     block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs, q_stride, qpos, cos_sin);
+}
+
+template <int D, int G>
+static void pf3_dispatch(int var, bool fp8, bf16_t* out, const bf16_t* q, const void* kv, long block_stride,
+                         const int* block_tables, int bt_stride, const int* qsl, const int* seq_lens, int num_seqs,
+                         int max_q_len, int Hkv, float sc, float vs, int q_stride, const int64_t* qpos,
+                         const float* cos_sin, hipStream_t s) {
+#define MXS_PF3_ARGS out, q, kv, block_stride, block_tables, bt_stride, qsl, seq_lens, num_seqs, max_q_len, Hkv, sc, vs, \
+                     q_stride, qpos, cos_sin, s
+  if (fp8) return pf3_launch<D, G, 1, kPf3DefaultVar>(MXS_PF3_ARGS);
+  if constexpr (G == 4) {  // the other variants: G = 4 only (A/B probes and tests)
+    switch (var) {
+      case 1: return pf3_launch<D, G, 2, 1>(MXS_PF3_ARGS);
+      case 2: return pf3_launch<D, G, 2, 2>(MXS_PF3_ARGS);
+      case 4: return pf3_launch<D, G, 2, 4>(MXS_PF3_ARGS);
+      case 6: return pf3_launch<D, G, 2, 6>(MXS_PF3_ARGS);
+      case 7: return pf3_launch<D, G, 2, 7>(MXS_PF3_ARGS);
+      case 8: return pf3_launch<D, G, 2, 8>(MXS_PF3_ARGS);
+      case 10: return pf3_launch<D, G, 2, 10>(MXS_PF3_ARGS);
+      case 12: return pf3_launch<D, G, 2, 12>(MXS_PF3_ARGS);
+      case 14: return pf3_launch<D, G, 2, 14>(MXS_PF3_ARGS);
+      case 16: return pf3_launch<D, G, 2, 16>(MXS_PF3_ARGS);
+      default: break;
+    }
+  }
+  pf3_launch<D, G, 2, kPf3DefaultVar>(MXS_PF3_ARGS);
+#undef MXS_PF3_ARGS
+}
+
 // q_stride: elements between consecutive q rows (Hq * D for a dense q; (Hq + 2 Hkv) * D when q is
 // read from the fused qkv output); cos_sin != nullptr applies RoPE at positions qpos (v3 only).
+// version 0x100 | VAR selects a v3 softmax variant explicitly (probes, tests).
 void launch_paged_prefill(bf16_t* out, const bf16_t* q, const void* kv_ptr, bool kv_fp8, long block_stride,
                           const int* block_tables, int bt_stride, const int* qsl, const int* seq_lens,
                           int num_seqs, int max_q_len, int Hq, int Hkv, int D, float scale, int version,
@@ -592,20 +752,14 @@ void launch_paged_prefill(bf16_t* out, const bf16_t* q, const void* kv_ptr, bool
   const bf16_t* kv = static_cast<const bf16_t*>(kv_ptr);
   if (q_stride <= 0) q_stride = Hq * D;
   if (version != 2 || kv_fp8 || cos_sin != nullptr || q_stride != Hq * D) {  // fp8 / fused q: the v3 path only
-    dim3 grid3((max_q_len + 256 / G - 1) / (256 / G), Hkv, num_seqs), blk3(512);
     const float sc = kv_fp8 ? scale * k_scale : scale, vs = kv_fp8 ? v_scale : 1.f;
-#define MXS_PF3(DD, GG)                                                                                    \
-    if (D == DD && G == GG) {                                                                              \
-      if (kv_fp8)                                                                                          \
-        hipLaunchKernelGGL((paged_prefill_v3_kernel<DD, GG, 1>), grid3, blk3, 0, s, out, q, kv_ptr,        \
-                           block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs, q_stride,    \
-                           qpos, cos_sin);                                                                 \
-      else                                                                                                 \
-        hipLaunchKernelGGL((paged_prefill_v3_kernel<DD, GG, 2>), grid3, blk3, 0, s, out, q, kv_ptr,        \
-                           block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs, q_stride,    \
-                           qpos, cos_sin);                                                                 \
-      MXS_CHECK_LAUNCH();                                                                                  \
-      return;                                                                                              \
+    const int var = version >= 0x100 ? (version & 0xff) : kPf3DefaultVar;
+#define MXS_PF3(DD, GG)                                                                                     \
+    if (D == DD && G == GG) {                                                                               \
+      pf3_dispatch<DD, GG>(var, kv_fp8, out, q, kv_ptr, block_stride, block_tables, bt_stride, qsl, seq_lens, \
+                           num_seqs, max_q_len, Hkv, sc, vs, q_stride, qpos, cos_sin, s);                   \
+      MXS_CHECK_LAUNCH();                                                                                   \
+      return;                                                                                               \
     }
     MXS_PF3(64, 1) MXS_PF3(64, 2) MXS_PF3(64, 4) MXS_PF3(64, 8)
     MXS_PF3(128, 1) MXS_PF3(128, 2) MXS_PF3(128, 4) MXS_PF3(128, 8)

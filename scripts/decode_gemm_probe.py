@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Every decode-GEMM kernel configuration vs hipBLASLt at the Llama-3.2-1B projection shapes, timed
-inside hipGraphs (20 calls per replay).  JSON lines: shape, M, config, microseconds, weight GB/s."""
+inside hipGraphs (20 calls per replay).  JSON lines: shape, M, config, microseconds, weight GB/s.
+  python scripts/decode_gemm_probe.py [M,M,...] [proj,proj,...]"""
 import json
 import os
 import sys
@@ -18,7 +19,10 @@ def main():
               "lm_head": (128256, 2048, 0)}
     Ms = [int(m) for m in (sys.argv[1].split(",") if len(sys.argv) > 1 else "256,192,128,64,16,1".split(","))]
     dg.TABLE.part = torch.empty(8 * 256 * 128256, dtype=torch.float32, device=dev)
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else list(shapes)
     for name, (N, K, epi) in shapes.items():
+        if name not in only:
+            continue
         w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
         for M in Ms:
             x = torch.randn(M, K, device=dev).to(torch.bfloat16)

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Paged prefill attention alone (csrc/kernels/attention_prefill.hip v3): causal, fresh sequences of
 `per` tokens each (the bench's 8192-token chunk = 2 x 4096), Llama-3.2-1B heads (32 q / 8 kv, D 64)
-and Llama-3-8B-like D 128; one JSON line per case with ms and TFLOP/s (causal half counted)."""
+and Llama-3-8B-like D 128; one JSON line per case with ms and TFLOP/s (causal half counted).
+PA_VARS=0,2,6 times the softmax variants of the v3 kernel (version 0x100 | VAR, G = 4 only) round-robin
+on the same inputs and reports each one's max |diff| against the first."""
 import json
 import math
 import os
@@ -26,20 +28,33 @@ def main():
         q = torch.randn(T, hq, D, dtype=torch.bfloat16, device=dev)
         qsl = torch.tensor([i * per for i in range(nseq + 1)], dtype=torch.int32, device=dev)
         sl = torch.full((nseq,), per, dtype=torch.int32, device=dev)
-        fn = lambda: ops.paged_attention_prefill(q, kv, bt, qsl, sl, D ** -0.5, per)  # noqa: E731
-        for _ in range(3):
-            fn()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(20):
-            fn()
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / 20
+        variants = [int(v) for v in os.environ.get("PA_VARS", "").split(",") if v != ""] or [None]
         flops = 4 * nseq * per * per / 2 * D * hq
-        print(json.dumps({"D": D, "hq": hq, "hkv": hkv, "seqs": nseq, "per_seq": per, "ms": round(ms, 4),
-                          "TFLOPs": round(flops / ms / 1e9, 1)}), flush=True)
+        ref_out, times = None, {v: [] for v in variants}
+        for rnd in range(3):
+            for v in variants:
+                ver = 0 if v is None else 0x100 | v
+                fn = lambda: ops.paged_attention_prefill(q, kv, bt, qsl, sl, D ** -0.5, per, version=ver)  # noqa: E731
+                for _ in range(3):
+                    out = fn()
+                if rnd == 0:
+                    if ref_out is None:
+                        ref_out = out.float()
+                    err = (out.float() - ref_out).abs().max().item()
+                    if err > 0.05 or not torch.isfinite(out).all():
+                        print(json.dumps({"D": D, "var": v, "error": "mismatch", "max_diff": err}), flush=True)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(20):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) / 20)
+        for v in variants:
+            ms = sorted(times[v])[1]
+            print(json.dumps({"D": D, "hq": hq, "hkv": hkv, "seqs": nseq, "per_seq": per, "var": v, "ms": round(ms, 4),
+                              "TFLOPs": round(flops / ms / 1e9, 1)}), flush=True)
 
 
 if __name__ == "__main__":

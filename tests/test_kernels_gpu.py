@@ -201,6 +201,49 @@ def test_prefill_softmax_rescale_spike(gpu, version):
     _close(out, exp, 0.03, 0.03, "prefill-spike")
 
 
+# v3 softmax variants (attention_prefill.hip VAR bits: 1 biased reference + overflow redo, 2 row sum
+# on the matrix pipe, 4 persistent -m accumulator block), launched as version 0x100 | VAR at G = 4
+@pytest.mark.parametrize("var", [0, 1, 2, 4, 6, 7, 8, 10, 12, 14])
+@pytest.mark.parametrize("D", [64, 128])
+def test_paged_prefill_softmax_variants(gpu, D, var):
+    G, hkv = 4, 2
+    specs = [(0, 77), (300, 45), (16, 1), (0, 130), (33, 200)]
+    seq_lens = [c + n for c, n in specs]
+    kv, bt = _paged_setup(seq_lens, hkv, D, device=gpu)
+    qsl = [0]
+    for _, n in specs:
+        qsl.append(qsl[-1] + n)
+    q = torch.randn(qsl[-1], hkv * G, D, device=gpu, dtype=torch.bfloat16)
+    qsl_t, sl = torch.tensor(qsl, dtype=torch.int32), torch.tensor(seq_lens, dtype=torch.int32)
+    out = ops.paged_attention_prefill(q, kv[:, 1], bt.to(gpu), qsl_t.to(gpu), sl.to(gpu), 1 / math.sqrt(D),
+                                      max(n for _, n in specs), version=0x100 | var)
+    exp = ref.paged_attention(q.cpu(), kv[:, 1].cpu(), bt, qsl_t, sl, 1 / math.sqrt(D))
+    _close(out, exp, 0.03, 0.03, f"prefill var {var}")
+
+
+@pytest.mark.parametrize("factor", [4, 12])
+@pytest.mark.parametrize("var", [0, 1, 7, 8, 14])
+def test_prefill_softmax_variant_spikes(gpu, var, factor):
+    """Late keys far above every earlier score of their rows: at factor 12 the score passes the running
+    max by ~140 (log2 units), past exp2's f32 range, so VAR & 1 must take its redo path; several rows
+    and both 32-key halves of a tile spike, one row twice (rule 26: the branch is data-dependent)."""
+    torch.manual_seed(0)  # the bf16 rounding of near-one-hot rows sits close to the tolerance on some draws
+    D, G, hkv = 64, 4, 1
+    lens = [256]
+    kv, bt = _paged_setup(lens, hkv, D, device=gpu)
+    q = torch.randn(256, G, D, device=gpu, dtype=torch.bfloat16)
+    for key, (tok, head) in ((200, (255, 0)), (130, (140, 2)), (161, (200, 1)), (230, (255, 0))):
+        nb_idx = int(bt[0, key // 16])
+        kv[nb_idx, 1, 0, 0, key % 16, :] = q[tok, head] * factor
+    qsl = torch.tensor([0, 256], dtype=torch.int32)
+    sl = torch.tensor(lens, dtype=torch.int32)
+    out = ops.paged_attention_prefill(q, kv[:, 1], bt.to(gpu), qsl.to(gpu), sl.to(gpu), 0.125, 256,
+                                      version=0x100 | var)
+    assert torch.isfinite(out).all()
+    exp = ref.paged_attention(q.cpu(), kv[:, 1].cpu(), bt, qsl, sl, 0.125)
+    _close(out, exp, 0.03, 0.03, f"prefill-spike var {var} x{factor}")
+
+
 # ---- fp8 (e4m3fn) KV cache: the cache bytes are shared by kernel and reference, so attention must
 # match the reference over the same dequantised values; the write path is checked byte-for-byte
 # against torch's e4m3fn rounding (off by one ulp allowed where f32 rounding of RoPE differs).
