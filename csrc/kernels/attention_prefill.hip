@@ -618,13 +618,12 @@ paged_prefill_v3_kernel(
     return (x & 0x40004000u) != 0u;
   };
 
-  auto compute = [&](int buf, int k0) {
+  // QK^T + softmax of one tile into P (bf16 fragments pf); pv(): O += V^T . P^T of that tile
+  auto softmax_phase = [&](int buf, int k0, bf16x8_t (&pf)[2][2]) {
     const char* kl = lds[buf];
-    const char* vl = lds[buf] + KBYTES;
     const bool first = k0 == 0;
     const bool diag = k0 + KT - 1 > wave_min_pos;  // tile crosses the diagonal (or the end) of some row
     float16_ sacc[2];
-    bf16x8_t pf[2][2];
     float ps;
     qk(kl, sacc, first ? 0.f : -m);
     if (diag) mask(sacc, k0);
@@ -659,6 +658,9 @@ paged_prefill_v3_kernel(
     } else {
       l += ps;
     }
+  };
+  auto pv = [&](int buf, const bf16x8_t (&pf)[2][2]) {
+    const char* vl = lds[buf] + KBYTES;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -671,16 +673,57 @@ paged_prefill_v3_kernel(
         }
   };
 
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int it = 0, k0 = 0; k0 < nkeys; ++it, k0 += KT) {
-    const int buf = it & 1;
-    const bool more = k0 + KT < nkeys;
-    if (more) gload(k0 + KT);           // in flight under this tile's MFMAs
-    if (k0 <= wave_max_pos) compute(buf, k0);  // waves whose rows all precede the tile skip it
-    if (more) sstore(buf ^ 1);
+  auto compute = [&](int buf, int k0) {
+    bf16x8_t pf[2][2];
+    softmax_phase(buf, k0, pf);
+    pv(buf, pf);
+  };
+
+  if constexpr (VAR & 32) {
+    // Ping-pong (VAR & 32): a tile is two phases, softmax (QK^T MFMAs, then a VALU-dense max / exp /
+    // convert) and PV (MFMAs only), one barrier each; waves 4-7 run one phase behind waves 0-3, so on
+    // every SIMD (waves w and w + 4) one wave's softmax VALU issues beside the other's PV MFMAs instead
+    // of all eight waves alternating MFMA and VALU in step.  Slot s: waves 0-3 run phase s, waves 4-7
+    // phase s - 1.  Tile t is loaded from L2 in slot 2t - 2 and written to LDS buffer t & 1 in slot
+    // 2t - 1: its previous occupant, tile t - 2, was last read by the late group's PV in slot 2t - 2,
+    // and the early group's QK^T of tile t starts in slot 2t.
+    const int ntile = (nkeys + KT - 1) / KT, grp = wid >> 2;
+    gload(0);
+    sstore(0);
+    if (ntile > 1) {
+      gload(KT);
+      sstore(1);
+    }
     __syncthreads();
+    bf16x8_t pf[2][2];
+    for (int sl = 0; sl <= 2 * ntile; ++sl) {
+      if (sl > 0) __syncthreads();
+      const int tl = sl / 2 + 1;  // even slot: load tile sl / 2 + 1; odd slot: store tile (sl + 1) / 2
+      if ((sl & 1) == 0 && sl >= 2 && tl < ntile) gload(tl * KT);
+      const int ph = sl - grp;
+      if (ph >= 0 && ph < 2 * ntile) {
+        const int i = ph >> 1, k0 = i * KT;
+        if (k0 <= wave_max_pos) {
+          if ((ph & 1) == 0)
+            softmax_phase(i & 1, k0, pf);
+          else
+            pv(i & 1, pf);
+        }
+      }
+      if ((sl & 1) == 1 && sl >= 3 && (sl + 1) / 2 < ntile) sstore(((sl + 1) / 2) & 1);
+    }
+  } else {
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    for (int it = 0, k0 = 0; k0 < nkeys; ++it, k0 += KT) {
+      const int buf = it & 1;
+      const bool more = k0 + KT < nkeys;
+      if (more) gload(k0 + KT);           // in flight under this tile's MFMAs
+      if (k0 <= wave_max_pos) compute(buf, k0);  // waves whose rows all precede the tile skip it
+      if (more) sstore(buf ^ 1);
+      __syncthreads();
+    }
   }
 
   if constexpr (MSUM)
@@ -732,6 +775,8 @@ static void pf3_dispatch(int var, bool fp8, bf16_t* out, const bf16_t* q, const 
       case 12: return pf3_launch<D, G, 2, 12>(MXS_PF3_ARGS);
       case 14: return pf3_launch<D, G, 2, 14>(MXS_PF3_ARGS);
       case 16: return pf3_launch<D, G, 2, 16>(MXS_PF3_ARGS);
+      case 32: return pf3_launch<D, G, 2, 32>(MXS_PF3_ARGS);
+      case 36: return pf3_launch<D, G, 2, 36>(MXS_PF3_ARGS);
       default: break;
     }
   }

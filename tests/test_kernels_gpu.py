@@ -203,7 +203,7 @@ def test_prefill_softmax_rescale_spike(gpu, version):
 
 # v3 softmax variants (attention_prefill.hip VAR bits: 1 biased reference + overflow redo, 2 row sum
 # on the matrix pipe, 4 persistent -m accumulator block), launched as version 0x100 | VAR at G = 4
-@pytest.mark.parametrize("var", [0, 1, 2, 4, 6, 7, 8, 10, 12, 14])
+@pytest.mark.parametrize("var", [0, 1, 2, 4, 6, 7, 8, 10, 12, 14, 16, 32, 36])
 @pytest.mark.parametrize("D", [64, 128])
 def test_paged_prefill_softmax_variants(gpu, D, var):
     G, hkv = 4, 2
@@ -222,7 +222,7 @@ def test_paged_prefill_softmax_variants(gpu, D, var):
 
 
 @pytest.mark.parametrize("factor", [4, 12])
-@pytest.mark.parametrize("var", [0, 1, 7, 8, 14])
+@pytest.mark.parametrize("var", [0, 1, 7, 8, 14, 32])
 def test_prefill_softmax_variant_spikes(gpu, var, factor):
     """Late keys far above every earlier score of their rows: at factor 12 the score passes the running
     max by ~140 (log2 units), past exp2's f32 range, so VAR & 1 must take its redo path; several rows
