@@ -64,11 +64,18 @@ __device__ __forceinline__ void ld8(const float* p, int v, float (&o)[8]) {
   o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
 }
 
-__device__ __forceinline__ float gumbel(uint32_t key, int v) {
+// Gumbel noise in base-2 units: argmax_v (z_v / T + G_v) with G = -ln(-ln u) is argmax_v of
+// (z_v / T + G_v) log2(e) = z_v log2(e) / T - log2(-log2 u) + const, so the scores are taken as
+// x * (log2(e) / T) + gumbel2(u) with two native v_log_f32 (log2) per logit instead of two
+// full-precision logf (u is in [2^-25, 1 - 2^-25]: both logarithms see normal inputs).  The final
+// Gumbel-max pass over a 128k-vocab row is the sampling kernel's dominant cost (79 us per 448-row
+// decode step with logf, profiles/r5/headline).
+__device__ __forceinline__ float gumbel2(uint32_t key, int v) {
   const uint32_t h = hash_u32(key ^ hash_u32(static_cast<uint32_t>(v) + 0x632BE5ABu));
   const float u = (static_cast<float>(h >> 8) + 0.5f) * (1.f / 16777216.f);
-  return -logf(-logf(u));
+  return -__builtin_amdgcn_logf(-__builtin_amdgcn_logf(u));
 }
+constexpr float kSLog2e = 1.4426950408889634f;
 
 template <typename T>
 __global__ void __launch_bounds__(1024) sample_kernel(int64_t* __restrict__ out, const T* __restrict__ logits,
@@ -142,6 +149,7 @@ __global__ void __launch_bounds__(1024) sample_kernel(int64_t* __restrict__ out,
   }
   const uint32_t key = hash_u32(static_cast<uint32_t>(static_cast<uint64_t>(seeds[row]) * 0x9E3779B1ull +
                                                       static_cast<uint64_t>(steps[row])));
+  const float invt2 = invt * kSLog2e;
   ArgMax a{-INFINITY, 0x7FFFFFFF};
   if (vec) {
     for (int v = 8 * threadIdx.x; v < V; v += 8 * blockDim.x) {
@@ -149,12 +157,12 @@ __global__ void __launch_bounds__(1024) sample_kernel(int64_t* __restrict__ out,
       ld8(z, v, x);
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (x[u] >= thr) a = better(a, ArgMax{x[u] * invt + gumbel(key, v + u), v + u});
+        if (x[u] >= thr) a = better(a, ArgMax{x[u] * invt2 + gumbel2(key, v + u), v + u});
     }
   } else {
     for (int v = threadIdx.x; v < V; v += blockDim.x) {
       const float zv = ld(z, v);
-      if (zv >= thr) a = better(a, ArgMax{zv * invt + gumbel(key, v), v});
+      if (zv >= thr) a = better(a, ArgMax{zv * invt2 + gumbel2(key, v), v});
     }
   }
   ArgMax r = block_argmax(a, sv, si);
@@ -262,13 +270,14 @@ __global__ void __launch_bounds__(1024) sample_reg_kernel(int64_t* __restrict__ 
   }
   const uint32_t key = hash_u32(static_cast<uint32_t>(static_cast<uint64_t>(seeds[row]) * 0x9E3779B1ull +
                                                       static_cast<uint64_t>(steps[row])));
+  const float invt2 = invt * kSLog2e;
   ArgMax a{-INFINITY, 0x7FFFFFFF};
 #pragma unroll
   for (int e = 0; e < NE; ++e) {
     const float x = val(e);
     const int v = idx(e);
-    if (v < V && x >= thr) a = better(a, ArgMax{x * invt + gumbel(key, v), v});
-    __builtin_amdgcn_sched_barrier(0);
+    if (v < V && x >= thr) a = better(a, ArgMax{x * invt2 + gumbel2(key, v), v});
+    if ((e & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // 4 independent hash/log chains in flight
   }
   ArgMax res = block_argmax(a, sv, si);
   if (tid == 0) out[row] = res.i;
