@@ -22,10 +22,12 @@ Phases (--mode auto: agg for N = 1, agg then disagg for N >= 2, both in the one 
           measured: a decode GPU is KV-bandwidth bound at 76.7 req/s, a prefill GPU computes 127.6
           req/s: 1P+1D at N = 2, 2P+2D at 4, 3P+5D at 8)
           and offers the node the rate that loads the tighter role to 85 %; when the split carries
-          the agg rate, the disagg phase runs at it (like-for-like).  Default rate 49 req/s per GPU:
-          sustained on one MI355X at 22.6k tok/s, TTFT p50 52 ms / ITL p90 21.2 ms with 6144-token
-          steps (profiles/r4/s2/bench_q49_kvrope.json; QPS 50 queues at every step budget from 3072
-          to 6144: TTFT p50 0.5-1.1 s, profiles/r4/s2/step_budget/).  The realised Poisson rate of the fixed-seed arrival stream over those windows
+          the agg rate, the disagg phase runs at it (like-for-like).  Default rate 47 req/s per GPU,
+          6 % below the measured saturation of one MI355X (50 req/s: the running set reaches the
+          448-sequence cap and TTFT p90 leaves the 100 ms range; 51 queues, TTFT p50 276 ms), so a
+          slower device of the pool still holds TTFT: QPS 45 / 47 / 48 / 49 / 50 / 51 give 21.6 / 22.1 /
+          22.3 / 22.8 / 23.2 / 23.5k tok/s at TTFT p50 30 / 34 / 41 / 49 / 64 / 277 ms
+          (profiles/r5/qps_sweep/).  The realised Poisson rate of the fixed-seed arrival stream over those windows
           is 97-98 % of nominal, which with the request tail bounds value at ~94 % of QPS x OSL.
           Requests arrive at the decode ranks (routed over them like the agg phase's when D >= 2);
           a decode rank reserves KV blocks and hands each
@@ -79,6 +81,15 @@ if _VERBOSE:  # stacks of every thread once a minute: where a stalled rank is wa
     faulthandler.dump_traceback_later(45, repeat=True)
 
 
+
+# One MI355X, this build, bench.py --steps 20 --warmup 5 --qps Q (profiles/r5/qps_sweep/): QPS ->
+# (tok/s, TTFT p50 ms, TTFT p90 ms).  Saturation: 50 req/s (the running set reaches the 448 cap, TTFT
+# p90 205 ms; 51 queues).  The default sits 6 % below it.
+SATURATION_QPS = 50.0
+SATURATION_SWEEP = {45: (21636, 30, 53), 47: (22116, 34, 60), 48: (22265, 41, 73), 49: (22815, 49, 82),
+                    50: (23189, 64, 205), 51: (23471, 277, 626)}
+DEFAULT_QPS = 47.0
+
 def vlog(msg: str) -> None:
     if _VERBOSE:
         print(f"[bench r{os.environ.get('RANK', '0')} {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr,
@@ -97,7 +108,7 @@ def parse(argv=None):
     ap.add_argument("--model", default="meta-llama/Llama-3.2-1B-Instruct")
     ap.add_argument("--isl", type=int, default=4000)
     ap.add_argument("--osl", type=int, default=500)
-    ap.add_argument("--qps", type=float, default=float(os.environ.get("MXS_BENCH_QPS", "49")),
+    ap.add_argument("--qps", type=float, default=float(os.environ.get("MXS_BENCH_QPS", str(DEFAULT_QPS))),
                     help="Poisson arrival rate per GPU (requests/s)")
     ap.add_argument("--arrivals", choices=["router", "local"], default=os.environ.get("MXS_BENCH_ARRIVALS", "router"),
                     help="N >= 2: router = one Poisson stream at the node's rate, each request routed to a rank "
@@ -1118,6 +1129,10 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
               "warmup_steps_executed", "warmup_s", "steady_state", "running_mean", "sla_isl4000_osl500"):
         line[k] = head[k]
     line["ttft_window"] = "steady state: post-warmup soak + timed steps"
+    if on_gpu:  # where the default rate sits (measured, one MI355X per rank; profiles/r5/qps_sweep/)
+        line["operating_point"] = {"qps_per_gpu": a.qps, "measured_saturation_qps_per_gpu": SATURATION_QPS,
+                                   "headroom": round(1.0 - a.qps / SATURATION_QPS, 3),
+                                   "sweep": SATURATION_SWEEP}
     if agg is not None and dis is not None:
         line["agg"] = {k: agg[k] for k in ("value", "ttft_p50_ms", "itl_p50_ms", "ms_per_step")}
         line["agg_vs_disagg"] = compare_modes(agg, dis, a.qps)

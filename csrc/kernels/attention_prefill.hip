@@ -321,8 +321,10 @@ __device__ __forceinline__ uint4 ld8_kv(const char* p) {
 // Bits 2 / 4 need more than the 128 registers of 4 waves per SIMD: with 512 threads they run 2 per SIMD.
 constexpr int kPf3DefaultVar = 0;
 constexpr int pf3_threads(int VAR) { return (VAR & 8) ? 256 : 512; }
+//  64  Q fragments re-read from LDS each tile (4 ds_read_b128) instead of held in 16 registers, so
+//      bit 2 fits the 128 registers of 4 waves per SIMD (VAR 66).
 constexpr int pf3_wpe(int D, int VAR) {
-  return (VAR & 8) ? (D == 64 ? 3 : 2) : (D == 64 ? ((VAR & 6) ? 2 : 4) : 0);
+  return (VAR & 8) ? (D == 64 ? 3 : 2) : (D == 64 ? (((VAR & 6) && !(VAR & 64)) ? 2 : 4) : 0);
 }
 
 template <int D, int G, int EB, int VAR>
@@ -352,6 +354,8 @@ paged_prefill_v3_kernel(
   auto kswz = [](int key) { return D == 64 ? ((key >> 1) & 7) : (key & 15); };
   auto vswz = [](int dim) { return (dim >> 1) & 7; };
   __shared__ __attribute__((aligned(16))) char lds[2][KBYTES + VBYTES];
+  constexpr bool QLDS = VAR & 64;
+  __shared__ __attribute__((aligned(16))) char qlds[QLDS ? (NT / 64) * KS * 1024 : 16];
 
   const int NTL = gridDim.x, total = NTL * gridDim.y * gridDim.z;
   const int lin = blockIdx.x + NTL * (blockIdx.y + gridDim.y * blockIdx.z);
@@ -414,6 +418,11 @@ paged_prefill_v3_kernel(
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int j = 0; j < 8; ++j) qf[ks][j] = static_cast<__bf16>(x[ks][j] * qs);
+  }
+  if constexpr (QLDS) {  // this wave's own slice: read back only by the wave itself
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      *reinterpret_cast<uint4*>(qlds + ((wid * KS + ks) * 64 + lane) * 16) = __builtin_bit_cast(uint4, qf[ks]);
   }
 
   const int* bt = block_tables + static_cast<size_t>(seq) * bt_stride;
@@ -513,6 +522,10 @@ paged_prefill_v3_kernel(
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[kt][i] = off;
     }
+    bf16x8_t qv[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      qv[ks] = QLDS ? as_bf16x8(*reinterpret_cast<const uint4*>(qlds + ((wid * KS + ks) * 64 + lane) * 16)) : qf[ks];
     uint4 ka[2 * KS];
 #pragma unroll
     for (int idx = 0; idx < 2 * KS; ++idx) {
@@ -521,9 +534,9 @@ paged_prefill_v3_kernel(
     }
 #pragma unroll
     for (int idx = 0; idx < 2 * KS; ++idx)
-      sacc[idx / KS] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ka[idx]), qf[idx % KS],
+      sacc[idx / KS] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ka[idx]), qv[idx % KS],
                                                                (CBLK && idx % KS == 0) ? negm : sacc[idx / KS], 0, 0, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, QLDS ? 2 + KS : 2, 0);
 #pragma unroll
     for (int idx = 0; idx < 2 * KS - 2; ++idx) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -777,6 +790,8 @@ static void pf3_dispatch(int var, bool fp8, bf16_t* out, const bf16_t* q, const 
       case 16: return pf3_launch<D, G, 2, 16>(MXS_PF3_ARGS);
       case 32: return pf3_launch<D, G, 2, 32>(MXS_PF3_ARGS);
       case 36: return pf3_launch<D, G, 2, 36>(MXS_PF3_ARGS);
+      case 64: return pf3_launch<D, G, 2, 64>(MXS_PF3_ARGS);
+      case 66: return pf3_launch<D, G, 2, 66>(MXS_PF3_ARGS);
       default: break;
     }
   }
