@@ -34,6 +34,7 @@ namespace mxs {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2_gv_t __attribute__((ext_vector_type(2)));
 
 constexpr int EPI_NONE = 0;
 constexpr int EPI_SILU = 1;
@@ -452,6 +453,146 @@ bool launch_skinny_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W
     MXS_CHECK_LAUNCH();
   }
   return true;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Row-stream form ("gv"): M <= 4 decode rows (small-batch decode of the TP shards, batch-1 decode of any
+// model) against a weight read exactly once.  The skinny form above reads 16 W rows x 64 B per load
+// instruction (16 partial lines per instruction) and goes through MFMA fragments sized for 16 tokens;
+// this one walks WHOLE rows: lane l of a wave holds the 16-byte chunks l, l + 64, ... of the wave's
+// k-range, so every load instruction is one contiguous 1 KiB of a row, the NR rows x CH chunks of a wave
+// are all issued before the first use (non-temporal), and the dot products are v_dot2_f32_bf16 against
+// x chunks the workgroup staged in LDS once.
+//   * a workgroup is 4 waves; KW of them split one row group's K (partial sums meet in LDS), so narrow
+//     shards (TP-8 qkv: 1280 rows x 8192) still put ~2.5 workgroups on every CU, and 4 / KW row groups
+//     of NR rows run side by side when K is short (o at TP 8: K = 1024);
+//   * EPI_SILU: a wave's NR rows are NR / 2 gate rows and the matching up rows (inter + n), so the
+//     workgroup writes SiLU(gate) * up directly -- no fp32 slabs, no reduce kernel;
+//   * the output is bf16 Y, or with `part` an fp32 [M][N] row-parallel partial (the TP all-reduce +
+//     RMSNorm epilogue reads it as a one-slab split-K result).
+template <int MR, int NR, int KW, int EPI>
+__global__ void __launch_bounds__(256) gemv_stream_kernel(bf16_t* __restrict__ Y, float* __restrict__ part,
+                                                          const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
+                                                          int M, int N, int K, int ldx, int ldy, int inter) {
+  extern __shared__ __attribute__((aligned(16))) char gv_smem[];
+  constexpr int RG = 4 / KW;                           // row groups per workgroup
+  constexpr int OUT = EPI == EPI_SILU ? NR / 2 : NR;  // output columns per row group
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int rg = wid / KW, kq = wid % KW;
+  const int ch = K / (512 * KW);  // 16-byte chunks per lane of this wave's k-range
+  const int kbase = kq * (K / KW);
+  // stage the M x rows into LDS: [MR][K] bf16, 16-byte chunks
+  const int nchunk = K / 8;
+  for (int i = tid; i < MR * nchunk; i += 256) {
+    const int m = i / nchunk, c = i % nchunk;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (m < M) v = *reinterpret_cast<const u32x4*>(X + static_cast<size_t>(m) * ldx + 8 * c);
+    *reinterpret_cast<u32x4*>(gv_smem + (static_cast<size_t>(m) * nchunk + c) * 16) = v;
+  }
+  __syncthreads();
+  const int col0 = (blockIdx.x * RG + rg) * OUT;  // first output column of this row group
+  const bf16_t* wrow[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int n = EPI == EPI_SILU ? (r < OUT ? col0 + r : inter + col0 + r - OUT) : col0 + r;
+    wrow[r] = W + static_cast<size_t>(n) * K + kbase + 8 * lane;
+  }
+  float acc[MR][NR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[m][r] = 0.f;
+  constexpr int JC = 16 / NR;  // chunks per row per batch: 16 loads (64 VGPRs) in flight per wave
+  for (int j0 = 0; j0 < ch; j0 += JC) {
+    u32x4 wv[NR][JC];
+#pragma unroll
+    for (int j = 0; j < JC; ++j)
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+        if (j0 + j < ch) wv[r][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow[r] + 512 * (j0 + j)));
+#pragma unroll
+    for (int j = 0; j < JC; ++j) {
+      if (j0 + j >= ch) break;
+      const int c = (kbase >> 3) + lane + 64 * (j0 + j);
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        const u32x4 xv = *reinterpret_cast<const u32x4*>(gv_smem + (static_cast<size_t>(m) * nchunk + c) * 16);
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            // copy the vector elements out first: hipcc (ROCm 7.2) bit-casts an ext_vector element
+            // subscript as element 0 whatever the index (every dot2 would read the chunk's first pair)
+            const uint32_t we = wv[r][j][e], xe = xv[e];
+            acc[m][r] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_gv_t, we),
+                                                        __builtin_bit_cast(bf16x2_gv_t, xe), acc[m][r], false);
+          }
+      }
+    }
+  }
+  // 64-lane sums, then the KW partial sums of a row group through LDS
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      float v = acc[m][r];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      acc[m][r] = v;
+    }
+  __syncthreads();  // the x tiles are no longer read: the LDS is reused for the partials
+  float* red = reinterpret_cast<float*>(gv_smem);  // [4 waves][MR][NR]
+  if (lane == 0) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) red[(wid * MR + m) * NR + r] = acc[m][r];
+  }
+  __syncthreads();
+  if (kq != 0 || lane >= MR * OUT) return;
+  const int m = lane / OUT, o = lane % OUT;
+  if (m >= M) return;
+  auto sum = [&](int r) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < KW; ++q) s += red[((rg * KW + q) * MR + m) * NR + r];
+    return s;
+  };
+  const float v = EPI == EPI_SILU ? silu(sum(o)) * sum(o + OUT) : sum(o);
+  if (part != nullptr)
+    part[static_cast<size_t>(m) * N + col0 + o] = v;
+  else
+    Y[static_cast<size_t>(m) * ldy + col0 + o] = f2bf(v);
+}
+
+bool launch_gemv_stream(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx,
+                        int ldy, int nr, int kw, int epi, hipStream_t s) {
+  if (M <= 0 || M > 4 || K % (512 * kw) != 0 || ldx % 8 != 0) return false;
+  if (!(nr == 2 || nr == 4) || !(kw == 1 || kw == 2 || kw == 4)) return false;
+  if (epi != EPI_NONE && (epi != EPI_SILU || part != nullptr || N % 2 != 0)) return false;
+  const int out_cols = epi == EPI_SILU ? N / 2 : N;
+  const int per_wg = (4 / kw) * (epi == EPI_SILU ? nr / 2 : nr);
+  if (out_cols % per_wg != 0) return false;
+  const int mr = M <= 1 ? 1 : (M <= 2 ? 2 : 4);
+  const size_t lds = std::max<size_t>(static_cast<size_t>(mr) * K * 2, 4 * 4 * 4 * sizeof(float));
+  if (lds > 64 * 1024) return false;
+  const dim3 grid(out_cols / per_wg), blk(256);
+  const int inter = epi == EPI_SILU ? N / 2 : 0;
+#define MXS_GV(MRR, NRR, KWW, EE)                                                                           \
+  if (mr == MRR && nr == NRR && kw == KWW && epi == EE) {                                                   \
+    hipLaunchKernelGGL((gemv_stream_kernel<MRR, NRR, KWW, EE>), grid, blk, lds, s, Y, part, X, W, M, N, K, ldx, \
+                       ldy, inter);                                                                         \
+    MXS_CHECK_LAUNCH();                                                                                     \
+    return true;                                                                                            \
+  }
+#define MXS_GV_K(MRR, NRR, EE) MXS_GV(MRR, NRR, 1, EE) MXS_GV(MRR, NRR, 2, EE) MXS_GV(MRR, NRR, 4, EE)
+  MXS_GV_K(1, 2, EPI_NONE) MXS_GV_K(1, 4, EPI_NONE) MXS_GV_K(2, 2, EPI_NONE) MXS_GV_K(2, 4, EPI_NONE)
+  MXS_GV_K(4, 2, EPI_NONE) MXS_GV_K(4, 4, EPI_NONE)
+  MXS_GV_K(1, 2, EPI_SILU) MXS_GV_K(1, 4, EPI_SILU) MXS_GV_K(2, 2, EPI_SILU) MXS_GV_K(2, 4, EPI_SILU)
+  MXS_GV_K(4, 2, EPI_SILU) MXS_GV_K(4, 4, EPI_SILU)
+#undef MXS_GV_K
+#undef MXS_GV
+  return false;
 }
 
 // ---------------------------------------------------------------------------------------------------

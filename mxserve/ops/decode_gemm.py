@@ -68,6 +68,10 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
         return out
     if M >= PF_MIN_M and N % 256 == 0 and K % 64 == 0 and N >= PF_MIN_N:
         out.append(("pf", 0))
+    # M <= 4: whole weight rows streamed once, 1 KiB per load instruction (gemv_stream_kernel; SwiGLU
+    # in the epilogue): ("gv", rows per wave, waves splitting K)
+    if M <= GV_MAX_M:
+        out += gv_candidates(M, N, K, epi)
     # small batches: 16-column weight slices streamed with every load in flight (skinny_gemm_kernel;
     # SwiGLU: slabs + the SiLU*mul reduce)
     if M <= 64 and N % (32 if epi else 16) == 0:
@@ -78,6 +82,21 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
 
 PF_MIN_M = 128
 PF_MIN_N = 32768
+GV_MAX_M = 4
+
+
+def gv_candidates(M: int, N: int, K: int, epi: int) -> list[tuple]:
+    """Row-stream GEMV configurations (gemm_decode.hip launch_gemv_stream) that tile the shape."""
+    mr = 1 if M <= 1 else (2 if M <= 2 else 4)
+    if mr * K * 2 > 64 * 1024:
+        return []
+    out = []
+    for nr in (2, 4):
+        for kw in (1, 2, 4):
+            per_wg = (4 // kw) * (nr // 2 if epi else nr)
+            if K % (512 * kw) == 0 and (N // 2 if epi else N) % per_wg == 0:
+                out.append(("gv", nr, kw))
+    return out
 
 
 MT_MIN_M = 64
@@ -164,7 +183,7 @@ class DecodeGemmTable:
         if MODE == "off" or M > MAX_M:
             return None
         if MODE == "force":
-            c = [x for x in candidates(M, N, K, epi) if x[0] not in ("mt", "pf", "sk")]
+            c = [x for x in candidates(M, N, K, epi) if x[0] not in ("mt", "pf", "sk", "gv")]
             return next((x for x in c if x[3] == 1), c[0] if c else None)
         ent = self.entries.get((N, K, epi))
         if not ent:
@@ -176,7 +195,7 @@ class DecodeGemmTable:
 
     @staticmethod
     def splitk(cfg: tuple) -> int:
-        if cfg[0] == "pf":
+        if cfg[0] in ("pf", "gv"):
             return 1
         if cfg[0] == "sk":  # ("sk", kr, k-groups of 4 x kr)
             return cfg[2]
@@ -190,6 +209,8 @@ class DecodeGemmTable:
         if cfg[0] == "pf":
             from . import gemm_pf
             return gemm_pf(x, w, epi, out, int(cfg[1])) is not None
+        if cfg[0] == "gv":
+            return bool(ext().gemv_stream(out, x, w, None, int(cfg[1]), int(cfg[2]), int(epi)))
         if cfg[0] == "sk":
             groups = w.shape[1] // (4 * int(cfg[1]))
             if groups != cfg[2] or (epi and not reduce):
@@ -376,7 +397,7 @@ def tune(shapes: dict, buckets: list, device, dtype=torch.bfloat16) -> list:
                     lib_fn = lambda i: torch.nn.functional.linear(x, ws[i % len(ws)])  # noqa: E731
                 fns = {}
                 for cfg in candidates(M, N, K, epi):
-                    if cfg[0] not in ("mt", "pf", "sk") and M > OLD_FORMS_MAX_M:
+                    if cfg[0] not in ("mt", "pf", "sk", "gv") and M > OLD_FORMS_MAX_M:
                         continue
                     if not TABLE.run(out, x, w, cfg, epi):
                         continue

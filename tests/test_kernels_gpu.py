@@ -573,7 +573,7 @@ def test_decode_gemm_all_configs(gpu, M, N, K, epi):
         out = torch.full((M, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
         if c[0] == "mt":
             assert ops.ext().mt_gemm(out, x, w, part, *c[1:6], epi, None, c[6] if len(c) > 6 else 0)
-        elif c[0] in ("sk", "pf"):
+        elif c[0] in ("sk", "pf", "gv"):
             assert decode_gemm.TABLE.run(out, x, w, c, epi)
         else:
             assert ops.ext().decode_gemm(out, x, w, part, *c[:4], epi, c[4])
@@ -1169,6 +1169,34 @@ def test_skinny_gemm(gpu, M, N, K):
             slabs = part.view(groups, M, N).sum(0)
             _close(slabs, want, atol=2e-2, rtol=2e-2, name=f"skinny slabs {M}x{N}x{K} kr{kr}")
             assert torch.isnan(out2.float()).all(), "reduce=False must leave the output untouched"
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,K,epi", [(1280, 8192, 0), (8192, 1024, 0), (8192, 3584, 0), (7168, 8192, 1),
+                                     (3072, 2048, 0), (16384, 2048, 1), (2048, 8192, 0)])
+def test_gemv_stream(gpu, M, N, K, epi):
+    """gemv_stream_kernel (M <= 4, whole W rows streamed, kw waves splitting K, SwiGLU in the epilogue)
+    at every configuration the decode tuner would try, vs an fp32 reference: Llama-3-70B TP-8 shard
+    shapes and the 1B projections; plus the fp32 result form (epi 0) the fused epilogues read."""
+    from mxserve.ops import decode_gemm
+    g = torch.Generator(device="cuda").manual_seed(M * 17 + N + K + epi)
+    x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16, generator=g)
+    w = (torch.randn(N, K, device=gpu, generator=g) * K ** -0.5).to(torch.bfloat16)
+    w[N // 2:] *= 1.5  # halves differ: a swapped gate / up pair or a transposed store shows
+    y = x.float() @ w.float().t()
+    want = torch.nn.functional.silu(y[:, :N // 2]) * y[:, N // 2:] if epi else y
+    cfgs = decode_gemm.gv_candidates(M, N, K, epi)
+    assert cfgs, "every shape here has a row-stream configuration"
+    for cfg in cfgs:
+        out = torch.full(want.shape, float("nan"), device=gpu, dtype=torch.bfloat16)
+        assert decode_gemm.TABLE.run(out, x, w, cfg, epi), cfg
+        _close(out, want, atol=2e-2, rtol=2e-2, name=f"gemv {M}x{N}x{K} epi {epi} {cfg}")
+        if not epi:
+            part = torch.full((M * N,), float("nan"), dtype=torch.float32, device=gpu)
+            assert ops.ext().gemv_stream(out, x, w, part, cfg[1], cfg[2], 0)
+            _close(part.view(M, N), want, atol=2e-3, rtol=2e-3, name=f"gemv fp32 {M}x{N}x{K} {cfg}")
+    assert not ops.ext().gemv_stream(torch.empty(5, want.shape[1], device=gpu, dtype=torch.bfloat16),
+                                     torch.zeros(5, K, device=gpu, dtype=torch.bfloat16), w, None, 2, 1, epi), "M <= 4"
 
 
 @pytest.mark.parametrize("M", [1, 8, 16, 32, 64])
