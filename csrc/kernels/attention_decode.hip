@@ -22,6 +22,8 @@
 //   * EB = 1: fp8 (e4m3fn) cache.  Same lane -> (token, dims) map with 8-byte loads (still whole
 //     512-byte wave-instructions), converted to bf16 words in registers right before the math, so
 //     the step reads half the bytes; k_scale folds into q, v_scale into the output.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace mxs {
@@ -647,7 +649,11 @@ __global__ void __launch_bounds__(D) paged_decode_reduce_kernel(bf16_t* __restri
 // Partition plan: enough workgroups to fill 256 CUs ~8 deep, partitions as long as possible, a
 // multiple of one full wave sweep (kWaves * kBPI blocks <= 8 blocks = 128 tokens).
 void decode_plan(int B, int Hkv, int max_seq_len, int* P, int* part_len) {
-  const int target = 2048;
+  static const int target = [] {  // MXS_DECODE_TARGET_WGS: the workgroup floor (A/B probes)
+    const char* e = std::getenv("MXS_DECODE_TARGET_WGS");
+    const int v = e != nullptr ? std::atoi(e) : 0;
+    return v > 0 ? v : 2048;
+  }();
   const int sweep = kSweepBlocks * kBS;
   int p = (target + B * Hkv - 1) / (B * Hkv);
   const int max_p = (max_seq_len + 255) / 256;  // never below 256 tokens per partition
