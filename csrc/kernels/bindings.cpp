@@ -32,8 +32,8 @@ void launch_penalties(void*, bool, int, int, long, const int*, long, const int64
 void launch_moe_topk_softmax(float*, int*, const bf16_t*, int, int, int, hipStream_t);
 void launch_moe_align(int*, int*, const int*, int, int, int, int*, hipStream_t);
 void launch_moe_combine(bf16_t*, const bf16_t*, const float*, const int*, int, int, int, hipStream_t);
-bool launch_gemv_stream(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int,
-                        hipStream_t);
+bool launch_gemv_stream(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int,
+                        bool, hipStream_t);
 bool launch_skinny_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, bool, int,
                         hipStream_t);
 bool launch_decode_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, int, int,
@@ -321,25 +321,27 @@ bool decode_gemm(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::T
                                  epi, stream(), nullptr, 0, 0, lu, reduce ? 1 : 0);
 }
 
-// Row-stream form (gemm_decode.hip gemv_stream_kernel): M <= 4 rows, whole W rows streamed once; nr rows
-// per wave, kw waves splitting K.  epi 1: w = [gate; up], out [M, N / 2] = SiLU(gate) * up.  With part
-// (epi 0): an fp32 [M][N] result instead of bf16 out (a one-slab split-K partial for the fused epilogues).
+// Row-stream form (gemm_decode.hip gemv_stream_kernel): M <= 16 rows, whole W rows streamed once; nr rows
+// per wave, kw waves splitting a workgroup's K, kg workgroups splitting K over the grid.  epi 1:
+// w = [gate; up], out [M, N / 2] = SiLU(gate) * up.  kg = 1 with part (epi 0): an fp32 [M][N] result
+// instead of bf16 out.  kg > 1: fp32 slabs [kg][M][N] in part, summed (with SiLU*mul for epi 1) into out
+// when reduce, else left for the caller's fused epilogue.
 bool gemv_stream(at::Tensor out, at::Tensor x, at::Tensor w, c10::optional<at::Tensor> part, int64_t nr, int64_t kw,
-                 int64_t epi) {
+                 int64_t epi, int64_t kg, bool reduce) {
   CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
   TORCH_CHECK(epi == 0 || epi == 1, "epi 0 (none) or 1 (SiLU*mul)");
   const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
   TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == (epi ? N / 2 : N), "shape mismatch");
-  if (x.stride(1) != 1 || out.stride(1) != 1) return false;
+  if (x.stride(1) != 1 || out.stride(1) != 1 || kg < 1) return false;
   float* p = nullptr;
   if (part.has_value()) {
-    TORCH_CHECK(epi == 0 && part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
-                    part->numel() >= M * N, "the fp32 result needs an M * N workspace (epi 0)");
+    TORCH_CHECK(part->is_cuda() && part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->numel() >= kg * M * N, "the fp32 result / slabs need a kg * M * N workspace");
     p = part->data_ptr<float>();
   }
   return mxs::launch_gemv_stream(bf(out), p, bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), nr, kw,
-                                 static_cast<int>(epi), stream());
+                                 static_cast<int>(epi), static_cast<int>(kg), reduce, stream());
 }
 
 // Skinny form (gemm_decode.hip skinny_gemm_kernel): M <= 16 rows, 16-column W slices x 4 k-ranges of
@@ -558,7 +560,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("e_lo"), pybind11::arg("e_local"), pybind11::arg("inv") = pybind11::none());
   m.def("moe_combine", &moe_combine);
   m.def("gemv_stream", &gemv_stream, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
-        pybind11::arg("part") = c10::nullopt, pybind11::arg("nr") = 2, pybind11::arg("kw") = 1, pybind11::arg("epi") = 0);
+        pybind11::arg("part") = c10::nullopt, pybind11::arg("nr") = 2, pybind11::arg("kw") = 1, pybind11::arg("epi") = 0,
+        pybind11::arg("kg") = 1, pybind11::arg("reduce") = true);
   m.def("skinny_gemm", &skinny_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("part") = pybind11::none(), pybind11::arg("kr") = 256, pybind11::arg("reduce") = true,
         pybind11::arg("epi") = 0);

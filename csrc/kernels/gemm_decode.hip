@@ -473,20 +473,23 @@ bool launch_skinny_gemm(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W
 template <int MR, int NR, int KW, int EPI>
 __global__ void __launch_bounds__(256) gemv_stream_kernel(bf16_t* __restrict__ Y, float* __restrict__ part,
                                                           const bf16_t* __restrict__ X, const bf16_t* __restrict__ W,
-                                                          int M, int N, int K, int ldx, int ldy, int inter) {
+                                                          int M, int N, int K, int ldx, int ldy, int inter,
+                                                          int kslice) {
   extern __shared__ __attribute__((aligned(16))) char gv_smem[];
   constexpr int RG = 4 / KW;                           // row groups per workgroup
   constexpr int OUT = EPI == EPI_SILU ? NR / 2 : NR;  // output columns per row group
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int rg = wid / KW, kq = wid % KW;
-  const int ch = K / (512 * KW);  // 16-byte chunks per lane of this wave's k-range
-  const int kbase = kq * (K / KW);
-  // stage the M x rows into LDS: [MR][K] bf16, 16-byte chunks
-  const int nchunk = K / 8;
+  const int z = blockIdx.y, kg = gridDim.y;       // k-group of this workgroup (split-K over the grid)
+  const int ch = kslice / (512 * KW);             // 16-byte chunks per lane of this wave's k-range
+  const int kw0 = kq * (kslice / KW);             // the wave's k-range, relative to the workgroup's slice
+  const int kbase = z * kslice + kw0;
+  // stage the workgroup's k-slice of the M x rows into LDS: [MR][kslice] bf16, 16-byte chunks
+  const int nchunk = kslice / 8;
   for (int i = tid; i < MR * nchunk; i += 256) {
     const int m = i / nchunk, c = i % nchunk;
     u32x4 v = {0u, 0u, 0u, 0u};
-    if (m < M) v = *reinterpret_cast<const u32x4*>(X + static_cast<size_t>(m) * ldx + 8 * c);
+    if (m < M) v = *reinterpret_cast<const u32x4*>(X + static_cast<size_t>(m) * ldx + z * kslice + 8 * c);
     *reinterpret_cast<u32x4*>(gv_smem + (static_cast<size_t>(m) * nchunk + c) * 16) = v;
   }
   __syncthreads();
@@ -513,7 +516,7 @@ __global__ void __launch_bounds__(256) gemv_stream_kernel(bf16_t* __restrict__ Y
 #pragma unroll
     for (int j = 0; j < JC; ++j) {
       if (j0 + j >= ch) break;
-      const int c = (kbase >> 3) + lane + 64 * (j0 + j);
+      const int c = (kw0 >> 3) + lane + 64 * (j0 + j);
 #pragma unroll
       for (int m = 0; m < MR; ++m) {
         const u32x4 xv = *reinterpret_cast<const u32x4*>(gv_smem + (static_cast<size_t>(m) * nchunk + c) * 16);
@@ -549,50 +552,75 @@ __global__ void __launch_bounds__(256) gemv_stream_kernel(bf16_t* __restrict__ Y
       for (int r = 0; r < NR; ++r) red[(wid * MR + m) * NR + r] = acc[m][r];
   }
   __syncthreads();
-  if (kq != 0 || lane >= MR * OUT) return;
-  const int m = lane / OUT, o = lane % OUT;
-  if (m >= M) return;
-  auto sum = [&](int r) {
-    float s = 0.f;
+  if (kq != 0) return;
+  for (int idx = lane; idx < MR * OUT; idx += 64) {
+    const int m = idx / OUT, o = idx % OUT;
+    if (m >= M) break;
+    auto sum = [&](int r) {
+      float s = 0.f;
 #pragma unroll
-    for (int q = 0; q < KW; ++q) s += red[((rg * KW + q) * MR + m) * NR + r];
-    return s;
-  };
-  const float v = EPI == EPI_SILU ? silu(sum(o)) * sum(o + OUT) : sum(o);
-  if (part != nullptr)
-    part[static_cast<size_t>(m) * N + col0 + o] = v;
-  else
-    Y[static_cast<size_t>(m) * ldy + col0 + o] = f2bf(v);
+      for (int q = 0; q < KW; ++q) s += red[((rg * KW + q) * MR + m) * NR + r];
+      return s;
+    };
+    if (kg > 1) {  // split-K slab [z][M][N] of raw sums (SwiGLU: gate and up columns; the reduce applies it)
+      float* pr = part + (static_cast<size_t>(z) * M + m) * N;
+      pr[col0 + o] = sum(o);
+      if constexpr (EPI == EPI_SILU) pr[inter + col0 + o] = sum(o + OUT);
+      continue;
+    }
+    const float v = EPI == EPI_SILU ? silu(sum(o)) * sum(o + OUT) : sum(o);
+    if (part != nullptr)
+      part[static_cast<size_t>(m) * N + col0 + o] = v;
+    else
+      Y[static_cast<size_t>(m) * ldy + col0 + o] = f2bf(v);
+  }
 }
 
+// kg > 1: split-K over gridDim.y, fp32 slabs [kg][M][N] in `part` (summed with the epilogue by
+// splitk_reduce_kernel when reduce, else left for the caller's fused epilogue).
 bool launch_gemv_stream(bf16_t* Y, float* part, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx,
-                        int ldy, int nr, int kw, int epi, hipStream_t s) {
-  if (M <= 0 || M > 4 || K % (512 * kw) != 0 || ldx % 8 != 0) return false;
+                        int ldy, int nr, int kw, int epi, int kg, bool reduce, hipStream_t s) {
+  if (M <= 0 || M > 16 || kg < 1 || K % (512 * kw * kg) != 0 || ldx % 8 != 0) return false;
   if (!(nr == 2 || nr == 4) || !(kw == 1 || kw == 2 || kw == 4)) return false;
-  if (epi != EPI_NONE && (epi != EPI_SILU || part != nullptr || N % 2 != 0)) return false;
+  if (epi != EPI_NONE && (epi != EPI_SILU || N % 2 != 0)) return false;
+  if (kg == 1 && epi == EPI_SILU && part != nullptr) return false;  // the fp32 result form is epi 0 only
+  if (kg > 1 && part == nullptr) return false;
   const int out_cols = epi == EPI_SILU ? N / 2 : N;
+  if (kg > 1 && (out_cols % 4 != 0 || ldy % 4 != 0)) return false;  // the reduce writes 4 columns at a time
   const int per_wg = (4 / kw) * (epi == EPI_SILU ? nr / 2 : nr);
   if (out_cols % per_wg != 0) return false;
-  const int mr = M <= 1 ? 1 : (M <= 2 ? 2 : 4);
-  const size_t lds = std::max<size_t>(static_cast<size_t>(mr) * K * 2, 4 * 4 * 4 * sizeof(float));
+  const int mr = M <= 1 ? 1 : (M <= 2 ? 2 : (M <= 4 ? 4 : (M <= 8 ? 8 : 16)));
+  const int kslice = K / kg;
+  const size_t lds = std::max<size_t>(static_cast<size_t>(mr) * kslice * 2, 4 * 16 * 4 * sizeof(float));
   if (lds > 64 * 1024) return false;
-  const dim3 grid(out_cols / per_wg), blk(256);
+  const dim3 grid(out_cols / per_wg, kg), blk(256);
   const int inter = epi == EPI_SILU ? N / 2 : 0;
+  bool launched = false;
 #define MXS_GV(MRR, NRR, KWW, EE)                                                                           \
-  if (mr == MRR && nr == NRR && kw == KWW && epi == EE) {                                                   \
+  if (!launched && mr == MRR && nr == NRR && kw == KWW && epi == EE) {                                      \
     hipLaunchKernelGGL((gemv_stream_kernel<MRR, NRR, KWW, EE>), grid, blk, lds, s, Y, part, X, W, M, N, K, ldx, \
-                       ldy, inter);                                                                         \
+                       ldy, inter, kslice);                                                                 \
     MXS_CHECK_LAUNCH();                                                                                     \
-    return true;                                                                                            \
+    launched = true;                                                                                        \
   }
 #define MXS_GV_K(MRR, NRR, EE) MXS_GV(MRR, NRR, 1, EE) MXS_GV(MRR, NRR, 2, EE) MXS_GV(MRR, NRR, 4, EE)
-  MXS_GV_K(1, 2, EPI_NONE) MXS_GV_K(1, 4, EPI_NONE) MXS_GV_K(2, 2, EPI_NONE) MXS_GV_K(2, 4, EPI_NONE)
-  MXS_GV_K(4, 2, EPI_NONE) MXS_GV_K(4, 4, EPI_NONE)
-  MXS_GV_K(1, 2, EPI_SILU) MXS_GV_K(1, 4, EPI_SILU) MXS_GV_K(2, 2, EPI_SILU) MXS_GV_K(2, 4, EPI_SILU)
-  MXS_GV_K(4, 2, EPI_SILU) MXS_GV_K(4, 4, EPI_SILU)
+#define MXS_GV_M(MRR, EE) MXS_GV_K(MRR, 2, EE) MXS_GV_K(MRR, 4, EE)
+  MXS_GV_M(1, EPI_NONE) MXS_GV_M(2, EPI_NONE) MXS_GV_M(4, EPI_NONE) MXS_GV_M(8, EPI_NONE) MXS_GV_M(16, EPI_NONE)
+  MXS_GV_M(1, EPI_SILU) MXS_GV_M(2, EPI_SILU) MXS_GV_M(4, EPI_SILU) MXS_GV_M(8, EPI_SILU) MXS_GV_M(16, EPI_SILU)
+#undef MXS_GV_M
 #undef MXS_GV_K
 #undef MXS_GV
-  return false;
+  if (!launched) return false;
+  if (kg > 1 && reduce) {
+    const long total4 = static_cast<long>(M) * out_cols / 4;
+    const int blocks = static_cast<int>(std::min<long>((total4 + 255) / 256, 1024));
+    if (epi == EPI_SILU)
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_SILU>, dim3(blocks), dim3(256), 0, s, Y, part, M, N, kg, ldy, N / 2);
+    else
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_NONE>, dim3(blocks), dim3(256), 0, s, Y, part, M, N, kg, ldy, 0);
+    MXS_CHECK_LAUNCH();
+  }
+  return true;
 }
 
 // ---------------------------------------------------------------------------------------------------

@@ -69,7 +69,7 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
     if M >= PF_MIN_M and N % 256 == 0 and K % 64 == 0 and N >= PF_MIN_N:
         out.append(("pf", 0))
     # M <= 4: whole weight rows streamed once, 1 KiB per load instruction (gemv_stream_kernel; SwiGLU
-    # in the epilogue): ("gv", rows per wave, waves splitting K)
+    # in the epilogue or the split-K reduce): ("gv", rows per wave, waves splitting K[, k-groups])
     if M <= GV_MAX_M:
         out += gv_candidates(M, N, K, epi)
     # small batches: 16-column weight slices streamed with every load in flight (skinny_gemm_kernel;
@@ -82,20 +82,25 @@ def candidates(M: int, N: int, K: int, epi: int, all_mf: bool = False, lds: bool
 
 PF_MIN_M = 128
 PF_MIN_N = 32768
+# the kernel takes M <= 16, but from 8 rows on its dot2 VALU work outgrows the weight stream: at M = 8 /
+# 16 the skinny form and hipBLASLt win every shape measured (profiles/r5/gemv/gv_probe_8_16.jsonl)
 GV_MAX_M = 4
 
 
 def gv_candidates(M: int, N: int, K: int, epi: int) -> list[tuple]:
-    """Row-stream GEMV configurations (gemm_decode.hip launch_gemv_stream) that tile the shape."""
-    mr = 1 if M <= 1 else (2 if M <= 2 else 4)
-    if mr * K * 2 > 64 * 1024:
-        return []
+    """Row-stream GEMV configurations (gemm_decode.hip launch_gemv_stream) that tile the shape:
+    ("gv", rows per wave, waves splitting a workgroup's K, workgroups splitting K over the grid)."""
+    mr = 1 if M <= 1 else (2 if M <= 2 else (4 if M <= 4 else (8 if M <= 8 else 16)))
+    ocols = N // 2 if epi else N
     out = []
-    for nr in (2, 4):
-        for kw in (1, 2, 4):
-            per_wg = (4 // kw) * (nr // 2 if epi else nr)
-            if K % (512 * kw) == 0 and (N // 2 if epi else N) % per_wg == 0:
-                out.append(("gv", nr, kw))
+    for kg in ((1, 2) if M <= 4 else (1, 2, 4, 8)):
+        if mr * (K // kg) * 2 > 64 * 1024 or (kg > 1 and ocols % 4):
+            continue
+        for nr in (2, 4):
+            for kw in (1, 2, 4):
+                per_wg = (4 // kw) * (nr // 2 if epi else nr)
+                if K % (512 * kw * kg) == 0 and ocols % per_wg == 0:
+                    out.append(("gv", nr, kw) if kg == 1 else ("gv", nr, kw, kg))
     return out
 
 
@@ -195,8 +200,10 @@ class DecodeGemmTable:
 
     @staticmethod
     def splitk(cfg: tuple) -> int:
-        if cfg[0] in ("pf", "gv"):
+        if cfg[0] == "pf":
             return 1
+        if cfg[0] == "gv":  # ("gv", nr, kw[, kg])
+            return int(cfg[3]) if len(cfg) > 3 else 1
         if cfg[0] == "sk":  # ("sk", kr, k-groups of 4 x kr)
             return cfg[2]
         return cfg[5] if cfg[0] == "mt" else cfg[3]
@@ -210,7 +217,18 @@ class DecodeGemmTable:
             from . import gemm_pf
             return gemm_pf(x, w, epi, out, int(cfg[1])) is not None
         if cfg[0] == "gv":
-            return bool(ext().gemv_stream(out, x, w, None, int(cfg[1]), int(cfg[2]), int(epi)))
+            kg = int(cfg[3]) if len(cfg) > 3 else 1
+            if epi and kg > 1 and not reduce:
+                return False  # SwiGLU applies in the reduce
+            part = None
+            if kg > 1:
+                need = kg * x.shape[0] * w.shape[0]
+                if self.part is None or self.part.numel() < need:
+                    if torch.cuda.is_current_stream_capturing():
+                        return False
+                    self.part = torch.empty(need, dtype=torch.float32, device=x.device)
+                part = self.part
+            return bool(ext().gemv_stream(out, x, w, part, int(cfg[1]), int(cfg[2]), int(epi), kg, reduce))
         if cfg[0] == "sk":
             groups = w.shape[1] // (4 * int(cfg[1]))
             if groups != cfg[2] or (epi and not reduce):

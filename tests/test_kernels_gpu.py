@@ -1171,13 +1171,15 @@ def test_skinny_gemm(gpu, M, N, K):
             assert torch.isnan(out2.float()).all(), "reduce=False must leave the output untouched"
 
 
-@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 8, 13])
 @pytest.mark.parametrize("N,K,epi", [(1280, 8192, 0), (8192, 1024, 0), (8192, 3584, 0), (7168, 8192, 1),
                                      (3072, 2048, 0), (16384, 2048, 1), (2048, 8192, 0)])
 def test_gemv_stream(gpu, M, N, K, epi):
-    """gemv_stream_kernel (M <= 4, whole W rows streamed, kw waves splitting K, SwiGLU in the epilogue)
-    at every configuration the decode tuner would try, vs an fp32 reference: Llama-3-70B TP-8 shard
-    shapes and the 1B projections; plus the fp32 result form (epi 0) the fused epilogues read."""
+    """gemv_stream_kernel (M <= 16, whole W rows streamed, kw waves splitting a workgroup's K, kg
+    workgroups splitting K over the grid, SwiGLU in the epilogue or the split-K reduce) at every
+    configuration the decode tuner would try, vs an fp32 reference: Llama-3-70B TP-8 shard shapes and the
+    1B projections; plus the fp32 result form (kg = 1, epi 0) and the raw slabs (kg > 1, reduce=False)
+    the fused epilogues read."""
     from mxserve.ops import decode_gemm
     g = torch.Generator(device="cuda").manual_seed(M * 17 + N + K + epi)
     x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16, generator=g)
@@ -1186,17 +1188,25 @@ def test_gemv_stream(gpu, M, N, K, epi):
     y = x.float() @ w.float().t()
     want = torch.nn.functional.silu(y[:, :N // 2]) * y[:, N // 2:] if epi else y
     cfgs = decode_gemm.gv_candidates(M, N, K, epi)
-    assert cfgs, "every shape here has a row-stream configuration"
+    assert cfgs or M > 4, "every shape here has a row-stream configuration up to M = 4"
+    decode_gemm.TABLE.part = torch.empty(8 * M * N, dtype=torch.float32, device=gpu)
     for cfg in cfgs:
+        kg = decode_gemm.DecodeGemmTable.splitk(cfg)
         out = torch.full(want.shape, float("nan"), device=gpu, dtype=torch.bfloat16)
         assert decode_gemm.TABLE.run(out, x, w, cfg, epi), cfg
         _close(out, want, atol=2e-2, rtol=2e-2, name=f"gemv {M}x{N}x{K} epi {epi} {cfg}")
-        if not epi:
+        if not epi and kg == 1:
             part = torch.full((M * N,), float("nan"), dtype=torch.float32, device=gpu)
             assert ops.ext().gemv_stream(out, x, w, part, cfg[1], cfg[2], 0)
             _close(part.view(M, N), want, atol=2e-3, rtol=2e-3, name=f"gemv fp32 {M}x{N}x{K} {cfg}")
-    assert not ops.ext().gemv_stream(torch.empty(5, want.shape[1], device=gpu, dtype=torch.bfloat16),
-                                     torch.zeros(5, K, device=gpu, dtype=torch.bfloat16), w, None, 2, 1, epi), "M <= 4"
+        elif not epi:
+            part = torch.full((kg * M * N,), float("nan"), dtype=torch.float32, device=gpu)
+            out2 = torch.full(want.shape, float("nan"), device=gpu, dtype=torch.bfloat16)
+            assert ops.ext().gemv_stream(out2, x, w, part, cfg[1], cfg[2], 0, kg, False)
+            _close(part.view(kg, M, N).sum(0), want, atol=2e-3, rtol=2e-3, name=f"gemv slabs {M}x{N}x{K} {cfg}")
+            assert torch.isnan(out2.float()).all(), "reduce=False leaves the output untouched"
+    assert not ops.ext().gemv_stream(torch.empty(17, want.shape[1], device=gpu, dtype=torch.bfloat16),
+                                     torch.zeros(17, K, device=gpu, dtype=torch.bfloat16), w, None, 2, 1, epi), "M <= 16"
 
 
 @pytest.mark.parametrize("M", [1, 8, 16, 32, 64])
