@@ -20,6 +20,8 @@ def main():
     cases = ((64, 32, 8, 2, 4096), (64, 32, 8, 1, 8192), (128, 32, 8, 2, 4096))
     if os.environ.get("PA_CASE"):  # one case (counter passes): index into cases
         cases = (cases[int(os.environ["PA_CASE"])],)
+    if os.environ.get("PA_SHAPES"):  # D=64 Llama-3.2-1B heads at NxL shapes, e.g. "1x4096,4x2048"
+        cases = tuple((64, 32, 8, int(c.split("x")[0]), int(c.split("x")[1])) for c in os.environ["PA_SHAPES"].split(","))
     for D, hq, hkv, nseq, per in cases:
         T = nseq * per
         pb = math.ceil(per / 16)
