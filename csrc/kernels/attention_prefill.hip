@@ -16,6 +16,8 @@
 //                    tile as the next MFMA's operand"): no LDS round trip, no shuffles.
 // Causal tiles past a workgroup's last query position are skipped; heavy tiles launch first.
 #include "common.h"
+#include <algorithm>
+#include <cstdlib>
 
 namespace mxs {
 
@@ -323,6 +325,18 @@ constexpr int kPf3DefaultVar = 0;
 constexpr int pf3_threads(int VAR) { return (VAR & 8) ? 256 : 512; }
 //  64  Q fragments re-read from LDS each tile (4 ds_read_b128) instead of held in 16 registers, so
 //      bit 2 fits the 128 registers of 4 waves per SIMD (VAR 66).
+// 128  split-KV for heavy q-tiles (causal load balance): a workgroup owns a q-tile for ALL its keys, so
+//      below ~8k tokens per launch the tiles with the most keys set the launch time (1 x 4096: 512
+//      workgroups of 1..64 key tiles, mean 32.5).  Every q-tile gets two grid slots; a tile with at
+//      least split_min (8) key tiles runs its key range as two halves, each half writes its partial (O
+//      normalised to bf16, m, l) with agent-scope atomic stores, takes a ticket on the tile's counter,
+//      and the half that arrives second (odd ticket) reads the other half and writes the merged rows
+//      (cdna_hip_programming.md §5 "Projection GEMM at M = 256" item 2, the last-arriver form).  Both
+//      halves merge from the same rounded partials in a fixed order, so the output does not depend on
+//      which half arrives last.  Counters are never reset: each launch adds exactly 2 per split tile, so
+//      the ticket parity names the last arriver.  The default launch picks it when the unsplit grid is
+//      under ~1.25 waves of resident workgroups (pf3_split_blocks): 1 x 1024 1.29x, 1 x 2048 1.19x,
+//      1 x 4096 1.07x at D = 64 (profiles/r5/prefill_attn/split/).
 constexpr int pf3_wpe(int D, int VAR) {
   return (VAR & 8) ? (D == 64 ? 3 : 2) : (D == 64 ? (((VAR & 6) && !(VAR & 64)) ? 2 : 4) : 0);
 }
@@ -334,9 +348,11 @@ paged_prefill_v3_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const void* __restrict__ kv, long block_stride,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ qsl,
     const int* __restrict__ seq_lens, int Hkv, float scale, float v_scale, int q_stride,
-    const int64_t* __restrict__ qpos_tab, const float* __restrict__ cos_sin) {
+    const int64_t* __restrict__ qpos_tab, const float* __restrict__ cos_sin, char* __restrict__ split_ws,
+    int* __restrict__ split_cnt, int split_min) {
   constexpr int KS = D / 16, DT = D / 32;
   constexpr int NT = pf3_threads(VAR);
+  constexpr bool SPLIT = VAR & 128;
   constexpr int BQ = NT / 2 / G;     // query tokens per workgroup (32 rows per wave)
   constexpr int KT = 64;             // keys per tile
   constexpr int KROW = D * 2;        // bytes of one K row in LDS
@@ -357,14 +373,18 @@ paged_prefill_v3_kernel(
   constexpr bool QLDS = VAR & 64;
   __shared__ __attribute__((aligned(16))) char qlds[QLDS ? (NT / 64) * KS * 1024 : 16];
 
-  const int NTL = gridDim.x, total = NTL * gridDim.y * gridDim.z;
-  const int lin = blockIdx.x + NTL * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int NSL = gridDim.x, total = NSL * gridDim.y * gridDim.z;  // grid slots per (kv head, sequence)
+  const int NTL = SPLIT ? NSL / 2 : NSL;                             // q-tiles per (kv head, sequence)
+  const int lin = blockIdx.x + NSL * (blockIdx.y + gridDim.y * blockIdx.z);
   const int vix = (total % 8 == 0) ? (lin % 8) * (total / 8) + lin / 8 : lin;
-  const int pair = vix / NTL;
+  const int pair = vix / NSL;
   const int kvh = pair % gridDim.y, seq = pair / gridDim.y;
   const int q0 = qsl[seq];
   const int ql = qsl[seq + 1] - q0;
-  const int t0 = (NTL - 1 - (vix - pair * NTL)) * BQ;  // heaviest tiles first
+  const int slot = vix - pair * NSL;
+  const int tile = NTL - 1 - (SPLIT ? slot / 2 : slot);  // heaviest tiles first (both halves together)
+  const int half = SPLIT ? slot & 1 : 0;
+  const int t0 = tile * BQ;
   if (t0 >= ql) return;
   const int L = seq_lens[seq];
   const int ctx0 = L - ql;
@@ -377,6 +397,16 @@ paged_prefill_v3_kernel(
   const bool rvalid = tok < ql;
   const int qpos = ctx0 + (rvalid ? tok : 0);
   const int nkeys = ctx0 + min(t0 + BQ, ql);
+  const int nkt = (nkeys + KT - 1) / KT;
+  const int kmid = (nkt / 2) * KT;  // half 0: keys [0, kmid), half 1: [kmid, nkeys)
+  // split only where every valid row of the tile has a key in the second half (its first tile then
+  // sets m from real scores; padding rows past the sequence end see only masked keys there, and their
+  // NaNs stay in their own P columns and are never stored)
+  // split_min: low 16 bits, the key-tile floor; bit 16: also require half the sequence's heaviest tile
+  const bool heavy = nkt >= (split_min & 0xffff) && (!(split_min >> 16) || 2 * nkt >= (L + KT - 1) / KT);
+  const bool split = SPLIT && heavy && ctx0 + t0 >= kmid;
+  if (SPLIT && !split && half == 1) return;  // the tile runs unsplit in its first slot
+  const int kbeg = split && half == 1 ? kmid : 0, kend = split && half == 0 ? kmid : nkeys;
   const int wave_min_pos = ctx0 + min(t0 + (wid * 32) / G, ql - 1);
   const int wave_max_pos = ctx0 + min(t0 + (wid * 32 + 31) / G, ql - 1);
 
@@ -634,7 +664,7 @@ paged_prefill_v3_kernel(
   // QK^T + softmax of one tile into P (bf16 fragments pf); pv(): O += V^T . P^T of that tile
   auto softmax_phase = [&](int buf, int k0, bf16x8_t (&pf)[2][2]) {
     const char* kl = lds[buf];
-    const bool first = k0 == 0;
+    const bool first = k0 == kbeg;
     const bool diag = k0 + KT - 1 > wave_min_pos;  // tile crosses the diagonal (or the end) of some row
     float16_ sacc[2];
     float ps;
@@ -726,12 +756,12 @@ paged_prefill_v3_kernel(
       if ((sl & 1) == 1 && sl >= 3 && (sl + 1) / 2 < ntile) sstore(((sl + 1) / 2) & 1);
     }
   } else {
-    gload(0);
+    gload(kbeg);
     sstore(0);
     __syncthreads();
-    for (int it = 0, k0 = 0; k0 < nkeys; ++it, k0 += KT) {
+    for (int it = 0, k0 = kbeg; k0 < kend; ++it, k0 += KT) {
       const int buf = it & 1;
-      const bool more = k0 + KT < nkeys;
+      const bool more = k0 + KT < kend;
       if (more) gload(k0 + KT);           // in flight under this tile's MFMAs
       if (k0 <= wave_max_pos) compute(buf, k0);  // waves whose rows all precede the tile skip it
       if (more) sstore(buf ^ 1);
@@ -743,6 +773,76 @@ paged_prefill_v3_kernel(
     l = lsum[0];  // ones^T . P^T summed both half-waves' keys already
   else
     l += __shfl_xor(l, 32, 64);
+  if constexpr (SPLIT) {
+    if (split) {
+      // this half's partial: O / l rounded to bf16 (16 words per lane), then (m, l); a lane's 72 bytes
+      // sit at a fixed place per (tile, half, wave, lane), so the other half reads exactly its own lanes
+      const int item = pair * NTL + tile;
+      const float pin = l > 0.f ? 1.f / l : 0.f;  // rows past the sequence end have no keys
+      uint32_t mine[DT * 8];
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) mine[dt * 8 + i] = pack2(o[dt][2 * i] * pin, o[dt][2 * i + 1] * pin);
+      // agent-scope relaxed atomic stores / loads (write through to, and read from, the cross-XCD
+      // coherence point): only the partials bypass the caches.  Release / acquire fences would write
+      // back and invalidate this XCD's whole L2 instead, and with it every K/V tile cached for the
+      // other workgroups (measured: VAR 128 slower than VAR 0 at every shape that way).
+      constexpr int NJ = DT * 4 + 1;  // 8-byte words per lane: O slice, then (m, l); word-major, lane-minor
+      uint64_t* wsw = reinterpret_cast<uint64_t*>(split_ws) + ((static_cast<size_t>(item) * 2 + half) * (NT / 64) + wid) * 64 * NJ;
+#pragma unroll
+      for (int j = 0; j < NJ - 1; ++j)
+        __hip_atomic_store(wsw + j * 64 + lane, static_cast<uint64_t>(mine[2 * j]) | (static_cast<uint64_t>(mine[2 * j + 1]) << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(wsw + (NJ - 1) * 64 + lane,
+                         static_cast<uint64_t>(__float_as_uint(m)) | (static_cast<uint64_t>(__float_as_uint(l)) << 32),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's partial has reached memory
+      __syncthreads();
+      int* last_flag = reinterpret_cast<int*>(lds[0]);  // the K/V tiles are no longer read
+      if (tid == 0)
+        *last_flag = __hip_atomic_fetch_add(split_cnt + item, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1;
+      __syncthreads();
+      if (!*last_flag) return;
+      // the second arriver merges both halves' rounded partials in half order
+      const uint64_t* wso = reinterpret_cast<const uint64_t*>(split_ws) +
+                            ((static_cast<size_t>(item) * 2 + (half ^ 1)) * (NT / 64) + wid) * 64 * NJ;
+      uint32_t other[DT * 8];
+#pragma unroll
+      for (int j = 0; j < NJ - 1; ++j) {
+        const uint64_t v = __hip_atomic_load(wso + j * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        other[2 * j] = static_cast<uint32_t>(v);
+        other[2 * j + 1] = static_cast<uint32_t>(v >> 32);
+      }
+      const uint64_t mlv = __hip_atomic_load(wso + (NJ - 1) * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float2 mlo = make_float2(__uint_as_float(static_cast<uint32_t>(mlv)), __uint_as_float(static_cast<uint32_t>(mlv >> 32)));
+      if (!rvalid) return;
+      const float m0 = half == 0 ? m : mlo.x, l0 = half == 0 ? l : mlo.y;
+      const float m1 = half == 0 ? mlo.x : m, l1 = half == 0 ? mlo.y : l;
+      const uint32_t* p0 = half == 0 ? mine : other;
+      const uint32_t* p1 = half == 0 ? other : mine;
+      const float mm = fmaxf(m0, m1);
+      const float w0 = l0 > 0.f ? l0 * __builtin_amdgcn_exp2f(m0 - mm) : 0.f;
+      const float w1 = l1 > 0.f ? l1 * __builtin_amdgcn_exp2f(m1 - mm) : 0.f;
+      const float sc = v_scale / (w0 + w1);
+      bf16_t* op = out + (static_cast<size_t>(q0 + tok) * Hq + head) * D;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = 32 * dt + 8 * g4 + 4 * h;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const uint32_t a = p0[dt * 8 + 2 * g4 + e], b = p1[dt * 8 + 2 * g4 + e];
+            v[2 * e] = (bf2f_lo(a) * w0 + bf2f_lo(b) * w1) * sc;
+            v[2 * e + 1] = (bf2f_hi(a) * w0 + bf2f_hi(b) * w1) * sc;
+          }
+          *reinterpret_cast<uint2*>(op + d0) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+      return;
+    }
+  }
   if (!rvalid) return;
   const float inv = v_scale / l;
   bf16_t* op = out + (static_cast<size_t>(q0 + tok) * Hq + head) * D;
@@ -758,24 +858,65 @@ paged_prefill_v3_kernel(
     }
 }
 
+// split-variant scratch per q-tile item: 2 halves x waves x 64 lanes x (bf16 O row slice + (m, l))
+static constexpr long pf3_split_item_bytes(int D, int VAR) { return 2L * (pf3_threads(VAR) / 64) * 64 * (D * 2 + 8); }
+
+static int pf3_env(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e != nullptr ? std::atoi(e) : dflt;
+}
+static int pf3_split_min() {
+  static const int v = std::max(4, pf3_env("MXS_PF_SPLIT_MIN", 8)) | (pf3_env("MXS_PF_SPLIT_REL", 0) ? 1 << 16 : 0);
+  return v;
+}
+// the default launch splits when its unsplit grid is under this many workgroups (about 1.25 waves of
+// resident workgroups: 2 per CU at D = 64, 1 at D = 128)
+static int pf3_split_blocks(int D) {
+  static const int v = pf3_env("MXS_PF_SPLIT_BLOCKS", -1);
+  return v >= 0 ? v : (D == 64 ? 640 : 320);
+}
+
 template <int D, int G, int EB, int VAR>
 static void pf3_launch(bf16_t* out, const bf16_t* q, const void* kv, long block_stride, const int* block_tables,
                        int bt_stride, const int* qsl, const int* seq_lens, int num_seqs, int max_q_len, int Hkv,
-                       float sc, float vs, int q_stride, const int64_t* qpos, const float* cos_sin, hipStream_t s) {
+                       float sc, float vs, int q_stride, const int64_t* qpos, const float* cos_sin, hipStream_t s,
+                       char* split_ws, int* split_cnt) {
   constexpr int NT = pf3_threads(VAR), BQ = NT / 2 / G;
-  const dim3 grid((max_q_len + BQ - 1) / BQ, Hkv, num_seqs);
+  constexpr bool SPLIT = VAR & 128;
+  const int ntl = (max_q_len + BQ - 1) / BQ;
+  const dim3 grid(ntl * (SPLIT ? 2 : 1), Hkv, num_seqs);
   hipLaunchKernelGGL((paged_prefill_v3_kernel<D, G, EB, VAR>), grid, dim3(NT), 0, s, out, q, kv, block_stride,
-                     block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs, q_stride, qpos, cos_sin);
+                     block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs, q_stride, qpos, cos_sin, split_ws, split_cnt,
+                     pf3_split_min());
+}
+
+// the variant a v3 launch runs: explicit (version 0x100 | VAR; other than 128: bf16 caches, G = 4 only),
+// else the split variant for grids too small to fill the chip twice over, else the default
+static int pf3_effective_var(int version, bool fp8, int G, int D, long blocks) {
+  if (version >= 0x100) {
+    const int var = version & 0xff;
+    if (var == 128) return 128;
+    return !fp8 && G == 4 ? var : kPf3DefaultVar;
+  }
+  return blocks <= pf3_split_blocks(D) ? 128 : kPf3DefaultVar;
+}
+static long pf3_blocks(int num_seqs, int max_q_len, int Hkv, int G) {
+  const int BQ = pf3_threads(0) / 2 / G;
+  return static_cast<long>(num_seqs) * Hkv * ((max_q_len + BQ - 1) / BQ);
 }
 
 template <int D, int G>
 static void pf3_dispatch(int var, bool fp8, bf16_t* out, const bf16_t* q, const void* kv, long block_stride,
                          const int* block_tables, int bt_stride, const int* qsl, const int* seq_lens, int num_seqs,
                          int max_q_len, int Hkv, float sc, float vs, int q_stride, const int64_t* qpos,
-                         const float* cos_sin, hipStream_t s) {
+                         const float* cos_sin, hipStream_t s, char* split_ws, int* split_cnt) {
 #define MXS_PF3_ARGS out, q, kv, block_stride, block_tables, bt_stride, qsl, seq_lens, num_seqs, max_q_len, Hkv, sc, vs, \
-                     q_stride, qpos, cos_sin, s
-  if (fp8) return pf3_launch<D, G, 1, kPf3DefaultVar>(MXS_PF3_ARGS);
+                     q_stride, qpos, cos_sin, s, split_ws, split_cnt
+  if (var == 128 && split_ws != nullptr && split_cnt != nullptr) {
+    if (fp8) return pf3_launch<D, G, 1, 128>(MXS_PF3_ARGS);
+    return pf3_launch<D, G, 2, 128>(MXS_PF3_ARGS);
+  }
+  if (fp8) return pf3_launch<D, G, 1, (kPf3DefaultVar & ~128)>(MXS_PF3_ARGS);
   if constexpr (G == 4) {  // the other variants: G = 4 only (A/B probes and tests)
     switch (var) {
       case 1: return pf3_launch<D, G, 2, 1>(MXS_PF3_ARGS);
@@ -795,8 +936,23 @@ static void pf3_dispatch(int var, bool fp8, bf16_t* out, const bf16_t* q, const 
       default: break;
     }
   }
-  pf3_launch<D, G, 2, kPf3DefaultVar>(MXS_PF3_ARGS);
+  pf3_launch<D, G, 2, (kPf3DefaultVar & ~128)>(MXS_PF3_ARGS);
 #undef MXS_PF3_ARGS
+}
+
+// Bytes of scratch and int32 counters the launch needs (0 when it does not run the split variant).
+// Counters must start at zero once and are never reset (see the split comment above the kernel).
+void paged_prefill_split_need(int version, bool kv_fp8, int num_seqs, int max_q_len, int Hq, int Hkv, int D,
+                              long* ws_bytes, long* counters) {
+  *ws_bytes = 0;
+  *counters = 0;
+  if (num_seqs == 0 || max_q_len == 0 || Hkv == 0 || Hq % Hkv != 0 || (D != 64 && D != 128)) return;
+  const int G = Hq / Hkv;
+  const long items = pf3_blocks(num_seqs, max_q_len, Hkv, G);
+  if (version == 2 && !kv_fp8) return;  // v2 unless the launch needs v3 (fused q): not split either way
+  if (pf3_effective_var(version, kv_fp8, G, D, items) != 128) return;
+  *counters = items;
+  *ws_bytes = items * (D == 64 ? pf3_split_item_bytes(64, 128) : pf3_split_item_bytes(128, 128));
 }
 
 // q_stride: elements between consecutive q rows (Hq * D for a dense q; (Hq + 2 Hkv) * D when q is
@@ -806,18 +962,18 @@ void launch_paged_prefill(bf16_t* out, const bf16_t* q, const void* kv_ptr, bool
                           const int* block_tables, int bt_stride, const int* qsl, const int* seq_lens,
                           int num_seqs, int max_q_len, int Hq, int Hkv, int D, float scale, int version,
                           float k_scale, float v_scale, hipStream_t s, int q_stride, const int64_t* qpos,
-                          const float* cos_sin) {
+                          const float* cos_sin, char* split_ws, int* split_cnt) {
   if (num_seqs == 0 || max_q_len == 0) return;
   const int G = Hq / Hkv;
   const bf16_t* kv = static_cast<const bf16_t*>(kv_ptr);
   if (q_stride <= 0) q_stride = Hq * D;
   if (version != 2 || kv_fp8 || cos_sin != nullptr || q_stride != Hq * D) {  // fp8 / fused q: the v3 path only
     const float sc = kv_fp8 ? scale * k_scale : scale, vs = kv_fp8 ? v_scale : 1.f;
-    const int var = version >= 0x100 ? (version & 0xff) : kPf3DefaultVar;
+    const int var = pf3_effective_var(version, kv_fp8, G, D, pf3_blocks(num_seqs, max_q_len, Hkv, G));
 #define MXS_PF3(DD, GG)                                                                                     \
     if (D == DD && G == GG) {                                                                               \
       pf3_dispatch<DD, GG>(var, kv_fp8, out, q, kv_ptr, block_stride, block_tables, bt_stride, qsl, seq_lens, \
-                           num_seqs, max_q_len, Hkv, sc, vs, q_stride, qpos, cos_sin, s);                   \
+                           num_seqs, max_q_len, Hkv, sc, vs, q_stride, qpos, cos_sin, s, split_ws, split_cnt); \
       MXS_CHECK_LAUNCH();                                                                                   \
       return;                                                                                               \
     }

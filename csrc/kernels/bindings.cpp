@@ -4,6 +4,8 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
 #include <optional>
 
 namespace mxs {
@@ -22,7 +24,8 @@ bool launch_paged_decode(bf16_t*, float*, float*, const bf16_t*, const void*, bo
                          const int64_t* = nullptr, const float* = nullptr);
 void launch_paged_prefill(bf16_t*, const bf16_t*, const void*, bool, long, const int*, int, const int*, const int*,
                           int, int, int, int, int, float, int, float, float, hipStream_t, int = 0,
-                          const int64_t* = nullptr, const float* = nullptr);
+                          const int64_t* = nullptr, const float* = nullptr, char* = nullptr, int* = nullptr);
+void paged_prefill_split_need(int, bool, int, int, int, int, int, long*, long*);
 void launch_sample(int64_t*, const void*, bool, int, int, long, const float*, const float*, const int*,
                    const int64_t*, const int64_t*, hipStream_t);
 void launch_logprobs(float*, int64_t*, float*, const void*, bool, int, int, long, const int64_t*, const int64_t*, int,
@@ -237,11 +240,37 @@ void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Te
   TORCH_CHECK(qsl.scalar_type() == at::kInt && seq_lens.scalar_type() == at::kInt, "int32 metadata");
   TORCH_CHECK(block_tables.scalar_type() == at::kInt && block_tables.stride(1) == 1, "block_tables");
   const int S = seq_lens.size(0);
+  // the split variant: scratch from the caching allocator per call, tile counters persistent per device
+  // (zeroed once, never reset: each launch adds 2 per split tile)
+  long ws_bytes = 0, ncnt = 0;
+  mxs::paged_prefill_split_need(static_cast<int>(version), fp8, S, static_cast<int>(max_q_len), Hq, Hkv, D,
+                                &ws_bytes, &ncnt);
+  at::Tensor ws;
+  int* cnt = nullptr;
+  if (ws_bytes > 0) {
+    static std::mutex mu;
+    static std::map<int, at::Tensor> counters;
+    std::lock_guard<std::mutex> lock(mu);
+    at::Tensor& c = counters[q.get_device()];
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    TORCH_CHECK(hipStreamIsCapturing(stream(), &cap) == hipSuccess, "hipStreamIsCapturing");
+    if (!c.defined() || c.numel() < ncnt) {
+      if (cap == hipStreamCaptureStatusNone)
+        c = at::zeros({std::max<long>(ncnt, 1L << 14)}, q.options().dtype(at::kInt));
+      else
+        ws_bytes = 0;  // no counters outside a graph's pool: run this launch unsplit
+    }
+    if (ws_bytes > 0) {
+      cnt = c.data_ptr<int>();
+      ws = at::empty({ws_bytes}, q.options().dtype(at::kByte));
+    }
+  }
   mxs::launch_paged_prefill(bf(out), bf(q), kv.data_ptr(), fp8, kv.stride(0), block_tables.data_ptr<int>(),
                             block_tables.stride(0), qsl.data_ptr<int>(), seq_lens.data_ptr<int>(), S,
                             static_cast<int>(max_q_len), Hq, Hkv, D, static_cast<float>(scale),
                             static_cast<int>(version), static_cast<float>(k_scale), static_cast<float>(v_scale),
-                            stream(), qa.stride, qa.pos, qa.cs);
+                            stream(), qa.stride, qa.pos, qa.cs,
+                            ws_bytes > 0 ? reinterpret_cast<char*>(ws.data_ptr()) : nullptr, cnt);
 }
 
 void sample(at::Tensor out, at::Tensor logits, at::Tensor temperature, at::Tensor top_p, at::Tensor top_k,

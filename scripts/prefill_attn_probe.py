@@ -3,7 +3,8 @@
 `per` tokens each (the bench's 8192-token chunk = 2 x 4096), Llama-3.2-1B heads (32 q / 8 kv, D 64)
 and Llama-3-8B-like D 128; one JSON line per case with ms and TFLOP/s (causal half counted).
 PA_VARS=0,2,6 times the softmax variants of the v3 kernel (version 0x100 | VAR, G = 4 only) round-robin
-on the same inputs and reports each one's max |diff| against the first."""
+on the same inputs and reports each one's max |diff| against the first; -1 is the default launch (which
+picks the split variant 128 for small grids)."""
 import json
 import math
 import os
@@ -20,8 +21,9 @@ def main():
     cases = ((64, 32, 8, 2, 4096), (64, 32, 8, 1, 8192), (128, 32, 8, 2, 4096))
     if os.environ.get("PA_CASE"):  # one case (counter passes): index into cases
         cases = (cases[int(os.environ["PA_CASE"])],)
-    if os.environ.get("PA_SHAPES"):  # D=64 Llama-3.2-1B heads at NxL shapes, e.g. "1x4096,4x2048"
-        cases = tuple((64, 32, 8, int(c.split("x")[0]), int(c.split("x")[1])) for c in os.environ["PA_SHAPES"].split(","))
+    if os.environ.get("PA_SHAPES"):  # Llama-3.2-1B heads at NxL[xD] shapes (D 64 default), e.g. "1x4096,4x2048x128"
+        cases = tuple((int((c.split("x") + ["64"])[2]), 32, 8, int(c.split("x")[0]), int(c.split("x")[1]))
+                      for c in os.environ["PA_SHAPES"].split(","))
     for D, hq, hkv, nseq, per in cases:
         T = nseq * per
         pb = math.ceil(per / 16)
@@ -35,7 +37,7 @@ def main():
         ref_out, times = None, {v: [] for v in variants}
         for rnd in range(3):
             for v in variants:
-                ver = 0 if v is None else 0x100 | v
+                ver = 0 if v is None else (3 if v < 0 else 0x100 | v)  # -1: the default launch (split gate)
                 fn = lambda: ops.paged_attention_prefill(q, kv, bt, qsl, sl, D ** -0.5, per, version=ver)  # noqa: E731
                 for _ in range(3):
                     out = fn()

@@ -203,7 +203,7 @@ def test_prefill_softmax_rescale_spike(gpu, version):
 
 # v3 softmax variants (attention_prefill.hip VAR bits: 1 biased reference + overflow redo, 2 row sum
 # on the matrix pipe, 4 persistent -m accumulator block), launched as version 0x100 | VAR at G = 4
-@pytest.mark.parametrize("var", [0, 1, 2, 4, 6, 7, 8, 10, 12, 14, 16, 32, 36, 64, 66])
+@pytest.mark.parametrize("var", [0, 1, 2, 4, 6, 7, 8, 10, 12, 14, 16, 32, 36, 64, 66, 128])
 @pytest.mark.parametrize("D", [64, 128])
 def test_paged_prefill_softmax_variants(gpu, D, var):
     G, hkv = 4, 2
@@ -219,6 +219,37 @@ def test_paged_prefill_softmax_variants(gpu, D, var):
                                       max(n for _, n in specs), version=0x100 | var)
     exp = ref.paged_attention(q.cpu(), kv[:, 1].cpu(), bt, qsl_t, sl, 1 / math.sqrt(D))
     _close(out, exp, 0.03, 0.03, f"prefill var {var}")
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("D,G", [(64, 4), (128, 4), (64, 1), (128, 8)])
+def test_paged_prefill_split(gpu, D, G, fp8):
+    """VAR 128: q-tiles with >= 24 key tiles run as two workgroups over the two halves of their key
+    range, merged by the second to finish.  Long prompts, a prefix-cache hit, a short chunk over a long
+    context and a short prompt (unsplit) in one launch; launched three times, the output must not change
+    (the tile counters are never reset: the ticket parity names the merging half)."""
+    hkv = 2
+    specs = [(0, 2000), (1500, 700), (3000, 5), (0, 100)]
+    seq_lens = [c + n for c, n in specs]
+    kv, bt = _paged_setup(seq_lens, hkv, D, device=gpu)
+    ks, vs = (0.5, 0.25) if fp8 else (1.0, 1.0)
+    cache = _fp8_cache(kv, 1.0) if fp8 else kv
+    qsl = [0]
+    for _, n in specs:
+        qsl.append(qsl[-1] + n)
+    q = torch.randn(qsl[-1], hkv * G, D, device=gpu, dtype=torch.bfloat16)
+    qsl_t, sl = torch.tensor(qsl, dtype=torch.int32), torch.tensor(seq_lens, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    outs = [ops.paged_attention_prefill(q, cache[:, 1], bt.to(gpu), qsl_t.to(gpu), sl.to(gpu), scale,
+                                        max(n for _, n in specs), version=0x100 | 128, k_scale=ks, v_scale=vs)
+            for _ in range(3)]
+    exp = ref.paged_attention(q.cpu(), cache[:, 1].cpu(), bt, qsl_t, sl, scale, ks, vs)
+    _close(outs[0], exp, 0.03, 0.03, f"prefill split D{D} G{G} fp8={fp8}")
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    base = ops.paged_attention_prefill(q, cache[:, 1], bt.to(gpu), qsl_t.to(gpu), sl.to(gpu), scale,
+                                       max(n for _, n in specs), version=0x100, k_scale=ks, v_scale=vs)
+    # the unsplit kernel on the same inputs: the split changes only rounding
+    assert (outs[0].float() - base.float()).abs().max().item() < 0.03
 
 
 @pytest.mark.parametrize("factor", [4, 12])
