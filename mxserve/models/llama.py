@@ -224,6 +224,15 @@ class TransformerLM:
                 self.hd in (64, 128) and self.nh // self.nkv >= 4 and self.nh % self.nkv == 0 and
                 (qkv_given or not ops.qkv_uses_slabs(h, self.w[f"l{i}.qkv"])))
 
+    def _side_stream(self, device) -> Optional[torch.cuda.Stream]:
+        """The mixed-step prefill-attention stream (None while a graph is being captured)."""
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        st = getattr(self, "_attn_side", None)
+        if st is None:
+            st = self._attn_side = torch.cuda.Stream(device=device)
+        return st
+
     def _attention(self, i: int, h: Optional[torch.Tensor], md: AttnMetadata, kv_layer: torch.Tensor,
                    project: bool = True, qkv: Optional[torch.Tensor] = None):
         """qkv: the projection already computed (_forward_pf); h is then unused."""
@@ -259,11 +268,25 @@ class TransformerLM:
             rd = rp = None
             if rope is not None:
                 rd, rp = (md.positions[:nd], self.cos_sin), (md.positions[nd:], self.cos_sin)
+            # mixed step: the prefill chunk's attention (MFMA-bound) on a second stream under the
+            # decode rows' attention (HBM-bound); both only read the cache written above, and the main
+            # stream joins before o_proj (scripts/probes/attn_overlap_probe.py)
+            side = self._side_stream(q.device) if _ATTN_OVERLAP else None
+            if side is not None:
+                main = torch.cuda.current_stream(q.device)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    ops.paged_attention_prefill(q[nd:], kv_layer, md.block_tables[nd:], md.prefill_query_start_loc,
+                                                md.seq_lens[nd:], self.scale, md.max_query_len, out=o[nd:], rope=rp,
+                                                **self.kv_scales[i])
             ops.paged_attention_decode(q[:nd], kv_layer, md.block_tables[:nd], md.seq_lens[:nd], self.scale,
                                        md.max_seq_len, out=o[:nd], rope=rd, **self.kv_scales[i])
-            ops.paged_attention_prefill(q[nd:], kv_layer, md.block_tables[nd:], md.prefill_query_start_loc,
-                                        md.seq_lens[nd:], self.scale, md.max_query_len, out=o[nd:], rope=rp,
-                                        **self.kv_scales[i])
+            if side is not None:
+                main.wait_stream(side)
+            else:
+                ops.paged_attention_prefill(q[nd:], kv_layer, md.block_tables[nd:], md.prefill_query_start_loc,
+                                            md.seq_lens[nd:], self.scale, md.max_query_len, out=o[nd:], rope=rp,
+                                            **self.kv_scales[i])
         if not project:  # the caller fuses o_proj with the residual add + next norm
             return o.reshape(o.shape[0], -1)
         out = ops.linear(o.reshape(o.shape[0], -1), w[p + "o"])
@@ -470,6 +493,7 @@ class TransformerLM:
 
 _FUSED_Q_ROPE = os.environ.get("MXS_FUSED_Q_ROPE", "1") == "1"
 _SAMPLED_QROPE = os.environ.get("MXS_SAMPLED_QROPE", "1") == "1"  # pruned last layer: q rotated in-kernel
+_ATTN_OVERLAP = os.environ.get("MXS_ATTN_OVERLAP", "1") == "1"  # mixed steps: prefill attention on a side stream
 
 
 def _pad_rows(t: torch.Tensor, n: int) -> torch.Tensor:

@@ -79,6 +79,8 @@ def run(model: str, qps: float, isl: int, osl: int, warmup_s: float, window_s: f
                HSA_ENABLE_IPC_MODE_LEGACY="0", MXS_STREAM_PORT=str(s_port))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR", "TORCHELASTIC_RUN_ID"):
         env.pop(k, None)
+    if log_dir:
+        os.makedirs(log_dir, exist_ok=True)
     out = open(os.path.join(log_dir, "served_frontend.log"), "w") if log_dir else subprocess.DEVNULL
     wout = open(os.path.join(log_dir, "served_worker.log"), "w") if log_dir else subprocess.DEVNULL
     fe = w = None
