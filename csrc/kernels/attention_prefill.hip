@@ -337,19 +337,23 @@ constexpr int pf3_threads(int VAR) { return (VAR & 8) ? 256 : 512; }
 //      the ticket parity names the last arriver.  The default launch picks it when the unsplit grid is
 //      under ~1.25 waves of resident workgroups (pf3_split_blocks): 1 x 1024 1.29x, 1 x 2048 1.19x,
 //      1 x 4096 1.07x at D = 64 (profiles/r5/prefill_attn/split/).
+// 256  paired q-tiles (causal load balance at two waves and up): workgroup s of a sequence's n tiles
+//      runs tile n - 1 - s and then tile s, n + 1 key tiles each, half the workgroups; picked when the
+//      paired grid fills the resident workgroups at least once: 8 x 1024 1.21x, 4 x 2048 1.11x,
+//      2 x 4096 1.09x (883 TF/s), 1 x 8192 1.02x at D = 64 (profiles/r5/prefill_attn/pair/).
 constexpr int pf3_wpe(int D, int VAR) {
   return (VAR & 8) ? (D == 64 ? 3 : 2) : (D == 64 ? (((VAR & 6) && !(VAR & 64)) ? 2 : 4) : 0);
 }
 
+// one q-tile (`tile` of (kv head, sequence) `pair`; `half` of its key range when split) of the v3
+// kernel; NTL: q-tiles per pair (the split workspace's stride)
 template <int D, int G, int EB, int VAR>
-__global__ void __launch_bounds__(pf3_threads(VAR))
-__attribute__((amdgpu_waves_per_eu(pf3_wpe(D, VAR) ? pf3_wpe(D, VAR) : 1, pf3_wpe(D, VAR) ? pf3_wpe(D, VAR) : 8)))
-paged_prefill_v3_kernel(
+__device__ __forceinline__ void pf3_tile(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const void* __restrict__ kv, long block_stride,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ qsl,
     const int* __restrict__ seq_lens, int Hkv, float scale, float v_scale, int q_stride,
     const int64_t* __restrict__ qpos_tab, const float* __restrict__ cos_sin, char* __restrict__ split_ws,
-    int* __restrict__ split_cnt, int split_min) {
+    int* __restrict__ split_cnt, int split_min, int tile, int half, int pair, int NTL) {
   constexpr int KS = D / 16, DT = D / 32;
   constexpr int NT = pf3_threads(VAR);
   constexpr bool SPLIT = VAR & 128;
@@ -373,17 +377,9 @@ paged_prefill_v3_kernel(
   constexpr bool QLDS = VAR & 64;
   __shared__ __attribute__((aligned(16))) char qlds[QLDS ? (NT / 64) * KS * 1024 : 16];
 
-  const int NSL = gridDim.x, total = NSL * gridDim.y * gridDim.z;  // grid slots per (kv head, sequence)
-  const int NTL = SPLIT ? NSL / 2 : NSL;                             // q-tiles per (kv head, sequence)
-  const int lin = blockIdx.x + NSL * (blockIdx.y + gridDim.y * blockIdx.z);
-  const int vix = (total % 8 == 0) ? (lin % 8) * (total / 8) + lin / 8 : lin;
-  const int pair = vix / NSL;
   const int kvh = pair % gridDim.y, seq = pair / gridDim.y;
   const int q0 = qsl[seq];
   const int ql = qsl[seq + 1] - q0;
-  const int slot = vix - pair * NSL;
-  const int tile = NTL - 1 - (SPLIT ? slot / 2 : slot);  // heaviest tiles first (both halves together)
-  const int half = SPLIT ? slot & 1 : 0;
   const int t0 = tile * BQ;
   if (t0 >= ql) return;
   const int L = seq_lens[seq];
@@ -858,6 +854,44 @@ paged_prefill_v3_kernel(
     }
 }
 
+// Grid slots of a (kv head, sequence) pair, heaviest q-tiles first; workgroups visit the pairs
+// XCD-aware (the 8 XCDs take contiguous ranges of slots).  VAR & 256 (PAIR): slot s runs q-tile
+// n - 1 - s and then q-tile s of its sequence's n tiles, so every workgroup does n + 1 tiles of keys
+// (no causal tail); VAR & 128 (SPLIT): two slots per q-tile.
+template <int D, int G, int EB, int VAR>
+__global__ void __launch_bounds__(pf3_threads(VAR))
+__attribute__((amdgpu_waves_per_eu(pf3_wpe(D, VAR) ? pf3_wpe(D, VAR) : 1, pf3_wpe(D, VAR) ? pf3_wpe(D, VAR) : 8)))
+paged_prefill_v3_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ q, const void* __restrict__ kv, long block_stride,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ qsl,
+    const int* __restrict__ seq_lens, int Hkv, float scale, float v_scale, int q_stride,
+    const int64_t* __restrict__ qpos_tab, const float* __restrict__ cos_sin, char* __restrict__ split_ws,
+    int* __restrict__ split_cnt, int split_min) {
+  constexpr bool SPLIT = VAR & 128, PAIR = VAR & 256;
+  static_assert(!(SPLIT && PAIR), "one slot map per variant");
+  constexpr int BQ = pf3_threads(VAR) / 2 / G;
+  const int NSL = gridDim.x, total = NSL * gridDim.y * gridDim.z;  // grid slots per (kv head, sequence)
+  const int lin = blockIdx.x + NSL * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int vix = (total % 8 == 0) ? (lin % 8) * (total / 8) + lin / 8 : lin;
+  const int pair = vix / NSL, slot = vix - pair * NSL;
+#define MXS_PF3_TILE_ARGS out, q, kv, block_stride, block_tables, bt_stride, qsl, seq_lens, Hkv, scale, v_scale, \
+                          q_stride, qpos_tab, cos_sin, split_ws, split_cnt, split_min
+  if constexpr (PAIR) {
+    const int seq = pair / gridDim.y;
+    const int n = (qsl[seq + 1] - qsl[seq] + BQ - 1) / BQ;
+    if (2 * slot >= n) return;
+    pf3_tile<D, G, EB, VAR>(MXS_PF3_TILE_ARGS, n - 1 - slot, 0, pair, NSL);
+    if (slot != n - 1 - slot) {
+      __syncthreads();  // the first tile's last LDS reads are behind its loop's final barrier; cheap insurance
+      pf3_tile<D, G, EB, VAR>(MXS_PF3_TILE_ARGS, slot, 0, pair, NSL);
+    }
+  } else {
+    const int NTL = SPLIT ? NSL / 2 : NSL;
+    pf3_tile<D, G, EB, VAR>(MXS_PF3_TILE_ARGS, NTL - 1 - (SPLIT ? slot / 2 : slot), SPLIT ? slot & 1 : 0, pair, NTL);
+  }
+#undef MXS_PF3_TILE_ARGS
+}
+
 // split-variant scratch per q-tile item: 2 halves x waves x 64 lanes x (bf16 O row slice + (m, l))
 static constexpr long pf3_split_item_bytes(int D, int VAR) { return 2L * (pf3_threads(VAR) / 64) * 64 * (D * 2 + 8); }
 
@@ -882,23 +916,30 @@ static void pf3_launch(bf16_t* out, const bf16_t* q, const void* kv, long block_
                        float sc, float vs, int q_stride, const int64_t* qpos, const float* cos_sin, hipStream_t s,
                        char* split_ws, int* split_cnt) {
   constexpr int NT = pf3_threads(VAR), BQ = NT / 2 / G;
-  constexpr bool SPLIT = VAR & 128;
+  constexpr bool SPLIT = VAR & 128, PAIR = VAR & 256;
   const int ntl = (max_q_len + BQ - 1) / BQ;
-  const dim3 grid(ntl * (SPLIT ? 2 : 1), Hkv, num_seqs);
+  const dim3 grid(PAIR ? (ntl + 1) / 2 : ntl * (SPLIT ? 2 : 1), Hkv, num_seqs);
   hipLaunchKernelGGL((paged_prefill_v3_kernel<D, G, EB, VAR>), grid, dim3(NT), 0, s, out, q, kv, block_stride,
                      block_tables, bt_stride, qsl, seq_lens, Hkv, sc, vs, q_stride, qpos, cos_sin, split_ws, split_cnt,
                      pf3_split_min());
 }
 
-// the variant a v3 launch runs: explicit (version 0x100 | VAR; other than 128: bf16 caches, G = 4 only),
-// else the split variant for grids too small to fill the chip twice over, else the default
-static int pf3_effective_var(int version, bool fp8, int G, int D, long blocks) {
+// the variant a v3 launch runs: explicit (version 0x100 + VAR; other than 128 / 256: bf16 caches, G = 4
+// only), else by grid size against the resident workgroups W (2 per CU at D = 64, 1 at D = 128):
+// split (128) when the unsplit grid is under ~1.25 W, paired (256) when the paired grid fills at
+// least W, else the default (profiles/r5/prefill_attn/split/, pair/).
+static int pf3_effective_var(int version, bool fp8, int G, int D, int num_seqs, int max_q_len, int Hkv) {
   if (version >= 0x100) {
-    const int var = version & 0xff;
-    if (var == 128) return 128;
+    const int var = version - 0x100;
+    if (var == 128 || var == 256) return var;
     return !fp8 && G == 4 ? var : kPf3DefaultVar;
   }
-  return blocks <= pf3_split_blocks(D) ? 128 : kPf3DefaultVar;
+  const int BQ = pf3_threads(0) / 2 / G, ntl = (max_q_len + BQ - 1) / BQ;
+  const long pairs = static_cast<long>(num_seqs) * Hkv;
+  if (pairs * ntl <= pf3_split_blocks(D)) return 128;
+  static const int pair_on = pf3_env("MXS_PF_PAIR", 1);
+  if (pair_on && pairs * ((ntl + 1) / 2) >= (D == 64 ? 512 : 256)) return 256;
+  return kPf3DefaultVar;
 }
 static long pf3_blocks(int num_seqs, int max_q_len, int Hkv, int G) {
   const int BQ = pf3_threads(0) / 2 / G;
@@ -915,6 +956,10 @@ static void pf3_dispatch(int var, bool fp8, bf16_t* out, const bf16_t* q, const 
   if (var == 128 && split_ws != nullptr && split_cnt != nullptr) {
     if (fp8) return pf3_launch<D, G, 1, 128>(MXS_PF3_ARGS);
     return pf3_launch<D, G, 2, 128>(MXS_PF3_ARGS);
+  }
+  if (var == 256) {
+    if (fp8) return pf3_launch<D, G, 1, 256>(MXS_PF3_ARGS);
+    return pf3_launch<D, G, 2, 256>(MXS_PF3_ARGS);
   }
   if (fp8) return pf3_launch<D, G, 1, (kPf3DefaultVar & ~128)>(MXS_PF3_ARGS);
   if constexpr (G == 4) {  // the other variants: G = 4 only (A/B probes and tests)
@@ -950,14 +995,14 @@ void paged_prefill_split_need(int version, bool kv_fp8, int num_seqs, int max_q_
   const int G = Hq / Hkv;
   const long items = pf3_blocks(num_seqs, max_q_len, Hkv, G);
   if (version == 2 && !kv_fp8) return;  // v2 unless the launch needs v3 (fused q): not split either way
-  if (pf3_effective_var(version, kv_fp8, G, D, items) != 128) return;
+  if (pf3_effective_var(version, kv_fp8, G, D, num_seqs, max_q_len, Hkv) != 128) return;
   *counters = items;
   *ws_bytes = items * (D == 64 ? pf3_split_item_bytes(64, 128) : pf3_split_item_bytes(128, 128));
 }
 
 // q_stride: elements between consecutive q rows (Hq * D for a dense q; (Hq + 2 Hkv) * D when q is
 // read from the fused qkv output); cos_sin != nullptr applies RoPE at positions qpos (v3 only).
-// version 0x100 | VAR selects a v3 softmax variant explicitly (probes, tests).
+// version 0x100 + VAR selects a v3 variant explicitly (probes, tests).
 void launch_paged_prefill(bf16_t* out, const bf16_t* q, const void* kv_ptr, bool kv_fp8, long block_stride,
                           const int* block_tables, int bt_stride, const int* qsl, const int* seq_lens,
                           int num_seqs, int max_q_len, int Hq, int Hkv, int D, float scale, int version,
@@ -969,7 +1014,7 @@ void launch_paged_prefill(bf16_t* out, const bf16_t* q, const void* kv_ptr, bool
   if (q_stride <= 0) q_stride = Hq * D;
   if (version != 2 || kv_fp8 || cos_sin != nullptr || q_stride != Hq * D) {  // fp8 / fused q: the v3 path only
     const float sc = kv_fp8 ? scale * k_scale : scale, vs = kv_fp8 ? v_scale : 1.f;
-    const int var = pf3_effective_var(version, kv_fp8, G, D, pf3_blocks(num_seqs, max_q_len, Hkv, G));
+    const int var = pf3_effective_var(version, kv_fp8, G, D, num_seqs, max_q_len, Hkv);
 #define MXS_PF3(DD, GG)                                                                                     \
     if (D == DD && G == GG) {                                                                               \
       pf3_dispatch<DD, GG>(var, kv_fp8, out, q, kv_ptr, block_stride, block_tables, bt_stride, qsl, seq_lens, \

@@ -37,7 +37,7 @@ def main():
         ref_out, times = None, {v: [] for v in variants}
         for rnd in range(3):
             for v in variants:
-                ver = 0 if v is None else (3 if v < 0 else 0x100 | v)  # -1: the default launch (split gate)
+                ver = 0 if v is None else (3 if v < 0 else 0x100 + v)  # -1: the default launch (split gate)
                 fn = lambda: ops.paged_attention_prefill(q, kv, bt, qsl, sl, D ** -0.5, per, version=ver)  # noqa: E731
                 for _ in range(3):
                     out = fn()

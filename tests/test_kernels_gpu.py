@@ -203,7 +203,7 @@ def test_prefill_softmax_rescale_spike(gpu, version):
 
 # v3 softmax variants (attention_prefill.hip VAR bits: 1 biased reference + overflow redo, 2 row sum
 # on the matrix pipe, 4 persistent -m accumulator block), launched as version 0x100 | VAR at G = 4
-@pytest.mark.parametrize("var", [0, 1, 2, 4, 6, 7, 8, 10, 12, 14, 16, 32, 36, 64, 66, 128])
+@pytest.mark.parametrize("var", [0, 1, 2, 4, 6, 7, 8, 10, 12, 14, 16, 32, 36, 64, 66, 128, 256])
 @pytest.mark.parametrize("D", [64, 128])
 def test_paged_prefill_softmax_variants(gpu, D, var):
     G, hkv = 4, 2
@@ -216,16 +216,17 @@ def test_paged_prefill_softmax_variants(gpu, D, var):
     q = torch.randn(qsl[-1], hkv * G, D, device=gpu, dtype=torch.bfloat16)
     qsl_t, sl = torch.tensor(qsl, dtype=torch.int32), torch.tensor(seq_lens, dtype=torch.int32)
     out = ops.paged_attention_prefill(q, kv[:, 1], bt.to(gpu), qsl_t.to(gpu), sl.to(gpu), 1 / math.sqrt(D),
-                                      max(n for _, n in specs), version=0x100 | var)
+                                      max(n for _, n in specs), version=0x100 + var)
     exp = ref.paged_attention(q.cpu(), kv[:, 1].cpu(), bt, qsl_t, sl, 1 / math.sqrt(D))
     _close(out, exp, 0.03, 0.03, f"prefill var {var}")
 
 
-@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("var,fp8", [(128, False), (128, True), (256, False)])
 @pytest.mark.parametrize("D,G", [(64, 4), (128, 4), (64, 1), (128, 8)])
-def test_paged_prefill_split(gpu, D, G, fp8):
-    """VAR 128: q-tiles with >= 24 key tiles run as two workgroups over the two halves of their key
-    range, merged by the second to finish.  Long prompts, a prefix-cache hit, a short chunk over a long
+def test_paged_prefill_split(gpu, D, G, var, fp8):
+    """VAR 128: q-tiles with >= 8 key tiles run as two workgroups over the two halves of their key
+    range, merged by the second to finish.  VAR 256: each workgroup runs a heavy and a light q-tile of
+    its sequence.  Long prompts, a prefix-cache hit, a short chunk over a long
     context and a short prompt (unsplit) in one launch; launched three times, the output must not change
     (the tile counters are never reset: the ticket parity names the merging half)."""
     hkv = 2
@@ -241,10 +242,10 @@ def test_paged_prefill_split(gpu, D, G, fp8):
     qsl_t, sl = torch.tensor(qsl, dtype=torch.int32), torch.tensor(seq_lens, dtype=torch.int32)
     scale = 1 / math.sqrt(D)
     outs = [ops.paged_attention_prefill(q, cache[:, 1], bt.to(gpu), qsl_t.to(gpu), sl.to(gpu), scale,
-                                        max(n for _, n in specs), version=0x100 | 128, k_scale=ks, v_scale=vs)
+                                        max(n for _, n in specs), version=0x100 + var, k_scale=ks, v_scale=vs)
             for _ in range(3)]
     exp = ref.paged_attention(q.cpu(), cache[:, 1].cpu(), bt, qsl_t, sl, scale, ks, vs)
-    _close(outs[0], exp, 0.03, 0.03, f"prefill split D{D} G{G} fp8={fp8}")
+    _close(outs[0], exp, 0.03, 0.03, f"prefill var {var} D{D} G{G} fp8={fp8}")
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
     base = ops.paged_attention_prefill(q, cache[:, 1], bt.to(gpu), qsl_t.to(gpu), sl.to(gpu), scale,
                                        max(n for _, n in specs), version=0x100, k_scale=ks, v_scale=vs)
