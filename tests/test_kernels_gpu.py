@@ -1031,12 +1031,14 @@ def test_paged_decode_fused_rope(gpu, D, G, kv_fp8):
     _close(out, exp, 0.02 * max(1.0, exp.abs().max().item()), 0.02, "decode fused rope")
 
 
+@pytest.mark.parametrize("var", [None, 128, 256])
 @pytest.mark.parametrize("D,G", [(64, 4), (128, 4), (128, 8)])
-def test_paged_prefill_fused_rope(gpu, D, G):
-    """Prefill v3 attention reading un-rotated q from the qkv rows (RoPE applied in the kernel)."""
+def test_paged_prefill_fused_rope(gpu, D, G, var):
+    """Prefill v3 attention reading un-rotated q from the qkv rows (RoPE applied in the kernel); with
+    long prompts the split-KV (128) and paired-tile (256) variants too."""
     hkv = 2
     hq = hkv * G
-    specs = [(0, 77), (300, 45), (16, 1), (0, 130), (33, 200)]
+    specs = [(0, 77), (300, 45), (16, 1), (0, 130), (33, 200)] if var is None else [(0, 1500), (1200, 700), (16, 1)]
     seq_lens = [c + n for c, n in specs]
     kv, bt = _paged_setup(seq_lens, hkv, D, device=gpu)
     qsl = [0]
@@ -1050,7 +1052,8 @@ def test_paged_prefill_fused_rope(gpu, D, G):
     sl = torch.tensor(seq_lens, dtype=torch.int32)
     scale = 1 / math.sqrt(D)
     out = ops.paged_attention_prefill(q, kv[:, 1], bt.to(gpu), qsl_t.to(gpu), sl.to(gpu), scale,
-                                      max(n for _, n in specs), rope=(pos, cos_sin))
+                                      max(n for _, n in specs), rope=(pos, cos_sin),
+                                      version=0 if var is None else 0x100 + var)
     q_rot = ref.apply_rope(q.cpu().float(), pos.cpu(), cos_sin.cpu()).to(torch.bfloat16)
     exp = ref.paged_attention(q_rot, kv[:, 1].cpu(), bt, qsl_t, sl, scale)
     _close(out, exp, 0.03, 0.03, "prefill fused rope")
