@@ -81,8 +81,45 @@ def main():
             main_s.wait_stream(side)
             return torch.cat([a, b])
 
+        # the decode rows' forward replayed from a hipGraph (as the engine's decode steps run)
+        g = None
+        if os.environ.get("MS_GRAPH", "1") == "1":
+            with torch.inference_mode():
+                for _ in range(2):
+                    m.compute_logits(m.forward(ids[:B], md_d, kv))
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    glog = m.compute_logits(m.forward(ids[:B], md_d, kv))
+
+        def split_seq_graph():
+            g.replay()
+            b = m.compute_logits(m.forward(ids[B:], md_p, kv))
+            return torch.cat([glog, b])
+
+        def split_par_graph():
+            side.wait_stream(main_s)
+            with torch.cuda.stream(side):
+                b = m.compute_logits(m.forward(ids[B:], md_p, kv))
+            g.replay()
+            main_s.wait_stream(side)
+            return torch.cat([glog, b])
+
+        def split_par_graph_rev():  # decode graph on the side stream, prefill on the main one
+            side.wait_stream(main_s)
+            with torch.cuda.stream(side):
+                g.replay()
+            b = m.compute_logits(m.forward(ids[B:], md_p, kv))
+            main_s.wait_stream(side)
+            return torch.cat([glog, b])
+
         modes = {"combined": (combined, 0), "combined_attn_overlap": (combined, 1), "split_sequential": (split_seq, 0),
                  "split_parallel": (split_par, 0)}
+        if g is not None:
+            modes.update({"split_seq_graph": (split_seq_graph, 0), "split_par_graph": (split_par_graph, 0),
+                          "split_par_graph_rev": (split_par_graph_rev, 0)})
+        if os.environ.get("MS_MODES"):  # e.g. "combined_attn_overlap" under rocprofv3
+            modes = {k: v for k, v in modes.items() if k in os.environ["MS_MODES"].split(",")}
         times = {k: [] for k in modes}
         outs = {}
         with torch.inference_mode():
@@ -100,9 +137,10 @@ def main():
                     torch.cuda.synchronize()
                     times[name].append(e0.elapsed_time(e1) / 5)
         r = {k: round(sorted(v)[len(v) // 2], 3) for k, v in times.items()}
-        diff = {k: round((outs[k].float() - outs["combined"].float()).abs().max().item(), 4) for k in outs}
+        base = outs.get("combined", next(iter(outs.values())))
+        diff = {k: round((outs[k].float() - base.float()).abs().max().item(), 4) for k in outs}
         print(json.dumps({"B": B, "ctx": ctx, "chunk": chunk, "prefix": prefix, "ms": r,
-                          "gain_vs_combined": {k: round(r["combined"] / v, 3) for k, v in r.items()},
+                          "gain_vs_combined": {k: round(r.get("combined", v) / v, 3) for k, v in r.items()},
                           "logits_max_diff": diff}), flush=True)
         del kv
 
