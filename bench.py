@@ -682,6 +682,26 @@ def run_disagg_prefill(eng, temperature: float, barrier, conns: list) -> int:
         targets.append(target)
         arenas.append(arena)
     vlog(f"prefill rank serving {len(conns)} decode rank(s) (mapped={arenas})")
+    # results go out through one sender thread per channel: a host-staged KV payload can exceed the
+    # socket buffer, and a blocking send here while the decode rank sits in a phase barrier would
+    # keep this loop from ever reading the phase message that joins that barrier (a deadlock)
+    import queue
+    import threading
+    outq = [queue.Queue() for _ in conns]
+
+    def sender(ci: int) -> None:
+        while True:
+            msg = outq[ci].get()
+            if msg is None:
+                return
+            try:
+                conns[ci].send(msg)
+            except (OSError, EOFError):  # the decode rank closed its end after the last barrier
+                return
+    senders = [threading.Thread(target=sender, args=(ci,), name=f"disagg-send-{ci}", daemon=True)
+               for ci in range(len(conns))]
+    for t in senders:
+        t.start()
     pending: dict = {}
     announced: dict = {}
     moved = 0
@@ -702,6 +722,10 @@ def run_disagg_prefill(eng, temperature: float, barrier, conns: list) -> int:
                                 request_id=rid, disagg_role="prefill_only")
                 pending[rid] = (ci, dst, skip, start, shm_start)
         if stop:
+            for q in outq:
+                q.put(None)
+            for t in senders:
+                t.join(timeout=10)
             agent.close()
             return moved
         if not eng.has_unfinished():
@@ -722,7 +746,7 @@ def run_disagg_prefill(eng, temperature: float, barrier, conns: list) -> int:
                 data = agent.read_blocks(src)
             moved += len(src)
             eng.release_prefill_blocks(o.request_id)
-            conns[ci].send(("done", o.request_id, o.token_id, data))
+            outq[ci].put(("done", o.request_id, o.token_id, data))
 
 
 # ---------------------------------------------------------------------------- phases

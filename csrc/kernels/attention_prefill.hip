@@ -941,6 +941,13 @@ static int pf3_effective_var(int version, bool fp8, int G, int D, int num_seqs, 
   if (pair_on && pairs * ((ntl + 1) / 2) >= (D == 64 ? 512 : 256)) return 256;
   return kPf3DefaultVar;
 }
+// the v3 variant a launch would run (host only: the selection of pf3_effective_var, for tests and logs);
+// -1 when the launch takes the v2 kernel
+int paged_prefill_variant(int version, bool kv_fp8, bool fused_q, int num_seqs, int max_q_len, int Hq, int Hkv,
+                          int D) {
+  if (version == 2 && !kv_fp8 && !fused_q) return -1;
+  return pf3_effective_var(version, kv_fp8, Hq / Hkv, D, num_seqs, max_q_len, Hkv);
+}
 static long pf3_blocks(int num_seqs, int max_q_len, int Hkv, int G) {
   const int BQ = pf3_threads(0) / 2 / G;
   return static_cast<long>(num_seqs) * Hkv * ((max_q_len + BQ - 1) / BQ);

@@ -26,6 +26,7 @@ void launch_paged_prefill(bf16_t*, const bf16_t*, const void*, bool, long, const
                           int, int, int, int, int, float, int, float, float, hipStream_t, int = 0,
                           const int64_t* = nullptr, const float* = nullptr, char* = nullptr, int* = nullptr);
 void paged_prefill_split_need(int, bool, int, int, int, int, int, long*, long*);
+int paged_prefill_variant(int, bool, bool, int, int, int, int, int);
 void launch_sample(int64_t*, const void*, bool, int, int, long, const float*, const float*, const int*,
                    const int64_t*, const int64_t*, hipStream_t);
 void launch_logprobs(float*, int64_t*, float*, const void*, bool, int, int, long, const int64_t*, const int64_t*, int,
@@ -576,6 +577,10 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("max_seq_len"), pybind11::arg("k_scale") = 1.0, pybind11::arg("v_scale") = 1.0,
         pybind11::arg("impl") = 0, pybind11::arg("rope_pos") = pybind11::none(),
         pybind11::arg("cos_sin") = pybind11::none());
+  m.def("paged_prefill_variant", &mxs::paged_prefill_variant, pybind11::arg("version"), pybind11::arg("kv_fp8"),
+        pybind11::arg("fused_q"), pybind11::arg("num_seqs"), pybind11::arg("max_q_len"), pybind11::arg("hq"),
+        pybind11::arg("hkv"), pybind11::arg("head_dim"),
+        "prefill attention v3 variant a launch picks (0 default, 128 split-KV, 256 paired tiles; -1: v2)");
   m.def("paged_attention_prefill", &paged_attention_prefill, pybind11::arg("out"), pybind11::arg("q"),
         pybind11::arg("kv"), pybind11::arg("block_tables"), pybind11::arg("qsl"), pybind11::arg("seq_lens"),
         pybind11::arg("scale"), pybind11::arg("max_q_len"), pybind11::arg("version") = 3,
