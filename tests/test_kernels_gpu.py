@@ -1273,3 +1273,59 @@ def test_skinny_gemm_swiglu(gpu, M, N, K):
             decode_gemm.TABLE.part = None
             assert decode_gemm.TABLE.run(out, x, w, cfg, 1), cfg
             _close(out, want, atol=2e-2, rtol=2e-2, name=f"TABLE.run {cfg}")
+
+
+def _gather_seq_kv(kv_layer, bt_row, L):
+    """K, V [L, hkv, D] in fp32 from a paged layer (V blocks are dim-major: ref.gather_kv), on the GPU."""
+    k, v = ref.gather_kv(kv_layer, bt_row, L)
+    return k.float(), v.float()
+
+
+def _attn_fp32(q, k, v, qpos, scale):
+    """Causal GQA attention in fp32 on the GPU: q [T, Hq, D] at positions qpos over k / v [L, Hkv, D]."""
+    T, Hq, D = q.shape
+    G = Hq // k.shape[1]
+    kk = k.repeat_interleave(G, dim=1).permute(1, 2, 0)  # [Hq, D, L]
+    vv = v.repeat_interleave(G, dim=1).permute(1, 0, 2)  # [Hq, L, D]
+    s = torch.bmm(q.float().permute(1, 0, 2), kk) * scale  # [Hq, T, L]
+    keys = torch.arange(k.shape[0], device=q.device)
+    s = s.masked_fill(keys[None, None, :] > qpos[None, :, None], float("-inf"))
+    return torch.bmm(torch.softmax(s, dim=-1), vv).permute(1, 0, 2)  # [T, Hq, D]
+
+
+@pytest.mark.parametrize("var", [None, 128, 256])
+def test_paged_prefill_long_context(gpu, var):
+    """A 1024-token chunk after 64,000 cached tokens (chunked prefill at long context) next to a fresh
+    3,000-token prompt, every launch form, against fp32 attention over the gathered cache."""
+    D, G, hkv = 64, 4, 2
+    specs = [(64000, 1024), (0, 3000)]
+    seq_lens = [c + n for c, n in specs]
+    kv, bt = _paged_setup(seq_lens, hkv, D, L=1, device=gpu)
+    qsl = [0]
+    for _, n in specs:
+        qsl.append(qsl[-1] + n)
+    q = torch.randn(qsl[-1], hkv * G, D, device=gpu, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    out = ops.paged_attention_prefill(q, kv[:, 0], bt.to(gpu), torch.tensor(qsl, dtype=torch.int32, device=gpu),
+                                      torch.tensor(seq_lens, dtype=torch.int32, device=gpu), scale,
+                                      max(n for _, n in specs), version=0 if var is None else 0x100 + var)
+    for i, (c, n) in enumerate(specs):
+        k, v = _gather_seq_kv(kv[:, 0], bt[i].to(gpu), c + n)
+        exp = _attn_fp32(q[qsl[i]:qsl[i + 1]], k, v, torch.arange(c, c + n, device=gpu), scale)
+        _close(out[qsl[i]:qsl[i + 1]], exp, 0.03, 0.03, f"long-context prefill seq {i} var {var}")
+
+
+def test_paged_decode_long_context(gpu):
+    """Decode rows at 131,072 / 70,001 / 17 tokens of context (split-KV partitions + merge) against fp32
+    attention over the gathered cache."""
+    D, G, hkv = 64, 4, 2
+    lens = [131072, 70001, 17]
+    kv, bt = _paged_setup(lens, hkv, D, L=1, device=gpu)
+    q = torch.randn(len(lens), hkv * G, D, device=gpu, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    out = ops.paged_attention_decode(q, kv[:, 0], bt.to(gpu), torch.tensor(lens, dtype=torch.int32, device=gpu),
+                                     scale, max(lens))
+    for i, L in enumerate(lens):
+        k, v = _gather_seq_kv(kv[:, 0], bt[i].to(gpu), L)
+        exp = _attn_fp32(q[i:i + 1], k, v, torch.tensor([L - 1], device=gpu), scale)
+        _close(out[i:i + 1], exp, 0.02, 0.02, f"long-context decode L={L}")
