@@ -7,6 +7,7 @@
 #include <map>
 #include <mutex>
 #include <optional>
+#include <vector>
 
 namespace mxs {
 typedef unsigned short bf16_t;
@@ -256,10 +257,14 @@ void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Te
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     TORCH_CHECK(hipStreamIsCapturing(stream(), &cap) == hipSuccess, "hipStreamIsCapturing");
     if (!c.defined() || c.numel() < ncnt) {
-      if (cap == hipStreamCaptureStatusNone)
+      if (cap == hipStreamCaptureStatusNone) {
+        // a grown table's predecessor stays allocated: a launch on another stream may still use it
+        static std::vector<at::Tensor> retired;
+        if (c.defined()) retired.push_back(c);
         c = at::zeros({std::max<long>(ncnt, 1L << 14)}, q.options().dtype(at::kInt));
-      else
+      } else {
         ws_bytes = 0;  // no counters outside a graph's pool: run this launch unsplit
+      }
     }
     if (ws_bytes > 0) {
       cnt = c.data_ptr<int>();
