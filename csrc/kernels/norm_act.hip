@@ -3,6 +3,7 @@
 // Memory-bound: every access is a 16-byte bf16x8 vector (cdna_hip_programming.md Guideline 13),
 // the row stays in registers between the reduction and the scaled write (one HBM pass).
 #include "common.h"
+#include <cstdlib>
 
 namespace mxs {
 
@@ -65,10 +66,93 @@ __global__ void __launch_bounds__(1024) rmsnorm_kernel(bf16_t* __restrict__ out,
   }
 }
 
+// One WAVE per row (4 rows per 256-thread workgroup) for H = 512 NVW: lane l holds vectors l + 64 i,
+// so every load / store instruction of a wave moves 1 KiB contiguous, and the sum of squares is a
+// wave reduction (no LDS, no barrier).  The workgroup-per-row form above spends a block reduction and
+// a barrier on each 4 KiB row at H = 2048; at prefill row counts it reads and writes at ~4.5 TB/s.
+template <int NVW, bool ADD>
+__global__ void __launch_bounds__(256) rmsnorm_rows_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ x,
+                                                          bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
+                                                          int rows, int H, int x_stride, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;  // wave-uniform: no barrier below
+  const bf16_t* xr = x + static_cast<int64_t>(row) * x_stride;
+  bf16_t* rr = ADD ? residual + static_cast<size_t>(row) * H : nullptr;
+  // every load of the row (x, the residual, the weight) issued before the first use: one latency
+  uint4 v[NVW], rv[ADD ? NVW : 1], wv[NVW];
+#pragma unroll
+  for (int i = 0; i < NVW; ++i) {
+    v[i] = *reinterpret_cast<const uint4*>(xr + (lane + 64 * i) * 8);
+    if constexpr (ADD) rv[i] = *reinterpret_cast<const uint4*>(rr + (lane + 64 * i) * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < NVW; ++i) wv[i] = *reinterpret_cast<const uint4*>(w + (lane + 64 * i) * 8);
+  if constexpr (ADD) {
+#pragma unroll
+    for (int i = 0; i < NVW; ++i) {
+      uint32_t* pa = reinterpret_cast<uint32_t*>(&v[i]);
+      const uint32_t* pb = reinterpret_cast<const uint32_t*>(&rv[i]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        pa[k] = pack2(bf2f_lo(pa[k]) + bf2f_lo(pb[k]), bf2f_hi(pa[k]) + bf2f_hi(pb[k]));
+      *reinterpret_cast<uint4*>(rr + (lane + 64 * i) * 8) = v[i];
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NVW; ++i) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(&v[i]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float lo = bf2f_lo(p[k]), hi = bf2f_hi(p[k]);
+      ss += lo * lo + hi * hi;
+    }
+  }
+  const float inv = rsqrtf(wave_sum(ss) / static_cast<float>(H) + eps);
+  bf16_t* orow = out + static_cast<size_t>(row) * H;
+#pragma unroll
+  for (int i = 0; i < NVW; ++i) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(&v[i]);
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(&wv[i]);
+    uint4 o;
+    uint32_t* po = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      po[k] = pack2(bf2f_lo(p[k]) * inv * bf2f_lo(pw[k]), bf2f_hi(p[k]) * inv * bf2f_hi(pw[k]));
+    *reinterpret_cast<uint4*>(orow + (lane + 64 * i) * 8) = o;
+  }
+}
+
 template <bool ADD, bool EMBED = false>
 static void launch_rmsnorm_t(bf16_t* out, const bf16_t* x, bf16_t* res, const bf16_t* w, int rows, int H,
                              int x_stride, float eps, hipStream_t s, const int64_t* ids = nullptr) {
   if (rows == 0) return;
+  if constexpr (!EMBED) {
+    const int nvw = H % 512 == 0 ? H / 512 : 0;  // vectors per lane of the wave-per-row form
+    static const bool block_only = [] {  // MXS_RMS_BLOCK=1: the workgroup-per-row form (A/B only)
+      const char* e = std::getenv("MXS_RMS_BLOCK");
+      return e != nullptr && e[0] == '1';
+    }();
+    // the workgroup-per-row form has the lower latency for decode-sized row counts; the wave form
+    // moves more bytes per second from ~2k rows (4k with the residual add): 6,144 x 2,048 plain
+    // 11.2 -> 9.6 us, 8,192 14.1 -> 11.4 us (scripts/probes/rmsnorm_probe.py)
+    const bool wave_form = !block_only && rows >= (ADD ? 4096 : 2048) &&
+                           ((nvw >= 1 && nvw <= 8) || nvw == 10 || nvw == 12 || nvw == 14 || nvw == 16);
+    if (wave_form && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && x_stride % 8 == 0) {
+      dim3 g((rows + 3) / 4), b(256);
+#define MXS_RMSW(NV) \
+  case NV:           \
+    hipLaunchKernelGGL((rmsnorm_rows_kernel<NV, ADD>), g, b, 0, s, out, x, res, w, rows, H, x_stride, eps); break;
+      switch (nvw) {
+        MXS_RMSW(1) MXS_RMSW(2) MXS_RMSW(3) MXS_RMSW(4) MXS_RMSW(5) MXS_RMSW(6) MXS_RMSW(7) MXS_RMSW(8)
+        MXS_RMSW(10) MXS_RMSW(12) MXS_RMSW(14) MXS_RMSW(16)
+        default: break;
+      }
+#undef MXS_RMSW
+      MXS_CHECK_LAUNCH();
+      return;
+    }
+  }
   const int nvec = H / 8;
   // one bf16x8 per thread up to H = 8192 (1024 threads); wider rows keep NV vectors per thread
   const int threads = nvec <= 1024 ? ((nvec + 63) / 64) * 64 : 1024;

@@ -19,16 +19,16 @@ def _close(a, b, atol, rtol=0.0, name=""):
 
 
 @pytest.mark.parametrize("H", [1024, 2048, 4096, 8192])
-@pytest.mark.parametrize("T", [1, 7, 128])
+@pytest.mark.parametrize("T", [1, 7, 128, 2050])  # 2050: the wave-per-row form
 def test_rms_norm(gpu, H, T):
     x = torch.randn(T, H, device=gpu, dtype=torch.bfloat16)
     w = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16()
     _close(ops.rms_norm(x, w, 1e-5), ref.rms_norm(x.cpu(), w.cpu(), 1e-5), 0.02, 0.02, "rms_norm")
 
 
+@pytest.mark.parametrize("T", [33, 4099])  # 4099: the wave-per-row form
 @pytest.mark.parametrize("H", [2048, 4096])
-def test_fused_add_rms_norm(gpu, H):
-    T = 33
+def test_fused_add_rms_norm(gpu, H, T):
     x = torch.randn(T, H, device=gpu, dtype=torch.bfloat16)
     r = torch.randn(T, H, device=gpu, dtype=torch.bfloat16)
     w = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16()
