@@ -13,7 +13,7 @@ from mxserve import ops  # noqa: E402
 dev = torch.device("cuda:0")
 torch.manual_seed(0)
 D, G, Hkv = 64, 4, 8
-for B in (256, 288, 320, 384, 448):
+for B in [int(b) for b in os.environ.get("DP_BATCHES", "256,288,320,384,448").split(",")]:
     lens = torch.randint(4000, 4501, (B,), dtype=torch.int32)
     nb = [(int(l) + 15) // 16 for l in lens]
     mb = max(nb)
