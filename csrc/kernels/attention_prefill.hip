@@ -337,6 +337,10 @@ constexpr int pf3_threads(int VAR) { return (VAR & 8) ? 256 : 512; }
 //      the ticket parity names the last arriver.  The default launch picks it when the unsplit grid is
 //      under ~1.25 waves of resident workgroups (pf3_split_blocks): 1 x 1024 1.29x, 1 x 2048 1.19x,
 //      1 x 4096 1.07x at D = 64 (profiles/r5/prefill_attn/split/).
+// 1024 the row sum on a 16x16x32 MFMA fed the bf16 P^T fragments (4 MFMAs instead of 33 adds a
+//      tile; a lane-group swap at the end): correct, but at D = 64 its 4-register accumulator spills
+//      12 VGPRs of the 128 budget and it runs 4-11 % slower; at D = 128 equal (not adopted,
+//      profiles/r5/prefill_attn/ms16_row_sum_not_adopted.jsonl).
 // 256  paired q-tiles (causal load balance at two waves and up): workgroup s of a sequence's n tiles
 //      runs tile n - 1 - s and then tile s, n + 1 key tiles each, half the workgroups; picked when the
 //      paired grid fills the resident workgroups at least once: 8 x 1024 1.21x, 4 x 2048 1.11x,
@@ -523,7 +527,7 @@ __device__ __forceinline__ void pf3_tile(
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
   float m = -INFINITY, l = 0.f;
-  constexpr bool ORCHK = VAR & 1, MSUM = VAR & 2, CBLK = VAR & 4;
+  constexpr bool ORCHK = VAR & 1, MSUM = VAR & 2, CBLK = VAR & 4, MS16 = VAR & 1024;
   constexpr float kBias = 64.f;
   float16_ negm, lsum;  // CBLK: -m in every element; MSUM: the row sum (every element holds it)
   bf16x8_t ones;
@@ -531,6 +535,13 @@ __device__ __forceinline__ void pf3_tile(
   for (int i = 0; i < 16; ++i) negm[i] = lsum[i] = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = static_cast<__bf16>(1.f);
+  // MS16: the row sum on a 16x16x32 MFMA fed the P^T fragments as its B operand.  That MFMA reads
+  // lane l's 8 values as keys 8 (l >> 4) .. + 7 of column l & 15, i.e. query 16 ((l >> 4) & 1) + (l & 15)
+  // and key half l >> 5 of ours; an A row m selecting k-groups of parity (m >= 8) sums both key
+  // halves of query (l & 15) + 16 (m >= 8): 4 MFMAs a tile instead of 33 adds.  Lane l then holds
+  // the sum of query (l & 15) + 16 (l >= 32) in all four accumulator elements.
+  // (the selector and the lane's query are rebuilt where used: kept live they spill at D = 64)
+  float4_ lsum4 = {0.f, 0.f, 0.f, 0.f};
 
   // Scores are accumulated relative to the reference m: the QK^T accumulator starts at -m, so exp2
   // reads the MFMA output directly and the per-element subtraction is gone from the VALU stream (at
@@ -614,6 +625,9 @@ __device__ __forceinline__ void pf3_tile(
       if constexpr (MSUM) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) lsum[i] *= alpha;
+      } else if constexpr (MS16) {
+        // the factor of the query this lane sums, (lane & 15) + 16 (lane >= 32); both halves hold it
+        lsum4 *= __shfl(alpha, (lane & 15) + ((lane >> 1) & 16), 64);
       } else {
         l *= alpha;
       }
@@ -640,7 +654,7 @@ __device__ __forceinline__ void pf3_tile(
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float p = __builtin_amdgcn_exp2f(sacc[kt][i]);
-        if constexpr (!MSUM) ps += p;
+        if constexpr (!MSUM && !MS16) ps += p;
         pf[kt][i >> 3][i & 7] = static_cast<__bf16>(p);
       }
     return ps;
@@ -694,6 +708,14 @@ __device__ __forceinline__ void pf3_tile(
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) lsum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[kt][s2], lsum, 0, 0, 0);
+    } else if constexpr (MS16) {
+      // A row m takes the k-groups of parity (m >= 8): one dword pattern per lane, all ones or zero
+      const uint32_t w1 = (((lane >> 4) ^ (lane >> 3)) & 1) ? 0u : 0x3F803F80u;
+      const bf16x8_t sel = as_bf16x8(make_uint4(w1, w1, w1, w1));
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) lsum4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf[kt][s2], lsum4, 0, 0, 0);
     } else {
       l += ps;
     }
@@ -765,10 +787,15 @@ __device__ __forceinline__ void pf3_tile(
     }
   }
 
-  if constexpr (MSUM)
+  if constexpr (MSUM) {
     l = lsum[0];  // ones^T . P^T summed both half-waves' keys already
-  else
+  } else if constexpr (MS16) {
+    // lanes 16-31 hold queries 0-15 and lanes 32-47 queries 16-31: swap those two groups
+    const int src = (lane >= 16 && lane < 32) ? lane + 16 : (lane >= 32 && lane < 48) ? lane - 16 : lane;
+    l = __shfl(lsum4[0], src, 64);
+  } else {
     l += __shfl_xor(l, 32, 64);
+  }
   if constexpr (SPLIT) {
     if (split) {
       // this half's partial: O / l rounded to bf16 (16 words per lane), then (m, l); a lane's 72 bytes
@@ -985,6 +1012,8 @@ static void pf3_dispatch(int var, bool fp8, bf16_t* out, const bf16_t* q, const 
       case 36: return pf3_launch<D, G, 2, 36>(MXS_PF3_ARGS);
       case 64: return pf3_launch<D, G, 2, 64>(MXS_PF3_ARGS);
       case 66: return pf3_launch<D, G, 2, 66>(MXS_PF3_ARGS);
+      case 1024: return pf3_launch<D, G, 2, 1024>(MXS_PF3_ARGS);
+      case 1280: return pf3_launch<D, G, 2, 1280>(MXS_PF3_ARGS);
       default: break;
     }
   }

@@ -203,7 +203,7 @@ def test_prefill_softmax_rescale_spike(gpu, version):
 
 # v3 softmax variants (attention_prefill.hip VAR bits: 1 biased reference + overflow redo, 2 row sum
 # on the matrix pipe, 4 persistent -m accumulator block), launched as version 0x100 | VAR at G = 4
-@pytest.mark.parametrize("var", [0, 1, 2, 4, 6, 7, 8, 10, 12, 14, 16, 32, 36, 64, 66, 128, 256])
+@pytest.mark.parametrize("var", [0, 1, 2, 4, 6, 7, 8, 10, 12, 14, 16, 32, 36, 64, 66, 128, 256, 1024, 1280])
 @pytest.mark.parametrize("D", [64, 128])
 def test_paged_prefill_softmax_variants(gpu, D, var):
     G, hkv = 4, 2
