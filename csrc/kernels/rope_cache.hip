@@ -317,27 +317,29 @@ __global__ void __launch_bounds__(256) kv_rope_t16_kernel(
     KT* __restrict__ kv, long block_stride, const int64_t* __restrict__ slot_mapping, int Hq, int Hkv, int BS, int T,
     float k_inv_scale, float v_inv_scale) {
   constexpr int HALF = D / 2, CH = HALF / 8, TPB = 16;
-  extern __shared__ __attribute__((aligned(16))) bf16_t vstage[];  // [TPB][Hkv * D]
+  extern __shared__ __attribute__((aligned(16))) bf16_t vstage[];  // [TPB][hpw * D]
   __shared__ unsigned s_runs;       // bit k: token k starts a run
   __shared__ int64_t s_slot[TPB];
+  // blockIdx.y: a group of hpw kv heads (gridDim.y groups), so short chunks still fill the chip
+  const int hpw = Hkv / gridDim.y, h0 = blockIdx.y * hpw;
   const int t0 = blockIdx.x * TPB, nt = min(TPB, T - t0), tid = threadIdx.x;
-  const int row_stride = (Hq + 2 * Hkv) * D, hkd = Hkv * D;
-  const int n_k = nt * Hkv * CH, n_v = nt * (hkd / 8);
+  const int row_stride = (Hq + 2 * Hkv) * D, hkd = hpw * D;
+  const int n_k = nt * hpw * CH, n_v = nt * (hkd / 8);
   const bf16_t* tile = qkv + static_cast<size_t>(t0) * row_stride;
   // V rows into registers (independent of everything else)
   uint4 vr[NV];
 #pragma unroll
   for (int u = 0; u < NV; ++u) {
     const int i = min(tid + 256 * u, n_v - 1), tt = i / (hkd / 8), j = (i - tt * (hkd / 8)) * 8;
-    vr[u] = *reinterpret_cast<const uint4*>(tile + static_cast<size_t>(tt) * row_stride + (Hq + Hkv) * D + j);
+    vr[u] = *reinterpret_cast<const uint4*>(tile + static_cast<size_t>(tt) * row_stride + (Hq + Hkv + h0) * D + j);
   }
   // K chunks: both halves of 8 pairs, and the token's position / slot
   uint4 ka[NI], kb[NI];
   int64_t pos[NI], slot[NI];
 #pragma unroll
   for (int u = 0; u < NI; ++u) {
-    const int i = min(tid + 256 * u, n_k - 1), tt = i / (Hkv * CH), r = i - tt * (Hkv * CH), h = r / CH,
-              c = r - h * CH;
+    const int i = min(tid + 256 * u, n_k - 1), tt = i / (hpw * CH), r = i - tt * (hpw * CH), h = h0 + r / CH,
+              c = r % CH;
     const bf16_t* src = tile + static_cast<size_t>(tt) * row_stride + (Hq + h) * D + 8 * c;
     ka[u] = *reinterpret_cast<const uint4*>(src);
     kb[u] = *reinterpret_cast<const uint4*>(src + HALF);
@@ -363,7 +365,7 @@ __global__ void __launch_bounds__(256) kv_rope_t16_kernel(
   // rotate and store K
 #pragma unroll
   for (int u = 0; u < NI; ++u) {
-    const int i = tid + 256 * u, r = i % (Hkv * CH), h = r / CH, c = r - h * CH;
+    const int i = tid + 256 * u, r = i % (hpw * CH), h = h0 + r / CH, c = r % CH;
     const float* cs = cos_sin + pos[u] * D + 8 * c;
     const float4 c0 = *reinterpret_cast<const float4*>(cs), c1 = *reinterpret_cast<const float4*>(cs + 4);
     const float4 s0 = *reinterpret_cast<const float4*>(cs + HALF), s1 = *reinterpret_cast<const float4*>(cs + HALF + 4);
@@ -396,7 +398,7 @@ __global__ void __launch_bounds__(256) kv_rope_t16_kernel(
       const int b = rest ? __builtin_ctz(rest) : nt;  // run = tokens [a, b)
       const int64_t sl = s_slot[a];
       if (sl < 0) continue;
-      KT* row = kv + (sl / BS) * block_stride + static_cast<size_t>(Hkv) * BS * D + static_cast<size_t>(j) * BS;
+      KT* row = kv + (sl / BS) * block_stride + static_cast<size_t>(Hkv) * BS * D + static_cast<size_t>(h0 * D + j) * BS;
       kv_put(row, static_cast<int>(sl % BS), b - a, vstage + a * hkd + j, hkd, v_inv_scale);
     }
   }
@@ -416,8 +418,13 @@ static void launch_rope_typed(bf16_t* q_out, const bf16_t* qkv, const int64_t* p
                               hipStream_t s) {
   const bool norm = qn != nullptr;
   if (!norm && q_out == nullptr && T >= 512 && (D == 64 || D == 128) && Hkv * D <= 1024 && !kv_t16_legacy()) {
-    const dim3 g16((T + 15) / 16), b16(256);
-    const size_t lds = static_cast<size_t>(16) * Hkv * D * sizeof(bf16_t);
+    // kv-head groups per 16-token tile: about 2 workgroups per CU for short chunks (a 2,400-token
+    // chunk is only 150 tiles), whole-head groups that divide Hkv
+    const int tiles = (T + 15) / 16;
+    int hgroups = 1;
+    while (hgroups * 2 <= Hkv && Hkv % (hgroups * 2) == 0 && tiles * hgroups < 512) hgroups *= 2;
+    const dim3 g16(tiles, hgroups), b16(256);
+    const size_t lds = static_cast<size_t>(16) * (Hkv / hgroups) * D * sizeof(bf16_t);
     const bool small = Hkv * D <= 512;
 #define MXS_KV16(DD, NI, NV)                                                                                    \
   hipLaunchKernelGGL((kv_rope_t16_kernel<DD, KT, NI, NV>), g16, b16, lds, s, qkv, positions, cos_sin, kv,       \
