@@ -251,16 +251,17 @@ void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Te
   int* cnt = nullptr;
   if (ws_bytes > 0) {
     static std::mutex mu;
-    static std::map<int, at::Tensor> counters;
+    // never destroyed: a static tensor's destructor would run after the HIP runtime has shut down
+    static auto* counters = new std::map<int, at::Tensor>();
     std::lock_guard<std::mutex> lock(mu);
-    at::Tensor& c = counters[q.get_device()];
+    at::Tensor& c = (*counters)[q.get_device()];
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     TORCH_CHECK(hipStreamIsCapturing(stream(), &cap) == hipSuccess, "hipStreamIsCapturing");
     if (!c.defined() || c.numel() < ncnt) {
       if (cap == hipStreamCaptureStatusNone) {
         // a grown table's predecessor stays allocated: a launch on another stream may still use it
-        static std::vector<at::Tensor> retired;
-        if (c.defined()) retired.push_back(c);
+        static auto* retired = new std::vector<at::Tensor>();
+        if (c.defined()) retired->push_back(c);
         c = at::zeros({std::max<long>(ncnt, 1L << 14)}, q.options().dtype(at::kInt));
       } else {
         ws_bytes = 0;  // no counters outside a graph's pool: run this launch unsplit
