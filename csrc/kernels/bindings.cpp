@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <map>
+#include <utility>
 #include <mutex>
 #include <optional>
 #include <vector>
@@ -242,8 +243,9 @@ void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Te
   TORCH_CHECK(qsl.scalar_type() == at::kInt && seq_lens.scalar_type() == at::kInt, "int32 metadata");
   TORCH_CHECK(block_tables.scalar_type() == at::kInt && block_tables.stride(1) == 1, "block_tables");
   const int S = seq_lens.size(0);
-  // the split variant: scratch from the caching allocator per call, tile counters persistent per device
-  // (zeroed once, never reset: each launch adds 2 per split tile)
+  // the split variant: scratch from the caching allocator per call, tile counters persistent per
+  // (device, stream) (zeroed once, never reset: each launch adds 2 per split tile, and launches on one
+  // stream run in order, so the ticket parity holds; two streams never share a table)
   long ws_bytes = 0, ncnt = 0;
   mxs::paged_prefill_split_need(static_cast<int>(version), fp8, S, static_cast<int>(max_q_len), Hq, Hkv, D,
                                 &ws_bytes, &ncnt);
@@ -252,14 +254,14 @@ void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Te
   if (ws_bytes > 0) {
     static std::mutex mu;
     // never destroyed: a static tensor's destructor would run after the HIP runtime has shut down
-    static auto* counters = new std::map<int, at::Tensor>();
+    static auto* counters = new std::map<std::pair<int, hipStream_t>, at::Tensor>();
     std::lock_guard<std::mutex> lock(mu);
-    at::Tensor& c = (*counters)[q.get_device()];
+    at::Tensor& c = (*counters)[{static_cast<int>(q.get_device()), stream()}];
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     TORCH_CHECK(hipStreamIsCapturing(stream(), &cap) == hipSuccess, "hipStreamIsCapturing");
     if (!c.defined() || c.numel() < ncnt) {
       if (cap == hipStreamCaptureStatusNone) {
-        // a grown table's predecessor stays allocated: a launch on another stream may still use it
+        // a grown table's predecessor stays allocated: launches still queued on the stream may use it
         static auto* retired = new std::vector<at::Tensor>();
         if (c.defined()) retired->push_back(c);
         c = at::zeros({std::max<long>(ncnt, 1L << 14)}, q.options().dtype(at::kInt));
