@@ -970,9 +970,12 @@ static int pf3_effective_var(int version, bool fp8, int G, int D, int num_seqs, 
 }
 // the v3 variant a launch would run (host only: the selection of pf3_effective_var, for tests and logs);
 // -1 when the launch takes the v2 kernel
+// the one v2-vs-v3 decision, shared by the launch, the split-scratch sizing and the variant report:
+// fp8 KV and a fused q (RoPE inside the kernel, or q read from the qkv output) exist only on v3
+static bool pf_takes_v3(int version, bool kv_fp8, bool fused_q) { return version != 2 || kv_fp8 || fused_q; }
 int paged_prefill_variant(int version, bool kv_fp8, bool fused_q, int num_seqs, int max_q_len, int Hq, int Hkv,
                           int D) {
-  if (version == 2 && !kv_fp8 && !fused_q) return -1;
+  if (!pf_takes_v3(version, kv_fp8, fused_q)) return -1;
   return pf3_effective_var(version, kv_fp8, Hq / Hkv, D, num_seqs, max_q_len, Hkv);
 }
 static long pf3_blocks(int num_seqs, int max_q_len, int Hkv, int G) {
@@ -1023,14 +1026,14 @@ static void pf3_dispatch(int var, bool fp8, bf16_t* out, const bf16_t* q, const 
 
 // Bytes of scratch and int32 counters the launch needs (0 when it does not run the split variant).
 // Counters must start at zero once and are never reset (see the split comment above the kernel).
-void paged_prefill_split_need(int version, bool kv_fp8, int num_seqs, int max_q_len, int Hq, int Hkv, int D,
-                              long* ws_bytes, long* counters) {
+void paged_prefill_split_need(int version, bool kv_fp8, bool fused_q, int num_seqs, int max_q_len, int Hq, int Hkv,
+                              int D, long* ws_bytes, long* counters) {
   *ws_bytes = 0;
   *counters = 0;
   if (num_seqs == 0 || max_q_len == 0 || Hkv == 0 || Hq % Hkv != 0 || (D != 64 && D != 128)) return;
   const int G = Hq / Hkv;
   const long items = pf3_blocks(num_seqs, max_q_len, Hkv, G);
-  if (version == 2 && !kv_fp8) return;  // v2 unless the launch needs v3 (fused q): not split either way
+  if (!pf_takes_v3(version, kv_fp8, fused_q)) return;  // the v2 kernel has no split form
   if (pf3_effective_var(version, kv_fp8, G, D, num_seqs, max_q_len, Hkv) != 128) return;
   *counters = items;
   *ws_bytes = items * (D == 64 ? pf3_split_item_bytes(64, 128) : pf3_split_item_bytes(128, 128));
@@ -1048,7 +1051,7 @@ void launch_paged_prefill(bf16_t* out, const bf16_t* q, const void* kv_ptr, bool
   const int G = Hq / Hkv;
   const bf16_t* kv = static_cast<const bf16_t*>(kv_ptr);
   if (q_stride <= 0) q_stride = Hq * D;
-  if (version != 2 || kv_fp8 || cos_sin != nullptr || q_stride != Hq * D) {  // fp8 / fused q: the v3 path only
+  if (pf_takes_v3(version, kv_fp8, cos_sin != nullptr || q_stride != Hq * D)) {
     const float sc = kv_fp8 ? scale * k_scale : scale, vs = kv_fp8 ? v_scale : 1.f;
     const int var = pf3_effective_var(version, kv_fp8, G, D, num_seqs, max_q_len, Hkv);
 #define MXS_PF3(DD, GG)                                                                                     \

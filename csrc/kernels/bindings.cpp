@@ -27,7 +27,7 @@ bool launch_paged_decode(bf16_t*, float*, float*, const bf16_t*, const void*, bo
 void launch_paged_prefill(bf16_t*, const bf16_t*, const void*, bool, long, const int*, int, const int*, const int*,
                           int, int, int, int, int, float, int, float, float, hipStream_t, int = 0,
                           const int64_t* = nullptr, const float* = nullptr, char* = nullptr, int* = nullptr);
-void paged_prefill_split_need(int, bool, int, int, int, int, int, long*, long*);
+void paged_prefill_split_need(int, bool, bool, int, int, int, int, int, long*, long*);
 int paged_prefill_variant(int, bool, bool, int, int, int, int, int);
 void launch_sample(int64_t*, const void*, bool, int, int, long, const float*, const float*, const int*,
                    const int64_t*, const int64_t*, hipStream_t);
@@ -247,8 +247,9 @@ void paged_attention_prefill(at::Tensor out, at::Tensor q, at::Tensor kv, at::Te
   // (device, stream) (zeroed once, never reset: each launch adds 2 per split tile, and launches on one
   // stream run in order, so the ticket parity holds; two streams never share a table)
   long ws_bytes = 0, ncnt = 0;
-  mxs::paged_prefill_split_need(static_cast<int>(version), fp8, S, static_cast<int>(max_q_len), Hq, Hkv, D,
-                                &ws_bytes, &ncnt);
+  const bool fused_q = qa.cs != nullptr || qa.stride != Hq * D;  // as launch_paged_prefill decides v2 / v3
+  mxs::paged_prefill_split_need(static_cast<int>(version), fp8, fused_q, S, static_cast<int>(max_q_len), Hq, Hkv,
+                                D, &ws_bytes, &ncnt);
   at::Tensor ws;
   int* cnt = nullptr;
   if (ws_bytes > 0) {
@@ -589,6 +590,15 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("fused_q"), pybind11::arg("num_seqs"), pybind11::arg("max_q_len"), pybind11::arg("hq"),
         pybind11::arg("hkv"), pybind11::arg("head_dim"),
         "prefill attention v3 variant a launch picks (0 default, 128 split-KV, 256 paired tiles; -1: v2)");
+  m.def("paged_prefill_split_need",
+        [](int version, bool kv_fp8, bool fused_q, int num_seqs, int max_q_len, int hq, int hkv, int head_dim) {
+          long ws = 0, cnt = 0;
+          mxs::paged_prefill_split_need(version, kv_fp8, fused_q, num_seqs, max_q_len, hq, hkv, head_dim, &ws, &cnt);
+          return std::make_pair(ws, cnt);
+        },
+        pybind11::arg("version"), pybind11::arg("kv_fp8"), pybind11::arg("fused_q"), pybind11::arg("num_seqs"),
+        pybind11::arg("max_q_len"), pybind11::arg("hq"), pybind11::arg("hkv"), pybind11::arg("head_dim"),
+        "(scratch bytes, tile counters) the split-KV prefill variant of this launch needs (0, 0: unsplit)");
   m.def("paged_attention_prefill", &paged_attention_prefill, pybind11::arg("out"), pybind11::arg("q"),
         pybind11::arg("kv"), pybind11::arg("block_tables"), pybind11::arg("qsl"), pybind11::arg("seq_lens"),
         pybind11::arg("scale"), pybind11::arg("max_q_len"), pybind11::arg("version") = 3,

@@ -72,6 +72,7 @@ struct PfArgs {
   const bf16_t* W;
   float* slab;  // stream-K partials: [grid][34 fragments][512 threads][4] fp32 (one per workgroup)
   int* cnt;     // per stream-K tile arrival counters (zero between launches)
+  int* err;     // count of stream-K heads whose wait timed out (checked by the host; never reset here)
   const int* tile_map;  // logical tile -> token tile | weight tile << 16 (pf_tile_map)
   int M, K, ldx, ldy, inter, ntm, ntn, nk;
   int nrows_w;  // rows of W
@@ -494,13 +495,21 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
         // ((s0 + s1) + s2) ... with s0 in registers -- fp32 addition commutes, so the bits do not depend
         // on which workgroup finishes when.  No own slab round trip, no arrival ticket.
         if (tid == 0) {
+          // Deadlock-free only while every owner is resident: true for one grid (G <= CUs, one
+          // workgroup per CU) but not guaranteed when another process's grid holds CUs.  The wait is
+          // bounded by the 100 MHz wall clock (0.5 s); a timeout is counted in *err (the host reads it,
+          // ops.gemm_pf_faults) instead of passing silently.  The counter is re-armed by subtracting
+          // `want`, so segments arriving after a timeout bring it back to zero for the next launch.
           const int want = o_hi - o_lo;
-          for (long spin = 0; __hip_atomic_load(a.cnt + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want;
-               ++spin) {
-            if (spin > (1L << 30)) break;  // every owner is a running workgroup of this grid: never taken
+          const long long t_end = wall_clock64() + 50000000LL;
+          while (__hip_atomic_load(a.cnt + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+            if (wall_clock64() > t_end) {
+              __hip_atomic_fetch_add(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
             __builtin_amdgcn_s_sleep(2);
           }
-          a.cnt[l] = 0;  // re-armed for the next launch
+          __hip_atomic_fetch_add(a.cnt + l, -want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         PF_BAR();
         for (int q = o_lo + 1; q <= o_hi; ++q) {
@@ -581,7 +590,7 @@ int pf_plan(int M, int N, int K, int epi, int num_cu, int min_iters, int* dp_rou
 
 // epi 0: Y [M, N] = X W^T (N % 256 == 0).  epi 1 (SwiGLU): W = [gate; up] rows [2 I, K], Y [M, I]
 // (I % 128 == 0).  epi 2: Y = R + X W^T.  row_scale (epi 0 / 1): rows scaled by rsqrt(mean(x^2) + eps).  K % 64 == 0, 16-byte aligned rows.  slab: >= 2 * grid * 32 * 512 * 4 floats; cnt:
-// >= sk_tiles ints, zero (left zero by every launch).  False when the shape is not supported.
+// > sk_tiles ints, zero (left zero by every launch; the last word counts stream-K wait timeouts).  False when the shape is not supported.
 bool launch_gemm_pf(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, int K, int ldx, int ldy, int epi,
                     float* slab, long slab_floats, int* cnt, int cnt_len, const int* tile_map, int map_len,
                     int num_cu, int min_iters, hipStream_t s, const bf16_t* R, int ldr, bool row_scale,
@@ -596,7 +605,7 @@ bool launch_gemm_pf(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, i
   int dp, sk, G;
   if (!pf_plan(M, N, K, epi, num_cu, min_iters, &dp, &sk, &G, trows)) return false;
   if (row_scale && trows != 256) return false;  // the fused-RMSNorm forms exist at 256 rows
-  if (sk > 0 && (slab == nullptr || cnt == nullptr || cnt_len < sk || slab_floats < 2L * G * PF_SLAB_FRAGS * 512 * 4))
+  if (sk > 0 && (slab == nullptr || cnt == nullptr || cnt_len <= sk || slab_floats < 2L * G * PF_SLAB_FRAGS * 512 * 4))
     return false;
   if (tile_map == nullptr || map_len < ((M + trows - 1) / trows) * (N / 256)) return false;
   if (static_cast<long>(M) * ldx * 2 > 0x7FFFFFFFL) return false;  // X rows addressed by 32-bit buffer offsets
@@ -606,6 +615,7 @@ bool launch_gemm_pf(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, i
   a.W = W;
   a.slab = slab;
   a.cnt = cnt;
+  a.err = cnt + cnt_len - 1;  // the counters' last word (never a tile counter: cnt_len > sk_tiles)
   a.tile_map = tile_map;
   a.nrows_w = N;
   a.M = M;

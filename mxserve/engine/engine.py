@@ -14,6 +14,7 @@ from dataclasses import dataclass
 from typing import Optional
 
 from ..config import EngineArgs
+from .. import ops
 from ..models.config import get_model_config
 from .kv_manager import KVCacheManager
 from .model_runner import ModelRunner
@@ -284,6 +285,11 @@ class LLMEngine:
         s = self.scheduler.stats()
         s.update(num_steps=self.num_steps, num_generated=self.num_generated, **self.runner.kv_stats())
         s["custom_ar_timeouts"] = self.num_collective_faults
+        if self.runner.is_gpu:
+            s["gemm_pf_timeouts"] = ops.gemm_pf_faults(self.runner.device)
+            if s["gemm_pf_timeouts"]:
+                log.error("gemm_pf: %d stream-K waits timed out (grid not resident); prefill sums of "
+                          "those tiles are wrong", s["gemm_pf_timeouts"])
         la = self._late
         if la is not None:
             s["late_admission"] = {"waits": la.waits, "late_wakes": la.late, "margin_ms": round(1e3 * la.margin, 3),

@@ -449,6 +449,7 @@ class Frontend:
                 break
             w, ids, sp, purl = pick
             w.inflight += 1
+            n0 = len(generated)
             try:
                 async for evs in self._worker_stream(w, ids, sp, rid, purl):
                     generated.extend(ev.token_id for ev in evs)
@@ -457,7 +458,8 @@ class Frontend:
                         return
                 raise ConnectionError(f"worker {w.worker_id} ended the stream early")
             except _STREAM_ERRORS as e:
-                self.router.forget(w, rid)
+                if len(generated) == n0:  # never reached the worker's queue: stop counting it there
+                    self.router.forget(w, rid)
                 self._attempt_failed(model, w, e, generated, tried)
             finally:
                 w.inflight -= 1
@@ -475,6 +477,7 @@ class Frontend:
                 break
             w, ids, sp, purl = pick
             w.inflight += 1
+            n0 = len(generated)
             try:
                 await self._push_attempt(w, ids, sp, rid, purl, ps)
                 return
@@ -482,7 +485,10 @@ class Frontend:
                 from .fastpath import ClientGone
                 if isinstance(e, ClientGone):  # nobody to stream to: no retry
                     raise
-                self.router.forget(w, rid)
+                # a failure after tokens arrived: the worker queued it, and its num_added (or the
+                # unseen TTL) retires the entry -- forgetting here would retire a later request's
+                if len(generated) == n0:
+                    self.router.forget(w, rid)
                 self._attempt_failed(model, w, e, generated, tried)
             finally:
                 w.inflight -= 1

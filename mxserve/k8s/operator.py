@@ -50,6 +50,7 @@ class LeaderElector:
         self.id = identity or f"{socket.gethostname()}-{os.getpid()}"
         self.lease_s = lease_s
         self.leader = False
+        self.observed = False  # one election step reached the apiserver (leader or healthy standby)
 
     @staticmethod
     def _now() -> str:
@@ -71,12 +72,13 @@ class LeaderElector:
                 self.k.create({"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
                                "metadata": {"name": self.name, "namespace": self.ns},
                                "spec": dict(spec, acquireTime=spec["renewTime"], leaseTransitions=0)})
-                self.leader = True
+                self.leader = self.observed = True
                 return True
             cur = lease.get("spec") or {}
             holder = cur.get("holderIdentity")
             expired = time.time() > self._parse(cur.get("renewTime")) + float(cur.get("leaseDurationSeconds") or
                                                                                self.lease_s)
+            self.observed = True
             if holder != self.id and not expired:
                 self.leader = False
                 return False
@@ -90,6 +92,27 @@ class LeaderElector:
             log.info("leader election: %s", e)
             self.leader = False
         return self.leader
+
+    def release(self) -> bool:
+        """Give the lease up (SIGTERM of the leader): clear the holder and back-date renewTime, so a
+        standby takes over at its next step instead of after leaseDurationSeconds (the client-go
+        ReleaseOnCancel behaviour).  Returns whether this replica held it."""
+        if not self.leader:
+            return False
+        try:
+            lease = self.k.get("Lease", self.name, self.ns)
+            if lease is None or (lease.get("spec") or {}).get("holderIdentity") != self.id:
+                return False
+            self.k.merge_patch("Lease", self.name, self.ns,
+                               {"metadata": {"resourceVersion": lease["metadata"].get("resourceVersion")},
+                                "spec": {"holderIdentity": "", "leaseDurationSeconds": 1,
+                                         "renewTime": "1970-01-01T00:00:00.000000Z"}})
+            return True
+        except ApiError as e:
+            log.info("lease release: %s", e)
+            return False
+        finally:
+            self.leader = False
 
 
 class Operator:
@@ -380,9 +403,15 @@ class Operator:
         return ok, detail
 
     def ready(self) -> bool:
-        """Ready once a reconcile pass has completed (a standby replica of a leader-elected
-        deployment stays unready: it does not reconcile)."""
-        return self.last_pass is not None and (self.elector is None or self.elector.leader)
+        """Ready once this replica works: a reconcile pass completed, or -- with leader election -- an
+        election step reached the apiserver (the leader after its first pass, a standby as soon as it
+        sees the lease held).  Leadership only gates reconciling: a standby reporting unready would
+        stall a RollingUpdate (maxUnavailable 0) for as long as the old leader renews its lease."""
+        if self.elector is None:
+            return self.last_pass is not None
+        if self.elector.leader:
+            return self.last_pass is not None
+        return self.elector.observed
 
     def serve_probes(self, port: int, host: str = "0.0.0.0"):
         """/healthz (liveness) and /readyz (readiness) on a daemon thread; returns the server."""
@@ -445,7 +474,18 @@ def main(argv=None) -> None:
         op.elector = LeaderElector(client, a.lease_namespace)
     if a.health_port:
         op.serve_probes(a.health_port)
-    op.run(a.interval, watch=not a.no_watch)
+    stop = threading.Event()
+
+    def on_term(signum, frame):  # noqa: ARG001
+        stop.set()
+        op._wake.set()
+    import signal
+    signal.signal(signal.SIGTERM, on_term)
+    try:
+        op.run(a.interval, watch=not a.no_watch, stop=stop)
+    finally:
+        if op.elector is not None and op.elector.release():
+            log.info("released the operator lease")
 
 
 if __name__ == "__main__":

@@ -229,6 +229,18 @@ def _pf_workspace(device) -> tuple:
     return ws
 
 
+def gemm_pf_faults(device=None) -> int:
+    """Stream-K tile heads of gemm_pf whose wait for the tile's other segments timed out since the
+    workspace was made (csrc/kernels/gemm_pf.hip: the counters' last word).  Non-zero means a launch
+    ran while its grid was not fully resident (another process holding CUs) and produced wrong sums
+    for those tiles; the engine reports it in stats() and the GPU tests require zero."""
+    dev = torch.device(device) if device is not None else torch.device("cuda")
+    if dev.index is None:
+        dev = torch.device(dev.type, torch.cuda.current_device())
+    ws = _PF_WS.get(dev)
+    return 0 if ws is None else int(ws[1][-1].item())
+
+
 _PF_MAPS: dict = {}
 
 

@@ -199,8 +199,8 @@ def folded_weight_needed(N: int, K: int, code: int, max_rows: int, device) -> bo
     store = TunedStore("prefill_pf", device_tag(device))
     for M in buckets_for(max_rows):
         st = store.get(f"{N}x{K}:{code}@{M}")
-        if st is None or isinstance(st.get("cfg"), int):
-            return True  # not measured here yet, or gemm_pf kept at this bucket
+        if st is None or is_pf(st.get("cfg")):
+            return True  # not measured here yet, or gemm_pf kept at this bucket (int or [rows, min_iters])
     return False
 
 

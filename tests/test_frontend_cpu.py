@@ -379,11 +379,17 @@ def test_mid_stream_migration_keeps_greedy_output():
     bs_.start()
     body = {"model": MODEL, "messages": [{"role": "user", "content": "migrate me"}], "max_tokens": 12,
             "temperature": 0, "ignore_eos": True}
+    forgot = []
+    real_forget = fe.router.forget
+    fe.router.forget = lambda w, rid: forgot.append((w.worker_id, rid)) or real_forget(w, rid)
     try:
         wait_for(lambda: len(fe.registry.list()) == 2)
         outs = [httpx.post(fs.url + "/v1/chat/completions", json=body, timeout=120).json() for _ in range(2)]
         texts = {o["choices"][0]["message"]["content"] for o in outs}
         assert len(texts) == 1, outs  # one request hit the flaky worker first, the other did not
+        # the flaky worker queued the request (it streamed a token), so its routed entry is
+        # retired by the worker's num_added, not forgotten (that would retire a later request's)
+        assert not forgot, forgot
         assert all(o["usage"]["completion_tokens"] == 12 for o in outs)
         text = httpx.get(fs.url + "/metrics").text
         assert "dynamo_frontend_request_migrations_total" in text

@@ -697,8 +697,10 @@ def test_operator_health_fails_after_a_stalled_watch(cluster):
 
 
 def test_lease_leader_election(cluster):
-    """Two operator replicas: one holds the Lease and reconciles; the other stays on standby (not
-    ready) until the holder stops renewing and the lease expires, then takes over."""
+    """Two operator replicas: one holds the Lease and reconciles; the other stays on standby until
+    the holder stops renewing and the lease expires, then takes over.  A healthy standby reports
+    ready (otherwise a RollingUpdate never completes while the old leader lives), and a
+    leader that releases its lease on SIGTERM hands over at the standby's next step."""
     from mxserve.k8s.operator import LeaderElector
     fake, k = cluster
     a = LeaderElector(k, "dynamo-system", identity="a", lease_s=1.0)
@@ -716,4 +718,13 @@ def test_lease_leader_election(cluster):
     op.last_pass = time.monotonic()
     assert op.ready()
     op.elector = a
-    assert not op.ready()  # standby
+    assert op.ready()  # healthy standby: ready, does not reconcile
+    op.elector = LeaderElector(k, "dynamo-system", identity="c", lease_s=1.0)
+    assert not op.ready()  # no election step reached the apiserver yet
+    # hand-over without waiting for expiry
+    c = LeaderElector(k, "dynamo-system", identity="c", lease_s=30.0)
+    assert b.step() and not c.step()
+    assert b.release() and not b.leader
+    assert c.step()
+    assert k.get("Lease", "mxserve-operator", "dynamo-system")["spec"]["holderIdentity"] == "c"
+    assert not a.release()  # not the holder: nothing to release

@@ -50,3 +50,15 @@ def test_v2_only_for_bf16_dense_q():
     assert pick(1, 4096, version=2, fused_q=False) == -1
     assert pick(1, 4096, version=2, fused_q=True) == 128  # fused q needs v3
     assert pick(1, 4096, version=2, fp8=True, fused_q=False) == 128
+
+
+@pytest.mark.parametrize("version", [2, 3])
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("fused_q", [False, True])
+@pytest.mark.parametrize("shape", [(1, 2048), (2, 4096), (1, 6144)])
+def test_split_scratch_matches_the_reported_variant(version, fp8, fused_q, shape):
+    """the split scratch / counters are sized from the same v2-vs-v3 decision the launch and
+    the variant report use -- version 2 with a fused q runs v3, so its split variant gets scratch."""
+    var = pick(*shape, version=version, fp8=fp8, fused_q=fused_q)
+    ws, cnt = ops.ext().paged_prefill_split_need(version, fp8, fused_q, shape[0], shape[1], 32, 8, 64)
+    assert (ws > 0 and cnt > 0) == (var == 128), (var, ws, cnt)

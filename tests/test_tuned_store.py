@@ -90,3 +90,25 @@ def test_pick_keeps_library_within_margin(fake_clock):
     cands = {"a": _fn(9.8, 9.8, 9.8, 9.8)}  # 2 % faster: below the 3 % margin
     best, t, t_lib = decode_gemm.pick(lib, cands)
     assert best is None and t == t_lib == 10.0
+
+
+@pytest.mark.parametrize("cfgs,want", [
+    ({512: None, 1024: None}, False),             # every bucket rejects the fused form: no folded copy
+    ({512: None, 1024: [256, 16]}, True),         # tune_fused()'s list form keeps gemm_pf at one bucket
+    ({512: 8, 1024: None}, True),                 # earlier rounds' int form
+    ({512: None}, True),                          # a bucket not measured yet
+    ({512: "addmm", 1024: None}, False),          # code-2 string choices are not gemm_pf
+])
+def test_folded_weight_needed_reads_every_cfg_form(tmp_path, monkeypatch, cfgs, want):
+    """a stored [rows, min_iters] choice must count as 'gemm_pf kept' so the norm-folded
+    weight the fused kernel needs is made at start-up."""
+    from mxserve.ops import prefill_pf
+    monkeypatch.setenv("MXS_TUNED_DIR", str(tmp_path))
+    monkeypatch.setattr(tuned, "device_tag", lambda device=None: "gfxtest_256cu")
+    monkeypatch.setattr(prefill_pf, "MODE", "auto")
+    monkeypatch.setattr(tuned, "PKG_DIR", str(tmp_path / "none"))
+    entries = {f"2048x2048:3@{m}": {"cfg": c, "us": 1.0, "base_us": 2.0} for m, c in cfgs.items()}
+    (tmp_path / "prefill_pf_gfxtest_256cu.json").write_text(json.dumps({"device": "gfxtest_256cu",
+                                                                        "entries": entries}))
+    assert prefill_pf.buckets_for(1024) == [512, 1024]
+    assert prefill_pf.folded_weight_needed(2048, 2048, 3, 1024, None) is want
