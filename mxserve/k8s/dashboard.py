@@ -18,6 +18,12 @@ import sys
 import yaml
 
 NS = 'namespace=~"$namespace"'
+# the reference ConfigMap's contract (grafana-dynamo-dashboard-configmap.yaml:12,1006): anything
+# provisioned or bookmarked against the reference dashboard keeps working
+UID = "dynamo-dashboard"
+DATA_KEY = "dynamo-dashboard.json"
+# reference DCGM series -> the AMD device-metrics-exporter gauge plotted in their place
+DCGM_TO_AMD = {"DCGM_FI_DEV_GPU_UTIL": "gpu_gfx_activity", "DCGM_FI_DEV_POWER_USAGE": "gpu_power_usage"}
 
 
 def _ratio(metric: str, scale: str = "1000*") -> str:
@@ -26,8 +32,9 @@ def _ratio(metric: str, scale: str = "1000*") -> str:
 
 # (title, unit, [(expr, legend)])
 PANELS = [
+    # the reference's split: one series per (request_type = stream | unary, status), every label kept
     ("Frontend Requests / Sec", "reqps",
-     [(f"sum by (model, status) (rate(dynamo_frontend_requests_total{{{NS}}}[1m]))", "{{model}} {{status}}")]),
+     [(f"rate(dynamo_frontend_requests_total{{{NS}}}[1m])", "{{request_type}}, {{status}},")]),
     ("Frontend Avg Time to First Token", "ms",
      [(_ratio("dynamo_frontend_time_to_first_token_seconds"), "{{model}}")]),
     ("Frontend Avg Inter-Token Latency", "ms",
@@ -82,7 +89,7 @@ def dashboard() -> dict:
                         for j, (e, lg) in enumerate(targets)],
         })
     return {
-        "title": "mxserve Dashboard (MI355X)", "uid": "mxserve-mi355x", "schemaVersion": 39, "version": 1,
+        "title": "Dynamo Dashboard (MI355X)", "uid": UID, "schemaVersion": 39, "version": 1,
         "editable": True, "refresh": "10s", "time": {"from": "now-30m", "to": "now"}, "tags": ["mxserve", "dynamo"],
         "templating": {"list": [
             {"name": "datasource", "type": "datasource", "query": "prometheus", "current": {}},
@@ -98,7 +105,7 @@ def configmap(namespace: str = "monitoring") -> dict:
     return {"apiVersion": "v1", "kind": "ConfigMap",
             "metadata": {"name": "grafana-dynamo-dashboard", "namespace": namespace,
                          "labels": {"grafana_dashboard": "1"}},
-            "data": {"mxserve-dashboard.json": json.dumps(dashboard(), indent=2)}}
+            "data": {DATA_KEY: json.dumps(dashboard(), indent=2)}}
 
 
 class _BlockDumper(yaml.SafeDumper):
