@@ -722,6 +722,7 @@ def test_lease_leader_election(cluster):
     op.elector = LeaderElector(k, "dynamo-system", identity="c", lease_s=1.0)
     assert not op.ready()  # no election step reached the apiserver yet
     # hand-over without waiting for expiry
+    b = LeaderElector(k, "dynamo-system", identity="b", lease_s=30.0)  # a lease that cannot expire here
     c = LeaderElector(k, "dynamo-system", identity="c", lease_s=30.0)
     assert b.step() and not c.step()
     assert b.release() and not b.leader
