@@ -371,6 +371,7 @@ class Driver:
         self.hist: list = []
         self.source = None  # ArrivalClient: requests routed here by the node's router (--arrivals router)
         self.load_fn = None
+        self.breakdown: list = []  # disagg decode rank: per-request TTFT components (BREAKDOWN_KEYS), seconds
 
     def attach(self, source, load_fn) -> None:
         self.source, self.load_fn = source, load_fn
@@ -467,13 +468,19 @@ class Driver:
         ttft = np.array(self.c["ttft"]) if self.c["ttft"] else np.array([np.nan])
         itl = np.array(self.itls) if self.itls else np.array([np.nan])
         running = float(np.mean([x[1] for x in self.hist[-200:]])) if self.hist else 0.0
+        bd = (np.median(np.asarray(self.breakdown), axis=0).tolist() if self.breakdown
+              else [float("nan")] * len(BREAKDOWN_KEYS))
         return [dt, float(self.c["tokens"]), float(np.nanmedian(ttft)), float(np.nanmedian(itl)),
                 float(len(self.c["ttft"])), float(self.warmup_steps), float(self.warmup_s), float(self.steady),
-                running, float(np.nanpercentile(ttft, 90)), float(np.nanpercentile(itl, 90))]
+                running, float(np.nanpercentile(ttft, 90)), float(np.nanpercentile(itl, 90))] + bd
 
 
+# disagg TTFT components (decode ranks; columns 11.. of the stat rows): arrival -> sent to a prefill
+# rank (decode-side reservation queue), -> first scheduled there (pipe + prefill queue), -> first token
+# sampled (prefill compute), -> KV push complete (transfer), -> first token emitted here (admission)
+BREAKDOWN_KEYS = ("decode_queue_ms", "to_prefill_ms", "prefill_ms", "transfer_ms", "admit_ms")
 _STAT_NAN = [0.0, 0.0, float("nan"), float("nan"), 0.0, float("nan"), float("nan"), float("nan"), float("nan"),
-             float("nan"), float("nan")]
+             float("nan"), float("nan")] + [float("nan")] * len(BREAKDOWN_KEYS)
 
 
 def timed_phases(a, step, barrier, agree, drv, running, on_phase=lambda phase: None) -> float:
@@ -624,13 +631,12 @@ def run_disagg_decode(a, eng, sp, drv, barrier, agree, conns: list) -> float:
             shm_start = agent.acquire_shm(len(dst)) if start is None else None
             backlog.pop(0)
             conns[k].send(("prefill", rid, toks, dst, skip, start, shm_start))
-            inflight[rid] = (k, dst, start, shm_start)
+            inflight[rid] = (k, dst, start, shm_start, time.perf_counter())
             load[k] += 1
-        now = time.perf_counter()
         for conn in conns:
             while conn.poll():
-                _, rid, tok, data = conn.recv()
-                k, dst, start, shm_start = inflight.pop(rid)
+                _, rid, tok, data, tm = conn.recv()
+                k, dst, start, shm_start, t_sent = inflight.pop(rid)
                 load[k] -= 1
                 if start is not None:  # staging extent -> pool blocks, ordered before the next step
                     agent.land(start, dst)
@@ -639,6 +645,12 @@ def run_disagg_decode(a, eng, sp, drv, barrier, agree, conns: list) -> float:
                 elif data is not None:  # host-staged transfer
                     agent.write_blocks(dst, data)
                 out = eng.complete_remote_prefill(rid, tok)
+                now = time.perf_counter()
+                if drv.record_ttft and rid in drv.arrival_of:
+                    # TTFT = decode queue + hand-off to prefill + prefill + KV transfer + admission here
+                    t_recv, t_sched, t_first, t_done = tm
+                    drv.breakdown.append((t_sent - drv.arrival_of[rid], t_sched - t_sent, t_first - t_sched,
+                                          t_done - t_first, now - t_done))
                 drv.token(rid, now, out.finished)
         if eng.has_unfinished():
             outs = eng.step()
@@ -662,91 +674,10 @@ def run_disagg_decode(a, eng, sp, drv, barrier, agree, conns: list) -> float:
 
 
 def run_disagg_prefill(eng, temperature: float, barrier, conns: list) -> int:
-    """Serve this rank's decode ranks until they say stop, joining each of their barriers once (a
-    phase's barrier is entered when every served decode rank has announced it); returns blocks moved."""
-    from mxserve.disagg.kv_transfer import KVTransferAgent
-    from mxserve.engine.request import SamplingParams
-    agent = KVTransferAgent(eng.runner, "xgmi")
-    targets, arenas = [], []
-    for conn in conns:
-        kind, target = conn.recv()
-        assert kind == "desc", kind
-        arena = False
-        if agent.backend == "xgmi" and target["backend"] == "xgmi":
-            try:
-                agent.connect(target)
-                arena = True
-            except (RuntimeError, OSError) as e:  # the decode GPU's arena cannot be mapped here
-                vlog(f"decode arena not mappable ({e!r}); KV goes through the /dev/shm arena")
-        conn.send(("mapped", arena))
-        targets.append(target)
-        arenas.append(arena)
-    vlog(f"prefill rank serving {len(conns)} decode rank(s) (mapped={arenas})")
-    # results go out through one sender thread per channel: a host-staged KV payload can exceed the
-    # socket buffer, and a blocking send here while the decode rank sits in a phase barrier would
-    # keep this loop from ever reading the phase message that joins that barrier (a deadlock)
-    import queue
-    import threading
-    outq = [queue.Queue() for _ in conns]
-
-    def sender(ci: int) -> None:
-        while True:
-            msg = outq[ci].get()
-            if msg is None:
-                return
-            try:
-                conns[ci].send(msg)
-            except (OSError, EOFError):  # the decode rank closed its end after the last barrier
-                return
-    senders = [threading.Thread(target=sender, args=(ci,), name=f"disagg-send-{ci}", daemon=True)
-               for ci in range(len(conns))]
-    for t in senders:
-        t.start()
-    pending: dict = {}
-    announced: dict = {}
-    moved = 0
-    while True:
-        stop = False
-        for ci, conn in enumerate(conns):
-            while conn.poll():
-                msg = conn.recv()
-                if msg[0] == "phase":
-                    announced[msg[1]] = announced.get(msg[1], 0) + 1
-                    if announced[msg[1]] == len(conns):
-                        vlog(f"phase {msg[1]}; {moved} blocks pushed so far")
-                        barrier()
-                        stop = msg[1] == "stop"
-                    continue
-                _, rid, toks, dst, skip, start, shm_start = msg
-                eng.add_request(toks, SamplingParams(max_tokens=1, temperature=temperature, ignore_eos=True),
-                                request_id=rid, disagg_role="prefill_only")
-                pending[rid] = (ci, dst, skip, start, shm_start)
-        if stop:
-            for q in outq:
-                q.put(None)
-            for t in senders:
-                t.join(timeout=10)
-            agent.close()
-            return moved
-        if not eng.has_unfinished():
-            conns[0].poll(0.0005) if len(conns) == 1 else time.sleep(0.0005)
-            continue
-        for o in eng.step():
-            if not o.finished or o.request_id not in pending:
-                continue
-            ci, dst, skip, start, shm_start = pending.pop(o.request_id)
-            target = targets[ci]
-            src = list(eng.requests[o.request_id].block_ids[skip:skip + len(dst)])
-            data = None
-            if start is not None:
-                agent.push_xgmi(src, target, start)
-            elif shm_start is not None:
-                agent.push_shm(src, target, shm_start)
-            else:
-                data = agent.read_blocks(src)
-            moved += len(src)
-            eng.release_prefill_blocks(o.request_id)
-            outq[ci].put(("done", o.request_id, o.token_id, data))
+    """Prefill rank: serve this rank's decode ranks until they say stop (mxserve/disagg/prefill_loop.py);
+    returns blocks moved."""
+    from mxserve.disagg.prefill_loop import serve_prefill
+    return serve_prefill(eng, temperature, barrier, conns, log=vlog)
 
 
 # ---------------------------------------------------------------------------- phases
@@ -1076,8 +1007,11 @@ def main():
             dis = disagg_summary(np.array(r["col"], dtype=np.float64), r["info"], a, world)
             dis["ran_in"] = "probe processes (crash-isolated)"
         else:
-            err = (r or probe_res or {}).get("error", "no result from the probe processes")
+            src = r or probe_res or {}
+            err = src.get("error", "no result from the probe processes")
             dis = {"status": "failed", "error": err}
+            if src.get("where"):
+                dis.update(where=src["where"], rank=src.get("rank"))
             if agg is None:
                 raise SystemExit(f"bench.py: disagg phase failed: {err}")
     if mode in ("disagg", "both") and agg is None:
@@ -1101,6 +1035,11 @@ def disagg_summary(col_d: np.ndarray, info_d: dict, a, world: int) -> dict:
     p_d = info_d["prefill_ranks"]
     dis = summarize(col_d, a.steps, list(range(p_d, world)))
     dis.update(info_d, parallelism=f"disagg {p_d}P+{world - p_d}D")
+    if col_d.shape[1] >= 11 + len(BREAKDOWN_KEYS):  # median over decode ranks of their per-request p50s
+        bd = col_d[p_d:, 11:11 + len(BREAKDOWN_KEYS)]
+        dis["ttft_breakdown_p50_ms"] = {k: (round(float(np.nanmedian(bd[:, i])) * 1e3, 2)
+                                            if not np.all(np.isnan(bd[:, i])) else None)
+                                        for i, k in enumerate(BREAKDOWN_KEYS)}
     return dis
 
 

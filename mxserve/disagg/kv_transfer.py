@@ -307,15 +307,8 @@ class KVTransferAgent:
         self.staging = None
         self._desc = None
 
-    def push_shm(self, src_ids: list[int], target: dict, start: int) -> float:
-        """Prefill side: copy blocks into the decode worker's /dev/shm arena (same pod / host);
-        blocking, returns seconds.  Raises OSError when that arena is not visible here."""
-        if not src_ids:
-            return 0.0
+    def _shm_peer(self, target: dict) -> ShmArena:
         name = target["shm_name"]
-        if start < 0 or start + len(src_ids) > int(target["shm_blocks"]):
-            raise ValueError(f"extent [{start}, +{len(src_ids)}) outside the shm arena")
-        t0 = time.perf_counter()
         with self._lock:
             arena = self._shm_peers.get(name)
             if arena is None:
@@ -324,16 +317,15 @@ class KVTransferAgent:
                 self._shm_peers[name] = arena
         if arena.block_bytes != self.block_bytes:
             raise ValueError("KV block layout mismatch between prefill and decode workers")
-        idx = torch.tensor(src_ids, dtype=torch.long, device=self.kv.device)
-        if self.is_gpu:
-            self._stream.wait_stream(torch.cuda.current_stream(self.kv.device))
-            with torch.cuda.stream(self._stream):
-                arena.t[start:start + len(src_ids)].copy_(self.kv.index_select(0, idx), non_blocking=True)
-            self._stream.synchronize()
-        else:
-            arena.t[start:start + len(src_ids)].copy_(self.kv.index_select(0, idx))
-        self.bytes_moved += len(src_ids) * self.block_bytes
-        self.transfers += 1
+        return arena
+
+    def push_shm(self, src_ids: list[int], target: dict, start: int) -> float:
+        """Prefill side: copy blocks into the decode worker's /dev/shm arena (same pod / host);
+        blocking, returns seconds.  Raises OSError when that arena is not visible here."""
+        t0 = time.perf_counter()
+        ev = self.push_async([(src_ids, target, start, "shm")])
+        if ev is not None:
+            ev.synchronize()
         return time.perf_counter() - t0
 
     # -------------------------------------------------------------- prefill side
@@ -362,24 +354,68 @@ class KVTransferAgent:
     def push_xgmi(self, src_ids: list[int], target: dict, start: int) -> float:
         """Copy blocks into the target's staging arena at block offset `start` (IPC-mapped);
         blocking, returns seconds."""
-        from .. import ops
-        if not src_ids:
-            return 0.0
-        if int(target["block_bytes"]) != self.block_bytes:
-            raise ValueError("KV block layout mismatch between prefill and decode workers")
-        if start < 0 or start + len(src_ids) > int(target["arena_blocks"]):
-            raise ValueError(f"extent [{start}, +{len(src_ids)}) outside the staging arena")
         t0 = time.perf_counter()
-        ptr = self._remote_ptr(target)
-        base = start
-        # the blocks were written on the compute stream: order the copy after everything queued there
-        self._stream.wait_stream(torch.cuda.current_stream(self.kv.device))
-        with torch.cuda.stream(self._stream):
-            s = torch.tensor(src_ids, dtype=torch.int32).pin_memory().to(self.kv.device, non_blocking=True)
-            d = torch.arange(base, base + len(src_ids), dtype=torch.int32).pin_memory().to(self.kv.device,
-                                                                                         non_blocking=True)
-            ops.ext().copy_blocks(ptr, self.kv, s, d, self.block_bytes)
-        self._stream.synchronize()
-        self.bytes_moved += len(src_ids) * self.block_bytes
-        self.transfers += 1
+        ev = self.push_async([(src_ids, target, start, "xgmi")])
+        if ev is not None:
+            ev.synchronize()
         return time.perf_counter() - t0
+
+    def push_async(self, jobs: list, after=None):
+        """Issue the KV pushes of `jobs` -- (src_ids, target, start, via) with via "xgmi" (the
+        target's IPC-mapped GPU arena) or "shm" (its /dev/shm arena) -- without waiting for them.
+
+        Ordering: the transfer stream waits on `after`, the event recorded right after the step that
+        wrote these requests' last KV blocks (Request.kv_ready), not on everything queued on the
+        compute stream: with async scheduling the next step is already queued when a step's outputs
+        land, and waiting for it would hold every push one step back.  With
+        `after` None the push orders after the whole current stream (callers without the event).
+        Every xgmi job to one target goes out in ONE copy_blocks launch.  Returns an event recorded on
+        the transfer stream after the copies (poll it; the source blocks must stay allocated until it
+        fires), or None when the copies are already done (CPU)."""
+        from .. import ops
+        jobs = [j for j in jobs if j[0]]
+        if not jobs:
+            return None
+        groups: dict = {}
+        shm_jobs = []
+        for src_ids, target, start, via in jobs:
+            if via == "xgmi":
+                if int(target["block_bytes"]) != self.block_bytes:
+                    raise ValueError("KV block layout mismatch between prefill and decode workers")
+                if start < 0 or start + len(src_ids) > int(target["arena_blocks"]):
+                    raise ValueError(f"extent [{start}, +{len(src_ids)}) outside the staging arena")
+                g = groups.setdefault(self._remote_ptr(target), ([], []))
+                g[0].extend(src_ids)
+                g[1].extend(range(start, start + len(src_ids)))
+            elif via == "shm":
+                if start < 0 or start + len(src_ids) > int(target["shm_blocks"]):
+                    raise ValueError(f"extent [{start}, +{len(src_ids)}) outside the shm arena")
+                shm_jobs.append((src_ids, self._shm_peer(target), start))
+            else:
+                raise ValueError(f"unknown KV push backend {via!r}")
+        n = sum(len(j[0]) for j in jobs)
+        self.bytes_moved += n * self.block_bytes
+        self.transfers += len(jobs)
+        if not self.is_gpu:
+            for src_ids, arena, start in shm_jobs:
+                idx = torch.tensor(src_ids, dtype=torch.long)
+                arena.t[start:start + len(src_ids)].copy_(self.kv.index_select(0, idx))
+            if groups:
+                raise RuntimeError("xgmi push without a GPU")
+            return None
+        dev = self.kv.device
+        if after is not None:
+            self._stream.wait_event(after)
+        else:
+            self._stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(self._stream):
+            for ptr, (s_ids, d_ids) in groups.items():
+                s_t = torch.tensor(s_ids, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
+                d_t = torch.tensor(d_ids, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
+                ops.ext().copy_blocks(ptr, self.kv, s_t, d_t, self.block_bytes)
+            for src_ids, arena, start in shm_jobs:
+                idx = torch.tensor(src_ids, dtype=torch.long).pin_memory().to(dev, non_blocking=True)
+                arena.t[start:start + len(src_ids)].copy_(self.kv.index_select(0, idx), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+        return ev

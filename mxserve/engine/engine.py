@@ -184,8 +184,15 @@ class LLMEngine:
                     handle = self.runner.launch(so)
             else:
                 handle = self.runner.launch(so)
+            kv_ev = None
             for s in so.prefills:
                 self.num_prompt_computed += s.num_new_tokens
+                if s.sample and s.req.disagg_role == "prefill_only" and self.runner.is_gpu:
+                    if kv_ev is None:  # this step completes a prompt whose KV will be pushed
+                        import torch
+                        kv_ev = torch.cuda.Event()
+                        kv_ev.record()
+                    s.req.kv_ready = kv_ev
             self.num_steps += 1
         if tm is not None:
             t2 = time.perf_counter()

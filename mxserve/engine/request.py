@@ -98,6 +98,9 @@ class Request:
     # scheduled before step N's sampled ids reach the host; a decode's input is then read on the
     # device from the row's last sampled token)
     num_pending: int = 0
+    # prefill_only on the GPU: an event recorded right after the launch of the step that wrote the
+    # prompt's last KV block -- a KV push waits on it, not on everything queued behind that step
+    kv_ready: Optional[object] = None
 
     def __post_init__(self):
         self.seed = self.sampling.seed if self.sampling.seed is not None else _next_seed()

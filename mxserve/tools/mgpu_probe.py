@@ -488,7 +488,9 @@ class Probe:
                 res[name] = fn()
             except Exception as e:  # noqa: BLE001 - report, keep the other sections
                 traceback.print_exc()
-                res[name] = {"status": "failed", "error": repr(e)[:300]}
+                tb = traceback.extract_tb(e.__traceback__)
+                res[name] = {"status": "failed", "error": repr(e)[:300], "rank": self.rank,
+                             "where": [f"{os.path.basename(f.filename)}:{f.lineno} {f.name}" for f in tb[-4:]]}
             if isinstance(res[name], dict):
                 res[name]["wall_s"] = round(time.perf_counter() - t0, 1)
             try:

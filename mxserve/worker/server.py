@@ -438,6 +438,15 @@ class Worker:
         self.kv_quarantined += 1
         post.add_done_callback(done)
 
+    async def _push(self, loop, jobs: list, after) -> float:
+        """Issue a KV push (an executor thread: a first IPC mapping may take milliseconds) and wait
+        for its event without blocking any thread; returns seconds from issue to completion."""
+        t0 = time.perf_counter()
+        ev = await loop.run_in_executor(None, self.agent.push_async, jobs, after)
+        while ev is not None and not ev.query():
+            await asyncio.sleep(0.0002)
+        return time.perf_counter() - t0
+
     async def _prefill(self, body: dict) -> dict:
         """Prefill side: compute, push KV into the decode worker's pool, return the first token."""
         rid = body["request_id"]
@@ -461,17 +470,19 @@ class Worker:
         try:
             if len(src) != len(dst):
                 raise RuntimeError(f"block count mismatch: {len(src)} local vs {len(dst)} remote")
+            # the push waits (on the transfer stream) for the step that wrote this prompt's last KV
+            # block, not for whatever the engine queued after it; the event is polled here, so
+            # neither the engine thread nor an executor thread blocks on the copy
+            after = getattr(req, "kv_ready", None)
             if target["backend"] == "xgmi" and self.agent.backend == "xgmi" and target.get("arena_start") is not None:
                 try:
-                    xfer_s = await loop.run_in_executor(None, self.agent.push_xgmi, src, target,
-                                                        int(target["arena_start"]))
+                    xfer_s = await self._push(loop, [(src, target, int(target["arena_start"]), "xgmi")], after)
                     via = "xgmi"
                 except (RuntimeError, OSError) as e:  # the decode GPU's arena cannot be mapped here
                     log.warning("xGMI push to %s failed (%r); trying the shm / host paths", target.get("url"), e)
             if via is None and target.get("shm_start") is not None:
                 try:
-                    xfer_s = await loop.run_in_executor(None, self.agent.push_shm, src, target,
-                                                        int(target["shm_start"]))
+                    xfer_s = await self._push(loop, [(src, target, int(target["shm_start"]), "shm")], after)
                     via = "shm"
                 except OSError:  # the decode worker's /dev/shm is not ours (another pod / host)
                     pass

@@ -208,11 +208,15 @@ def test_bench_contract_cpu(mode, nproc, launcher, tmp_path):
     want = {"auto": "agg" if nproc == 1 else "both"}.get(mode, mode)
     assert d["config"]["mode"] == want
     if want == "both":
-        assert "value" in d["disagg"], d["disagg"]
+        # on a failure, both ranks' (and their probe processes') last log lines go with the assertion
+        assert "value" in d["disagg"], (d["disagg"], r.stderr[-4000:])
         assert d["agg"]["value"] == d["value"] and d["disagg"]["value"] > 0
         assert d["disagg"]["parallelism"] == f"disagg {nproc // 2}P+{nproc // 2}D"
     if want in ("both", "disagg"):  # hosted by the crash-isolated probe processes
-        assert d["disagg"]["ran_in"].startswith("probe"), d["disagg"]
+        assert d["disagg"].get("ran_in", "").startswith("probe"), (d["disagg"], r.stderr[-4000:])
+        bd = d["disagg"]["ttft_breakdown_p50_ms"]  # where disagg TTFT goes, component by component
+        assert set(bd) == {"decode_queue_ms", "to_prefill_ms", "prefill_ms", "transfer_ms", "admit_ms"}, bd
+        assert all(v is not None and v >= 0 for v in bd.values()), bd
         assert "disagg_headline" not in d["multi_gpu_probe"]
     if want == "disagg" and nproc == 3:  # disagg_plan: 1 prefill rank serving 2 decode ranks
         assert d["disagg"]["prefill_ranks"] == 1 and d["disagg"]["decode_ranks"] == 2, d["disagg"]
