@@ -916,6 +916,9 @@ def phase_served(a, ctx, agg: dict, info: dict, guard) -> dict:
                                    "itl_p50_delta_ms": round(res["itl_p50_ms"] - agg["itl_p50_ms"], 3)
                                    if res.get("itl_p50_ms") is not None and agg.get("itl_p50_ms") is not None
                                    else None}
+        it = (res.get("worker_engine") or {}).get("iteration_ms")
+        if it and res.get("itl_req_p50_ms") is not None:  # each running request gets one token per iteration
+            res["itl_req_p50_vs_worker_iteration"] = round(res["itl_req_p50_ms"] / it, 3)
     vlog(f"served: {res}")
     return res
 

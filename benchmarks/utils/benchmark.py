@@ -66,9 +66,13 @@ async def one_request(sess, url: str, model: str, prompt, osl: int, t_sched: flo
     if err or first is None:
         return {"ok": False, "error": err or "no tokens"}
     out_tokens = usage["completion_tokens"] if usage else n_chunks
+    # per-request ITL: the mean gap over the request's own tokens, (last - first) / (tokens - 1).  It
+    # does not depend on how chunks were grouped on the way (a reader that falls behind sees several
+    # chunks back to back: small chunk gaps, then one large one)
+    itl_req = (last - first) / (out_tokens - 1) if out_tokens > 1 else None
     return {"ok": True, "ttft": first - t_sched, "e2e": last - t_sched, "itl": gaps, "out": out_tokens, "chunks": n_chunks,
             "in": usage["prompt_tokens"] if usage else None, "start": t0, "sched": t_sched, "first": first,
-            "last": last}
+            "last": last, "itl_req": itl_req}
 
 
 def steady_window(results: list, t_a: float, t_b: float) -> dict:
@@ -92,10 +96,12 @@ def steady_window(results: list, t_a: float, t_b: float) -> dict:
         toks += (r["out"] - 1) * (hi - lo) / span + (1 if t_a <= r["first"] <= t_b else 0)
     ttft = [r["ttft"] for r in ok if t_a <= r["sched"] <= t_b]
     itl = [g for r in ok if t_a <= r["sched"] <= t_b for g in r["itl"]]
+    itl_req = [r["itl_req"] for r in ok if t_a <= r["sched"] <= t_b and r.get("itl_req") is not None]
     pct = lambda xs, q: float(np.percentile(xs, q)) * 1e3 if xs else None  # noqa: E731
     return {"steady_window_s": t_b - t_a, "steady_output_tok_per_s": toks / max(t_b - t_a, 1e-9),
             "steady_requests": len(ttft), "steady_ttft_ms_p50": pct(ttft, 50), "steady_ttft_ms_p90": pct(ttft, 90),
-            "steady_itl_ms_p50": pct(itl, 50), "steady_itl_ms_p90": pct(itl, 90)}
+            "steady_itl_ms_p50": pct(itl, 50), "steady_itl_ms_p90": pct(itl, 90),
+            "steady_itl_req_ms_p50": pct(itl_req, 50), "steady_itl_req_ms_p90": pct(itl_req, 90)}
 
 
 def summarize(results: list, wall: float, label: dict) -> dict:
@@ -104,12 +110,14 @@ def summarize(results: list, wall: float, label: dict) -> dict:
         return float(np.percentile(xs, q)) * 1e3 if xs else None
     ttft = [r["ttft"] for r in ok]
     itl = [g for r in ok for g in r["itl"]]
+    itl_req = [r["itl_req"] for r in ok if r.get("itl_req") is not None]
     e2e = [r["e2e"] for r in ok]
     out = sum(r["out"] for r in ok)
     return dict(label, requests=len(results), failed=len(results) - len(ok), duration_s=wall,
                 output_tok_per_s=out / wall if wall > 0 else 0.0, requests_per_s=len(ok) / wall if wall > 0 else 0.0,
                 ttft_ms_p50=pct(ttft, 50), ttft_ms_p90=pct(ttft, 90), ttft_ms_p99=pct(ttft, 99),
                 itl_ms_p50=pct(itl, 50), itl_ms_p90=pct(itl, 90), itl_ms_p99=pct(itl, 99),
+                itl_req_ms_p50=pct(itl_req, 50), itl_req_ms_p90=pct(itl_req, 90),
                 e2e_ms_p50=pct(e2e, 50), errors=[r["error"] for r in results if not r["ok"]][:5])
 
 
@@ -130,28 +138,67 @@ async def run_concurrency(url, model, conc, n, isl, osl, token_ids, vocab, seed)
     return summarize(results, wall, {"mode": "concurrency", "concurrency": conc, "isl": isl, "osl": osl})
 
 
+async def _fire(url, model, osl, sched, prompts) -> list:
+    """Send each prompt at its absolute perf_counter time in `sched`; the results in order."""
+    conn = aiohttp.TCPConnector(limit=0)
+    async with aiohttp.ClientSession(connector=conn, timeout=aiohttp.ClientTimeout(total=None)) as sess:
+        tasks = []
+        for t, p in zip(sched, prompts):
+            await asyncio.sleep(max(0.0, t - time.perf_counter()))
+            tasks.append(asyncio.create_task(one_request(sess, url, model, p, osl, t)))
+        return list(await asyncio.gather(*tasks))
+
+
+def _fire_shard(args) -> list:  # a client process (spawned: imports nothing of the caller's GPU state)
+    return asyncio.run(_fire(*args))
+
+
+def _ready() -> float:
+    return time.perf_counter()
+
+
+def client_procs() -> int:
+    """Client processes for open-loop points (BENCH_CLIENT_PROCS).  At ~20k streamed tokens/s one
+    asyncio process reads its sockets late and in bursts -- its chunk gaps and first-token times then
+    measure the client, not the server -- so the served bench spreads the streams over several."""
+    return max(1, int(os.environ.get("BENCH_CLIENT_PROCS", "1")))
+
+
 async def run_rate(url, model, rate, n, isl, osl, token_ids, vocab, seed, warmup_s: float = 0.0, gaps=None,
-                   prompts=None):
+                   prompts=None, procs: int = 0):
     """Open-loop Poisson arrivals.  gaps / prompts: an explicit arrival stream (bench.py's served
-    phase replays the engine-direct phase's exact stream) instead of one drawn from `seed`."""
+    phase replays the engine-direct phase's exact stream) instead of one drawn from `seed`.
+    procs > 1: request i is sent by client process i % procs at the same absolute schedule
+    (perf_counter is CLOCK_MONOTONIC, one clock for every process on the host)."""
     if prompts is None:
         rng = random.Random(seed)
         prompts = [synth_prompt(rng, isl, token_ids, vocab) for _ in range(n)]
     if gaps is None:
         gaps = np.random.default_rng(seed).exponential(1.0 / rate, size=n)
-    conn = aiohttp.TCPConnector(limit=0)
-    async with aiohttp.ClientSession(connector=conn, timeout=aiohttp.ClientTimeout(total=None)) as sess:
+    procs = procs or client_procs()
+    prompts = list(prompts)[:len(gaps)]
+    if procs <= 1:
         t0 = time.perf_counter()
-        tasks = []
-        t = t0
-        for p, g in zip(prompts, gaps):
-            t += g
-            await asyncio.sleep(max(0.0, t - time.perf_counter()))
-            tasks.append(asyncio.create_task(one_request(sess, url, model, p, osl, t)))
-        t_arrivals_end = time.perf_counter()
-        results = await asyncio.gather(*tasks)
-        wall = time.perf_counter() - t0
-    s = summarize(list(results), wall, {"mode": "request_rate", "request_rate": rate, "isl": isl, "osl": osl})
+        sched = (t0 + np.cumsum(np.asarray(gaps[:len(prompts)], dtype=np.float64))).tolist()
+        results = await _fire(url, model, osl, sched, prompts)
+    else:
+        import concurrent.futures
+        import multiprocessing
+        with concurrent.futures.ProcessPoolExecutor(procs, mp_context=multiprocessing.get_context("spawn")) as ex:
+            list(ex.map(_ready, range(procs)))  # every client process up (imports done) before t0
+            loop = asyncio.get_running_loop()
+            t0 = time.perf_counter() + 0.2
+            sched = (t0 + np.cumsum(np.asarray(gaps[:len(prompts)], dtype=np.float64))).tolist()
+            futs = [loop.run_in_executor(ex, _fire_shard, (url, model, osl, sched[k::procs], prompts[k::procs]))
+                    for k in range(procs)]
+            shards = await asyncio.gather(*futs)
+        results = [None] * len(prompts)
+        for k, sh in enumerate(shards):
+            results[k::procs] = sh
+    t_arrivals_end = sched[-1] if sched else t0
+    wall = max([r["last"] for r in results if r.get("ok")] + [time.perf_counter() if procs <= 1 else t0]) - t0
+    s = summarize(list(results), wall, {"mode": "request_rate", "request_rate": rate, "isl": isl, "osl": osl,
+                                        "client_procs": procs})
     if warmup_s > 0 and t0 + warmup_s < t_arrivals_end:
         s.update(steady_window(list(results), t0 + warmup_s, t_arrivals_end))
     return s
