@@ -747,7 +747,16 @@ def engine_args(a, ctx, **kw):
     if not ctx.on_gpu:  # plumbing run only (CPU container): keep it tiny
         args = args.replace(model="tiny-llama", max_model_len=1024, cpu_num_blocks=4096)
     elif ctx.shared_gpu:  # functional run: ranks share a GPU, split its memory
-        args = args.replace(num_gpu_blocks=int(os.environ.get("MXS_BENCH_SHARED_BLOCKS", "40000")))
+        blocks = int(os.environ.get("MXS_BENCH_SHARED_BLOCKS", "40000"))
+        role = kw.get("disagg_mode")
+        if role in ("prefill", "decode"):
+            # by role: a decode rank holds the running set of world / D GPUs' arrivals (at 40 req/s a
+            # 1P+1D decode rank runs ~140 requests x 282 blocks: 40,000 blocks refused reservations and
+            # queued arrivals for ~50 ms); a prefill rank holds only the prompts in flight
+            p_ranks, d_ranks, _ = disagg_plan(a, ctx.world)
+            blocks = (min(2 * blocks, blocks * ctx.world // max(1, d_ranks)) if role == "decode"
+                      else max(8192, blocks // 4))
+        args = args.replace(num_gpu_blocks=blocks)
     if a.num_gpu_blocks and ctx.on_gpu:
         args = args.replace(num_gpu_blocks=a.num_gpu_blocks)
     return args

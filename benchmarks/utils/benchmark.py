@@ -153,7 +153,7 @@ def _fire_shard(args) -> list:  # a client process (spawned: imports nothing of 
     return asyncio.run(_fire(*args))
 
 
-def _ready() -> float:
+def _ready(_i: int = 0) -> float:
     return time.perf_counter()
 
 

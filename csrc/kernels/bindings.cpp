@@ -52,6 +52,8 @@ bool launch_splitk_rope_and_cache(bf16_t*, const float*, int, const int64_t*, co
                                   float, hipStream_t);
 bool launch_prefill_gemm(bf16_t*, float*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int,
                          hipStream_t);
+bool launch_gemm_w4(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, int, hipStream_t,
+                    const bf16_t*, int);
 bool launch_gemm_pf(bf16_t*, const bf16_t*, const bf16_t*, int, int, int, int, int, int, float*, long, int*, int,
                     const int*, int, int, int, hipStream_t, const bf16_t*, int, bool, float, int);
 int pf_plan(int, int, int, int, int, int, int*, int*, int*, int);
@@ -488,6 +490,29 @@ bool gemm_pf(at::Tensor out, at::Tensor x, at::Tensor w, int64_t epi, at::Tensor
                              static_cast<float>(eps), static_cast<int>(trows));
 }
 
+// K05-K08 at prefill chunks, four-wave form (csrc/kernels/gemm_w4.hip, data-parallel persistent): the
+// epilogues of gemm_pf (epi 0 / 1 SwiGLU / 2 residual), no row scale, no stream-K.
+bool gemm_w4(at::Tensor out, at::Tensor x, at::Tensor w, int64_t epi, int64_t num_cu,
+             c10::optional<at::Tensor> resid) {
+  CHECK_CUDA(x); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(out); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "2-D operands");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(x.size(1) == K && out.size(0) == M && out.size(1) == (epi == 1 ? N / 2 : N), "shape mismatch");
+  if (x.stride(1) != 1 || out.stride(1) != 1 || M > (1 << 24)) return false;
+  const bf16_t* R = nullptr;
+  int ldr = 0;
+  if (epi == 2) {
+    TORCH_CHECK(resid.has_value(), "epi 2 needs resid");
+    CHECK_BF16((*resid));
+    TORCH_CHECK(resid->dim() == 2 && resid->size(0) == M && resid->size(1) == N && resid->stride(1) == 1,
+                "resid shape");
+    R = bf(*resid);
+    ldr = static_cast<int>(resid->stride(0));
+  }
+  return mxs::launch_gemm_w4(bf(out), bf(x), bf(w), M, N, K, x.stride(0), out.stride(0), epi, num_cu, stream(), R,
+                             ldr);
+}
+
 // Grouped decode form of decode_gemm (K16 at decode batches): w [E, N, K], x = routed rows sorted by
 // expert (offs = moe_align offsets), rows_max = the most rows one expert can hold (tokens).  Output
 // as moe_grouped_gemm: out [rows, N or N/2] (splitk 1) or fp32 partials [splitk, rows, N].
@@ -626,6 +651,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("reduce") = true);
   m.def("prefill_gemm", &prefill_gemm, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("part"), pybind11::arg("bm"), pybind11::arg("splitk"));
+  m.def("gemm_w4", &gemm_w4, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("epi"),
+        pybind11::arg("num_cu"), pybind11::arg("resid") = pybind11::none());
   m.def("gemm_pf", &gemm_pf, pybind11::arg("out"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("epi"),
         pybind11::arg("slab"), pybind11::arg("cnt"), pybind11::arg("tile_map"), pybind11::arg("num_cu"),
         pybind11::arg("min_iters") = 16, pybind11::arg("resid") = pybind11::none(),

@@ -261,6 +261,23 @@ def pf_tile_map(ntm: int, ntn: int, device, gm: int = 8) -> torch.Tensor:
     return t
 
 
+def gemm_w4(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None,
+            resid: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """Prefill GEMM, four-wave form (csrc/kernels/gemm_w4.hip: 128 x 128 per wave, data-parallel
+    persistent): epi 0 x @ w.T, epi 1 SwiGLU over w = [gate; up], epi 2 resid + x @ w.T (out may be
+    resid).  None when the shape is not supported (N % 256, K % 64)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if M == 0 or N % 256 or K % 64 or w.shape[1] != K:
+        return None
+    if out is None:
+        out = torch.empty(M, N // 2 if epi == 1 else N, dtype=x.dtype, device=x.device)
+    ncu = _pf_workspace(x.device)[2]
+    if not ext().gemm_w4(out, x, w, epi, ncu, resid):
+        return None
+    return out
+
+
 def gemm_pf(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.Tensor] = None,
             min_iters: int = 16, resid: Optional[torch.Tensor] = None, row_scale: bool = False,
             eps: float = 1e-5, trows: int = 256) -> Optional[torch.Tensor]:

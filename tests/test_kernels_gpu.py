@@ -1329,3 +1329,31 @@ def test_paged_decode_long_context(gpu):
         k, v = _gather_seq_kv(kv[:, 0], bt[i].to(gpu), L)
         exp = _attn_fp32(q[i:i + 1], k, v, torch.tensor([L - 1], device=gpu), scale)
         _close(out[i:i + 1], exp, 0.02, 0.02, f"long-context decode L={L}")
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(4240, 2048, 2048, 0), (4240, 3072, 2048, 0), (6592, 2048, 8192, 2),
+                                       (4240, 16384, 2048, 1), (1, 256, 64, 0), (300, 512, 192, 1),
+                                       (777, 768, 4096, 2), (8192, 2048, 2048, 2), (2048, 4096, 1024, 1)])
+def test_gemm_w4(gpu, M, N, K, epi):
+    """Four-wave prefill GEMM (csrc/kernels/gemm_w4.hip) vs fp32: several tiles per workgroup (the
+    k-block stream runs across tiles), partial last token tile, SwiGLU and residual epilogues, the
+    residual form in place; bitwise repeatable."""
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K + epi)
+    x = (torch.rand(M, K, device=gpu, generator=g) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=gpu, generator=g) * 2 - 1) * 2 * K ** -0.5).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    r = None
+    if epi == 1:
+        ref = torch.nn.functional.silu(ref[:, :N // 2]) * ref[:, N // 2:]
+    elif epi == 2:
+        r = (torch.randn(M, N, device=gpu, generator=g) * 2).to(torch.bfloat16)
+        ref = ref + r.float()
+    out = torch.full((M, N // 2 if epi == 1 else N), float("nan"), device=gpu, dtype=torch.bfloat16)
+    assert ops.gemm_w4(x, w, epi, out, resid=r) is not None
+    _close(out, ref, atol=3e-2, rtol=2e-2, name=f"gemm_w4 {M}x{N}x{K} epi{epi}")
+    again = ops.gemm_w4(x, w, epi, None, resid=r)
+    assert torch.equal(again, out)
+    if epi == 2:  # in place on the residual stream
+        rr = r.clone()
+        assert ops.gemm_w4(x, w, 2, rr, resid=rr) is not None
+        assert torch.equal(rr, out)
