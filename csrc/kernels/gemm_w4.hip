@@ -67,12 +67,12 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const W4Args a) {
   constexpr int STG = 32768, XO = 16384;  // stage bytes (a 32-deep k-block); X image offset in a stage
   __shared__ __attribute__((aligned(16))) char smem[4 * STG];
 
-  const int G = gridDim.x, nk = a.nk;  // nk: 32-deep k-blocks
+  const int G = gridDim.x, nk = a.nk;  // one workgroup per tile; nk: 32-deep k-blocks
+  // blocks b and b + 8 share an XCD: give each XCD a contiguous range of the tile order, so the 32
+  // workgroups an XCD runs at a time share W and X panels in its L2
   const int bid = blockIdx.x, xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
   const int o = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int my_tiles = o < a.ntiles ? (a.ntiles - 1 - o) / G + 1 : 0;
-  if (my_tiles == 0) return;  // the whole workgroup leaves together
-  const int ns = my_tiles * nk;
+  const int ns = nk;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -103,26 +103,18 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const W4Args a) {
   const long w_bytes = 2L * a.K * a.nrows_w;
   typedef __attribute__((address_space(3))) void lds_t;
 
-  // the DMA stream's position (tile, k-block) and the compute stream's, advanced one k-block a call
-  int d_ti = 0, d_k = 0, d_tm, d_tn, e_tm, e_tn;
-  w4_tile(o, a.ntm, a.ntn, d_tm, d_tn);
-  e_tm = d_tm;
-  e_tn = d_tn;
+  int tm, tn;
+  w4_tile(o, a.ntm, a.ntn, tm, tn);
   // the 8 DMA pieces (4 W, 4 X) this wave issues for stream position c, into stage c & 3
+  const long woff = 2L * tn * WSTEP * a.K;
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(a.W) + woff / 2, static_cast<short>(0),
+      static_cast<int>(min(w_bytes - woff, 0x7FFFFFFFL)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(a.X) + static_cast<size_t>(tm) * 256 * a.ldx, static_cast<short>(0),
+      (a.M - tm * 256) * a.ldx * 2, 0x00020000);
   auto dma = [&](int c) {
-    const int tm = d_tm, tn = d_tn, k = d_k;
-    if (++d_k == nk) {
-      d_k = 0;
-      ++d_ti;
-      w4_tile(d_ti * G + o, a.ntm, a.ntn, d_tm, d_tn);
-    }
-    const long woff = 2L * tn * WSTEP * a.K;
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<bf16_t*>(a.W) + woff / 2, static_cast<short>(0),
-        static_cast<int>(min(w_bytes - woff, 0x7FFFFFFFL)), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<bf16_t*>(a.X) + static_cast<size_t>(tm) * 256 * a.ldx, static_cast<short>(0),
-        (a.M - tm * 256) * a.ldx * 2, 0x00020000);
+    const int k = c;
     char* st = smem + (c & 3) * STG;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -184,6 +176,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const W4Args a) {
             ov.x = w4_pack(w4_silu(gv[4 * g]) * uv[4 * g], w4_silu(gv[4 * g + 1]) * uv[4 * g + 1]);
             ov.y = w4_pack(w4_silu(gv[4 * g + 2]) * uv[4 * g + 2], w4_silu(gv[4 * g + 3]) * uv[4 * g + 3]);
             *reinterpret_cast<uint2*>(yr + n) = ov;
+            __builtin_amdgcn_sched_barrier(0);  // one group of accumulators at a time: no mass AGPR reads
           }
         }
       } else {
@@ -205,6 +198,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const W4Args a) {
             ov.x = w4_pack(v[4 * g] + r0, v[4 * g + 1] + r1);
             ov.y = w4_pack(v[4 * g + 2] + r2, v[4 * g + 3] + r3);
             *reinterpret_cast<uint2*>(yr + n) = ov;
+            __builtin_amdgcn_sched_barrier(0);  // one group of accumulators at a time: no mass AGPR reads
           }
         }
       }
@@ -228,60 +222,42 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const W4Args a) {
   W4_BAR();
   rd(fa0, fb0, 0, 0);
 
-  bool stores_pending = false;  // the previous position ended a whole tile: 64 / 32 stores are in flight
-  int c = 0;
-  for (int ti = 0; ti < my_tiles; ++ti) {
 #pragma unroll
-    for (int f = 0; f < 4; ++f)
+  for (int f = 0; f < 4; ++f)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[f][t] = float16_{};
-    for (int kb = 0; kb < nk; ++kb, ++c) {
-      const int s = c & 3;
-      // half 1: DMA of position c + 3 into the stage read at c - 1 (every wave passed the barrier after
-      // those reads), the reads of k-step 1, the MFMAs of k-step 0
-      if (c + 3 < ns) dma(c + 3);
-      rd(fa1, fb1, s, 1);
-      mma(fa0, fb0);
+    for (int t = 0; t < 4; ++t) acc[f][t] = float16_{};
+  for (int c = 0; c < ns; ++c) {
+    const int s = c & 3;
+    // half 1: DMA of k-block c + 3 into the stage read at c - 1 (every wave passed the barrier after
+    // those reads), the reads of k-step 1, the MFMAs of k-step 0
+    if (c + 3 < ns) dma(c + 3);
+    rd(fa1, fb1, s, 1);
+    mma(fa0, fb0);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {  // one MFMA, one DMA piece, one fragment read, ...
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      // position c + 1 landed: the younger positions' pieces (8 each, issued at c - 1 and c) and an
-      // epilogue's stores (issued between them) may stay in flight; the count runs oldest-first
-      // (stores: 64 plain / 32 SwiGLU, counted only for whole tiles; vmcnt tops out at 63)
-      if (c + 3 < ns) {
-        if (!stores_pending) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else if constexpr (EPI == W4_EPI_SWIGLU) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-      } else if (c + 2 < ns) {
-        if (!stores_pending) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if constexpr (EPI == W4_EPI_SWIGLU) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      stores_pending = false;
-      W4_BAR();  // position c + 1 visible in its stage; every wave is done reading stage s
-      // half 2: the reads of position c + 1's k-step 0 beside the MFMAs of k-step 1
-      if (c + 1 < ns) rd(fa0, fb0, (c + 1) & 3, 0);
-      mma(fa1, fb1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {  // two MFMAs, one fragment read, ...
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+    for (int i = 0; i < 8; ++i) {  // one MFMA, one DMA piece, one fragment read, ...
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    epilogue(e_tm, e_tn);
-    // a whole tile (no row past M skipped) issued a known count of stores, the youngest VMEM ops; the
-    // residual form's loads are waited for inside the epilogue, so it counts as drained
-    stores_pending = EPI != W4_EPI_RESID && e_tm * 256 + 256 <= a.M;
-    w4_tile((ti + 1) * G + o, a.ntm, a.ntn, e_tm, e_tn);
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // k-block c + 1 landed: the pieces of c + 2 and c + 3 (8 each, issued at c - 1 and c) may stay in
+    // flight; the count runs oldest-first
+    if (c + 3 < ns) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (c + 2 < ns) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    W4_BAR();  // k-block c + 1 visible in its stage; every wave is done reading stage s
+    // half 2: the reads of k-block c + 1's k-step 0 beside the MFMAs of k-step 1
+    if (c + 1 < ns) rd(fa0, fb0, (c + 1) & 3, 0);
+    mma(fa1, fb1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // two MFMAs, one fragment read, ...
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
+  epilogue(tm, tn);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #undef W4_BAR
 }
@@ -313,8 +289,8 @@ bool launch_gemm_w4(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, i
   a.ntiles = ntiles;
   a.inter = epi == W4_EPI_SWIGLU ? N / 2 : 0;
   a.nrows_w = N;
-  const int G = std::min(num_cu, ntiles);
-  const dim3 g(G), b(256);
+  (void)num_cu;  // one workgroup per tile; the LDS (128 KB) admits one per CU
+  const dim3 g(ntiles), b(256);
   if (epi == W4_EPI_SWIGLU) hipLaunchKernelGGL(gemm_w4_kernel<W4_EPI_SWIGLU>, g, b, 0, s, a);
   else if (epi == W4_EPI_RESID) hipLaunchKernelGGL(gemm_w4_kernel<W4_EPI_RESID>, g, b, 0, s, a);
   else hipLaunchKernelGGL(gemm_w4_kernel<W4_EPI_NONE>, g, b, 0, s, a);
