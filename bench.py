@@ -613,11 +613,11 @@ def run_disagg_decode(a, eng, sp, drv, barrier, agree, conns: list) -> float:
     inflight: dict = {}
     load = [0] * len(conns)
 
-    def step():
+    def pump():
+        """Arrivals due -> reserved and sent to a prefill rank; finished prefills -> landed and admitted.
+        Runs every loop pass and, as the engine's late-admission hook, once more right before the next
+        step is scheduled: a prefill that finished while a step ran joins the very next step."""
         backlog.extend(drv.due())
-        if not eng.has_unfinished() and not backlog and not inflight:
-            drv.wait_next()
-            backlog.extend(drv.due())
         while backlog:
             rid, toks = backlog[0]
             req = eng.reserve_remote_prefill(toks, sp, rid)
@@ -652,14 +652,22 @@ def run_disagg_decode(a, eng, sp, drv, barrier, agree, conns: list) -> float:
                     drv.breakdown.append((t_sent - drv.arrival_of[rid], t_sched - t_sent, t_first - t_sched,
                                           t_done - t_first, now - t_done))
                 drv.token(rid, now, out.finished)
+
+    eng.admit_hook = pump
+
+    def step():
+        backlog.extend(drv.due())
+        if not eng.has_unfinished() and not backlog and not inflight:
+            drv.wait_next()
+        pump()
         if eng.has_unfinished():
             outs = eng.step()
             now = time.perf_counter()
             for o in outs:
                 drv.token(o.request_id, now, o.finished)
-        elif inflight:  # nothing to decode yet: block until a prefill lands (or an arrival is due)
+        elif inflight:  # nothing to decode yet: wait briefly for a prefill to land (arrivals keep coming)
             if len(conns) == 1:
-                conns[0].poll(0.02)
+                conns[0].poll(0.002)
             else:
                 time.sleep(0.0005)
         drv.report()

@@ -28,7 +28,7 @@ from typing import Optional
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 # load-generator processes (benchmarks/utils/benchmark.py run_rate): ~22k streamed tokens/s is more
 # than one asyncio reader keeps up with, and a late reader shows up as bursty chunk gaps and TTFT
-CLIENT_PROCS = int(os.environ.get("MXS_SERVED_CLIENT_PROCS", "4"))
+CLIENT_PROCS = int(os.environ.get("MXS_SERVED_CLIENT_PROCS", "2"))
 
 
 def _free_port() -> int:

@@ -255,7 +255,7 @@ print("RESULT " + json.dumps(info), flush=True)
 """
 
 
-def _run_engine(tp: int, tmp_path) -> dict:
+def _run_engine(tp: int, tmp_path, fused_tp1: bool = False) -> dict:
     # the decode-GEMM tuner picks kernels by timing (noise-dependent per run); both sides stay on
     # hipBLASLt so the comparison isolates the TP path (the kernel has its own numerics tests).  The
     # TP = 1 fused prefill chain (llama.py _forward_pf: residual added inside the o / down GEMM, one
@@ -263,6 +263,8 @@ def _run_engine(tp: int, tmp_path) -> dict:
     # (test_engine_gpu.py test_fused_prefill_chain_matches_unfused)
     env = dict(os.environ, MXS_ROOT=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=ROOT, MXS_DECODE_GEMM="off",
                MXS_PF_FUSED="0")
+    if fused_tp1:  # the default TP = 1 chain (fused prefill on)
+        env.pop("MXS_PF_FUSED", None)
     env.pop("MXS_CUSTOM_AR", None)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
@@ -283,3 +285,16 @@ def test_tp4_engine_on_one_gpu_matches_tp1(tmp_path):
     # greedy bf16: a 4-way sharded reduction order may flip a near-tied argmax late in a sequence
     assert all(ra[:4] == rb[:4] for ra, rb in zip(ref["tokens"], got["tokens"])), (ref, got)
     assert same >= 0.9 * total, (ref, got)
+
+
+def test_tp4_engine_matches_the_default_tp1_chain(tmp_path):
+    """TP = 4 against the TP = 1 engine as it runs by default (fused prefill chain
+    on: RMSNorm inside the consumer GEMMs, residual adds inside o / down).  The two differ in bf16
+    rounding order on both sides, so the check is on greedy tokens: every prompt's first tokens agree
+    and most of the rest."""
+    ref = _run_engine(1, tmp_path, fused_tp1=True)
+    got = _run_engine(4, tmp_path)
+    same = sum(a == b for ra, rb in zip(ref["tokens"], got["tokens"]) for a, b in zip(ra, rb))
+    total = sum(len(x) for x in ref["tokens"])
+    assert all(ra[:2] == rb[:2] for ra, rb in zip(ref["tokens"], got["tokens"])), (ref, got)
+    assert same >= 0.8 * total, (ref, got)

@@ -1293,10 +1293,11 @@ def _attn_fp32(q, k, v, qpos, scale):
     return torch.bmm(torch.softmax(s, dim=-1), vv).permute(1, 0, 2)  # [T, Hq, D]
 
 
-@pytest.mark.parametrize("var", [None, 128, 256])
+@pytest.mark.parametrize("var", [None, 0, 128, 256, "v2"])
 def test_paged_prefill_long_context(gpu, var):
     """A 1024-token chunk after 64,000 cached tokens (chunked prefill at long context) next to a fresh
-    3,000-token prompt, every launch form, against fp32 attention over the gathered cache."""
+    3,000-token prompt, every launch form -- the automatic pick, the explicit default (VAR 0), split-KV
+    (128), paired tiles (256) and the v2 kernel -- against fp32 attention over the gathered cache."""
     D, G, hkv = 64, 4, 2
     specs = [(64000, 1024), (0, 3000)]
     seq_lens = [c + n for c, n in specs]
@@ -1308,7 +1309,8 @@ def test_paged_prefill_long_context(gpu, var):
     scale = 1 / math.sqrt(D)
     out = ops.paged_attention_prefill(q, kv[:, 0], bt.to(gpu), torch.tensor(qsl, dtype=torch.int32, device=gpu),
                                       torch.tensor(seq_lens, dtype=torch.int32, device=gpu), scale,
-                                      max(n for _, n in specs), version=0 if var is None else 0x100 + var)
+                                      max(n for _, n in specs),
+                                      version=0 if var is None else (2 if var == "v2" else 0x100 + var))
     for i, (c, n) in enumerate(specs):
         k, v = _gather_seq_kv(kv[:, 0], bt[i].to(gpu), c + n)
         exp = _attn_fp32(q[qsl[i]:qsl[i + 1]], k, v, torch.arange(c, c + n, device=gpu), scale)
