@@ -430,7 +430,14 @@ class Driver:
             self.c["tokens"] += 1
 
     def sample(self, running: int) -> None:
-        self.hist.append((time.perf_counter(), running, self.nxt, self.finished))
+        now = time.perf_counter()
+        self.hist.append((now, running, self.nxt, self.finished))
+        if len(self.hist) > 20000:  # the steady-state test reads the last two windows (seconds); bound
+            # the list (and is_steady's array of it) when a stalled engine makes step() calls cheap
+            import bisect
+            cut = bisect.bisect_left(self.hist, (now - 60.0,))
+            if cut > 0:
+                del self.hist[:min(cut, len(self.hist) - 1000)]
 
     def is_steady(self, window: float) -> bool:
         """Running set flat over two consecutive windows, completions ~= arrivals in the last, and two

@@ -206,6 +206,14 @@ class Scheduler:
                 if n <= 0:
                     break
             if not self.kv.allocate_slots(req, n):
+                # a waiting request holds no blocks: give back the cached prefix get_computed_blocks
+                # pinned for it.  Kept, it stays pinned while the request waits; under overload (every
+                # running request preempted, each re-queued one pinning its own cached prompt at the
+                # head in turn) those pins exhausted the pool with nothing running to free it -- a
+                # deadlock seen with 8 engines on one GPU (profiles/r6/overload_deadlock/)
+                if req.block_ids:
+                    self.kv.free(req)
+                req.num_computed_tokens = req.num_cached_tokens = 0
                 break
             self.waiting.popleft()
             if req.scheduled_time is None:

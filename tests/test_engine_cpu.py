@@ -249,3 +249,29 @@ def test_collective_fault_discards_and_recomputes(async_sched, blocks, budget):
     assert calls["recovered"] == len(fault_at) == eng.stats()["custom_ar_timeouts"]
     assert eng.kv.num_free() == blocks and eng.kv.check_invariants()
     assert not eng.requests and eng._inflight is None
+
+
+@pytest.mark.parametrize("async_sched", [False, True])
+def test_overload_with_preemption_never_deadlocks(async_sched):
+    """Arrivals far beyond capacity into a small pool, prefix caching on: running requests are
+    preempted, and a re-queued one finds its own prompt in the prefix cache.  A waiting request that
+    cannot be admitted must give back the cached blocks it was handed -- kept, they stayed pinned
+    while it waited, until pinned prefixes filled the pool with nothing running (the 8-rank one-GPU
+    rehearsal hung this way, 0 requests finished in 90 s)."""
+    import random as _r
+    ea = EngineArgs(model="tiny-llama", device="cpu", cpu_num_blocks=252, max_model_len=1024,
+                    max_num_batched_tokens=384, max_num_seqs=45, load_format="random", seed=3,
+                    async_scheduling=async_sched)
+    e = LLMEngine(ea)
+    e.check_invariants = True
+    rng = _r.Random(1)
+    finished = idle = worst_idle = 0
+    for i in range(300):
+        e.add_request([rng.randrange(3, 500) for _ in range(250)],
+                      SamplingParams(max_tokens=250, temperature=1.0, ignore_eos=True), request_id=f"r{i}")
+        outs = e.step()
+        finished += sum(o.finished for o in outs)
+        idle = 0 if outs else idle + 1
+        worst_idle = max(worst_idle, idle)
+    assert e.scheduler.num_preemptions > 0  # the regime the test is about
+    assert worst_idle < 20, (finished, worst_idle, len(e.scheduler.waiting), e.kv.num_free())
