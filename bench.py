@@ -308,12 +308,20 @@ def finish_probe(p, guard: Guard, ctx):
     if p is None:
         return None
     port = ctx.gather([float(_free_port()) if ctx.rank == 0 else 0.0])[0, 0]
+    # ranks > 0 hand their probe over ("detach": it no longer exits with its bench rank) and leave:
+    # only rank 0's probe reports, and a rank that stays holds a GPU context and its memory while the
+    # probe runs -- on a node every process maps every GPU, so N ranks + N probes is 2N processes on
+    # each GPU against the pool's limit of 16 per GPU, and the probe's engines want the memory
+    detach = ctx.rank != 0
     try:
-        p.stdin.write(f"go {int(port)}\n".encode())
+        p.stdin.write(f"go {int(port)}{' detach' if detach else ''}\n".encode())
         p.stdin.close()
     except OSError:
         pass
     p.stdin = None  # closed above: communicate() must not flush it again
+    if detach:
+        guard.children.remove(p)  # not ours to kill any more
+        return None
     timeout_s = max(1.0, guard.remaining() - 10.0)
     try:
         out, _ = p.communicate(timeout=timeout_s)
@@ -1053,7 +1061,8 @@ def main():
         line["wall_s"] = round(time.time() - _WALL0, 1)
         guard.emit(line)
     if world > 1:
-        ctx.dist.barrier()
+        if probe is None:  # with a probe, ranks > 0 left at finish_probe: no final barrier
+            ctx.dist.barrier()
         ctx.dist.destroy_process_group()
     return 0
 

@@ -507,6 +507,7 @@ class Probe:
 
 _EMIT_LOCK = None
 _EMITTED = []
+_DETACHED = False
 
 
 def _emit(result_out, res: dict) -> None:
@@ -535,7 +536,7 @@ def _watch(result_out, probe_box: list, t0: float) -> None:
     def loop():
         while True:
             time.sleep(0.5)
-            if os.getppid() != ppid:
+            if os.getppid() != ppid and not _DETACHED:  # a detached probe outlives its bench rank
                 os._exit(1)
             if deadline and time.time() > deadline:
                 break
@@ -566,6 +567,9 @@ def main() -> int:
         return 0
     if len(line) > 1:  # the rendezvous port rank 0's bench process picked
         os.environ["MASTER_PORT"] = line[1]
+    if "detach" in line[2:]:  # bench ranks > 0 leave once they have released their probe
+        global _DETACHED
+        _DETACHED = True
     t0 = time.perf_counter()
     try:
         p = Probe()
