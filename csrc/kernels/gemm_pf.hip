@@ -92,7 +92,7 @@ struct PfSeg {
 template <int EPI, bool RS, int TMF>
 __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
   constexpr int HT = 16384, QT = 8192, KT = 4 * HT, XB = 2 * HT;  // W halves at 0 / HT, X halves at XB
-  // token tile: TMF 16-row fragments per wave row-half, 32 TMF rows (256, 192, 160, 128); a wave's
+  // token tile: TMF 16-row fragments per wave row-half, 32 TMF rows (256, 224, 192, 160, 128); a wave's
   // fragments split over the two phases of a k-tile as P0 + P1.  The X image keeps its four 64-row
   // quarters (h, t): quarter (wr, hb) holds the P_hb fragments wave row-half wr multiplies in phase
   // hb -- tile rows 16 TMF h + 16 P0 t + [0, 16 P_t) -- so a phase reads only its own quarters and the
@@ -560,12 +560,12 @@ __global__ void __launch_bounds__(512, 1) gemm_pf_kernel(const PfArgs a) {
 }
 
 // Launch geometry: grid = min(CUs, work / min_iters) workgroups; full rounds of tiles data-parallel,
-// the rest stream-K.  trows: token-tile height (256, 192, 160 or 128 rows).  Returns the grid (0 = not
+// the rest stream-K.  trows: token-tile height (256, 224, 192, 160 or 128 rows).  Returns the grid (0 = not
 // launched: shape unsupported).
 int pf_plan(int M, int N, int K, int epi, int num_cu, int min_iters, int* dp_rounds, int* sk_tiles, int* grid,
             int trows) {
   if (M <= 0 || K % 64 != 0 || N % 256 != 0) return 0;
-  if (trows != 256 && trows != 192 && trows != 160 && trows != 128) return 0;
+  if (trows != 256 && trows != 224 && trows != 192 && trows != 160 && trows != 128) return 0;
   const int ntm = (M + trows - 1) / trows, ntn = N / 256;
   const int T = ntm * ntn, nk = K / 64;
   const long work = static_cast<long>(T) * nk;
@@ -636,6 +636,7 @@ bool launch_gemm_pf(bf16_t* Y, const bf16_t* X, const bf16_t* W, int M, int N, i
 #define MXS_PF(E, RSV, T) hipLaunchKernelGGL((gemm_pf_kernel<E, RSV, T>), g, b, 0, s, a)
 #define MXS_PF_ROWS(E)              \
   switch (trows) {                  \
+    case 224: MXS_PF(E, false, 7); break; \
     case 192: MXS_PF(E, false, 6); break; \
     case 160: MXS_PF(E, false, 5); break; \
     case 128: MXS_PF(E, false, 4); break; \

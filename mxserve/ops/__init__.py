@@ -285,7 +285,7 @@ def gemm_pf(x: torch.Tensor, w: torch.Tensor, epi: int = 0, out: Optional[torch.
     gate.T) * (x @ up.T) with w = [gate; up], epi 2 resid + x @ w.T (out may be resid: in place).
     row_scale (epi 0 / 1): every row of the product is scaled by rsqrt(mean(x_row^2) + eps), i.e.
     RMSNorm(x) @ w'.T with the norm weight folded into w' (fold_norm_weight).  None when the shape is
-    not supported.  trows: token-tile height (256, 192, 160, 128): fewer rows per tile fill the CUs
+    not supported.  trows: token-tile height (256, 224, 192, 160, 128): fewer rows per tile fill the CUs
     better when a 256-row tiling leaves a partial last round (e.g. 6,656 rows x 2,048 columns: 208
     tiles of 256 rows on 256 CUs, 240 of 224... 256 of 128 would be one full round at half the work
     per tile)."""

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 from mxserve import ops  # noqa: E402
 
 SHAPES = [("qkv", 3072, 2048, 0), ("o", 2048, 2048, 2), ("gate_up", 16384, 2048, 1), ("down", 2048, 8192, 2)]
-PF_CFGS = [(256, 0), (256, 8), (256, 16), (192, 0), (192, 32), (160, 0), (128, 0)]
+PF_CFGS = [(256, 0), (256, 8), (256, 16), (224, 0), (224, 16), (192, 0), (192, 32), (160, 0), (128, 0)]
 
 
 def timed(fn, iters=10):

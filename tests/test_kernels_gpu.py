@@ -1126,7 +1126,7 @@ def test_gemm_pf(gpu, M, N, K, epi):
     ref = x.float() @ w.float().t()
     if epi == 1:
         ref = torch.nn.functional.silu(ref[:, :N // 2]) * ref[:, N // 2:]
-    for tr, mi in [(256, 4), (256, 16), (256, 64), (192, 0), (192, 8), (160, 0), (160, 16), (128, 0), (128, 8)]:
+    for tr, mi in [(256, 4), (256, 16), (256, 64), (224, 0), (224, 16), (192, 0), (192, 8), (160, 0), (160, 16), (128, 0), (128, 8)]:
         out = torch.full((M, N // 2 if epi else N), float("nan"), device=gpu, dtype=torch.bfloat16)
         assert ops.gemm_pf(x, w, epi, out, mi, trows=tr) is not None
         _close(out, ref, atol=2e-2, rtol=2e-2, name=f"gemm_pf {M}x{N}x{K} epi{epi} rows {tr} min_iters {mi}")
@@ -1171,7 +1171,7 @@ def test_gemm_pf_residual(gpu, M, N, K):
     w = (torch.randn(N, K, device=gpu, generator=g) * K ** -0.5).to(torch.bfloat16)
     r = (torch.randn(M, N, device=gpu, generator=g) * 4).to(torch.bfloat16)
     ref = r.float() + x.float() @ w.float().t()
-    for mi, tr in ((0, 256), (16, 256), (8, 160), (0, 128)):
+    for mi, tr in ((0, 256), (16, 256), (0, 224), (8, 160), (0, 128)):
         out = ops.gemm_pf(x, w, 2, None, mi, resid=r, trows=tr)
         _close(out, ref, atol=3e-2, rtol=2e-2, name=f"gemm_pf resid {M}x{N}x{K} mi {mi} rows {tr}")
         rr = r.clone()
