@@ -31,7 +31,7 @@ MIN_ITERS = (0, 8, 16, 32)  # 0: data-parallel tiles only (no stream-K)
 # (token-tile rows, min_iters) candidates of the plain / SwiGLU / residual forms: the 256-row tile is the
 # most efficient per CU, the shorter ones fill the CUs when 256-row tiles leave a partial last round
 # (qkv at 6,144 rows: 192-row tiles 1.16x hipBLASLt where 256 reach 0.92x, profiles/r5/prefill_gemm)
-CANDIDATES = tuple((256, mi) for mi in MIN_ITERS) + ((192, 0), (192, 32), (160, 0), (160, 32), (128, 0), (128, 8))
+CANDIDATES = tuple((256, mi) for mi in MIN_ITERS) + ((224, 0), (224, 16), (192, 0), (192, 32), (160, 0), (160, 32), (128, 0), (128, 8))
 WIN_MARGIN = 0.98  # gemm_pf must be this much faster than the path it replaces
 ROUNDS = 3
 
