@@ -293,8 +293,9 @@ class LLMEngine:
         s.update(num_steps=self.num_steps, num_generated=self.num_generated, **self.runner.kv_stats())
         s["custom_ar_timeouts"] = self.num_collective_faults
         if self.runner.is_gpu:
-            s["gemm_pf_timeouts"] = ops.gemm_pf_faults(self.runner.device)
-            if s["gemm_pf_timeouts"]:
+            s["gemm_pf_timeouts"] = ops.gemm_pf_faults_async(self.runner.device)  # no device sync
+            if s["gemm_pf_timeouts"] > getattr(self, "_pf_faults_seen", 0):
+                self._pf_faults_seen = s["gemm_pf_timeouts"]
                 log.error("gemm_pf: %d stream-K waits timed out (grid not resident); prefill sums of "
                           "those tiles are wrong", s["gemm_pf_timeouts"])
         la = self._late

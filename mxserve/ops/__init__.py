@@ -241,6 +241,34 @@ def gemm_pf_faults(device=None) -> int:
     return 0 if ws is None else int(ws[1][-1].item())
 
 
+_PF_FAULT_HOST: dict = {}
+
+
+def gemm_pf_faults_async(device=None) -> int:
+    """gemm_pf_faults() without a device sync, for callers on a serving loop (AsyncEngine reads the
+    engine's stats every 20 ms; an .item() there drained the queue the host had run ahead with): the
+    word is copied into pinned memory behind the work already queued, and each call returns the
+    latest copy that has landed (0 before the first)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda")
+    if dev.index is None:
+        dev = torch.device(dev.type, torch.cuda.current_device())
+    ws = _PF_WS.get(dev)
+    if ws is None:
+        return 0
+    ent = _PF_FAULT_HOST.get(dev)
+    if ent is None:
+        ent = _PF_FAULT_HOST[dev] = [torch.zeros(1, dtype=torch.int32, pin_memory=True), None, 0]
+    buf, ev, last = ent
+    if ev is not None and not ev.query():
+        return last  # the previous copy is still behind queued work
+    if ev is not None:
+        ent[2] = last = int(buf[0])
+    buf.copy_(ws[1][-1:], non_blocking=True)
+    ent[1] = ev = torch.cuda.Event()
+    ev.record()
+    return last
+
+
 _PF_MAPS: dict = {}
 
 

@@ -123,7 +123,7 @@ def run(model: str, qps: float, isl: int, osl: int, warmup_s: float, window_s: f
                             async with sess.get(w_url + "/stats") as r:
                                 st = await r.json()
                             marks.append((time.perf_counter(), st.get("num_steps", 0), st.get("num_generated", 0),
-                                          st.get("num_running", 0)))
+                                          st.get("num_running", 0), st.get("late_admission")))
                         except (aiohttp.ClientError, ValueError):
                             pass
             smp = asyncio.create_task(sample())
@@ -143,10 +143,10 @@ def run(model: str, qps: float, isl: int, osl: int, warmup_s: float, window_s: f
                "path": "client -> frontend (dynamo.frontend, 4 processes: HTTP/SSE, router) -> worker "
                        "(dynamo.vllm: streamer process + engine) on the same GPU"}
         if len(marks) == 2:
-            (ta, sa, ga, ra), (tb, sb, gb, rb) = marks
+            (ta, sa, ga, ra, _), (tb, sb, gb, rb, la) = marks
             res["worker_engine"] = {"tok_per_s": round((gb - ga) / (tb - ta), 1),
                                     "iteration_ms": round(1e3 * (tb - ta) / max(1, sb - sa), 3),
-                                    "running_at_window_ends": [ra, rb]}
+                                    "running_at_window_ends": [ra, rb], "late_admission": la}
         for k in ("value", "ttft_p50_ms", "ttft_p90_ms", "itl_p50_ms", "itl_p90_ms", "itl_req_p50_ms",
                   "itl_req_p90_ms", "steady_window_s"):
             if isinstance(res.get(k), float):

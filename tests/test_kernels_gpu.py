@@ -1136,6 +1136,17 @@ def test_gemm_pf(gpu, M, N, K, epi):
     assert int(cnt.abs().sum()) == 0
 
 
+def test_gemm_pf_fault_word_read_without_sync(gpu):
+    """The engine's stats() reads gemm_pf's timeout word through a pinned copy behind the queued work
+    (no device sync on the serving loop); once the copy lands it agrees with the synchronous read."""
+    x = torch.randn(4240, 2048, device=gpu).to(torch.bfloat16)
+    w = (torch.randn(3072, 2048, device=gpu) * 0.02).to(torch.bfloat16)
+    assert ops.gemm_pf(x, w, 0, None, 16) is not None
+    ops.gemm_pf_faults_async(gpu)  # queues the first copy
+    torch.cuda.synchronize()
+    assert ops.gemm_pf_faults_async(gpu) == ops.gemm_pf_faults(gpu) == 0
+
+
 @pytest.mark.parametrize("M,N,K,epi", [(4240, 3072, 2048, 0), (4240, 16384, 2048, 1), (777, 768, 4096, 0),
                                        (300, 512, 192, 1), (6400, 3072, 2048, 0)])
 def test_gemm_pf_row_scale(gpu, M, N, K, epi):
