@@ -13,4 +13,5 @@ python3 scripts/rocpd_stats.py "$DB" --top 80 --by-grid Cijk > $D/hipblaslt_by_g
 python3 scripts/rocpd_stats.py "$DB" --top 40 --by-grid gemm_pf > $D/gemm_pf_by_grid.txt
 python3 scripts/rocpd_stats.py "$DB" --top 40 --by-grid paged > $D/attn_by_grid.txt
 python3 scripts/rocpd_stats.py "$DB" --busy 1 --top 0 > $D/gpu_busy.txt
+python3 scripts/rocpd_stats.py "$DB" --exclusive > $D/kernel_families_exclusive.txt
 head -30 $D/kernel_stats.txt

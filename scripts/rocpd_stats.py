@@ -17,8 +17,14 @@ def main():
     ap.add_argument("--by-grid", default="", help="also break kernels whose name contains this down by grid size")
     ap.add_argument("--busy", type=float, default=0.0,
                     help="print the GPU-busy fraction (union of kernel intervals) per bin of this many seconds")
+    ap.add_argument("--exclusive", action="store_true",
+                    help="per kernel family, time with concurrent kernels' overlap split evenly among them "
+                         "(kernels on side streams overlap; raw durations then over-count)")
     a = ap.parse_args()
     db = sqlite3.connect(a.db)
+    if a.exclusive:
+        exclusive(db)
+        return
     if a.busy:
         iv = db.execute("select start, end from kernels order by start").fetchall()
         t0, t1 = iv[0][0], max(e for _, e in iv)
@@ -67,6 +73,46 @@ def main():
     print(f"total {tot / 1e3 / a.per:.1f} us per unit ({a.per:g} units)")
     for n, c, t, m, p in out[:a.top]:
         print(f"{p:6.2f}%  {t / a.per:9.1f} us/unit  {c / a.per:7.1f} calls/unit  {m:8.2f} us  {n[:110]}")
+
+
+def family(name: str) -> str:
+    if name.startswith(("Cijk", "Custom_Cijk")):
+        return "hipblaslt"
+    n = name.split("(")[0].replace("void ", "")
+    return n.split("<")[0]
+
+
+def exclusive(db) -> None:
+    """Sweep the kernel intervals: each slice between consecutive start / end events is shared evenly
+    by the kernels active in it; a family's exclusive time is the sum of its shares, and the shares add
+    up to the GPU-busy time (the union of the intervals)."""
+    iv = db.execute("select name, start, end from kernels").fetchall()
+    ev = []
+    for i, (n, s_, e_) in enumerate(iv):
+        ev.append((s_, 1, i))
+        ev.append((e_, 0, i))
+    ev.sort()
+    active, t_prev, share, raw = set(), None, {}, {}
+    for n, s_, e_ in iv:
+        f = family(n)
+        raw[f] = raw.get(f, 0) + (e_ - s_)
+    for t, kind, i in ev:
+        if active and t_prev is not None and t > t_prev:
+            d = (t - t_prev) / len(active)
+            for j in active:
+                f = family(iv[j][0])
+                share[f] = share.get(f, 0.0) + d
+        t_prev = t
+        if kind:
+            active.add(i)
+        else:
+            active.discard(i)
+    busy, tot_raw = sum(share.values()), sum(raw.values())
+    print(f"# busy {busy / 1e6:.1f} ms (union of kernel intervals), raw kernel time {tot_raw / 1e6:.1f} ms "
+          f"(overlap {100.0 * (tot_raw - busy) / busy:.1f} %)")
+    print("# family: exclusive share of busy time | raw-duration share")
+    for f, v in sorted(share.items(), key=lambda kv: -kv[1]):
+        print(f"{100.0 * v / busy:6.2f}%  {100.0 * raw[f] / tot_raw:6.2f}%  {f}")
 
 
 if __name__ == "__main__":
