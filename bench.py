@@ -891,6 +891,13 @@ def phase_agg(a, ctx) -> tuple:
                                 "fused": {p: sum(r["chosen"].startswith("gemm_pf") for r in fu if r["proj"] == p)
                                           for p in sorted({r["proj"] for r in fu})},
                                 "from_table": sum(r.get("source") == "table" for r in rep)}
+    rep = getattr(eng.runner, "prefill_hblt_report", None)
+    if rep:  # start-up choice per (projection, form, row bucket): a measured hipBLASLt solution vs its default
+        info["prefill_hblt"] = {"buckets": len(rep), "tuned": sum(r["chosen"] != "default" for r in rep),
+                                "by_proj": {f"{p}{'+resid' if rs else ''}": sum(r["chosen"] != "default" for r in rep
+                                                                          if r["proj"] == p and r["resid"] == rs)
+                                            for p, rs in sorted({(r["proj"], r["resid"]) for r in rep})},
+                                "from_table": sum(r.get("source") == "table" for r in rep)}
     la = getattr(eng, "_late", None)
     if la is not None:  # engine/pacing.py: how often the host waited for a late admission, and how long
         info["late_admission"] = {"waits": la.waits, "mean_wait_ms": round(1e3 * la.wait_s / max(1, la.waits), 3),

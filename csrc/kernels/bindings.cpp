@@ -593,6 +593,9 @@ void moe_combine(at::Tensor out, at::Tensor ys, at::Tensor topk_w, at::Tensor in
 }  // namespace
 
 void register_comm(pybind11::module_& m);  // comm.cpp: KV transfer agent + custom all-reduce
+namespace mxs {
+void register_hblt(pybind11::module_& m);  // hblt.cpp: hipBLASLt with a tuned solution
+}
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "mxserve gfx950 HIP kernels";
@@ -695,4 +698,5 @@ PYBIND11_MODULE(_C, m) {
     return std::make_pair(P, len);
   });
   register_comm(m);
+  mxs::register_hblt(m);
 }

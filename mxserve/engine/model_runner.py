@@ -640,6 +640,13 @@ class ModelRunner:
             from ..ops import mplan
             self.mplan_report = mplan.tune({k: v[0] for k, v in shapes.items() if k != "lm_head"},
                                            self.args.max_num_batched_tokens + self.args.max_num_seqs, self.device)
+            # prefill projections left on hipBLASLt: its fastest solution per row bucket (the gemm_pf
+            # tuner below then compares against this path)
+            from ..ops import prefill_hblt
+            self.prefill_hblt_report = prefill_hblt.tune(
+                {k: v[0] for k, v in shapes.items() if k != "lm_head"},
+                {"o", "down"} if getattr(m, "pf_chain", False) else set(),
+                self.args.max_num_batched_tokens + self.args.max_num_seqs, self.device, self.dtype)
             # prefill projections: the stream-K MFMA kernel (SwiGLU fused for gate_up) vs that path
             from ..ops import prefill_pf
             pf_w = {k: (v[0], v[1]) for k, v in shapes.items() if k != "lm_head"}

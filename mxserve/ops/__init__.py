@@ -119,6 +119,11 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
                 out = torch.empty(M, w.shape[0], dtype=x.dtype, device=x.device)
                 if prefill_gemm(out, x, w, cfg):
                     return out
+            # hipBLASLt with the solution measured fastest for this bucket (ops/prefill_hblt.py)
+            from . import prefill_hblt
+            out = prefill_hblt.linear(x, w)
+            if out is not None:
+                return out
             plan = _mplan(M, w.shape[0], w.shape[1], x.device)
             if plan is not None:
                 return _run_mplan(x, w, plan)
@@ -239,6 +244,35 @@ def gemm_pf_faults(device=None) -> int:
         dev = torch.device(dev.type, torch.cuda.current_device())
     ws = _PF_WS.get(dev)
     return 0 if ws is None else int(ws[1][-1].item())
+
+
+_HBLT_WS: dict = {}
+HBLT_WS_BYTES = 64 << 20  # hipBLASLt stream-K solutions' workspace
+
+
+def _hblt_ws(device) -> torch.Tensor:
+    ws = _HBLT_WS.get(device)
+    if ws is None:
+        ws = _HBLT_WS[device] = torch.empty(HBLT_WS_BYTES, dtype=torch.uint8, device=device)
+    return ws
+
+
+def hblt_candidates(M: int, N: int, K: int, resid: bool = False, heuristic: int = 8) -> list:
+    """hipBLASLt solution indices that support x [M, K] @ w [N, K].T (+ a residual, beta 1): the
+    library heuristic's top `heuristic` first, then every other supporting gfx950 solution
+    (csrc/kernels/hblt.cpp)."""
+    return list(ext().hblt_candidates(M, N, K, resid, heuristic, HBLT_WS_BYTES))
+
+
+def hblt_mm(x: torch.Tensor, w: torch.Tensor, index: int, out: Optional[torch.Tensor] = None,
+            resid: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """out = x @ w.T (+ resid; out may be resid: in place) with hipBLASLt solution `index`; None when
+    that solution does not support the shape (the caller takes the default path)."""
+    if out is None:
+        out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+    if not ext().hblt_mm(out, x, w, resid, int(index), _hblt_ws(x.device)):
+        return None
+    return out
 
 
 _PF_FAULT_HOST: dict = {}

@@ -183,7 +183,8 @@ def resid_linear(x: torch.Tensor, w: torch.Tensor, r: torch.Tensor) -> torch.Ten
     if is_pf(mi) and ops.gemm_pf(x, w, 2, r, pf_cfg(mi)[0], resid=r, trows=pf_cfg(mi)[1]) is not None:
         return r
     if mi == "addmm":
-        return r.addmm_(x, w.t())
+        from . import prefill_hblt
+        return prefill_hblt.addmm_(r, x, w)  # its tuned solution, else torch's addmm_
     return r.add_(ops.linear(x, w))
 
 
@@ -211,6 +212,7 @@ def tune_fused(weights: dict, max_rows: int, device, dtype=torch.bfloat16, eps: 
     if MODE != "auto":
         return []
     from .. import ops
+    from . import prefill_hblt
     from .tuned import TunedStore, device_tag, median
     store = TunedStore("prefill_pf", device_tag(device))
     rows = []
@@ -231,7 +233,7 @@ def tune_fused(weights: dict, max_rows: int, device, dtype=torch.bfloat16, eps: 
                 nw = torch.ones(K, device=device, dtype=dtype)
                 if code == CODE_RESID:
                     r = torch.randn(M, N, device=device).to(dtype)
-                    bases = {None: lambda: r.add_(ops.linear(x, w)), "addmm": lambda: r.addmm_(x, w.t())}
+                    bases = {None: lambda: r.add_(ops.linear(x, w)), "addmm": lambda: prefill_hblt.addmm_(r, x, w)}
                     cand = {c: (lambda c=c: ops.gemm_pf(x, w, 2, r, c[1], resid=r, trows=c[0])) for c in CANDIDATES}
                 else:
                     bases = {None: (lambda: ops.linear(ops.rms_norm(x, nw, eps), w)) if epi == 0 else

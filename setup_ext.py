@@ -46,6 +46,9 @@ def _torch_flags():
     libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
     libs = [f"-L{libdir}", f"-Wl,-rpath,{libdir}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",
             "-lc10_hip", "-ltorch_hip"]
+    # hipBLASLt: the copy torch loads (one library, one set of solutions in the process)
+    hblt = os.path.join(libdir, "libhipblaslt.so")
+    libs.append(hblt if os.path.exists(hblt) else "-lhipblaslt")
     return inc, defs, libs
 
 

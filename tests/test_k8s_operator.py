@@ -703,13 +703,15 @@ def test_lease_leader_election(cluster):
     leader that releases its lease on SIGTERM hands over at the standby's next step."""
     from mxserve.k8s.operator import LeaderElector
     fake, k = cluster
-    a = LeaderElector(k, "dynamo-system", identity="a", lease_s=1.0)
-    b = LeaderElector(k, "dynamo-system", identity="b", lease_s=1.0)
+    # renewTime has second granularity: a renewal can read up to ~1 s older than it is, so the lease
+    # is 2 s (a 1 s lease could read as expired right after its renewal under a loaded test run)
+    a = LeaderElector(k, "dynamo-system", identity="a", lease_s=2.0)
+    b = LeaderElector(k, "dynamo-system", identity="b", lease_s=2.0)
     assert a.step() and not b.step()
     lease = k.get("Lease", "mxserve-operator", "dynamo-system")
     assert lease["spec"]["holderIdentity"] == "a"
     assert a.step() and not b.step()  # renewal keeps it
-    time.sleep(2.2)  # a stops renewing: expired (second-granularity renewTime)
+    time.sleep(4.2)  # a stops renewing: expired
     assert b.step() and not a.step()
     lease = k.get("Lease", "mxserve-operator", "dynamo-system")
     assert lease["spec"]["holderIdentity"] == "b" and lease["spec"]["leaseTransitions"] == 1

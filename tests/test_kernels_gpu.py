@@ -1136,6 +1136,28 @@ def test_gemm_pf(gpu, M, N, K, epi):
     assert int(cnt.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("M,N,K", [(4240, 3072, 2048), (6592, 2048, 8192), (777, 2048, 2048)])
+def test_hblt_solutions(gpu, M, N, K):
+    """hipBLASLt with an explicit solution (csrc/kernels/hblt.cpp) vs fp32: the heuristic's first
+    pick and the last supporting solution, plain and r += x W^T in place; an index that names no
+    solution is refused (None), not run."""
+    x = (torch.rand(M, K, device=gpu) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device=gpu) * 2 - 1) * K ** -0.5).to(torch.bfloat16)
+    r = (torch.rand(M, N, device=gpu) * 2 - 1).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    for resid in (False, True):
+        cands = ops.hblt_candidates(M, N, K, resid)
+        assert len(cands) > 1
+        for sol in (cands[0], cands[-1]):
+            if resid:
+                rr = r.clone()
+                assert ops.hblt_mm(x, w, sol, out=rr, resid=rr) is not None
+                _close(rr, ref + r.float(), atol=3e-2, rtol=2e-2, name=f"hblt resid sol {sol}")
+            else:
+                _close(ops.hblt_mm(x, w, sol), ref, atol=2e-2, rtol=2e-2, name=f"hblt sol {sol}")
+    assert ops.hblt_mm(x, w, -12345) is None
+
+
 def test_gemm_pf_fault_word_read_without_sync(gpu):
     """The engine's stats() reads gemm_pf's timeout word through a pinned copy behind the queued work
     (no device sync on the serving loop); once the copy lands it agrees with the synchronous read."""
