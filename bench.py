@@ -1148,7 +1148,7 @@ def build_line(a, ctx, mode, agg, dis, info) -> dict:
     if "arrivals" in info:
         line["arrivals"] = info["arrivals"]
     line["engine"] = {"kv_blocks": info["kv_blocks"], "preemptions": info["preemptions"], "graphs": info["graphs"]}
-    for k in ("late_admission", "decode_gemm", "prefill_gemm", "chunk_budget", "gc"):
+    for k in ("late_admission", "decode_gemm", "prefill_gemm", "prefill_hblt", "chunk_budget", "gc"):
         if k in info:
             line["engine"][k] = info[k]
     return line

@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Step-level A/B of the tuned hipBLASLt solutions (mxserve/ops/prefill_hblt.py): one mixed engine step
+of the headline workload (B decode rows at ~CTX context + one CHUNK-token prefill after PREFIX cached
+tokens; Llama-3.2-1B forward + logits, the engine's own routing tables loaded by building an
+LLMEngine with the bench's limits) timed with prefill_hblt.MODE "auto" and "off" alternately in one
+process.  MS_CASES="B:CTX:CHUNK:PREFIX,..."; one JSON line per case."""
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def main():
+    from mxserve.config import EngineArgs
+    from mxserve.engine.engine import LLMEngine
+    from mxserve.models.llama import AttnMetadata
+    from mxserve.ops import prefill_hblt
+    dev = torch.device("cuda:0")
+    eng = LLMEngine(EngineArgs(model="meta-llama/Llama-3.2-1B-Instruct", device="cuda", max_num_seqs=448,
+                               cuda_graph_max_bs=448, max_num_batched_tokens=6144, max_model_len=8192,
+                               num_gpu_blocks=4096))
+    m, cfg = eng.runner.model, eng.runner.cfg
+    i32 = dict(dtype=torch.int32, device=dev)
+    cases = [tuple(int(x) for x in c.split(":")) for c in
+             os.environ.get("MS_CASES", "300:4250:2400:1600,300:4250:4000:0,400:4250:1200:2800,"
+                                        "350:4250:5700:0,0:0:4000:0").split(",")]
+    for B, ctx, chunk, prefix in cases:
+        torch.manual_seed(0)
+        dl = torch.randint(max(1, ctx - 250), ctx + 250, (B,)).tolist() if B else []
+        plen = prefix + chunk
+        lens = [d + 1 for d in dl] + [plen]
+        nbs = [math.ceil(n / 16) for n in lens]
+        nb = sum(nbs) + 8
+        kv = torch.randn(nb, cfg.num_layers, 2, m.nkv, 16, cfg.head_dim, dtype=torch.bfloat16, device=dev) * 0.1
+        perm = torch.randperm(nb - 8, device=dev).to(torch.int32)
+        bt = torch.zeros(B + 1, max(nbs), **i32)
+        o = 0
+        for i, n in enumerate(nbs):
+            bt[i, :n] = perm[o:o + n]
+            o += n
+        pos_d = torch.tensor(dl, dtype=torch.int64, device=dev)
+        pos_p = torch.arange(prefix, plen, dtype=torch.int64, device=dev)
+        positions = torch.cat([pos_d, pos_p])
+        rows = torch.cat([torch.arange(B, device=dev), torch.full((chunk,), B, device=dev)])
+        slot = bt[rows, (positions // 16)].long() * 16 + positions % 16
+        qsl = torch.tensor(list(range(B + 1)) + [B + chunk], **i32)
+        md = AttnMetadata(positions=positions, slot_mapping=slot, block_tables=bt,
+                          seq_lens=torch.tensor(lens, **i32), query_start_loc=qsl,
+                          logits_indices=torch.cat([torch.arange(B, device=dev), torch.tensor([B + chunk - 1], device=dev)]),
+                          num_decodes=B, num_prefills=1, num_prefill_tokens=chunk, max_query_len=chunk,
+                          max_seq_len=max(lens), prefill_query_start_loc=torch.tensor([0, chunk], **i32),
+                          sample_seq=torch.arange(B + 1, **i32))
+        ids = torch.randint(0, cfg.vocab_size, (B + chunk,), device=dev)
+        times = {"auto": [], "off": []}
+        outs = {}
+        with torch.inference_mode():
+            for _ in range(8):
+                for mode in times:
+                    prefill_hblt.MODE = mode
+                    for _ in range(2):
+                        outs[mode] = m.compute_logits(m.forward(ids, md, kv))
+                    torch.cuda.synchronize()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(5):
+                        m.compute_logits(m.forward(ids, md, kv))
+                    e1.record()
+                    torch.cuda.synchronize()
+                    times[mode].append(e0.elapsed_time(e1) / 5)
+        prefill_hblt.MODE = "auto"
+        r = {k: round(sorted(v)[len(v) // 2], 3) for k, v in times.items()}
+        diff = (outs["auto"].float() - outs["off"].float()).abs().max().item()
+        print(json.dumps({"B": B, "ctx": ctx, "chunk": chunk, "prefix": prefix, "rows": B + chunk, "ms": r,
+                          "auto_vs_off": round(r["off"] / r["auto"], 4), "logits_max_abs_diff": round(diff, 4),
+                          "all_ms": {k: [round(x, 3) for x in v] for k, v in times.items()}}), flush=True)
+        del kv
+
+
+if __name__ == "__main__":
+    main()
