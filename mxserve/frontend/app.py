@@ -376,16 +376,27 @@ class Frontend:
             async for data in r.content.iter_any():
                 buf += data
                 *lines, buf = buf.split(b"\n")
-                evs = []
-                for line in lines:
-                    if line.strip():
-                        _parse_token_line(json.loads(line), evs)
+                evs, err = [], None
+                try:
+                    for line in lines:
+                        if line.strip():
+                            _parse_token_line(json.loads(line), evs)
+                except (ConnectionError, RuntimeError) as e:
+                    err = e  # the tokens before the marker still count as generated (migration, router)
                 if evs:
                     yield evs
+                if err is not None:
+                    raise err
             if buf.strip():
-                evs = []
-                _parse_token_line(json.loads(buf), evs)
-                yield evs
+                evs, err = [], None
+                try:
+                    _parse_token_line(json.loads(buf), evs)
+                except (ConnectionError, RuntimeError) as e:
+                    err = e
+                if evs:
+                    yield evs
+                if err is not None:
+                    raise err
 
     async def _mux_stream(self, sess, mc: MuxClient, body: dict, rid: str) -> AsyncIterator[list]:
         q: asyncio.Queue = asyncio.Queue()
@@ -410,15 +421,22 @@ class Frontend:
                 if isinstance(item, BaseException):
                     raise item
                 evs: list = []
-                _parse_token_line(item, evs)
-                while not evs[-1].finished and not q.empty():
-                    item = q.get_nowait()
-                    if isinstance(item, BaseException):
-                        raise item
+                err = None
+                try:
                     _parse_token_line(item, evs)
-                if evs[-1].finished:
+                    while not evs[-1].finished and not q.empty():
+                        item = q.get_nowait()
+                        if isinstance(item, BaseException):
+                            raise item
+                        _parse_token_line(item, evs)
+                except (ConnectionError, RuntimeError) as e:
+                    err = e  # deliver the tokens that came before the failure first
+                if evs and evs[-1].finished:
                     done = True
-                yield evs
+                if evs:
+                    yield evs
+                if err is not None:
+                    raise err
                 if done:
                     return
         finally:

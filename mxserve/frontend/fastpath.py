@@ -150,8 +150,10 @@ class PushStream:
         toks = d["t"]
         if not isinstance(toks, list):
             toks = [toks]
-        for t in toks:
+        for i, t in enumerate(toks):
             if t < 0:
+                if i:  # the tokens before the marker were generated: deliver them (they count for migration)
+                    self._tokens(toks[:i], False, None, d.get("tm"))
                 if t == -2:  # the worker dropped the stream (fault injection): retry / migrate
                     raise ConnectionError("worker dropped the stream")
                 raise RuntimeError("worker failed the request")

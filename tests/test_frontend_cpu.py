@@ -365,10 +365,28 @@ def test_disagg_prefill_failure_falls_back_to_local():
         dw.aeng.shutdown()
 
 
-def test_mid_stream_migration_keeps_greedy_output():
+@pytest.mark.parametrize("together", [False, True])
+def test_mid_stream_migration_keeps_greedy_output(monkeypatch, together):
     """a worker that drops the stream after its first token; the frontend re-prefills
-    prompt + generated tokens on the other worker and the client sees the same greedy text."""
+    prompt + generated tokens on the other worker and the client sees the same greedy text.
+    together: the first token and the drop marker reach the frontend in one channel write (a loaded
+    worker: two steps' outputs before the channel drains) -- the token still counts as generated."""
     from mxserve.utils.tracing import Faults
+    if together:
+        from mxserve.engine.engine import StepOutput
+        from mxserve.worker import server as wsrv
+        held: dict = {}
+
+        def put_nowait(self, o):
+            self.n += 1
+            if self.n == 1:
+                held[id(self)] = o
+            elif self.n == 2:
+                self.ch.pending.append(held.pop(id(self)))
+                self.ch.pending.append(StepOutput(o.request_id, -2, True, "abort", 0, 0, 0))
+                self.ch.wake.set()
+                self.on_drop(o.request_id)
+        monkeypatch.setattr(wsrv._DropSink, "put_nowait", put_nowait)
     fe = Frontend(router_mode="round_robin", ttl=30)
     fs = Server(fe.app).start()
     a, as_ = _worker(fs.url, role="agg")
