@@ -11,7 +11,10 @@ csrc/kernels/hblt.cpp runs it (descriptors cached per shape, the solution re-che
 
 Solution indices belong to one hipBLASLt build: each entry stores the solution's kernel name, and a
 table entry whose index names another kernel in the loaded library is re-measured.
-MXS_HBLT=auto (default) | off.  Choices persist in mxserve/ops/tuned/prefill_hblt_<arch>_<cus>cu.json.
+MXS_HBLT=auto (default: the packaged / MXS_TUNED_DIR table only -- a shape it does not hold stays on
+torch's call, so start-up stays fast and every process runs the same kernels) | tune (also measure
+the shapes the table lacks; with MXS_TUNED_SAVE=1 they are written back) | off.  Choices persist in
+mxserve/ops/tuned/prefill_hblt_<arch>_<cus>cu.json.
 """
 from __future__ import annotations
 
@@ -36,7 +39,7 @@ class HbltTable:
         self.report: list = []
 
     def lookup(self, M: int, N: int, K: int, resid: bool) -> Optional[int]:
-        if MODE == "off" or M <= 256:
+        if MODE not in ("auto", "tune") or M <= 256:
             return None
         ent = self.entries.get((N, K, bool(resid)))
         if not ent:
@@ -46,6 +49,9 @@ class HbltTable:
 
 
 TABLE = HbltTable()
+# choices measured in this process (not in the packaged table): a later engine start in the same
+# process reuses them, so its kernels -- and bf16 roundings -- match the first engine's
+_MEASURED: dict = {}
 
 
 def linear(x: torch.Tensor, w: torch.Tensor) -> Optional[torch.Tensor]:
@@ -75,7 +81,7 @@ def _points(lo: int, hi: int) -> list:
 def tune(weights: dict, resid_names: set, max_rows: int, device, dtype=torch.bfloat16) -> list:
     """weights: {name: w [N, K]}; resid_names: projections that also run as r += x W^T (o / down of the
     fused prefill chain).  Fills TABLE; returns report rows."""
-    if MODE != "auto":
+    if MODE not in ("auto", "tune"):
         return []
     from .. import ops
     from . import prefill_pf
@@ -92,8 +98,8 @@ def tune(weights: dict, resid_names: set, max_rows: int, device, dtype=torch.bfl
             for Mb in buckets_for(max_rows):
                 key = f"{N}x{K}:{int(resid)}@{Mb}"
                 pts = _points(lo, Mb)
-                xs = {M: (torch.rand(M, K, device=device) * 2 - 1).to(dtype) for M in pts}
-                rs = {M: (torch.rand(M, N, device=device) * 2 - 1).to(dtype) for M in pts} if resid else {}
+                xs: dict = {}
+                rs: dict = {}
 
                 def base(M):
                     if resid:
@@ -107,13 +113,20 @@ def tune(weights: dict, resid_names: set, max_rows: int, device, dtype=torch.bfl
                 def run(sol, M):
                     return ops.hblt_mm(xs[M], w, sol, out=rs[M] if resid else None, resid=rs[M] if resid else None)
 
-                st = store.get(key)
+                st = store.get(key) or _MEASURED.get((store.tag, key))
                 if st is not None and st.get("sol") is not None and \
                         ops.ext().hblt_kernel_name(int(st["sol"])) != st.get("kernel"):
                     st = None  # another hipBLASLt build: its index names another kernel
                 if st is not None:
                     sol, t_best, t_base, source = st.get("sol"), st.get("us"), st.get("base_us"), "table"
-                else:
+                elif MODE != "tune":  # not in the table: torch's call (measuring is opt-in)
+                    ent.append((Mb, None))
+                    lo = Mb
+                    continue
+                xs.update({M: (torch.rand(M, K, device=device) * 2 - 1).to(dtype) for M in pts})
+                if resid:
+                    rs.update({M: (torch.rand(M, N, device=device) * 2 - 1).to(dtype) for M in pts})
+                if st is None:  # MXS_HBLT=tune and not in the table: measure
                     source = "measured"
                     top = pts[-1]
                     screen = {}
@@ -149,8 +162,10 @@ def tune(weights: dict, resid_names: set, max_rows: int, device, dtype=torch.bfl
                     if got is None or not (got.float() - want).abs().max().item() <= 0.02 * max(1.0, want.abs().max().item()):
                         sol, t_best = None, t_base
                 if source == "measured":
-                    store.put(key, {"sol": sol, "kernel": ops.ext().hblt_kernel_name(int(sol)) if sol is not None else None,
-                                    "us": t_best and round(t_best, 2), "base_us": round(t_base, 2), "points": pts})
+                    ent_d = {"sol": sol, "kernel": ops.ext().hblt_kernel_name(int(sol)) if sol is not None else None,
+                             "us": t_best and round(t_best, 2), "base_us": round(t_base, 2), "points": pts}
+                    store.put(key, ent_d)
+                    _MEASURED[(store.tag, key)] = ent_d
                 ent.append((Mb, sol))
                 rows.append({"proj": name, "M": Mb, "N": N, "K": K, "resid": resid, "base_us": t_base and round(t_base, 2),
                              "chosen": "default" if sol is None else f"sol{sol}", "us": t_best and round(t_best, 2),

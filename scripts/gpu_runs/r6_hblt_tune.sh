@@ -11,7 +11,7 @@ trap 'kill $HB' EXIT
 timeout -k 10 200 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread \
   -k "hblt or fault_word" > $D/tests.log 2>&1
 tail -1 $D/tests.log
-MXS_RETUNE=prefill_hblt,prefill_pf MXS_TUNED_SAVE=1 MXS_TUNED_DIR=$GRAFT_REPO_ROOT/$D/tuned MXS_BENCH_SERVED=0 \
+MXS_HBLT=tune MXS_RETUNE=prefill_hblt,prefill_pf MXS_TUNED_SAVE=1 MXS_TUNED_DIR=$GRAFT_REPO_ROOT/$D/tuned MXS_BENCH_SERVED=0 \
   timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > $D/bench_retune.json 2> $D/bench_retune.err
 ls $D/tuned
 MXS_TUNED_DIR=$GRAFT_REPO_ROOT/$D/tuned MXS_BENCH_SERVED=0 timeout -k 10 400 python -u bench.py --steps 40 --warmup 10 > $D/bench_after.json 2> $D/bench_after.err

@@ -42,8 +42,11 @@ print("RESULT " + json.dumps(info), flush=True)
 
 
 def _run(tmp_path, **extra) -> dict:
+    # the two runs must match token for token: no start-up tuner may pick kernels by timing on either
+    # side (small-llama's shapes are in no packaged table, so each process would measure afresh and a
+    # different prefill GEMM solution rounds differently -- a late near-tie flip, not a fault effect)
     env = dict(os.environ, MXS_ROOT=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=ROOT, MXS_DECODE_GEMM="off",
-               MXS_PF_FUSED="0", **extra)
+               MXS_PF_FUSED="0", MXS_HBLT="off", MXS_GEMM_PF="off", MXS_MPLAN="0", **extra)
     env.pop("MXS_CUSTOM_AR", None)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
