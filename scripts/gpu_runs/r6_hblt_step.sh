@@ -4,4 +4,4 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 D=gpurun_out/${OUT:-r6hblstep}
 mkdir -p $D
-MXS_TUNED_DIR=$GRAFT_REPO_ROOT/profiles/r6/hblt/tuned timeout -k 10 500 python -u scripts/probes/hblt_step_probe.py > $D/step.jsonl 2> $D/step.err
+MXS_TUNED_DIR=$GRAFT_REPO_ROOT/profiles/r6/hblt/tuned timeout -k 10 500 python -u scripts/probes/step_ab_probe.py > $D/step.jsonl 2> $D/step.err

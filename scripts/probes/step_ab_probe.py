@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""Step-level A/B of the tuned hipBLASLt solutions (mxserve/ops/prefill_hblt.py): one mixed engine step
-of the headline workload (B decode rows at ~CTX context + one CHUNK-token prefill after PREFIX cached
-tokens; Llama-3.2-1B forward + logits, the engine's own routing tables loaded by building an
-LLMEngine with the bench's limits) timed with prefill_hblt.MODE "auto" and "off" alternately in one
-process.  MS_CASES="B:CTX:CHUNK:PREFIX,..."; one JSON line per case."""
+"""Step-level A/B of engine settings that can change in-process: one mixed engine step of the headline
+workload (B decode rows at ~CTX context + one CHUNK-token prefill after PREFIX cached tokens;
+Llama-3.2-1B forward + logits, the engine's own routing tables loaded by building an LLMEngine with
+the bench's limits), each mode timed in turn, rounds interleaved.  Modes (STEP_MODES, comma list):
+base, hblt_off (mxserve/ops/prefill_hblt.py table off), var0 (prefill attention forced to the
+default v3 variant instead of the split / paired choice), no_overlap (prefill-chunk attention on the
+main stream), no_overlap_var0.  MS_CASES="B:CTX:CHUNK:PREFIX,..."; one JSON line per case."""
 import json
 import math
 import os
@@ -18,7 +20,19 @@ def main():
     from mxserve.config import EngineArgs
     from mxserve.engine.engine import LLMEngine
     from mxserve.models.llama import AttnMetadata
+    from mxserve import ops
+    from mxserve.models import llama
     from mxserve.ops import prefill_hblt
+    all_modes = {"base": {}, "hblt_off": {"hblt": "off"}, "var0": {"pv": 0x100}, "no_overlap": {"ov": False},
+                 "no_overlap_var0": {"ov": False, "pv": 0x100}}
+    names = [m for m in os.environ.get("STEP_MODES", "base,hblt_off").split(",") if m]
+    pv0, ov0, hb0 = ops._PREFILL_VERSION, llama._ATTN_OVERLAP, prefill_hblt.MODE
+
+    def apply(mode):
+        st = all_modes[mode]
+        ops._PREFILL_VERSION = st.get("pv", pv0)
+        llama._ATTN_OVERLAP = st.get("ov", ov0)
+        prefill_hblt.MODE = st.get("hblt", hb0)
     dev = torch.device("cuda:0")
     eng = LLMEngine(EngineArgs(model="meta-llama/Llama-3.2-1B-Instruct", device="cuda", max_num_seqs=448,
                                cuda_graph_max_bs=448, max_num_batched_tokens=6144, max_model_len=8192,
@@ -55,12 +69,12 @@ def main():
                           max_seq_len=max(lens), prefill_query_start_loc=torch.tensor([0, chunk], **i32),
                           sample_seq=torch.arange(B + 1, **i32))
         ids = torch.randint(0, cfg.vocab_size, (B + chunk,), device=dev)
-        times = {"auto": [], "off": []}
+        times = {k: [] for k in names}
         outs = {}
         with torch.inference_mode():
             for _ in range(8):
                 for mode in times:
-                    prefill_hblt.MODE = mode
+                    apply(mode)
                     for _ in range(2):
                         outs[mode] = m.compute_logits(m.forward(ids, md, kv))
                     torch.cuda.synchronize()
@@ -71,11 +85,13 @@ def main():
                     e1.record()
                     torch.cuda.synchronize()
                     times[mode].append(e0.elapsed_time(e1) / 5)
-        prefill_hblt.MODE = "auto"
+        apply("base")
         r = {k: round(sorted(v)[len(v) // 2], 3) for k, v in times.items()}
-        diff = (outs["auto"].float() - outs["off"].float()).abs().max().item()
+        b = names[0]
+        diff = {k: round((outs[k].float() - outs[b].float()).abs().max().item(), 4) for k in names[1:]}
         print(json.dumps({"B": B, "ctx": ctx, "chunk": chunk, "prefix": prefix, "rows": B + chunk, "ms": r,
-                          "auto_vs_off": round(r["off"] / r["auto"], 4), "logits_max_abs_diff": round(diff, 4),
+                          "time_vs_" + b: {k: round(r[k] / r[b], 4) for k in names[1:]},
+                          "logits_max_abs_diff": diff,
                           "all_ms": {k: [round(x, 3) for x in v] for k, v in times.items()}}), flush=True)
         del kv
 
