@@ -39,35 +39,44 @@ def main():
                                num_gpu_blocks=4096))
     m, cfg = eng.runner.model, eng.runner.cfg
     i32 = dict(dtype=torch.int32, device=dev)
-    cases = [tuple(int(x) for x in c.split(":")) for c in
-             os.environ.get("MS_CASES", "300:4250:2400:1600,300:4250:4000:0,400:4250:1200:2800,"
-                                        "350:4250:5700:0,0:0:4000:0").split(",")]
-    for B, ctx, chunk, prefix in cases:
+    # "B:CTX:CHUNK:PREFIX[+CHUNK:PREFIX...]": B decode rows, then one or more prefill sequences
+    cases = []
+    for c in os.environ.get("MS_CASES", "300:4250:2400:1600,300:4250:4000:0,400:4250:1200:2800,"
+                                        "350:4250:5700:0,0:0:4000:0").split(","):
+        head, *more = c.split("+")
+        B, ctx, chunk, prefix = (int(x) for x in head.split(":"))
+        cases.append((B, ctx, [(chunk, prefix)] + [tuple(int(x) for x in m.split(":")) for m in more]))
+    for B, ctx, pf in cases:
         torch.manual_seed(0)
         dl = torch.randint(max(1, ctx - 250), ctx + 250, (B,)).tolist() if B else []
-        plen = prefix + chunk
-        lens = [d + 1 for d in dl] + [plen]
+        lens = [d + 1 for d in dl] + [p + c for c, p in pf]
         nbs = [math.ceil(n / 16) for n in lens]
         nb = sum(nbs) + 8
         kv = torch.randn(nb, cfg.num_layers, 2, m.nkv, 16, cfg.head_dim, dtype=torch.bfloat16, device=dev) * 0.1
         perm = torch.randperm(nb - 8, device=dev).to(torch.int32)
-        bt = torch.zeros(B + 1, max(nbs), **i32)
+        bt = torch.zeros(B + len(pf), max(nbs), **i32)
         o = 0
         for i, n in enumerate(nbs):
             bt[i, :n] = perm[o:o + n]
             o += n
+        chunk = sum(c for c, _ in pf)
         pos_d = torch.tensor(dl, dtype=torch.int64, device=dev)
-        pos_p = torch.arange(prefix, plen, dtype=torch.int64, device=dev)
+        pos_p = torch.cat([torch.arange(p, p + c, dtype=torch.int64, device=dev) for c, p in pf])
         positions = torch.cat([pos_d, pos_p])
-        rows = torch.cat([torch.arange(B, device=dev), torch.full((chunk,), B, device=dev)])
+        rows = torch.cat([torch.arange(B, device=dev)] + [torch.full((c,), B + j, device=dev) for j, (c, _) in enumerate(pf)])
         slot = bt[rows, (positions // 16)].long() * 16 + positions % 16
-        qsl = torch.tensor(list(range(B + 1)) + [B + chunk], **i32)
+        cum = [0]
+        for c, _ in pf:
+            cum.append(cum[-1] + c)
+        qsl = torch.tensor(list(range(B + 1)) + [B + x for x in cum[1:]], **i32)
         md = AttnMetadata(positions=positions, slot_mapping=slot, block_tables=bt,
                           seq_lens=torch.tensor(lens, **i32), query_start_loc=qsl,
-                          logits_indices=torch.cat([torch.arange(B, device=dev), torch.tensor([B + chunk - 1], device=dev)]),
-                          num_decodes=B, num_prefills=1, num_prefill_tokens=chunk, max_query_len=chunk,
-                          max_seq_len=max(lens), prefill_query_start_loc=torch.tensor([0, chunk], **i32),
-                          sample_seq=torch.arange(B + 1, **i32))
+                          logits_indices=torch.cat([torch.arange(B, device=dev),
+                                                    torch.tensor([B + x - 1 for x in cum[1:]], device=dev)]),
+                          num_decodes=B, num_prefills=len(pf), num_prefill_tokens=chunk,
+                          max_query_len=max(c for c, _ in pf), max_seq_len=max(lens),
+                          prefill_query_start_loc=torch.tensor(cum, **i32),
+                          sample_seq=torch.arange(B + len(pf), **i32))
         ids = torch.randint(0, cfg.vocab_size, (B + chunk,), device=dev)
         times = {k: [] for k in names}
         outs = {}
@@ -89,7 +98,7 @@ def main():
         r = {k: round(sorted(v)[len(v) // 2], 3) for k, v in times.items()}
         b = names[0]
         diff = {k: round((outs[k].float() - outs[b].float()).abs().max().item(), 4) for k in names[1:]}
-        print(json.dumps({"B": B, "ctx": ctx, "chunk": chunk, "prefix": prefix, "rows": B + chunk, "ms": r,
+        print(json.dumps({"B": B, "ctx": ctx, "prefills": pf, "rows": B + chunk, "ms": r,
                           "time_vs_" + b: {k: round(r[k] / r[b], 4) for k in names[1:]},
                           "logits_max_abs_diff": diff,
                           "all_ms": {k: [round(x, 3) for x in v] for k, v in times.items()}}), flush=True)
