@@ -20,9 +20,29 @@ SHAPES = [("qkv", 3072, 2048, False), ("o", 2048, 2048, True), ("down", 2048, 81
           ("gate_up", 16384, 2048, False)]
 
 
+GRAPH = os.environ.get("HB_GRAPH", "0") == "1"  # time hipGraph replays (decode sizes: no host overhead)
+
+
 def timed(fn, iters=10):
     fn()
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if GRAPH:
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(iters):
+                    fn()
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()
+        e0.record()
+        for _ in range(3):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / (3 * iters)
     e0.record()
     for _ in range(iters):
         fn()
