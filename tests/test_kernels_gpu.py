@@ -1158,6 +1158,24 @@ def test_hblt_solutions(gpu, M, N, K):
     assert ops.hblt_mm(x, w, -12345) is None
 
 
+def test_hblt_descriptor_cache_eviction(gpu):
+    """Prefill row counts differ step to step: hblt.cpp keeps at most 4096 problem descriptors and
+    drops them all past that.  Runs across the eviction stay correct (the solution is re-checked
+    for every re-created problem)."""
+    N, K = 256, 128
+    w = (torch.randn(N, K, device=gpu) * 0.1).to(torch.bfloat16)
+    xs = (torch.randn(4500, K, device=gpu)).to(torch.bfloat16)
+    sol = ops.hblt_candidates(4500, N, K)[0]
+    ref = xs.float() @ w.float().t()
+    for M in range(257, 257 + 4200):  # 4200 distinct problems: one eviction on the way
+        out = ops.hblt_mm(xs[:M], w, sol)
+        if out is None:
+            continue  # this solution does not take every row count: nothing to check there
+        if M % 700 == 0 or M >= 4450:
+            _close(out, ref[:M], atol=2e-2, rtol=2e-2, name=f"hblt after {M - 256} problems")
+    assert ops.hblt_mm(xs[:300], w, sol) is not None
+
+
 def test_gemm_pf_fault_word_read_without_sync(gpu):
     """The engine's stats() reads gemm_pf's timeout word through a pinned copy behind the queued work
     (no device sync on the serving loop); once the copy lands it agrees with the synchronous read."""
