@@ -60,6 +60,38 @@ def _registered(url: str, model: str) -> bool:
         return False
 
 
+def _trace_breakdown(url: str, polls: int = 24) -> dict:
+    """Median per-stage times of the served requests' first tokens, from the frontend processes'
+    trace rings (/debug/traces; each GET reaches one of the frontend processes, so several GETs cover
+    them all): frontend spans from the request's arrival at the frontend (tokenized, routed,
+    first_token) and the worker's spans carried on the first token (inbox: the engine thread's inbox,
+    queue: waiting for admission, prefill: admission to the sampled token, delivery: worker emit to the
+    frontend's receipt)."""
+    import json
+    import statistics
+    import urllib.request
+    seen: dict = {}
+    for _ in range(polls):
+        try:
+            with urllib.request.urlopen(url + "/debug/traces?n=1024", timeout=5) as r:
+                for t in json.loads(r.read()).get("traces", []):
+                    seen[t.get("request_id")] = t
+        except (OSError, ValueError):
+            break
+    vals: dict = {}
+    for t in seen.values():
+        for k, v in (t.get("spans_ms") or {}).items():
+            if k in ("tokenized", "routed", "first_token"):
+                vals.setdefault("frontend_" + k, []).append(v)
+        for k, v in (t.get("worker_ms") or {}).items():
+            if k in ("inbox_ms", "queue_ms", "prefill_ms", "delivery_ms") and isinstance(v, (int, float)):
+                vals.setdefault("worker_" + k[:-3], []).append(v)
+    out = {k: round(statistics.median(v), 3) for k, v in sorted(vals.items()) if v}
+    if out:
+        out["requests"] = len(seen)
+    return out
+
+
 def arrival_stream(qps: float, n: int, isl: int, vocab: int, rank: int = 0) -> tuple:
     """The engine-direct phase's exact Poisson stream (bench.py Driver, rank 0): the same generator
     draws the 65,536 inter-arrival gaps first, then each prompt in arrival order -- so both phases
@@ -132,6 +164,7 @@ def run(model: str, qps: float, isl: int, osl: int, warmup_s: float, window_s: f
             await smp
             return res
         s = asyncio.run(main())
+        breakdown = _trace_breakdown(url)
         res = {"status": "ok", "value": s.get("steady_output_tok_per_s"), "unit": "tok/s",
                "ttft_p50_ms": s.get("steady_ttft_ms_p50"), "ttft_p90_ms": s.get("steady_ttft_ms_p90"),
                "itl_p50_ms": s.get("steady_itl_ms_p50"), "itl_p90_ms": s.get("steady_itl_ms_p90"),
@@ -142,6 +175,8 @@ def run(model: str, qps: float, isl: int, osl: int, warmup_s: float, window_s: f
                "stack_start_s": round(setup_s, 1),
                "path": "client -> frontend (dynamo.frontend, 4 processes: HTTP/SSE, router) -> worker "
                        "(dynamo.vllm: streamer process + engine) on the same GPU"}
+        if breakdown:
+            res["ttft_breakdown_p50_ms"] = breakdown
         if len(marks) == 2:
             (ta, sa, ga, ra, _), (tb, sb, gb, rb, la) = marks
             res["worker_engine"] = {"tok_per_s": round((gb - ga) / (tb - ta), 1),
