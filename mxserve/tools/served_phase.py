@@ -60,9 +60,9 @@ def _registered(url: str, model: str) -> bool:
         return False
 
 
-def _trace_breakdown(url: str, polls: int = 24) -> dict:
-    """Median per-stage times of the served requests' first tokens, from the frontend processes'
-    trace rings (/debug/traces; each GET reaches one of the frontend processes, so several GETs cover
+def _trace_breakdown(url: str, polls: int = 24, window: Optional[tuple] = None) -> dict:
+    """Median per-stage times of the served requests' first tokens (those that arrived inside
+    `window`, wall clock), from the frontend processes' trace rings (/debug/traces; each GET reaches one of the frontend processes, so several GETs cover
     them all): frontend spans from the request's arrival at the frontend (tokenized, routed,
     first_token) and the worker's spans carried on the first token (inbox: the engine thread's inbox,
     queue: waiting for admission, prefill: admission to the sampled token, delivery: worker emit to the
@@ -75,7 +75,9 @@ def _trace_breakdown(url: str, polls: int = 24) -> dict:
         try:
             with urllib.request.urlopen(url + "/debug/traces?n=1024", timeout=5) as r:
                 for t in json.loads(r.read()).get("traces", []):
-                    seen[t.get("request_id")] = t
+                    tu = t.get("t_unix")
+                    if window is None or (tu is not None and window[0] <= tu <= window[1]):
+                        seen[t.get("request_id")] = t
         except (OSError, ValueError):
             break
     vals: dict = {}
@@ -163,8 +165,11 @@ def run(model: str, qps: float, isl: int, osl: int, warmup_s: float, window_s: f
                                  gaps=gaps, prompts=prompts, procs=CLIENT_PROCS if on_gpu else 1)
             await smp
             return res
+        t_run = time.time()
         s = asyncio.run(main())
-        breakdown = _trace_breakdown(url)
+        # the steady window's requests only (the trace rings also hold the ramp-up's, which see an
+        # emptier engine)
+        breakdown = _trace_breakdown(url, window=(t_run + warmup_s, t_run + warmup_s + window_s))
         res = {"status": "ok", "value": s.get("steady_output_tok_per_s"), "unit": "tok/s",
                "ttft_p50_ms": s.get("steady_ttft_ms_p50"), "ttft_p90_ms": s.get("steady_ttft_ms_p90"),
                "itl_p50_ms": s.get("steady_itl_ms_p50"), "itl_p90_ms": s.get("steady_itl_ms_p90"),

@@ -50,7 +50,9 @@ class Tracer:
         self._lock = threading.Lock()
 
     def start(self, request_id: str) -> Trace:
-        return Trace(request_id)
+        tr = Trace(request_id)
+        tr.attrs["t_unix"] = round(time.time(), 3)  # wall clock of the request's arrival (window filters)
+        return tr
 
     def finish(self, tr: Trace) -> None:
         tr.mark("done")
