@@ -535,7 +535,10 @@ class Frontend:
         fut = asyncio.get_running_loop().create_future()
         sink = _PushSink(ps, fut)
         mc.queues[rid] = sink
+        tr = getattr(ps, "trace", None)
         try:
+            if tr is not None and not tr.spans_named("dispatched"):
+                tr.mark("dispatched")  # routed, channel open: the submit POST starts
             for attempt in range(2):
                 async with sess.post(mc.url + "/submit", json=dict(body, sid=mc.sid)) as r:
                     status = r.status
@@ -548,6 +551,8 @@ class Frontend:
                 if status != 200:
                     raise ConnectionError(f"submit to {mc.url} returned {status}")
                 break
+            if tr is not None and not tr.spans_named("submitted"):
+                tr.mark("submitted")  # the worker's streamer accepted it (its command is in the engine's ring)
             await fut
         finally:
             mc.queues.pop(rid, None)

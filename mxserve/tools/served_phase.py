@@ -63,8 +63,8 @@ def _registered(url: str, model: str) -> bool:
 def _trace_breakdown(url: str, polls: int = 24, window: Optional[tuple] = None) -> dict:
     """Median per-stage times of the served requests' first tokens (those that arrived inside
     `window`, wall clock), from the frontend processes' trace rings (/debug/traces; each GET reaches one of the frontend processes, so several GETs cover
-    them all): frontend spans from the request's arrival at the frontend (tokenized, routed,
-    first_token) and the worker's spans carried on the first token (inbox: the engine thread's inbox,
+    them all): frontend spans from the request's arrival at the frontend (tokenized, dispatched: the
+    submit POST to the worker's streamer starts, submitted: it returned, first_token) and the worker's spans carried on the first token (inbox: the engine thread's inbox,
     queue: waiting for admission, prefill: admission to the sampled token, delivery: worker emit to the
     frontend's receipt)."""
     import json
@@ -83,7 +83,7 @@ def _trace_breakdown(url: str, polls: int = 24, window: Optional[tuple] = None) 
     vals: dict = {}
     for t in seen.values():
         for k, v in (t.get("spans_ms") or {}).items():
-            if k in ("tokenized", "routed", "first_token"):
+            if k in ("tokenized", "routed", "dispatched", "submitted", "first_token"):
                 vals.setdefault("frontend_" + k, []).append(v)
         for k, v in (t.get("worker_ms") or {}).items():
             if k in ("inbox_ms", "queue_ms", "prefill_ms", "delivery_ms") and isinstance(v, (int, float)):

@@ -39,6 +39,9 @@ class Trace:
     def mark(self, name: str) -> None:
         self.spans.append((name, round((time.perf_counter() - self.t0) * 1e3, 3)))
 
+    def spans_named(self, name: str) -> bool:
+        return any(n == name for n, _ in self.spans)
+
     def to_dict(self) -> dict:
         return {"request_id": self.request_id, "spans_ms": dict(self.spans), **self.attrs}
 
