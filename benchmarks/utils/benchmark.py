@@ -16,6 +16,7 @@ import json
 import os
 import random
 import time
+from typing import Optional
 
 import aiohttp
 import numpy as np
@@ -165,11 +166,13 @@ def client_procs() -> int:
 
 
 async def run_rate(url, model, rate, n, isl, osl, token_ids, vocab, seed, warmup_s: float = 0.0, gaps=None,
-                   prompts=None, procs: int = 0):
+                   prompts=None, procs: int = 0, clock: Optional[dict] = None):
     """Open-loop Poisson arrivals.  gaps / prompts: an explicit arrival stream (bench.py's served
     phase replays the engine-direct phase's exact stream) instead of one drawn from `seed`.
     procs > 1: request i is sent by client process i % procs at the same absolute schedule
-    (perf_counter is CLOCK_MONOTONIC, one clock for every process on the host)."""
+    (perf_counter is CLOCK_MONOTONIC, one clock for every process on the host).  clock: filled with the
+    schedule's origin once it is fixed ("t0": perf_counter, "t0_unix": wall clock), so a caller can
+    align its own measurements with the steady window (t0 + warmup_s)."""
     if prompts is None:
         rng = random.Random(seed)
         prompts = [synth_prompt(rng, isl, token_ids, vocab) for _ in range(n)]
@@ -177,8 +180,12 @@ async def run_rate(url, model, rate, n, isl, osl, token_ids, vocab, seed, warmup
         gaps = np.random.default_rng(seed).exponential(1.0 / rate, size=n)
     procs = procs or client_procs()
     prompts = list(prompts)[:len(gaps)]
+    def mark(t0: float) -> None:
+        if clock is not None:
+            clock["t0"], clock["t0_unix"] = t0, time.time() + (t0 - time.perf_counter())
     if procs <= 1:
         t0 = time.perf_counter()
+        mark(t0)
         sched = (t0 + np.cumsum(np.asarray(gaps[:len(prompts)], dtype=np.float64))).tolist()
         results = await _fire(url, model, osl, sched, prompts)
     else:
@@ -188,6 +195,7 @@ async def run_rate(url, model, rate, n, isl, osl, token_ids, vocab, seed, warmup
             list(ex.map(_ready, range(procs)))  # every client process up (imports done) before t0
             loop = asyncio.get_running_loop()
             t0 = time.perf_counter() + 0.2
+            mark(t0)
             sched = (t0 + np.cumsum(np.asarray(gaps[:len(prompts)], dtype=np.float64))).tolist()
             futs = [loop.run_in_executor(ex, _fire_shard, (url, model, osl, sched[k::procs], prompts[k::procs]))
                     for k in range(procs)]

@@ -144,12 +144,18 @@ def run(model: str, qps: float, isl: int, osl: int, warmup_s: float, window_s: f
         w_url = f"http://127.0.0.1:{w_port}"
         marks: list = []
 
+        clock: dict = {}
+
         async def main():
             # the worker engine's own counters at both ends of the steady window: engine iterations and
-            # tokens generated inside it (separates the engine's rate from the client's view of it)
+            # tokens generated inside it (separates the engine's rate from the client's view of it);
+            # timed from the client's schedule origin (after its processes are up), like its window
             async def sample():
                 import aiohttp
-                t0 = time.perf_counter()
+                t_wait = time.perf_counter() + 120
+                while "t0" not in clock and time.perf_counter() < t_wait:
+                    await asyncio.sleep(0.02)
+                t0 = clock.get("t0", time.perf_counter())
                 async with aiohttp.ClientSession() as sess:
                     for t in (warmup_s, warmup_s + window_s):
                         await asyncio.sleep(max(0.0, t0 + t - time.perf_counter()))
@@ -162,13 +168,14 @@ def run(model: str, qps: float, isl: int, osl: int, warmup_s: float, window_s: f
                             pass
             smp = asyncio.create_task(sample())
             res = await run_rate(url + "/v1/completions", model, qps, n, isl, osl, True, vocab, seed, warmup_s,
-                                 gaps=gaps, prompts=prompts, procs=CLIENT_PROCS if on_gpu else 1)
+                                 gaps=gaps, prompts=prompts, procs=CLIENT_PROCS if on_gpu else 1, clock=clock)
             await smp
             return res
         t_run = time.time()
         s = asyncio.run(main())
         # the steady window's requests only (the trace rings also hold the ramp-up's, which see an
-        # emptier engine)
+        # emptier engine), from the client's schedule origin
+        t_run = clock.get("t0_unix", t_run)
         breakdown = _trace_breakdown(url, window=(t_run + warmup_s, t_run + warmup_s + window_s))
         res = {"status": "ok", "value": s.get("steady_output_tok_per_s"), "unit": "tok/s",
                "ttft_p50_ms": s.get("steady_ttft_ms_p50"), "ttft_p90_ms": s.get("steady_ttft_ms_p90"),
